@@ -1,0 +1,42 @@
+/*
+ * nuSIprop oracle -- special functions.  TEST INFRASTRUCTURE ONLY.
+ *
+ * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may
+ * load anything under oracle/.  The product path (nusiprop_amd/) never does.
+ *
+ * The reference calls three third-party functions that are absent from
+ * /root/reference:
+ *   - GSL gsl_sf_dilog(x)                 (version unpinned; Homebrew build)
+ *       aux.hpp:112,129,147,165  nuSIprop.hpp:1098,1202,1375-1398
+ *   - GSL gsl_sf_complex_dilog_xy_e(x,y)  aux.hpp:92-93  nuSIprop.hpp:1444-1451
+ *   - Expander/polylogarithm Li2(double), Li3(double)  (un-vendored submodule)
+ *       nuSIprop.hpp:628-636
+ * Their published semantics are restated here:
+ *   gsl_sf_dilog(x)             = Re Li2(x) for all real x (x>1 included)
+ *   gsl_sf_complex_dilog_xy_e   = principal-branch Li2(x+iy); for y == 0 and
+ *                                 x >= 1 GSL returns Im = -pi*log(x)
+ *                                 (and Re = gsl_sf_dilog(x)); for y == 0 and
+ *                                 x < 1, Im = 0
+ *   polylogarithm::Li2 / Li3    = real Li2 / Li3 (only x in [-1,0) reached)
+ * The values are computed in x87 long double (64-bit mantissa) from standard
+ * series (Bernoulli series for Li2 after the z->1/z and z->1-z maps; Dirichlet
+ * eta / power series for Li3) and rounded once to double, so they are within
+ * ~0.5 ulp of the exact function -- i.e. at least as accurate as GSL's quoted
+ * error.  They are pinned by mpmath known-answer vectors in
+ * tests/golden/specfun_kat.json (tests/test_oracle_specfun.py).
+ */
+#ifndef NUSI_ORA_SPECFUN_H
+#define NUSI_ORA_SPECFUN_H
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+double ora_dilog(double x);                                  /* gsl_sf_dilog */
+void ora_complex_dilog_xy(double x, double y, double *re, double *im);
+double ora_li2(double x);                                    /* polylogarithm::Li2 */
+double ora_li3(double x);                                    /* polylogarithm::Li3, x in [-1,0.5] */
+
+#ifdef __cplusplus
+}
+#endif
+#endif
