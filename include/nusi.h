@@ -1,0 +1,150 @@
+/*
+ * nusi.h -- C ABI of the MI355X-native nuSIprop cascade solver (libnusi.so).
+ *
+ * Drop-in boundary for the reference's calculate_flux / pyprop surface
+ * (quarkquartet/nuSIprop @ 2025-02-13).  Plain C types only: pointers, sizes,
+ * ints and doubles.  Every function returns 0 on success or a negative
+ * NUSI_E* code; nusi_last_error() gives the message (thread-local).  Nothing
+ * in the library calls exit(): the C++ facade (include/nuSIprop.hpp) maps
+ * errors back to the reference's stderr text + exit(1).
+ *
+ * Two levels:
+ *   1. object API -- one parameter point, host-side results, the exact
+ *      semantics of nuSIprop::calculate_flux (each entry cites the member it
+ *      replaces, nuSIprop.hpp:line);
+ *   2. plan API   -- a batch of parameter points sharing one energy/redshift
+ *      grid, evolved on one GPU with device-resident inputs/outputs (the
+ *      MI355X throughput path; multi-GPU = one plan per device, no
+ *      collectives).
+ * All arithmetic is IEEE fp64.  The table build and the cascade run as HIP
+ * kernels on the GPU; there is no CPU fallback -- without a usable GPU the
+ * calls fail with NUSI_EHIP.
+ */
+#ifndef NUSI_H
+#define NUSI_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* error codes */
+#define NUSI_OK 0
+#define NUSI_EPARAM -1        /* bad parameters / range                          */
+#define NUSI_ENOSPECTRUM -2   /* no neutrino mass spectrum (aux.hpp:48-49)       */
+#define NUSI_ETABLE -3        /* phi-phi table missing (interp.hpp:251-254)      */
+#define NUSI_EINTERP -4       /* phi-phi lookup out of bounds (interp.hpp:355-361) */
+#define NUSI_EHIP -5          /* HIP runtime error / no GPU                      */
+#define NUSI_ESTATE -6        /* call order (e.g. results before evolve)         */
+
+/* source models.  DSNB is the reference's active Lum (nuSIprop.hpp:659-662);
+ * POWER_LAW is its commented-out power law (nuSIprop.hpp:656) used by the
+ * BASELINE workloads. */
+#define NUSI_SOURCE_DSNB 0
+#define NUSI_SOURCE_POWER_LAW 1
+
+/* warning bits (negative cross sections, nuSIprop.hpp:909-918, 1215-1231, 1505-1516) */
+#define NUSI_WARN_GAMMA 1
+#define NUSI_WARN_ALPHATILDE 2
+#define NUSI_WARN_ALPHA 4
+
+/* All constructor arguments of calculate_flux (nuSIprop.hpp:61-65), in order,
+ * plus the source model.  Defaults of the reference C++ constructor:
+ * norm=1, majorana=1, non_resonant=1, normal_ordering=1, N_bins_E=300,
+ * lEmin=12, lEmax=17, zmax=5, flav=2, phiphi=0 (see nusi_params_default). */
+typedef struct nusi_params {
+    double mphi;        /* mediator mass [eV]                      */
+    double g;           /* coupling                                */
+    double mntot;       /* sum of neutrino masses [eV]             */
+    double si;          /* spectral index                          */
+    double norm;        /* free-streaming normalisation at 100 TeV */
+    int majorana;
+    int non_resonant;
+    int normal_ordering;
+    int N_bins_E;
+    double lEmin;
+    double lEmax;
+    double zmax;
+    int flav;           /* 0=e 1=mu 2=tau */
+    int phiphi;
+    int source_model;   /* NUSI_SOURCE_* */
+} nusi_params;
+
+/* Fills the reference C++ constructor defaults (nuSIprop.hpp:61-65) around
+ * the four mandatory parameters; source_model = NUSI_SOURCE_DSNB. */
+void nusi_params_default(nusi_params *p, double mphi, double g, double mntot, double si);
+
+const char *nusi_last_error(void);
+int nusi_device_count(void);
+
+/* ---------------------------------------------------------------------------
+ * 1. object API  (nuSIprop::calculate_flux)
+ * ------------------------------------------------------------------------- */
+typedef struct nusi_handle nusi_handle;
+
+/* calculate_flux(mphi, g, mntot, si, norm, ...)   nuSIprop.hpp:61-171.
+ * Builds the energy/redshift grid and the mixing matrix.  With
+ * non_resonant && phiphi the phi-phi tables are loaded like the reference,
+ * from xsec/alphatilde_phiphi.bin and xsec/alpha_phiphi.bin relative to the
+ * current directory (or $NUSI_XSEC_DIR), -> NUSI_ETABLE if missing.
+ * The object evolves on GPU `$NUSI_DEVICE` (default 0). */
+int nusi_create(const nusi_params *p, nusi_handle **out);
+/* copy constructor / operator=  (nuSIprop.hpp:434-525) */
+int nusi_copy(const nusi_handle *src, nusi_handle **out);
+void nusi_destroy(nusi_handle *h);
+/* the public members mphi, g, mntot, si, norm  (nuSIprop.hpp:174) */
+int nusi_set_params(nusi_handle *h, double mphi, double g, double mntot, double si, double norm);
+int nusi_get_params(const nusi_handle *h, double *mphi_g_mntot_si_norm /* [5] */);
+/* evolve()  (nuSIprop.hpp:176-337) */
+int nusi_evolve(nusi_handle *h);
+/* check_energy_conservation()  (nuSIprop.hpp:339-357): calls evolve() */
+int nusi_check_energy_conservation(nusi_handle *h, double *out);
+/* results of the last evolve(), row-major [k][b] (mass basis) / [f][b] (flavour) */
+int nusi_get_flux(const nusi_handle *h, double *out_3xN);      /* get_flux(i,j)     :359-381 */
+int nusi_get_flux_fla(const nusi_handle *h, double *out_3xN);  /* get_flux_fla(i,j) :383-405 */
+int nusi_get_energies(const nusi_handle *h, double *out_N);    /* get_energy(i)     :412-429 */
+int nusi_get_N_bins_E(const nusi_handle *h);                   /* get_N_bins_E()    :407-410 */
+int nusi_get_N_steps_z(const nusi_handle *h);
+int nusi_get_warnings(const nusi_handle *h);                   /* NUSI_WARN_* of the last evolve */
+
+/* ---------------------------------------------------------------------------
+ * 2. plan API -- batched parameter scans on one GPU
+ * ------------------------------------------------------------------------- */
+typedef struct nusi_plan nusi_plan;
+
+/* One plan = one device, one grid (N_bins_E, lEmin, lEmax, zmax), room for
+ * max_points points per call (tables for all of them stay in HBM). */
+int nusi_plan_create(int device, int N_bins_E, double lEmin, double lEmax, double zmax, int max_points,
+                     nusi_plan **out);
+void nusi_plan_destroy(nusi_plan *plan);
+/* Load the phi-phi tables (float32 records {x0..x_{d-1}, f}, last index
+ * fastest; interp.hpp:249-291).  dims == NULL -> the reference's
+ * {5000,100} and {1000,1000,100} (nuSIprop.hpp:168-169). */
+int nusi_plan_load_phiphi(nusi_plan *plan, const char *alphatilde_path, const int *alphatilde_dims,
+                          const char *alpha_path, const int *alpha_dims);
+int nusi_plan_grid(const nusi_plan *plan, int *N, int *Nz, double *Enu /* [N] or NULL */);
+/* Evolve n points (their grid fields must equal the plan's).  d_flux /
+ * d_flux_fla are DEVICE pointers of n*3*N doubles ([point][k][b]); either may
+ * be NULL.  stream is a hipStream_t (NULL = the plan's own stream).  The call
+ * is asynchronous w.r.t. the host except for the small host->device copy of
+ * the per-point constants; results are ready when the stream is. */
+int nusi_plan_evolve(nusi_plan *plan, const nusi_params *pts, int n, double *d_flux, double *d_flux_fla, void *stream);
+/* Same with host result buffers; synchronous. */
+int nusi_plan_evolve_host(nusi_plan *plan, const nusi_params *pts, int n, double *flux, double *flux_fla);
+/* Kernel times (ms) of the last nusi_plan_evolve*: [0] Gamma/alphaTilde
+ * tables, [1] alpha table, [2] cascade.  Synchronises the plan's stream. */
+int nusi_plan_stage_ms(nusi_plan *plan, float *ms3);
+/* per-point NUSI_WARN_* bits of the last call */
+int nusi_plan_warnings(nusi_plan *plan, int *out, int n);
+/* Copy point `i`'s Stage-A tables of the last call to the host (parity
+ * tests): Gamma[T], alphaTilde[T], alpha packed transposed [T(T-1)/2] with
+ * alpha(n,m), n<m, at m(m-1)/2+n.  Any pointer may be NULL. */
+int nusi_plan_tables(nusi_plan *plan, int i, double *Gamma, double *alphaTilde, double *alpha_packed);
+
+/* Convenience: evolve n points on `device` with host buffers (creates a
+ * transient plan; points must share the grid). */
+int nusi_evolve_batch(int device, const nusi_params *pts, int n, double *flux, double *flux_fla);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* NUSI_H */

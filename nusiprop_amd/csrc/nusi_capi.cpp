@@ -1,0 +1,780 @@
+// nuSIprop MI355X -- C ABI (include/nusi.h): host set-up, plans, object API.
+//
+// Host work here is the reference's per-object scalar set-up only (grid,
+// mixing matrix, masses, normalisation; nuSIprop.hpp:102-171, 184-205) and
+// the energy-conservation diagnostic; the table build and the cascade run
+// on the GPU (nusi_kernels.hip).  There is no CPU fallback.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "nusi.h"
+#include "nusi_internal.hpp"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg)
+{
+    g_err = msg;
+    return code;
+}
+
+#define HIPCHECK(x)                                                                              \
+    do {                                                                                         \
+        hipError_t e_ = (x);                                                                     \
+        if (e_ != hipSuccess) return fail(NUSI_EHIP, std::string("HIP error: ") + hipGetErrorString(e_) + " (" #x ")"); \
+    } while (0)
+
+inline double sq(double a) { return a * a; }
+inline double cu(double a) { return a * a * a; }
+
+// ---------------------------------------------------------------------------
+// grid: constructor nuSIprop.hpp:113-128, table axis :224-233, per-step
+// scalars of the cascade :256-259, 268-269, 283
+// ---------------------------------------------------------------------------
+struct HostGrid {
+    int N = 0, Nz = 0, T = 0;
+    double lEmin = 0, lEmax = 0, zmax_in = 0, zmax_eff = 0;
+    std::vector<double> Emin, Emax, Enu, z, lo, hi, step_c, step_s, sfr;
+};
+
+double hubble_h(double z) { return 1.5e-33 * pow(0.692 + 0.308 * cu(1 + z), 0.5); }
+double n_nu_h(double z) { return 4.3528e-13 * cu(1 + z); }
+double sfr_h(double z)
+{
+    return pow(pow(1 + z, -3.4 * 10) + pow((1 + z) / 5161, 0.3 * 10) + pow((1 + z) / 9.06, 3.5 * 10), -1. / 10.);
+}
+
+HostGrid make_grid(int N, double lEmin, double lEmax, double zmax)
+{
+    HostGrid G;
+    G.N = N;
+    G.lEmin = lEmin;
+    G.lEmax = lEmax;
+    G.zmax_in = zmax;
+    G.Emin.resize(N);
+    G.Emax.resize(N);
+    G.Enu.resize(N);
+    for (int i = 0; i < N; ++i) {
+        G.Emin[i] = pow(10, lEmin + (lEmax - lEmin) * (i * 1.0) / N);
+        G.Enu[i] = pow(10, lEmin + (lEmax - lEmin) * (i + 0.5) / N);
+        G.Emax[i] = pow(10, lEmin + (lEmax - lEmin) * (i + 1.0) / N);
+    }
+    G.Nz = (int)(log((1 + zmax) / (1 + 0)) / log(G.Emax[0] / G.Emin[0]) + 2);
+    G.z.resize(G.Nz);
+    for (int i = 0; i < G.Nz; ++i) G.z[i] = (1 + 0) * pow(G.Emax[0] / G.Emin[0], i) - 1;
+    G.zmax_eff = G.z[G.Nz - 1];
+    G.T = N + G.Nz - 2;
+    G.lo.resize(G.T);
+    G.hi.resize(G.T);
+    for (int n = 0; n < G.T; ++n) {
+        if (n < N) {
+            G.lo[n] = G.Emin[n];
+            G.hi[n] = G.Emax[n];
+        } else {
+            G.lo[n] = G.Emin[N - 1] * (1 + G.z[n - N + 1]);
+            G.hi[n] = G.Emax[N - 1] * (1 + G.z[n - N + 1]);
+        }
+    }
+    G.step_c.assign(G.Nz, 0.0);
+    G.step_s.assign(G.Nz, 0.0);
+    const double dlogz = log(1 + G.z[1]) - log(1 + G.z[0]);
+    for (int i = 1; i < G.Nz; ++i) {
+        const double zz = G.z[i - 1];
+        G.step_c[i] = (1 + zz) * dlogz / hubble_h(zz);
+        G.step_s[i] = n_nu_h(zz) / sq(1 + zz);
+    }
+    G.sfr.resize(G.Nz);
+    for (int i = 0; i < G.Nz; ++i) G.sfr[i] = sfr_h(G.z[i]);
+    return G;
+}
+
+// |U_fk|^2 from NuFIT 5.0 angles, nuSIprop.hpp:130-163.  Only std::norm(U)
+// is used by the reference; the complex entries are formed with explicit real
+// operations (real*complex component-wise, s13/del by Smith's division, the
+// algorithm of libgcc's __divdc3 for finite operands) so that the result does
+// not depend on the host compiler's complex runtime.
+void pmns_sq(bool normal, double U2[9])
+{
+    double t12, t13, t23, dcp;
+    if (normal) {
+        t12 = 33.44 * (M_PI / 180);
+        t13 = 8.57 * (M_PI / 180);
+        t23 = 49.0 * (M_PI / 180);
+        dcp = 195.0 * (M_PI / 180);
+    } else {
+        t12 = 33.45 * (M_PI / 180);
+        t13 = 8.61 * (M_PI / 180);
+        t23 = 49.3 * (M_PI / 180);
+        dcp = 286.0 * (M_PI / 180);
+    }
+    const double c12 = cos(t12), c13 = cos(t13), c23 = cos(t23);
+    const double s12 = sin(t12), s13 = sin(t13), s23 = sin(t23);
+    const nusi::cd del = nusi::C(cos(dcp), sin(dcp));
+    nusi::cd U[3][3];
+    U[0][0] = nusi::C(c12 * c13);
+    U[0][1] = nusi::C(s12 * c13);
+    U[0][2] = (s13 * 1.0) / del;
+    U[1][0] = -s12 * c23 - (c12 * s23 * s13) * del;
+    U[1][1] = c12 * c23 - (s12 * s23 * s13) * del;
+    U[1][2] = nusi::C(s23 * c13);
+    U[2][0] = s12 * s23 - (c12 * c23 * s13) * del;
+    U[2][1] = -c12 * s23 - (s12 * c23 * s13) * del;
+    U[2][2] = nusi::C(c23 * c13);
+    for (int f = 0; f < 3; ++f)
+        for (int k = 0; k < 3; ++k) U2[3 * f + k] = U[f][k].r * U[f][k].r + U[f][k].i * U[f][k].i;
+}
+
+// Lightest mass, aux.hpp:12-50.  The reference's quartic + constraint filter
+// selects the unique root of the un-squared mass-sum equation, found here by
+// bisection to full precision; at the minimal mass sum (root 0, where GSL
+// returns rounding noise and m = 0 would make the tables NaN) the lightest
+// mass is set to kMlFloor.
+constexpr double kMlFloor = 1e-12;
+double mass_sum(double m, double dmqSL, double dmqAT)
+{
+    if (dmqAT > 0) return m + sqrt(sq(m) + dmqSL) + sqrt(sq(m) + dmqAT);
+    const double m2 = sqrt(sq(m) - dmqAT);
+    return m + m2 + sqrt(sq(m2) - dmqSL);
+}
+bool lightest_mass(double mSum, double dmqSL, double dmqAT, double* mL)
+{
+    const double f0 = mass_sum(0.0, dmqSL, dmqAT) - mSum;
+    double ml;
+    if (f0 >= 0) {
+        if (f0 > 64 * 2.220446049250313e-16 * mSum) return false;
+        ml = kMlFloor;
+    } else {
+        double lo = 0.0, hi = mSum;
+        for (int it = 0; it < 2000; ++it) {
+            const double mid = 0.5 * (lo + hi);
+            if (mid <= lo || mid >= hi) break;
+            if (mass_sum(mid, dmqSL, dmqAT) - mSum > 0) hi = mid;
+            else lo = mid;
+        }
+        ml = (fabs(mass_sum(hi, dmqSL, dmqAT) - mSum) < fabs(mass_sum(lo, dmqSL, dmqAT) - mSum)) ? hi : lo;
+        if (ml <= 0) ml = kMlFloor;
+    }
+    const bool ok1 = (mSum - ml > 1.0e-7);
+    const bool ok2 = (dmqAT > 0) ? (sq(mSum) - dmqAT - dmqSL - sq(ml) - 2 * ml * mSum > 1.0e-7)
+                                 : (sq(mSum) + 2 * dmqAT + dmqSL - sq(ml) - 2 * ml * mSum > 1.0e-7);
+    if (!(ok1 && ok2)) return false;
+    *mL = ml;
+    return true;
+}
+
+const double kGLw[3] = {5. / 9., 8. / 9., 5. / 9.};
+const double kGLx[3] = {-0.7745966692414834, 0.0, 0.7745966692414834};
+
+// flux_FS_E0, nuSIprop.hpp:666-692
+double flux_fs_e0(double si, double zmax_eff)
+{
+    double res = 0;
+    const double z_min = 0, z_max = zmax_eff;
+    const int NI = 100;
+    for (int f = 0; f < NI; f++) {
+        const double a = z_min + f * (z_max - z_min) / NI;
+        const double b = z_min + (f + 1.0) * (z_max - z_min) / NI;
+        double zz[3];
+        for (int q = 0; q < 3; ++q) zz[q] = (b - a) / 2. * kGLx[q] + (b + a) / 2.;
+        res += (b - a) / 2. * (kGLw[0] * pow(1 + zz[0], -si) * sfr_h(zz[0]) / hubble_h(zz[0])
+                               + kGLw[1] * pow(1 + zz[1], -si) * sfr_h(zz[1]) / hubble_h(zz[1])
+                               + kGLw[2] * pow(1 + zz[2], -si) * sfr_h(zz[2]) / hubble_h(zz[2]));
+    }
+    return res;
+}
+
+// energy_FS / Lum_times_E, nuSIprop.hpp:694-744 (power law; stale norm_total)
+double energy_fs(double si, double norm_total, double zmax_eff, double lEmin, double lEmax)
+{
+    const double E0 = 1e14;
+    auto lte = [&](double z, double Em, double Ep) {
+        if (fabs(si - 2) < 1e-5)
+            return norm_total * sfr_h(z) * pow(E0 / (1 + z), si) * (log(Ep / Em) + (2 - si) / 2.0 * (sq(log(Ep)) - sq(log(Em))));
+        return norm_total * sfr_h(z) * pow(E0 / (1 + z), si) * (pow(Ep, 2 - si) - pow(Em, 2 - si)) / (2 - si);
+    };
+    double res = 0;
+    const double z_min = 0, z_max = zmax_eff, lo = pow(10, lEmin), hi = pow(10, lEmax);
+    for (int f = 0; f < 100; f++) {
+        const double a = z_min + f * (z_max - z_min) / 100;
+        const double b = z_min + (f + 1.0) * (z_max - z_min) / 100;
+        double zz[3];
+        for (int q = 0; q < 3; ++q) zz[q] = (b - a) / 2. * kGLx[q] + (b + a) / 2.;
+        res += (b - a) / 2. * (kGLw[0] * lte(zz[0], lo, hi) / hubble_h(zz[0]) + kGLw[1] * lte(zz[1], lo, hi) / hubble_h(zz[1])
+                               + kGLw[2] * lte(zz[2], lo, hi) / hubble_h(zz[2]));
+    }
+    return res;
+}
+
+// ---------------------------------------------------------------------------
+// phi-phi tables (interp.hpp:173-320, binary branch) -> device SplineDev
+// ---------------------------------------------------------------------------
+struct SplineStore {
+    int device = 0;
+    std::vector<void*> bufs;
+    nusi::SplineSet set;
+    ~SplineStore()
+    {
+        if (bufs.empty()) return;
+        int prev = 0;
+        hipGetDevice(&prev);
+        hipSetDevice(device);
+        for (void* b : bufs) hipFree(b);
+        hipSetDevice(prev);
+    }
+};
+
+// weights of interp.hpp:576-636 (the last node's weights are never read)
+void spline_weights(const std::vector<double>& x, std::vector<double>& w)
+{
+    const int n = (int)x.size();
+    w.assign((size_t)16 * n, 0.0);
+    auto W = [&](int a, int b, int j) -> double& { return w[(size_t)(a * 4 + b) * n + j]; };
+    for (int j = 0; j + 1 < n; ++j) {
+        const double xm = (j > 0) ? x[j - 1] : 0.0, x0 = x[j], x1 = x[j + 1], x2 = (j + 2 < n) ? x[j + 2] : 0.0;
+        if (j == 0) {
+            W(0, 1, j) = (x0 - x1) / (x0 - x2);
+            W(0, 2, j) = (-1 + (x1 - x0) / (x0 - x2));
+            W(0, 3, j) = 1;
+            W(1, 1, j) = (x1 - x0) / (x1 - x2);
+            W(1, 2, j) = (x0 - x2) / (x1 - x2);
+            W(2, 1, j) = sq(x1 - x0) / ((x2 - x1) * (x2 - x0));
+            W(2, 2, j) = sq(x1 - x0) / ((x2 - x1) * (x0 - x2));
+        } else if (j == n - 2) {
+            W(0, 1, j) = sq(x1 - x0) / ((xm - x0) * (xm - x1));
+            W(0, 2, j) = sq(x1 - x0) / ((x0 - xm) * (xm - x1));
+            W(1, 1, j) = (x1 - x0) / (xm - x0);
+            W(1, 2, j) = (2 * x0 - x1 - xm) / (xm - x0);
+            W(1, 3, j) = 1;
+            W(2, 1, j) = (x0 - x1) / (xm - x1);
+            W(2, 2, j) = (xm - x0) / (xm - x1);
+        } else {
+            W(0, 0, j) = sq(x1 - x0) / ((x0 - xm) * (xm - x1));
+            W(0, 1, j) = 2 * sq(x1 - x0) / ((xm - x0) * (xm - x1));
+            W(0, 2, j) = sq(x1 - x0) / ((x0 - xm) * (xm - x1));
+            W(1, 0, j) = (x0 - x1) * (1 / (xm - x0) + 1 / (x0 - x2));
+            W(1, 1, j) = (x0 - x1) * (2 / (x0 - xm) + 1 / (x2 - x0));
+            W(1, 2, j) = (2 * x0 - x1 - xm) / (xm - x0);
+            W(1, 3, j) = 1;
+            W(2, 0, j) = (x1 - x0) * (1 / (xm - x1) + 1 / (x1 - x2));
+            W(2, 1, j) = (x1 - x0) * (2 / (x1 - xm) + 1 / (x2 - x1));
+            W(2, 2, j) = (xm - x0) / (xm - x1);
+            W(3, 0, j) = sq(x1 - x0) / ((-x1 + x2) * (-x0 + x2));
+            W(3, 1, j) = sq(x1 - x0) / ((x1 - x2) * (-x0 + x2));
+        }
+    }
+}
+
+int load_spline(const char* path, int ndim, const int* dims, SplineStore& st, nusi::SplineDev& out)
+{
+    FILE* fp = fopen(path, "rb");
+    if (!fp)
+        return fail(NUSI_ETABLE, std::string("Error at interp: the input file ") + path + " does not exist");
+    std::vector<std::vector<double>> x(ndim);
+    size_t nf = 1;
+    for (int i = 0; i < ndim; ++i) {
+        x[i].assign(dims[i], 0.0);
+        nf *= (size_t)dims[i];
+    }
+    std::vector<float> f(nf);
+    std::vector<float> chunk((size_t)(ndim + 1) * 65536);
+    size_t r = 0;
+    while (r < nf) {
+        const size_t want = std::min<size_t>(65536, nf - r);
+        if (fread(chunk.data(), sizeof(float) * (ndim + 1), want, fp) != want) {
+            fclose(fp);
+            return fail(NUSI_ETABLE, std::string("Error at interp: the input file ") + path + " is truncated");
+        }
+        for (size_t q = 0; q < want; ++q, ++r) {
+            size_t rem = r;
+            int idx[nusi::kSplMaxDim];
+            for (int i = ndim - 1; i >= 0; --i) {
+                idx[i] = (int)(rem % (size_t)dims[i]);
+                rem /= (size_t)dims[i];
+            }
+            const float* rec = &chunk[q * (ndim + 1)];
+            for (int i = 0; i < ndim; ++i) x[i][idx[i]] = (double)rec[i];
+            f[r] = rec[ndim];
+        }
+    }
+    fclose(fp);
+    nusi::SplineDev sd;
+    sd.ndim = ndim;
+    sd.islog[0] = 1;  // both reference tables interpolate in log(x0) (nuSIprop.hpp:168-169)
+    for (int i = 0; i < ndim; ++i) {
+        sd.n[i] = dims[i];
+        if (sd.islog[i])
+            for (double& v : x[i]) v = log(v);
+        std::vector<double> w;
+        spline_weights(x[i], w);
+        double *dx = nullptr, *dw = nullptr;
+        HIPCHECK(hipMalloc(&dx, sizeof(double) * x[i].size()));
+        st.bufs.push_back(dx);
+        HIPCHECK(hipMalloc(&dw, sizeof(double) * w.size()));
+        st.bufs.push_back(dw);
+        HIPCHECK(hipMemcpy(dx, x[i].data(), sizeof(double) * x[i].size(), hipMemcpyHostToDevice));
+        HIPCHECK(hipMemcpy(dw, w.data(), sizeof(double) * w.size(), hipMemcpyHostToDevice));
+        sd.x[i] = dx;
+        sd.w[i] = dw;
+    }
+    float* df = nullptr;
+    HIPCHECK(hipMalloc(&df, sizeof(float) * nf));
+    st.bufs.push_back(df);
+    HIPCHECK(hipMemcpy(df, f.data(), sizeof(float) * nf, hipMemcpyHostToDevice));
+    sd.f = df;
+    out = sd;
+    return NUSI_OK;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// plan
+// ---------------------------------------------------------------------------
+struct nusi_plan {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    HostGrid grid;
+    int max_points = 0;
+    nusi::GridDev gd{};
+    double* d_grid = nullptr;
+    nusi::Point* d_pts = nullptr;
+    nusi::Point* h_pts = nullptr;  // pinned
+    int* d_warn = nullptr;
+    nusi::TablesDev tabs{};
+    double* d_scratch = nullptr;   // flux outputs when the caller passes NULL
+    std::shared_ptr<SplineStore> spl;
+    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+    hipEvent_t ev_copy = nullptr;
+    bool ran = false;
+    int last_n = 0;
+    double U2[2][9];
+    std::map<double, double> fs_cache;                      // si -> flux_FS_E0
+    std::map<std::pair<double, int>, std::vector<double>> mass_cache;
+};
+
+namespace {
+
+int build_point(nusi_plan* pl, const nusi_params& p, nusi::Point& P)
+{
+    const HostGrid& G = pl->grid;
+    if (p.N_bins_E != G.N || p.lEmin != G.lEmin || p.lEmax != G.lEmax || p.zmax != G.zmax_in)
+        return fail(NUSI_EPARAM, "point grid (N_bins_E, lEmin, lEmax, zmax) differs from the plan's");
+    if (p.flav < 0 || p.flav > 2) return fail(NUSI_EPARAM, "flav must be 0, 1 or 2");
+    if (p.source_model != NUSI_SOURCE_DSNB && p.source_model != NUSI_SOURCE_POWER_LAW)
+        return fail(NUSI_EPARAM, "unknown source_model");
+    const int no = p.normal_ordering ? 1 : 0;
+    // masses, nuSIprop.hpp:184-203
+    const double dmq21 = 7.42e-5;
+    const double dmqAT = no ? 2.514e-3 : -2.497e-3;
+    auto key = std::make_pair(p.mntot, no);
+    auto it = pl->mass_cache.find(key);
+    if (it == pl->mass_cache.end()) {
+        double mL;
+        if (!lightest_mass(p.mntot, dmq21, dmqAT, &mL)) {
+            char buf[256];
+            snprintf(buf, sizeof buf,
+                     "No neutrino mass spectrum was found corresponding to \\sum m = %g, dmqAT = %g, dmqSL = %g. Exiting...",
+                     p.mntot, dmqAT, dmq21);
+            return fail(NUSI_ENOSPECTRUM, buf);
+        }
+        std::vector<double> mn(3);
+        if (no) {
+            mn[0] = mL;
+            mn[1] = sqrt(dmq21 + sq(mL));
+            mn[2] = sqrt(dmqAT + sq(mL));
+        } else {
+            mn[2] = mL;
+            mn[1] = sqrt(sq(mL) - dmqAT);
+            mn[0] = sqrt(sq(mn[1]) - dmq21);
+        }
+        it = pl->mass_cache.emplace(key, mn).first;
+    }
+    auto fit = pl->fs_cache.find(p.si);
+    if (fit == pl->fs_cache.end()) fit = pl->fs_cache.emplace(p.si, flux_fs_e0(p.si, G.zmax_eff)).first;
+    memset(&P, 0, sizeof(P));
+    P.mphi = p.mphi;
+    P.g = p.g;
+    P.mntot = p.mntot;
+    P.si = p.si;
+    P.norm = p.norm;
+    P.norm_total = p.norm / fit->second;
+    P.Ga = p.majorana ? sq(p.g) * p.mphi / (16.0 * M_PI) : sq(p.g) * p.mphi / (8.0 * M_PI);
+    for (int k = 0; k < 3; ++k) P.mn[k] = it->second[k];
+    for (int k = 0; k < 9; ++k) P.U2[k] = pl->U2[no][k];
+    for (int k = 0; k < 3; ++k) P.u[k] = pl->U2[no][3 * p.flav + k];
+    P.majorana = p.majorana ? 1 : 0;
+    P.non_resonant = p.non_resonant ? 1 : 0;
+    P.phiphi = p.phiphi ? 1 : 0;
+    P.source = p.source_model;
+    if (P.non_resonant && P.phiphi && !pl->spl)
+        return fail(NUSI_ETABLE, "phiphi requested but the phi-phi tables are not loaded (nusi_plan_load_phiphi)");
+    return NUSI_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* nusi_last_error(void) { return g_err.c_str(); }
+
+int nusi_device_count(void)
+{
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+void nusi_params_default(nusi_params* p, double mphi, double g, double mntot, double si)
+{
+    p->mphi = mphi;
+    p->g = g;
+    p->mntot = mntot;
+    p->si = si;
+    p->norm = 1;
+    p->majorana = 1;
+    p->non_resonant = 1;
+    p->normal_ordering = 1;
+    p->N_bins_E = 300;
+    p->lEmin = 12.0;
+    p->lEmax = 17.0;
+    p->zmax = 5.0;
+    p->flav = 2;
+    p->phiphi = 0;
+    p->source_model = NUSI_SOURCE_DSNB;
+}
+
+void nusi_plan_destroy(nusi_plan* pl)
+{
+    if (!pl) return;
+    int prev = 0;
+    hipGetDevice(&prev);
+    hipSetDevice(pl->device);
+    if (pl->stream) hipStreamSynchronize(pl->stream);
+    for (auto& e : pl->ev)
+        if (e) hipEventDestroy(e);
+    if (pl->ev_copy) hipEventDestroy(pl->ev_copy);
+    hipFree(pl->d_grid);
+    hipFree(pl->d_pts);
+    hipFree(pl->d_warn);
+    hipFree(pl->tabs.G);
+    hipFree(pl->tabs.At);
+    hipFree(pl->tabs.A);
+    hipFree(pl->d_scratch);
+    if (pl->h_pts) hipHostFree(pl->h_pts);
+    if (pl->stream) hipStreamDestroy(pl->stream);
+    pl->spl.reset();
+    hipSetDevice(prev);
+    delete pl;
+}
+
+int nusi_plan_create(int device, int N_bins_E, double lEmin, double lEmax, double zmax, int max_points, nusi_plan** out)
+{
+    *out = nullptr;
+    if (N_bins_E < 2 || !(lEmax > lEmin) || !(zmax > 0) || max_points < 1)
+        return fail(NUSI_EPARAM, "bad grid: need N_bins_E >= 2, lEmax > lEmin, zmax > 0, max_points >= 1");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(NUSI_EHIP, "no HIP device available");
+    if (device < 0 || device >= ndev) return fail(NUSI_EPARAM, "device index out of range");
+    HIPCHECK(hipSetDevice(device));
+    std::unique_ptr<nusi_plan, void (*)(nusi_plan*)> pl(new nusi_plan, nusi_plan_destroy);
+    pl->device = device;
+    pl->grid = make_grid(N_bins_E, lEmin, lEmax, zmax);
+    pl->max_points = max_points;
+    pmns_sq(true, pl->U2[1]);
+    pmns_sq(false, pl->U2[0]);
+    const HostGrid& G = pl->grid;
+    if (G.Nz < 2) return fail(NUSI_EPARAM, "redshift grid has fewer than two steps");
+    HIPCHECK(hipStreamCreateWithFlags(&pl->stream, hipStreamNonBlocking));
+    for (auto& e : pl->ev) HIPCHECK(hipEventCreate(&e));
+    HIPCHECK(hipEventCreateWithFlags(&pl->ev_copy, hipEventDisableTiming));
+    // grid arrays in one allocation
+    const size_t ng = 2 * (size_t)G.N + 2 * (size_t)G.T + 4 * (size_t)G.Nz;
+    HIPCHECK(hipMalloc(&pl->d_grid, sizeof(double) * ng));
+    std::vector<double> hg;
+    hg.reserve(ng);
+    hg.insert(hg.end(), G.Emin.begin(), G.Emin.end());
+    hg.insert(hg.end(), G.Emax.begin(), G.Emax.end());
+    hg.insert(hg.end(), G.lo.begin(), G.lo.end());
+    hg.insert(hg.end(), G.hi.begin(), G.hi.end());
+    hg.insert(hg.end(), G.z.begin(), G.z.end());
+    hg.insert(hg.end(), G.step_c.begin(), G.step_c.end());
+    hg.insert(hg.end(), G.step_s.begin(), G.step_s.end());
+    hg.insert(hg.end(), G.sfr.begin(), G.sfr.end());
+    HIPCHECK(hipMemcpy(pl->d_grid, hg.data(), sizeof(double) * ng, hipMemcpyHostToDevice));
+    nusi::GridDev& gd = pl->gd;
+    gd.N = G.N;
+    gd.Nz = G.Nz;
+    gd.T = G.T;
+    gd.PT = (long long)G.T * (G.T - 1) / 2;
+    double* q = pl->d_grid;
+    gd.Emin = q;
+    q += G.N;
+    gd.Emax = q;
+    q += G.N;
+    gd.lo = q;
+    q += G.T;
+    gd.hi = q;
+    q += G.T;
+    gd.z = q;
+    q += G.Nz;
+    gd.step_c = q;
+    q += G.Nz;
+    gd.step_s = q;
+    q += G.Nz;
+    gd.sfr = q;
+    HIPCHECK(hipMalloc(&pl->d_pts, sizeof(nusi::Point) * max_points));
+    HIPCHECK(hipHostMalloc((void**)&pl->h_pts, sizeof(nusi::Point) * max_points, hipHostMallocDefault));
+    HIPCHECK(hipMalloc(&pl->d_warn, sizeof(int) * max_points));
+    HIPCHECK(hipMalloc(&pl->tabs.G, sizeof(double) * (size_t)G.T * max_points));
+    HIPCHECK(hipMalloc(&pl->tabs.At, sizeof(double) * (size_t)G.T * max_points));
+    HIPCHECK(hipMalloc(&pl->tabs.A, sizeof(double) * (size_t)gd.PT * max_points));
+    *out = pl.release();
+    return NUSI_OK;
+}
+
+int nusi_plan_load_phiphi(nusi_plan* pl, const char* at_path, const int* at_dims, const char* a_path, const int* a_dims)
+{
+    static const int def2[2] = {5000, 100}, def3[3] = {1000, 1000, 100};
+    HIPCHECK(hipSetDevice(pl->device));
+    auto st = std::make_shared<SplineStore>();
+    st->device = pl->device;
+    int r = load_spline(at_path, 2, at_dims ? at_dims : def2, *st, st->set.at);
+    if (r) return r;
+    r = load_spline(a_path, 3, a_dims ? a_dims : def3, *st, st->set.a);
+    if (r) return r;
+    pl->spl = st;
+    return NUSI_OK;
+}
+
+int nusi_plan_grid(const nusi_plan* pl, int* N, int* Nz, double* Enu)
+{
+    if (N) *N = pl->grid.N;
+    if (Nz) *Nz = pl->grid.Nz;
+    if (Enu) memcpy(Enu, pl->grid.Enu.data(), sizeof(double) * pl->grid.N);
+    return NUSI_OK;
+}
+
+int nusi_plan_evolve(nusi_plan* pl, const nusi_params* pts, int n, double* d_flux, double* d_fla, void* stream)
+{
+    if (n < 1 || n > pl->max_points) return fail(NUSI_EPARAM, "number of points outside [1, max_points]");
+    HIPCHECK(hipSetDevice(pl->device));
+    hipStream_t s = stream ? (hipStream_t)stream : pl->stream;
+    if (pl->ran) HIPCHECK(hipEventSynchronize(pl->ev_copy));   // h_pts is reused
+    for (int i = 0; i < n; ++i) {
+        const int r = build_point(pl, pts[i], pl->h_pts[i]);
+        if (r) return r;
+    }
+    const size_t N3 = (size_t)3 * pl->grid.N;
+    if (!d_flux || !d_fla) {
+        if (!pl->d_scratch) HIPCHECK(hipMalloc(&pl->d_scratch, sizeof(double) * 2 * N3 * pl->max_points));
+        if (!d_flux) d_flux = pl->d_scratch;
+        if (!d_fla) d_fla = pl->d_scratch + N3 * pl->max_points;
+    }
+    HIPCHECK(hipMemcpyAsync(pl->d_pts, pl->h_pts, sizeof(nusi::Point) * n, hipMemcpyHostToDevice, s));
+    HIPCHECK(hipEventRecord(pl->ev_copy, s));
+    HIPCHECK(hipMemsetAsync(pl->d_warn, 0, sizeof(int) * n, s));
+    const nusi::SplineSet spl = pl->spl ? pl->spl->set : nusi::SplineSet{};
+    HIPCHECK(hipEventRecord(pl->ev[0], s));
+    HIPCHECK(nusi::launch_gamma_alphat(pl->gd, pl->d_pts, n, spl, pl->tabs, pl->d_warn, s));
+    HIPCHECK(hipEventRecord(pl->ev[1], s));
+    HIPCHECK(nusi::launch_alpha(pl->gd, pl->d_pts, n, spl, pl->tabs, pl->d_warn, s));
+    HIPCHECK(hipEventRecord(pl->ev[2], s));
+    HIPCHECK(nusi::launch_cascade(pl->gd, pl->d_pts, n, pl->tabs, d_flux, d_fla, s));
+    HIPCHECK(hipEventRecord(pl->ev[3], s));
+    pl->ran = true;
+    pl->last_n = n;
+    return NUSI_OK;
+}
+
+int nusi_plan_stage_ms(nusi_plan* pl, float* ms3)
+{
+    if (!pl->ran) return fail(NUSI_ESTATE, "no evolve has run on this plan");
+    HIPCHECK(hipSetDevice(pl->device));
+    HIPCHECK(hipEventSynchronize(pl->ev[3]));
+    for (int k = 0; k < 3; ++k) HIPCHECK(hipEventElapsedTime(&ms3[k], pl->ev[k], pl->ev[k + 1]));
+    return NUSI_OK;
+}
+
+int nusi_plan_warnings(nusi_plan* pl, int* out, int n)
+{
+    if (!pl->ran) return fail(NUSI_ESTATE, "no evolve has run on this plan");
+    if (n > pl->last_n) n = pl->last_n;
+    HIPCHECK(hipSetDevice(pl->device));
+    HIPCHECK(hipEventSynchronize(pl->ev[3]));
+    HIPCHECK(hipMemcpy(out, pl->d_warn, sizeof(int) * n, hipMemcpyDeviceToHost));
+    return NUSI_OK;
+}
+
+int nusi_plan_tables(nusi_plan* pl, int i, double* G, double* At, double* A)
+{
+    if (!pl->ran) return fail(NUSI_ESTATE, "no evolve has run on this plan");
+    if (i < 0 || i >= pl->last_n) return fail(NUSI_EPARAM, "point index out of range");
+    HIPCHECK(hipSetDevice(pl->device));
+    HIPCHECK(hipEventSynchronize(pl->ev[3]));
+    const size_t T = (size_t)pl->gd.T, PT = (size_t)pl->gd.PT;
+    if (G) HIPCHECK(hipMemcpy(G, pl->tabs.G + T * i, sizeof(double) * T, hipMemcpyDeviceToHost));
+    if (At) HIPCHECK(hipMemcpy(At, pl->tabs.At + T * i, sizeof(double) * T, hipMemcpyDeviceToHost));
+    if (A) HIPCHECK(hipMemcpy(A, pl->tabs.A + PT * i, sizeof(double) * PT, hipMemcpyDeviceToHost));
+    return NUSI_OK;
+}
+
+int nusi_plan_evolve_host(nusi_plan* pl, const nusi_params* pts, int n, double* flux, double* fla)
+{
+    int r = nusi_plan_evolve(pl, pts, n, nullptr, nullptr, nullptr);
+    if (r) return r;
+    const size_t N3 = (size_t)3 * pl->grid.N;
+    HIPCHECK(hipStreamSynchronize(pl->stream));
+    int bad = 0;
+    std::vector<int> w(n);
+    HIPCHECK(hipMemcpy(w.data(), pl->d_warn, sizeof(int) * n, hipMemcpyDeviceToHost));
+    for (int i = 0; i < n; ++i) bad |= (w[i] & nusi::kWarnSplineOOB);
+    if (bad) return fail(NUSI_EINTERP, "Error at interp: a phi-phi table lookup fell outside the node range");
+    if (flux) HIPCHECK(hipMemcpy(flux, pl->d_scratch, sizeof(double) * N3 * n, hipMemcpyDeviceToHost));
+    if (fla) HIPCHECK(hipMemcpy(fla, pl->d_scratch + N3 * pl->max_points, sizeof(double) * N3 * n, hipMemcpyDeviceToHost));
+    return NUSI_OK;
+}
+
+int nusi_evolve_batch(int device, const nusi_params* pts, int n, double* flux, double* fla)
+{
+    if (n < 1) return fail(NUSI_EPARAM, "n must be >= 1");
+    nusi_plan* pl = nullptr;
+    int r = nusi_plan_create(device, pts[0].N_bins_E, pts[0].lEmin, pts[0].lEmax, pts[0].zmax, n, &pl);
+    if (r) return r;
+    r = nusi_plan_evolve_host(pl, pts, n, flux, fla);
+    nusi_plan_destroy(pl);
+    return r;
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------------------
+// object API
+// ---------------------------------------------------------------------------
+struct nusi_handle {
+    nusi_params p{};
+    nusi_plan* plan = nullptr;
+    std::vector<double> flux, fla;
+    double norm_total = 0.0;   // of the last evolve() (stale in check_energy_conservation)
+    int warn = 0;
+    ~nusi_handle() { nusi_plan_destroy(plan); }
+};
+
+extern "C" {
+
+static int open_handle(const nusi_params* p, const std::shared_ptr<SplineStore>* share, nusi_handle** out)
+{
+    *out = nullptr;
+    if (p->flav < 0 || p->flav > 2) return fail(NUSI_EPARAM, "flav must be 0, 1 or 2");
+    int dev = 0;
+    if (const char* e = getenv("NUSI_DEVICE")) dev = atoi(e);
+    std::unique_ptr<nusi_handle> h(new nusi_handle);
+    h->p = *p;
+    int r = nusi_plan_create(dev, p->N_bins_E, p->lEmin, p->lEmax, p->zmax, 1, &h->plan);
+    if (r) return r;
+    if (p->non_resonant && p->phiphi) {   // nuSIprop.hpp:166-170
+        if (share && *share) h->plan->spl = *share;
+        else {
+            std::string dir = "xsec";
+            if (const char* e = getenv("NUSI_XSEC_DIR")) dir = e;
+            r = nusi_plan_load_phiphi(h->plan, (dir + "/alphatilde_phiphi.bin").c_str(), nullptr,
+                                      (dir + "/alpha_phiphi.bin").c_str(), nullptr);
+            if (r) return r;
+        }
+    }
+    h->flux.assign((size_t)3 * p->N_bins_E, 0.0);
+    h->fla.assign((size_t)3 * p->N_bins_E, 0.0);
+    *out = h.release();
+    return NUSI_OK;
+}
+
+int nusi_create(const nusi_params* p, nusi_handle** out) { return open_handle(p, nullptr, out); }
+
+int nusi_copy(const nusi_handle* src, nusi_handle** out)
+{
+    int r = open_handle(&src->p, &src->plan->spl, out);
+    if (r) return r;
+    (*out)->flux = src->flux;
+    (*out)->fla = src->fla;
+    (*out)->norm_total = src->norm_total;
+    (*out)->warn = src->warn;
+    return NUSI_OK;
+}
+
+void nusi_destroy(nusi_handle* h) { delete h; }
+
+int nusi_set_params(nusi_handle* h, double mphi, double g, double mntot, double si, double norm)
+{
+    h->p.mphi = mphi;
+    h->p.g = g;
+    h->p.mntot = mntot;
+    h->p.si = si;
+    h->p.norm = norm;
+    return NUSI_OK;
+}
+
+int nusi_get_params(const nusi_handle* h, double* v)
+{
+    v[0] = h->p.mphi;
+    v[1] = h->p.g;
+    v[2] = h->p.mntot;
+    v[3] = h->p.si;
+    v[4] = h->p.norm;
+    return NUSI_OK;
+}
+
+int nusi_evolve(nusi_handle* h)
+{
+    int r = nusi_plan_evolve_host(h->plan, &h->p, 1, h->flux.data(), h->fla.data());
+    if (r) return r;
+    h->norm_total = h->plan->h_pts[0].norm_total;
+    int w = 0;
+    r = nusi_plan_warnings(h->plan, &w, 1);
+    h->warn = w & (NUSI_WARN_GAMMA | NUSI_WARN_ALPHATILDE | NUSI_WARN_ALPHA);
+    return r;
+}
+
+int nusi_check_energy_conservation(nusi_handle* h, double* out)
+{
+    const HostGrid& G = h->plan->grid;
+    const double E_FS = energy_fs(h->p.si, h->norm_total, G.zmax_eff, G.lEmin, G.lEmax);
+    int r = nusi_evolve(h);
+    if (r) return r;
+    double E_int = 0;
+    const int N = G.N;
+    for (int i = 0; i < N; ++i)
+        for (int k = 0; k < 3; ++k) E_int += (log(G.Emax[i]) - log(G.Emin[i])) * sq(G.Enu[i]) * h->flux[(size_t)k * N + i];
+    *out = (E_int - E_FS) / E_FS;
+    return NUSI_OK;
+}
+
+int nusi_get_flux(const nusi_handle* h, double* out)
+{
+    memcpy(out, h->flux.data(), sizeof(double) * h->flux.size());
+    return NUSI_OK;
+}
+int nusi_get_flux_fla(const nusi_handle* h, double* out)
+{
+    memcpy(out, h->fla.data(), sizeof(double) * h->fla.size());
+    return NUSI_OK;
+}
+int nusi_get_energies(const nusi_handle* h, double* out)
+{
+    memcpy(out, h->plan->grid.Enu.data(), sizeof(double) * h->plan->grid.N);
+    return NUSI_OK;
+}
+int nusi_get_N_bins_E(const nusi_handle* h) { return h->plan->grid.N; }
+int nusi_get_N_steps_z(const nusi_handle* h) { return h->plan->grid.Nz; }
+int nusi_get_warnings(const nusi_handle* h) { return h->warn; }
+
+}  // extern "C"

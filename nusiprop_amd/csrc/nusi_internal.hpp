@@ -1,0 +1,41 @@
+// nuSIprop MI355X -- internal interfaces between the C-ABI host layer and the kernels.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include "nusi_physics.hpp"
+
+namespace nusi {
+
+// Grid shared by every point of a batch (constructor, nuSIprop.hpp:113-128, and
+// the table axis of evolve(), nuSIprop.hpp:224-233).  Device pointers.
+struct GridDev {
+    int N, Nz, T;
+    long long PT;          // alpha entries per point = T(T-1)/2
+    const double* Emin;    // [N]
+    const double* Emax;    // [N]
+    const double* lo;      // [T] table-axis bin edges
+    const double* hi;      // [T]
+    const double* z;       // [Nz]
+    const double* step_c;  // [Nz] c_i = (1+z[i-1]) dlogz / H(z[i-1]), index i (0 unused)
+    const double* step_s;  // [Nz] s_i = n_nu(z[i-1]) / (1+z[i-1])^2
+    const double* sfr;     // [Nz] get_SFR(z[i])
+};
+
+// Device tables of one batch.  alpha is stored transposed and packed:
+// alpha(n, m), n < m, lives at m(m-1)/2 + n, so that the cascade's column
+// reads (all n < m for one m) are contiguous.
+struct TablesDev {
+    double* G;    // [npts][T]
+    double* At;   // [npts][T]
+    double* A;    // [npts][PT]
+};
+
+hipError_t launch_gamma_alphat(const GridDev& g, const Point* pts, int npts, const SplineSet& spl, TablesDev t,
+                               int* warn, hipStream_t s);
+hipError_t launch_alpha(const GridDev& g, const Point* pts, int npts, const SplineSet& spl, TablesDev t, int* warn,
+                        hipStream_t s);
+hipError_t launch_cascade(const GridDev& g, const Point* pts, int npts, TablesDev t, double* flux, double* flux_fla,
+                          hipStream_t s);
+
+}  // namespace nusi

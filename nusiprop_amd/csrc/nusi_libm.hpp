@@ -1,0 +1,350 @@
+// nuSIprop MI355X -- elementary functions with a fixed fp64 operation sequence.
+//
+// Why: the reference's interaction integrals (nuSIprop.hpp:759-1520) cancel
+// catastrophically for small |t|, s' (mphi >> sqrt(2 m E)): a 1-ulp change in
+// a log or dilog moves some table entries by ~1e-5 relative.  The reference's
+// own output therefore depends on the last bits of its libm/GSL.  To make the
+// GPU reproduce the CPU oracle bit for bit, both evaluate these functions with
+// the same algorithm built only from IEEE-correctly-rounded operations
+// (+ - * / sqrt fma) -- the GPU's ocml and the host's glibc differ in the last
+// ulp.  Algorithms: Sun fdlibm 5.3 (e_log.c, s_log1p.c, e_exp.c, s_atan.c,
+// e_atan2.c, e_atanh.c, e_log10.c; "Developed at SunPro ... Permission to
+// use, copy, modify, and distribute this software is freely granted, provided
+// that this notice is preserved."), error < 1 ulp each.  pow(x>0, y) =
+// exp(y*log(x)) (a few ulp; only the power-law source uses it).
+// The oracle carries its own C copy of the same algorithms (oracle/ora_libm.c).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <math.h>
+
+#ifndef NUSI_FN
+#define NUSI_FN __host__ __device__ inline
+#endif
+
+namespace nusi {
+namespace nm {
+
+NUSI_FN unsigned long long bits(double x) { return __builtin_bit_cast(unsigned long long, x); }
+NUSI_FN double from_bits(unsigned long long b) { return __builtin_bit_cast(double, b); }
+NUSI_FN int hiw(double x) { return (int)(bits(x) >> 32); }
+NUSI_FN unsigned low(double x) { return (unsigned)bits(x); }
+NUSI_FN double with_hi(double x, int hi)
+{
+    return from_bits((bits(x) & 0xffffffffULL) | ((unsigned long long)(unsigned)hi << 32));
+}
+
+constexpr double ln2_hi = 6.93147180369123816490e-01, ln2_lo = 1.90821492927058770002e-10;
+constexpr double two54 = 1.80143985094819840000e+16;
+constexpr double Lg1 = 6.666666666666735130e-01, Lg2 = 3.999999999940941908e-01, Lg3 = 2.857142874366239149e-01,
+                 Lg4 = 2.222219843214978396e-01, Lg5 = 1.818357216161805012e-01, Lg6 = 1.531383769920937332e-01,
+                 Lg7 = 1.479819860511658591e-01;
+
+// e_log.c
+NUSI_FN double log(double x)
+{
+    int hx = hiw(x);
+    const unsigned lx = low(x);
+    int k = 0;
+    if (hx < 0x00100000) {                       // x < 2^-1022
+        if (((hx & 0x7fffffff) | lx) == 0) return -1.0 / 0.0;
+        if (hx < 0) return (x - x) / 0.0;
+        k -= 54;
+        x *= two54;
+        hx = hiw(x);
+    }
+    if (hx >= 0x7ff00000) return x + x;
+    k += (hx >> 20) - 1023;
+    hx &= 0x000fffff;
+    int i = (hx + 0x95f64) & 0x100000;
+    x = with_hi(x, hx | (i ^ 0x3ff00000));       // normalise x or x/2
+    k += (i >> 20);
+    const double f = x - 1.0;
+    if ((0x000fffff & (2 + hx)) < 3) {           // |f| < 2^-20
+        if (f == 0.0) {
+            if (k == 0) return 0.0;
+            const double dk = (double)k;
+            return dk * ln2_hi + dk * ln2_lo;
+        }
+        const double R = f * f * (0.5 - 0.33333333333333333 * f);
+        if (k == 0) return f - R;
+        const double dk = (double)k;
+        return dk * ln2_hi - ((R - dk * ln2_lo) - f);
+    }
+    const double s = f / (2.0 + f);
+    const double dk = (double)k;
+    const double z = s * s;
+    i = hx - 0x6147a;
+    const double w = z * z;
+    const int j = 0x6b851 - hx;
+    const double t1 = w * (Lg2 + w * (Lg4 + w * Lg6));
+    const double t2 = z * (Lg1 + w * (Lg3 + w * (Lg5 + w * Lg7)));
+    i |= j;
+    const double R = t2 + t1;
+    if (i > 0) {
+        const double hfsq = 0.5 * f * f;
+        if (k == 0) return f - (hfsq - s * (hfsq + R));
+        return dk * ln2_hi - ((hfsq - (s * (hfsq + R) + dk * ln2_lo)) - f);
+    }
+    if (k == 0) return f - s * (f - R);
+    return dk * ln2_hi - ((s * (f - R) - dk * ln2_lo) - f);
+}
+
+// s_log1p.c
+NUSI_FN double log1p(double x)
+{
+    const int hx = hiw(x);
+    const int ax = hx & 0x7fffffff;
+    int k = 1, hu = 0;
+    double f = 0.0, c = 0.0;
+    if (hx < 0x3FDA827A) {                       // x < 0.41422
+        if (ax >= 0x3ff00000) {                  // x <= -1
+            if (x == -1.0) return -1.0 / 0.0;
+            return (x - x) / (x - x);
+        }
+        if (ax < 0x3e200000) {                   // |x| < 2^-29
+            if (ax < 0x3c900000) return x;       // |x| < 2^-54
+            return x - x * x * 0.5;
+        }
+        if (hx > 0 || hx <= (int)0xbfd2bec3) {   // -0.2929 < x < 0.41422
+            k = 0;
+            f = x;
+            hu = 1;
+        }
+    }
+    if (hx >= 0x7ff00000) return x + x;
+    if (k != 0) {
+        double u;
+        if (hx < 0x43400000) {
+            u = 1.0 + x;
+            hu = hiw(u);
+            k = (hu >> 20) - 1023;
+            c = (k > 0) ? 1.0 - (u - x) : x - (u - 1.0);   // correction term
+            c /= u;
+        } else {
+            u = x;
+            hu = hiw(u);
+            k = (hu >> 20) - 1023;
+            c = 0;
+        }
+        hu &= 0x000fffff;
+        if (hu < 0x6a09e) {
+            u = with_hi(u, hu | 0x3ff00000);     // normalise u
+        } else {
+            k += 1;
+            u = with_hi(u, hu | 0x3fe00000);     // normalise u/2
+            hu = (0x00100000 - hu) >> 2;
+        }
+        f = u - 1.0;
+    }
+    const double hfsq = 0.5 * f * f;
+    if (hu == 0) {                               // |f| < 2^-20
+        if (f == 0.0) {
+            if (k == 0) return 0.0;
+            c += k * ln2_lo;
+            return k * ln2_hi + c;
+        }
+        const double R = hfsq * (1.0 - 0.66666666666666666 * f);
+        if (k == 0) return f - R;
+        return k * ln2_hi - ((R - (k * ln2_lo + c)) - f);
+    }
+    const double s = f / (2.0 + f);
+    const double z = s * s;
+    const double R = z * (Lg1 + z * (Lg2 + z * (Lg3 + z * (Lg4 + z * (Lg5 + z * (Lg6 + z * Lg7))))));
+    if (k == 0) return f - (hfsq - s * (hfsq + R));
+    return k * ln2_hi - ((hfsq - (s * (hfsq + R) + (k * ln2_lo + c))) - f);
+}
+
+// e_exp.c
+NUSI_FN double exp(double x)
+{
+    constexpr double invln2 = 1.44269504088896338700e+00;
+    constexpr double P1 = 1.66666666666666019037e-01, P2 = -2.77777777770155933842e-03,
+                     P3 = 6.61375632143793436117e-05, P4 = -1.65339022054652515390e-06,
+                     P5 = 4.13813679705723846039e-08;
+    constexpr double o_threshold = 7.09782712893383973096e+02, u_threshold = -7.45133219101941108420e+02;
+    constexpr double twom1000 = 9.33263618503218878990e-302;
+    int hx = hiw(x);
+    const int xsb = (hx >> 31) & 1;
+    hx &= 0x7fffffff;
+    if (hx >= 0x40862E42) {                      // |x| >= 709.78
+        if (hx >= 0x7ff00000) {
+            if (((hx & 0xfffff) | low(x)) != 0) return x + x;   // NaN
+            return (xsb == 0) ? x : 0.0;
+        }
+        if (x > o_threshold) return 1.0 / 0.0;
+        if (x < u_threshold) return 0.0;
+    }
+    double hi = 0.0, lo = 0.0;
+    int k = 0;
+    if (hx > 0x3fd62e42) {                       // |x| > 0.5 ln2
+        if (hx < 0x3FF0A2B2) {                   // and |x| < 1.5 ln2
+            hi = xsb ? x + ln2_hi : x - ln2_hi;
+            lo = xsb ? -ln2_lo : ln2_lo;
+            k = 1 - xsb - xsb;
+        } else {
+            k = (int)(invln2 * x + (xsb ? -0.5 : 0.5));
+            const double t = k;
+            hi = x - t * ln2_hi;                 // t*ln2_hi is exact here
+            lo = t * ln2_lo;
+        }
+        x = hi - lo;
+    } else if (hx < 0x3e300000) {                // |x| < 2^-28
+        return 1.0 + x;
+    }
+    const double t = x * x;
+    const double c = x - t * (P1 + t * (P2 + t * (P3 + t * (P4 + t * P5))));
+    if (k == 0) return 1.0 - ((x * c) / (c - 2.0) - x);
+    const double y = 1.0 - ((lo - (x * c) / (2.0 - c)) - hi);
+    if (k >= -1021) return from_bits(bits(y) + ((unsigned long long)(long long)k << 52));
+    return from_bits(bits(y) + ((unsigned long long)(long long)(k + 1000) << 52)) * twom1000;
+}
+
+// s_atan.c
+NUSI_FN double atan(double x)
+{
+    constexpr double atanhi[4] = {4.63647609000806093515e-01, 7.85398163397448278999e-01, 9.82793723247329054082e-01,
+                                  1.57079632679489655800e+00};
+    constexpr double atanlo[4] = {2.26987774529616870924e-17, 3.06161699786838301793e-17, 1.39033110312309984516e-17,
+                                  6.12323399573676603587e-17};
+    constexpr double aT[11] = {3.33333333333329318027e-01,  -1.99999999998764832476e-01, 1.42857142725034663711e-01,
+                               -1.11111104054623557880e-01, 9.09088713343650656196e-02,  -7.69187620504482999495e-02,
+                               6.66107313738753120669e-02,  -5.83357013379057348645e-02, 4.97687799461593236017e-02,
+                               -3.65315727442169155270e-02, 1.62858201153657823623e-02};
+    const int hx = hiw(x);
+    const int ix = hx & 0x7fffffff;
+    int id;
+    if (ix >= 0x44100000) {                      // |x| >= 2^66
+        if (ix > 0x7ff00000 || (ix == 0x7ff00000 && low(x) != 0)) return x + x;
+        return (hx > 0) ? atanhi[3] + atanlo[3] : -atanhi[3] - atanlo[3];
+    }
+    if (ix < 0x3fdc0000) {                       // |x| < 0.4375
+        if (ix < 0x3e200000) return x;           // |x| < 2^-29
+        id = -1;
+    } else {
+        x = fabs(x);
+        if (ix < 0x3ff30000) {                   // |x| < 1.1875
+            if (ix < 0x3fe60000) {               // 7/16 <= |x| < 11/16
+                id = 0;
+                x = (2.0 * x - 1.0) / (2.0 + x);
+            } else {                             // 11/16 <= |x| < 19/16
+                id = 1;
+                x = (x - 1.0) / (x + 1.0);
+            }
+        } else {
+            if (ix < 0x40038000) {               // |x| < 2.4375
+                id = 2;
+                x = (x - 1.5) / (1.0 + 1.5 * x);
+            } else {                             // 2.4375 <= |x| < 2^66
+                id = 3;
+                x = -1.0 / x;
+            }
+        }
+    }
+    const double z = x * x;
+    const double w = z * z;
+    const double s1 = z * (aT[0] + w * (aT[2] + w * (aT[4] + w * (aT[6] + w * (aT[8] + w * aT[10])))));
+    const double s2 = w * (aT[1] + w * (aT[3] + w * (aT[5] + w * (aT[7] + w * aT[9]))));
+    if (id < 0) return x - x * (s1 + s2);
+    const double r = atanhi[id] - ((x * (s1 + s2) - atanlo[id]) - x);
+    return (hx < 0) ? -r : r;
+}
+
+// e_atan2.c
+NUSI_FN double atan2(double y, double x)
+{
+    constexpr double pi_o_2 = 1.5707963267948965580E+00, pi = 3.1415926535897931160E+00,
+                     pi_lo = 1.2246467991473531772E-16, pi_o_4 = 7.8539816339744827900E-01;
+    const int hx = hiw(x), hy = hiw(y);
+    const unsigned lx = low(x), ly = low(y);
+    const int ix = hx & 0x7fffffff, iy = hy & 0x7fffffff;
+    if (((unsigned)ix | ((lx | (0u - lx)) >> 31)) > 0x7ff00000u || ((unsigned)iy | ((ly | (0u - ly)) >> 31)) > 0x7ff00000u)
+        return x + y;                            // NaN
+    if (((hx - 0x3ff00000) | (int)lx) == 0) return atan(y);   // x = 1.0
+    const int m = ((hy >> 31) & 1) | ((hx >> 30) & 2);         // 2*sign(x)+sign(y)
+    if ((iy | (int)ly) == 0) {                   // y = 0
+        switch (m) {
+        case 0:
+        case 1: return y;
+        case 2: return pi;
+        default: return -pi;
+        }
+    }
+    if ((ix | (int)lx) == 0) return (hy < 0) ? -pi_o_2 : pi_o_2;
+    if (ix == 0x7ff00000) {                      // x = +-inf
+        if (iy == 0x7ff00000) {
+            switch (m) {
+            case 0: return pi_o_4;
+            case 1: return -pi_o_4;
+            case 2: return 3.0 * pi_o_4;
+            default: return -3.0 * pi_o_4;
+            }
+        }
+        switch (m) {
+        case 0: return 0.0;
+        case 1: return -0.0;
+        case 2: return pi;
+        default: return -pi;
+        }
+    }
+    if (iy == 0x7ff00000) return (hy < 0) ? -pi_o_2 : pi_o_2;
+    const int k = (iy - ix) >> 20;
+    double z;
+    if (k > 60) z = pi_o_2 + 0.5 * pi_lo;        // |y/x| > 2^60
+    else if (hx < 0 && k < -60) z = 0.0;         // |y|/x < -2^60
+    else z = atan(fabs(y / x));
+    switch (m) {
+    case 0: return z;
+    case 1: return -z;
+    case 2: return pi - (z - pi_lo);
+    default: return (z - pi_lo) - pi;
+    }
+}
+
+// e_atanh.c
+NUSI_FN double atanh(double x)
+{
+    const int hx = hiw(x);
+    const int ix = hx & 0x7fffffff;
+    if (ix > 0x3ff00000 || (ix == 0x3ff00000 && low(x) != 0)) return (x - x) / (x - x);   // |x| > 1
+    if (ix == 0x3ff00000 && low(x) == 0) return x / 0.0;
+    if (ix < 0x3e300000) return x;               // |x| < 2^-28
+    const double ax = fabs(x);
+    double t;
+    if (ix < 0x3fe00000) {                       // |x| < 0.5
+        t = ax + ax;
+        t = 0.5 * log1p(t + t * ax / (1.0 - ax));
+    } else
+        t = 0.5 * log1p((ax + ax) / (1.0 - ax));
+    return (hx >= 0) ? t : -t;
+}
+
+// e_log10.c
+NUSI_FN double log10(double x)
+{
+    constexpr double ivln10 = 4.34294481903251816668e-01, log10_2hi = 3.01029995663611771306e-01,
+                     log10_2lo = 3.69423907715893078616e-13;
+    int hx = hiw(x);
+    int k = 0;
+    if (hx < 0x00100000) {
+        if (((hx & 0x7fffffff) | low(x)) == 0) return -1.0 / 0.0;
+        if (hx < 0) return (x - x) / 0.0;
+        k -= 54;
+        x *= two54;
+        hx = hiw(x);
+    }
+    if (hx >= 0x7ff00000) return x + x;
+    k += (hx >> 20) - 1023;
+    const int i = (int)(((unsigned)k & 0x80000000u) >> 31);
+    hx = (hx & 0x000fffff) | ((0x3ff - i) << 20);
+    const double y = (double)(k + i);
+    x = with_hi(x, hx);
+    const double z = y * log10_2lo + ivln10 * log(x);
+    return z + y * log10_2hi;
+}
+
+// x > 0
+NUSI_FN double pow(double x, double y) { return exp(y * log(x)); }
+
+}  // namespace nm
+}  // namespace nusi

@@ -1,0 +1,257 @@
+// nuSIprop MI355X -- fp64 special functions for the table-build kernels.
+//
+// Replaces the reference's third-party arithmetic boundary:
+//   gsl_sf_dilog                 aux.hpp:112,129,147,165  nuSIprop.hpp:1098,1202,1375-1398
+//   gsl_sf_complex_dilog_xy_e    aux.hpp:92-93            nuSIprop.hpp:1444-1451
+//   polylogarithm::Li2 / Li3     nuSIprop.hpp:628-636
+// and restates the cancellation-safe differences of aux.hpp:63-166.
+//
+// Algorithms are branch-light so that a wavefront stays converged:
+//   * real / complex Li2: map z -> 1/z (|z| > 1) and z -> 1-z (Re z > 1/2),
+//     then the Bernoulli series in u = -log(1-z) (|u| <= pi/3) -- one log1p
+//     and a fixed-length Horner polynomial, no data-dependent iteration count;
+//   * Li3 on [-1, 1/2]: Taylor series of Li3(1 - e^-u), |u| <= ln 2.
+// GSL conventions kept: gsl_sf_dilog(x>1) = Re Li2(x); complex dilog on the
+// real axis (y == 0) has Im = -pi*log(x) for x >= 1 and 0 below.
+//
+// Everything is NUSI_FN (host+device) so that tests/ can compile the same
+// source for the CPU and check it against the oracle; the product library
+// only ever executes it on the GPU.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <math.h>
+
+#include "nusi_coeffs.hpp"
+#include "nusi_libm.hpp"
+
+#define NUSI_FN __host__ __device__ inline
+
+namespace nusi {
+
+constexpr double kPi = 3.14159265358979323846;
+constexpr double kZeta2 = 1.64493406684822643647;  // pi^2/6
+
+// ---------------------------------------------------------------------------
+// complex double with C99 `double _Complex` semantics (GNU C): real operands
+// are not promoted in +,-,* ; division uses Smith's algorithm like libgcc's
+// __divdc3 does for finite operands.
+// ---------------------------------------------------------------------------
+struct cd {
+    double r, i;
+};
+NUSI_FN cd C(double r, double i = 0.0) { return cd{r, i}; }
+NUSI_FN cd operator+(cd a, cd b) { return cd{a.r + b.r, a.i + b.i}; }
+NUSI_FN cd operator-(cd a, cd b) { return cd{a.r - b.r, a.i - b.i}; }
+NUSI_FN cd operator-(cd a) { return cd{-a.r, -a.i}; }
+NUSI_FN cd operator+(cd a, double s) { return cd{a.r + s, a.i}; }
+NUSI_FN cd operator+(double s, cd a) { return cd{s + a.r, a.i}; }
+NUSI_FN cd operator-(cd a, double s) { return cd{a.r - s, a.i}; }
+NUSI_FN cd operator-(double s, cd a) { return cd{s - a.r, -a.i}; }
+NUSI_FN cd operator*(cd a, cd b) { return cd{a.r * b.r - a.i * b.i, a.r * b.i + a.i * b.r}; }
+NUSI_FN cd operator*(double s, cd a) { return cd{s * a.r, s * a.i}; }
+NUSI_FN cd operator*(cd a, double s) { return cd{a.r * s, a.i * s}; }
+NUSI_FN cd operator/(cd a, double s) { return cd{a.r / s, a.i / s}; }
+NUSI_FN cd operator/(cd a, cd b)
+{
+    const double c = b.r, d = b.i;
+    if (fabs(c) < fabs(d)) {
+        const double ratio = c / d, den = (c * ratio) + d;
+        return cd{((a.r * ratio) + a.i) / den, ((a.i * ratio) - a.r) / den};
+    }
+    const double ratio = d / c, den = (d * ratio) + c;
+    return cd{((a.i * ratio) + a.r) / den, (a.i - (a.r * ratio)) / den};
+}
+NUSI_FN cd operator/(double s, cd b) { return C(s) / b; }
+NUSI_FN cd conj(cd a) { return cd{a.r, -a.i}; }
+NUSI_FN double carg(cd z) { return nm::atan2(z.i, z.r); }
+NUSI_FN double carg_real(double x) { return nm::atan2(0.0, x); }  // carg of a real promoted to complex
+NUSI_FN double cabs(cd z) { return sqrt(z.r * z.r + z.i * z.i); }
+NUSI_FN cd clog(cd z) { return cd{0.5 * nm::log(z.r * z.r + z.i * z.i), carg(z)}; }
+NUSI_FN cd clog_real(double x) { return clog(C(x, 0.0)); }   // clog of a promoted real
+NUSI_FN cd sqr(cd a) { return a * a; }
+constexpr cd kI = {0.0, 1.0};
+
+// ---------------------------------------------------------------------------
+// polylogarithms
+// ---------------------------------------------------------------------------
+// u - u^2/4 + sum_k B_2k u^(2k+1)/(2k+1)!  for |u| <= ln 2 (10 terms reach 1e-17)
+NUSI_FN double li2_useries(double u)
+{
+    const double u2 = u * u;
+    double p = kLi2Bern[9];
+#pragma unroll
+    for (int k = 8; k >= 0; --k) p = fma(p, u2, kLi2Bern[k]);
+    return fma(u * u2, p, u - 0.25 * u2);
+}
+
+// Re Li2(x) for real x (gsl_sf_dilog semantics)
+NUSI_FN double li2(double x)
+{
+    double add = 0.0, sgn = 1.0;
+    if (x > 1.0) {
+        const double L = nm::log(x);
+        add = 2.0 * kZeta2 - 0.5 * L * L;
+        sgn = -1.0;
+        x = 1.0 / x;
+    } else if (x < -1.0) {
+        const double L = nm::log(-x);
+        add = -kZeta2 - 0.5 * L * L;
+        sgn = -1.0;
+        x = 1.0 / x;
+    }
+    if (x == 1.0) return add + sgn * kZeta2;
+    if (x > 0.5) {
+        add += sgn * (kZeta2 - nm::log(x) * nm::log1p(-x));
+        sgn = -sgn;
+        x = 1.0 - x;
+    }
+    if (x == 0.0) return add;
+    return add + sgn * li2_useries(-nm::log1p(-x));
+}
+
+// principal-branch Li2(x+iy); y == 0 follows gsl_sf_complex_dilog_xy_e
+NUSI_FN cd cli2(double x, double y)
+{
+    if (y == 0.0) return cd{li2(x), (x >= 1.0) ? -kPi * nm::log(x) : 0.0};
+    cd z = C(x, y), add = C(0.0);
+    double sgn = 1.0;
+    if (x * x + y * y > 1.0) {
+        const cd l = clog(-z);
+        add = -kZeta2 - 0.5 * (l * l);
+        sgn = -1.0;
+        z = 1.0 / z;
+    }
+    if (z.r > 0.5) {
+        add = add + sgn * (kZeta2 - clog(z) * clog(1.0 - z));
+        sgn = -sgn;
+        z = 1.0 - z;
+    }
+    // u = -log(1 - z), formed without the cancellation of 1 - z for small z
+    const double a = -z.r, b = -z.i;
+    const cd u = C(-0.5 * nm::log1p(2.0 * a + (a * a + b * b)), -nm::atan2(b, 1.0 + a));
+    const cd u2 = u * u;
+    cd p = C(kLi2Bern[kLi2Terms - 1]);
+#pragma unroll
+    for (int k = kLi2Terms - 2; k >= 0; --k) p = p * u2 + kLi2Bern[k];
+    const cd s = (u - 0.25 * u2) + (u * u2) * p;
+    return add + sgn * s;
+}
+NUSI_FN cd cli2(cd z) { return cli2(z.r, z.i); }
+
+// Li3(x), x in [-1, 1/2] (the DSNB source only reaches [-1, 0))
+NUSI_FN double li3(double x)
+{
+    const double u = -nm::log1p(-x);
+    double p = kLi3U[kLi3Terms - 1];
+#pragma unroll
+    for (int k = kLi3Terms - 2; k >= 0; --k) p = fma(p, u, kLi3U[k]);
+    return p * u;
+}
+
+// ---------------------------------------------------------------------------
+// aux.hpp restatements (same thresholds and Taylor coefficients)
+// ---------------------------------------------------------------------------
+// 3-point Gauss-Legendre, aux.hpp:53-54
+constexpr double kGLw[3] = {5. / 9., 8. / 9., 5. / 9.};
+constexpr double kGLx[3] = {-0.7745966692414834, 0.0, 0.7745966692414834};  // sqrt(3./5.)
+
+// aux.hpp:63-75
+NUSI_FN double atandiff(double x, double y)
+{
+    if (fabs(x) < 1e2 || fabs(y) < 1e2 || x * y < 0) return nm::atan(x) - nm::atan(y);
+    const double ix = 1. / x, iy = 1. / y;
+    return -ix + ix * ix * ix / 3. - (-iy + iy * iy * iy / 3.);
+}
+
+// large-|z| Li2 used by aux.hpp:84-89
+NUSI_FN cd li2_asym(cd z)
+{
+    const double s = (z.i >= 0) ? 1.0 : -1.0;
+    const cd L = clog(z);
+    const cd z2 = z * z;
+    const cd t = (-s * 2 * kPi) * L - kI * (L * L);
+    return -1 / (16. * (z2 * z2)) - 1 / (9. * (z * z * z)) - 1 / (4. * z2) - 1 / z - C(0.0, 0.5) * t;
+}
+
+// aux.hpp:77-96
+NUSI_FN cd dilogdiff_c(cd x, cd y)
+{
+    if (cabs(x) > 1e2 && cabs(y) > 1e2) return li2_asym(x) - li2_asym(y);
+    const cd a = cli2(x), b = cli2(y);
+    return C(a.r - b.r, a.i - b.i);
+}
+
+// aux.hpp:98-113 : Li2(-x) - Li2(-y)
+NUSI_FN double dilogdiff(double x, double y)
+{
+    if (x > 1e2 && y > 1e2) {
+        const double lx = nm::log(x), ly = nm::log(y), ix = 1. / x, iy = 1. / y;
+        return -lx * lx / 2. + ix - ix * ix / 4. + ix * ix * ix / 9. - (ix * ix) * (ix * ix) / 16
+               - (-ly * ly / 2. + iy - iy * iy / 4. + iy * iy * iy / 9. - (iy * iy) * (iy * iy) / 16);
+    }
+    if (x < 1e-2 && y < 1e-2)
+        return -x + x * x / 4. - x * x * x / 9. + (x * x) * (x * x) / 16.
+               - (-y + y * y / 4. - y * y * y / 9. + (y * y) * (y * y) / 16.);
+    return li2(-x) - li2(-y);
+}
+
+// aux.hpp:115-130 : Li2(-1-x) - Li2(-1-y)
+NUSI_FN double d1m_big(double v)
+{
+    const double l = nm::log(v);
+    return -l * l / 2. + (1 - l) / v + (-7 + 2 * l) / (4. * (v * v)) + (19 - 3 * l) / (9. * (v * v * v))
+           + (-125 + 12 * l) / (48. * ((v * v) * (v * v)));
+}
+NUSI_FN double d1m_small(double v)
+{
+    const double ln2 = 0.6931471805599453, ln4 = 1.3862943611198906;
+    return -v * ln2 + (v * v * (-1 + ln4)) / 4. + (v * v * v * (5 - 8 * ln2)) / 24.
+           + (v * v) * (v * v) * (-1. / 6. + ln2 / 4.);
+}
+NUSI_FN double dilog1mdiff(double x, double y)
+{
+    if (x > 1e2 && y > 1e2) return d1m_big(x) - d1m_big(y);
+    if (x < 1e-2 && y < 1e-2) return d1m_small(x) - d1m_small(y);
+    return li2(-1 - x) - li2(-1 - y);
+}
+
+// aux.hpp:132-148 : Li2(1+x) - Li2(1+y), x,y < 0
+NUSI_FN double d1p_big(double v)
+{
+    const double l = nm::log(-v);
+    return (-1 - 3 * l) / (9. * (v * v * v)) + (-1 - l) / v - l * l / 2. + (1 + 2 * l) / (4. * (v * v))
+           + (1 + 4 * l) / (16. * ((v * v) * (v * v)));
+}
+NUSI_FN double d1p_small(double v)
+{
+    const double l = nm::log(-v);
+    return v * (1 - l) + (v * v * (-1 + 2 * l)) / 4. + (v * v * v * (1 - 3 * l)) / 9.
+           + ((v * v) * (v * v) * (-1 + 4 * l)) / 16.;
+}
+NUSI_FN double dilog1pdiff(double x, double y)
+{
+    if (-x > 1e2 && -y > 1e2) return d1p_big(x) - d1p_big(y);
+    if (-x < 1e-2 && -y < 1e-2) return d1p_small(x) - d1p_small(y);
+    return li2(1 + x) - li2(1 + y);
+}
+
+// aux.hpp:150-166 : Li2(1/(1-x)) - Li2(1/(1-y)), x,y < 0
+NUSI_FN double d1o_big(double v)
+{
+    return -25 / (48. * ((v * v) * (v * v))) - 11 / (18. * (v * v * v)) - 3 / (4. * (v * v)) - 1 / v;
+}
+NUSI_FN double d1o_small(double v)
+{
+    const double l = nm::log(-v);
+    return ((v * v) * (v * v) * (-19 - 12 * l)) / 48. + (v * v * v * (-7 - 6 * l)) / 18.
+           + (v * v * (-1 - 2 * l)) / 4. + v * (1 - l);
+}
+NUSI_FN double dilog1over1mdiff(double x, double y)
+{
+    if (-x > 1e2 && -y > 1e2) return d1o_big(x) - d1o_big(y);
+    if (-x < 1e-2 && -y < 1e-2) return d1o_small(x) - d1o_small(y);
+    return li2(1 / (1 - x)) - li2(1 / (1 - y));
+}
+
+}  // namespace nusi

@@ -1,0 +1,568 @@
+// nuSIprop MI355X -- interaction integrals and source term, one table entry per call.
+//
+// Device restatement of calculate_flux's private physics (nuSIprop.hpp):
+//   scalar_width   748-757      gamma_entry       759-922   (absorption Gamma)
+//   alphat_entry   924-1235     (same-bin regeneration alphaTilde)
+//   alpha_entry    1237-1520    (inter-bin regeneration alpha)
+//   Lum / Lum_int / RSN / SFR / H / n_nu  573-662 (DSNB source and the
+//   commented-out power-law source of :656, selected by Point::source)
+// Same formulas, thresholds (Taylor switches, x<0 quadrature fallbacks,
+// |t+1|<1e-7 nudges) and quirks (shadowed alpha_tu fallback :1406) as the
+// reference; repeated sub-expressions are hoisted.  The double-scalar (phi-phi)
+// spline lookups (:1199, :1483) go through a SplineSet (nusi_spline.hpp).
+#pragma once
+
+#include "nusi_math.hpp"
+#include "nusi_spline.hpp"
+
+namespace nusi {
+
+// Per-parameter-point constants, built on the host (nusi_capi.cpp) from the
+// reference's constructor/evolve() set-up (nuSIprop.hpp:130-163, 184-205).
+struct Point {
+    double mphi, g, mntot, si, norm;
+    double norm_total;   // norm / flux_FS_E0()  (nuSIprop.hpp:205)
+    double Ga;           // scalar_width()       (nuSIprop.hpp:748-757)
+    double mn[3];        // masses               (nuSIprop.hpp:191-203)
+    double u[3];         // |U_flav,k|^2
+    double U2[9];        // |U_fk|^2, row-major, for the flavour basis
+    int majorana, non_resonant, phiphi, source;
+};
+
+enum { kWarnGamma = 1, kWarnAlphaTilde = 2, kWarnAlpha = 4, kWarnSplineOOB = 8 };
+
+// ---------------------------------------------------------------------------
+// cosmology and source (nuSIprop.hpp:573-662)
+// ---------------------------------------------------------------------------
+NUSI_FN double lum_int_dsnb(double z, double E)
+{
+    const double T = 6e6;
+    const double ey = nm::exp(-E * (1 + z) / T);
+    const double pref = 1.5252316492673872e-14;  // Etot*120/(6*7*pow(M_PI,4)*pow(Tnue,2)), as libm evaluates it
+    return pref * (-E * E * (1 + z) * nm::log(ey + 1) / T + 2 * E * li2(-ey) + 2 * T * li3(-ey) / (1 + z));
+}
+// integral of the source over [Em,Ep] at redshift z (nuSIprop.hpp:656 / 659-662);
+// sfr_z = get_SFR(z) (nuSIprop.hpp:591-605), a grid quantity computed on the host
+NUSI_FN double lum(const Point& P, double z, double sfr_z, double Em, double Ep)
+{
+    if (P.source == 1) {
+        const double E0 = 1e14, si = P.si;
+        return P.norm_total / 3.0 * sfr_z * (Ep * nm::pow(Ep / E0 * (1 + z), -si) - Em * nm::pow(Em / E0 * (1 + z), -si)) / (1 - si);
+    }
+    const double rsn = sfr_z * 0.01 / (1.989 * 56.1);
+    return (lum_int_dsnb(z, Ep) - lum_int_dsnb(z, Em)) * rsn;
+}
+
+// ---------------------------------------------------------------------------
+// quadrature fallbacks
+// ---------------------------------------------------------------------------
+NUSI_FN double gl3_Gtu_nores(double a, double b)  // nuSIprop.hpp:805-809
+{
+    double s = 0;
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+        const double z = (b - a) / 2. * kGLx[q] + (b + a) / 2.;
+        s += kGLw[q] * ((z + 2) / (z * (z + 1)) - 2 / (z * z) * nm::log1p(z));
+    }
+    return s;
+}
+NUSI_FN double gl3_Gtu_int(double a, double b)  // nuSIprop.hpp:829-833
+{
+    double s = 0;
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+        const double z = (b - a) / 2. * kGLx[q] + (b + a) / 2.;
+        s += kGLw[q] * (1 / z - 2 * (1 + z) / ((z * z) * (2 + z)) * nm::log1p(z));
+    }
+    return s;
+}
+NUSI_FN double gl3_Gpp(double a, double b)  // nuSIprop.hpp:895-900
+{
+    double s = 0;
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+        const double z = (b - a) / 2. * kGLx[q] + (b + a) / 2.;
+        const double r = sqrt(z * (z - 4));
+        const double qq = (r + z - 2) / (r - z + 2);
+        s += kGLw[q] * ((z * z - 4 * z + 6) / ((z * z) * (z - 2)) * nm::log(qq * qq) - 6 * r / (z * z));
+    }
+    return s;
+}
+// kind: 0 = Majorana t (two terms), 1 = Dirac t/u, 2 = t-u interference
+NUSI_FN double Fkernel(int kind, double y, double x)
+{
+    if (kind == 0) {
+        const double a = y / x, b = (-x - y) / x, c = (-x - y) - 1;
+        return (a * a) / ((y - 1) * (y - 1)) + (b * b) / (c * c);
+    }
+    if (kind == 1) {
+        const double a = y / x;
+        return (a * a) / ((y - 1) * (y - 1));
+    }
+    return 2 * y * (-y - x) / (x * x) / ((y - 1) * (-y - x - 1));
+}
+// y in [tp,tm], x in [-y,-tp] (nuSIprop.hpp:987-1003)
+NUSI_FN double gl33_tri(int kind, double tp, double tm)
+{
+    double acc = 0;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        const double y = (tm - tp) / 2. * kGLx[i] + (tm + tp) / 2.;
+        const double ax = -y, bx = -tp;
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            const double x = (bx - ax) / 2. * kGLx[j] + (bx + ax) / 2.;
+            acc += 1. / 4. * (tm - tp) * (bx - ax) * kGLw[i] * kGLw[j] * Fkernel(kind, y, x);
+        }
+    }
+    return acc;
+}
+// y in [tp,tm], x in [Sm,Sp] (nuSIprop.hpp:1288-1301)
+NUSI_FN double gl33_rect(int kind, double tp, double tm, double Sm, double Sp)
+{
+    double acc = 0;
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            const double y = (tm - tp) / 2. * kGLx[i] + (tm + tp) / 2.;
+            const double x = (Sp - Sm) / 2. * kGLx[j] + (Sp + Sm) / 2.;
+            acc += kGLw[i] * kGLw[j] * Fkernel(kind, y, x);
+        }
+    return acc * (1. / 4. * (tm - tp) * (Sp - Sm));
+}
+
+NUSI_FN double gpp_analytic(double a, double b)  // nuSIprop.hpp:885 with a = max(s-,4)
+{
+    const double ra4 = sqrt(-4 + a), ra = sqrt(a), rb4 = sqrt(-4 + b), rb = sqrt(b);
+    const double qa = sqrt((-4 + a) * a), qb = sqrt((-4 + b) * b);
+    const double A1 = ra4 - ra, A2 = -2 + a + qa, A3 = 2 - a + qa, A4 = ra4 + ra;
+    const double B1 = rb4 - rb, B2 = -2 + b + qb, B3 = 2 - b + qb, B4 = rb4 + rb;
+    return 12 * sqrt((-4 + a) / a) - 12 * sqrt((-4 + b) / b)
+           - 2 * nm::log(A1 * A1 / 4.) * nm::log(A2 * A2 / 4.)
+           - ((6 + a * nm::log((-2 + a) * a)) * nm::log(A2 * A2 / (A3 * A3))) / a
+           - 24 * (sqrt((-4 + a) / a) - sqrt((-4 + b) / b) - nm::log(A4) + nm::log(B4))
+           + 2 * nm::log(B1 * B1 / 4.) * nm::log(B2 * B2 / 4.)
+           + ((6 + b * nm::log((-2 + b) * b)) * nm::log(B2 * B2 / (B3 * B3))) / b
+           + 8 * dilogdiff(4 / (A4 * A4), 4 / (B4 * B4))
+           + 2 * dilogdiff(4 / (A2 * A2), 4 / (B2 * B2));
+}
+
+// ---------------------------------------------------------------------------
+// Gamma(Em, Ep)  -- nuSIprop.hpp:759-922
+// ---------------------------------------------------------------------------
+NUSI_FN double gamma_entry(const Point& P, double Em, double Ep, int& warn)
+{
+    const double g = P.g, mphi = P.mphi, Ga = P.Ga;
+    const double g4 = (g * g) * (g * g), m2 = mphi * mphi;
+    const double gr = Ga / mphi, gr2 = gr * gr;
+    double tot = 0;
+    for (int j = 0; j < 3; ++j) {
+        const double mj = P.mn[j], uj = P.u[j];
+        const double sp = 2 * mj * Ep / m2, sm = 2 * mj * Em / m2;
+        const double cs = m2 / (m2 + Ga * Ga);
+        const double lg = Ga * (nm::log1p(cs * sp * (sp - 2)) - nm::log1p(cs * sm * (sm - 2)));
+        double Gs;
+        if (sp < 1e-5)
+            Gs = g4 / (32 * kPi * m2 * Ga) *
+                 (2 * mphi * ((gr * (1 + gr2 + 2 * sm)) / ((1 + gr2) * (1 + gr2)) * (sp - sm) + gr / ((1 + gr2) * (1 + gr2)) * ((sp - sm) * (sp - sm))) + lg);
+        else
+            Gs = g4 / (32 * kPi * m2 * Ga) * (2 * mphi * atandiff(mphi * (sp - 1) / Ga, mphi * (sm - 1) / Ga) + lg);
+        Gs *= uj;
+        const double wgt = m2 / (2 * mj);
+        tot += wgt * Gs;
+        if (!P.non_resonant) continue;
+
+        const double L1p = nm::log1p(sp), L1m = nm::log1p(sm);
+        double Gtu0 = g4 / (16 * kPi * m2) * (2 * L1p / sp - 2 * L1m / sm + L1p - L1m);
+        if (Gtu0 < 0) Gtu0 = g4 / (16 * kPi * m2) * (sp - sm) / 2. * gl3_Gtu_nores(sm, sp);
+        Gtu0 *= 2 * uj;
+        tot += wgt * Gtu0;
+
+        double Gint = g4 / (32 * kPi * m2 * sm * sp) *
+                      (sm * L1p * (2 + 2 * sp + sp * nm::log(2 + sp)) - sp * L1m * (2 + 2 * sm + sm * nm::log(2 + sm))
+                       + sm * sp * (dilog1mdiff(sp, sm) + dilogdiff(sp, sm)));
+        if (Gint < 0) Gint = g4 / (16 * kPi * m2) * (sp - sm) / 2. * gl3_Gtu_int(sm, sp);
+        Gint *= P.majorana ? uj : 0.5 * uj;
+        tot += wgt * Gint;
+
+        // s-t interference
+        const cd den = C(gr, 2.0);                    // 2*I + gr
+        const cd z1p = C(0.0, 1 + sp) / den, z1m = C(0.0, 1 + sm) / den;
+        const cd z2p = conj(z1p), z2m = conj(z1m);
+        cd d1, d2;
+        if (sp < 1e-5) {
+            const cd l1 = clog(C(gr, 1.0) / den), l2 = clog(C(gr, -1.0) / C(gr, -2.0));
+            d1 = (sm * sm) * (C(-0.0, -0.5) / C(gr, 1.0) - l1 / 2.) + sm * l1 - sp * l1 + ((sp * sp) * (kI / C(gr, 1.0) + l1)) / 2.;
+            d2 = (sm * sm) * (C(0.0, 0.5) / C(gr, -1.0) - l2 / 2.) + sm * l2 - sp * l2 + ((sp * sp) * (C(-0.0, -1.0) / C(gr, -1.0) + l2)) / 2.;
+        } else {
+            d1 = dilogdiff_c(z1p, z1m);
+            d2 = dilogdiff_c(z2p, z2m);
+        }
+        const double Lgp = nm::log1p(((-1 + sp) * (-1 + sp)) / gr2), Lgm = nm::log1p(((-1 + sm) * (-1 + sm)) / gr2);
+        double Gst = -g4 / (32 * kPi * m2 * (1 + gr2)) *
+                     (d1.r + d2.r + gr * (d2.i - d1.i) + 2 * gr * carg(1.0 - z2p) * L1p - 2 * gr * carg(1.0 - z2m) * L1m
+                      + nm::log1p(4 / gr2) * (L1m - L1p) + Lgp * L1p - Lgm * L1m + (1 + gr2) * (Lgm - Lgp) + 2 * dilogdiff(sp, sm));
+        Gst *= uj;
+        tot += wgt * Gst;
+        const double Gsu = P.majorana ? Gst : 0;
+        tot += wgt * Gsu;
+
+        double Gpp = 0;
+        if (sp > 4 && P.phiphi) {
+            const double a = (sm > 4) ? sm : 4.0;
+            Gpp = g4 / (128. * kPi * m2) * gpp_analytic(a, sp);
+            if (Gpp < 0) Gpp = g4 / (64 * kPi * m2) * (sp - a) / 2. * gl3_Gpp(a, sp);
+            Gpp *= uj;
+            if (P.majorana) Gpp *= 2;
+        }
+        tot += wgt * Gpp;
+        if (Gs < 0 || Gtu0 < 0 || Gint < 0 || (Gs + Gtu0 + Gst + Gsu) < 0) warn |= kWarnGamma;
+    }
+    return tot;
+}
+
+// ---------------------------------------------------------------------------
+// alphaTilde(Em, Ep)  -- nuSIprop.hpp:924-1235
+// ---------------------------------------------------------------------------
+NUSI_FN double alphat_entry(const Point& P, const SplineSet& spl, double Em, double Ep, int& warn)
+{
+    const double g = P.g, mphi = P.mphi, Ga = P.Ga;
+    const double g4 = (g * g) * (g * g), m2 = mphi * mphi, m4 = (mphi * mphi) * (mphi * mphi);
+    const double gr = Ga / mphi, gr2 = gr * gr;
+    const bool maj = P.majorana;
+    double tot = 0;
+    for (int k = 0; k < 3; ++k) {
+        const double mk = P.mn[k], uk = P.u[k];
+        double tp = -2 * mk * Ep / m2, tm = -2 * mk * Em / m2;
+        if (fabs(tm + 1) < 1e-7) tm += tm * 1e-6;
+        if (fabs(tp + 1) < 1e-7) tp += tp * 1e-6;
+        const double wgt = m4 / (2 * mk);
+
+        const double cs = m2 / (m2 + Ga * Ga);
+        const double lg = Ga * (nm::log1p(cs * tp * (tp + 2)) - nm::log1p(cs * tm * (tm + 2)));
+        double as;
+        if (fabs(tp) < 1e-5)
+            as = g4 / (16 * kPi * Ga * m4) *
+                 (2 * mphi * (1 + tm) * (-((gr * (1 + gr2 - 2 * tm) * (-tm + tp)) / ((1 + gr2) * (1 + gr2))) + (gr * ((-tm + tp) * (-tm + tp))) / ((1 + gr2) * (1 + gr2))) + lg);
+        else
+            as = g4 / (16 * kPi * Ga * m4) * (2 * mphi * (1 + tm) * atandiff(mphi * (1 + tm) / Ga, mphi * (1 + tp) / Ga) + lg);
+        as *= uk;
+        if (!maj) as /= 2.;
+        tot += wgt * as;
+        if (!P.non_resonant) continue;
+
+        const double Lmt = nm::log1p(-tm), Lmp = nm::log1p(-tp), Ld = nm::log1p(tm - tp);
+        const double brk = (-2 + tm) * (tm - tp) - (-1 + tm) * (-2 + tp) * (Lmt - Lmp);
+        double at;
+        if (maj) {
+            at = g4 * (1 / (16 * m4 * kPi * (-1 + tm) * tp) * brk
+                       + 1 / (16 * m4 * kPi * ((1 + tm) * (1 + tm)) * tp) *
+                             ((1 + tm) * (2 + tm) * (tm - tp) + (-2 * ((1 + tm) * (1 + tm)) + tp + 2 * tm * tp) * Ld - (tm * tm) * tp * nm::log(tm / tp)));
+            if (at < 0) at = gl33_tri(0, tp, tm) * (g4 / (16 * kPi * m4));
+        } else {
+            at = 3. / 2. * g4 / (32 * m4 * kPi * (-1 + tm) * tp) * brk;
+            if (at < 0) at = gl33_tri(1, tp, tm) * (3. / 2. * g4 / (32 * kPi * m4));
+        }
+        at *= uk;
+        tot += wgt * at;
+
+        double au;
+        if (maj) au = at;
+        else {
+            au = 1. / 2. * g4 / (32 * m4 * kPi * (-1 + tm) * tp) * brk;
+            if (au < 0) au = gl33_tri(1, tp, tm) * (1. / 2. * g4 / (32 * kPi * m4));
+            au *= uk;
+        }
+        tot += wgt * au;
+
+        double atu = 0;
+        if (maj) {
+            double combi;
+            if (-tp < 1e-2 && -tm < 1e-2) {
+                // log(2), log(256), log(4096) as the reference's libm calls return them
+                const double d = tp / tm, lt = nm::log(-tp);
+                const double ln2 = 0.6931471805599453, ln256 = 5.545177444479562, ln4096 = 8.317766166719343;
+                const double d2 = d * d, d3 = d * d * d, d4 = (d * d) * (d * d);
+                combi = -(((-1 + d) * tp * nm::log(-2 * tp)) / d)
+                        - ((-1 + d) * (tp * tp) * (-2 + d + d * ln2 + nm::log(-2 / tp) - d * lt)) / (2. * d2)
+                        + ((tp * tp * tp) * (8 - 30 * d + 21 * d2 + d3 - 8 * d3 * ln2 + ln256 + 8 * lt - 8 * d3 * lt)) / (24. * d3)
+                        + (((tp * tp) * (tp * tp)) * (-32 + 56 * d - 51 * d2 + 30 * d3 - 3 * d4 + ln4096 - d4 * ln4096 - 12 * lt + 12 * d4 * lt)) / (48. * d4);
+            } else if (-tp > 1e2 && -tm > 1e2) {
+                const double d = tp / tm, lq = nm::log((-1 + d) / d), lt = nm::log(-tp);
+                const double d2 = d * d, d3 = d * d * d, d4 = (d * d) * (d * d);
+                combi = (-2 * (-1 + d) * lq) / tp - (2 * (-1 + nm::log(-(d / ((-1 + d) * tp))))) / (tp * tp)
+                        + (-6 + 4 * d + d2 - 2 * d3 - 8 * lq + 8 * d * lq + 2 * d3 * lq - 2 * d4 * lq - 6 * lt + 6 * d * lt) / (3. * (-1 + d) * (tp * tp * tp))
+                        + (8 - 12 * d + 3 * d2 + 12 * lq - 24 * d * lq + 12 * d2 * lq + 12 * lt - 24 * d * lt + 12 * d2 * lt) / (3. * ((-1 + d) * (-1 + d)) * ((tp * tp) * (tp * tp)));
+            } else
+                combi = li2(1 + 1 / (-2 + tp)) - li2((-1 + tm) / (-2 + tp)) + li2(1 + (1 + tm - tp) / tp) - li2(1 + 1 / tp);
+            atu = g4 / (32 * kPi * m4 * (1 + tm) * tp) *
+                  (2 * (2 * (1 + tm) * (tm - tp) - 2 * (1 + tm) * tp * nm::atanh(1 / (1 - tp)) * nm::atanh((tm - tp) / (-2 + tm + tp))
+                        + tm * tp * (-Lmt + Lmp) + (1 + tm) * (Lmt - Lmp - Ld) + tp * (-Lmt + Lmp + Ld) - tm * tp * nm::log(tm / tp))
+                   + (1 + tm) * tp * ((-(Lmt * Lmt) + Lmp * Lmp) / 2. + dilog1over1mdiff(tp, tm))
+                   - (1 + tm) * tp * (dilog1pdiff(tm, tp) + combi));
+            if (atu < 0) atu = gl33_tri(2, tp, tm) * (g4 / (16 * kPi * m4));
+        }
+        atu *= uk;
+        tot += wgt * atu;
+
+        // s-t interference
+        const cd den = C(gr, 2.0);                  // 2*I + gr
+        const cd dt_m = C(2 + tm, -gr);             // 2 - I*gr + tm
+        cd d78, d51, d26, d43;
+        if (-tp < 1e-5) {
+            const double d = tp / tm;
+            const cd ltm = clog_real(tm), ltp = clog_real(tp), ld = clog_real(d);
+            const cd lq = clog(1.0 - kI / den), lr = clog(C(gr, 1.0) / den);
+            d78 = tm * (-1.0 + ltm) + ((tm * tm) * (-1.0 + 2 * ltm)) / 4. - (tp * (-1.0 + ltp) + ((tp * tp) * (-1.0 + 2 * ltp)) / 4.);
+            d51 = (-tm + tp) * lq + ((-(tm * tm) + tp * tp) * (kI * (1.0 + lq) + lq * gr)) / (2. * C(gr, 1.0));
+            d26 = (tp * (-1.0 + d - ld + ltp - d * ltp)) / d
+                  + ((tp * tp) * (-1.0 + d * d + 2 * ld - 2 * ltp + 4 * d * ltp - 2 * (d * d) * ltp)) / (4. * (d * d))
+                  + ((tp * tp * tp) * (7 - 9 * d + 2 * (d * d * d) - 6 * ld + 6 * ltp - 18 * d * ltp + 18 * (d * d) * ltp - 6 * (d * d * d) * ltp)) / (18. * (d * d * d));
+            d43 = ((-1 + d) * tp * lr) / d + ((-1 + d) * (tp * tp) * (kI * ((1 + d) / C(gr, 1.0) - 2 / den) + (-1 + d) * lr)) / (2. * (d * d));
+        } else {
+            const cd z1 = C(0.0, 1 - tm) / den;      // (-I*(-1+tm))/(2I+gr)
+            const double z2 = 1 / (1 + tm);
+            const cd z3 = 1 / dt_m;
+            const cd z4 = (1 + tm - tp) / dt_m;
+            const cd z5 = C(0.0, 1 - tp) / den;
+            const double z6 = 1 - tp / (1 + tm);
+            d78 = dilogdiff_c(C(1 - tm), C(1 - tp));
+            d51 = dilogdiff_c(z5, z1);
+            d26 = dilogdiff_c(C(z2), C(z6));
+            d43 = dilogdiff_c(z4, z3);
+        }
+        const double Lgp = nm::log1p(((1 + tp) * (1 + tp)) / gr2), Lgm = nm::log1p(((1 + tm) * (1 + tm)) / gr2);
+        const double Am = carg(C(-1 - tm, gr)), Ap = carg(C(-1 - tp, gr));
+        const double Bm = carg(C(gr, 1 + tm) / den), Bp = carg(C(gr, 1 + tp) / den);
+        double ast;
+        if (maj)
+            ast = g4 / (32 * kPi * (1 + gr2) * m4) *
+                  (2 * kPi * Am - 2 * kPi * Ap + 2 * gr * (d51.i + d26.i + d43.i) - 2 * (d51.r + d26.r + d43.r + d78.r)
+                   - Bm * (2 * kPi + 2 * gr * Lmt) + Bp * (2 * kPi + 2 * gr * Lmp) + (Am - Ap) * (4 * gr * tm + 2 * gr * Lmt)
+                   + 2 * gr * (carg_real(1 + tm) - carg(dt_m) + carg(C(1 + tp, -gr))) * Ld
+                   + nm::log(4 + gr2) * (Lmp - Lmt) + nm::log(gr2 + (2 + tm) * (2 + tm)) * Ld - 2 * Lmt * nm::log(-tp)
+                   - 2 * gr * kPi * (nm::log(tp * tp) + Ld) + 2 * gr * kPi * nm::log(tp * tp) + 4 * tm * nm::log(tm / tp)
+                   + (-Lmp + Lmt - Ld) * (Lgp + 2 * nm::log(gr)) - Ld * nm::log1p(tm * tm + 2 * tm)
+                   + 2 * (gr2 + tm) * (Lgp - Lgm) + 2 * (nm::log(-tp) * (Lmp + Ld) + (Lgp - Lgm)));
+        else
+            ast = g4 / (32 * kPi * (1 + gr2) * m4) *
+                  (gr * d51.i - 2 * (d51.r + d78.r) + 2 * Bm * (-kPi - gr * Lmt) + 2 * Am * (kPi + gr * tm + gr * Lmt)
+                   - 2 * Ap * (kPi + gr * tm + gr * Lmt) + 2 * Bp * (kPi + gr * Lmp) - 2 * Lmt * nm::log(-tp)
+                   + 2 * tm * nm::log(tm / tp) + 2 * Lmp * nm::log(-tp) + (Lmp - Lmt) * (nm::log(4 + gr2) - 2 * nm::log(gr) - Lgp)
+                   + (1 + tm + gr2) * (Lgp - Lgm));
+        ast *= uk;
+        tot += wgt * ast;
+        const double asu = maj ? ast : 0;
+        tot += wgt * asu;
+
+        double app = 0;
+        if (-tp > 4 && P.phiphi) {
+            if (-tp < 1e4) {
+                const double xx[2] = {-tp, nm::log10(tp / tm)};
+                double v = 0;
+                if (!spl.at.eval(xx, v)) warn |= kWarnSplineOOB;
+                app = g4 / m4 * v;
+            } else {
+                const double lm = nm::log(-tm), lp = nm::log(-tp);
+                app = g4 / m4 *
+                      (6 * tm * lm - tp * (lm * lm) + 2 * (-8 * tm + 8 * tp + 4 * tp * lm + nm::log(tm - tp) * (tm - tp - tp * nm::log(tm / tp)))
+                       - 2 * (2 * tm + 5 * tp) * lp + tp * (lp * lp) - 2 * tp * li2(1 - tm / tp)) / (128. * kPi * tp);
+            }
+            app *= uk;
+            if (maj) app *= 2;
+            app *= 2;
+            if (maj) app *= 2;
+        }
+        tot += wgt * app;
+
+        const double nrm = (g / mphi) * (g / mphi) * ((g / mphi) * (g / mphi));
+        if (as < 0 || at < 0 || au < 0 || atu / nrm < -1e-11 || (ast + at + as) / nrm < -1e-11 || (asu + au + as) / nrm < -1e-11)
+            warn |= kWarnAlphaTilde;
+    }
+    return tot;
+}
+
+// ---------------------------------------------------------------------------
+// alpha(Em, Ep, Em', Ep')  -- nuSIprop.hpp:1237-1520
+// ---------------------------------------------------------------------------
+NUSI_FN double alpha_entry(const Point& P, const SplineSet& spl, double Em, double Ep, double Emp, double Epp, int& warn)
+{
+    const double g = P.g, mphi = P.mphi, Ga = P.Ga;
+    const double g4 = (g * g) * (g * g), m2 = mphi * mphi, m4 = (mphi * mphi) * (mphi * mphi);
+    const double gr = Ga / mphi, gr2 = gr * gr;
+    const bool maj = P.majorana;
+    double tot = 0;
+    for (int k = 0; k < 3; ++k) {
+        const double mk = P.mn[k], uk = P.u[k];
+        double tp = -2 * mk * Ep / m2, tm = -2 * mk * Em / m2;
+        const double Sp = 2 * mk * Epp / m2, Sm = 2 * mk * Emp / m2;
+        if (fabs(tm + 1) < 1e-7) tm += tm * 1e-6;
+        if (fabs(tp + 1) < 1e-7) tp += tp * 1e-6;
+        const double wgt = m4 / (2 * mk);
+
+        double as;
+        if (Sp < 1e-5)
+            as = g4 / (8 * kPi * Ga * (mphi * mphi * mphi)) * (tm - tp) *
+                 ((gr * (1 + gr2 + 2 * Sm)) / ((1 + gr2) * (1 + gr2)) * (Sp - Sm) + gr / ((1 + gr2) * (1 + gr2)) * ((Sp - Sm) * (Sp - Sm)));
+        else
+            as = g4 / (8 * kPi * Ga * (mphi * mphi * mphi)) * (tm - tp) * atandiff(mphi * (Sp - 1) / Ga, mphi * (Sm - 1) / Ga);
+        as *= uk;
+        if (!maj) as /= 2.;
+        tot += wgt * as;
+        if (!P.non_resonant) continue;
+
+        const double Lmt = nm::log1p(-tm), Lmp = nm::log1p(-tp);
+        const double lSm = nm::log(Sm), lSp = nm::log(Sp);
+        const double Lmm = nm::log1p(Sm + tm), Lpm = nm::log1p(Sp + tm), Lmq = nm::log1p(Sm + tp), Lpq = nm::log1p(Sp + tp);
+        const double SS = Sm * Sp;
+        double at;
+        if (maj) {
+            const double LA = nm::log(((1 + Sm + tm) * (-1 + tp)) / ((-1 + tm) * (1 + Sm + tp)));
+            const double LB = nm::log(((1 + Sp + tm) * (-1 + tp)) / ((-1 + tm) * (1 + Sp + tp)));
+            const double inner = SS * (-tm + tp) * lSm + SS * (tm - tp) * lSp - SS * Lmm - SS * tp * Lmm + SS * Lpm + SS * tp * Lpm
+                                 - Sp * LA - Sp * tm * LA - Sp * tp * LA - Sp * tm * tp * LA
+                                 + SS * nm::log(1 + Sm + tp) + SS * tm * Lmq
+                                 + Sm * LB + Sm * tm * LB + Sm * tp * LB + Sm * tm * tp * LB
+                                 - SS * nm::log(1 + Sp + tp) - SS * tm * Lpq;
+            at = g4 / (Sm * Sp * 16 * kPi * m4) *
+                 (-((Sm - Sp) * (3 + 2 * tm * (-1 + tp) - 2 * tp) * (tm - tp)) / ((-1 + tm) * (-1 + tp))
+                  + 2 * inner / ((1 + tm) * (1 + tp))
+                  - ((SS * nm::log((Sm * (1 + Sp + tm)) / (Sp * (1 + Sm + tm)))) / ((1 + tm) * (1 + tm))
+                     + (((Sm - Sp) * (tm - tp) * (1 + tp)) / (1 + tm) - SS * nm::log((Sm * (1 + Sp + tp)) / (Sp * (1 + Sm + tp)))) / ((1 + tp) * (1 + tp))));
+            if (at < 0) at = gl33_rect(0, tp, tm, Sm, Sp) * (g4 / (16 * kPi * m4));
+        } else {
+            const double brk = -((tm - tp) * (2 + tm * (-1 + tp) - tp)) - 2 * (-1 + tm) * (-1 + tp) * (Lmt - Lmp);
+            at = 3. / 2. * g4 / (32 * kPi * m4 * Sm * Sp * (-1 + tm) * (-1 + tp)) * (Sm - Sp) * brk;
+            if (at < 0) at = gl33_rect(1, tp, tm, Sm, Sp) * (3. / 2. * g4 / (32 * kPi * m4));
+        }
+        at *= uk;
+        tot += wgt * at;
+
+        double au;
+        if (maj) au = at;
+        else {
+            const double brk = -((tm - tp) * (2 + tm * (-1 + tp) - tp)) - 2 * (-1 + tm) * (-1 + tp) * (Lmt - Lmp);
+            au = 1. / 2. * g4 / (32 * kPi * m4 * Sm * Sp * (-1 + tm) * (-1 + tp)) * (Sm - Sp) * brk;
+            if (au < 0) au = gl33_rect(1, tp, tm, Sm, Sp) * (1. / 2. * g4 / (32 * kPi * m4));
+            au *= uk;
+        }
+        tot += wgt * au;
+
+        double atu = 0.;
+        if (maj) {
+            const double Qmp = (1 + Sm + tp) / Sm, Qpp = (1 + Sp + tp) / Sp, Qmm = (1 + Sm + tm) / Sm, Qpm = (1 + Sp + tm) / Sp;
+            double Fp, Fm;
+            if (tp < -1) Fp = li2(Qmp) - li2(Qpp);
+            else {
+                const double a = nm::log(Qmp), b = nm::log(Qpp);
+                Fp = -li2(Sm / (1 + Sm + tp)) + li2(Sp / (1 + Sp + tp)) - 0.5 * (a * a - b * b);
+            }
+            if (tm < -1) Fm = -li2(Qmm) + li2(Qpm);
+            else {
+                const double a = nm::log(Qmm), b = nm::log(Qpm);
+                Fm = li2(Sm / (1 + Sm + tm)) - li2(Sp / (1 + Sp + tm)) + 0.5 * (a * a - b * b);
+            }
+            const double lap = (tp > -1) ? nm::log1p(tp) : nm::log(-1 - tp);
+            const double lam = (tm > -1) ? nm::log1p(tm) : nm::log(-1 - tm);
+            const double Pq = (1 + tm) * (1 + tp);
+            const double l2m = nm::log((2 + Sm) / Sm), l2p = nm::log((2 + Sp) / Sp);
+            const double SSP = SS * (1 + tm) * (1 + tp);
+            atu = g4 / (32 * kPi * m4 * Sm * Sp * (1 + tm) * (1 + tp)) *
+                  (-4 * (Sm - Sp) * (1 + tm) * (tm - tp) * (1 + tp)
+                   + 2 * SS * tp * (nm::log(Sm / Sp) - Lmm + Lpm)
+                   + 2 * Sp * (1 + tm) * (1 + tp) * (Lmt - Lmm - Lmp + Lmq)
+                   - 2 * Sm * (1 + tm) * (1 + tp) * (Lmt - Lpm - Lmp + Lpq)
+                   + 2 * SS * (-Lmm + Lpm + Lmq - Lpq)
+                   + SSP * (l2m * (lSp + Lmq) - l2p * (lSm + Lpq) + Lmp * (nm::log(Sm / Sp) - Lmq + Lpq))
+                   + SSP * ((lSp + Lmm) * (nm::log(Sm / (2 + Sm)) + Lmt - lam) + (lSm + Lpm) * (l2p - Lmt + lam))
+                   + SS * (nm::log(Sp / Sm) + Lmq - Lpq) * (2 * tm + Pq * lap)
+                   + SSP * (li2((1 + Sm + tm) / (2 + Sm)) - li2((1 + Sp + tm) / (2 + Sp)) - li2((1 + Sm + tp) / (2 + Sm)) + li2((1 + Sp + tp) / (2 + Sp)))
+                   + SSP * (Fp + Fm));
+            // nuSIprop.hpp:1401-1418: the fallback assigns a shadowing local; a negative alpha_tu stays.
+        }
+        atu *= uk;
+        tot += wgt * atu;
+
+        // s-t interference: eight complex dilogarithms (nuSIprop.hpp:1431-1451)
+        const cd dtm = C(2 + tm, -gr), dtp = C(2 + tp, -gr);      // 2 - I*gr + t
+        const double z1 = (1 + Sm + tm) / (1 + tm), z3 = (1 + Sp + tm) / (1 + tm);
+        const double z5 = (1 + Sm + tp) / (1 + tp), z7 = (1 + Sp + tp) / (1 + tp);
+        const cd z2 = (1 + Sm + tm) / dtm, z4 = (1 + Sp + tm) / dtm;
+        const cd z6 = (1 + Sm + tp) / dtp, z8 = (1 + Sp + tp) / dtp;
+        const cd D1 = cli2(z1, 0.0), D2 = cli2(z2), D3 = cli2(z3, 0.0), D4 = cli2(z4);
+        const cd D5 = cli2(z5, 0.0), D6 = cli2(z6), D7 = cli2(z7, 0.0), D8 = cli2(z8);
+        const double Lsm = nm::log1p(((-1 + Sm) * (-1 + Sm)) / gr2), Lsp = nm::log1p(((-1 + Sp) * (-1 + Sp)) / gr2);
+        double ast;
+        if (maj) {
+            const double cm = carg_real(-(1 / (1 + tm))), cp = carg_real(-(1 / (1 + tp)));
+            const double L2m = nm::log1p(((2 + tm) * (2 + tm)) / gr2), L2p = nm::log1p(((2 + tp) * (2 + tp)) / gr2);
+            const double am = nm::log(fabs(1 + tm)), ap = nm::log(fabs(1 + tp));
+            const cd nm = C(-1 + Sm, gr), np = C(-1 + Sp, gr);      // -1 + I*gr + S
+            ast = g4 / (32 * kPi * (1 + gr2) * m4) *
+                  (2 * gr * (D1.i - D2.i - D3.i + D4.i - D5.i + D6.i + D7.i - D8.i)
+                   - 2 * (D1.r - D2.r - D3.r + D4.r - D5.r + D6.r + D7.r - D8.r)
+                   + 2 * gr * (cm - carg(-(nm / dtm))) * Lmm
+                   - 2 * gr * (cm - carg(-(np / dtm))) * Lpm
+                   + 2 * gr * (cp - carg(-(np / dtp))) * Lpq
+                   - 2 * gr * (cp - carg(-(nm / dtp))) * Lmq
+                   + 2 * (gr * carg(nm) - gr * carg(np) + Lsp / 2. - Lsm / 2. + lSm - lSp) * (2 * (tm - tp) + (Lmt - Lmp))
+                   + Lmm * (Lsm - L2m - 2 * (lSm - am)) - Lpm * (Lsp - L2m - 2 * (lSp - am))
+                   - Lmq * (Lsm - L2p - 2 * (lSm - ap)) + Lpq * (Lsp - L2p - 2 * (lSp - ap)));
+        } else
+            ast = g4 / (32 * kPi * (1 + gr2) * m4) *
+                  ((2 * gr * carg(C(-1 + Sm, gr)) - 2 * gr * carg(C(-1 + Sp, gr)) + 2 * lSm - 2 * lSp + Lsp - Lsm) * (tm - tp + Lmt - Lmp));
+        ast *= uk;
+        tot += wgt * ast;
+        const double asu = maj ? ast : 0.;
+        tot += wgt * asu;
+
+        double app = 0;
+        if (Sm > 4 && P.phiphi) {
+            if (Sm < 1e4) {
+                const double d = Sp / Sm;
+                const double xx[3] = {Sm, nm::log(-Sm / tm) / nm::log(d) * 1.0001, nm::log10(d)};
+                double v = 0;
+                if (!spl.a.eval(xx, v)) warn |= kWarnSplineOOB;
+                app = g4 / m4 * fabs(v);
+            } else if (tm < -1) {
+                const double l1m = nm::log(-1 - tm), l0m = nm::log(-tm), l1p = nm::log(-1 - tp), l0p = nm::log(-tp);
+                app = g4 / m4 *
+                      ((-Sm + Sp) * ((tm - tp) * (Sp * (-2 + tm + tp) + Sm * (-2 - 24 * Sp + tm + tp))
+                                     + 4 * (-(Sp * (1 + tm)) + Sm * (-1 + 2 * Sp + (-1 + Sp) * tm)) * l1m
+                                     + 2 * (3 * Sp + Sm * (3 + 4 * Sp)) * tm * l0m
+                                     + 4 * (Sp + Sp * tp + Sm * (1 + tp - Sp * (2 + tp))) * l1p
+                                     - 2 * (3 * Sp + Sm * (3 + 4 * Sp)) * tp * l0p)
+                       + 2 * (Sm * Sm) * lSp * ((3 + 2 * Sp) * (tm - tp) + 2 * (Sp * Sp) * ((-1 - tm) * l1m + tm * l0m + (1 + tp) * l1p - tp * l0p))
+                       + 2 * (Sp * Sp) * lSm * ((-3 - 2 * Sm) * (tm - tp) + 2 * (Sm * Sm) * ((1 + tm) * l1m - tm * l0m - (1 + tp) * l1p + tp * l0p)))
+                      / (256. * kPi * (Sm * Sm) * (Sp * Sp));
+            } else if (tp < -1) {
+                const double l1p = nm::log(-1 - tp), l0p = nm::log(-tp);
+                app = g4 / m4 *
+                      ((2 * (Sm * Sm) * lSp * ((1 + tp) * (-3 - 2 * Sp + 2 * (Sp * Sp) * l1p) - 2 * (Sp * Sp) * tp * l0p)
+                        + (Sm - Sp) * ((1 + tp) * (-3 * (Sm + Sp + 8 * Sm * Sp) + (Sm + Sp) * tp)
+                                       + 4 * (-(Sp * (1 + tp)) + Sm * (-1 + 2 * Sp + (-1 + Sp) * tp)) * l1p
+                                       + 2 * (3 * Sp + Sm * (3 + 4 * Sp)) * tp * l0p)
+                        + 2 * (Sp * Sp) * lSm * ((3 + 2 * Sm) * (1 + tp) + 2 * (Sm * Sm) * (-((1 + tp) * l1p) + tp * l0p)))
+                           / (256. * kPi * (Sm * Sm) * (Sp * Sp))
+                       + (-1 - tm) * (-6 * Sm + 6 * Sp - 2 * (-2 + Sm) * Sp * lSm + Sm * Sp * (lSm * lSm) + 2 * Sm * (-2 + Sp) * lSp - Sm * Sp * (lSp * lSp))
+                             / (128. * kPi * Sm * Sp));
+            } else
+                app = g4 / m4 * (tp - tm) *
+                      (-6 * Sm + 6 * Sp - 2 * (-2 + Sm) * Sp * lSm + Sm * Sp * (lSm * lSm) + 2 * Sm * (-2 + Sp) * lSp - Sm * Sp * (lSp * lSp))
+                      / (128. * kPi * Sm * Sp);
+            app *= uk;
+            if (maj) app *= 2;
+            app *= 2;
+            if (maj) app *= 2;
+        }
+        tot += wgt * app;
+
+        const double nrm = (g / mphi) * (g / mphi) * ((g / mphi) * (g / mphi));
+        if (as < 0 || at / nrm < -1e-11 || au / nrm < -1e-11 || atu / nrm < -1e-11 || (ast + as + at) / nrm < -1e-11)
+            warn |= kWarnAlpha;
+    }
+    return tot;
+}
+
+}  // namespace nusi

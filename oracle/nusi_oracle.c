@@ -7,8 +7,12 @@
  * (shadowed alpha_tu fallback, zmax overwrite, stale norm_total in the
  * energy check).  Sub-expressions that the reference repeats verbatim are
  * hoisted into locals; additions keep the reference's left-to-right order.
- * Complex arithmetic is C99 `double _Complex` with glibc clog/carg/cabs, as
- * in the reference (which uses GNU `_Complex` from C++).
+ * The functions feeding the tables (log/log1p/exp/atan/atan2/atanh, Li2,
+ * Li3) and the complex arithmetic (ora_cplx.h) use a fixed operation
+ * sequence shared with the GPU (ora_libm.c): the reference's closed forms
+ * cancel catastrophically at small |t|, s', so bit-exact table parity needs
+ * identical arithmetic.  Host-level set-up (grid, cosmology, normalisation)
+ * uses glibc, as the product's host code does.
  */
 #define _GNU_SOURCE
 #include <complex.h>
@@ -21,6 +25,8 @@
 #include "ora_aux.h"
 #include "ora_specfun.h"
 #include "ora_spline.h"
+#include "ora_libm.h"
+#include "ora_cplx.h"
 
 #define SQ(a) ((a) * (a))
 #define CU(a) ((a) * (a) * (a))
@@ -30,7 +36,7 @@ struct ora_state {
     int N, Nz, T;
     double *Emin, *Emax, *Enu, *z;
     double zmax_eff;                    /* member zmax after the overwrite, nuSIprop.hpp:128 */
-    ora_c U[3][3];
+    double U2m[3][3];                   /* |U_fk|^2 (only the moduli are used) */
     double mn[3];
     double norm_total;
     int have_pp;
@@ -61,15 +67,15 @@ static double lum_int(double z, double E)
 {
     const double Etot = 3 * 6.24, T = 6e6;
     const double y = -E * (1 + z) / T;
-    const double ey = exp(y);
-    const double pref = (Etot * 120 / (6 * 7 * pow(M_PI, 4) * pow(T, 2)));
-    return pref * (-E * E * (1 + z) * log(ey + 1) / T + 2 * E * ora_li2(-ey) + 2 * T * ora_li3(-ey) / (1 + z));
+    const double ey = ora_exp(y);
+    const double pref = (Etot * 120 / (6 * 7 * pow(M_PI, 4) * pow(T, 2)));   /* host libm constant */
+    return pref * (-E * E * (1 + z) * ora_log(ey + 1) / T + 2 * E * ora_li2(-ey) + 2 * T * ora_li3(-ey) / (1 + z));
 }
 double ora_Lum(const ora_state *S, double z, double Em, double Ep)
 {
     if (S->p.source == 1) {   /* power law, nuSIprop.hpp:656 */
         const double si = S->p.si;
-        return S->norm_total / 3.0 * sfr_of(z) * (Ep * pow(Ep / E0 * (1 + z), -si) - Em * pow(Em / E0 * (1 + z), -si)) / (1 - si);
+        return S->norm_total / 3.0 * sfr_of(z) * (Ep * ora_pow(Ep / E0 * (1 + z), -si) - Em * ora_pow(Em / E0 * (1 + z), -si)) / (1 - si);
     }
     return (lum_int(z, Ep) - lum_int(z, Em)) * rsn_of(z);   /* DSNB, nuSIprop.hpp:659-662 */
 }
@@ -126,7 +132,7 @@ static double width_of(const ora_state *S)   /* nuSIprop.hpp:748-757 */
     if (S->p.majorana) return SQ(g) * mphi / (16.0 * M_PI);
     return SQ(g) * mphi / (8.0 * M_PI);
 }
-static double u2(const ora_state *S, int k) { const ora_c u = S->U[S->p.flav][k]; return creal(u) * creal(u) + cimag(u) * cimag(u); }
+static double u2(const ora_state *S, int k) { return S->U2m[S->p.flav][k]; }
 
 /* 3-point Gauss-Legendre over [a,b] of f(z) */
 typedef double (*ora_f1)(double);
@@ -136,12 +142,12 @@ static double gl3(double a, double b, ora_f1 f)
     for (int q = 0; q < 3; ++q) z[q] = (b - a) / 2. * ora_gl_x[q] + (b + a) / 2.;
     return ora_gl_w[0] * f(z[0]) + ora_gl_w[1] * f(z[1]) + ora_gl_w[2] * f(z[2]);
 }
-static double f_Gtu_nores(double z) { return (z + 2) / (z * (z + 1)) - 2 / SQ(z) * log1p(z); }          /* :809 */
-static double f_Gtu_int(double z) { return 1 / z - 2 * (1 + z) / (SQ(z) * (2 + z)) * log1p(z); }         /* :833 */
+static double f_Gtu_nores(double z) { return (z + 2) / (z * (z + 1)) - 2 / SQ(z) * ora_log1p(z); }          /* :809 */
+static double f_Gtu_int(double z) { return 1 / z - 2 * (1 + z) / (SQ(z) * (2 + z)) * ora_log1p(z); }         /* :833 */
 static double f_Gpp(double z)                                                                              /* :900 */
 {
     const double r = sqrt(z * (z - 4));
-    return (SQ(z) - 4 * z + 6) / (SQ(z) * (z - 2)) * log(SQ((r + z - 2) / (r - z + 2))) - 6 * r / SQ(z);
+    return (SQ(z) - 4 * z + 6) / (SQ(z) * (z - 2)) * ora_log(SQ((r + z - 2) / (r - z + 2))) - 6 * r / SQ(z);
 }
 
 /* the double-scalar analytic absorption piece, nuSIprop.hpp:885 (a = max(s-,4)) */
@@ -150,11 +156,11 @@ static double Gpp_analytic(double a, double b)
     const double ra4 = sqrt(-4 + a), ra = sqrt(a), rb4 = sqrt(-4 + b), rb = sqrt(b);
     const double qa = sqrt((-4 + a) * a), qb = sqrt((-4 + b) * b);
     return 12 * sqrt((-4 + a) / a) - 12 * sqrt((-4 + b) / b)
-           - 2 * log(SQ(ra4 - ra) / 4.) * log(SQ(-2 + a + qa) / 4.)
-           - ((6 + a * log((-2 + a) * a)) * log(SQ(-2 + a + qa) / SQ(2 - a + qa))) / a
-           - 24 * (sqrt((-4 + a) / a) - sqrt((-4 + b) / b) - log(ra4 + ra) + log(rb4 + rb))
-           + 2 * log(SQ(rb4 - rb) / 4.) * log(SQ(-2 + b + qb) / 4.)
-           + ((6 + b * log((-2 + b) * b)) * log(SQ(-2 + b + qb) / SQ(2 - b + qb))) / b
+           - 2 * ora_log(SQ(ra4 - ra) / 4.) * ora_log(SQ(-2 + a + qa) / 4.)
+           - ((6 + a * ora_log((-2 + a) * a)) * ora_log(SQ(-2 + a + qa) / SQ(2 - a + qa))) / a
+           - 24 * (sqrt((-4 + a) / a) - sqrt((-4 + b) / b) - ora_log(ra4 + ra) + ora_log(rb4 + rb))
+           + 2 * ora_log(SQ(rb4 - rb) / 4.) * ora_log(SQ(-2 + b + qb) / 4.)
+           + ((6 + b * ora_log((-2 + b) * b)) * ora_log(SQ(-2 + b + qb) / SQ(2 - b + qb))) / b
            + 8 * ora_dilogdiff(4 / SQ(ra4 + ra), 4 / SQ(rb4 + rb))
            + 2 * ora_dilogdiff(4 / SQ(-2 + a + qa), 4 / SQ(-2 + b + qb));
 }
@@ -170,7 +176,7 @@ double ora_Gamma(ora_state *S, double Em, double Ep)       /* nuSIprop.hpp:759-9
         const double mj = S->mn[j], uj = u2(S, j);
         const double sp = 2 * mj * Ep / m2, sm = 2 * mj * Em / m2;
         const double cs = m2 / (m2 + SQ(Ga));
-        const double lg = Ga * (log1p(cs * sp * (sp - 2)) - log1p(cs * sm * (sm - 2)));
+        const double lg = Ga * (ora_log1p(cs * sp * (sp - 2)) - ora_log1p(cs * sm * (sm - 2)));
         double Gs;
         if (sp < 1e-5)
             Gs = g4 / (32 * M_PI * m2 * Ga) *
@@ -182,7 +188,7 @@ double ora_Gamma(ora_state *S, double Em, double Ep)       /* nuSIprop.hpp:759-9
         tot += wgt * Gs;
         if (!S->p.non_resonant) continue;
 
-        const double L1p = log1p(sp), L1m = log1p(sm);
+        const double L1p = ora_log1p(sp), L1m = ora_log1p(sm);
         /* t + u channels */
         double Gtu0 = g4 / (16 * M_PI * m2) * (2 * L1p / sp - 2 * L1m / sm + L1p - L1m);
         if (Gtu0 < 0) Gtu0 = g4 / (16 * M_PI * m2) * (sp - sm) / 2. * gl3(sm, sp, f_Gtu_nores);
@@ -191,28 +197,33 @@ double ora_Gamma(ora_state *S, double Em, double Ep)       /* nuSIprop.hpp:759-9
 
         /* t-u interference */
         double Gint = g4 / (32 * M_PI * m2 * sm * sp) *
-                      (sm * L1p * (2 + 2 * sp + sp * log(2 + sp)) - sp * L1m * (2 + 2 * sm + sm * log(2 + sm))
+                      (sm * L1p * (2 + 2 * sp + sp * ora_log(2 + sp)) - sp * L1m * (2 + 2 * sm + sm * ora_log(2 + sm))
                        + sm * sp * (ora_dilog1mdiff(sp, sm) + ora_dilogdiff(sp, sm)));
         if (Gint < 0) Gint = g4 / (16 * M_PI * m2) * (sp - sm) / 2. * gl3(sm, sp, f_Gtu_int);
         Gint *= S->p.majorana ? uj : 0.5 * uj;
         tot += wgt * Gint;
 
         /* s-t interference */
-        const ora_c z1p = I * (1 + sp) / (2 * I + gr), z1m = I * (1 + sm) / (2 * I + gr);
-        const ora_c z2p = conj(z1p), z2m = conj(z1m);
-        ora_c d1, d2;
-        if (sp < 1e-5) {
-            const ora_c l1 = clog((I + gr) / (2 * I + gr)), l2 = clog((-I + gr) / (-2 * I + gr));
-            d1 = SQ(sm) * (-I / 2 / (I + gr) - l1 / 2.) + sm * l1 - sp * l1 + (SQ(sp) * (I / (I + gr) + l1)) / 2.;
-            d2 = SQ(sm) * (I / 2 / (-I + gr) - l2 / 2.) + sm * l2 - sp * l2 + (SQ(sp) * (-I / (-I + gr) + l2)) / 2.;
+        /* z1 = I(1+s)/(2I+gr), z2 = conj(z1)  (nuSIprop.hpp:846-849) */
+        const zc den = zmk(gr, 2.0);
+        const zc z1p = zdiv(zmk(0.0, 1 + sp), den), z1m = zdiv(zmk(0.0, 1 + sm), den);
+        const zc z2p = zconj(z1p), z2m = zconj(z1m);
+        zc d1, d2;
+        if (sp < 1e-5) {   /* nuSIprop.hpp:855-860 */
+            const zc ipg = zmk(gr, 1.0), mipg = zmk(gr, -1.0);   /* I+gr, -I+gr */
+            const zc l1 = zlog(zdiv(ipg, den)), l2 = zlog(zdiv(mipg, zmk(gr, -2.0)));
+            d1 = zadd(zsub(zadd(zscale(SQ(sm), zsub(zdiv(zmk(-0.0, -0.5), ipg), zdivr(l1, 2.))), zscale(sm, l1)), zscale(sp, l1)),
+                      zdivr(zscale(SQ(sp), zadd(zdiv(zmk(0.0, 1.0), ipg), l1)), 2.));
+            d2 = zadd(zsub(zadd(zscale(SQ(sm), zsub(zdiv(zmk(0.0, 0.5), mipg), zdivr(l2, 2.))), zscale(sm, l2)), zscale(sp, l2)),
+                      zdivr(zscale(SQ(sp), zadd(zdiv(zmk(-0.0, -1.0), mipg), l2)), 2.));
         } else {
             d1 = ora_dilogdiff_c(z1p, z1m);
             d2 = ora_dilogdiff_c(z2p, z2m);
         }
-        const double Lgp = log1p(SQ(-1 + sp) / SQ(gr)), Lgm = log1p(SQ(-1 + sm) / SQ(gr));
+        const double Lgp = ora_log1p(SQ(-1 + sp) / SQ(gr)), Lgm = ora_log1p(SQ(-1 + sm) / SQ(gr));
         double Gst = -g4 / (32 * M_PI * m2 * (1 + SQ(gr))) *
-                     (creal(d1) + creal(d2) + gr * (cimag(d2) - cimag(d1)) + 2 * gr * carg(1 - z2p) * L1p
-                      - 2 * gr * carg(1 - z2m) * L1m + log1p(4 / SQ(gr)) * (L1m - L1p) + Lgp * L1p - Lgm * L1m
+                     (d1.r + d2.r + gr * (d2.i - d1.i) + 2 * gr * zarg(zrsub(1, z2p)) * L1p
+                      - 2 * gr * zarg(zrsub(1, z2m)) * L1m +ora_log1p(4 / SQ(gr)) * (L1m - L1p) + Lgp * L1p - Lgm * L1m
                       + (1 + SQ(gr)) * (Lgm - Lgp) + 2 * ora_dilogdiff(sp, sm));
         Gst *= uj;
         tot += wgt * Gst;
@@ -295,7 +306,7 @@ double ora_alphaTilde(ora_state *S, double Em, double Ep)   /* nuSIprop.hpp:924-
 
         /* s channel */
         const double cs = m2 / (m2 + SQ(Ga));
-        const double lg = Ga * (log1p(cs * tp * (tp + 2)) - log1p(cs * tm * (tm + 2)));
+        const double lg = Ga * (ora_log1p(cs * tp * (tp + 2)) - ora_log1p(cs * tm * (tm + 2)));
         double as;
         if (fabs(tp) < 1e-5)
             as = g4 / (16 * M_PI * Ga * m4) *
@@ -307,14 +318,14 @@ double ora_alphaTilde(ora_state *S, double Em, double Ep)   /* nuSIprop.hpp:924-
         tot += wgt * as;
         if (!S->p.non_resonant) continue;
 
-        const double Lmt = log1p(-tm), Lmp = log1p(-tp), Ld = log1p(tm - tp);
+        const double Lmt = ora_log1p(-tm), Lmp = ora_log1p(-tp), Ld = ora_log1p(tm - tp);
         const double brk = (-2 + tm) * (tm - tp) - (-1 + tm) * (-2 + tp) * (Lmt - Lmp);
         /* t channel */
         double at;
         if (maj) {
             at = g4 * (1 / (16 * m4 * M_PI * (-1 + tm) * tp) * brk
                        + 1 / (16 * m4 * M_PI * SQ(1 + tm) * tp) *
-                             ((1 + tm) * (2 + tm) * (tm - tp) + (-2 * SQ(1 + tm) + tp + 2 * tm * tp) * Ld - SQ(tm) * tp * log(tm / tp)));
+                             ((1 + tm) * (2 + tm) * (tm - tp) + (-2 * SQ(1 + tm) + tp + 2 * tm * tp) * Ld - SQ(tm) * tp * ora_log(tm / tp)));
             if (at < 0) at = gl33_tri(tp, tm, F_t_maj) * (g4 / (16 * M_PI * m4));
         } else {
             at = 3. / 2. * g4 / (32 * m4 * M_PI * (-1 + tm) * tp) * brk;
@@ -338,23 +349,23 @@ double ora_alphaTilde(ora_state *S, double Em, double Ep)   /* nuSIprop.hpp:924-
         if (maj) {
             double combi;
             if (-tp < 1e-2 && -tm < 1e-2) {
-                const double d = tp / tm, lt = log(-tp);
-                combi = -(((-1 + d) * tp * log(-2 * tp)) / d)
-                        - ((-1 + d) * SQ(tp) * (-2 + d + d * log(2) + log(-2 / tp) - d * lt)) / (2. * SQ(d))
-                        + (CU(tp) * (8 - 30 * d + 21 * SQ(d) + CU(d) - 8 * CU(d) * log(2) + log(256) + 8 * lt - 8 * CU(d) * lt)) / (24. * CU(d))
-                        + (SQ(SQ(tp)) * (-32 + 56 * d - 51 * SQ(d) + 30 * CU(d) - 3 * SQ(SQ(d)) + log(4096) - SQ(SQ(d)) * log(4096)
+                const double d = tp / tm, lt = ora_log(-tp);
+                combi = -(((-1 + d) * tp * ora_log(-2 * tp)) / d)
+                        - ((-1 + d) * SQ(tp) * (-2 + d + d * 0.6931471805599453 + ora_log(-2 / tp) - d * lt)) / (2. * SQ(d))
+                        + (CU(tp) * (8 - 30 * d + 21 * SQ(d) + CU(d) - 8 * CU(d) * 0.6931471805599453 + 5.545177444479562 + 8 * lt - 8 * CU(d) * lt)) / (24. * CU(d))
+                        + (SQ(SQ(tp)) * (-32 + 56 * d - 51 * SQ(d) + 30 * CU(d) - 3 * SQ(SQ(d)) + 8.317766166719343 - SQ(SQ(d)) * 8.317766166719343
                                          - 12 * lt + 12 * SQ(SQ(d)) * lt)) / (48. * SQ(SQ(d)));
             } else if (-tp > 1e2 && -tm > 1e2) {
-                const double d = tp / tm, lq = log((-1 + d) / d), lt = log(-tp);
-                combi = (-2 * (-1 + d) * lq) / tp - (2 * (-1 + log(-(d / ((-1 + d) * tp))))) / SQ(tp)
+                const double d = tp / tm, lq = ora_log((-1 + d) / d), lt = ora_log(-tp);
+                combi = (-2 * (-1 + d) * lq) / tp - (2 * (-1 + ora_log(-(d / ((-1 + d) * tp))))) / SQ(tp)
                         + (-6 + 4 * d + SQ(d) - 2 * CU(d) - 8 * lq + 8 * d * lq + 2 * CU(d) * lq - 2 * SQ(SQ(d)) * lq - 6 * lt + 6 * d * lt) / (3. * (-1 + d) * CU(tp))
                         + (8 - 12 * d + 3 * SQ(d) + 12 * lq - 24 * d * lq + 12 * SQ(d) * lq + 12 * lt - 24 * d * lt + 12 * SQ(d) * lt) / (3. * SQ(-1 + d) * SQ(SQ(tp)));
             } else
                 combi = ora_dilog(1 + 1 / (-2 + tp)) - ora_dilog((-1 + tm) / (-2 + tp)) + ora_dilog(1 + (1 + tm - tp) / tp) - ora_dilog(1 + 1 / tp);
 
             atu = g4 / (32 * M_PI * m4 * (1 + tm) * tp) *
-                  (2 * (2 * (1 + tm) * (tm - tp) - 2 * (1 + tm) * tp * atanh(1 / (1 - tp)) * atanh((tm - tp) / (-2 + tm + tp))
-                        + tm * tp * (-Lmt + Lmp) + (1 + tm) * (Lmt - Lmp - Ld) + tp * (-Lmt + Lmp + Ld) - tm * tp * log(tm / tp))
+                  (2 * (2 * (1 + tm) * (tm - tp) - 2 * (1 + tm) * tp * ora_atanh(1 / (1 - tp)) * ora_atanh((tm - tp) / (-2 + tm + tp))
+                        + tm * tp * (-Lmt + Lmp) + (1 + tm) * (Lmt - Lmp - Ld) + tp * (-Lmt + Lmp + Ld) - tm * tp * ora_log(tm / tp))
                    + (1 + tm) * tp * ((-SQ(Lmt) + SQ(Lmp)) / 2. + ora_dilog1over1mdiff(tp, tm))
                    - (1 + tm) * tp * (ora_dilog1pdiff(tm, tp) + combi));
             if (atu < 0) atu = gl33_tri(tp, tm, F_tu) * (g4 / (16 * M_PI * m4));
@@ -364,50 +375,69 @@ double ora_alphaTilde(ora_state *S, double Em, double Ep)   /* nuSIprop.hpp:924-
         tot += wgt * atu;
 
         /* s-t interference */
-        const ora_c z1 = (-I * (-1 + tm)) / (2 * I + gr);
-        const double z2 = 1 / (1 + tm);
-        const ora_c z3 = 1 / (2 - I * gr + tm);
-        const ora_c z4 = (1 + tm - tp) / (2 - I * gr + tm);
-        const ora_c z5 = (-I * (-1 + tp)) / (2 * I + gr);
-        const double z6 = 1 - tp / (1 + tm);
-        const double z7 = 1 - tm, z8 = 1 - tp;
-        ora_c d78, d51, d26, d43;
-        if (-tp < 1e-5) {
+        /* nuSIprop.hpp:1137-1144 */
+        const zc den = zmk(gr, 2.0);          /* 2I + gr   */
+        const zc ipg = zmk(gr, 1.0);          /* I + gr    */
+        const zc dtm = zmk(2 + tm, -gr);      /* 2 - I gr + tm */
+        zc d78, d51, d26, d43;
+        if (-tp < 1e-5) {   /* nuSIprop.hpp:1151-1167 */
             const double d = tp / tm;
-            const ora_c ltm = clog(tm), ltp = clog(tp), ld = clog(d);
-            const ora_c lq = clog(1 - I / (2 * I + gr)), lr = clog((I + gr) / (2 * I + gr));
-            d78 = tm * (-1 + ltm) + (SQ(tm) * (-1 + 2 * ltm)) / 4. - (tp * (-1 + ltp) + (SQ(tp) * (-1 + 2 * ltp)) / 4.);
-            d51 = (-tm + tp) * lq + ((-SQ(tm) + SQ(tp)) * (I * (1 + lq) + lq * gr)) / (2. * (I + gr));
-            d26 = (tp * (-1 + d - ld + ltp - d * ltp)) / d
-                  + (SQ(tp) * (-1 + SQ(d) + 2 * ld - 2 * ltp + 4 * d * ltp - 2 * SQ(d) * ltp)) / (4. * SQ(d))
-                  + (CU(tp) * (7 - 9 * d + 2 * CU(d) - 6 * ld + 6 * ltp - 18 * d * ltp + 18 * SQ(d) * ltp - 6 * CU(d) * ltp)) / (18. * CU(d));
-            d43 = ((-1 + d) * tp * lr) / d + ((-1 + d) * SQ(tp) * (I * ((1 + d) / (I + gr) - 2 / (2 * I + gr)) + (-1 + d) * lr)) / (2. * SQ(d));
+            const zc ltm = zlog(zre(tm)), ltp = zlog(zre(tp)), ld = zlog(zre(d));
+            const zc lq = zlog(zrsub(1.0, zdiv(zmk(0.0, 1.0), den))), lr = zlog(zdiv(ipg, den));
+            d78 = zsub(zadd(zscale(tm, zaddr(ltm, -1.0)), zdivr(zscale(SQ(tm), zaddr(zscale(2, ltm), -1.0)), 4.)),
+                       zadd(zscale(tp, zaddr(ltp, -1.0)), zdivr(zscale(SQ(tp), zaddr(zscale(2, ltp), -1.0)), 4.)));
+            d51 = zadd(zscale(-tm + tp, lq),
+                       zdiv(zscale(-SQ(tm) + SQ(tp), zadd(zmul(zmk(0.0, 1.0), zaddr(lq, 1.0)), zscale(gr, lq))), zscale(2., ipg)));
+            {
+                const zc a1 = zsub(zadd(zrsub(-1.0 + d, ld), ltp), zscale(d, ltp));
+                zc b2 = zaddr(zscale(2, ld), -1.0 + SQ(d));          /* -1 + d^2 + 2 ld */
+                b2 = zsub(b2, zscale(2, ltp));
+                b2 = zadd(b2, zscale(4 * d, ltp));
+                b2 = zsub(b2, zscale(2 * SQ(d), ltp));
+                zc b3 = zrsub(7 - 9 * d + 2 * CU(d), zscale(6, ld));  /* 7 - 9d + 2d^3 - 6 ld */
+                b3 = zadd(b3, zscale(6, ltp));
+                b3 = zsub(b3, zscale(18 * d, ltp));
+                b3 = zadd(b3, zscale(18 * SQ(d), ltp));
+                b3 = zsub(b3, zscale(6 * CU(d), ltp));
+                d26 = zadd(zadd(zdivr(zscale(tp, a1), d), zdivr(zscale(SQ(tp), b2), 4. * SQ(d))),
+                           zdivr(zscale(CU(tp), b3), 18. * CU(d)));
+            }
+            d43 = zadd(zdivr(zscale((-1 + d) * tp, lr), d),
+                       zdivr(zscale((-1 + d) * SQ(tp),
+                                    zadd(zmul(zmk(0.0, 1.0), zsub(zrdiv(1 + d, ipg), zrdiv(2, den))), zscale(-1 + d, lr))),
+                             2. * SQ(d)));
         } else {
-            d78 = ora_dilogdiff_c(z7, z8);
+            const zc z1 = zdiv(zmk(0.0, 1 - tm), den);     /* (-I(-1+tm))/(2I+gr) */
+            const double z2 = 1 / (1 + tm);
+            const zc z3 = zrdiv(1, dtm);
+            const zc z4 = zrdiv(1 + tm - tp, dtm);
+            const zc z5 = zdiv(zmk(0.0, 1 - tp), den);
+            const double z6 = 1 - tp / (1 + tm);
+            d78 = ora_dilogdiff_c(zre(1 - tm), zre(1 - tp));
             d51 = ora_dilogdiff_c(z5, z1);
-            d26 = ora_dilogdiff_c(z2, z6);
+            d26 = ora_dilogdiff_c(zre(z2), zre(z6));
             d43 = ora_dilogdiff_c(z4, z3);
         }
-        const double Lgp = log1p(SQ(1 + tp) / SQ(gr)), Lgm = log1p(SQ(1 + tm) / SQ(gr));
-        const double Am = carg(-1 + I * gr - tm), Ap = carg(-1 + I * gr - tp);
-        const double Bm = carg((gr + I * (1 + tm)) / (2 * I + gr)), Bp = carg((gr + I * (1 + tp)) / (2 * I + gr));
+        const double Lgp = ora_log1p(SQ(1 + tp) / SQ(gr)), Lgm = ora_log1p(SQ(1 + tm) / SQ(gr));
+        const double Am = zarg(zmk(-1 - tm, gr)), Ap = zarg(zmk(-1 - tp, gr));          /* carg(-1 + I gr - t) */
+        const double Bm = zarg(zdiv(zmk(gr, 1 + tm), den)), Bp = zarg(zdiv(zmk(gr, 1 + tp), den));
         double ast;
         if (maj)
             ast = g4 / (32 * M_PI * (1 + SQ(gr)) * m4) *
-                  (2 * M_PI * Am - 2 * M_PI * Ap + 2 * gr * (cimag(d51) + cimag(d26) + cimag(d43))
-                   - 2 * (creal(d51) + creal(d26) + creal(d43) + creal(d78)) - Bm * (2 * M_PI + 2 * gr * Lmt)
+                  (2 * M_PI * Am - 2 * M_PI * Ap + 2 * gr * (d51.i + d26.i + d43.i)
+                   - 2 * (d51.r + d26.r + d43.r + d78.r) - Bm * (2 * M_PI + 2 * gr * Lmt)
                    + Bp * (2 * M_PI + 2 * gr * Lmp) + (Am - Ap) * (4 * gr * tm + 2 * gr * Lmt)
-                   + 2 * gr * (carg(1 + tm) - carg(2 - I * gr + tm) + carg(1 - I * gr + tp)) * Ld
-                   + log(4 + SQ(gr)) * (Lmp - Lmt) + log(SQ(gr) + SQ(2 + tm)) * Ld - 2 * Lmt * log(-tp)
-                   - 2 * gr * M_PI * (log(SQ(tp)) + Ld) + 2 * gr * M_PI * log(SQ(tp)) + 4 * tm * log(tm / tp)
-                   + (-Lmp + Lmt - Ld) * (Lgp + 2 * log(gr)) - Ld * log1p(SQ(tm) + 2 * tm)
-                   + 2 * (SQ(gr) + tm) * (Lgp - Lgm) + 2 * (log(-tp) * (Lmp + Ld) + (Lgp - Lgm)));
+                   + 2 * gr * (zarg_real(1 + tm) - zarg(dtm) + zarg(zmk(1 + tp, -gr))) * Ld
+                   + ora_log(4 + SQ(gr)) * (Lmp - Lmt) + ora_log(SQ(gr) + SQ(2 + tm)) * Ld - 2 * Lmt * ora_log(-tp)
+                   - 2 * gr * M_PI * (ora_log(SQ(tp)) + Ld) + 2 * gr * M_PI * ora_log(SQ(tp)) + 4 * tm * ora_log(tm / tp)
+                   + (-Lmp + Lmt - Ld) * (Lgp + 2 * ora_log(gr)) - Ld * ora_log1p(SQ(tm) + 2 * tm)
+                   + 2 * (SQ(gr) + tm) * (Lgp - Lgm) + 2 * (ora_log(-tp) * (Lmp + Ld) + (Lgp - Lgm)));
         else
             ast = g4 / (32 * M_PI * (1 + SQ(gr)) * m4) *
-                  (gr * cimag(d51) - 2 * (creal(d51 + d78)) + 2 * Bm * (-M_PI - gr * Lmt)
+                  (gr * d51.i - 2 * (d51.r + d78.r) + 2 * Bm * (-M_PI - gr * Lmt)
                    + 2 * Am * (M_PI + gr * tm + gr * Lmt) - 2 * Ap * (M_PI + gr * tm + gr * Lmt)
-                   + 2 * Bp * (M_PI + gr * Lmp) - 2 * Lmt * log(-tp) + 2 * tm * log(tm / tp) + 2 * Lmp * log(-tp)
-                   + (Lmp - Lmt) * (log(4 + SQ(gr)) - 2 * log(gr) - Lgp) + (1 + tm + SQ(gr)) * (Lgp - Lgm));
+                   + 2 * Bp * (M_PI + gr * Lmp) - 2 * Lmt * ora_log(-tp) + 2 * tm * ora_log(tm / tp) + 2 * Lmp * ora_log(-tp)
+                   + (Lmp - Lmt) * (ora_log(4 + SQ(gr)) - 2 * ora_log(gr) - Lgp) + (1 + tm + SQ(gr)) * (Lgp - Lgm));
         ast *= uk;
         tot += wgt * ast;
         const double asu = maj ? ast : 0;
@@ -417,14 +447,14 @@ double ora_alphaTilde(ora_state *S, double Em, double Ep)   /* nuSIprop.hpp:924-
         double app = 0;
         if (-tp > 4 && S->p.phiphi) {
             if (-tp < 1e4) {
-                const double xx[2] = {-tp, log10(tp / tm)};
+                const double xx[2] = {-tp, ora_log10(tp / tm)};
                 double v;
                 pp_lookup(S, &S->spl_at, xx, &v);
                 app = g4 / m4 * v;
             } else
                 app = g4 / m4 *
-                      (6 * tm * log(-tm) - tp * SQ(log(-tm)) + 2 * (-8 * tm + 8 * tp + 4 * tp * log(-tm) + log(tm - tp) * (tm - tp - tp * log(tm / tp)))
-                       - 2 * (2 * tm + 5 * tp) * log(-tp) + tp * SQ(log(-tp)) - 2 * tp * ora_dilog(1 - tm / tp)) / (128. * M_PI * tp);
+                      (6 * tm * ora_log(-tm) - tp * SQ(ora_log(-tm)) + 2 * (-8 * tm + 8 * tp + 4 * tp * ora_log(-tm) + ora_log(tm - tp) * (tm - tp - tp * ora_log(tm / tp)))
+                       - 2 * (2 * tm + 5 * tp) * ora_log(-tp) + tp * SQ(ora_log(-tp)) - 2 * tp * ora_dilog(1 - tm / tp)) / (128. * M_PI * tp);
             app *= uk;
             if (maj) app *= 2;
             app *= 2;
@@ -467,25 +497,25 @@ double ora_alpha(ora_state *S, double Em, double Ep, double Emp, double Epp)   /
         tot += wgt * as;
         if (!S->p.non_resonant) continue;
 
-        const double Lmt = log1p(-tm), Lmp = log1p(-tp);
-        const double lSm = log(Sm), lSp = log(Sp);
-        const double Lmm = log1p(Sm + tm), Lpm = log1p(Sp + tm), Lmq = log1p(Sm + tp), Lpq = log1p(Sp + tp);
+        const double Lmt = ora_log1p(-tm), Lmp = ora_log1p(-tp);
+        const double lSm = ora_log(Sm), lSp = ora_log(Sp);
+        const double Lmm = ora_log1p(Sm + tm), Lpm = ora_log1p(Sp + tm), Lmq = ora_log1p(Sm + tp), Lpq = ora_log1p(Sp + tp);
         /* t channel */
         double at;
         if (maj) {
-            const double LA = log(((1 + Sm + tm) * (-1 + tp)) / ((-1 + tm) * (1 + Sm + tp)));
-            const double LB = log(((1 + Sp + tm) * (-1 + tp)) / ((-1 + tm) * (1 + Sp + tp)));
+            const double LA = ora_log(((1 + Sm + tm) * (-1 + tp)) / ((-1 + tm) * (1 + Sm + tp)));
+            const double LB = ora_log(((1 + Sp + tm) * (-1 + tp)) / ((-1 + tm) * (1 + Sp + tp)));
             const double SS = Sm * Sp;
             const double inner = SS * (-tm + tp) * lSm + SS * (tm - tp) * lSp - SS * Lmm - SS * tp * Lmm + SS * Lpm + SS * tp * Lpm
                                  - Sp * LA - Sp * tm * LA - Sp * tp * LA - Sp * tm * tp * LA
-                                 + SS * log(1 + Sm + tp) + SS * tm * Lmq
+                                 + SS * ora_log(1 + Sm + tp) + SS * tm * Lmq
                                  + Sm * LB + Sm * tm * LB + Sm * tp * LB + Sm * tm * tp * LB
-                                 - SS * log(1 + Sp + tp) - SS * tm * Lpq;
+                                 - SS * ora_log(1 + Sp + tp) - SS * tm * Lpq;
             at = g4 / (Sm * Sp * 16 * M_PI * m4) *
                  (-((Sm - Sp) * (3 + 2 * tm * (-1 + tp) - 2 * tp) * (tm - tp)) / ((-1 + tm) * (-1 + tp))
                   + 2 * inner / ((1 + tm) * (1 + tp))
-                  - ((SS * log((Sm * (1 + Sp + tm)) / (Sp * (1 + Sm + tm)))) / SQ(1 + tm)
-                     + (((Sm - Sp) * (tm - tp) * (1 + tp)) / (1 + tm) - SS * log((Sm * (1 + Sp + tp)) / (Sp * (1 + Sm + tp)))) / SQ(1 + tp)));
+                  - ((SS * ora_log((Sm * (1 + Sp + tm)) / (Sp * (1 + Sm + tm)))) / SQ(1 + tm)
+                     + (((Sm - Sp) * (tm - tp) * (1 + tp)) / (1 + tm) - SS * ora_log((Sm * (1 + Sp + tp)) / (Sp * (1 + Sm + tp)))) / SQ(1 + tp)));
             if (at < 0) at = gl33_rect(tp, tm, Sm, Sp, F_t_maj) * (g4 / (16 * M_PI * m4));
         } else {
             const double brk = -((tm - tp) * (2 + tm * (-1 + tp) - tp)) - 2 * (-1 + tm) * (-1 + tp) * (Lmt - Lmp);
@@ -512,23 +542,23 @@ double ora_alpha(ora_state *S, double Em, double Ep, double Emp, double Epp)   /
             double Fp, Fm;
             if (tp < -1) Fp = ora_dilog((1 + Sm + tp) / Sm) - ora_dilog((1 + Sp + tp) / Sp);
             else Fp = -ora_dilog(Sm / (1 + Sm + tp)) + ora_dilog(Sp / (1 + Sp + tp))
-                      - 0.5 * (SQ(log((1 + Sm + tp) / Sm)) - SQ(log((1 + Sp + tp) / Sp)));
+                      - 0.5 * (SQ(ora_log((1 + Sm + tp) / Sm)) - SQ(ora_log((1 + Sp + tp) / Sp)));
             if (tm < -1) Fm = -ora_dilog((1 + Sm + tm) / Sm) + ora_dilog((1 + Sp + tm) / Sp);
             else Fm = ora_dilog(Sm / (1 + Sm + tm)) - ora_dilog(Sp / (1 + Sp + tm))
-                      + 0.5 * (SQ(log((1 + Sm + tm) / Sm)) - SQ(log((1 + Sp + tm) / Sp)));
-            const double lap = (tp > -1) ? log1p(tp) : log(-1 - tp);
-            const double lam = (tm > -1) ? log1p(tm) : log(-1 - tm);
+                      + 0.5 * (SQ(ora_log((1 + Sm + tm) / Sm)) - SQ(ora_log((1 + Sp + tm) / Sp)));
+            const double lap = (tp > -1) ? ora_log1p(tp) : ora_log(-1 - tp);
+            const double lam = (tm > -1) ? ora_log1p(tm) : ora_log(-1 - tm);
             const double SS = Sm * Sp, P = (1 + tm) * (1 + tp);
-            const double l2m = log((2 + Sm) / Sm), l2p = log((2 + Sp) / Sp);
+            const double l2m = ora_log((2 + Sm) / Sm), l2p = ora_log((2 + Sp) / Sp);
             atu = g4 / (32 * M_PI * m4 * Sm * Sp * (1 + tm) * (1 + tp)) *
                   (-4 * (Sm - Sp) * (1 + tm) * (tm - tp) * (1 + tp)
-                   + 2 * SS * tp * (log(Sm / Sp) - Lmm + Lpm)
+                   + 2 * SS * tp * (ora_log(Sm / Sp) - Lmm + Lpm)
                    + 2 * Sp * (1 + tm) * (1 + tp) * (Lmt - Lmm - Lmp + Lmq)
                    - 2 * Sm * (1 + tm) * (1 + tp) * (Lmt - Lpm - Lmp + Lpq)
                    + 2 * SS * (-Lmm + Lpm + Lmq - Lpq)
-                   + SS * (1 + tm) * (1 + tp) * (l2m * (lSp + Lmq) - l2p * (lSm + Lpq) + Lmp * (log(Sm / Sp) - Lmq + Lpq))
-                   + SS * (1 + tm) * (1 + tp) * ((lSp + Lmm) * (log(Sm / (2 + Sm)) + Lmt - lam) + (lSm + Lpm) * (l2p - Lmt + lam))
-                   + SS * (log(Sp / Sm) + Lmq - Lpq) * (2 * tm + P * lap)
+                   + SS * (1 + tm) * (1 + tp) * (l2m * (lSp + Lmq) - l2p * (lSm + Lpq) + Lmp * (ora_log(Sm / Sp) - Lmq + Lpq))
+                   + SS * (1 + tm) * (1 + tp) * ((lSp + Lmm) * (ora_log(Sm / (2 + Sm)) + Lmt - lam) + (lSm + Lpm) * (l2p - Lmt + lam))
+                   + SS * (ora_log(Sp / Sm) + Lmq - Lpq) * (2 * tm + P * lap)
                    + SS * (1 + tm) * (1 + tp) * (ora_dilog((1 + Sm + tm) / (2 + Sm)) - ora_dilog((1 + Sp + tm) / (2 + Sp))
                                                  - ora_dilog((1 + Sm + tp) / (2 + Sm)) + ora_dilog((1 + Sp + tp) / (2 + Sp)))
                    + SS * (1 + tm) * (1 + tp) * (Fp + Fm));
@@ -541,41 +571,43 @@ double ora_alpha(ora_state *S, double Em, double Ep, double Emp, double Epp)   /
 
         /* s-t interference: 8 GSL complex dilogs (nuSIprop.hpp:1431-1451) */
         const double z1 = (1 + Sm + tm) / (1 + tm);
-        const ora_c z2 = (1 + Sm + tm) / (2 - I * gr + tm);
+        const zc dtm = zmk(2 + tm, -gr), dtp = zmk(2 + tp, -gr);       /* 2 - I gr + t */
+        const zc z2 = zrdiv(1 + Sm + tm, dtm);
         const double z3 = (1 + Sp + tm) / (1 + tm);
-        const ora_c z4 = (1 + Sp + tm) / (2 - I * gr + tm);
+        const zc z4 = zrdiv(1 + Sp + tm, dtm);
         const double z5 = (1 + Sm + tp) / (1 + tp);
-        const ora_c z6 = (1 + Sm + tp) / (2 - I * gr + tp);
+        const zc z6 = zrdiv(1 + Sm + tp, dtp);
         const double z7 = (1 + Sp + tp) / (1 + tp);
-        const ora_c z8 = (1 + Sp + tp) / (2 - I * gr + tp);
+        const zc z8 = zrdiv(1 + Sp + tp, dtp);
         double R[9], J[9];
         ora_complex_dilog_xy(z1, 0, &R[1], &J[1]);
-        ora_complex_dilog_xy(creal(z2), cimag(z2), &R[2], &J[2]);
+        ora_complex_dilog_xy(z2.r, z2.i, &R[2], &J[2]);
         ora_complex_dilog_xy(z3, 0, &R[3], &J[3]);
-        ora_complex_dilog_xy(creal(z4), cimag(z4), &R[4], &J[4]);
+        ora_complex_dilog_xy(z4.r, z4.i, &R[4], &J[4]);
         ora_complex_dilog_xy(z5, 0, &R[5], &J[5]);
-        ora_complex_dilog_xy(creal(z6), cimag(z6), &R[6], &J[6]);
+        ora_complex_dilog_xy(z6.r, z6.i, &R[6], &J[6]);
         ora_complex_dilog_xy(z7, 0, &R[7], &J[7]);
-        ora_complex_dilog_xy(creal(z8), cimag(z8), &R[8], &J[8]);
-        const double Lsm = log1p(SQ(-1 + Sm) / SQ(gr)), Lsp = log1p(SQ(-1 + Sp) / SQ(gr));
+        ora_complex_dilog_xy(z8.r, z8.i, &R[8], &J[8]);
+        const double Lsm = ora_log1p(SQ(-1 + Sm) / SQ(gr)), Lsp = ora_log1p(SQ(-1 + Sp) / SQ(gr));
         double ast;
         if (maj) {
-            const double cm = carg(-(1 / (1 + tm))), cp = carg(-(1 / (1 + tp)));
-            const double L2m = log1p(SQ(2 + tm) / SQ(gr)), L2p = log1p(SQ(2 + tp) / SQ(gr));
-            const double am = log(fabs(1 + tm)), ap = log(fabs(1 + tp));
+            const double cm = zarg_real(-(1 / (1 + tm))), cp = zarg_real(-(1 / (1 + tp)));
+            const zc nm_ = zmk(-1 + Sm, gr), np_ = zmk(-1 + Sp, gr);      /* -1 + I gr + S */
+            const double L2m = ora_log1p(SQ(2 + tm) / SQ(gr)), L2p = ora_log1p(SQ(2 + tp) / SQ(gr));
+            const double am = ora_log(fabs(1 + tm)), ap = ora_log(fabs(1 + tp));
             ast = g4 / (32 * M_PI * (1 + SQ(gr)) * m4) *
                   (2 * gr * (J[1] - J[2] - J[3] + J[4] - J[5] + J[6] + J[7] - J[8])
                    - 2 * (R[1] - R[2] - R[3] + R[4] - R[5] + R[6] + R[7] - R[8])
-                   + 2 * gr * (cm - carg(-((-1 + I * gr + Sm) / (2 - I * gr + tm)))) * Lmm
-                   - 2 * gr * (cm - carg(-((-1 + I * gr + Sp) / (2 - I * gr + tm)))) * Lpm
-                   + 2 * gr * (cp - carg(-((-1 + I * gr + Sp) / (2 - I * gr + tp)))) * Lpq
-                   - 2 * gr * (cp - carg(-((-1 + I * gr + Sm) / (2 - I * gr + tp)))) * Lmq
-                   + 2 * (gr * carg(-1 + I * gr + Sm) - gr * carg(-1 + I * gr + Sp) + Lsp / 2. - Lsm / 2. + lSm - lSp) * (2 * (tm - tp) + (Lmt - Lmp))
+                   + 2 * gr * (cm - zarg(zneg(zdiv(nm_, dtm)))) * Lmm
+                   - 2 * gr * (cm - zarg(zneg(zdiv(np_, dtm)))) * Lpm
+                   + 2 * gr * (cp - zarg(zneg(zdiv(np_, dtp)))) * Lpq
+                   - 2 * gr * (cp - zarg(zneg(zdiv(nm_, dtp)))) * Lmq
+                   + 2 * (gr * zarg(nm_) - gr * zarg(np_) + Lsp / 2. - Lsm / 2. + lSm - lSp) * (2 * (tm - tp) + (Lmt - Lmp))
                    + Lmm * (Lsm - L2m - 2 * (lSm - am)) - Lpm * (Lsp - L2m - 2 * (lSp - am))
                    - Lmq * (Lsm - L2p - 2 * (lSm - ap)) + Lpq * (Lsp - L2p - 2 * (lSp - ap)));
         } else
             ast = g4 / (32 * M_PI * (1 + SQ(gr)) * m4) *
-                  ((2 * gr * carg(-1 + I * gr + Sm) - 2 * gr * carg(-1 + I * gr + Sp) + 2 * lSm - 2 * lSp + Lsp - Lsm) * (tm - tp + Lmt - Lmp));
+                  ((2 * gr * zarg(zmk(-1 + Sm, gr)) - 2 * gr * zarg(zmk(-1 + Sp, gr)) + 2 * lSm - 2 * lSp + Lsp - Lsm) * (tm - tp + Lmt - Lmp));
         ast *= uk;
         tot += wgt * ast;
         const double asu = maj ? ast : 0.;
@@ -586,12 +618,12 @@ double ora_alpha(ora_state *S, double Em, double Ep, double Emp, double Epp)   /
         if (Sm > 4 && S->p.phiphi) {
             if (Sm < 1e4) {
                 const double d = Sp / Sm;
-                const double xx[3] = {Sm, log(-Sm / tm) / log(d) * 1.0001, log10(d)};
+                const double xx[3] = {Sm, ora_log(-Sm / tm) / ora_log(d) * 1.0001, ora_log10(d)};
                 double v;
                 pp_lookup(S, &S->spl_a, xx, &v);
                 app = g4 / m4 * fabs(v);
             } else if (tm < -1) {
-                const double l1m = log(-1 - tm), l0m = log(-tm), l1p = log(-1 - tp), l0p = log(-tp);
+                const double l1m = ora_log(-1 - tm), l0m = ora_log(-tm), l1p = ora_log(-1 - tp), l0p = ora_log(-tp);
                 app = g4 / m4 *
                       ((-Sm + Sp) * ((tm - tp) * (Sp * (-2 + tm + tp) + Sm * (-2 - 24 * Sp + tm + tp))
                                      + 4 * (-(Sp * (1 + tm)) + Sm * (-1 + 2 * Sp + (-1 + Sp) * tm)) * l1m
@@ -602,7 +634,7 @@ double ora_alpha(ora_state *S, double Em, double Ep, double Emp, double Epp)   /
                        + 2 * SQ(Sp) * lSm * ((-3 - 2 * Sm) * (tm - tp) + 2 * SQ(Sm) * ((1 + tm) * l1m - tm * l0m - (1 + tp) * l1p + tp * l0p)))
                       / (256. * M_PI * SQ(Sm) * SQ(Sp));
             } else if (tp < -1) {
-                const double l1p = log(-1 - tp), l0p = log(-tp);
+                const double l1p = ora_log(-1 - tp), l0p = ora_log(-tp);
                 app = g4 / m4 *
                       ((2 * SQ(Sm) * lSp * ((1 + tp) * (-3 - 2 * Sp + 2 * SQ(Sp) * l1p) - 2 * SQ(Sp) * tp * l0p)
                         + (Sm - Sp) * ((1 + tp) * (-3 * (Sm + Sp + 8 * Sm * Sp) + (Sm + Sp) * tp)
@@ -644,6 +676,10 @@ static void build_grid(ora_state *S)
     }
 }
 
+/* nuSIprop.hpp:130-163.  The reference keeps std::complex<double> U and uses
+ * only std::norm(U); the entries are formed here with the same real
+ * operations (real*complex component-wise, s13/del by Smith's division) so
+ * that the product's host code, which does the same, gets identical bits. */
 static void build_pmns(ora_state *S)
 {
     double t12, t13, t23, dcp;
@@ -651,16 +687,19 @@ static void build_pmns(ora_state *S)
     else { t12 = 33.45 * (M_PI / 180); t13 = 8.61 * (M_PI / 180); t23 = 49.3 * (M_PI / 180); dcp = 286.0 * (M_PI / 180); }
     const double c12 = cos(t12), c13 = cos(t13), c23 = cos(t23);
     const double s12 = sin(t12), s13 = sin(t13), s23 = sin(t23);
-    const ora_c del = cos(dcp) + I * sin(dcp);
-    S->U[0][0] = c12 * c13;
-    S->U[0][1] = s12 * c13;
-    S->U[0][2] = s13 * 1.0 / del;
-    S->U[1][0] = -s12 * c23 - c12 * s23 * s13 * del;
-    S->U[1][1] = c12 * c23 - s12 * s23 * s13 * del;
-    S->U[1][2] = s23 * c13;
-    S->U[2][0] = s12 * s23 - c12 * c23 * s13 * del;
-    S->U[2][1] = -c12 * s23 - s12 * c23 * s13 * del;
-    S->U[2][2] = c23 * c13;
+    const zc del = zmk(cos(dcp), sin(dcp));
+    zc U[3][3];
+    U[0][0] = zre(c12 * c13);
+    U[0][1] = zre(s12 * c13);
+    U[0][2] = zrdiv(s13 * 1.0, del);
+    U[1][0] = zrsub(-s12 * c23, zscale(c12 * s23 * s13, del));
+    U[1][1] = zrsub(c12 * c23, zscale(s12 * s23 * s13, del));
+    U[1][2] = zre(s23 * c13);
+    U[2][0] = zrsub(s12 * s23, zscale(c12 * c23 * s13, del));
+    U[2][1] = zrsub(-c12 * s23, zscale(s12 * c23 * s13, del));
+    U[2][2] = zre(c23 * c13);
+    for (int f = 0; f < 3; ++f)
+        for (int k = 0; k < 3; ++k) S->U2m[f][k] = U[f][k].r * U[f][k].r + U[f][k].i * U[f][k].i;
 }
 
 ora_state *ora_create(const ora_params *p, int *err)
@@ -735,10 +774,7 @@ void ora_grid(const ora_state *S, double *Emin, double *Emax, double *Enu, doubl
 void ora_mixing(const ora_state *S, double *U2)
 {
     for (int f = 0; f < 3; ++f)
-        for (int k = 0; k < 3; ++k) {
-            const ora_c u = S->U[f][k];
-            U2[3 * f + k] = creal(u) * creal(u) + cimag(u) * cimag(u);
-        }
+        for (int k = 0; k < 3; ++k) U2[3 * f + k] = S->U2m[f][k];
 }
 
 int ora_prepare(ora_state *S)   /* nuSIprop.hpp:184-205 */

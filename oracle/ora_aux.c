@@ -5,8 +5,8 @@
  */
 #define _GNU_SOURCE
 #include <math.h>
-#include <complex.h>
 #include "ora_aux.h"
+#include "ora_libm.h"
 #include "ora_specfun.h"
 
 #define SQ(a) ((a) * (a))
@@ -19,41 +19,46 @@ const double ora_gl_x[3] = {-0.7745966692414834, 0.0, 0.7745966692414834}; /* = 
 /* aux.hpp:63-75 */
 double ora_atandiff(double x, double y)
 {
-    if (fabs(x) < 1e2 || fabs(y) < 1e2 || x * y < 0) return atan(x) - atan(y);
+    if (fabs(x) < 1e2 || fabs(y) < 1e2 || x * y < 0) return ora_atan(x) - ora_atan(y);
     const double ix = 1. / x, iy = 1. / y;
     return -ix + CU(ix) / 3. - (-iy + CU(iy) / 3.);
 }
 
-static ora_c cli2(ora_c z)
+static zc cli2(zc z)
 {
     double re, im;
-    ora_complex_dilog_xy(creal(z), cimag(z), &re, &im);
-    return re + I * im;
+    ora_complex_dilog_xy(z.r, z.i, &re, &im);
+    return zmk(re, im);
 }
 
-/* asymptotic Li2 for |z| >> 1 used by aux.hpp:84-89 */
-static ora_c li2_asym(ora_c z)
+/* asymptotic Li2 for |z| >> 1 used by aux.hpp:84-89:
+ *   -1/(16 z^4) - 1/(9 z^3) - 1/(4 z^2) - 1/z - (I/2)(-s 2 pi log z - I log^2 z) */
+static zc li2_asym(zc z)
 {
-    const int s = (cimag(z) >= 0) ? 1 : -1;
-    const ora_c L = clog(z);
-    const ora_c z2 = z * z;
-    return -1 / (16. * (z2 * z2)) - 1 / (9. * (z * z * z)) - 1 / (4. * z2) - 1 / z
-           - I / 2 * (-s * 2 * M_PI * L - I * (L * L));
+    const double s = (z.i >= 0) ? 1.0 : -1.0;
+    const zc L = zlog(z);
+    const zc z2 = zmul(z, z);
+    const zc t = zsub(zscale(-s * 2 * M_PI, L), zmul(zmk(0.0, 1.0), zmul(L, L)));
+    zc r = zrdiv(-1, zscale(16., zmul(z2, z2)));
+    r = zsub(r, zrdiv(1, zscale(9., zmul(zmul(z, z), z))));
+    r = zsub(r, zrdiv(1, zscale(4., z2)));
+    r = zsub(r, zrdiv(1, z));
+    return zsub(r, zmul(zmk(0.0, 0.5), t));
 }
 
 /* aux.hpp:77-96 */
-ora_c ora_dilogdiff_c(ora_c x, ora_c y)
+zc ora_dilogdiff_c(zc x, zc y)
 {
-    if (cabs(x) > 1e2 && cabs(y) > 1e2) return li2_asym(x) - li2_asym(y);
-    const ora_c a = cli2(x), b = cli2(y);
-    return creal(a) + I * cimag(a) - creal(b) - I * cimag(b);
+    if (zabs(x) > 1e2 && zabs(y) > 1e2) return zsub(li2_asym(x), li2_asym(y));
+    const zc a = cli2(x), b = cli2(y);
+    return zmk(a.r - b.r, a.i - b.i);
 }
 
 /* aux.hpp:98-113 : Li2(-x) - Li2(-y) */
 double ora_dilogdiff(double x, double y)
 {
     if (x > 1e2 && y > 1e2) {
-        const double lx = log(x), ly = log(y), ix = 1. / x, iy = 1. / y;
+        const double lx = ora_log(x), ly = ora_log(y), ix = 1. / x, iy = 1. / y;
         return -SQ(lx) / 2. + ix - SQ(ix) / 4. + CU(ix) / 9. - SQ(SQ(ix)) / 16
                - (-SQ(ly) / 2. + iy - SQ(iy) / 4. + CU(iy) / 9. - SQ(SQ(iy)) / 16);
     }
@@ -66,14 +71,14 @@ double ora_dilogdiff(double x, double y)
 /* aux.hpp:115-130 : Li2(-1-x) - Li2(-1-y) */
 static double d1m_big(double v)
 {
-    const double l = log(v);
+    const double l = ora_log(v);
     return -SQ(l) / 2. + (1 - l) / v + (-7 + 2 * l) / (4. * SQ(v)) + (19 - 3 * l) / (9. * CU(v))
            + (-125 + 12 * l) / (48. * SQ(SQ(v)));
 }
 static double d1m_small(double v)
 {
-    return -v * log(2) + (SQ(v) * (-1 + log(4))) / 4. + (CU(v) * (5 - 8 * log(2))) / 24.
-           + SQ(SQ(v)) * (-1. / 6. + log(2) / 4.);
+    return -v * 0.6931471805599453 + (SQ(v) * (-1 + 1.3862943611198906)) / 4. + (CU(v) * (5 - 8 * 0.6931471805599453)) / 24.
+           + SQ(SQ(v)) * (-1. / 6. + 0.6931471805599453 / 4.);
 }
 double ora_dilog1mdiff(double x, double y)
 {
@@ -85,13 +90,13 @@ double ora_dilog1mdiff(double x, double y)
 /* aux.hpp:132-148 : Li2(1+x) - Li2(1+y), x,y < 0 */
 static double d1p_big(double v)
 {
-    const double l = log(-v);
+    const double l = ora_log(-v);
     return (-1 - 3 * l) / (9. * CU(v)) + (-1 - l) / v - SQ(l) / 2. + (1 + 2 * l) / (4. * SQ(v))
            + (1 + 4 * l) / (16. * SQ(SQ(v)));
 }
 static double d1p_small(double v)
 {
-    const double l = log(-v);
+    const double l = ora_log(-v);
     return v * (1 - l) + (SQ(v) * (-1 + 2 * l)) / 4. + (CU(v) * (1 - 3 * l)) / 9.
            + (SQ(SQ(v)) * (-1 + 4 * l)) / 16.;
 }
@@ -109,7 +114,7 @@ static double d1o_big(double v)
 }
 static double d1o_small(double v)
 {
-    const double l = log(-v);
+    const double l = ora_log(-v);
     return (SQ(SQ(v)) * (-19 - 12 * l)) / 48. + (CU(v) * (-7 - 6 * l)) / 18.
            + (SQ(v) * (-1 - 2 * l)) / 4. + v * (1 - l);
 }

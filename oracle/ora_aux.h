@@ -13,15 +13,13 @@
  */
 #ifndef NUSI_ORA_AUX_H
 #define NUSI_ORA_AUX_H
-#include <complex.h>
-
-typedef double _Complex ora_c;
+#include "ora_cplx.h"
 
 extern const double ora_gl_w[3];
 extern const double ora_gl_x[3];
 
 double ora_atandiff(double x, double y);
-ora_c ora_dilogdiff_c(ora_c x, ora_c y);
+zc ora_dilogdiff_c(zc x, zc y);
 double ora_dilogdiff(double x, double y);
 double ora_dilog1mdiff(double x, double y);
 double ora_dilog1pdiff(double x, double y);

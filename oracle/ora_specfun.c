@@ -1,20 +1,114 @@
 /*
  * nuSIprop oracle -- special functions.  TEST INFRASTRUCTURE ONLY.
  * See ora_specfun.h for what is restated and how it is pinned.
+ *
+ * Two implementations:
+ *   ora_dilog / ora_complex_dilog_xy / ora_li2 / ora_li3  (used by the
+ *     restatement): fp64, Bernoulli series in u = -log(1-z) after the
+ *     z->1/z, z->1-z maps (Li2) and the Taylor series of Li3(1-e^-u), built
+ *     from ora_libm.c and correctly rounded IEEE operations only, so that the
+ *     GPU, which runs the same sequence, reproduces them bit for bit;
+ *   ora_*_ld: the same functions in x87 long double, ~0.5 ulp after the
+ *     final rounding -- an independent accuracy yardstick for the tests.
  */
 #define _GNU_SOURCE
 #include <complex.h>
 #include <math.h>
 #include "ora_specfun.h"
+#include "ora_libm.h"
+#include "ora_cplx.h"
 #include "coeffs.h"
 
-typedef long double _Complex lcplx;
+/* ------------------------------------------------------------------ fp64 -- */
+static const double ZETA2 = 1.64493406684822643647;   /* pi^2/6 */
+static const double PI_D = 3.14159265358979323846;
 
+static double li2_useries(double u)
+{
+    const double u2 = u * u;
+    double p = ora_li2_bern_d[9];
+    for (int k = 8; k >= 0; --k) p = fma(p, u2, ora_li2_bern_d[k]);
+    return fma(u * u2, p, u - 0.25 * u2);
+}
+
+double ora_dilog(double x)
+{
+    double add = 0.0, sgn = 1.0;
+    if (x > 1.0) {
+        const double L = ora_log(x);
+        add = 2.0 * ZETA2 - 0.5 * L * L;
+        sgn = -1.0;
+        x = 1.0 / x;
+    } else if (x < -1.0) {
+        const double L = ora_log(-x);
+        add = -ZETA2 - 0.5 * L * L;
+        sgn = -1.0;
+        x = 1.0 / x;
+    }
+    if (x == 1.0) return add + sgn * ZETA2;
+    if (x > 0.5) {
+        add += sgn * (ZETA2 - ora_log(x) * ora_log1p(-x));
+        sgn = -sgn;
+        x = 1.0 - x;
+    }
+    if (x == 0.0) return add;
+    return add + sgn * li2_useries(-ora_log1p(-x));
+}
+
+double ora_li2(double x) { return ora_dilog(x); }
+
+void ora_complex_dilog_xy(double x, double y, double *re, double *im)
+{
+    if (y == 0.0) {
+        /* GSL: on the real axis the imaginary part is -pi*log(x) for x >= 1 */
+        *re = ora_dilog(x);
+        *im = (x >= 1.0) ? -PI_D * ora_log(x) : 0.0;
+        return;
+    }
+    zc z = zmk(x, y), add = zmk(0.0, 0.0);
+    double sgn = 1.0;
+    if (x * x + y * y > 1.0) {
+        const zc l = zlog(zmk(-z.r, -z.i));
+        const zc h = zscale(0.5, zmul(l, l));
+        add = zmk(-ZETA2 - h.r, -h.i);
+        sgn = -1.0;
+        z = zrdiv(1.0, z);
+    }
+    if (z.r > 0.5) {
+        const zc P = zmul(zlog(z), zlog(zmk(1.0 - z.r, -z.i)));
+        add = zadd(add, zscale(sgn, zmk(ZETA2 - P.r, -P.i)));
+        sgn = -sgn;
+        z = zmk(1.0 - z.r, -z.i);
+    }
+    const double a = -z.r, b = -z.i;
+    const zc u = zmk(-0.5 * ora_log1p(2.0 * a + (a * a + b * b)), -ora_atan2(b, 1.0 + a));
+    const zc u2 = zmul(u, u);
+    zc p = zmk(ora_li2_bern_d[ORA_LI2D_N - 1], 0.0);
+    for (int k = ORA_LI2D_N - 2; k >= 0; --k) {
+        p = zmul(p, u2);
+        p.r = p.r + ora_li2_bern_d[k];
+    }
+    const zc q = zscale(0.25, u2);
+    const zc s = zadd(zmk(u.r - q.r, u.i - q.i), zmul(zmul(u, u2), p));
+    const zc r = zadd(add, zscale(sgn, s));
+    *re = r.r;
+    *im = r.i;
+}
+
+double ora_li3(double x)
+{
+    const double u = -ora_log1p(-x);
+    double p = ora_li3_u_d[ORA_LI3U_N - 1];
+    for (int k = ORA_LI3U_N - 2; k >= 0; --k) p = fma(p, u, ora_li3_u_d[k]);
+    return p * u;
+}
+
+/* ----------------------------------------------------------- long double -- */
+typedef long double _Complex lcplx;
 static const long double LPI = 3.141592653589793238462643383279502884L;
 #define LZETA2 (LPI * LPI / 6.0L)
 static const long double LEPS = 1.0e-21L;
 
-/* Li2(z) = u - u^2/4 + sum_k B_2k u^(2k+1)/(2k+1)!,  u = -log(1-z)  (real) */
 static long double li2_bern_real(long double x)
 {
     const long double u = -log1pl(-x);
@@ -30,43 +124,36 @@ static long double li2_bern_real(long double x)
     return sum;
 }
 
-/* Re Li2(x) for every real x (GSL gsl_sf_dilog semantics). */
 static long double li2_real_ld(long double x)
 {
-    if (x > 1.0L) {                  /* Re Li2(x) = pi^2/3 - ln^2(x)/2 - Li2(1/x) */
+    if (x > 1.0L) {
         const long double L = logl(x);
         return 2.0L * LZETA2 - 0.5L * L * L - li2_real_ld(1.0L / x);
     }
     if (x == 1.0L) return LZETA2;
-    if (x > 0.5L)                    /* Li2(x) = pi^2/6 - ln(x) ln(1-x) - Li2(1-x) */
-        return LZETA2 - logl(x) * log1pl(-x) - li2_real_ld(1.0L - x);
-    if (x < -1.0L) {                 /* Li2(x) = -pi^2/6 - ln^2(-x)/2 - Li2(1/x) */
+    if (x > 0.5L) return LZETA2 - logl(x) * log1pl(-x) - li2_real_ld(1.0L - x);
+    if (x < -1.0L) {
         const long double L = logl(-x);
         return -LZETA2 - 0.5L * L * L - li2_real_ld(1.0L / x);
     }
     if (x == 0.0L) return 0.0L;
-    return li2_bern_real(x);         /* -1 <= x <= 1/2: |u| <= ln 2 */
+    return li2_bern_real(x);
 }
 
-/* log(1+w) without the cancellation of forming 1+w for small w */
 static lcplx clog1pl(lcplx w)
 {
     const long double a = creall(w), b = cimagl(w);
-    const long double re = 0.5L * log1pl(2.0L * a + (a * a + b * b));
-    const long double im = atan2l(b, 1.0L + a);
-    return re + im * I;
+    return 0.5L * log1pl(2.0L * a + (a * a + b * b)) + atan2l(b, 1.0L + a) * I;
 }
 
-/* principal-branch complex Li2 */
 static lcplx li2_cplx_ld(lcplx z)
 {
     const long double x = creall(z), y = cimagl(z);
-    if (x * x + y * y > 1.0L) {      /* Li2(z) = -pi^2/6 - ln^2(-z)/2 - Li2(1/z) */
+    if (x * x + y * y > 1.0L) {
         const lcplx l = clogl(-z);
         return -LZETA2 - 0.5L * l * l - li2_cplx_ld(1.0L / z);
     }
-    if (x > 0.5L)                    /* Li2(z) = pi^2/6 - ln z ln(1-z) - Li2(1-z) */
-        return LZETA2 - clogl(z) * clogl(1.0L - z) - li2_cplx_ld(1.0L - z);
+    if (x > 0.5L) return LZETA2 - clogl(z) * clogl(1.0L - z) - li2_cplx_ld(1.0L - z);
     if (x == 0.0L && y == 0.0L) return 0.0L;
     const lcplx u = -clog1pl(-z);
     const lcplx u2 = u * u;
@@ -81,16 +168,13 @@ static lcplx li2_cplx_ld(lcplx z)
     return sum;
 }
 
-double ora_dilog(double x) { return (double)li2_real_ld((long double)x); }
+double ora_dilog_ld(double x) { return (double)li2_real_ld((long double)x); }
 
-double ora_li2(double x) { return (double)li2_real_ld((long double)x); }
-
-void ora_complex_dilog_xy(double x, double y, double *re, double *im)
+void ora_complex_dilog_xy_ld(double x, double y, double *re, double *im)
 {
     if (y == 0.0) {
-        /* GSL: on the real axis the imaginary part is -pi*log(x) for x >= 1 */
-        *im = (x >= 1.0) ? -M_PI * log(x) : 0.0;
-        *re = ora_dilog(x);
+        *im = (x >= 1.0) ? (double)(-LPI * logl((long double)x)) : 0.0;
+        *re = ora_dilog_ld(x);
         return;
     }
     const lcplx r = li2_cplx_ld((long double)x + (long double)y * I);
@@ -98,12 +182,11 @@ void ora_complex_dilog_xy(double x, double y, double *re, double *im)
     *im = (double)cimagl(r);
 }
 
-/* Li3(x), real x in [-1, 1/2]. */
-double ora_li3(double xd)
+double ora_li3_ld(double xd)
 {
     const long double x = xd;
     if (x == 0.0L) return 0.0;
-    if (x >= -0.5L && x <= 0.5L) {   /* sum x^k / k^3 */
+    if (x >= -0.5L && x <= 0.5L) {
         long double sum = 0.0L, p = 1.0L;
         for (int k = 1; k < 400; ++k) {
             p *= x;
@@ -113,7 +196,7 @@ double ora_li3(double xd)
         }
         return (double)sum;
     }
-    if (x < -0.5L && x >= -1.0L) {   /* Li3(-e^w) = -sum_k eta(3-k) w^k/k!,  w = ln(-x) */
+    if (x < -0.5L && x >= -1.0L) {   /* Li3(-e^w) = -sum_k eta(3-k) w^k/k! */
         const long double w = logl(-x);
         long double sum = 0.0L, p = 1.0L;
         for (int k = 0; k < ORA_LI3_NE; ++k) {
@@ -124,5 +207,5 @@ double ora_li3(double xd)
         }
         return (double)(-sum);
     }
-    return NAN;  /* not reached by the reference's Lum_int (argument -exp(-y) in [-1,0)) */
+    return NAN;
 }

@@ -7,6 +7,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include "ora_spline.h"
+#include "ora_libm.h"
 
 #define SQ(a) ((a) * (a))
 
@@ -125,7 +126,7 @@ int ora_spline_eval(const ora_spline *s, const double *x0in, double *out)
 {
     const int D = s->ndim;
     double x0[ORA_SPL_MAXDIM];
-    for (int i = 0; i < D; ++i) x0[i] = s->islog[i] ? log(x0in[i]) : x0in[i];
+    for (int i = 0; i < D; ++i) x0[i] = s->islog[i] ? ora_log(x0in[i]) : x0in[i];   /* evaluated like the GPU */
     for (int i = 0; i < D; ++i)
         if (x0[i] <= s->x[i][0] || x0[i] >= s->x[i][s->n[i] - 1]) return -4;
     int k[ORA_SPL_MAXDIM];
