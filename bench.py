@@ -1,0 +1,177 @@
+#!/usr/bin/env python3
+"""bench.py -- full propagations/s of the MI355X nuSIprop solver (BASELINE.json metric).
+
+A step = one calculate_flux::evolve() (nuSIprop.hpp:176-337: Stage-A tables +
+cascade + finalisation) for every point of the rank's batch, on its GPU, with
+inputs and outputs resident in HBM.  Default workload = BASELINE config 4
+(1024-point (mphi, g) scan, N_E = 300, power-law source, every point building
+its own tables) per GPU; with N GPUs each rank evolves its own 1024 points
+(weak scaling, gamma shifted per rank so every rank's points are distinct), no
+collective on the data path.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c4|c5|c2] [--points P]
+Multi-GPU: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+
+Prints one JSON line (rank 0) with roofline (cascade kernel, HBM) and the
+cpu_baseline (the C oracle, single thread, bounded sample).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "full propagations/sec at N_E=300, 1 & 8 GPU; achieved HBM GB/s on cascade kernel"
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
+FP64_PEAK_TFLOPS = 78.6        # MI355X fp64 vector spec
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--workload", default="c4", choices=["c4", "c5", "c2"])
+    ap.add_argument("--points", type=int, default=0, help="points per GPU (default: 1024 for c4/c5, 1 for c2)")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0, help="budget of the oracle CPU baseline sample")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--traffic-json", default="", help="per-launch HBM bytes from a separate rocprofv3 --pmc pass")
+    return ap.parse_args()
+
+
+def rank_points(args, rank, world):
+    from nusiprop_amd import scan
+    if args.workload == "c2":
+        pts = [dict(scan.BASE, mphi=6e5, g=0.01, si=2.5, norm=6.0)]
+        return pts * max(1, args.points or 1), "C2b: single propagation, N_E=300, lE 12->17, power-law source, test.cpp physics"
+    P = args.points or 1024
+    if args.workload == "c4":
+        pts = scan.c4_points(si=2.5 + 0.05 * rank)
+        desc = "C4: (m_phi 32 x g 32) scan per GPU, N_E=300, lE 12->17, power-law source, gamma=2.5+0.05*rank"
+    else:
+        allp = scan.c5_points()
+        lo, hi = scan.shard(len(allp), world, rank)
+        pts = allp[lo:hi]
+        desc = "C5: rank slice of the 65536-point (m_phi, g, gamma) scan, N_E=300, power-law source"
+    while len(pts) < P:
+        pts = pts + pts
+    return pts[:P], desc
+
+
+def cpu_baseline(pts, budget_s):
+    """The C oracle (single thread) on the first points of the same workload until the budget is spent."""
+    from oracle import oracle
+    oracle.build()
+    n, t0 = 0, time.perf_counter()
+    for p in pts:
+        kw = dict(p)
+        kw["source"] = kw.pop("source_model")
+        o = oracle.Oracle(**kw)
+        o.evolve()
+        n += 1
+        if time.perf_counter() - t0 > budget_s:
+            break
+    dt = time.perf_counter() - t0
+    return {"value": n / dt, "unit": "propagations/s", "cores": 1, "kind": "port",
+            "sample": "%d full propagations (first points of the same workload), single-threaded C oracle, %.1f s" % (n, dt)}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(local)
+    import nusiprop_amd as nu
+    from nusiprop_amd import scan
+
+    pts, desc = rank_points(args, rank, world)
+    P = len(pts)
+    p0 = pts[0]
+    plan = nu.Plan(p0["N_bins_E"], p0["lEmin"], p0["lEmax"], p0["zmax"], max_points=P, device=local)
+    arr = plan.params_array(pts)
+    dev = torch.device("cuda", local)
+    flux = torch.empty((P, 3, plan.N), dtype=torch.float64, device=dev)
+    fla = torch.empty((P, 3, plan.N), dtype=torch.float64, device=dev)
+    stream = torch.cuda.current_stream().cuda_stream
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        plan.evolve_device(arr, flux.data_ptr(), fla.data_ptr(), stream)
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    plan.profile_begin(args.steps)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        plan.evolve_device(arr, flux.data_ptr(), fla.data_ptr(), stream)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    barrier()
+    dt = t1 - t0
+    if dist is not None:
+        tt = torch.tensor([dt], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+    sum_ms, ncalls = plan.profile_end()
+    bad = int(torch.isnan(fla).sum().item()) + int((fla < 0).sum().item())
+
+    N, Nz = plan.N, plan.Nz
+    props = world * P * args.steps
+    value = props / dt
+    casc_bytes = scan.cascade_bytes_per_point(N, Nz) * P
+    casc_s = sum_ms[2] / max(ncalls, 1) / 1e3
+    alpha_s = sum_ms[1] / max(ncalls, 1) / 1e3
+    traffic = None
+    if args.traffic_json and os.path.exists(args.traffic_json):
+        with open(args.traffic_json) as fh:
+            traffic = json.load(fh).get("k_cascade_bytes_per_launch")
+    achieved = casc_bytes / casc_s / 1e9
+    out = {
+        "metric": METRIC,
+        "value": value,
+        "unit": "propagations/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": dt / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (deterministic scan grid; power-law source)",
+        "config": {"workload": desc, "N_E": N, "N_z": Nz, "points_per_gpu": P, "lEmin": p0["lEmin"],
+                   "lEmax": p0["lEmax"], "parallelism": "independent points, %d GPU(s), no collective" % world},
+        "roofline": {"bound": "hbm", "kernel": "k_cascade", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "algorithmic_bytes_per_launch": casc_bytes, "avg_launch_ms": casc_s * 1e3},
+        "stage_ms_per_step": {"gamma_alphatilde": sum_ms[0] / max(ncalls, 1), "alpha": sum_ms[1] / max(ncalls, 1),
+                              "cascade": sum_ms[2] / max(ncalls, 1)},
+        "alpha_table": {"kernel": "k_alpha", "bound": "fp64 VALU (transcendental)",
+                        "entries_per_s": scan.alpha_entries_per_point(N, Nz) * P / alpha_s,
+                        "avg_launch_ms": alpha_s * 1e3},
+        "invalid_outputs": bad,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(pts, args.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -133,6 +133,12 @@ int nusi_plan_evolve_host(nusi_plan *plan, const nusi_params *pts, int n, double
 /* Kernel times (ms) of the last nusi_plan_evolve*: [0] Gamma/alphaTilde
  * tables, [1] alpha table, [2] cascade.  Synchronises the plan's stream. */
 int nusi_plan_stage_ms(nusi_plan *plan, float *ms3);
+/* Kernel-time accounting over many calls (bench): after profile_begin, each
+ * nusi_plan_evolve records HIP events around its three kernels on the launch
+ * stream (up to max_calls calls); profile_end synchronises and returns the
+ * summed ms per stage and the number of calls recorded. */
+int nusi_plan_profile_begin(nusi_plan *plan, int max_calls);
+int nusi_plan_profile_end(nusi_plan *plan, double *sum_ms3, int *ncalls);
 /* per-point NUSI_WARN_* bits of the last call */
 int nusi_plan_warnings(nusi_plan *plan, int *out, int n);
 /* Copy point `i`'s Stage-A tables of the last call to the host (parity

@@ -49,7 +49,8 @@ EXPORTS = [
     "nusi_check_energy_conservation", "nusi_get_flux", "nusi_get_flux_fla", "nusi_get_energies",
     "nusi_get_N_bins_E", "nusi_get_N_steps_z", "nusi_get_warnings",
     "nusi_plan_create", "nusi_plan_destroy", "nusi_plan_load_phiphi", "nusi_plan_grid", "nusi_plan_evolve",
-    "nusi_plan_evolve_host", "nusi_plan_stage_ms", "nusi_plan_warnings", "nusi_plan_tables", "nusi_evolve_batch",
+    "nusi_plan_evolve_host", "nusi_plan_stage_ms", "nusi_plan_profile_begin", "nusi_plan_profile_end",
+    "nusi_plan_warnings", "nusi_plan_tables", "nusi_evolve_batch",
 ]
 
 _lib = None
@@ -90,6 +91,8 @@ def load():
         "nusi_plan_evolve": (i, [vp, pp, i, vp, vp, vp]),
         "nusi_plan_evolve_host": (i, [vp, pp, i, dp, dp]),
         "nusi_plan_stage_ms": (i, [vp, ctypes.POINTER(ctypes.c_float)]),
+        "nusi_plan_profile_begin": (i, [vp, i]),
+        "nusi_plan_profile_end": (i, [vp, dp, ip]),
         "nusi_plan_warnings": (i, [vp, ip, i]),
         "nusi_plan_tables": (i, [vp, i, dp, dp, dp]),
         "nusi_evolve_batch": (i, [i, pp, i, dp, dp]),

@@ -358,6 +358,9 @@ struct nusi_plan {
     hipEvent_t ev_copy = nullptr;
     bool ran = false;
     int last_n = 0;
+    std::vector<hipEvent_t> prof_ev;   // 4 per recorded call
+    hipEvent_t* last_ev = nullptr;
+    int prof_max = 0, prof_n = 0;
     double U2[2][9];
     std::map<double, double> fs_cache;                      // si -> flux_FS_E0
     std::map<std::pair<double, int>, std::vector<double>> mass_cache;
@@ -464,6 +467,7 @@ void nusi_plan_destroy(nusi_plan* pl)
     for (auto& e : pl->ev)
         if (e) hipEventDestroy(e);
     if (pl->ev_copy) hipEventDestroy(pl->ev_copy);
+    for (auto& e : pl->prof_ev) hipEventDestroy(e);
     hipFree(pl->d_grid);
     hipFree(pl->d_pts);
     hipFree(pl->d_warn);
@@ -585,15 +589,51 @@ int nusi_plan_evolve(nusi_plan* pl, const nusi_params* pts, int n, double* d_flu
     HIPCHECK(hipEventRecord(pl->ev_copy, s));
     HIPCHECK(hipMemsetAsync(pl->d_warn, 0, sizeof(int) * n, s));
     const nusi::SplineSet spl = pl->spl ? pl->spl->set : nusi::SplineSet{};
-    HIPCHECK(hipEventRecord(pl->ev[0], s));
+    hipEvent_t* ev = pl->ev;
+    if (pl->prof_n < pl->prof_max) ev = &pl->prof_ev[4 * (size_t)pl->prof_n++];
+    HIPCHECK(hipEventRecord(ev[0], s));
     HIPCHECK(nusi::launch_gamma_alphat(pl->gd, pl->d_pts, n, spl, pl->tabs, pl->d_warn, s));
-    HIPCHECK(hipEventRecord(pl->ev[1], s));
+    HIPCHECK(hipEventRecord(ev[1], s));
     HIPCHECK(nusi::launch_alpha(pl->gd, pl->d_pts, n, spl, pl->tabs, pl->d_warn, s));
-    HIPCHECK(hipEventRecord(pl->ev[2], s));
+    HIPCHECK(hipEventRecord(ev[2], s));
     HIPCHECK(nusi::launch_cascade(pl->gd, pl->d_pts, n, pl->tabs, d_flux, d_fla, s));
-    HIPCHECK(hipEventRecord(pl->ev[3], s));
+    HIPCHECK(hipEventRecord(ev[3], s));
+    pl->last_ev = ev;   // stage_ms / warnings / tables refer to the latest call
     pl->ran = true;
     pl->last_n = n;
+    return NUSI_OK;
+}
+
+int nusi_plan_profile_begin(nusi_plan* pl, int max_calls)
+{
+    HIPCHECK(hipSetDevice(pl->device));
+    if (max_calls < 0) return fail(NUSI_EPARAM, "max_calls < 0");
+    if ((int)pl->prof_ev.size() < 4 * max_calls) {
+        const size_t old = pl->prof_ev.size();
+        pl->prof_ev.resize(4 * (size_t)max_calls, nullptr);
+        for (size_t k = old; k < pl->prof_ev.size(); ++k) HIPCHECK(hipEventCreate(&pl->prof_ev[k]));
+    }
+    pl->prof_max = max_calls;
+    pl->prof_n = 0;
+    return NUSI_OK;
+}
+
+int nusi_plan_profile_end(nusi_plan* pl, double* sum_ms3, int* ncalls)
+{
+    HIPCHECK(hipSetDevice(pl->device));
+    for (int k = 0; k < 3; ++k) sum_ms3[k] = 0.0;
+    for (int c = 0; c < pl->prof_n; ++c) {
+        hipEvent_t* e = &pl->prof_ev[4 * (size_t)c];
+        HIPCHECK(hipEventSynchronize(e[3]));
+        for (int k = 0; k < 3; ++k) {
+            float ms = 0.f;
+            HIPCHECK(hipEventElapsedTime(&ms, e[k], e[k + 1]));
+            sum_ms3[k] += ms;
+        }
+    }
+    *ncalls = pl->prof_n;
+    pl->prof_max = 0;
+    pl->prof_n = 0;
     return NUSI_OK;
 }
 
@@ -601,8 +641,8 @@ int nusi_plan_stage_ms(nusi_plan* pl, float* ms3)
 {
     if (!pl->ran) return fail(NUSI_ESTATE, "no evolve has run on this plan");
     HIPCHECK(hipSetDevice(pl->device));
-    HIPCHECK(hipEventSynchronize(pl->ev[3]));
-    for (int k = 0; k < 3; ++k) HIPCHECK(hipEventElapsedTime(&ms3[k], pl->ev[k], pl->ev[k + 1]));
+    HIPCHECK(hipEventSynchronize(pl->last_ev[3]));
+    for (int k = 0; k < 3; ++k) HIPCHECK(hipEventElapsedTime(&ms3[k], pl->last_ev[k], pl->last_ev[k + 1]));
     return NUSI_OK;
 }
 
@@ -611,7 +651,7 @@ int nusi_plan_warnings(nusi_plan* pl, int* out, int n)
     if (!pl->ran) return fail(NUSI_ESTATE, "no evolve has run on this plan");
     if (n > pl->last_n) n = pl->last_n;
     HIPCHECK(hipSetDevice(pl->device));
-    HIPCHECK(hipEventSynchronize(pl->ev[3]));
+    HIPCHECK(hipEventSynchronize(pl->last_ev[3]));
     HIPCHECK(hipMemcpy(out, pl->d_warn, sizeof(int) * n, hipMemcpyDeviceToHost));
     return NUSI_OK;
 }
@@ -621,7 +661,7 @@ int nusi_plan_tables(nusi_plan* pl, int i, double* G, double* At, double* A)
     if (!pl->ran) return fail(NUSI_ESTATE, "no evolve has run on this plan");
     if (i < 0 || i >= pl->last_n) return fail(NUSI_EPARAM, "point index out of range");
     HIPCHECK(hipSetDevice(pl->device));
-    HIPCHECK(hipEventSynchronize(pl->ev[3]));
+    HIPCHECK(hipEventSynchronize(pl->last_ev[3]));
     const size_t T = (size_t)pl->gd.T, PT = (size_t)pl->gd.PT;
     if (G) HIPCHECK(hipMemcpy(G, pl->tabs.G + T * i, sizeof(double) * T, hipMemcpyDeviceToHost));
     if (At) HIPCHECK(hipMemcpy(At, pl->tabs.At + T * i, sizeof(double) * T, hipMemcpyDeviceToHost));

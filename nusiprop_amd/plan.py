@@ -77,6 +77,16 @@ class Plan:
                                                 ctypes.c_void_p(d_fla_ptr),
                                                 ctypes.c_void_p(stream_ptr) if stream_ptr else None))
 
+    def profile_begin(self, max_calls):
+        _lib.check(_lib.load().nusi_plan_profile_begin(self._h, int(max_calls)))
+
+    def profile_end(self):
+        """Summed kernel ms [gamma/alphaTilde, alpha, cascade] and the number of calls recorded."""
+        ms = (ctypes.c_double * 3)()
+        n = ctypes.c_int()
+        _lib.check(_lib.load().nusi_plan_profile_end(self._h, ms, ctypes.byref(n)))
+        return list(ms), n.value
+
     def stage_ms(self):
         ms = (ctypes.c_float * 3)()
         _lib.check(_lib.load().nusi_plan_stage_ms(self._h, ms))

@@ -1,0 +1,46 @@
+"""Parameter-scan grids and their partition over GPUs.
+
+Scan points are independent propagations (one calculate_flux::evolve() each),
+so a multi-GPU scan is a pure partition: contiguous blocks of the flattened
+grid per rank, no collective on the data path; results are gathered on the
+host at the end.  Points that share (mphi, g, mntot, flags,
+grid) also share their Stage-A tables (nuSIprop.hpp:217-253 do not depend on
+si or norm), so the partition keeps such groups whole when it can.
+"""
+import numpy as np
+
+BASE = dict(mntot=0.1, norm=1.0, majorana=True, non_resonant=True, normal_ordering=True, flav=2, phiphi=False,
+            source_model=1, N_bins_E=300, lEmin=12.0, lEmax=17.0, zmax=5.0)
+
+
+def c4_points(si=2.5, n_mphi=32, n_g=32, **over):
+    """BASELINE config 4: mphi in logspace(5.5, 8, 32) x g in logspace(-3, 0, 32), gamma = 2.5, power law."""
+    base = dict(BASE, **over)
+    return [dict(base, mphi=float(m), g=float(g), si=float(si))
+            for m in np.logspace(5.5, 8.0, n_mphi) for g in np.logspace(-3.0, 0.0, n_g)]
+
+
+def c5_points(**over):
+    """BASELINE config 5: mphi (64) x g (64) x gamma in linspace(2, 3, 16) = 65 536 points, gamma fastest."""
+    base = dict(BASE, **over)
+    return [dict(base, mphi=float(m), g=float(g), si=float(s))
+            for m in np.logspace(5.5, 8.0, 64) for g in np.logspace(-3.0, 0.0, 64) for s in np.linspace(2.0, 3.0, 16)]
+
+
+def shard(n_points, world, rank):
+    """Contiguous block [lo, hi) of rank `rank` (sizes differ by at most one)."""
+    q, r = divmod(n_points, world)
+    lo = rank * q + min(rank, r)
+    return lo, lo + q + (1 if rank < r else 0)
+
+
+def cascade_bytes_per_point(N, Nz):
+    """Algorithmic HBM bytes of one propagation's cascade:
+    8 * [ (Nz-1) N(N-1)/2 alpha reads + 6 N (Nz-1) Gamma/alphaTilde/flux terms + Nz N ]."""
+    return 8 * ((Nz - 1) * N * (N - 1) // 2 + 6 * N * (Nz - 1) + Nz * N)
+
+
+def alpha_entries_per_point(N, Nz):
+    """Stage-A alpha entries per propagation, T(T-1)/2 with T = N + Nz - 2 (each summed over 3 mass states)."""
+    T = N + Nz - 2
+    return T * (T - 1) // 2
