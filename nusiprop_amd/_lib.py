@@ -8,7 +8,7 @@ import ctypes
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libnusi.so")
+LIB_PATH = os.environ.get("NUSIPROP_LIB") or os.path.join(HERE, "libnusi.so")   # override: A/B builds only
 
 NUSI_OK = 0
 NUSI_EPARAM = -1

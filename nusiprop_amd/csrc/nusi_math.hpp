@@ -26,6 +26,13 @@
 #include "nusi_libm.hpp"
 
 #define NUSI_FN __host__ __device__ inline
+// Polylogarithms are called from many sites; outlining them keeps the table
+// kernels' code small (NUSI_INLINE_POLYLOG inlines them everywhere, A/B builds).
+#ifdef NUSI_INLINE_POLYLOG
+#define NUSI_FN_OUT NUSI_FN
+#else
+#define NUSI_FN_OUT __host__ __device__ inline __attribute__((noinline))
+#endif
 
 namespace nusi {
 
@@ -86,7 +93,7 @@ NUSI_FN double li2_useries(double u)
 }
 
 // Re Li2(x) for real x (gsl_sf_dilog semantics)
-NUSI_FN double li2(double x)
+NUSI_FN_OUT double li2(double x)
 {
     double add = 0.0, sgn = 1.0;
     if (x > 1.0) {
@@ -111,7 +118,7 @@ NUSI_FN double li2(double x)
 }
 
 // principal-branch Li2(x+iy); y == 0 follows gsl_sf_complex_dilog_xy_e
-NUSI_FN cd cli2(double x, double y)
+NUSI_FN_OUT cd cli2(double x, double y)
 {
     if (y == 0.0) return cd{li2(x), (x >= 1.0) ? -kPi * nm::log(x) : 0.0};
     cd z = C(x, y), add = C(0.0);

@@ -15,6 +15,15 @@
 #include "nusi_math.hpp"
 #include "nusi_spline.hpp"
 
+// The three-mass loops (j/k = 0..2) are kept rolled by default: unrolled, the
+// alpha kernel is ~225 KB of code (instruction-cache thrashing) and 300+
+// VGPRs.  -DNUSI_MASS_UNROLLED restores full unrolling (A/B builds).
+#ifdef NUSI_MASS_UNROLLED
+#define NUSI_MASS_LOOP
+#else
+#define NUSI_MASS_LOOP _Pragma("unroll 1")
+#endif
+
 namespace nusi {
 
 // Per-parameter-point constants, built on the host (nusi_capi.cpp) from the
@@ -157,6 +166,7 @@ NUSI_FN double gamma_entry(const Point& P, double Em, double Ep, int& warn)
     const double g4 = (g * g) * (g * g), m2 = mphi * mphi;
     const double gr = Ga / mphi, gr2 = gr * gr;
     double tot = 0;
+    NUSI_MASS_LOOP
     for (int j = 0; j < 3; ++j) {
         const double mj = P.mn[j], uj = P.u[j];
         const double sp = 2 * mj * Ep / m2, sm = 2 * mj * Em / m2;
@@ -232,6 +242,7 @@ NUSI_FN double alphat_entry(const Point& P, const SplineSet& spl, double Em, dou
     const double gr = Ga / mphi, gr2 = gr * gr;
     const bool maj = P.majorana;
     double tot = 0;
+    NUSI_MASS_LOOP
     for (int k = 0; k < 3; ++k) {
         const double mk = P.mn[k], uk = P.u[k];
         double tp = -2 * mk * Ep / m2, tm = -2 * mk * Em / m2;
@@ -393,6 +404,7 @@ NUSI_FN double alpha_entry(const Point& P, const SplineSet& spl, double Em, doub
     const double gr = Ga / mphi, gr2 = gr * gr;
     const bool maj = P.majorana;
     double tot = 0;
+    NUSI_MASS_LOOP
     for (int k = 0; k < 3; ++k) {
         const double mk = P.mn[k], uk = P.u[k];
         double tp = -2 * mk * Ep / m2, tm = -2 * mk * Em / m2;

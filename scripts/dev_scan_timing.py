@@ -14,5 +14,6 @@ for rep in range(3):
     t = time.time(); flux, fla = plan.evolve(arr); dt = time.time() - t
     ms = plan.stage_ms()
     print("rep %d: wall %.3f s  props/s %.1f  stages ms gamma/aT %.2f alpha %.2f cascade %.2f" % (rep, dt, npts / dt, *ms), flush=True)
+import hashlib; print("flux sha1", hashlib.sha1(fla.tobytes()).hexdigest())
 w = plan.warnings(npts)
 print("warnings set on", sum(1 for x in w if x), "points; nan", int(np.isnan(fla).sum()))
