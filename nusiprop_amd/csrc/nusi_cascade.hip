@@ -1,0 +1,393 @@
+// nuSIprop MI355X -- Stage B: the implicit redshift cascade + finalisation
+// (calculate_flux::evolve, nuSIprop.hpp:255-336), one wavefront per point.
+//
+//   k_cascade_reg<NQ, D>  register-resident chain, N <= 64 NQ (default path)
+//   k_cascade             LDS-resident generic path (any N; NUSI_CASCADE_LDS=1)
+#include <hip/hip_runtime.h>
+
+#include <cstdlib>
+#include <utility>
+
+#include "nusi_internal.hpp"
+
+namespace nusi {
+// ---------------------------------------------------------------------------
+// Stage B -- the cascade.
+//
+// For each redshift step i (sequential, z_max -> 0) the bins are swept from
+// the top down; bin b needs the already-updated bins m > b of the same step
+// (nuSIprop.hpp:289-291), i.e. an upper-triangular solve.  It is done
+// right-looking: as soon as bin b is final, its weight
+//     T_b = s_i * sum_l u_l F_l[b] / dE_b
+// is pushed into every lower bin's accumulator acc[b'] += alpha(b', b) T_b
+// (one coalesced column read of the packed transposed table per bin), so the
+// sequential chain per bin is only the 3x3 solve.  Everything that does not
+// depend on the flux (Zdr, the LU of M, the source term) is precomputed for
+// 64 bins at a time, one bin per lane, into LDS.
+//
+// One wavefront (64 lanes) per point; F[3][N] and acc[N] live in LDS.
+// ---------------------------------------------------------------------------
+constexpr int kPreFields = 14;
+enum { PR_RZ0, PR_RZ1, PR_RZ2, PR_SRC, PR_L10, PR_L20, PR_L21, PR_U01, PR_U02, PR_U12, PR_RU00, PR_RU11, PR_RU22, PR_SDE };
+
+size_t cascade_lds_bytes(int N) { return sizeof(double) * (4 * (size_t)N + kPreFields * 64) + sizeof(int) * 64; }
+
+// gsl_linalg_LU_decomp on 3x3 (partial pivoting, Doolittle), nuSIprop.hpp:309
+NUSI_FN void lu3_factor(double A[3][3], int perm[3])
+{
+    perm[0] = 0; perm[1] = 1; perm[2] = 2;
+    for (int j = 0; j < 2; ++j) {
+        double amax = fabs(A[j][j]);
+        int ip = j;
+        for (int i = j + 1; i < 3; ++i)
+            if (fabs(A[i][j]) > amax) { amax = fabs(A[i][j]); ip = i; }
+        if (ip != j) {
+            for (int c = 0; c < 3; ++c) { const double t = A[j][c]; A[j][c] = A[ip][c]; A[ip][c] = t; }
+            const int t = perm[j]; perm[j] = perm[ip]; perm[ip] = t;
+        }
+        const double ajj = A[j][j];
+        if (ajj != 0.0)
+            for (int i = j + 1; i < 3; ++i) {
+                const double aij = A[i][j] / ajj;
+                A[i][j] = aij;
+                for (int c = j + 1; c < 3; ++c) A[i][c] = A[i][c] - aij * A[j][c];
+            }
+    }
+}
+
+__global__ __launch_bounds__(64) void k_cascade(GridDev g, const Point* __restrict__ pts, TablesDev t,
+                                                double* __restrict__ flux, double* __restrict__ flux_fla)
+{
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    const int N = g.N, Nz = g.Nz, T = g.T;
+    const int p = blockIdx.x, lane = threadIdx.x;
+    const Point& P = pts[p];
+    double* F0 = lds;
+    double* F1 = lds + N;
+    double* F2 = lds + 2 * N;
+    double* acc = lds + 3 * N;
+    double* pre = lds + 4 * N;
+    int* perm = (int*)(pre + kPreFields * 64);
+    const double u0 = P.u[0], u1 = P.u[1], u2 = P.u[2];
+    const double uk[3] = {u0, u1, u2};
+    const double* __restrict__ Gt = t.G + (size_t)p * T;
+    const double* __restrict__ At = t.At + (size_t)p * T;
+    const double* __restrict__ Al = t.A + (size_t)p * g.PT;
+    const bool nonres = P.non_resonant;
+
+    for (int b = lane; b < N; b += 64) F0[b] = F1[b] = F2[b] = 0.0;
+
+    for (int i = Nz - 1; i > 0; --i) {
+        const double c = g.step_c[i], s = g.step_s[i], zi = g.z[i], sfri = g.sfr[i];
+        for (int b = lane; b < N; b += 64) acc[b] = 0.0;
+        double next_acc = 0.0;     // acc of the next (lower) bin, carried in registers
+        double racc = 0.0;         // resonant-only running sum (nuSIprop.hpp:261-278)
+        double px0 = 0.0, px1 = 0.0, px2 = 0.0;   // F[:, b+1] of this step
+        for (int base = ((N - 1) / 64) * 64; base >= 0; base -= 64) {
+            __syncthreads();
+            {   // ---- parallel: flux-independent quantities for bins base..base+63
+                const int b = base + lane;
+                if (b < N) {
+                    const double dEb = g.Emax[b] - g.Emin[b];
+                    const double Gw = s * Gt[b + i - 1], Aw = s * At[b + i - 1];
+                    double Zd[3], M[3][3];
+                    for (int k = 0; k < 3; ++k) Zd[k] = 1.0 + c * (Gw * uk[k] - Aw * (uk[k] * uk[k])) / dEb;
+                    for (int k = 0; k < 3; ++k)
+                        for (int l = 0; l < 3; ++l) M[k][l] = (k == l) ? 1.0 : (Aw * uk[k] * uk[l] / dEb) / Zd[k];
+                    int pm[3];
+                    lu3_factor(M, pm);
+                    const double src0 = c * lum(P, zi, sfri, g.Emin[b], g.Emax[b]);
+                    pre[PR_RZ0 * 64 + lane] = 1.0 / Zd[0];
+                    pre[PR_RZ1 * 64 + lane] = 1.0 / Zd[1];
+                    pre[PR_RZ2 * 64 + lane] = 1.0 / Zd[2];
+                    pre[PR_SRC * 64 + lane] = src0;
+                    pre[PR_L10 * 64 + lane] = M[1][0];
+                    pre[PR_L20 * 64 + lane] = M[2][0];
+                    pre[PR_L21 * 64 + lane] = M[2][1];
+                    pre[PR_U01 * 64 + lane] = M[0][1];
+                    pre[PR_U02 * 64 + lane] = M[0][2];
+                    pre[PR_U12 * 64 + lane] = M[1][2];
+                    pre[PR_RU00 * 64 + lane] = 1.0 / M[0][0];
+                    pre[PR_RU11 * 64 + lane] = 1.0 / M[1][1];
+                    pre[PR_RU22 * 64 + lane] = 1.0 / M[2][2];
+                    pre[PR_SDE * 64 + lane] = nonres ? s / dEb : dEb;
+                    perm[lane] = pm[0] | (pm[1] << 2) | (pm[2] << 4);
+                }
+            }
+            __syncthreads();
+            const int top = (base + 63 < N - 1) ? base + 63 : N - 1;
+            for (int b = top; b >= base; --b) {
+                const int l = b - base;
+                const double accb_lds = (b > 0) ? acc[b - 1] : 0.0;   // for next_acc (before this bin's pushes)
+                double src0 = pre[PR_SRC * 64 + l];
+                double add;   // c * (coupling of this bin to the bins above)
+                if (nonres) {
+                    add = c * next_acc;
+                } else {
+                    if (b != N - 1) {
+                        const double Sres = u0 * px0 + u1 * px1 + u2 * px2;
+                        const size_t rd = (size_t)(b + i) * (b + i - 1) / 2 + (b + i - 1);   // alpha(b+i-1, b+i)
+                        racc += Sres * (s * Al[rd]) / (g.Emax[b + 1] - g.Emin[b + 1]) / pre[PR_SDE * 64 + l];
+                    }
+                    add = c * racc * pre[PR_SDE * 64 + l];
+                }
+                const double v0 = (F0[b] + (src0 + u0 * add)) * pre[PR_RZ0 * 64 + l];
+                const double v1 = (F1[b] + (src0 + u1 * add)) * pre[PR_RZ1 * 64 + l];
+                const double v2 = (F2[b] + (src0 + u2 * add)) * pre[PR_RZ2 * 64 + l];
+                const int pmv = perm[l];
+                const int p0 = pmv & 3, p1 = (pmv >> 2) & 3, p2 = (pmv >> 4) & 3;
+                double x0 = (p0 == 0) ? v0 : (p0 == 1) ? v1 : v2;
+                double x1 = (p1 == 0) ? v0 : (p1 == 1) ? v1 : v2;
+                double x2 = (p2 == 0) ? v0 : (p2 == 1) ? v1 : v2;
+                x1 = x1 - pre[PR_L10 * 64 + l] * x0;
+                x2 = x2 - pre[PR_L20 * 64 + l] * x0;
+                x2 = x2 - pre[PR_L21 * 64 + l] * x1;
+                x2 = x2 * pre[PR_RU22 * 64 + l];
+                x1 = (x1 - pre[PR_U12 * 64 + l] * x2) * pre[PR_RU11 * 64 + l];
+                x0 = (x0 - pre[PR_U01 * 64 + l] * x1 - pre[PR_U02 * 64 + l] * x2) * pre[PR_RU00 * 64 + l];
+                if (lane == 0) { F0[b] = x0; F1[b] = x1; F2[b] = x2; }
+                px0 = x0; px1 = x1; px2 = x2;
+                if (nonres && b > 0) {
+                    const double Tb = (u0 * x0 + u1 * x1 + u2 * x2) * pre[PR_SDE * 64 + l];
+                    const int r = b + i - 1;                       // table column of bin b
+                    const double* col = Al + (size_t)r * (r - 1) / 2 + (i - 1);
+                    next_acc = accb_lds + col[b - 1] * Tb;
+                    for (int bp = lane; bp < b - 1; bp += 64) acc[bp] += col[bp] * Tb;
+                }
+            }
+        }
+    }
+    __syncthreads();
+    // finalise (nuSIprop.hpp:328-336)
+    for (int b = lane; b < N; b += 64) {
+        const double dE = g.Emax[b] - g.Emin[b];
+        const double f0 = F0[b] / dE, f1 = F1[b] / dE, f2 = F2[b] / dE;
+        double* fo = flux + (size_t)p * 3 * N;
+        double* fl = flux_fla + (size_t)p * 3 * N;
+        fo[b] = f0;
+        fo[N + b] = f1;
+        fo[2 * N + b] = f2;
+        for (int f = 0; f < 3; ++f) fl[f * N + b] = P.U2[3 * f + 0] * f0 + P.U2[3 * f + 1] * f1 + P.U2[3 * f + 2] * f2;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Register-resident cascade (N <= 64 * 20 = 1280).
+//
+// Same arithmetic, in the same order, as k_cascade, but nothing on the
+// per-bin chain touches memory:
+//   * bin b is owned by lane b % 64, slot b / 64: F_k[b] and acc[b] live in
+//     registers (F[k][q], acc[q]); uniform reads of one bin are readlanes;
+//   * the per-bin precomputed fields of the current 64-bin chunk sit in the
+//     owning lane's registers and are broadcast with readlane;
+//   * the alpha column each bin pushes (alpha(b', b), b' < b) is prefetched D
+//     bins ahead into a register ring, so the HBM latency of the table stream
+//     is hidden behind D bins of the chain.
+// The chunk loop is fully unrolled (NQ is a template parameter) so every
+// register array is statically indexed.
+// ---------------------------------------------------------------------------
+
+__device__ __forceinline__ double rl(double v, int l)
+{
+    const long long x = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)x, l);
+    const int hi = __builtin_amdgcn_readlane((int)(x >> 32), l);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
+template <int NQ>
+__device__ __forceinline__ void load_col(double (&dst)[NQ], const double* __restrict__ Al, int bn, int i, int N,
+                                         int lane, int qmax)
+{
+    // alpha(b', bn) for b' = lane + 64 q < bn  (column r = bn + i - 1 of the packed transposed table).
+    // The loads are unconditional (addresses clamped into column r, bins clamped into [1, N-1]) so
+    // that no exec-masked branch breaks the compiler's vmcnt bookkeeping: a masked load would force
+    // a full vmcnt(0) drain every bin and defeat the prefetch.  Lanes past the column read a valid
+    // neighbour; every consumer masks by b' < b - 1 (or reads lane b - 1), so those values are unused.
+    const int bc = bn < 1 ? 1 : (bn > N - 1 ? N - 1 : bn);
+    const int r = bc + i - 1;
+    const double* col = Al + (size_t)r * (r - 1) / 2 + (i - 1);
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+        const int bp = lane + 64 * q;
+        if (q <= qmax) dst[q] = col[bp < bc ? bp : bc - 1];   // qmax is a compile-time constant after unrolling
+    }
+}
+
+template <int NQ, int D>
+__global__ __launch_bounds__(64) void k_cascade_reg(GridDev g, const Point* __restrict__ pts, TablesDev t,
+                                                    double* __restrict__ flux, double* __restrict__ flux_fla)
+{
+    extern __shared__ __attribute__((aligned(16))) double sdiag[];   // resonant-only: alpha(b+i-1, b+i)
+    const int N = g.N, Nz = g.Nz, T = g.T;
+    const int p = blockIdx.x, lane = threadIdx.x;
+    const Point& P = pts[p];
+    const double u0 = P.u[0], u1 = P.u[1], u2 = P.u[2];
+    const double uk[3] = {u0, u1, u2};
+    const double* __restrict__ Gt = t.G + (size_t)p * T;
+    const double* __restrict__ At = t.At + (size_t)p * T;
+    const double* __restrict__ Al = t.A + (size_t)p * g.PT;
+    const bool nonres = P.non_resonant;
+
+    double F0[NQ], F1[NQ], F2[NQ];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) F0[q] = F1[q] = F2[q] = 0.0;
+
+    for (int i = Nz - 1; i > 0; --i) {
+        const double c = g.step_c[i], s = g.step_s[i], zi = g.z[i], sfri = g.sfr[i];
+        if (!nonres) {
+            __syncthreads();
+            for (int b = lane; b < N - 1; b += 64) sdiag[b] = Al[(size_t)(b + i) * (b + i - 1) / 2 + (b + i - 1)];
+            __syncthreads();
+        }
+        double acc[NQ];
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) acc[q] = 0.0;
+        double ring[D][NQ];   // loaded unconditionally (also when only the resonant chain uses none of it)
+#pragma unroll
+        for (int j = 0; j < D; ++j) load_col<NQ>(ring[j], Al, 64 * NQ - 1 - j, i, N, lane, NQ - 1);
+        double next_acc = 0.0, racc = 0.0;
+        double px0 = 0.0, px1 = 0.0, px2 = 0.0;
+#pragma unroll
+        for (int qc = NQ - 1; qc >= 0; --qc) {
+            const int base = 64 * qc;
+            // ---- flux-independent fields of bin base + lane (one bin per lane)
+            double pr[kPreFields];
+            int pmv = 0;
+            {
+                const int b = base + lane;
+                if (b < N) {
+                    const double dEb = g.Emax[b] - g.Emin[b];
+                    const double Gw = s * Gt[b + i - 1], Aw = s * At[b + i - 1];
+                    double Zd[3], M[3][3];
+                    for (int k = 0; k < 3; ++k) Zd[k] = 1.0 + c * (Gw * uk[k] - Aw * (uk[k] * uk[k])) / dEb;
+                    for (int k = 0; k < 3; ++k)
+                        for (int l = 0; l < 3; ++l) M[k][l] = (k == l) ? 1.0 : (Aw * uk[k] * uk[l] / dEb) / Zd[k];
+                    int pm[3];
+                    lu3_factor(M, pm);
+                    pr[PR_RZ0] = 1.0 / Zd[0];
+                    pr[PR_RZ1] = 1.0 / Zd[1];
+                    pr[PR_RZ2] = 1.0 / Zd[2];
+                    pr[PR_SRC] = c * lum(P, zi, sfri, g.Emin[b], g.Emax[b]);
+                    pr[PR_L10] = M[1][0];
+                    pr[PR_L20] = M[2][0];
+                    pr[PR_L21] = M[2][1];
+                    pr[PR_U01] = M[0][1];
+                    pr[PR_U02] = M[0][2];
+                    pr[PR_U12] = M[1][2];
+                    pr[PR_RU00] = 1.0 / M[0][0];
+                    pr[PR_RU11] = 1.0 / M[1][1];
+                    pr[PR_RU22] = 1.0 / M[2][2];
+                    pr[PR_SDE] = nonres ? s / dEb : dEb;
+                    pmv = pm[0] | (pm[1] << 2) | (pm[2] << 4);
+                } else {
+#pragma unroll
+                    for (int f = 0; f < kPreFields; ++f) pr[f] = 0.0;
+                }
+            }
+            for (int gq = 0; gq < 64 / D; ++gq) {
+#pragma unroll
+                for (int j = 0; j < D; ++j) {
+                    const int l = 63 - (gq * D + j);
+                    const int b = base + l;
+                    if (b <= N - 1) {
+                        double add;
+                        if (nonres) {
+                            add = c * next_acc;
+                        } else {
+                            if (b != N - 1) {
+                                const double Sres = u0 * px0 + u1 * px1 + u2 * px2;
+                                racc += Sres * (s * sdiag[b]) / (g.Emax[b + 1] - g.Emin[b + 1]) / rl(pr[PR_SDE], l);
+                            }
+                            add = c * racc * rl(pr[PR_SDE], l);
+                        }
+                        const double src0 = rl(pr[PR_SRC], l);
+                        const double v0 = (rl(F0[qc], l) + (src0 + u0 * add)) * rl(pr[PR_RZ0], l);
+                        const double v1 = (rl(F1[qc], l) + (src0 + u1 * add)) * rl(pr[PR_RZ1], l);
+                        const double v2 = (rl(F2[qc], l) + (src0 + u2 * add)) * rl(pr[PR_RZ2], l);
+                        const int pmb = __builtin_amdgcn_readlane(pmv, l);
+                        const int p0 = pmb & 3, p1 = (pmb >> 2) & 3, p2 = (pmb >> 4) & 3;
+                        double x0 = (p0 == 0) ? v0 : (p0 == 1) ? v1 : v2;
+                        double x1 = (p1 == 0) ? v0 : (p1 == 1) ? v1 : v2;
+                        double x2 = (p2 == 0) ? v0 : (p2 == 1) ? v1 : v2;
+                        x1 = x1 - rl(pr[PR_L10], l) * x0;
+                        x2 = x2 - rl(pr[PR_L20], l) * x0;
+                        x2 = x2 - rl(pr[PR_L21], l) * x1;
+                        x2 = x2 * rl(pr[PR_RU22], l);
+                        x1 = (x1 - rl(pr[PR_U12], l) * x2) * rl(pr[PR_RU11], l);
+                        x0 = (x0 - rl(pr[PR_U01], l) * x1 - rl(pr[PR_U02], l) * x2) * rl(pr[PR_RU00], l);
+                        if (lane == l) { F0[qc] = x0; F1[qc] = x1; F2[qc] = x2; }
+                        px0 = x0; px1 = x1; px2 = x2;
+                        if (nonres && b > 0) {
+                            const double Tb = (u0 * x0 + u1 * x1 + u2 * x2) * rl(pr[PR_SDE], l);
+                            double accb, diag;
+                            if (l > 0) {
+                                accb = rl(acc[qc], l - 1);
+                                diag = rl(ring[j][qc], l - 1);
+                            } else {
+                                accb = rl(acc[qc > 0 ? qc - 1 : 0], 63);
+                                diag = rl(ring[j][qc > 0 ? qc - 1 : 0], 63);
+                            }
+                            next_acc = accb + diag * Tb;
+#pragma unroll
+                            for (int q = 0; q <= qc; ++q)
+                                if (lane + 64 * q < b - 1) acc[q] += ring[j][q] * Tb;
+                        }
+                    }
+                    load_col<NQ>(ring[j], Al, b - D, i, N, lane, qc);
+                }
+            }
+        }
+    }
+    // finalise (nuSIprop.hpp:328-336)
+    double* fo = flux + (size_t)p * 3 * N;
+    double* fl = flux_fla + (size_t)p * 3 * N;
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+        const int b = lane + 64 * q;
+        if (b < N) {
+            const double dE = g.Emax[b] - g.Emin[b];
+            const double f0 = F0[q] / dE, f1 = F1[q] / dE, f2 = F2[q] / dE;
+            fo[b] = f0;
+            fo[N + b] = f1;
+            fo[2 * N + b] = f2;
+            for (int f = 0; f < 3; ++f)
+                fl[f * N + b] = P.U2[3 * f + 0] * f0 + P.U2[3 * f + 1] * f1 + P.U2[3 * f + 2] * f2;
+        }
+    }
+}
+
+template <int NQ>
+static void launch_reg(const GridDev& g, const Point* pts, int npts, TablesDev t, double* flux, double* flux_fla,
+                       hipStream_t s)
+{
+    constexpr int D = NQ <= 5 ? 8 : (NQ <= 10 ? 4 : 2);
+    hipLaunchKernelGGL((k_cascade_reg<NQ, D>), dim3(npts), dim3(64), sizeof(double) * (size_t)g.N, s, g, pts, t, flux,
+                       flux_fla);
+}
+
+// instantiated chunk counts; a kernel built for NQ serves every N <= 64 NQ
+template <int... Q>
+static bool dispatch_reg(int nq, const GridDev& g, const Point* pts, int npts, TablesDev t, double* flux,
+                         double* flux_fla, hipStream_t s, std::integer_sequence<int, Q...>)
+{
+    bool done = false;
+    ((!done && nq <= Q ? (launch_reg<Q>(g, pts, npts, t, flux, flux_fla, s), done = true) : false), ...);
+    return done;
+}
+using RegNQ = std::integer_sequence<int, 1, 2, 3, 4, 5, 6, 8, 10, 12, 16, 20>;
+
+hipError_t launch_cascade(const GridDev& g, const Point* pts, int npts, TablesDev t, double* flux, double* flux_fla,
+                          hipStream_t s)
+{
+    const int nq = (g.N + 63) / 64;
+    static const bool force_lds = getenv("NUSI_CASCADE_LDS") != nullptr;   // A/B switch
+    if (!force_lds &&
+        dispatch_reg(nq, g, pts, npts, t, flux, flux_fla, s, RegNQ{}))
+        return hipGetLastError();
+    const size_t lds = cascade_lds_bytes(g.N);
+    hipLaunchKernelGGL(k_cascade, dim3(npts), dim3(64), lds, s, g, pts, t, flux, flux_fla);
+    return hipGetLastError();
+}
+
+}  // namespace nusi

@@ -115,3 +115,20 @@ def test_scan_subset_vs_oracle(nusi, oracle_mod):
         f_ref, fla_ref = o.cascade(G, aT, al)
         assert cases.rel_err(flux[k], f_ref) <= FLUX_RTOL
         assert cases.rel_err(fla[k], fla_ref) <= FLUX_RTOL
+
+
+@pytest.mark.parametrize("N,nonres", [(37, True), (64, True), (65, False), (130, True), (200, False), (700, True),
+                                      (1200, True)])
+def test_cascade_sizes(nusi, oracle_mod, N, nonres):
+    """The register-resident cascade at every chunk-count regime (N <= 64 NQ for the
+    instantiated NQ; 64/65 straddle a chunk edge, 1200 is BASELINE config 3's size):
+    the GPU flux against the oracle's cascade run on the GPU's own tables (which are
+    bit-exact to the oracle's at the sizes the other tests cover)."""
+    kw = dict(cases.C2B_100, N_bins_E=N, non_resonant=nonres, majorana=(N % 2 == 0))
+    plan, flux, fla, tabs, _ = _gpu(nusi, [kw])
+    o = oracle_mod.Oracle(**cases.oracle_kwargs(kw))
+    o.prepare()
+    G, aT, A = tabs[0]
+    f_ref, fla_ref = o.cascade(G, aT, nusi.unpack_alpha(A, plan.T))
+    assert cases.rel_err(flux[0], f_ref) <= FLUX_RTOL
+    assert cases.rel_err(fla[0], fla_ref) <= FLUX_RTOL

@@ -1,0 +1,65 @@
+"""Stage-A table formulas of the product (nusiprop_amd/csrc/nusi_physics.hpp,
+compiled for the host by tests/hostcheck) against the oracle, BIT FOR BIT, on
+CPU.  The GPU runs the same source (tests/test_gpu_parity.py checks the device
+build); this catches a formula divergence without a GPU.
+
+The per-point scalars (masses, |U|^2, width, norm_total) are taken from the
+oracle, which is what the product's host code computes the same way
+(nusi_capi.cpp build_point; nuSIprop.hpp:130-205)."""
+import ctypes
+
+import numpy as np
+import pytest
+
+from tests import cases
+
+DP = ctypes.POINTER(ctypes.c_double)
+
+
+def _dp(a):
+    return a.ctypes.data_as(DP)
+
+
+def extended_axis(o):
+    """Stage-A energy axis (nuSIprop.hpp:217-252): the N bins, then the top bin
+    redshifted by (1+z_j), j = 1..N_z-2."""
+    Emin, Emax, _, z = o.grid()
+    N, T = o.N, o.T
+    lo, hi = np.empty(T), np.empty(T)
+    lo[:N], hi[:N] = Emin, Emax
+    for n in range(N, T):
+        lo[n] = Emin[N - 1] * (1 + z[n - N + 1])
+        hi[n] = Emax[N - 1] * (1 + z[n - N + 1])
+    return lo, hi
+
+
+def point_array(o, kw):
+    mn, norm_total = o.prepare()
+    U2 = o.mixing()
+    g, mphi = kw["g"], kw["mphi"]
+    Ga = g * g * mphi / (16.0 * np.pi) if kw["majorana"] else g * g * mphi / (8.0 * np.pi)
+    u = U2[kw["flav"]]
+    pt = np.array([mphi, g, kw["mntot"], kw["si"], kw["norm"], norm_total, Ga, *mn, *u], dtype=np.float64)
+    flags = (ctypes.c_int * 4)(int(kw["majorana"]), int(kw["non_resonant"]), int(kw["phiphi"]),
+                               int(kw.get("source_model", 0)))
+    return pt, flags
+
+
+@pytest.mark.parametrize("name", sorted(cases.SMALL_CASES))
+def test_tables_bit_identical(oracle_mod, name):
+    from tests.hostcheck import build_hostcheck
+    H = build_hostcheck()
+    kw = dict(cases.SMALL_CASES[name], N_bins_E=40)
+    o = oracle_mod.Oracle(**cases.oracle_kwargs(kw))
+    G, aT, al = o.tables()
+    lo, hi = extended_axis(o)
+    pt, flags = point_array(o, kw)
+    T = o.T
+    Gh, aTh, Ah = np.zeros(T), np.zeros(T), np.zeros((T, T))
+    H.hc_tables.restype = ctypes.c_int
+    w = H.hc_tables(_dp(pt), flags, T, _dp(lo), _dp(hi), _dp(Gh), _dp(aTh), _dp(Ah))
+    assert np.array_equal(Gh, G)
+    assert np.array_equal(aTh, aT)
+    iu = np.triu_indices(T, 1)
+    assert np.array_equal(Ah[iu], al[iu]), "%d alpha entries differ" % np.sum(Ah[iu] != al[iu])
+    assert (w & 7) == o.warnings()
