@@ -352,6 +352,7 @@ struct nusi_plan {
     nusi::Point* h_pts = nullptr;  // pinned
     int* d_warn = nullptr;
     nusi::TablesDev tabs{};
+    nusi::AlphaTilesDev atiles{};
     double* d_scratch = nullptr;   // flux outputs when the caller passes NULL
     std::shared_ptr<SplineStore> spl;
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
@@ -474,6 +475,7 @@ void nusi_plan_destroy(nusi_plan* pl)
     hipFree(pl->tabs.G);
     hipFree(pl->tabs.At);
     hipFree(pl->tabs.A);
+    nusi::alpha_tiles_destroy(&pl->atiles);
     hipFree(pl->d_scratch);
     if (pl->h_pts) hipHostFree(pl->h_pts);
     if (pl->stream) hipStreamDestroy(pl->stream);
@@ -543,6 +545,9 @@ int nusi_plan_create(int device, int N_bins_E, double lEmin, double lEmax, doubl
     HIPCHECK(hipMalloc(&pl->tabs.G, sizeof(double) * (size_t)G.T * max_points));
     HIPCHECK(hipMalloc(&pl->tabs.At, sizeof(double) * (size_t)G.T * max_points));
     HIPCHECK(hipMalloc(&pl->tabs.A, sizeof(double) * (size_t)gd.PT * max_points));
+    std::vector<unsigned char> shared(G.T, 0);   // bin edges shared bitwise with the next bin
+    for (int n = 0; n + 1 < G.T; ++n) shared[n] = (G.hi[n] == G.lo[n + 1]);
+    HIPCHECK(nusi::alpha_tiles_create(G.T, shared.data(), &pl->atiles));
     *out = pl.release();
     return NUSI_OK;
 }
@@ -594,7 +599,7 @@ int nusi_plan_evolve(nusi_plan* pl, const nusi_params* pts, int n, double* d_flu
     HIPCHECK(hipEventRecord(ev[0], s));
     HIPCHECK(nusi::launch_gamma_alphat(pl->gd, pl->d_pts, n, spl, pl->tabs, pl->d_warn, s));
     HIPCHECK(hipEventRecord(ev[1], s));
-    HIPCHECK(nusi::launch_alpha(pl->gd, pl->d_pts, n, spl, pl->tabs, pl->d_warn, s));
+    HIPCHECK(nusi::launch_alpha(pl->gd, pl->d_pts, n, spl, pl->atiles, pl->tabs, pl->d_warn, s));
     HIPCHECK(hipEventRecord(ev[2], s));
     HIPCHECK(nusi::launch_cascade(pl->gd, pl->d_pts, n, pl->tabs, d_flux, d_fla, s));
     HIPCHECK(hipEventRecord(ev[3], s));

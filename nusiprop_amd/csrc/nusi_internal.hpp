@@ -31,10 +31,23 @@ struct TablesDev {
     double* A;    // [npts][PT]
 };
 
+// Tiles of the alpha table for k_alpha_tile: kAlphaTile x kAlphaTile (n, m) bin blocks with
+// tn <= tm, in three launch classes by how many distinct bin edges a side has
+// (bins of the first N share edges, redshift-extended bins do not), which sets
+// each class's LDS footprint.  tiles[] packs tn | tm << 16.
+struct AlphaTilesDev {
+    int* tiles = nullptr;   // device [ncore + nmixed + nfull]
+    int ncls[3] = {0, 0, 0};
+    int cs_max[3] = {0, 0, 0}, ct_max[3] = {0, 0, 0};
+};
+// Classify the tiles of a grid on the host; `shared[n]` = (hi[n] == lo[n+1]) bitwise.
+hipError_t alpha_tiles_create(int T, const unsigned char* shared, AlphaTilesDev* out);
+void alpha_tiles_destroy(AlphaTilesDev* t);
+
 hipError_t launch_gamma_alphat(const GridDev& g, const Point* pts, int npts, const SplineSet& spl, TablesDev t,
                                int* warn, hipStream_t s);
-hipError_t launch_alpha(const GridDev& g, const Point* pts, int npts, const SplineSet& spl, TablesDev t, int* warn,
-                        hipStream_t s);
+hipError_t launch_alpha(const GridDev& g, const Point* pts, int npts, const SplineSet& spl, const AlphaTilesDev& tiles,
+                        TablesDev t, int* warn, hipStream_t s);
 hipError_t launch_cascade(const GridDev& g, const Point* pts, int npts, TablesDev t, double* flux, double* flux_fla,
                           hipStream_t s);
 

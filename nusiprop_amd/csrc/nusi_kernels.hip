@@ -6,6 +6,9 @@
 //   (Stage B, the cascade, is in nusi_cascade.hip)
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+#include <vector>
+
 #include "nusi_internal.hpp"
 
 namespace nusi {
@@ -56,11 +59,125 @@ hipError_t launch_gamma_alphat(const GridDev& g, const Point* pts, int npts, con
     return hipGetLastError();
 }
 
-hipError_t launch_alpha(const GridDev& g, const Point* pts, int npts, const SplineSet& spl, TablesDev t, int* warn,
-                        hipStream_t s)
+// ---------------------------------------------------------------------------
+// k_alpha_tile: one workgroup per (kAlphaTile x kAlphaTile bin tile, point).
+//
+//   1. the distinct bin edges of the tile's n side (t) and m side (S');
+//   2. edge and m-bin leaves of all three mass states -> LDS (one round);
+//   3. per mass state k: every (S', t) corner leaf -> LDS (one corner per
+//      work-item: a core tile has 16 x 16 = 256 corners), then every entry of
+//      the tile combines its four corners, four edges and its m bin
+//      (alpha_k<TileLeaves>), accumulating the k sum in a register.
+// A core tile evaluates 256 corners for its 225 entries where the per-entry
+// path evaluates 4 per entry: the dilogarithms, complex dilogarithms and
+// mixed logarithms that dominate the table cost are ~3.5x fewer.
+// ---------------------------------------------------------------------------
+constexpr int kTileThreads = 256;
+static_assert(kAlphaTile * kAlphaTile <= kTileThreads, "one entry per work-item");
+
+__host__ __device__ constexpr int alpha_tile_lds_doubles(int cs, int ct)
 {
-    dim3 grid((unsigned)((g.PT + 255) / 256), npts);
-    hipLaunchKernelGGL(k_alpha, grid, dim3(256), 0, s, g, pts, spl, t.A, warn);
+    return kCornerFields * cs * ct + 3 * (kTEdgeFields * ct + kSEdgeFields * cs + kMBinFields * kAlphaTile);   // = 3 alpha_tile_edge_stride
+}
+
+__global__ __launch_bounds__(kTileThreads) void k_alpha_tile(GridDev g, const Point* __restrict__ pts, SplineSet spl,
+                                                           const int* __restrict__ tiles, int cs_max, int ct_max,
+                                                           double* __restrict__ A, int* __restrict__ warn)
+{
+    extern __shared__ __attribute__((aligned(16))) double sm[];
+    __shared__ double tE[2 * kAlphaTile], sE[2 * kAlphaTile];
+    __shared__ int tl[kAlphaTile], th[kAlphaTile], sl[kAlphaTile], sh[kAlphaTile];
+    __shared__ int cnt[2];
+    const int p = blockIdx.y, tid = threadIdx.x, T = g.T;
+    const int tw = tiles[blockIdx.x];
+    const int n0 = (tw & 0xffff) * kAlphaTile, m0 = (tw >> 16) * kAlphaTile;
+    const Point& P = pts[p];
+    if (tid == 0) cnt[0] = alpha_edge_list(g.lo, g.hi, n0, T, tE, tl, th);
+    if (tid == 64) cnt[1] = alpha_edge_list(g.lo, g.hi, m0, T, sE, sl, sh);
+    __syncthreads();
+    const int ct = cnt[0], cs = cnt[1], cc = cs * ct;
+    const int ln = tid % kAlphaTile, lm = tid / kAlphaTile;
+    const int n = n0 + ln, m = m0 + lm;
+    const bool valid = tid < kAlphaTile * kAlphaTile && n < m && m < T;
+    if (cs > cs_max || ct > ct_max) {   // host classification guarantees this never happens
+        if (valid) A[(size_t)p * g.PT + (size_t)m * (m - 1) / 2 + n] = __builtin_nan("");
+        return;
+    }
+    const bool nonres = P.non_resonant, maj = P.majorana;
+    const bool needed = valid && (nonres || m == n + 1);
+    double* cor = sm;
+    double* edg = sm + kCornerFields * cc;
+    // ---- 2. edge and m-bin leaves, all k: 3 (ct + cs + kAlphaTile) <= 225 jobs, one round
+    if (tid < 3 * (ct + cs + kAlphaTile)) alpha_tile_edge_job(P, tid, tE, ct, sE, cs, g.lo, g.hi, m0, T, edg);
+    double tot = 0;
+    int w = 0;
+    for (int k = 0; k < 3; ++k) {
+        __syncthreads();   // edge leaves written / previous k's corners consumed
+        if (nonres && maj)
+            for (int j = tid; j < cc; j += kTileThreads) alpha_tile_corner_job(P, k, j, tE, ct, sE, cc, cor);
+        __syncthreads();
+        if (needed) {
+            const TileLeaves lv = alpha_tile_leaves(cor, edg, k, cs, ct, lm, sl, sh, tl, th, ln);
+            alpha_k(P, spl, k, g.lo[n], g.hi[n], g.lo[m], g.hi[m], lv, tot, w);
+        }
+    }
+    if (valid) A[(size_t)p * g.PT + (size_t)m * (m - 1) / 2 + n] = needed ? tot : 0.0;
+    if (w) atomicOr(&warn[p], w);
+}
+
+hipError_t alpha_tiles_create(int T, const unsigned char* shared, AlphaTilesDev* out)
+{
+    const int nt = (T + kAlphaTile - 1) / kAlphaTile;
+    // distinct edges of each tile side, exactly as alpha_edge_list counts them on the device
+    std::vector<int> ne(nt, 0);
+    for (int t = 0; t < nt; ++t)
+        for (int j = t * kAlphaTile; j < (t + 1) * kAlphaTile && j < T; ++j)
+            ne[t] += (j > t * kAlphaTile && shared[j - 1]) ? 1 : 2;
+    // class 0: both sides <= 16 edges; 1: t side <= 16, S' side <= 30; 2: both <= 30
+    const int cap_core = kAlphaTile + 1, cap_ext = 2 * kAlphaTile;
+    std::vector<int> cls[3];
+    for (int tm = 0; tm < nt; ++tm)
+        for (int tn = 0; tn <= tm; ++tn) {
+            const int c = (ne[tn] <= cap_core && ne[tm] <= cap_core) ? 0 : (ne[tn] <= cap_core) ? 1 : 2;
+            cls[c].push_back(tn | (tm << 16));
+        }
+    const int csm[3] = {cap_core, cap_ext, cap_ext}, ctm[3] = {cap_core, cap_core, cap_ext};
+    std::vector<int> all;
+    for (int c = 0; c < 3; ++c) {
+        out->ncls[c] = (int)cls[c].size();
+        out->cs_max[c] = csm[c];
+        out->ct_max[c] = ctm[c];
+        all.insert(all.end(), cls[c].begin(), cls[c].end());
+    }
+    hipError_t e = hipMalloc(&out->tiles, sizeof(int) * all.size());
+    if (e != hipSuccess) return e;
+    return hipMemcpy(out->tiles, all.data(), sizeof(int) * all.size(), hipMemcpyHostToDevice);
+}
+
+void alpha_tiles_destroy(AlphaTilesDev* t)
+{
+    if (t->tiles) (void)hipFree(t->tiles);
+    t->tiles = nullptr;
+}
+
+hipError_t launch_alpha(const GridDev& g, const Point* pts, int npts, const SplineSet& spl, const AlphaTilesDev& at,
+                        TablesDev t, int* warn, hipStream_t s)
+{
+    static const bool per_entry = getenv("NUSI_ALPHA_PER_ENTRY") != nullptr;   // A/B switch
+    if (per_entry) {
+        dim3 grid((unsigned)((g.PT + 255) / 256), npts);
+        hipLaunchKernelGGL(k_alpha, grid, dim3(256), 0, s, g, pts, spl, t.A, warn);
+        return hipGetLastError();
+    }
+    int off = 0;
+    for (int c = 0; c < 3; ++c) {
+        if (at.ncls[c] == 0) continue;
+        const int cs = at.cs_max[c], ct = at.ct_max[c];
+        const size_t lds = sizeof(double) * (size_t)alpha_tile_lds_doubles(cs, ct);
+        hipLaunchKernelGGL(k_alpha_tile, dim3(at.ncls[c], npts), dim3(kTileThreads), lds, s, g, pts, spl,
+                           at.tiles + off, cs, ct, t.A, warn);
+        off += at.ncls[c];
+    }
     return hipGetLastError();
 }
 

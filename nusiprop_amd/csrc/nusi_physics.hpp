@@ -396,184 +396,374 @@ NUSI_FN double alphat_entry(const Point& P, const SplineSet& spl, double Em, dou
 
 // ---------------------------------------------------------------------------
 // alpha(Em, Ep, Em', Ep')  -- nuSIprop.hpp:1237-1520
+//
+// The entry for bins n (t edges tm, tp) and m (S' edges Sm, Sp) is a fixed
+// combination of transcendental "leaves" that depend on ONE edge or on ONE
+// (S' edge, t edge) corner only.  Neighbouring bins share edges, so the tile
+// kernel (k_alpha_tile) evaluates each leaf once per edge / corner and the
+// entries of a tile combine them; the per-entry path evaluates them inline.
+// Both go through alpha_k<Leaves>() -- one expression text -- and the leaves
+// are pure functions of the same fp64 arguments, so the two paths (and the
+// oracle, which computes them inline in the reference's order) agree bit for
+// bit.
 // ---------------------------------------------------------------------------
-NUSI_FN double alpha_entry(const Point& P, const SplineSet& spl, double Em, double Ep, double Emp, double Epp, int& warn)
+NUSI_FN double alpha_t(double mk, double E, double m2)   // :1262-1266, incl. the |t+1| < 1e-7 nudge
+{
+    double t = -2 * mk * E / m2;
+    if (fabs(t + 1) < 1e-7) t += t * 1e-6;
+    return t;
+}
+NUSI_FN double alpha_S(double mk, double E, double m2) { return 2 * mk * E / m2; }   // :1263-1264
+
+// corner (S', t) leaves
+struct AlphaCorner {
+    double L;          // log1p(S + t)
+    double LL;         // log(1 + S + t)
+    double TU1, TU2;   // t < -1: li2((1+S+t)/S), 0 ; else li2(S/(1+S+t)), log((1+S+t)/S)   (:1375-1398)
+    double G;          // li2((1+S+t)/(2+S))
+    double Drr, Dri;   // cli2((1+S+t)/(1+t) + 0i)                                          (:1444-1451)
+    double Dcr, Dci;   // cli2((1+S+t)/(2 - i gr + t))
+    double A;          // arg(-(-1 + i gr + S)/(2 - i gr + t))
+};
+NUSI_FN void alpha_corner(double S, double t, double gr, AlphaCorner& c)
+{
+    c.L = nm::log1p(S + t);
+    c.LL = nm::log(1 + S + t);
+    if (t < -1) {
+        c.TU1 = li2((1 + S + t) / S);
+        c.TU2 = 0.0;
+    } else {
+        c.TU1 = li2(S / (1 + S + t));
+        c.TU2 = nm::log((1 + S + t) / S);
+    }
+    c.G = li2((1 + S + t) / (2 + S));
+    const cd Dr = cli2((1 + S + t) / (1 + t), 0.0);
+    const cd dt = C(2 + t, -gr);
+    const cd Dc = cli2((1 + S + t) / dt);
+    c.Drr = Dr.r;
+    c.Dri = Dr.i;
+    c.Dcr = Dc.r;
+    c.Dci = Dc.i;
+    c.A = carg(-(C(-1 + S, gr) / dt));
+}
+// t-edge leaves
+struct AlphaTEdge { double Lm1, la, cm, L2, am; };
+NUSI_FN void alpha_tedge(double t, double gr2, AlphaTEdge& e)
+{
+    e.Lm1 = nm::log1p(-t);
+    e.la = (t > -1) ? nm::log1p(t) : nm::log(-1 - t);
+    e.cm = carg_real(-(1 / (1 + t)));
+    e.L2 = nm::log1p(((2 + t) * (2 + t)) / gr2);
+    e.am = nm::log(fabs(1 + t));
+}
+// S'-edge leaves
+struct AlphaSEdge { double lS, l2, Ls, cS, lS2; };
+NUSI_FN void alpha_sedge(double S, double gr, double gr2, AlphaSEdge& e)
+{
+    e.lS = nm::log(S);
+    e.l2 = nm::log((2 + S) / S);
+    e.Ls = nm::log1p(((-1 + S) * (-1 + S)) / gr2);
+    e.cS = carg(C(-1 + S, gr));
+    e.lS2 = nm::log(S / (2 + S));
+}
+// m-bin leaves
+struct AlphaMBin { double lr, lr2, atd; };
+NUSI_FN void alpha_mbin(double Sm, double Sp, double mphi, double Ga, AlphaMBin& b)
+{
+    b.lr = nm::log(Sm / Sp);
+    b.lr2 = nm::log(Sp / Sm);
+    b.atd = (Sp < 1e-5) ? 0.0 : atandiff(mphi * (Sp - 1) / Ga, mphi * (Sm - 1) / Ga);
+}
+
+// leaves evaluated on the spot (per-entry path, host checks)
+struct DirectLeaves {
+    double gr, gr2, mphi, Ga;
+    NUSI_FN AlphaCorner corner(int, int, double S, double t) const { AlphaCorner c; alpha_corner(S, t, gr, c); return c; }
+    NUSI_FN AlphaTEdge tedge(int, double t) const { AlphaTEdge e; alpha_tedge(t, gr2, e); return e; }
+    NUSI_FN AlphaSEdge sedge(int, double S) const { AlphaSEdge e; alpha_sedge(S, gr, gr2, e); return e; }
+    NUSI_FN AlphaMBin mbin(double Sm, double Sp) const { AlphaMBin b; alpha_mbin(Sm, Sp, mphi, Ga, b); return b; }
+};
+
+// leaves read from a tile's precomputed arrays (structure of arrays):
+//   cor[v * cc + s * ct + t]  (v = field of AlphaCorner, cc = cs * ct), ted[v * ct + t],
+//   sed[v * cs + s], mbv[v * kAlphaTile + j]
+constexpr int kAlphaTile = 15;
+struct TileLeaves {
+    const double *cor, *ted, *sed, *mbv;
+    int cc, ct, cs, mb;
+    int sidx[2], tidx[2];   // slots of (Sm, Sp) and (tm, tp)
+    NUSI_FN AlphaCorner corner(int si, int ti, double, double) const
+    {
+        const double* c = cor + sidx[si] * ct + tidx[ti];
+        return AlphaCorner{c[0], c[cc], c[2 * cc], c[3 * cc], c[4 * cc], c[5 * cc], c[6 * cc], c[7 * cc], c[8 * cc], c[9 * cc]};
+    }
+    NUSI_FN AlphaTEdge tedge(int ti, double) const
+    {
+        const double* e = ted + tidx[ti];
+        return AlphaTEdge{e[0], e[ct], e[2 * ct], e[3 * ct], e[4 * ct]};
+    }
+    NUSI_FN AlphaSEdge sedge(int si, double) const
+    {
+        const double* e = sed + sidx[si];
+        return AlphaSEdge{e[0], e[cs], e[2 * cs], e[3 * cs], e[4 * cs]};
+    }
+    NUSI_FN AlphaMBin mbin(double, double) const
+    {
+        return AlphaMBin{mbv[mb], mbv[kAlphaTile + mb], mbv[2 * kAlphaTile + mb]};
+    }
+};
+constexpr int kCornerFields = 10, kTEdgeFields = 5, kSEdgeFields = 5, kMBinFields = 3;
+
+// Unique edge energies of bins b0 .. b0+kAlphaTile-1 (< T): E[0..count), il/ih = slot of each bin's
+// lower/upper edge.  Bins of the first N share edges bitwise (Emax[n] == Emin[n+1], same pow()
+// argument); the redshift-extended bins do not (nuSIprop.hpp:217-252).
+NUSI_FN int alpha_edge_list(const double* lo, const double* hi, int b0, int T, double* E, int* il, int* ih)
+{
+    int c = 0;
+    for (int j = 0; j < kAlphaTile && b0 + j < T; ++j) {
+        const double l = lo[b0 + j], h = hi[b0 + j];
+        if (c > 0 && l == E[c - 1]) il[j] = c - 1;
+        else { E[c] = l; il[j] = c++; }
+        E[c] = h;
+        ih[j] = c++;
+    }
+    return c;
+}
+
+// Tile precomputation jobs (k_alpha_tile; emulated on the host by tests/hostcheck).
+// Edge-leaf block of mass state k: [5][ct] t edges, [5][cs] S' edges, [3][kAlphaTile] m bins.
+NUSI_FN int alpha_tile_edge_stride(int cs, int ct) { return kTEdgeFields * ct + kSEdgeFields * cs + kMBinFields * kAlphaTile; }
+// job in [0, 3 (ct + cs + kAlphaTile)): one edge / m-bin leaf set of one mass state
+NUSI_FN void alpha_tile_edge_job(const Point& P, int job, const double* tE, int ct, const double* sE, int cs,
+                                 const double* lo, const double* hi, int m0, int T, double* edg)
+{
+    const double mphi = P.mphi, Ga = P.Ga, m2 = mphi * mphi, gr = Ga / mphi, gr2 = gr * gr;
+    const int per = ct + cs + kAlphaTile;
+    const int k = job / per, j = job - k * per;
+    const double mk = P.mn[k];
+    double* ted = edg + k * alpha_tile_edge_stride(cs, ct);
+    double* sed = ted + kTEdgeFields * ct;
+    double* mbv = sed + kSEdgeFields * cs;
+    if (j < ct) {
+        if (!P.non_resonant) return;
+        AlphaTEdge e;
+        alpha_tedge(alpha_t(mk, tE[j], m2), gr2, e);
+        ted[j] = e.Lm1; ted[ct + j] = e.la; ted[2 * ct + j] = e.cm; ted[3 * ct + j] = e.L2; ted[4 * ct + j] = e.am;
+    } else if (j < ct + cs) {
+        if (!P.non_resonant) return;
+        const int q = j - ct;
+        AlphaSEdge e;
+        alpha_sedge(alpha_S(mk, sE[q], m2), gr, gr2, e);
+        sed[q] = e.lS; sed[cs + q] = e.l2; sed[2 * cs + q] = e.Ls; sed[3 * cs + q] = e.cS; sed[4 * cs + q] = e.lS2;
+    } else {
+        const int q = j - ct - cs;
+        if (m0 + q >= T) return;
+        AlphaMBin b;
+        alpha_mbin(alpha_S(mk, lo[m0 + q], m2), alpha_S(mk, hi[m0 + q], m2), mphi, Ga, b);
+        mbv[q] = b.lr; mbv[kAlphaTile + q] = b.lr2; mbv[2 * kAlphaTile + q] = b.atd;
+    }
+}
+// job j in [0, cs ct): corner (S' slot j / ct, t slot j % ct) of mass state k
+NUSI_FN void alpha_tile_corner_job(const Point& P, int k, int j, const double* tE, int ct, const double* sE, int cc,
+                                   double* cor)
+{
+    const double mphi = P.mphi, m2 = mphi * mphi, gr = P.Ga / mphi, mk = P.mn[k];
+    const int si = j / ct, ti = j - si * ct;
+    AlphaCorner c;
+    alpha_corner(alpha_S(mk, sE[si], m2), alpha_t(mk, tE[ti], m2), gr, c);
+    cor[j] = c.L; cor[cc + j] = c.LL; cor[2 * cc + j] = c.TU1; cor[3 * cc + j] = c.TU2; cor[4 * cc + j] = c.G;
+    cor[5 * cc + j] = c.Drr; cor[6 * cc + j] = c.Dri; cor[7 * cc + j] = c.Dcr; cor[8 * cc + j] = c.Dci; cor[9 * cc + j] = c.A;
+}
+// leaves of entry (n0 + ln, m0 + lm) of a tile for mass state k
+NUSI_FN TileLeaves alpha_tile_leaves(const double* cor, const double* edg, int k, int cs, int ct, int lm,
+                                     const int* sl, const int* sh, const int* tl, const int* th, int ln)
+{
+    TileLeaves lv;
+    lv.cor = cor;
+    lv.cc = cs * ct;
+    lv.ct = ct;
+    lv.cs = cs;
+    lv.mb = lm;
+    lv.sidx[0] = sl[lm];
+    lv.sidx[1] = sh[lm];
+    lv.tidx[0] = tl[ln];
+    lv.tidx[1] = th[ln];
+    lv.ted = edg + k * alpha_tile_edge_stride(cs, ct);
+    lv.sed = lv.ted + kTEdgeFields * ct;
+    lv.mbv = lv.sed + kSEdgeFields * cs;
+    return lv;
+}
+
+// one mass state k of alpha(Em, Ep, Em', Ep'): tot += wgt * (every channel)
+template <class Lv>
+NUSI_FN void alpha_k(const Point& P, const SplineSet& spl, int k, double Em, double Ep, double Emp, double Epp,
+                     const Lv& lv, double& tot, int& warn)
 {
     const double g = P.g, mphi = P.mphi, Ga = P.Ga;
     const double g4 = (g * g) * (g * g), m2 = mphi * mphi, m4 = (mphi * mphi) * (mphi * mphi);
     const double gr = Ga / mphi, gr2 = gr * gr;
     const bool maj = P.majorana;
-    double tot = 0;
-    NUSI_MASS_LOOP
-    for (int k = 0; k < 3; ++k) {
-        const double mk = P.mn[k], uk = P.u[k];
-        double tp = -2 * mk * Ep / m2, tm = -2 * mk * Em / m2;
-        const double Sp = 2 * mk * Epp / m2, Sm = 2 * mk * Emp / m2;
-        if (fabs(tm + 1) < 1e-7) tm += tm * 1e-6;
-        if (fabs(tp + 1) < 1e-7) tp += tp * 1e-6;
-        const double wgt = m4 / (2 * mk);
+    const double mk = P.mn[k], uk = P.u[k];
+    const double tp = alpha_t(mk, Ep, m2), tm = alpha_t(mk, Em, m2);
+    const double Sp = alpha_S(mk, Epp, m2), Sm = alpha_S(mk, Emp, m2);
+    const double wgt = m4 / (2 * mk);
+    const AlphaMBin mb = lv.mbin(Sm, Sp);
 
-        double as;
-        if (Sp < 1e-5)
-            as = g4 / (8 * kPi * Ga * (mphi * mphi * mphi)) * (tm - tp) *
-                 ((gr * (1 + gr2 + 2 * Sm)) / ((1 + gr2) * (1 + gr2)) * (Sp - Sm) + gr / ((1 + gr2) * (1 + gr2)) * ((Sp - Sm) * (Sp - Sm)));
-        else
-            as = g4 / (8 * kPi * Ga * (mphi * mphi * mphi)) * (tm - tp) * atandiff(mphi * (Sp - 1) / Ga, mphi * (Sm - 1) / Ga);
-        as *= uk;
-        if (!maj) as /= 2.;
-        tot += wgt * as;
-        if (!P.non_resonant) continue;
+    double as;
+    if (Sp < 1e-5)
+        as = g4 / (8 * kPi * Ga * (mphi * mphi * mphi)) * (tm - tp) *
+             ((gr * (1 + gr2 + 2 * Sm)) / ((1 + gr2) * (1 + gr2)) * (Sp - Sm) + gr / ((1 + gr2) * (1 + gr2)) * ((Sp - Sm) * (Sp - Sm)));
+    else
+        as = g4 / (8 * kPi * Ga * (mphi * mphi * mphi)) * (tm - tp) * mb.atd;
+    as *= uk;
+    if (!maj) as /= 2.;
+    tot += wgt * as;
+    if (!P.non_resonant) return;
 
-        const double Lmt = nm::log1p(-tm), Lmp = nm::log1p(-tp);
-        const double lSm = nm::log(Sm), lSp = nm::log(Sp);
-        const double Lmm = nm::log1p(Sm + tm), Lpm = nm::log1p(Sp + tm), Lmq = nm::log1p(Sm + tp), Lpq = nm::log1p(Sp + tp);
-        const double SS = Sm * Sp;
-        double at;
-        if (maj) {
-            const double LA = nm::log(((1 + Sm + tm) * (-1 + tp)) / ((-1 + tm) * (1 + Sm + tp)));
-            const double LB = nm::log(((1 + Sp + tm) * (-1 + tp)) / ((-1 + tm) * (1 + Sp + tp)));
-            const double inner = SS * (-tm + tp) * lSm + SS * (tm - tp) * lSp - SS * Lmm - SS * tp * Lmm + SS * Lpm + SS * tp * Lpm
-                                 - Sp * LA - Sp * tm * LA - Sp * tp * LA - Sp * tm * tp * LA
-                                 + SS * nm::log(1 + Sm + tp) + SS * tm * Lmq
-                                 + Sm * LB + Sm * tm * LB + Sm * tp * LB + Sm * tm * tp * LB
-                                 - SS * nm::log(1 + Sp + tp) - SS * tm * Lpq;
-            at = g4 / (Sm * Sp * 16 * kPi * m4) *
-                 (-((Sm - Sp) * (3 + 2 * tm * (-1 + tp) - 2 * tp) * (tm - tp)) / ((-1 + tm) * (-1 + tp))
-                  + 2 * inner / ((1 + tm) * (1 + tp))
-                  - ((SS * nm::log((Sm * (1 + Sp + tm)) / (Sp * (1 + Sm + tm)))) / ((1 + tm) * (1 + tm))
-                     + (((Sm - Sp) * (tm - tp) * (1 + tp)) / (1 + tm) - SS * nm::log((Sm * (1 + Sp + tp)) / (Sp * (1 + Sm + tp)))) / ((1 + tp) * (1 + tp))));
-            if (at < 0) at = gl33_rect(0, tp, tm, Sm, Sp) * (g4 / (16 * kPi * m4));
-        } else {
-            const double brk = -((tm - tp) * (2 + tm * (-1 + tp) - tp)) - 2 * (-1 + tm) * (-1 + tp) * (Lmt - Lmp);
-            at = 3. / 2. * g4 / (32 * kPi * m4 * Sm * Sp * (-1 + tm) * (-1 + tp)) * (Sm - Sp) * brk;
-            if (at < 0) at = gl33_rect(1, tp, tm, Sm, Sp) * (3. / 2. * g4 / (32 * kPi * m4));
-        }
+    const AlphaTEdge eTm = lv.tedge(0, tm), eTp = lv.tedge(1, tp);
+    const AlphaSEdge eSm = lv.sedge(0, Sm), eSp = lv.sedge(1, Sp);
+    const double Lmt = eTm.Lm1, Lmp = eTp.Lm1;
+    const double lSm = eSm.lS, lSp = eSp.lS;
+    const double SS = Sm * Sp;
+    const double Lsm = eSm.Ls, Lsp = eSp.Ls;
+    double at, au, atu = 0., ast;
+    if (maj) {
+        const AlphaCorner cmm = lv.corner(0, 0, Sm, tm), cpm = lv.corner(1, 0, Sp, tm);
+        const AlphaCorner cmq = lv.corner(0, 1, Sm, tp), cpq = lv.corner(1, 1, Sp, tp);
+        const double Lmm = cmm.L, Lpm = cpm.L, Lmq = cmq.L, Lpq = cpq.L;
+        const double LA = nm::log(((1 + Sm + tm) * (-1 + tp)) / ((-1 + tm) * (1 + Sm + tp)));
+        const double LB = nm::log(((1 + Sp + tm) * (-1 + tp)) / ((-1 + tm) * (1 + Sp + tp)));
+        const double inner = SS * (-tm + tp) * lSm + SS * (tm - tp) * lSp - SS * Lmm - SS * tp * Lmm + SS * Lpm + SS * tp * Lpm
+                             - Sp * LA - Sp * tm * LA - Sp * tp * LA - Sp * tm * tp * LA
+                             + SS * cmq.LL + SS * tm * Lmq
+                             + Sm * LB + Sm * tm * LB + Sm * tp * LB + Sm * tm * tp * LB
+                             - SS * cpq.LL - SS * tm * Lpq;
+        at = g4 / (Sm * Sp * 16 * kPi * m4) *
+             (-((Sm - Sp) * (3 + 2 * tm * (-1 + tp) - 2 * tp) * (tm - tp)) / ((-1 + tm) * (-1 + tp))
+              + 2 * inner / ((1 + tm) * (1 + tp))
+              - ((SS * nm::log((Sm * (1 + Sp + tm)) / (Sp * (1 + Sm + tm)))) / ((1 + tm) * (1 + tm))
+                 + (((Sm - Sp) * (tm - tp) * (1 + tp)) / (1 + tm) - SS * nm::log((Sm * (1 + Sp + tp)) / (Sp * (1 + Sm + tp)))) / ((1 + tp) * (1 + tp))));
+        if (at < 0) at = gl33_rect(0, tp, tm, Sm, Sp) * (g4 / (16 * kPi * m4));
         at *= uk;
         tot += wgt * at;
-
-        double au;
-        if (maj) au = at;
-        else {
-            const double brk = -((tm - tp) * (2 + tm * (-1 + tp) - tp)) - 2 * (-1 + tm) * (-1 + tp) * (Lmt - Lmp);
-            au = 1. / 2. * g4 / (32 * kPi * m4 * Sm * Sp * (-1 + tm) * (-1 + tp)) * (Sm - Sp) * brk;
-            if (au < 0) au = gl33_rect(1, tp, tm, Sm, Sp) * (1. / 2. * g4 / (32 * kPi * m4));
-            au *= uk;
-        }
+        au = at;
         tot += wgt * au;
 
-        double atu = 0.;
-        if (maj) {
-            const double Qmp = (1 + Sm + tp) / Sm, Qpp = (1 + Sp + tp) / Sp, Qmm = (1 + Sm + tm) / Sm, Qpm = (1 + Sp + tm) / Sp;
-            double Fp, Fm;
-            if (tp < -1) Fp = li2(Qmp) - li2(Qpp);
-            else {
-                const double a = nm::log(Qmp), b = nm::log(Qpp);
-                Fp = -li2(Sm / (1 + Sm + tp)) + li2(Sp / (1 + Sp + tp)) - 0.5 * (a * a - b * b);
-            }
-            if (tm < -1) Fm = -li2(Qmm) + li2(Qpm);
-            else {
-                const double a = nm::log(Qmm), b = nm::log(Qpm);
-                Fm = li2(Sm / (1 + Sm + tm)) - li2(Sp / (1 + Sp + tm)) + 0.5 * (a * a - b * b);
-            }
-            const double lap = (tp > -1) ? nm::log1p(tp) : nm::log(-1 - tp);
-            const double lam = (tm > -1) ? nm::log1p(tm) : nm::log(-1 - tm);
-            const double Pq = (1 + tm) * (1 + tp);
-            const double l2m = nm::log((2 + Sm) / Sm), l2p = nm::log((2 + Sp) / Sp);
-            const double SSP = SS * (1 + tm) * (1 + tp);
-            atu = g4 / (32 * kPi * m4 * Sm * Sp * (1 + tm) * (1 + tp)) *
-                  (-4 * (Sm - Sp) * (1 + tm) * (tm - tp) * (1 + tp)
-                   + 2 * SS * tp * (nm::log(Sm / Sp) - Lmm + Lpm)
-                   + 2 * Sp * (1 + tm) * (1 + tp) * (Lmt - Lmm - Lmp + Lmq)
-                   - 2 * Sm * (1 + tm) * (1 + tp) * (Lmt - Lpm - Lmp + Lpq)
-                   + 2 * SS * (-Lmm + Lpm + Lmq - Lpq)
-                   + SSP * (l2m * (lSp + Lmq) - l2p * (lSm + Lpq) + Lmp * (nm::log(Sm / Sp) - Lmq + Lpq))
-                   + SSP * ((lSp + Lmm) * (nm::log(Sm / (2 + Sm)) + Lmt - lam) + (lSm + Lpm) * (l2p - Lmt + lam))
-                   + SS * (nm::log(Sp / Sm) + Lmq - Lpq) * (2 * tm + Pq * lap)
-                   + SSP * (li2((1 + Sm + tm) / (2 + Sm)) - li2((1 + Sp + tm) / (2 + Sp)) - li2((1 + Sm + tp) / (2 + Sm)) + li2((1 + Sp + tp) / (2 + Sp)))
-                   + SSP * (Fp + Fm));
-            // nuSIprop.hpp:1401-1418: the fallback assigns a shadowing local; a negative alpha_tu stays.
+        double Fp, Fm;
+        if (tp < -1) Fp = cmq.TU1 - cpq.TU1;
+        else {
+            const double a = cmq.TU2, b = cpq.TU2;
+            Fp = -cmq.TU1 + cpq.TU1 - 0.5 * (a * a - b * b);
         }
+        if (tm < -1) Fm = -cmm.TU1 + cpm.TU1;
+        else {
+            const double a = cmm.TU2, b = cpm.TU2;
+            Fm = cmm.TU1 - cpm.TU1 + 0.5 * (a * a - b * b);
+        }
+        const double lap = eTp.la, lam = eTm.la;
+        const double Pq = (1 + tm) * (1 + tp);
+        const double l2m = eSm.l2, l2p = eSp.l2;
+        const double SSP = SS * (1 + tm) * (1 + tp);
+        atu = g4 / (32 * kPi * m4 * Sm * Sp * (1 + tm) * (1 + tp)) *
+              (-4 * (Sm - Sp) * (1 + tm) * (tm - tp) * (1 + tp)
+               + 2 * SS * tp * (mb.lr - Lmm + Lpm)
+               + 2 * Sp * (1 + tm) * (1 + tp) * (Lmt - Lmm - Lmp + Lmq)
+               - 2 * Sm * (1 + tm) * (1 + tp) * (Lmt - Lpm - Lmp + Lpq)
+               + 2 * SS * (-Lmm + Lpm + Lmq - Lpq)
+               + SSP * (l2m * (lSp + Lmq) - l2p * (lSm + Lpq) + Lmp * (mb.lr - Lmq + Lpq))
+               + SSP * ((lSp + Lmm) * (eSm.lS2 + Lmt - lam) + (lSm + Lpm) * (l2p - Lmt + lam))
+               + SS * (mb.lr2 + Lmq - Lpq) * (2 * tm + Pq * lap)
+               + SSP * (cmm.G - cpm.G - cmq.G + cpq.G)
+               + SSP * (Fp + Fm));
+        // nuSIprop.hpp:1401-1418: the fallback assigns a shadowing local; a negative alpha_tu stays.
         atu *= uk;
         tot += wgt * atu;
 
         // s-t interference: eight complex dilogarithms (nuSIprop.hpp:1431-1451)
-        const cd dtm = C(2 + tm, -gr), dtp = C(2 + tp, -gr);      // 2 - I*gr + t
-        const double z1 = (1 + Sm + tm) / (1 + tm), z3 = (1 + Sp + tm) / (1 + tm);
-        const double z5 = (1 + Sm + tp) / (1 + tp), z7 = (1 + Sp + tp) / (1 + tp);
-        const cd z2 = (1 + Sm + tm) / dtm, z4 = (1 + Sp + tm) / dtm;
-        const cd z6 = (1 + Sm + tp) / dtp, z8 = (1 + Sp + tp) / dtp;
-        const cd D1 = cli2(z1, 0.0), D2 = cli2(z2), D3 = cli2(z3, 0.0), D4 = cli2(z4);
-        const cd D5 = cli2(z5, 0.0), D6 = cli2(z6), D7 = cli2(z7, 0.0), D8 = cli2(z8);
-        const double Lsm = nm::log1p(((-1 + Sm) * (-1 + Sm)) / gr2), Lsp = nm::log1p(((-1 + Sp) * (-1 + Sp)) / gr2);
-        double ast;
-        if (maj) {
-            const double cm = carg_real(-(1 / (1 + tm))), cp = carg_real(-(1 / (1 + tp)));
-            const double L2m = nm::log1p(((2 + tm) * (2 + tm)) / gr2), L2p = nm::log1p(((2 + tp) * (2 + tp)) / gr2);
-            const double am = nm::log(fabs(1 + tm)), ap = nm::log(fabs(1 + tp));
-            const cd nm = C(-1 + Sm, gr), np = C(-1 + Sp, gr);      // -1 + I*gr + S
-            ast = g4 / (32 * kPi * (1 + gr2) * m4) *
-                  (2 * gr * (D1.i - D2.i - D3.i + D4.i - D5.i + D6.i + D7.i - D8.i)
-                   - 2 * (D1.r - D2.r - D3.r + D4.r - D5.r + D6.r + D7.r - D8.r)
-                   + 2 * gr * (cm - carg(-(nm / dtm))) * Lmm
-                   - 2 * gr * (cm - carg(-(np / dtm))) * Lpm
-                   + 2 * gr * (cp - carg(-(np / dtp))) * Lpq
-                   - 2 * gr * (cp - carg(-(nm / dtp))) * Lmq
-                   + 2 * (gr * carg(nm) - gr * carg(np) + Lsp / 2. - Lsm / 2. + lSm - lSp) * (2 * (tm - tp) + (Lmt - Lmp))
-                   + Lmm * (Lsm - L2m - 2 * (lSm - am)) - Lpm * (Lsp - L2m - 2 * (lSp - am))
-                   - Lmq * (Lsm - L2p - 2 * (lSm - ap)) + Lpq * (Lsp - L2p - 2 * (lSp - ap)));
-        } else
-            ast = g4 / (32 * kPi * (1 + gr2) * m4) *
-                  ((2 * gr * carg(C(-1 + Sm, gr)) - 2 * gr * carg(C(-1 + Sp, gr)) + 2 * lSm - 2 * lSp + Lsp - Lsm) * (tm - tp + Lmt - Lmp));
-        ast *= uk;
-        tot += wgt * ast;
-        const double asu = maj ? ast : 0.;
-        tot += wgt * asu;
-
-        double app = 0;
-        if (Sm > 4 && P.phiphi) {
-            if (Sm < 1e4) {
-                const double d = Sp / Sm;
-                const double xx[3] = {Sm, nm::log(-Sm / tm) / nm::log(d) * 1.0001, nm::log10(d)};
-                double v = 0;
-                if (!spl.a.eval(xx, v)) warn |= kWarnSplineOOB;
-                app = g4 / m4 * fabs(v);
-            } else if (tm < -1) {
-                const double l1m = nm::log(-1 - tm), l0m = nm::log(-tm), l1p = nm::log(-1 - tp), l0p = nm::log(-tp);
-                app = g4 / m4 *
-                      ((-Sm + Sp) * ((tm - tp) * (Sp * (-2 + tm + tp) + Sm * (-2 - 24 * Sp + tm + tp))
-                                     + 4 * (-(Sp * (1 + tm)) + Sm * (-1 + 2 * Sp + (-1 + Sp) * tm)) * l1m
-                                     + 2 * (3 * Sp + Sm * (3 + 4 * Sp)) * tm * l0m
-                                     + 4 * (Sp + Sp * tp + Sm * (1 + tp - Sp * (2 + tp))) * l1p
-                                     - 2 * (3 * Sp + Sm * (3 + 4 * Sp)) * tp * l0p)
-                       + 2 * (Sm * Sm) * lSp * ((3 + 2 * Sp) * (tm - tp) + 2 * (Sp * Sp) * ((-1 - tm) * l1m + tm * l0m + (1 + tp) * l1p - tp * l0p))
-                       + 2 * (Sp * Sp) * lSm * ((-3 - 2 * Sm) * (tm - tp) + 2 * (Sm * Sm) * ((1 + tm) * l1m - tm * l0m - (1 + tp) * l1p + tp * l0p)))
-                      / (256. * kPi * (Sm * Sm) * (Sp * Sp));
-            } else if (tp < -1) {
-                const double l1p = nm::log(-1 - tp), l0p = nm::log(-tp);
-                app = g4 / m4 *
-                      ((2 * (Sm * Sm) * lSp * ((1 + tp) * (-3 - 2 * Sp + 2 * (Sp * Sp) * l1p) - 2 * (Sp * Sp) * tp * l0p)
-                        + (Sm - Sp) * ((1 + tp) * (-3 * (Sm + Sp + 8 * Sm * Sp) + (Sm + Sp) * tp)
-                                       + 4 * (-(Sp * (1 + tp)) + Sm * (-1 + 2 * Sp + (-1 + Sp) * tp)) * l1p
-                                       + 2 * (3 * Sp + Sm * (3 + 4 * Sp)) * tp * l0p)
-                        + 2 * (Sp * Sp) * lSm * ((3 + 2 * Sm) * (1 + tp) + 2 * (Sm * Sm) * (-((1 + tp) * l1p) + tp * l0p)))
-                           / (256. * kPi * (Sm * Sm) * (Sp * Sp))
-                       + (-1 - tm) * (-6 * Sm + 6 * Sp - 2 * (-2 + Sm) * Sp * lSm + Sm * Sp * (lSm * lSm) + 2 * Sm * (-2 + Sp) * lSp - Sm * Sp * (lSp * lSp))
-                             / (128. * kPi * Sm * Sp));
-            } else
-                app = g4 / m4 * (tp - tm) *
-                      (-6 * Sm + 6 * Sp - 2 * (-2 + Sm) * Sp * lSm + Sm * Sp * (lSm * lSm) + 2 * Sm * (-2 + Sp) * lSp - Sm * Sp * (lSp * lSp))
-                      / (128. * kPi * Sm * Sp);
-            app *= uk;
-            if (maj) app *= 2;
-            app *= 2;
-            if (maj) app *= 2;
-        }
-        tot += wgt * app;
-
-        const double nrm = (g / mphi) * (g / mphi) * ((g / mphi) * (g / mphi));
-        if (as < 0 || at / nrm < -1e-11 || au / nrm < -1e-11 || atu / nrm < -1e-11 || (ast + as + at) / nrm < -1e-11)
-            warn |= kWarnAlpha;
+        const double cm = eTm.cm, cp = eTp.cm;
+        const double L2m = eTm.L2, L2p = eTp.L2;
+        const double am = eTm.am, ap = eTp.am;
+        ast = g4 / (32 * kPi * (1 + gr2) * m4) *
+              (2 * gr * (cmm.Dri - cmm.Dci - cpm.Dri + cpm.Dci - cmq.Dri + cmq.Dci + cpq.Dri - cpq.Dci)
+               - 2 * (cmm.Drr - cmm.Dcr - cpm.Drr + cpm.Dcr - cmq.Drr + cmq.Dcr + cpq.Drr - cpq.Dcr)
+               + 2 * gr * (cm - cmm.A) * Lmm
+               - 2 * gr * (cm - cpm.A) * Lpm
+               + 2 * gr * (cp - cpq.A) * Lpq
+               - 2 * gr * (cp - cmq.A) * Lmq
+               + 2 * (gr * eSm.cS - gr * eSp.cS + Lsp / 2. - Lsm / 2. + lSm - lSp) * (2 * (tm - tp) + (Lmt - Lmp))
+               + Lmm * (Lsm - L2m - 2 * (lSm - am)) - Lpm * (Lsp - L2m - 2 * (lSp - am))
+               - Lmq * (Lsm - L2p - 2 * (lSm - ap)) + Lpq * (Lsp - L2p - 2 * (lSp - ap)));
+    } else {
+        const double brk = -((tm - tp) * (2 + tm * (-1 + tp) - tp)) - 2 * (-1 + tm) * (-1 + tp) * (Lmt - Lmp);
+        at = 3. / 2. * g4 / (32 * kPi * m4 * Sm * Sp * (-1 + tm) * (-1 + tp)) * (Sm - Sp) * brk;
+        if (at < 0) at = gl33_rect(1, tp, tm, Sm, Sp) * (3. / 2. * g4 / (32 * kPi * m4));
+        at *= uk;
+        tot += wgt * at;
+        au = 1. / 2. * g4 / (32 * kPi * m4 * Sm * Sp * (-1 + tm) * (-1 + tp)) * (Sm - Sp) * brk;
+        if (au < 0) au = gl33_rect(1, tp, tm, Sm, Sp) * (1. / 2. * g4 / (32 * kPi * m4));
+        au *= uk;
+        tot += wgt * au;
+        tot += wgt * atu;   // alpha_tu = 0 for Dirac
+        ast = g4 / (32 * kPi * (1 + gr2) * m4) *
+              ((2 * gr * eSm.cS - 2 * gr * eSp.cS + 2 * lSm - 2 * lSp + Lsp - Lsm) * (tm - tp + Lmt - Lmp));
     }
+    ast *= uk;
+    tot += wgt * ast;
+    const double asu = maj ? ast : 0.;
+    tot += wgt * asu;
+
+    double app = 0;
+    if (Sm > 4 && P.phiphi) {
+        if (Sm < 1e4) {
+            const double d = Sp / Sm;
+            const double xx[3] = {Sm, nm::log(-Sm / tm) / nm::log(d) * 1.0001, nm::log10(d)};
+            double v = 0;
+            if (!spl.a.eval(xx, v)) warn |= kWarnSplineOOB;
+            app = g4 / m4 * fabs(v);
+        } else if (tm < -1) {
+            const double l1m = nm::log(-1 - tm), l0m = nm::log(-tm), l1p = nm::log(-1 - tp), l0p = nm::log(-tp);
+            app = g4 / m4 *
+                  ((-Sm + Sp) * ((tm - tp) * (Sp * (-2 + tm + tp) + Sm * (-2 - 24 * Sp + tm + tp))
+                                 + 4 * (-(Sp * (1 + tm)) + Sm * (-1 + 2 * Sp + (-1 + Sp) * tm)) * l1m
+                                 + 2 * (3 * Sp + Sm * (3 + 4 * Sp)) * tm * l0m
+                                 + 4 * (Sp + Sp * tp + Sm * (1 + tp - Sp * (2 + tp))) * l1p
+                                 - 2 * (3 * Sp + Sm * (3 + 4 * Sp)) * tp * l0p)
+                   + 2 * (Sm * Sm) * lSp * ((3 + 2 * Sp) * (tm - tp) + 2 * (Sp * Sp) * ((-1 - tm) * l1m + tm * l0m + (1 + tp) * l1p - tp * l0p))
+                   + 2 * (Sp * Sp) * lSm * ((-3 - 2 * Sm) * (tm - tp) + 2 * (Sm * Sm) * ((1 + tm) * l1m - tm * l0m - (1 + tp) * l1p + tp * l0p)))
+                  / (256. * kPi * (Sm * Sm) * (Sp * Sp));
+        } else if (tp < -1) {
+            const double l1p = nm::log(-1 - tp), l0p = nm::log(-tp);
+            app = g4 / m4 *
+                  ((2 * (Sm * Sm) * lSp * ((1 + tp) * (-3 - 2 * Sp + 2 * (Sp * Sp) * l1p) - 2 * (Sp * Sp) * tp * l0p)
+                    + (Sm - Sp) * ((1 + tp) * (-3 * (Sm + Sp + 8 * Sm * Sp) + (Sm + Sp) * tp)
+                                   + 4 * (-(Sp * (1 + tp)) + Sm * (-1 + 2 * Sp + (-1 + Sp) * tp)) * l1p
+                                   + 2 * (3 * Sp + Sm * (3 + 4 * Sp)) * tp * l0p)
+                    + 2 * (Sp * Sp) * lSm * ((3 + 2 * Sm) * (1 + tp) + 2 * (Sm * Sm) * (-((1 + tp) * l1p) + tp * l0p)))
+                       / (256. * kPi * (Sm * Sm) * (Sp * Sp))
+                   + (-1 - tm) * (-6 * Sm + 6 * Sp - 2 * (-2 + Sm) * Sp * lSm + Sm * Sp * (lSm * lSm) + 2 * Sm * (-2 + Sp) * lSp - Sm * Sp * (lSp * lSp))
+                         / (128. * kPi * Sm * Sp));
+        } else
+            app = g4 / m4 * (tp - tm) *
+                  (-6 * Sm + 6 * Sp - 2 * (-2 + Sm) * Sp * lSm + Sm * Sp * (lSm * lSm) + 2 * Sm * (-2 + Sp) * lSp - Sm * Sp * (lSp * lSp))
+                  / (128. * kPi * Sm * Sp);
+        app *= uk;
+        if (maj) app *= 2;
+        app *= 2;
+        if (maj) app *= 2;
+    }
+    tot += wgt * app;
+
+    const double nrm = (g / mphi) * (g / mphi) * ((g / mphi) * (g / mphi));
+    if (as < 0 || at / nrm < -1e-11 || au / nrm < -1e-11 || atu / nrm < -1e-11 || (ast + as + at) / nrm < -1e-11)
+        warn |= kWarnAlpha;
+}
+
+NUSI_FN double alpha_entry(const Point& P, const SplineSet& spl, double Em, double Ep, double Emp, double Epp, int& warn)
+{
+    const DirectLeaves lv{P.Ga / P.mphi, (P.Ga / P.mphi) * (P.Ga / P.mphi), P.mphi, P.Ga};
+    double tot = 0;
+    NUSI_MASS_LOOP
+    for (int k = 0; k < 3; ++k) alpha_k(P, spl, k, Em, Ep, Emp, Epp, lv, tot, warn);
     return tot;
 }
 

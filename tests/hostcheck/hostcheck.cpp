@@ -2,6 +2,8 @@
 // (nusiprop_amd/csrc/nusi_physics.hpp) for the host so that tests/ can check
 // the table formulas against the oracle without a GPU.  Never linked into
 // libnusi.so; the product runs these functions only inside HIP kernels.
+#include <vector>
+
 #include "nusi_physics.hpp"
 
 extern "C" {
@@ -28,6 +30,47 @@ int hc_tables(const double* pt, const int* flags, int T, const double* lo, const
         for (int m = n + 1; m < T; ++m) A[(size_t)n * T + m] = nusi::alpha_entry(P, spl, lo[n], hi[n], lo[m], hi[m], w);
     }
     return w;
+}
+
+// Host emulation of k_alpha_tile: the same edge lists, job helpers and TileLeaves combine, one
+// tile at a time (work-items run sequentially, phases in kernel order).  alpha dense T*T, m > n.
+int hc_alpha_tiled(const double* pt, const int* flags, int T, const double* lo, const double* hi, double* A)
+{
+    using namespace nusi;
+    const Point P = mk(pt, flags);
+    SplineSet spl{};
+    const int nt = (T + kAlphaTile - 1) / kAlphaTile;
+    std::vector<double> sm(kCornerFields * 4 * kAlphaTile * kAlphaTile + 3 * 1000);
+    int warn = 0;
+    for (int tm = 0; tm < nt; ++tm)
+        for (int tn = 0; tn <= tm; ++tn) {
+            double tE[2 * kAlphaTile], sE[2 * kAlphaTile];
+            int tl[kAlphaTile], th[kAlphaTile], sl[kAlphaTile], sh[kAlphaTile];
+            const int n0 = tn * kAlphaTile, m0 = tm * kAlphaTile;
+            const int ct = alpha_edge_list(lo, hi, n0, T, tE, tl, th);
+            const int cs = alpha_edge_list(lo, hi, m0, T, sE, sl, sh);
+            const int cc = cs * ct;
+            double* cor = sm.data();
+            double* edg = cor + kCornerFields * cc;
+            for (int job = 0; job < 3 * (ct + cs + kAlphaTile); ++job)
+                alpha_tile_edge_job(P, job, tE, ct, sE, cs, lo, hi, m0, T, edg);
+            double tot[kAlphaTile * kAlphaTile] = {};
+            for (int k = 0; k < 3; ++k) {
+                if (P.non_resonant && P.majorana)
+                    for (int j = 0; j < cc; ++j) alpha_tile_corner_job(P, k, j, tE, ct, sE, cc, cor);
+                for (int e = 0; e < kAlphaTile * kAlphaTile; ++e) {
+                    const int ln = e % kAlphaTile, lm = e / kAlphaTile, n = n0 + ln, m = m0 + lm;
+                    if (!(n < m && m < T) || !(P.non_resonant || m == n + 1)) continue;
+                    const TileLeaves lv = alpha_tile_leaves(cor, edg, k, cs, ct, lm, sl, sh, tl, th, ln);
+                    alpha_k(P, spl, k, lo[n], hi[n], lo[m], hi[m], lv, tot[e], warn);
+                }
+            }
+            for (int e = 0; e < kAlphaTile * kAlphaTile; ++e) {
+                const int ln = e % kAlphaTile, lm = e / kAlphaTile, n = n0 + ln, m = m0 + lm;
+                if (n < m && m < T) A[(size_t)n * T + m] = tot[e];
+            }
+        }
+    return warn;
 }
 
 double hc_lum(const double* pt, const int* flags, double z, double sfr_z, double Em, double Ep)

@@ -63,3 +63,29 @@ def test_tables_bit_identical(oracle_mod, name):
     iu = np.triu_indices(T, 1)
     assert np.array_equal(Ah[iu], al[iu]), "%d alpha entries differ" % np.sum(Ah[iu] != al[iu])
     assert (w & 7) == o.warnings()
+
+
+@pytest.mark.parametrize("name,N", [("test_cpp", 40), ("c2b", 44), ("dirac", 31), ("resonant_only", 40),
+                                    ("inverted", 46), ("strong", 40)])
+def test_tiled_alpha_bit_identical(oracle_mod, name, N):
+    """The tile kernel's data path (edge dedup, per-edge / per-corner leaf arrays,
+    TileLeaves slot mapping), emulated on the host, against the oracle: bit for bit.
+    N is chosen so the tiles straddle the N | redshift-extended junction."""
+    from tests.hostcheck import build_hostcheck
+    H = build_hostcheck()
+    kw = dict(cases.SMALL_CASES[name], N_bins_E=N)
+    o = oracle_mod.Oracle(**cases.oracle_kwargs(kw))
+    _, _, al = o.tables()
+    lo, hi = extended_axis(o)
+    pt, flags = point_array(o, kw)
+    T = o.T
+    Ah = np.zeros((T, T))
+    H.hc_alpha_tiled.restype = ctypes.c_int
+    w = H.hc_alpha_tiled(_dp(pt), flags, T, _dp(lo), _dp(hi), _dp(Ah))
+    iu = np.triu_indices(T, 1)
+    if kw["non_resonant"]:
+        assert np.array_equal(Ah[iu], al[iu]), "%d alpha entries differ" % np.sum(Ah[iu] != al[iu])
+    else:
+        d = np.arange(T - 1)
+        assert np.array_equal(Ah[d, d + 1], al[d, d + 1])
+    assert (w & 4) == (o.warnings() & 4)
