@@ -38,7 +38,9 @@ def parse():
     ap.add_argument("--points", type=int, default=0, help="points per GPU (default: 1024 for c4/c5, 1 for c2)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="budget of the oracle CPU baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--traffic-json", default="", help="per-launch HBM bytes from a separate rocprofv3 --pmc pass")
+    ap.add_argument("--traffic-json", default="",
+                    help="per-launch HBM bytes / fp64 VALU work from rocprofv3 --pmc passes (scripts/pmc_summary.py); "
+                         "default for the default workload: the committed profiles/pmc_traffic_latest.json")
     return ap.parse_args()
 
 
@@ -135,10 +137,15 @@ def main():
     casc_bytes = scan.cascade_bytes_per_point(N, Nz) * P
     casc_s = sum_ms[2] / max(ncalls, 1) / 1e3
     alpha_s = sum_ms[1] / max(ncalls, 1) / 1e3
-    traffic = None
-    if args.traffic_json and os.path.exists(args.traffic_json):
-        with open(args.traffic_json) as fh:
-            traffic = json.load(fh).get("k_cascade_bytes_per_launch")
+    traffic, tsrc, pmc = None, None, {}
+    tj = args.traffic_json
+    if not tj and args.workload == "c4" and not args.points:
+        tj = os.path.join(ROOT, "profiles", "pmc_traffic_latest.json")
+    if tj and os.path.exists(tj):
+        with open(tj) as fh:
+            pmc = json.load(fh)
+        traffic = pmc.get("k_cascade_bytes_per_launch")
+        tsrc = os.path.relpath(tj, ROOT)
     achieved = casc_bytes / casc_s / 1e9
     out = {
         "metric": METRIC,
@@ -155,16 +162,23 @@ def main():
         "data": "synthetic (deterministic scan grid; power-law source)",
         "config": {"workload": desc, "N_E": N, "N_z": Nz, "points_per_gpu": P, "lEmin": p0["lEmin"],
                    "lEmax": p0["lEmax"], "parallelism": "independent points, %d GPU(s), no collective" % world},
-        "roofline": {"bound": "hbm", "kernel": "k_cascade", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+        "roofline": {"bound": "hbm", "kernel": "k_cascade_reg", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": tsrc,
                      "algorithmic_bytes_per_launch": casc_bytes, "avg_launch_ms": casc_s * 1e3},
         "stage_ms_per_step": {"gamma_alphatilde": sum_ms[0] / max(ncalls, 1), "alpha": sum_ms[1] / max(ncalls, 1),
                               "cascade": sum_ms[2] / max(ncalls, 1)},
-        "alpha_table": {"kernel": "k_alpha", "bound": "fp64 VALU (transcendental)",
+        "alpha_table": {"kernel": "k_alpha_tile", "bound": "fp64 VALU (transcendental)",
                         "entries_per_s": scan.alpha_entries_per_point(N, Nz) * P / alpha_s,
-                        "avg_launch_ms": alpha_s * 1e3},
+                        "avg_step_ms": alpha_s * 1e3},
         "invalid_outputs": bad,
     }
+    fl = pmc.get("k_alpha_fp64_flops_per_step")
+    if fl:   # the dominant kernel: executed fp64 VALU flops (PMC counts) per second vs the fp64 vector peak
+        ach = fl / alpha_s / 1e12
+        out["roofline_dominant"] = {"bound": "valu", "kernel": "k_alpha_tile", "achieved": ach, "peak": FP64_PEAK_TFLOPS,
+                                    "unit": "TFLOP/s", "frac": ach / FP64_PEAK_TFLOPS,
+                                    "traffic": pmc.get("k_alpha_hbm_bytes_per_step"), "traffic_source": tsrc,
+                                    "flops": "executed fp64 VALU (SQ_INSTS_VALU_{ADD,MUL,TRANS}_F64 + 2 FMA) x 64 lanes"}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(pts, args.cpu_seconds)
     if rank == 0:

@@ -12,6 +12,22 @@ import numpy as np
 from . import _lib
 
 
+def params_array(points, grid_args=None):
+    """ctypes array of struct nusi_params; dict points may omit the grid keys
+    when grid_args = (N_bins_E, lEmin, lEmax, zmax) is given."""
+    arr = (_lib.NusiParams * len(points))()
+    for k, p in enumerate(points):
+        if isinstance(p, _lib.NusiParams):
+            arr[k] = p
+        else:
+            q = dict(p)
+            if grid_args is not None:
+                for key, v in zip(("N_bins_E", "lEmin", "lEmax", "zmax"), grid_args):
+                    q.setdefault(key, v)
+            arr[k] = _lib.make_params(**q)
+    return arr
+
+
 class Plan:
     def __init__(self, N_bins_E=300, lEmin=12.0, lEmax=17.0, zmax=5.0, max_points=1, device=0):
         L = _lib.load()
@@ -47,19 +63,7 @@ class Plan:
 
     def params_array(self, points):
         """points: sequence of dicts (calculate_flux keyword arguments) or NusiParams."""
-        arr = (_lib.NusiParams * len(points))()
-        N, lo, hi, zmax = self.grid_args
-        for k, p in enumerate(points):
-            if isinstance(p, _lib.NusiParams):
-                arr[k] = p
-            else:
-                q = dict(p)
-                q.setdefault("N_bins_E", N)
-                q.setdefault("lEmin", lo)
-                q.setdefault("lEmax", hi)
-                q.setdefault("zmax", zmax)
-                arr[k] = _lib.make_params(**q)
-        return arr
+        return params_array(points, self.grid_args)
 
     def evolve(self, points):
         """Evolve on the GPU; returns host arrays flux, flux_fla of shape (n, 3, N)."""

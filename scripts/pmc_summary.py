@@ -1,0 +1,67 @@
+"""Per-launch HBM traffic from rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes.
+
+FETCH_SIZE is scaled by the calibration factor measured in the same session
+(scripts/calib/pmc_calib streams 2 GiB with 8-B/lane loads, the width of the
+cascade's alpha-column loads): factor = bytes read / (FETCH_SIZE KB * 1024).
+MI355X_MICROARCH.md (HBM) documents factor 2 for 16-B/lane loads on gfx950.
+
+fp64 VALU work per launch (for the table kernel's VALU roofline) comes from an
+optional fourth pass with SQ_INSTS_VALU_{ADD,MUL,FMA,TRANS}_F64: per-wave
+instruction counts, x 64 lanes, FMA counted as 2 flops.
+
+  python scripts/pmc_summary.py <fetch_dir> <write_dir> <calib_dir> [<valu_dir>] > traffic.json
+"""
+import csv
+import glob
+import json
+import sys
+from collections import defaultdict
+
+
+def per_kernel(d, counter):
+    vals = defaultdict(list)
+    for f in glob.glob(d + "/**/*counter_collection.csv", recursive=True):
+        for row in csv.DictReader(open(f)):
+            if row["Counter_Name"] == counter:
+                vals[row["Kernel_Name"]].append(float(row["Counter_Value"]))
+    return vals
+
+
+def main():
+    fetch_dir, write_dir, calib_dir = sys.argv[1:4]
+    calib_bytes = 2 << 30
+    cal = per_kernel(calib_dir, "FETCH_SIZE")
+    f64 = [v for k, v in cal.items() if "k_stream_b64" in k][0][0] * 1024.0
+    f128 = [v for k, v in cal.items() if "k_stream_b128" in k][0][0] * 1024.0
+    fac64, fac128 = calib_bytes / f64, calib_bytes / f128
+    fetch, write = per_kernel(fetch_dir, "FETCH_SIZE"), per_kernel(write_dir, "WRITE_SIZE")
+    out = {"calibration": {"bytes": calib_bytes, "fetch_factor_b64": fac64, "fetch_factor_b128": fac128}, "kernels": {}}
+    for k in sorted(set(fetch) | set(write)):
+        if "nusi::" not in k:
+            continue
+        fk = sum(fetch.get(k, [0])) / max(len(fetch.get(k, [])), 1)
+        wk = sum(write.get(k, [0])) / max(len(write.get(k, [])), 1)
+        out["kernels"][k] = {"FETCH_SIZE_KB_mean": fk, "WRITE_SIZE_KB_mean": wk, "launches": len(fetch.get(k, [])),
+                             "hbm_bytes_per_launch": fk * 1024.0 * fac64 + wk * 1024.0}
+    if len(sys.argv) > 4:
+        ctr = {c: per_kernel(sys.argv[4], c) for c in
+               ["SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_TRANS_F64"]}
+        for k, rec in out["kernels"].items():
+            mean = {c: (sum(v[k]) / len(v[k]) if v.get(k) else 0.0) for c, v in ctr.items()}
+            rec["valu_f64_insts_per_launch"] = mean
+            rec["fp64_flops_per_launch"] = 64.0 * (mean["SQ_INSTS_VALU_ADD_F64"] + mean["SQ_INSTS_VALU_MUL_F64"]
+                                                    + 2.0 * mean["SQ_INSTS_VALU_FMA_F64"]
+                                                    + mean["SQ_INSTS_VALU_TRANS_F64"])
+    casc = [v for k, v in out["kernels"].items() if "k_cascade" in k]
+    if casc:
+        out["k_cascade_bytes_per_launch"] = casc[0]["hbm_bytes_per_launch"]
+    alpha = [v for k, v in out["kernels"].items() if "k_alpha" in k]
+    if alpha and "fp64_flops_per_launch" in alpha[0]:
+        # one table build = every k_alpha_tile launch of a step (three tile classes)
+        out["k_alpha_fp64_flops_per_step"] = sum(v["fp64_flops_per_launch"] for v in alpha)
+        out["k_alpha_hbm_bytes_per_step"] = sum(v["hbm_bytes_per_launch"] for v in alpha)
+    json.dump(out, sys.stdout, indent=1)
+
+
+if __name__ == "__main__":
+    main()
