@@ -19,12 +19,24 @@ from collections import defaultdict
 
 
 def per_kernel(d, counter):
+    """{kernel name: [value per dispatch]}"""
     vals = defaultdict(list)
     for f in glob.glob(d + "/**/*counter_collection.csv", recursive=True):
         for row in csv.DictReader(open(f)):
             if row["Counter_Name"] == counter:
                 vals[row["Kernel_Name"]].append(float(row["Counter_Value"]))
     return vals
+
+
+def per_step(d, counter, name_part):
+    """Sum over one step's launches of a kernel: dispatches are grouped by grid size (the
+    alpha table is three launches of different grids per step); each group's mean is summed."""
+    groups = defaultdict(list)
+    for f in glob.glob(d + "/**/*counter_collection.csv", recursive=True):
+        for row in csv.DictReader(open(f)):
+            if row["Counter_Name"] == counter and name_part in row["Kernel_Name"]:
+                groups[row["Grid_Size"]].append(float(row["Counter_Value"]))
+    return sum(sum(v) / len(v) for v in groups.values()), len(groups)
 
 
 def main():
@@ -55,11 +67,17 @@ def main():
     casc = [v for k, v in out["kernels"].items() if "k_cascade" in k]
     if casc:
         out["k_cascade_bytes_per_launch"] = casc[0]["hbm_bytes_per_launch"]
-    alpha = [v for k, v in out["kernels"].items() if "k_alpha" in k]
-    if alpha and "fp64_flops_per_launch" in alpha[0]:
-        # one table build = every k_alpha_tile launch of a step (three tile classes)
-        out["k_alpha_fp64_flops_per_step"] = sum(v["fp64_flops_per_launch"] for v in alpha)
-        out["k_alpha_hbm_bytes_per_step"] = sum(v["hbm_bytes_per_launch"] for v in alpha)
+    fk, ng = per_step(fetch_dir, "FETCH_SIZE", "k_alpha_tile")
+    wk, _ = per_step(write_dir, "WRITE_SIZE", "k_alpha_tile")
+    if ng:
+        out["k_alpha_launches_per_step"] = ng
+        out["k_alpha_hbm_bytes_per_step"] = fk * 1024.0 * fac64 + wk * 1024.0
+        if len(sys.argv) > 4:
+            add = per_step(sys.argv[4], "SQ_INSTS_VALU_ADD_F64", "k_alpha_tile")[0]
+            mul = per_step(sys.argv[4], "SQ_INSTS_VALU_MUL_F64", "k_alpha_tile")[0]
+            fma = per_step(sys.argv[4], "SQ_INSTS_VALU_FMA_F64", "k_alpha_tile")[0]
+            trn = per_step(sys.argv[4], "SQ_INSTS_VALU_TRANS_F64", "k_alpha_tile")[0]
+            out["k_alpha_fp64_flops_per_step"] = 64.0 * (add + mul + 2.0 * fma + trn)
     json.dump(out, sys.stdout, indent=1)
 
 
