@@ -195,30 +195,38 @@ __device__ __forceinline__ double rl(double v, int l)
     return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
 
+// alpha(b', bn) for b' = lane + 64 q < bn (column r = bn + i - 1 of the packed transposed table),
+// slots q <= qmax.  The loads are unconditional -- a masked (exec-branched) load would break the
+// compiler's vmcnt bookkeeping and force a full drain every bin.  Slots q <= qmax - 2 lie entirely
+// below bn (bn >= 64 qmax - D) and need no clamp; the top two slots clamp the row index into the
+// column.  Lanes past the column read a valid neighbour that every consumer masks out.
 template <int NQ>
 __device__ __forceinline__ void load_col(double (&dst)[NQ], const double* __restrict__ Al, int bn, int i, int N,
                                          int lane, int qmax)
 {
-    // alpha(b', bn) for b' = lane + 64 q < bn  (column r = bn + i - 1 of the packed transposed table).
-    // The loads are unconditional (addresses clamped into column r, bins clamped into [1, N-1]) so
-    // that no exec-masked branch breaks the compiler's vmcnt bookkeeping: a masked load would force
-    // a full vmcnt(0) drain every bin and defeat the prefetch.  Lanes past the column read a valid
-    // neighbour; every consumer masks by b' < b - 1 (or reads lane b - 1), so those values are unused.
     const int bc = bn < 1 ? 1 : (bn > N - 1 ? N - 1 : bn);
     const int r = bc + i - 1;
     const double* col = Al + (size_t)r * (r - 1) / 2 + (i - 1);
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
+        if (q > qmax) continue;                // qmax is a compile-time constant after unrolling
         const int bp = lane + 64 * q;
-        if (q <= qmax) dst[q] = col[bp < bc ? bp : bc - 1];   // qmax is a compile-time constant after unrolling
+        dst[q] = (q <= qmax - 2) ? col[bp] : col[bp < bc ? bp : bc - 1];
     }
 }
+
+// per-bin record of the current 64-bin chunk in LDS, read by every lane with broadcast
+// ds_read_b128s: the 14 flux-independent fields, the LU permutation, and the bin's flux
+// of the previous step (which the chain needs once, so it is staged with the fields)
+constexpr int kRec = 18;   // doubles per record: PR_* (14), perm, F0, F1, F2
+enum { RC_PERM = kPreFields, RC_F0, RC_F1, RC_F2 };
 
 template <int NQ, int D>
 __global__ __launch_bounds__(64) void k_cascade_reg(GridDev g, const Point* __restrict__ pts, TablesDev t,
                                                     double* __restrict__ flux, double* __restrict__ flux_fla)
 {
     extern __shared__ __attribute__((aligned(16))) double sdiag[];   // resonant-only: alpha(b+i-1, b+i)
+    __shared__ __attribute__((aligned(16))) double rec[64 * kRec];
     const int N = g.N, Nz = g.Nz, T = g.T;
     const int p = blockIdx.x, lane = threadIdx.x;
     const Point& P = pts[p];
@@ -238,7 +246,6 @@ __global__ __launch_bounds__(64) void k_cascade_reg(GridDev g, const Point* __re
         if (!nonres) {
             __syncthreads();
             for (int b = lane; b < N - 1; b += 64) sdiag[b] = Al[(size_t)(b + i) * (b + i - 1) / 2 + (b + i - 1)];
-            __syncthreads();
         }
         double acc[NQ];
 #pragma unroll
@@ -251,11 +258,10 @@ __global__ __launch_bounds__(64) void k_cascade_reg(GridDev g, const Point* __re
 #pragma unroll
         for (int qc = NQ - 1; qc >= 0; --qc) {
             const int base = 64 * qc;
-            // ---- flux-independent fields of bin base + lane (one bin per lane)
-            double pr[kPreFields];
-            int pmv = 0;
-            {
+            __syncthreads();   // previous chunk's records consumed
+            {   // ---- flux-independent fields of bin base + lane (one bin per lane) -> LDS record
                 const int b = base + lane;
+                double* R = rec + lane * kRec;
                 if (b < N) {
                     const double dEb = g.Emax[b] - g.Emin[b];
                     const double Gw = s * Gt[b + i - 1], Aw = s * At[b + i - 1];
@@ -265,61 +271,68 @@ __global__ __launch_bounds__(64) void k_cascade_reg(GridDev g, const Point* __re
                         for (int l = 0; l < 3; ++l) M[k][l] = (k == l) ? 1.0 : (Aw * uk[k] * uk[l] / dEb) / Zd[k];
                     int pm[3];
                     lu3_factor(M, pm);
-                    pr[PR_RZ0] = 1.0 / Zd[0];
-                    pr[PR_RZ1] = 1.0 / Zd[1];
-                    pr[PR_RZ2] = 1.0 / Zd[2];
-                    pr[PR_SRC] = c * lum(P, zi, sfri, g.Emin[b], g.Emax[b]);
-                    pr[PR_L10] = M[1][0];
-                    pr[PR_L20] = M[2][0];
-                    pr[PR_L21] = M[2][1];
-                    pr[PR_U01] = M[0][1];
-                    pr[PR_U02] = M[0][2];
-                    pr[PR_U12] = M[1][2];
-                    pr[PR_RU00] = 1.0 / M[0][0];
-                    pr[PR_RU11] = 1.0 / M[1][1];
-                    pr[PR_RU22] = 1.0 / M[2][2];
-                    pr[PR_SDE] = nonres ? s / dEb : dEb;
-                    pmv = pm[0] | (pm[1] << 2) | (pm[2] << 4);
-                } else {
-#pragma unroll
-                    for (int f = 0; f < kPreFields; ++f) pr[f] = 0.0;
+                    R[PR_RZ0] = 1.0 / Zd[0];
+                    R[PR_RZ1] = 1.0 / Zd[1];
+                    R[PR_RZ2] = 1.0 / Zd[2];
+                    R[PR_SRC] = c * lum(P, zi, sfri, g.Emin[b], g.Emax[b]);
+                    R[PR_L10] = M[1][0];
+                    R[PR_L20] = M[2][0];
+                    R[PR_L21] = M[2][1];
+                    R[PR_U01] = M[0][1];
+                    R[PR_U02] = M[0][2];
+                    R[PR_U12] = M[1][2];
+                    R[PR_RU00] = 1.0 / M[0][0];
+                    R[PR_RU11] = 1.0 / M[1][1];
+                    R[PR_RU22] = 1.0 / M[2][2];
+                    R[PR_SDE] = nonres ? s / dEb : dEb;
+                    R[RC_PERM] = (double)(pm[0] | (pm[1] << 2) | (pm[2] << 4));
+                    R[RC_F0] = F0[qc];
+                    R[RC_F1] = F1[qc];
+                    R[RC_F2] = F2[qc];
                 }
             }
+            __syncthreads();
             for (int gq = 0; gq < 64 / D; ++gq) {
 #pragma unroll
                 for (int j = 0; j < D; ++j) {
                     const int l = 63 - (gq * D + j);
                     const int b = base + l;
                     if (b <= N - 1) {
+                        const double2* R2 = reinterpret_cast<const double2*>(rec + l * kRec);
+                        const double2 r01 = R2[0], r23 = R2[1], r45 = R2[2], r67 = R2[3], r89 = R2[4], r1011 = R2[5],
+                                      r1213 = R2[6], r1415 = R2[7], r1617 = R2[8];
+                        const double rz0 = r01.x, rz1 = r01.y, rz2 = r23.x, src0 = r23.y;
+                        const double l10 = r45.x, l20 = r45.y, l21 = r67.x, u01 = r67.y, u02 = r89.x, u12 = r89.y;
+                        const double ru00 = r1011.x, ru11 = r1011.y, ru22 = r1213.x, sde = r1213.y;
+                        const int pmb = (int)r1415.x;
+                        const double f0 = r1415.y, f1 = r1617.x, f2 = r1617.y;
                         double add;
                         if (nonres) {
                             add = c * next_acc;
                         } else {
                             if (b != N - 1) {
                                 const double Sres = u0 * px0 + u1 * px1 + u2 * px2;
-                                racc += Sres * (s * sdiag[b]) / (g.Emax[b + 1] - g.Emin[b + 1]) / rl(pr[PR_SDE], l);
+                                racc += Sres * (s * sdiag[b]) / (g.Emax[b + 1] - g.Emin[b + 1]) / sde;
                             }
-                            add = c * racc * rl(pr[PR_SDE], l);
+                            add = c * racc * sde;
                         }
-                        const double src0 = rl(pr[PR_SRC], l);
-                        const double v0 = (rl(F0[qc], l) + (src0 + u0 * add)) * rl(pr[PR_RZ0], l);
-                        const double v1 = (rl(F1[qc], l) + (src0 + u1 * add)) * rl(pr[PR_RZ1], l);
-                        const double v2 = (rl(F2[qc], l) + (src0 + u2 * add)) * rl(pr[PR_RZ2], l);
-                        const int pmb = __builtin_amdgcn_readlane(pmv, l);
+                        const double v0 = (f0 + (src0 + u0 * add)) * rz0;
+                        const double v1 = (f1 + (src0 + u1 * add)) * rz1;
+                        const double v2 = (f2 + (src0 + u2 * add)) * rz2;
                         const int p0 = pmb & 3, p1 = (pmb >> 2) & 3, p2 = (pmb >> 4) & 3;
                         double x0 = (p0 == 0) ? v0 : (p0 == 1) ? v1 : v2;
                         double x1 = (p1 == 0) ? v0 : (p1 == 1) ? v1 : v2;
                         double x2 = (p2 == 0) ? v0 : (p2 == 1) ? v1 : v2;
-                        x1 = x1 - rl(pr[PR_L10], l) * x0;
-                        x2 = x2 - rl(pr[PR_L20], l) * x0;
-                        x2 = x2 - rl(pr[PR_L21], l) * x1;
-                        x2 = x2 * rl(pr[PR_RU22], l);
-                        x1 = (x1 - rl(pr[PR_U12], l) * x2) * rl(pr[PR_RU11], l);
-                        x0 = (x0 - rl(pr[PR_U01], l) * x1 - rl(pr[PR_U02], l) * x2) * rl(pr[PR_RU00], l);
+                        x1 = x1 - l10 * x0;
+                        x2 = x2 - l20 * x0;
+                        x2 = x2 - l21 * x1;
+                        x2 = x2 * ru22;
+                        x1 = (x1 - u12 * x2) * ru11;
+                        x0 = (x0 - u01 * x1 - u02 * x2) * ru00;
                         if (lane == l) { F0[qc] = x0; F1[qc] = x1; F2[qc] = x2; }
                         px0 = x0; px1 = x1; px2 = x2;
                         if (nonres && b > 0) {
-                            const double Tb = (u0 * x0 + u1 * x1 + u2 * x2) * rl(pr[PR_SDE], l);
+                            const double Tb = (u0 * x0 + u1 * x1 + u2 * x2) * sde;
                             double accb, diag;
                             if (l > 0) {
                                 accb = rl(acc[qc], l - 1);
@@ -328,10 +341,14 @@ __global__ __launch_bounds__(64) void k_cascade_reg(GridDev g, const Point* __re
                                 accb = rl(acc[qc > 0 ? qc - 1 : 0], 63);
                                 diag = rl(ring[j][qc > 0 ? qc - 1 : 0], 63);
                             }
-                            next_acc = accb + diag * Tb;
+                            next_acc = fma(diag, Tb, accb);
+                            // push T_b into every lower bin b' < b - 1 (bin b - 1 is carried in next_acc):
+                            // slots below qc - 1 are entirely below b - 1; only the top two need a mask
 #pragma unroll
-                            for (int q = 0; q <= qc; ++q)
-                                if (lane + 64 * q < b - 1) acc[q] += ring[j][q] * Tb;
+                            for (int q = 0; q <= qc; ++q) {
+                                if (q <= qc - 2) acc[q] = fma(ring[j][q], Tb, acc[q]);
+                                else if (lane + 64 * q < b - 1) acc[q] = fma(ring[j][q], Tb, acc[q]);
+                            }
                         }
                     }
                     load_col<NQ>(ring[j], Al, b - D, i, N, lane, qc);

@@ -80,7 +80,13 @@ __host__ __device__ constexpr int alpha_tile_lds_doubles(int cs, int ct)
     return kCornerFields * cs * ct + 3 * (kTEdgeFields * ct + kSEdgeFields * cs + kMBinFields * kAlphaTile);   // = 3 alpha_tile_edge_stride
 }
 
-__global__ __launch_bounds__(kTileThreads) void k_alpha_tile(GridDev g, const Point* __restrict__ pts, SplineSet spl,
+// 3 waves per SIMD (<= 168 VGPRs): measured 38.5 ms vs 42.0 (2 waves, 222 VGPRs) and 42.4 (4 waves,
+// spills) per 1024-point table build (profiles/r1e/ab3_*.log); override with -DNUSI_TILE_WAVES=n
+#ifndef NUSI_TILE_WAVES
+#define NUSI_TILE_WAVES 3
+#endif
+#define NUSI_TILE_ATTR __attribute__((amdgpu_waves_per_eu(NUSI_TILE_WAVES, NUSI_TILE_WAVES)))
+__global__ __launch_bounds__(kTileThreads) NUSI_TILE_ATTR void k_alpha_tile(GridDev g, const Point* __restrict__ pts, SplineSet spl,
                                                            const int* __restrict__ tiles, int cs_max, int ct_max,
                                                            double* __restrict__ A, int* __restrict__ warn)
 {
@@ -113,9 +119,15 @@ __global__ __launch_bounds__(kTileThreads) void k_alpha_tile(GridDev g, const Po
     int w = 0;
     for (int k = 0; k < 3; ++k) {
         __syncthreads();   // edge leaves written / previous k's corners consumed
+#ifndef NUSI_AB_NO_CORNERS   // timing experiments only (scripts/build_variant.sh)
         if (nonres && maj)
             for (int j = tid; j < cc; j += kTileThreads) alpha_tile_corner_job(P, k, j, tE, ct, sE, cc, cor);
+#endif
         __syncthreads();
+#ifdef NUSI_AB_NO_COMBINE
+        if (needed) tot += cor[(tid * 7) % cc] + edg[tid % 64];
+        else
+#endif
         if (needed) {
             const TileLeaves lv = alpha_tile_leaves(cor, edg, k, cs, ct, lm, sl, sh, tl, th, ln);
             alpha_k(P, spl, k, g.lo[n], g.hi[n], g.lo[m], g.hi[m], lv, tot, w);

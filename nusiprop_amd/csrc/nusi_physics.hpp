@@ -111,7 +111,7 @@ NUSI_FN double Fkernel(int kind, double y, double x)
     return 2 * y * (-y - x) / (x * x) / ((y - 1) * (-y - x - 1));
 }
 // y in [tp,tm], x in [-y,-tp] (nuSIprop.hpp:987-1003)
-NUSI_FN double gl33_tri(int kind, double tp, double tm)
+NUSI_FN_OUT double gl33_tri(int kind, double tp, double tm)   // cold: fallback only
 {
     double acc = 0;
 #pragma unroll
@@ -127,7 +127,7 @@ NUSI_FN double gl33_tri(int kind, double tp, double tm)
     return acc;
 }
 // y in [tp,tm], x in [Sm,Sp] (nuSIprop.hpp:1288-1301)
-NUSI_FN double gl33_rect(int kind, double tp, double tm, double Sm, double Sp)
+NUSI_FN_OUT double gl33_rect(int kind, double tp, double tm, double Sm, double Sp)   // cold: fallback only
 {
     double acc = 0;
 #pragma unroll
@@ -594,6 +594,54 @@ NUSI_FN TileLeaves alpha_tile_leaves(const double* cor, const double* edg, int k
     return lv;
 }
 
+// phi-phi double-scalar production term of alpha (nuSIprop.hpp:1477-1503); out of line: only
+// the phiphi configuration reaches it, and inlined it would cost every entry registers
+NUSI_FN_OUT double alpha_phiphi(const Point& P, const SplineSet& spl, double uk, double Sm, double Sp, double tm,
+                                double tp, double lSm, double lSp, int& warn)
+{
+    const double g = P.g, mphi = P.mphi;
+    const double g4 = (g * g) * (g * g), m4 = (mphi * mphi) * (mphi * mphi);
+    const bool maj = P.majorana;
+    double app = 0;
+    if (Sm < 1e4) {
+        const double d = Sp / Sm;
+        const double xx[3] = {Sm, nm::log(-Sm / tm) / nm::log(d) * 1.0001, nm::log10(d)};
+        double v = 0;
+        if (!spl.a.eval(xx, v)) warn |= kWarnSplineOOB;
+        app = g4 / m4 * fabs(v);
+    } else if (tm < -1) {
+        const double l1m = nm::log(-1 - tm), l0m = nm::log(-tm), l1p = nm::log(-1 - tp), l0p = nm::log(-tp);
+        app = g4 / m4 *
+              ((-Sm + Sp) * ((tm - tp) * (Sp * (-2 + tm + tp) + Sm * (-2 - 24 * Sp + tm + tp))
+                             + 4 * (-(Sp * (1 + tm)) + Sm * (-1 + 2 * Sp + (-1 + Sp) * tm)) * l1m
+                             + 2 * (3 * Sp + Sm * (3 + 4 * Sp)) * tm * l0m
+                             + 4 * (Sp + Sp * tp + Sm * (1 + tp - Sp * (2 + tp))) * l1p
+                             - 2 * (3 * Sp + Sm * (3 + 4 * Sp)) * tp * l0p)
+               + 2 * (Sm * Sm) * lSp * ((3 + 2 * Sp) * (tm - tp) + 2 * (Sp * Sp) * ((-1 - tm) * l1m + tm * l0m + (1 + tp) * l1p - tp * l0p))
+               + 2 * (Sp * Sp) * lSm * ((-3 - 2 * Sm) * (tm - tp) + 2 * (Sm * Sm) * ((1 + tm) * l1m - tm * l0m - (1 + tp) * l1p + tp * l0p)))
+              / (256. * kPi * (Sm * Sm) * (Sp * Sp));
+    } else if (tp < -1) {
+        const double l1p = nm::log(-1 - tp), l0p = nm::log(-tp);
+        app = g4 / m4 *
+              ((2 * (Sm * Sm) * lSp * ((1 + tp) * (-3 - 2 * Sp + 2 * (Sp * Sp) * l1p) - 2 * (Sp * Sp) * tp * l0p)
+                + (Sm - Sp) * ((1 + tp) * (-3 * (Sm + Sp + 8 * Sm * Sp) + (Sm + Sp) * tp)
+                               + 4 * (-(Sp * (1 + tp)) + Sm * (-1 + 2 * Sp + (-1 + Sp) * tp)) * l1p
+                               + 2 * (3 * Sp + Sm * (3 + 4 * Sp)) * tp * l0p)
+                + 2 * (Sp * Sp) * lSm * ((3 + 2 * Sm) * (1 + tp) + 2 * (Sm * Sm) * (-((1 + tp) * l1p) + tp * l0p)))
+                   / (256. * kPi * (Sm * Sm) * (Sp * Sp))
+               + (-1 - tm) * (-6 * Sm + 6 * Sp - 2 * (-2 + Sm) * Sp * lSm + Sm * Sp * (lSm * lSm) + 2 * Sm * (-2 + Sp) * lSp - Sm * Sp * (lSp * lSp))
+                     / (128. * kPi * Sm * Sp));
+    } else
+        app = g4 / m4 * (tp - tm) *
+              (-6 * Sm + 6 * Sp - 2 * (-2 + Sm) * Sp * lSm + Sm * Sp * (lSm * lSm) + 2 * Sm * (-2 + Sp) * lSp - Sm * Sp * (lSp * lSp))
+              / (128. * kPi * Sm * Sp);
+    app *= uk;
+    if (maj) app *= 2;
+    app *= 2;
+    if (maj) app *= 2;
+    return app;
+}
+
 // one mass state k of alpha(Em, Ep, Em', Ep'): tot += wgt * (every channel)
 template <class Lv>
 NUSI_FN void alpha_k(const Point& P, const SplineSet& spl, int k, double Em, double Ep, double Emp, double Epp,
@@ -712,45 +760,7 @@ NUSI_FN void alpha_k(const Point& P, const SplineSet& spl, int k, double Em, dou
     const double asu = maj ? ast : 0.;
     tot += wgt * asu;
 
-    double app = 0;
-    if (Sm > 4 && P.phiphi) {
-        if (Sm < 1e4) {
-            const double d = Sp / Sm;
-            const double xx[3] = {Sm, nm::log(-Sm / tm) / nm::log(d) * 1.0001, nm::log10(d)};
-            double v = 0;
-            if (!spl.a.eval(xx, v)) warn |= kWarnSplineOOB;
-            app = g4 / m4 * fabs(v);
-        } else if (tm < -1) {
-            const double l1m = nm::log(-1 - tm), l0m = nm::log(-tm), l1p = nm::log(-1 - tp), l0p = nm::log(-tp);
-            app = g4 / m4 *
-                  ((-Sm + Sp) * ((tm - tp) * (Sp * (-2 + tm + tp) + Sm * (-2 - 24 * Sp + tm + tp))
-                                 + 4 * (-(Sp * (1 + tm)) + Sm * (-1 + 2 * Sp + (-1 + Sp) * tm)) * l1m
-                                 + 2 * (3 * Sp + Sm * (3 + 4 * Sp)) * tm * l0m
-                                 + 4 * (Sp + Sp * tp + Sm * (1 + tp - Sp * (2 + tp))) * l1p
-                                 - 2 * (3 * Sp + Sm * (3 + 4 * Sp)) * tp * l0p)
-                   + 2 * (Sm * Sm) * lSp * ((3 + 2 * Sp) * (tm - tp) + 2 * (Sp * Sp) * ((-1 - tm) * l1m + tm * l0m + (1 + tp) * l1p - tp * l0p))
-                   + 2 * (Sp * Sp) * lSm * ((-3 - 2 * Sm) * (tm - tp) + 2 * (Sm * Sm) * ((1 + tm) * l1m - tm * l0m - (1 + tp) * l1p + tp * l0p)))
-                  / (256. * kPi * (Sm * Sm) * (Sp * Sp));
-        } else if (tp < -1) {
-            const double l1p = nm::log(-1 - tp), l0p = nm::log(-tp);
-            app = g4 / m4 *
-                  ((2 * (Sm * Sm) * lSp * ((1 + tp) * (-3 - 2 * Sp + 2 * (Sp * Sp) * l1p) - 2 * (Sp * Sp) * tp * l0p)
-                    + (Sm - Sp) * ((1 + tp) * (-3 * (Sm + Sp + 8 * Sm * Sp) + (Sm + Sp) * tp)
-                                   + 4 * (-(Sp * (1 + tp)) + Sm * (-1 + 2 * Sp + (-1 + Sp) * tp)) * l1p
-                                   + 2 * (3 * Sp + Sm * (3 + 4 * Sp)) * tp * l0p)
-                    + 2 * (Sp * Sp) * lSm * ((3 + 2 * Sm) * (1 + tp) + 2 * (Sm * Sm) * (-((1 + tp) * l1p) + tp * l0p)))
-                       / (256. * kPi * (Sm * Sm) * (Sp * Sp))
-                   + (-1 - tm) * (-6 * Sm + 6 * Sp - 2 * (-2 + Sm) * Sp * lSm + Sm * Sp * (lSm * lSm) + 2 * Sm * (-2 + Sp) * lSp - Sm * Sp * (lSp * lSp))
-                         / (128. * kPi * Sm * Sp));
-        } else
-            app = g4 / m4 * (tp - tm) *
-                  (-6 * Sm + 6 * Sp - 2 * (-2 + Sm) * Sp * lSm + Sm * Sp * (lSm * lSm) + 2 * Sm * (-2 + Sp) * lSp - Sm * Sp * (lSp * lSp))
-                  / (128. * kPi * Sm * Sp);
-        app *= uk;
-        if (maj) app *= 2;
-        app *= 2;
-        if (maj) app *= 2;
-    }
+    const double app = (Sm > 4 && P.phiphi) ? alpha_phiphi(P, spl, uk, Sm, Sp, tm, tp, lSm, lSp, warn) : 0.0;
     tot += wgt * app;
 
     const double nrm = (g / mphi) * (g / mphi) * ((g / mphi) * (g / mphi));
