@@ -105,8 +105,8 @@ class pyprop:  # noqa: N801  (name of the reference class)
         return E
 
     def check_energy_conservation(self):
-        """(E_int - E_FS)/E_FS (nuSIprop.pyx:140-144); calls evolve()."""
+        """(E_int - E_FS)/E_FS (nuSIprop.pyx:140-144).  Evolves the C++ object, but -- as in the
+        reference -- does not set the Python-side evolved flag."""
         out = ctypes.c_double()
-        self.evolved = True
         _lib.check(_lib.load().nusi_check_energy_conservation(self._h, ctypes.byref(out)))
         return out.value

@@ -1,0 +1,88 @@
+"""The drop-in Python surface: nusiprop_amd.pyprop against the behaviour of the
+reference's Cython class (nuSIprop.pyx:12-144) and the oracle's numbers."""
+import os
+import warnings
+
+import numpy as np
+import pytest
+
+from tests import cases
+
+pytestmark = pytest.mark.gpu
+
+
+def _kw(d):
+    """calculate_flux keywords; source_model is pyprop's extension keyword (DSNB by default)."""
+    return dict(d)
+
+
+@pytest.fixture(scope="module")
+def nusi():
+    import nusiprop_amd
+    return nusiprop_amd
+
+
+def test_not_evolved_returns_zeros_with_warning(nusi):
+    ev = nusi.pyprop(**_kw(cases.TEST_CPP))
+    with pytest.warns(UserWarning, match="not evolved"):
+        f = ev.get_flux()
+    assert f.shape == (3, 100) and not f.any()
+    with pytest.warns(UserWarning, match="not evolved"):
+        assert not ev.get_flux_fla().any()
+
+
+def test_evolve_set_parameters_cycle(nusi, oracle_mod):
+    ev = nusi.pyprop(**_kw(cases.TEST_CPP))
+    ev.evolve()
+    o = oracle_mod.Oracle(**cases.oracle_kwargs(cases.TEST_CPP))
+    f_ref, fla_ref = o.evolve()
+    assert cases.rel_err(ev.get_flux(), f_ref) <= 1e-12
+    assert cases.rel_err(ev.get_flux_fla(), fla_ref) <= 1e-12
+    ev.set_parameters(g=0.05, mphi=2e6)            # resets the evolved flag (nuSIprop.pyx:83)
+    with pytest.warns(UserWarning):
+        assert not ev.get_flux().any()
+    ev.evolve()
+    o2 = oracle_mod.Oracle(**cases.oracle_kwargs(dict(cases.TEST_CPP, g=0.05, mphi=2e6)))
+    _, fla2 = o2.evolve()
+    assert cases.rel_err(ev.get_flux_fla(), fla2) <= 1e-12
+
+
+def test_energies_and_interp(nusi, oracle_mod):
+    import scipy.interpolate as interp
+    ev = nusi.pyprop(**_kw(cases.C2B_100))
+    ev.evolve()
+    o = oracle_mod.Oracle(**cases.oracle_kwargs(cases.C2B_100))
+    _, _, Enu, _ = o.grid()
+    E = ev.get_energies()
+    assert np.array_equal(E, Enu)
+    q = np.geomspace(E[0] * 1.01, E[-1] * 0.99, 17)
+    fla = ev.get_flux_fla()
+    si = cases.C2B_100["si"]
+    for f, fn in enumerate([ev.interp_flux_el, ev.interp_flux_mu, ev.interp_flux_ta]):
+        want = interp.interp1d(np.log10(E), fla[f] * E ** si)(np.log10(q)) / q ** si
+        np.testing.assert_array_equal(fn(q), want)
+
+
+def test_check_energy_conservation_matches_oracle(nusi, oracle_mod):
+    """Same call sequence as the oracle, stale norm_total semantics included."""
+    ev = nusi.pyprop(**_kw(cases.C2B_100))
+    o = oracle_mod.Oracle(**cases.oracle_kwargs(cases.C2B_100))
+    ev.evolve()
+    o.evolve()
+    r, r_ref = ev.check_energy_conservation(), o.check_energy_conservation()
+    assert abs(r - r_ref) <= 1e-12 * abs(r_ref)
+    with pytest.warns(UserWarning):      # the Python evolved flag is untouched (as in the reference)
+        ev2 = nusi.pyprop(**_kw(cases.C2B_100))
+        ev2.check_energy_conservation()
+        ev2.get_flux()
+
+
+def test_default_phiphi_needs_tables(nusi, tmp_path, monkeypatch):
+    """pyprop's default phiphi=True loads xsec/*.bin; without them the reference exits
+    (interp.hpp:251-254); here NUSI_ETABLE is raised."""
+    monkeypatch.chdir(tmp_path)
+    monkeypatch.delenv("NUSI_XSEC_DIR", raising=False)
+    with pytest.raises(nusi.NusiError) as e:
+        nusi.pyprop(6e5, 0.01, 0.1, 2.5, N_bins_E=50)
+    assert e.value.code == nusi._lib.NUSI_ETABLE
+    assert "does not exist" in str(e.value)
