@@ -35,7 +35,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--workload", default="c4", choices=["c4", "c5", "c2"])
-    ap.add_argument("--points", type=int, default=0, help="points per GPU (default: 1024 for c4/c5, 1 for c2)")
+    ap.add_argument("--points", type=int, default=0, help="points per GPU (default: 1024 for c4, 8192 for c5, 1 for c2)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="budget of the oracle CPU baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-json", default="",
@@ -49,15 +49,17 @@ def rank_points(args, rank, world):
     if args.workload == "c2":
         pts = [dict(scan.BASE, mphi=6e5, g=0.01, si=2.5, norm=6.0)]
         return pts * max(1, args.points or 1), "C2b: single propagation, N_E=300, lE 12->17, power-law source, test.cpp physics"
-    P = args.points or 1024
     if args.workload == "c4":
+        P = args.points or 1024
         pts = scan.c4_points(si=2.5 + 0.05 * rank)
         desc = "C4: (m_phi 32 x g 32) scan per GPU, N_E=300, lE 12->17, power-law source, gamma=2.5+0.05*rank"
     else:
+        P = args.points or 8192
         allp = scan.c5_points()
-        lo, hi = scan.shard(len(allp), world, rank)
-        pts = allp[lo:hi]
-        desc = "C5: rank slice of the 65536-point (m_phi, g, gamma) scan, N_E=300, power-law source"
+        lo = (rank * P) % len(allp)
+        pts = (allp + allp)[lo:lo + P]
+        desc = ("C5: a %d-point block per GPU of the 65536-point (m_phi 64 x g 64 x gamma 16) scan, N_E=300, "
+                "power-law source; %d distinct tables per block (gamma batches share them)" % (P, P // 16))
     while len(pts) < P:
         pts = pts + pts
     return pts[:P], desc

@@ -10,6 +10,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <array>
 #include <map>
 #include <memory>
 #include <string>
@@ -350,6 +351,10 @@ struct nusi_plan {
     double* d_grid = nullptr;
     nusi::Point* d_pts = nullptr;
     nusi::Point* h_pts = nullptr;  // pinned
+    nusi::Point* d_tpts = nullptr;  // one representative per distinct table (table kernels)
+    nusi::Point* h_tpts = nullptr;  // pinned
+    std::vector<int> slot_of;       // table slot of each point of the last call
+    int last_ntab = 0;
     int* d_warn = nullptr;
     nusi::TablesDev tabs{};
     nusi::AlphaTilesDev atiles{};
@@ -368,6 +373,14 @@ struct nusi_plan {
 };
 
 namespace {
+
+// the Point fields the Stage-A kernels read (nusi_physics.hpp gamma/alphat/alpha_entry)
+using TableKey = std::array<double, 12>;
+TableKey table_key(const nusi::Point& P)
+{
+    return TableKey{P.mphi, P.g, P.Ga, P.mn[0], P.mn[1], P.mn[2], P.u[0], P.u[1], P.u[2],
+                    (double)P.majorana, (double)P.non_resonant, (double)P.phiphi};
+}
 
 int build_point(nusi_plan* pl, const nusi_params& p, nusi::Point& P)
 {
@@ -471,6 +484,8 @@ void nusi_plan_destroy(nusi_plan* pl)
     for (auto& e : pl->prof_ev) hipEventDestroy(e);
     hipFree(pl->d_grid);
     hipFree(pl->d_pts);
+    hipFree(pl->d_tpts);
+    if (pl->h_tpts) hipHostFree(pl->h_tpts);
     hipFree(pl->d_warn);
     hipFree(pl->tabs.G);
     hipFree(pl->tabs.At);
@@ -541,6 +556,8 @@ int nusi_plan_create(int device, int N_bins_E, double lEmin, double lEmax, doubl
     gd.sfr = q;
     HIPCHECK(hipMalloc(&pl->d_pts, sizeof(nusi::Point) * max_points));
     HIPCHECK(hipHostMalloc((void**)&pl->h_pts, sizeof(nusi::Point) * max_points, hipHostMallocDefault));
+    HIPCHECK(hipMalloc(&pl->d_tpts, sizeof(nusi::Point) * max_points));
+    HIPCHECK(hipHostMalloc((void**)&pl->h_tpts, sizeof(nusi::Point) * max_points, hipHostMallocDefault));
     HIPCHECK(hipMalloc(&pl->d_warn, sizeof(int) * max_points));
     HIPCHECK(hipMalloc(&pl->tabs.G, sizeof(double) * (size_t)G.T * max_points));
     HIPCHECK(hipMalloc(&pl->tabs.At, sizeof(double) * (size_t)G.T * max_points));
@@ -584,6 +601,23 @@ int nusi_plan_evolve(nusi_plan* pl, const nusi_params* pts, int n, double* d_flu
         const int r = build_point(pl, pts[i], pl->h_pts[i]);
         if (r) return r;
     }
+    // one Stage-A table per distinct (mphi, g, Gamma_phi, masses, |U|^2, flags): the tables do not
+    // depend on si, norm or the source (nuSIprop.hpp:217-253), so e.g. a gamma scan shares them
+    std::map<TableKey, int> slots;
+    pl->slot_of.resize(n);
+    int ntab = 0;
+    for (int i = 0; i < n; ++i) {
+        nusi::Point& P = pl->h_pts[i];
+        const TableKey key = table_key(P);
+        auto it = slots.find(key);
+        if (it == slots.end()) {
+            it = slots.emplace(key, ntab).first;
+            pl->h_tpts[ntab++] = P;
+        }
+        P.tslot = it->second;
+        pl->slot_of[i] = it->second;
+    }
+    for (int j = 0; j < ntab; ++j) pl->h_tpts[j].tslot = j;
     const size_t N3 = (size_t)3 * pl->grid.N;
     if (!d_flux || !d_fla) {
         if (!pl->d_scratch) HIPCHECK(hipMalloc(&pl->d_scratch, sizeof(double) * 2 * N3 * pl->max_points));
@@ -591,21 +625,23 @@ int nusi_plan_evolve(nusi_plan* pl, const nusi_params* pts, int n, double* d_flu
         if (!d_fla) d_fla = pl->d_scratch + N3 * pl->max_points;
     }
     HIPCHECK(hipMemcpyAsync(pl->d_pts, pl->h_pts, sizeof(nusi::Point) * n, hipMemcpyHostToDevice, s));
+    HIPCHECK(hipMemcpyAsync(pl->d_tpts, pl->h_tpts, sizeof(nusi::Point) * ntab, hipMemcpyHostToDevice, s));
     HIPCHECK(hipEventRecord(pl->ev_copy, s));
-    HIPCHECK(hipMemsetAsync(pl->d_warn, 0, sizeof(int) * n, s));
+    HIPCHECK(hipMemsetAsync(pl->d_warn, 0, sizeof(int) * ntab, s));
     const nusi::SplineSet spl = pl->spl ? pl->spl->set : nusi::SplineSet{};
     hipEvent_t* ev = pl->ev;
     if (pl->prof_n < pl->prof_max) ev = &pl->prof_ev[4 * (size_t)pl->prof_n++];
     HIPCHECK(hipEventRecord(ev[0], s));
-    HIPCHECK(nusi::launch_gamma_alphat(pl->gd, pl->d_pts, n, spl, pl->tabs, pl->d_warn, s));
+    HIPCHECK(nusi::launch_gamma_alphat(pl->gd, pl->d_tpts, ntab, spl, pl->tabs, pl->d_warn, s));
     HIPCHECK(hipEventRecord(ev[1], s));
-    HIPCHECK(nusi::launch_alpha(pl->gd, pl->d_pts, n, spl, pl->atiles, pl->tabs, pl->d_warn, s));
+    HIPCHECK(nusi::launch_alpha(pl->gd, pl->d_tpts, ntab, spl, pl->atiles, pl->tabs, pl->d_warn, s));
     HIPCHECK(hipEventRecord(ev[2], s));
     HIPCHECK(nusi::launch_cascade(pl->gd, pl->d_pts, n, pl->tabs, d_flux, d_fla, s));
     HIPCHECK(hipEventRecord(ev[3], s));
     pl->last_ev = ev;   // stage_ms / warnings / tables refer to the latest call
     pl->ran = true;
     pl->last_n = n;
+    pl->last_ntab = ntab;
     return NUSI_OK;
 }
 
@@ -657,7 +693,9 @@ int nusi_plan_warnings(nusi_plan* pl, int* out, int n)
     if (n > pl->last_n) n = pl->last_n;
     HIPCHECK(hipSetDevice(pl->device));
     HIPCHECK(hipEventSynchronize(pl->last_ev[3]));
-    HIPCHECK(hipMemcpy(out, pl->d_warn, sizeof(int) * n, hipMemcpyDeviceToHost));
+    std::vector<int> w(pl->last_ntab);
+    HIPCHECK(hipMemcpy(w.data(), pl->d_warn, sizeof(int) * w.size(), hipMemcpyDeviceToHost));
+    for (int i = 0; i < n; ++i) out[i] = w[pl->slot_of[i]];
     return NUSI_OK;
 }
 
@@ -667,10 +705,10 @@ int nusi_plan_tables(nusi_plan* pl, int i, double* G, double* At, double* A)
     if (i < 0 || i >= pl->last_n) return fail(NUSI_EPARAM, "point index out of range");
     HIPCHECK(hipSetDevice(pl->device));
     HIPCHECK(hipEventSynchronize(pl->last_ev[3]));
-    const size_t T = (size_t)pl->gd.T, PT = (size_t)pl->gd.PT;
-    if (G) HIPCHECK(hipMemcpy(G, pl->tabs.G + T * i, sizeof(double) * T, hipMemcpyDeviceToHost));
-    if (At) HIPCHECK(hipMemcpy(At, pl->tabs.At + T * i, sizeof(double) * T, hipMemcpyDeviceToHost));
-    if (A) HIPCHECK(hipMemcpy(A, pl->tabs.A + PT * i, sizeof(double) * PT, hipMemcpyDeviceToHost));
+    const size_t T = (size_t)pl->gd.T, PT = (size_t)pl->gd.PT, j = (size_t)pl->slot_of[i];
+    if (G) HIPCHECK(hipMemcpy(G, pl->tabs.G + T * j, sizeof(double) * T, hipMemcpyDeviceToHost));
+    if (At) HIPCHECK(hipMemcpy(At, pl->tabs.At + T * j, sizeof(double) * T, hipMemcpyDeviceToHost));
+    if (A) HIPCHECK(hipMemcpy(A, pl->tabs.A + PT * j, sizeof(double) * PT, hipMemcpyDeviceToHost));
     return NUSI_OK;
 }
 
@@ -681,9 +719,9 @@ int nusi_plan_evolve_host(nusi_plan* pl, const nusi_params* pts, int n, double* 
     const size_t N3 = (size_t)3 * pl->grid.N;
     HIPCHECK(hipStreamSynchronize(pl->stream));
     int bad = 0;
-    std::vector<int> w(n);
-    HIPCHECK(hipMemcpy(w.data(), pl->d_warn, sizeof(int) * n, hipMemcpyDeviceToHost));
-    for (int i = 0; i < n; ++i) bad |= (w[i] & nusi::kWarnSplineOOB);
+    std::vector<int> w(pl->last_ntab);
+    HIPCHECK(hipMemcpy(w.data(), pl->d_warn, sizeof(int) * w.size(), hipMemcpyDeviceToHost));
+    for (int v : w) bad |= (v & nusi::kWarnSplineOOB);
     if (bad) return fail(NUSI_EINTERP, "Error at interp: a phi-phi table lookup fell outside the node range");
     if (flux) HIPCHECK(hipMemcpy(flux, pl->d_scratch, sizeof(double) * N3 * n, hipMemcpyDeviceToHost));
     if (fla) HIPCHECK(hipMemcpy(fla, pl->d_scratch + N3 * pl->max_points, sizeof(double) * N3 * n, hipMemcpyDeviceToHost));

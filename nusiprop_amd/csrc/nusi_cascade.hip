@@ -70,9 +70,9 @@ __global__ __launch_bounds__(64) void k_cascade(GridDev g, const Point* __restri
     int* perm = (int*)(pre + kPreFields * 64);
     const double u0 = P.u[0], u1 = P.u[1], u2 = P.u[2];
     const double uk[3] = {u0, u1, u2};
-    const double* __restrict__ Gt = t.G + (size_t)p * T;
-    const double* __restrict__ At = t.At + (size_t)p * T;
-    const double* __restrict__ Al = t.A + (size_t)p * g.PT;
+    const double* __restrict__ Gt = t.G + (size_t)P.tslot * T;
+    const double* __restrict__ At = t.At + (size_t)P.tslot * T;
+    const double* __restrict__ Al = t.A + (size_t)P.tslot * g.PT;
     const bool nonres = P.non_resonant;
 
     for (int b = lane; b < N; b += 64) F0[b] = F1[b] = F2[b] = 0.0;
@@ -232,9 +232,9 @@ __global__ __launch_bounds__(64) void k_cascade_reg(GridDev g, const Point* __re
     const Point& P = pts[p];
     const double u0 = P.u[0], u1 = P.u[1], u2 = P.u[2];
     const double uk[3] = {u0, u1, u2};
-    const double* __restrict__ Gt = t.G + (size_t)p * T;
-    const double* __restrict__ At = t.At + (size_t)p * T;
-    const double* __restrict__ Al = t.A + (size_t)p * g.PT;
+    const double* __restrict__ Gt = t.G + (size_t)P.tslot * T;
+    const double* __restrict__ At = t.At + (size_t)P.tslot * T;
+    const double* __restrict__ Al = t.A + (size_t)P.tslot * g.PT;
     const bool nonres = P.non_resonant;
 
     double F0[NQ], F1[NQ], F2[NQ];

@@ -36,6 +36,8 @@ struct Point {
     double u[3];         // |U_flav,k|^2
     double U2[9];        // |U_fk|^2, row-major, for the flavour basis
     int majorana, non_resonant, phiphi, source;
+    int tslot;           // Stage-A table slot of this point (points that differ only in si / norm /
+                         // source share their tables: nuSIprop.hpp:217-253 read none of them)
 };
 
 enum { kWarnGamma = 1, kWarnAlphaTilde = 2, kWarnAlpha = 4, kWarnSplineOOB = 8 };

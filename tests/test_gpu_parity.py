@@ -132,3 +132,22 @@ def test_cascade_sizes(nusi, oracle_mod, N, nonres):
     f_ref, fla_ref = o.cascade(G, aT, nusi.unpack_alpha(A, plan.T))
     assert cases.rel_err(flux[0], f_ref) <= FLUX_RTOL
     assert cases.rel_err(fla[0], fla_ref) <= FLUX_RTOL
+
+
+def test_gamma_batches_share_tables(nusi, oracle_mod):
+    """Points that differ only in si / norm / source share one Stage-A table (the
+    tables do not read them, nuSIprop.hpp:217-253); each point's flux still equals
+    its own single-point evolve bit for bit, and the oracle's to 1e-12."""
+    base = [dict(cases.C2B_100, mphi=m, g=g) for m, g in ((6e5, 0.01), (2e6, 0.1))]
+    pts = [dict(b, si=s, norm=nm, source_model=src) for s, nm, src in ((2.0, 1.0, 1), (2.5, 6.0, 1), (3.0, 2.0, 0))
+           for b in base]
+    plan, flux, fla, tabs, _ = _gpu(nusi, pts)
+    for i in range(2, len(pts)):
+        for a, b in zip(tabs[i], tabs[i % 2]):
+            assert np.array_equal(a, b)
+    for i, p in enumerate(pts):
+        _, f1, fl1, _, _ = _gpu(nusi, [p])
+        assert np.array_equal(f1[0], flux[i]) and np.array_equal(fl1[0], fla[i])
+        o = oracle_mod.Oracle(**cases.oracle_kwargs(p))
+        _, fla_ref = o.evolve()
+        assert cases.rel_err(fla[i], fla_ref) <= FLUX_RTOL
