@@ -77,7 +77,7 @@ static_assert(kAlphaTile * kAlphaTile <= kTileThreads, "one entry per work-item"
 
 __host__ __device__ constexpr int alpha_tile_lds_doubles(int cs, int ct)
 {
-    return kCornerFields * cs * ct + 3 * (kTEdgeFields * ct + kSEdgeFields * cs + kMBinFields * kAlphaTile);   // = 3 alpha_tile_edge_stride
+    return alpha_tile_corner_block(cs, ct) + 3 * alpha_tile_edge_stride(cs, ct);
 }
 
 // 3 waves per SIMD (<= 168 VGPRs): measured 38.5 ms vs 42.0 (2 waves, 222 VGPRs) and 42.4 (4 waves,
@@ -112,7 +112,7 @@ __global__ __launch_bounds__(kTileThreads) NUSI_TILE_ATTR void k_alpha_tile(Grid
     const bool nonres = P.non_resonant, maj = P.majorana;
     const bool needed = valid && (nonres || m == n + 1);
     double* cor = sm;
-    double* edg = sm + kCornerFields * cc;
+    double* edg = sm + alpha_tile_corner_block(cs, ct);
     // ---- 2. edge and m-bin leaves, all k: 3 (ct + cs + kAlphaTile) <= 225 jobs, one round
     if (tid < 3 * (ct + cs + kAlphaTile)) alpha_tile_edge_job(P, tid, tE, ct, sE, cs, g.lo, g.hi, m0, T, edg);
     double tot = 0;
@@ -120,8 +120,11 @@ __global__ __launch_bounds__(kTileThreads) NUSI_TILE_ATTR void k_alpha_tile(Grid
     for (int k = 0; k < 3; ++k) {
         __syncthreads();   // edge leaves written / previous k's corners consumed
 #ifndef NUSI_AB_NO_CORNERS   // timing experiments only (scripts/build_variant.sh)
-        if (nonres && maj)
+        if (nonres && maj) {
             for (int j = tid; j < cc; j += kTileThreads) alpha_tile_corner_job(P, k, j, tE, ct, sE, cc, cor);
+            for (int j = tid; j < kAlphaTile * (cs + ct); j += kTileThreads)
+                alpha_tile_mixed_job(P, k, j, tE, ct, sE, cs, tl, th, sl, sh, n0, m0, T, cor);
+        }
 #endif
         __syncthreads();
 #ifdef NUSI_AB_NO_COMBINE

@@ -50,7 +50,7 @@ constexpr double Lg1 = 6.666666666666735130e-01, Lg2 = 3.999999999940941908e-01,
                  Lg7 = 1.479819860511658591e-01;
 
 // e_log.c
-NUSI_LM double log(double x)
+NUSI_FN double log_i(double x)
 {
     int hx = hiw(x);
     const unsigned lx = low(x);
@@ -100,7 +100,7 @@ NUSI_LM double log(double x)
 }
 
 // s_log1p.c
-NUSI_LM double log1p(double x)
+NUSI_FN double log1p_i(double x)
 {
     const int hx = hiw(x);
     const int ax = hx & 0x7fffffff;
@@ -165,7 +165,7 @@ NUSI_LM double log1p(double x)
 }
 
 // e_exp.c
-NUSI_LM double exp(double x)
+NUSI_FN double exp_i(double x)
 {
     constexpr double invln2 = 1.44269504088896338700e+00;
     constexpr double P1 = 1.66666666666666019037e-01, P2 = -2.77777777770155933842e-03,
@@ -210,7 +210,7 @@ NUSI_LM double exp(double x)
 }
 
 // s_atan.c
-NUSI_LM double atan(double x)
+NUSI_FN double atan_i(double x)
 {
     constexpr double atanhi[4] = {4.63647609000806093515e-01, 7.85398163397448278999e-01, 9.82793723247329054082e-01,
                                   1.57079632679489655800e+00};
@@ -231,24 +231,32 @@ NUSI_LM double atan(double x)
         if (ix < 0x3e200000) return x;           // |x| < 2^-29
         id = -1;
     } else {
+        // the four argument reductions share one division (same operands, same result bits as
+        // fdlibm's per-range divisions; one v_div sequence instead of four under divergence)
         x = fabs(x);
+        double num, den;
         if (ix < 0x3ff30000) {                   // |x| < 1.1875
             if (ix < 0x3fe60000) {               // 7/16 <= |x| < 11/16
                 id = 0;
-                x = (2.0 * x - 1.0) / (2.0 + x);
+                num = 2.0 * x - 1.0;
+                den = 2.0 + x;
             } else {                             // 11/16 <= |x| < 19/16
                 id = 1;
-                x = (x - 1.0) / (x + 1.0);
+                num = x - 1.0;
+                den = x + 1.0;
             }
         } else {
             if (ix < 0x40038000) {               // |x| < 2.4375
                 id = 2;
-                x = (x - 1.5) / (1.0 + 1.5 * x);
+                num = x - 1.5;
+                den = 1.0 + 1.5 * x;
             } else {                             // 2.4375 <= |x| < 2^66
                 id = 3;
-                x = -1.0 / x;
+                num = -1.0;
+                den = x;
             }
         }
+        x = num / den;
     }
     const double z = x * x;
     const double w = z * z;
@@ -260,7 +268,7 @@ NUSI_LM double atan(double x)
 }
 
 // e_atan2.c
-NUSI_LM double atan2(double y, double x)
+NUSI_FN double atan2_i(double y, double x)
 {
     constexpr double pi_o_2 = 1.5707963267948965580E+00, pi = 3.1415926535897931160E+00,
                      pi_lo = 1.2246467991473531772E-16, pi_o_4 = 7.8539816339744827900E-01;
@@ -269,7 +277,7 @@ NUSI_LM double atan2(double y, double x)
     const int ix = hx & 0x7fffffff, iy = hy & 0x7fffffff;
     if (((unsigned)ix | ((lx | (0u - lx)) >> 31)) > 0x7ff00000u || ((unsigned)iy | ((ly | (0u - ly)) >> 31)) > 0x7ff00000u)
         return x + y;                            // NaN
-    if (((hx - 0x3ff00000) | (int)lx) == 0) return atan(y);   // x = 1.0
+    if (((hx - 0x3ff00000) | (int)lx) == 0) return atan_i(y);   // x = 1.0
     const int m = ((hy >> 31) & 1) | ((hx >> 30) & 2);         // 2*sign(x)+sign(y)
     if ((iy | (int)ly) == 0) {                   // y = 0
         switch (m) {
@@ -301,7 +309,7 @@ NUSI_LM double atan2(double y, double x)
     double z;
     if (k > 60) z = pi_o_2 + 0.5 * pi_lo;        // |y/x| > 2^60
     else if (hx < 0 && k < -60) z = 0.0;         // |y|/x < -2^60
-    else z = atan(fabs(y / x));
+    else z = atan_i(fabs(y / x));
     switch (m) {
     case 0: return z;
     case 1: return -z;
@@ -309,6 +317,14 @@ NUSI_LM double atan2(double y, double x)
     default: return (z - pi_lo) - pi;
     }
 }
+
+// Out-of-line entry points (see NUSI_LM); the *_i bodies above are inlined where a caller wants
+// them inline (the polylogarithms, which are themselves out of line).
+NUSI_LM double log(double x) { return log_i(x); }
+NUSI_LM double log1p(double x) { return log1p_i(x); }
+NUSI_LM double exp(double x) { return exp_i(x); }
+NUSI_LM double atan(double x) { return atan_i(x); }
+NUSI_LM double atan2(double y, double x) { return atan2_i(y, x); }
 
 // e_atanh.c
 NUSI_FN double atanh(double x)

@@ -34,6 +34,18 @@
 #define NUSI_FN_OUT __host__ __device__ inline __attribute__((noinline))
 #endif
 
+// Inside the (out-of-line) polylogarithms the elementary functions are inlined: a call there
+// costs a register save/restore round trip per log (-DNUSI_POLY_CALL_LIBM: calls, A/B builds).
+#ifdef NUSI_POLY_CALL_LIBM
+#define NUSI_PLOG nm::log
+#define NUSI_PLOG1P nm::log1p
+#define NUSI_PATAN2 nm::atan2
+#else
+#define NUSI_PLOG nm::log_i
+#define NUSI_PLOG1P nm::log1p_i
+#define NUSI_PATAN2 nm::atan2_i
+#endif
+
 namespace nusi {
 
 constexpr double kPi = 3.14159265358979323846;
@@ -72,9 +84,11 @@ NUSI_FN cd operator/(cd a, cd b)
 NUSI_FN cd operator/(double s, cd b) { return C(s) / b; }
 NUSI_FN cd conj(cd a) { return cd{a.r, -a.i}; }
 NUSI_FN double carg(cd z) { return nm::atan2(z.i, z.r); }
+NUSI_FN double carg_i(cd z) { return nm::atan2_i(z.i, z.r); }
 NUSI_FN double carg_real(double x) { return nm::atan2(0.0, x); }  // carg of a real promoted to complex
 NUSI_FN double cabs(cd z) { return sqrt(z.r * z.r + z.i * z.i); }
 NUSI_FN cd clog(cd z) { return cd{0.5 * nm::log(z.r * z.r + z.i * z.i), carg(z)}; }
+NUSI_FN cd clog_p(cd z) { return cd{0.5 * NUSI_PLOG(z.r * z.r + z.i * z.i), NUSI_PATAN2(z.i, z.r)}; }   // clog, polylog-internal
 NUSI_FN cd clog_real(double x) { return clog(C(x, 0.0)); }   // clog of a promoted real
 NUSI_FN cd sqr(cd a) { return a * a; }
 constexpr cd kI = {0.0, 1.0};
@@ -96,47 +110,42 @@ NUSI_FN double li2_useries(double u)
 NUSI_FN_OUT double li2(double x)
 {
     double add = 0.0, sgn = 1.0;
-    if (x > 1.0) {
-        const double L = nm::log(x);
-        add = 2.0 * kZeta2 - 0.5 * L * L;
-        sgn = -1.0;
-        x = 1.0 / x;
-    } else if (x < -1.0) {
-        const double L = nm::log(-x);
-        add = -kZeta2 - 0.5 * L * L;
+    if (fabs(x) > 1.0) {   // x > 1: 2 zeta2 - log^2(x)/2 ; x < -1: -zeta2 - log^2(-x)/2 (one log for both)
+        const double L = NUSI_PLOG(fabs(x));
+        add = (x > 1.0 ? 2.0 * kZeta2 : -kZeta2) - 0.5 * L * L;
         sgn = -1.0;
         x = 1.0 / x;
     }
     if (x == 1.0) return add + sgn * kZeta2;
     if (x > 0.5) {
-        add += sgn * (kZeta2 - nm::log(x) * nm::log1p(-x));
+        add += sgn * (kZeta2 - NUSI_PLOG(x) * NUSI_PLOG1P(-x));
         sgn = -sgn;
         x = 1.0 - x;
     }
     if (x == 0.0) return add;
-    return add + sgn * li2_useries(-nm::log1p(-x));
+    return add + sgn * li2_useries(-NUSI_PLOG1P(-x));
 }
 
 // principal-branch Li2(x+iy); y == 0 follows gsl_sf_complex_dilog_xy_e
 NUSI_FN_OUT cd cli2(double x, double y)
 {
-    if (y == 0.0) return cd{li2(x), (x >= 1.0) ? -kPi * nm::log(x) : 0.0};
+    if (y == 0.0) return cd{li2(x), (x >= 1.0) ? -kPi * NUSI_PLOG(x) : 0.0};
     cd z = C(x, y), add = C(0.0);
     double sgn = 1.0;
     if (x * x + y * y > 1.0) {
-        const cd l = clog(-z);
+        const cd l = clog_p(-z);
         add = -kZeta2 - 0.5 * (l * l);
         sgn = -1.0;
         z = 1.0 / z;
     }
     if (z.r > 0.5) {
-        add = add + sgn * (kZeta2 - clog(z) * clog(1.0 - z));
+        add = add + sgn * (kZeta2 - clog_p(z) * clog_p(1.0 - z));
         sgn = -sgn;
         z = 1.0 - z;
     }
     // u = -log(1 - z), formed without the cancellation of 1 - z for small z
     const double a = -z.r, b = -z.i;
-    const cd u = C(-0.5 * nm::log1p(2.0 * a + (a * a + b * b)), -nm::atan2(b, 1.0 + a));
+    const cd u = C(-0.5 * NUSI_PLOG1P(2.0 * a + (a * a + b * b)), -NUSI_PATAN2(b, 1.0 + a));
     const cd u2 = u * u;
     cd p = C(kLi2Bern[kLi2Terms - 1]);
 #pragma unroll

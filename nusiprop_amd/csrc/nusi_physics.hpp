@@ -427,16 +427,26 @@ struct AlphaCorner {
     double Dcr, Dci;   // cli2((1+S+t)/(2 - i gr + t))
     double A;          // arg(-(-1 + i gr + S)/(2 - i gr + t))
 };
+// the corner leaves' own elementary functions: inline by default (-DNUSI_CORNER_CALL_LIBM: calls)
+#ifdef NUSI_CORNER_CALL_LIBM
+#define NUSI_CLOG nm::log
+#define NUSI_CLOG1P nm::log1p
+#define NUSI_CARG carg
+#else
+#define NUSI_CLOG nm::log_i
+#define NUSI_CLOG1P nm::log1p_i
+#define NUSI_CARG carg_i
+#endif
 NUSI_FN void alpha_corner(double S, double t, double gr, AlphaCorner& c)
 {
-    c.L = nm::log1p(S + t);
-    c.LL = nm::log(1 + S + t);
+    c.L = NUSI_CLOG1P(S + t);
+    c.LL = NUSI_CLOG(1 + S + t);
     if (t < -1) {
         c.TU1 = li2((1 + S + t) / S);
         c.TU2 = 0.0;
     } else {
         c.TU1 = li2(S / (1 + S + t));
-        c.TU2 = nm::log((1 + S + t) / S);
+        c.TU2 = NUSI_CLOG((1 + S + t) / S);
     }
     c.G = li2((1 + S + t) / (2 + S));
     const cd Dr = cli2((1 + S + t) / (1 + t), 0.0);
@@ -446,7 +456,7 @@ NUSI_FN void alpha_corner(double S, double t, double gr, AlphaCorner& c)
     c.Dri = Dr.i;
     c.Dcr = Dc.r;
     c.Dci = Dc.i;
-    c.A = carg(-(C(-1 + S, gr) / dt));
+    c.A = NUSI_CARG(-(C(-1 + S, gr) / dt));
 }
 // t-edge leaves
 struct AlphaTEdge { double Lm1, la, cm, L2, am; };
@@ -468,6 +478,10 @@ NUSI_FN void alpha_sedge(double S, double gr, double gr2, AlphaSEdge& e)
     e.cS = carg(C(-1 + S, gr));
     e.lS2 = nm::log(S / (2 + S));
 }
+// mixed leaves of the Majorana t channel (nuSIprop.hpp:1284): each of its four logarithms
+// depends on one S' edge and the n bin (xlog) or on the m bin and one t edge (ylog)
+NUSI_FN double alpha_xlog(double S, double tm, double tp) { return nm::log(((1 + S + tm) * (-1 + tp)) / ((-1 + tm) * (1 + S + tp))); }
+NUSI_FN double alpha_ylog(double Sm, double Sp, double t) { return nm::log((Sm * (1 + Sp + t)) / (Sp * (1 + Sm + t))); }
 // m-bin leaves
 struct AlphaMBin { double lr, lr2, atd; };
 NUSI_FN void alpha_mbin(double Sm, double Sp, double mphi, double Ga, AlphaMBin& b)
@@ -484,15 +498,17 @@ struct DirectLeaves {
     NUSI_FN AlphaTEdge tedge(int, double t) const { AlphaTEdge e; alpha_tedge(t, gr2, e); return e; }
     NUSI_FN AlphaSEdge sedge(int, double S) const { AlphaSEdge e; alpha_sedge(S, gr, gr2, e); return e; }
     NUSI_FN AlphaMBin mbin(double Sm, double Sp) const { AlphaMBin b; alpha_mbin(Sm, Sp, mphi, Ga, b); return b; }
+    NUSI_FN double xlog(int, double S, double tm, double tp) const { return alpha_xlog(S, tm, tp); }
+    NUSI_FN double ylog(int, double Sm, double Sp, double t) const { return alpha_ylog(Sm, Sp, t); }
 };
 
 // leaves read from a tile's precomputed arrays (structure of arrays):
 //   cor[v * cc + s * ct + t]  (v = field of AlphaCorner, cc = cs * ct), ted[v * ct + t],
-//   sed[v * cs + s], mbv[v * kAlphaTile + j]
+//   sed[v * cs + s], mbv[v * kAlphaTile + j], xl[s * kAlphaTile + n bin], yl[m bin * ct + t]
 constexpr int kAlphaTile = 15;
 struct TileLeaves {
-    const double *cor, *ted, *sed, *mbv;
-    int cc, ct, cs, mb;
+    const double *cor, *ted, *sed, *mbv, *xl, *yl;
+    int cc, ct, cs, mb, nb;
     int sidx[2], tidx[2];   // slots of (Sm, Sp) and (tm, tp)
     NUSI_FN AlphaCorner corner(int si, int ti, double, double) const
     {
@@ -513,8 +529,12 @@ struct TileLeaves {
     {
         return AlphaMBin{mbv[mb], mbv[kAlphaTile + mb], mbv[2 * kAlphaTile + mb]};
     }
+    NUSI_FN double xlog(int si, double, double, double) const { return xl[sidx[si] * kAlphaTile + nb]; }
+    NUSI_FN double ylog(int ti, double, double, double) const { return yl[mb * ct + tidx[ti]]; }
 };
 constexpr int kCornerFields = 10, kTEdgeFields = 5, kSEdgeFields = 5, kMBinFields = 3;
+// per-k leaf block of the corner phase: corners, then xlog [cs][kAlphaTile], then ylog [kAlphaTile][ct]
+NUSI_FN int alpha_tile_corner_block(int cs, int ct) { return kCornerFields * cs * ct + kAlphaTile * (cs + ct); }
 
 // Unique edge energies of bins b0 .. b0+kAlphaTile-1 (< T): E[0..count), il/ih = slot of each bin's
 // lower/upper edge.  Bins of the first N share edges bitwise (Emax[n] == Emin[n+1], same pow()
@@ -576,6 +596,25 @@ NUSI_FN void alpha_tile_corner_job(const Point& P, int k, int j, const double* t
     cor[j] = c.L; cor[cc + j] = c.LL; cor[2 * cc + j] = c.TU1; cor[3 * cc + j] = c.TU2; cor[4 * cc + j] = c.G;
     cor[5 * cc + j] = c.Drr; cor[6 * cc + j] = c.Dri; cor[7 * cc + j] = c.Dcr; cor[8 * cc + j] = c.Dci; cor[9 * cc + j] = c.A;
 }
+// job j in [0, kAlphaTile (cs + ct)): the xlog leaf (S' slot, n bin) or the ylog leaf (m bin, t slot)
+// of mass state k, into the block after the corners; bins past the table are skipped
+NUSI_FN void alpha_tile_mixed_job(const Point& P, int k, int j, const double* tE, int ct, const double* sE, int cs,
+                                  const int* tl, const int* th, const int* sl, const int* sh, int n0, int m0, int T,
+                                  double* cor)
+{
+    const double mphi = P.mphi, m2 = mphi * mphi, mk = P.mn[k];
+    double* xl = cor + kCornerFields * cs * ct;
+    double* yl = xl + kAlphaTile * cs;
+    if (j < kAlphaTile * cs) {
+        const int s = j / kAlphaTile, ln = j - s * kAlphaTile;
+        if (n0 + ln >= T) return;
+        xl[j] = alpha_xlog(alpha_S(mk, sE[s], m2), alpha_t(mk, tE[tl[ln]], m2), alpha_t(mk, tE[th[ln]], m2));
+    } else {
+        const int q = j - kAlphaTile * cs, lm = q / ct, t = q - lm * ct;
+        if (m0 + lm >= T) return;
+        yl[q] = alpha_ylog(alpha_S(mk, sE[sl[lm]], m2), alpha_S(mk, sE[sh[lm]], m2), alpha_t(mk, tE[t], m2));
+    }
+}
 // leaves of entry (n0 + ln, m0 + lm) of a tile for mass state k
 NUSI_FN TileLeaves alpha_tile_leaves(const double* cor, const double* edg, int k, int cs, int ct, int lm,
                                      const int* sl, const int* sh, const int* tl, const int* th, int ln)
@@ -586,6 +625,9 @@ NUSI_FN TileLeaves alpha_tile_leaves(const double* cor, const double* edg, int k
     lv.ct = ct;
     lv.cs = cs;
     lv.mb = lm;
+    lv.nb = ln;
+    lv.xl = cor + kCornerFields * lv.cc;
+    lv.yl = lv.xl + kAlphaTile * cs;
     lv.sidx[0] = sl[lm];
     lv.sidx[1] = sh[lm];
     lv.tidx[0] = tl[ln];
@@ -644,6 +686,12 @@ NUSI_FN_OUT double alpha_phiphi(const Point& P, const SplineSet& spl, double uk,
     return app;
 }
 
+// compiler fence between the phases of alpha_k (device: no scheduling or LDS-load reuse across it)
+#ifdef __HIP_DEVICE_COMPILE__
+#define NUSI_PHASE() do { __builtin_amdgcn_sched_barrier(0); __asm__ volatile("" ::: "memory"); } while (0)
+#else
+#define NUSI_PHASE() do { } while (0)
+#endif
 // one mass state k of alpha(Em, Ep, Em', Ep'): tot += wgt * (every channel)
 template <class Lv>
 NUSI_FN void alpha_k(const Point& P, const SplineSet& spl, int k, double Em, double Ep, double Emp, double Epp,
@@ -670,79 +718,101 @@ NUSI_FN void alpha_k(const Point& P, const SplineSet& spl, int k, double Em, dou
     tot += wgt * as;
     if (!P.non_resonant) return;
 
+    // The Majorana channels run as three phases (t/u, tu, st) that each fetch the leaves they use:
+    // NUSI_PHASE stops the compiler from keeping all ~60 leaves of the entry live at once (which
+    // spilled to scratch); the leaves and the expressions are unchanged.
     const AlphaTEdge eTm = lv.tedge(0, tm), eTp = lv.tedge(1, tp);
     const AlphaSEdge eSm = lv.sedge(0, Sm), eSp = lv.sedge(1, Sp);
     const double Lmt = eTm.Lm1, Lmp = eTp.Lm1;
     const double lSm = eSm.lS, lSp = eSp.lS;
     const double SS = Sm * Sp;
-    const double Lsm = eSm.Ls, Lsp = eSp.Ls;
     double at, au, atu = 0., ast;
     if (maj) {
-        const AlphaCorner cmm = lv.corner(0, 0, Sm, tm), cpm = lv.corner(1, 0, Sp, tm);
-        const AlphaCorner cmq = lv.corner(0, 1, Sm, tp), cpq = lv.corner(1, 1, Sp, tp);
-        const double Lmm = cmm.L, Lpm = cpm.L, Lmq = cmq.L, Lpq = cpq.L;
-        const double LA = nm::log(((1 + Sm + tm) * (-1 + tp)) / ((-1 + tm) * (1 + Sm + tp)));
-        const double LB = nm::log(((1 + Sp + tm) * (-1 + tp)) / ((-1 + tm) * (1 + Sp + tp)));
-        const double inner = SS * (-tm + tp) * lSm + SS * (tm - tp) * lSp - SS * Lmm - SS * tp * Lmm + SS * Lpm + SS * tp * Lpm
-                             - Sp * LA - Sp * tm * LA - Sp * tp * LA - Sp * tm * tp * LA
-                             + SS * cmq.LL + SS * tm * Lmq
-                             + Sm * LB + Sm * tm * LB + Sm * tp * LB + Sm * tm * tp * LB
-                             - SS * cpq.LL - SS * tm * Lpq;
-        at = g4 / (Sm * Sp * 16 * kPi * m4) *
-             (-((Sm - Sp) * (3 + 2 * tm * (-1 + tp) - 2 * tp) * (tm - tp)) / ((-1 + tm) * (-1 + tp))
-              + 2 * inner / ((1 + tm) * (1 + tp))
-              - ((SS * nm::log((Sm * (1 + Sp + tm)) / (Sp * (1 + Sm + tm)))) / ((1 + tm) * (1 + tm))
-                 + (((Sm - Sp) * (tm - tp) * (1 + tp)) / (1 + tm) - SS * nm::log((Sm * (1 + Sp + tp)) / (Sp * (1 + Sm + tp)))) / ((1 + tp) * (1 + tp))));
-        if (at < 0) at = gl33_rect(0, tp, tm, Sm, Sp) * (g4 / (16 * kPi * m4));
-        at *= uk;
-        tot += wgt * at;
-        au = at;
-        tot += wgt * au;
-
-        double Fp, Fm;
-        if (tp < -1) Fp = cmq.TU1 - cpq.TU1;
-        else {
-            const double a = cmq.TU2, b = cpq.TU2;
-            Fp = -cmq.TU1 + cpq.TU1 - 0.5 * (a * a - b * b);
+        {
+            const AlphaCorner cmm = lv.corner(0, 0, Sm, tm), cpm = lv.corner(1, 0, Sp, tm);
+            const AlphaCorner cmq = lv.corner(0, 1, Sm, tp), cpq = lv.corner(1, 1, Sp, tp);
+            const double Lmm = cmm.L, Lpm = cpm.L, Lmq = cmq.L, Lpq = cpq.L;
+            const double LA = lv.xlog(0, Sm, tm, tp), LB = lv.xlog(1, Sp, tm, tp);
+            const double inner = SS * (-tm + tp) * lSm + SS * (tm - tp) * lSp - SS * Lmm - SS * tp * Lmm + SS * Lpm + SS * tp * Lpm
+                                 - Sp * LA - Sp * tm * LA - Sp * tp * LA - Sp * tm * tp * LA
+                                 + SS * cmq.LL + SS * tm * Lmq
+                                 + Sm * LB + Sm * tm * LB + Sm * tp * LB + Sm * tm * tp * LB
+                                 - SS * cpq.LL - SS * tm * Lpq;
+            at = g4 / (Sm * Sp * 16 * kPi * m4) *
+                 (-((Sm - Sp) * (3 + 2 * tm * (-1 + tp) - 2 * tp) * (tm - tp)) / ((-1 + tm) * (-1 + tp))
+                  + 2 * inner / ((1 + tm) * (1 + tp))
+                  - ((SS * lv.ylog(0, Sm, Sp, tm)) / ((1 + tm) * (1 + tm))
+                     + (((Sm - Sp) * (tm - tp) * (1 + tp)) / (1 + tm) - SS * lv.ylog(1, Sm, Sp, tp)) / ((1 + tp) * (1 + tp))));
+            if (at < 0) at = gl33_rect(0, tp, tm, Sm, Sp) * (g4 / (16 * kPi * m4));
+            at *= uk;
+            tot += wgt * at;
+            au = at;
+            tot += wgt * au;
         }
-        if (tm < -1) Fm = -cmm.TU1 + cpm.TU1;
-        else {
-            const double a = cmm.TU2, b = cpm.TU2;
-            Fm = cmm.TU1 - cpm.TU1 + 0.5 * (a * a - b * b);
+        NUSI_PHASE();
+        {
+            const AlphaCorner cmm = lv.corner(0, 0, Sm, tm), cpm = lv.corner(1, 0, Sp, tm);
+            const AlphaCorner cmq = lv.corner(0, 1, Sm, tp), cpq = lv.corner(1, 1, Sp, tp);
+            const AlphaSEdge fSm = lv.sedge(0, Sm), fSp = lv.sedge(1, Sp);
+            const AlphaTEdge fTm = lv.tedge(0, tm), fTp = lv.tedge(1, tp);
+            const AlphaMBin mc = lv.mbin(Sm, Sp);
+            const double Lmm = cmm.L, Lpm = cpm.L, Lmq = cmq.L, Lpq = cpq.L;
+            double Fp, Fm;
+            if (tp < -1) Fp = cmq.TU1 - cpq.TU1;
+            else {
+                const double a = cmq.TU2, b = cpq.TU2;
+                Fp = -cmq.TU1 + cpq.TU1 - 0.5 * (a * a - b * b);
+            }
+            if (tm < -1) Fm = -cmm.TU1 + cpm.TU1;
+            else {
+                const double a = cmm.TU2, b = cpm.TU2;
+                Fm = cmm.TU1 - cpm.TU1 + 0.5 * (a * a - b * b);
+            }
+            const double lap = fTp.la, lam = fTm.la;
+            const double Pq = (1 + tm) * (1 + tp);
+            const double l2m = fSm.l2, l2p = fSp.l2;
+            const double SSP = SS * (1 + tm) * (1 + tp);
+            const double lSm = fSm.lS, lSp = fSp.lS, Lmt = fTm.Lm1, Lmp = fTp.Lm1;
+            atu = g4 / (32 * kPi * m4 * Sm * Sp * (1 + tm) * (1 + tp)) *
+                  (-4 * (Sm - Sp) * (1 + tm) * (tm - tp) * (1 + tp)
+                   + 2 * SS * tp * (mc.lr - Lmm + Lpm)
+                   + 2 * Sp * (1 + tm) * (1 + tp) * (Lmt - Lmm - Lmp + Lmq)
+                   - 2 * Sm * (1 + tm) * (1 + tp) * (Lmt - Lpm - Lmp + Lpq)
+                   + 2 * SS * (-Lmm + Lpm + Lmq - Lpq)
+                   + SSP * (l2m * (lSp + Lmq) - l2p * (lSm + Lpq) + Lmp * (mc.lr - Lmq + Lpq))
+                   + SSP * ((lSp + Lmm) * (fSm.lS2 + Lmt - lam) + (lSm + Lpm) * (l2p - Lmt + lam))
+                   + SS * (mc.lr2 + Lmq - Lpq) * (2 * tm + Pq * lap)
+                   + SSP * (cmm.G - cpm.G - cmq.G + cpq.G)
+                   + SSP * (Fp + Fm));
+            // nuSIprop.hpp:1401-1418: the fallback assigns a shadowing local; a negative alpha_tu stays.
+            atu *= uk;
+            tot += wgt * atu;
         }
-        const double lap = eTp.la, lam = eTm.la;
-        const double Pq = (1 + tm) * (1 + tp);
-        const double l2m = eSm.l2, l2p = eSp.l2;
-        const double SSP = SS * (1 + tm) * (1 + tp);
-        atu = g4 / (32 * kPi * m4 * Sm * Sp * (1 + tm) * (1 + tp)) *
-              (-4 * (Sm - Sp) * (1 + tm) * (tm - tp) * (1 + tp)
-               + 2 * SS * tp * (mb.lr - Lmm + Lpm)
-               + 2 * Sp * (1 + tm) * (1 + tp) * (Lmt - Lmm - Lmp + Lmq)
-               - 2 * Sm * (1 + tm) * (1 + tp) * (Lmt - Lpm - Lmp + Lpq)
-               + 2 * SS * (-Lmm + Lpm + Lmq - Lpq)
-               + SSP * (l2m * (lSp + Lmq) - l2p * (lSm + Lpq) + Lmp * (mb.lr - Lmq + Lpq))
-               + SSP * ((lSp + Lmm) * (eSm.lS2 + Lmt - lam) + (lSm + Lpm) * (l2p - Lmt + lam))
-               + SS * (mb.lr2 + Lmq - Lpq) * (2 * tm + Pq * lap)
-               + SSP * (cmm.G - cpm.G - cmq.G + cpq.G)
-               + SSP * (Fp + Fm));
-        // nuSIprop.hpp:1401-1418: the fallback assigns a shadowing local; a negative alpha_tu stays.
-        atu *= uk;
-        tot += wgt * atu;
-
-        // s-t interference: eight complex dilogarithms (nuSIprop.hpp:1431-1451)
-        const double cm = eTm.cm, cp = eTp.cm;
-        const double L2m = eTm.L2, L2p = eTp.L2;
-        const double am = eTm.am, ap = eTp.am;
-        ast = g4 / (32 * kPi * (1 + gr2) * m4) *
-              (2 * gr * (cmm.Dri - cmm.Dci - cpm.Dri + cpm.Dci - cmq.Dri + cmq.Dci + cpq.Dri - cpq.Dci)
-               - 2 * (cmm.Drr - cmm.Dcr - cpm.Drr + cpm.Dcr - cmq.Drr + cmq.Dcr + cpq.Drr - cpq.Dcr)
-               + 2 * gr * (cm - cmm.A) * Lmm
-               - 2 * gr * (cm - cpm.A) * Lpm
-               + 2 * gr * (cp - cpq.A) * Lpq
-               - 2 * gr * (cp - cmq.A) * Lmq
-               + 2 * (gr * eSm.cS - gr * eSp.cS + Lsp / 2. - Lsm / 2. + lSm - lSp) * (2 * (tm - tp) + (Lmt - Lmp))
-               + Lmm * (Lsm - L2m - 2 * (lSm - am)) - Lpm * (Lsp - L2m - 2 * (lSp - am))
-               - Lmq * (Lsm - L2p - 2 * (lSm - ap)) + Lpq * (Lsp - L2p - 2 * (lSp - ap)));
+        NUSI_PHASE();
+        {
+            // s-t interference: eight complex dilogarithms (nuSIprop.hpp:1431-1451)
+            const AlphaCorner cmm = lv.corner(0, 0, Sm, tm), cpm = lv.corner(1, 0, Sp, tm);
+            const AlphaCorner cmq = lv.corner(0, 1, Sm, tp), cpq = lv.corner(1, 1, Sp, tp);
+            const AlphaSEdge fSm = lv.sedge(0, Sm), fSp = lv.sedge(1, Sp);
+            const AlphaTEdge fTm = lv.tedge(0, tm), fTp = lv.tedge(1, tp);
+            const double Lmm = cmm.L, Lpm = cpm.L, Lmq = cmq.L, Lpq = cpq.L;
+            const double lSm = fSm.lS, lSp = fSp.lS, Lmt = fTm.Lm1, Lmp = fTp.Lm1;
+            const double Lsm = fSm.Ls, Lsp = fSp.Ls;
+            const double cm = fTm.cm, cp = fTp.cm;
+            const double L2m = fTm.L2, L2p = fTp.L2;
+            const double am = fTm.am, ap = fTp.am;
+            ast = g4 / (32 * kPi * (1 + gr2) * m4) *
+                  (2 * gr * (cmm.Dri - cmm.Dci - cpm.Dri + cpm.Dci - cmq.Dri + cmq.Dci + cpq.Dri - cpq.Dci)
+                   - 2 * (cmm.Drr - cmm.Dcr - cpm.Drr + cpm.Dcr - cmq.Drr + cmq.Dcr + cpq.Drr - cpq.Dcr)
+                   + 2 * gr * (cm - cmm.A) * Lmm
+                   - 2 * gr * (cm - cpm.A) * Lpm
+                   + 2 * gr * (cp - cpq.A) * Lpq
+                   - 2 * gr * (cp - cmq.A) * Lmq
+                   + 2 * (gr * fSm.cS - gr * fSp.cS + Lsp / 2. - Lsm / 2. + lSm - lSp) * (2 * (tm - tp) + (Lmt - Lmp))
+                   + Lmm * (Lsm - L2m - 2 * (lSm - am)) - Lpm * (Lsp - L2m - 2 * (lSp - am))
+                   - Lmq * (Lsm - L2p - 2 * (lSm - ap)) + Lpq * (Lsp - L2p - 2 * (lSp - ap)));
+        }
+        NUSI_PHASE();
     } else {
         const double brk = -((tm - tp) * (2 + tm * (-1 + tp) - tp)) - 2 * (-1 + tm) * (-1 + tp) * (Lmt - Lmp);
         at = 3. / 2. * g4 / (32 * kPi * m4 * Sm * Sp * (-1 + tm) * (-1 + tp)) * (Sm - Sp) * brk;
@@ -754,6 +824,7 @@ NUSI_FN void alpha_k(const Point& P, const SplineSet& spl, int k, double Em, dou
         au *= uk;
         tot += wgt * au;
         tot += wgt * atu;   // alpha_tu = 0 for Dirac
+        const double Lsm = eSm.Ls, Lsp = eSp.Ls;
         ast = g4 / (32 * kPi * (1 + gr2) * m4) *
               ((2 * gr * eSm.cS - 2 * gr * eSp.cS + 2 * lSm - 2 * lSp + Lsp - Lsm) * (tm - tp + Lmt - Lmp));
     }
@@ -766,7 +837,11 @@ NUSI_FN void alpha_k(const Point& P, const SplineSet& spl, int k, double Em, dou
     tot += wgt * app;
 
     const double nrm = (g / mphi) * (g / mphi) * ((g / mphi) * (g / mphi));
-    if (as < 0 || at / nrm < -1e-11 || au / nrm < -1e-11 || atu / nrm < -1e-11 || (ast + as + at) / nrm < -1e-11)
+    // the reference's roundoff checks (:1505); every quotient needs a negative numerator (nrm > 0),
+    // so the divisions are only evaluated when one is
+    const double sst = ast + as + at;
+    if (as < 0 || ((at < 0 || au < 0 || atu < 0 || sst < 0) &&
+                   (at / nrm < -1e-11 || au / nrm < -1e-11 || atu / nrm < -1e-11 || sst / nrm < -1e-11)))
         warn |= kWarnAlpha;
 }
 

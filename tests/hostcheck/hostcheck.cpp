@@ -40,7 +40,7 @@ int hc_alpha_tiled(const double* pt, const int* flags, int T, const double* lo, 
     const Point P = mk(pt, flags);
     SplineSet spl{};
     const int nt = (T + kAlphaTile - 1) / kAlphaTile;
-    std::vector<double> sm(kCornerFields * 4 * kAlphaTile * kAlphaTile + 3 * 1000);
+    std::vector<double> sm(kCornerFields * 4 * kAlphaTile * kAlphaTile + 4 * 4 * kAlphaTile * kAlphaTile + 3 * 1000);
     int warn = 0;
     for (int tm = 0; tm < nt; ++tm)
         for (int tn = 0; tn <= tm; ++tn) {
@@ -51,13 +51,16 @@ int hc_alpha_tiled(const double* pt, const int* flags, int T, const double* lo, 
             const int cs = alpha_edge_list(lo, hi, m0, T, sE, sl, sh);
             const int cc = cs * ct;
             double* cor = sm.data();
-            double* edg = cor + kCornerFields * cc;
+            double* edg = cor + alpha_tile_corner_block(cs, ct);
             for (int job = 0; job < 3 * (ct + cs + kAlphaTile); ++job)
                 alpha_tile_edge_job(P, job, tE, ct, sE, cs, lo, hi, m0, T, edg);
             double tot[kAlphaTile * kAlphaTile] = {};
             for (int k = 0; k < 3; ++k) {
-                if (P.non_resonant && P.majorana)
+                if (P.non_resonant && P.majorana) {
                     for (int j = 0; j < cc; ++j) alpha_tile_corner_job(P, k, j, tE, ct, sE, cc, cor);
+                    for (int j = 0; j < kAlphaTile * (cs + ct); ++j)
+                        alpha_tile_mixed_job(P, k, j, tE, ct, sE, cs, tl, th, sl, sh, n0, m0, T, cor);
+                }
                 for (int e = 0; e < kAlphaTile * kAlphaTile; ++e) {
                     const int ln = e % kAlphaTile, lm = e / kAlphaTile, n = n0 + ln, m = m0 + lm;
                     if (!(n < m && m < T) || !(P.non_resonant || m == n + 1)) continue;
