@@ -50,8 +50,11 @@ EXPORTS = [
     "nusi_get_N_bins_E", "nusi_get_N_steps_z", "nusi_get_warnings",
     "nusi_plan_create", "nusi_plan_destroy", "nusi_plan_load_phiphi", "nusi_plan_grid", "nusi_plan_evolve",
     "nusi_plan_evolve_host", "nusi_plan_stage_ms", "nusi_plan_profile_begin", "nusi_plan_profile_end",
-    "nusi_plan_warnings", "nusi_plan_tables", "nusi_evolve_batch",
+    "nusi_plan_warnings", "nusi_plan_tables", "nusi_evolve_batch", "nusi_plan_set_cascade",
 ]
+
+# nusi_plan_set_cascade kinds (include/nusi.h)
+CASCADE_AUTO, CASCADE_WAVEFRONT, CASCADE_REG, CASCADE_LDS = 0, 1, 2, 3
 
 _lib = None
 
@@ -96,6 +99,7 @@ def load():
         "nusi_plan_warnings": (i, [vp, ip, i]),
         "nusi_plan_tables": (i, [vp, i, dp, dp, dp]),
         "nusi_evolve_batch": (i, [i, pp, i, dp, dp]),
+        "nusi_plan_set_cascade": (i, [vp, i]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)

@@ -367,6 +367,7 @@ struct nusi_plan {
     std::vector<hipEvent_t> prof_ev;   // 4 per recorded call
     hipEvent_t* last_ev = nullptr;
     int prof_max = 0, prof_n = 0;
+    int cascade_kind = NUSI_CASCADE_AUTO;
     double U2[2][9];
     std::map<double, double> fs_cache;                      // si -> flux_FS_E0
     std::map<std::pair<double, int>, std::vector<double>> mass_cache;
@@ -636,7 +637,7 @@ int nusi_plan_evolve(nusi_plan* pl, const nusi_params* pts, int n, double* d_flu
     HIPCHECK(hipEventRecord(ev[1], s));
     HIPCHECK(nusi::launch_alpha(pl->gd, pl->d_tpts, ntab, spl, pl->atiles, pl->tabs, pl->d_warn, s));
     HIPCHECK(hipEventRecord(ev[2], s));
-    HIPCHECK(nusi::launch_cascade(pl->gd, pl->d_pts, n, pl->tabs, d_flux, d_fla, s));
+    HIPCHECK(nusi::launch_cascade(pl->gd, pl->d_pts, n, pl->tabs, d_flux, d_fla, s, pl->cascade_kind));
     HIPCHECK(hipEventRecord(ev[3], s));
     pl->last_ev = ev;   // stage_ms / warnings / tables refer to the latest call
     pl->ran = true;
@@ -684,6 +685,14 @@ int nusi_plan_stage_ms(nusi_plan* pl, float* ms3)
     HIPCHECK(hipSetDevice(pl->device));
     HIPCHECK(hipEventSynchronize(pl->last_ev[3]));
     for (int k = 0; k < 3; ++k) HIPCHECK(hipEventElapsedTime(&ms3[k], pl->last_ev[k], pl->last_ev[k + 1]));
+    return NUSI_OK;
+}
+
+int nusi_plan_set_cascade(nusi_plan* pl, int kind)
+{
+    if (!pl) return fail(NUSI_EPARAM, "plan is NULL");
+    if (kind < NUSI_CASCADE_AUTO || kind > NUSI_CASCADE_LDS) return fail(NUSI_EPARAM, "unknown cascade kind");
+    pl->cascade_kind = kind;
     return NUSI_OK;
 }
 

@@ -55,6 +55,60 @@ NUSI_FN void lu3_factor(double A[3][3], int perm[3])
     }
 }
 
+// flux-independent fields of bin b at step i (every PR_* field, the LU permutation in R[kPreFields]):
+// Zdr, M = I + offdiag and its LU (nuSIprop.hpp:289-310) and the source term c_i Lum (:283)
+NUSI_FN void cascade_record(const GridDev& g, const Point& P, const double* __restrict__ Gt,
+                            const double* __restrict__ At, int i, int b, double* R, int stride)
+{
+    const double c = g.step_c[i], s = g.step_s[i];
+    const double uk[3] = {P.u[0], P.u[1], P.u[2]};
+    const double dEb = g.Emax[b] - g.Emin[b];
+    const double Gw = s * Gt[b + i - 1], Aw = s * At[b + i - 1];
+    double Zd[3], M[3][3];
+    for (int k = 0; k < 3; ++k) Zd[k] = 1.0 + c * (Gw * uk[k] - Aw * (uk[k] * uk[k])) / dEb;
+    for (int k = 0; k < 3; ++k)
+        for (int l = 0; l < 3; ++l) M[k][l] = (k == l) ? 1.0 : (Aw * uk[k] * uk[l] / dEb) / Zd[k];
+    int pm[3];
+    lu3_factor(M, pm);
+    R[PR_RZ0 * stride] = 1.0 / Zd[0];
+    R[PR_RZ1 * stride] = 1.0 / Zd[1];
+    R[PR_RZ2 * stride] = 1.0 / Zd[2];
+    R[PR_SRC * stride] = c * lum(P, g.z[i], g.sfr[i], g.Emin[b], g.Emax[b]);
+    R[PR_L10 * stride] = M[1][0];
+    R[PR_L20 * stride] = M[2][0];
+    R[PR_L21 * stride] = M[2][1];
+    R[PR_U01 * stride] = M[0][1];
+    R[PR_U02 * stride] = M[0][2];
+    R[PR_U12 * stride] = M[1][2];
+    R[PR_RU00 * stride] = 1.0 / M[0][0];
+    R[PR_RU11 * stride] = 1.0 / M[1][1];
+    R[PR_RU22 * stride] = 1.0 / M[2][2];
+    R[PR_SDE * stride] = P.non_resonant ? s / dEb : dEb;
+    R[kPreFields * stride] = (double)(pm[0] | (pm[1] << 2) | (pm[2] << 4));
+}
+
+// the 3x3 solve of one bin (nuSIprop.hpp:289-313) from its fields and the coupling `add` to the
+// bins above; x = F[:, b] of this step
+NUSI_FN void cascade_solve(double f0, double f1, double f2, double add, double src0, double u0, double u1, double u2,
+                           double rz0, double rz1, double rz2, int pmb, double l10, double l20, double l21, double u01,
+                           double u02, double u12, double ru00, double ru11, double ru22, double& x0, double& x1,
+                           double& x2)
+{
+    const double v0 = (f0 + (src0 + u0 * add)) * rz0;
+    const double v1 = (f1 + (src0 + u1 * add)) * rz1;
+    const double v2 = (f2 + (src0 + u2 * add)) * rz2;
+    const int p0 = pmb & 3, p1 = (pmb >> 2) & 3, p2 = (pmb >> 4) & 3;
+    x0 = (p0 == 0) ? v0 : (p0 == 1) ? v1 : v2;
+    x1 = (p1 == 0) ? v0 : (p1 == 1) ? v1 : v2;
+    x2 = (p2 == 0) ? v0 : (p2 == 1) ? v1 : v2;
+    x1 = x1 - l10 * x0;
+    x2 = x2 - l20 * x0;
+    x2 = x2 - l21 * x1;
+    x2 = x2 * ru22;
+    x1 = (x1 - u12 * x2) * ru11;
+    x0 = (x0 - u01 * x1 - u02 * x2) * ru00;
+}
+
 __global__ __launch_bounds__(64) void k_cascade(GridDev g, const Point* __restrict__ pts, TablesDev t,
                                                 double* __restrict__ flux, double* __restrict__ flux_fla)
 {
@@ -231,7 +285,6 @@ __global__ __launch_bounds__(64) void k_cascade_reg(GridDev g, const Point* __re
     const int p = blockIdx.x, lane = threadIdx.x;
     const Point& P = pts[p];
     const double u0 = P.u[0], u1 = P.u[1], u2 = P.u[2];
-    const double uk[3] = {u0, u1, u2};
     const double* __restrict__ Gt = t.G + (size_t)P.tslot * T;
     const double* __restrict__ At = t.At + (size_t)P.tslot * T;
     const double* __restrict__ Al = t.A + (size_t)P.tslot * g.PT;
@@ -242,7 +295,7 @@ __global__ __launch_bounds__(64) void k_cascade_reg(GridDev g, const Point* __re
     for (int q = 0; q < NQ; ++q) F0[q] = F1[q] = F2[q] = 0.0;
 
     for (int i = Nz - 1; i > 0; --i) {
-        const double c = g.step_c[i], s = g.step_s[i], zi = g.z[i], sfri = g.sfr[i];
+        const double c = g.step_c[i], s = g.step_s[i];
         if (!nonres) {
             __syncthreads();
             for (int b = lane; b < N - 1; b += 64) sdiag[b] = Al[(size_t)(b + i) * (b + i - 1) / 2 + (b + i - 1)];
@@ -263,29 +316,7 @@ __global__ __launch_bounds__(64) void k_cascade_reg(GridDev g, const Point* __re
                 const int b = base + lane;
                 double* R = rec + lane * kRec;
                 if (b < N) {
-                    const double dEb = g.Emax[b] - g.Emin[b];
-                    const double Gw = s * Gt[b + i - 1], Aw = s * At[b + i - 1];
-                    double Zd[3], M[3][3];
-                    for (int k = 0; k < 3; ++k) Zd[k] = 1.0 + c * (Gw * uk[k] - Aw * (uk[k] * uk[k])) / dEb;
-                    for (int k = 0; k < 3; ++k)
-                        for (int l = 0; l < 3; ++l) M[k][l] = (k == l) ? 1.0 : (Aw * uk[k] * uk[l] / dEb) / Zd[k];
-                    int pm[3];
-                    lu3_factor(M, pm);
-                    R[PR_RZ0] = 1.0 / Zd[0];
-                    R[PR_RZ1] = 1.0 / Zd[1];
-                    R[PR_RZ2] = 1.0 / Zd[2];
-                    R[PR_SRC] = c * lum(P, zi, sfri, g.Emin[b], g.Emax[b]);
-                    R[PR_L10] = M[1][0];
-                    R[PR_L20] = M[2][0];
-                    R[PR_L21] = M[2][1];
-                    R[PR_U01] = M[0][1];
-                    R[PR_U02] = M[0][2];
-                    R[PR_U12] = M[1][2];
-                    R[PR_RU00] = 1.0 / M[0][0];
-                    R[PR_RU11] = 1.0 / M[1][1];
-                    R[PR_RU22] = 1.0 / M[2][2];
-                    R[PR_SDE] = nonres ? s / dEb : dEb;
-                    R[RC_PERM] = (double)(pm[0] | (pm[1] << 2) | (pm[2] << 4));
+                    cascade_record(g, P, Gt, At, i, b, R, 1);
                     R[RC_F0] = F0[qc];
                     R[RC_F1] = F1[qc];
                     R[RC_F2] = F2[qc];
@@ -316,19 +347,9 @@ __global__ __launch_bounds__(64) void k_cascade_reg(GridDev g, const Point* __re
                             }
                             add = c * racc * sde;
                         }
-                        const double v0 = (f0 + (src0 + u0 * add)) * rz0;
-                        const double v1 = (f1 + (src0 + u1 * add)) * rz1;
-                        const double v2 = (f2 + (src0 + u2 * add)) * rz2;
-                        const int p0 = pmb & 3, p1 = (pmb >> 2) & 3, p2 = (pmb >> 4) & 3;
-                        double x0 = (p0 == 0) ? v0 : (p0 == 1) ? v1 : v2;
-                        double x1 = (p1 == 0) ? v0 : (p1 == 1) ? v1 : v2;
-                        double x2 = (p2 == 0) ? v0 : (p2 == 1) ? v1 : v2;
-                        x1 = x1 - l10 * x0;
-                        x2 = x2 - l20 * x0;
-                        x2 = x2 - l21 * x1;
-                        x2 = x2 * ru22;
-                        x1 = (x1 - u12 * x2) * ru11;
-                        x0 = (x0 - u01 * x1 - u02 * x2) * ru00;
+                        double x0, x1, x2;
+                        cascade_solve(f0, f1, f2, add, src0, u0, u1, u2, rz0, rz1, rz2, pmb, l10, l20, l21, u01, u02,
+                                      u12, ru00, ru11, ru22, x0, x1, x2);
                         if (lane == l) { F0[qc] = x0; F1[qc] = x1; F2[qc] = x2; }
                         px0 = x0; px1 = x1; px2 = x2;
                         if (nonres && b > 0) {
@@ -374,6 +395,189 @@ __global__ __launch_bounds__(64) void k_cascade_reg(GridDev g, const Point* __re
     }
 }
 
+// ---------------------------------------------------------------------------
+// Wavefront cascade: all redshift steps of a point in flight at once.
+//
+// Step i may solve bin b as soon as step i+1 has finalised F[:, b] and step i
+// has solved every bin above b.  Lagging step i by one bin behind step i+1
+// (lane j = Nz-1-i solves bin b = N-1-sg+j at stage sg) meets both conditions,
+// so the (Nz-1) N sequential solves of the reference's loop nest collapse into
+// T = N+Nz-2 stages of up to Nz-1 independent solves.  Along a stage b + i is
+// constant: every active step reads the SAME table column r = T-1-sg (the
+// index-shift identity, nuSIprop.hpp:262-275), so each column of the packed
+// alpha table is read from HBM once per point instead of once per step.
+//
+// Workgroup of ceil((T-1)/64) waves, thread rho owns table row rho: it holds
+// acc_j(rho) for every step j in registers and, per stage, pushes column r
+// into them (acc_j(rho) += alpha(rho, r) T_j, rho < r).  Per stage:
+//   P1  wave 0, lane j: the 3x3 solve of its (step, bin) from LDS records and
+//       the accumulator of row r (published by its owner), T_j -> LDS
+//   P2  every row: the push of column r; the owner of row r-1 publishes its
+//       accumulators for the next stage's chain
+// The flux-independent records of K = threads/NJ stages are computed by all
+// threads at once (one (stage, step) per thread) before those stages.
+// Every accumulator receives the same fma()s in the same (descending column)
+// order as in k_cascade_reg, and the solve is cascade_solve(): the two kernels
+// agree bit for bit.  Rows rho < i-1 of step j are pushed too (no mask); they
+// never feed a solve.
+// ---------------------------------------------------------------------------
+constexpr int kWfFields = kPreFields + 1;   // PR_* and the permutation
+#ifndef NUSI_WF_AB
+#define NUSI_WF_AB 0   // timing experiments only: 1 skip records, 2 skip push, 4 skip solve
+#endif
+constexpr int kWfMaxThreads = 512;
+
+template <int NJ>
+__global__ __launch_bounds__(kWfMaxThreads) void k_cascade_wf(GridDev g, const Point* __restrict__ pts, TablesDev t,
+                                                              double* __restrict__ flux, double* __restrict__ flux_fla,
+                                                              int K)
+{
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    const int N = g.N, Nz = g.Nz, T = g.T, nst = Nz - 1;
+    const int tid = threadIdx.x, nthr = blockDim.x;   // K: stages per record batch, K NJ <= nthr
+    const int KR = K * NJ;                   // records per batch (field stride)
+    double* F = lds;                         // [3][N]
+    double* rec = F + 3 * N;                 // [kWfFields][K][NJ]
+    double* Tp = rec + kWfFields * KR;       // [NJ]  T_j of this stage
+    double* AX = Tp + NJ;                    // [NJ]  accumulators of the row the chain solves next
+    const Point& P = pts[blockIdx.x];
+    const double u0 = P.u[0], u1 = P.u[1], u2 = P.u[2];
+    const double* __restrict__ Gt = t.G + (size_t)P.tslot * T;
+    const double* __restrict__ At = t.At + (size_t)P.tslot * T;
+    const double* __restrict__ Al = t.A + (size_t)P.tslot * g.PT;
+    const bool nonres = P.non_resonant;
+
+    for (int b = tid; b < 3 * N; b += nthr) F[b] = 0.0;
+    for (int j = tid; j < NJ; j += nthr) AX[j] = Tp[j] = 0.0;
+    double acc[NJ];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc[j] = 0.0;
+    const int rho = tid;
+    // chain lane state (wave 0, lane = step slot j)
+    const int ist = Nz - 1 - tid;
+    const double cj = (tid < nst) ? g.step_c[ist] : 0.0, sj = (tid < nst) ? g.step_s[ist] : 0.0;
+    double racc = 0.0, px0 = 0.0, px1 = 0.0, px2 = 0.0;
+    double a_cur = (nonres && rho < T - 1) ? Al[(size_t)(T - 1) * (T - 2) / 2 + rho] : 0.0;
+
+    for (int sg = 0; sg < T; ++sg) {
+        const int r = T - 1 - sg;
+        const int ks = sg % K;
+        if (ks == 0) {   // ---- records of stages sg .. sg+K-1, one (stage, step) per thread
+            __syncthreads();
+            const int q = tid / NJ, jj = tid - q * NJ, s2 = sg + q;
+            if (q < K && jj < nst && s2 < T) {
+                const int b = N - 1 - s2 + jj;
+                if (b >= 0 && b < N && !(NUSI_WF_AB & 1)) cascade_record(g, P, Gt, At, Nz - 1 - jj, b, rec + q * NJ + jj, KR);
+            }
+            __syncthreads();
+        }
+        // ---- P1: the chain, one lane per active step
+        if (tid < nst) {
+            const int b = N - 1 - sg + tid;
+            double T_j = 0.0;
+            if (b >= 0 && b < N) {
+                const double* R = rec + ks * NJ + tid;
+                double add;
+                if (nonres) {
+                    add = cj * AX[tid];
+                } else {
+                    if (b != N - 1) {
+                        const double Sres = u0 * px0 + u1 * px1 + u2 * px2;
+                        const double sd = Al[(size_t)(r + 1) * r / 2 + r];   // alpha(b+i-1, b+i)
+                        racc += Sres * (sj * sd) / (g.Emax[b + 1] - g.Emin[b + 1]) / R[PR_SDE * KR];
+                    }
+                    add = cj * racc * R[PR_SDE * KR];
+                }
+                double x0 = add, x1 = add, x2 = add;
+                if (!(NUSI_WF_AB & 4))
+                cascade_solve(F[b], F[N + b], F[2 * N + b], add, R[PR_SRC * KR], u0, u1, u2, R[PR_RZ0 * KR],
+                              R[PR_RZ1 * KR], R[PR_RZ2 * KR], (int)R[kPreFields * KR], R[PR_L10 * KR], R[PR_L20 * KR],
+                              R[PR_L21 * KR], R[PR_U01 * KR], R[PR_U02 * KR], R[PR_U12 * KR], R[PR_RU00 * KR],
+                              R[PR_RU11 * KR], R[PR_RU22 * KR], x0, x1, x2);
+                F[b] = x0;
+                F[N + b] = x1;
+                F[2 * N + b] = x2;
+                px0 = x0; px1 = x1; px2 = x2;
+                if (nonres && b > 0) T_j = (u0 * x0 + u1 * x1 + u2 * x2) * R[PR_SDE * KR];
+            }
+            Tp[tid] = T_j;
+        }
+        __syncthreads();
+        // ---- P2: push column r into rows rho < r (steps that have not started keep acc = 0)
+        if (nonres) {
+            const double a_next = (rho < r - 1) ? Al[(size_t)(r - 1) * (r - 2) / 2 + rho] : 0.0;
+            if (rho < r && !(NUSI_WF_AB & 2)) {
+                // T_j in groups of 8 (a fence per group keeps the compiler from holding all NJ
+                // broadcasts in registers next to the NJ accumulators)
+                if (sg >= NJ - 1) {
+#pragma unroll
+                    for (int j0 = 0; j0 < NJ; j0 += 8) {
+#pragma unroll
+                        for (int j = j0; j < j0 + 8; ++j) acc[j] = fma(a_cur, Tp[j], acc[j]);
+                        NUSI_PHASE();
+                    }
+                } else {
+#pragma unroll
+                    for (int j0 = 0; j0 < NJ; j0 += 8) {
+#pragma unroll
+                        for (int j = j0; j < j0 + 8; ++j)
+                            if (j <= sg) acc[j] = fma(a_cur, Tp[j], acc[j]);
+                        NUSI_PHASE();
+                    }
+                }
+                if (rho == r - 1) {
+#pragma unroll
+                    for (int j = 0; j < NJ; ++j) AX[j] = acc[j];
+                }
+            }
+            a_cur = a_next;
+        }
+        __syncthreads();
+    }
+    // finalise (nuSIprop.hpp:328-336)
+    double* fo = flux + (size_t)blockIdx.x * 3 * N;
+    double* fl = flux_fla + (size_t)blockIdx.x * 3 * N;
+    for (int b = tid; b < N; b += nthr) {
+        const double dE = g.Emax[b] - g.Emin[b];
+        const double f0 = F[b] / dE, f1 = F[N + b] / dE, f2 = F[2 * N + b] / dE;
+        fo[b] = f0;
+        fo[N + b] = f1;
+        fo[2 * N + b] = f2;
+        for (int f = 0; f < 3; ++f) fl[f * N + b] = P.U2[3 * f + 0] * f0 + P.U2[3 * f + 1] * f1 + P.U2[3 * f + 2] * f2;
+    }
+}
+
+// launch geometry of the wavefront kernel: one thread per pushed row (T-1), whole waves; K stages
+// of records per batch, as many as the threads cover and kWfMaxLds allows
+constexpr size_t kWfMaxLds = 64 * 1024;
+struct WfGeom { int nthr, K; size_t lds; };
+static WfGeom wf_geom(const GridDev& g, int NJ)
+{
+    WfGeom w;
+    w.nthr = ((g.T - 1 + 63) / 64) * 64;
+    w.K = w.nthr / NJ;
+    auto bytes = [&](int K) { return sizeof(double) * (3 * (size_t)g.N + (size_t)kWfFields * K * NJ + 2 * NJ); };
+    while (w.K > 1 && bytes(w.K) > kWfMaxLds) --w.K;
+    w.lds = bytes(w.K);
+    return w;
+}
+// step slots: up to 48 (64 accumulators would spill at two waves per SIMD)
+static int wf_nj(const GridDev& g) { const int n = g.Nz - 1; return n <= 16 ? 16 : n <= 32 ? 32 : n <= 48 ? 48 : 0; }
+static bool wf_fits(const GridDev& g)
+{
+    const int nj = wf_nj(g);
+    if (!nj || g.T - 1 > kWfMaxThreads || g.T < 2) return false;
+    return wf_geom(g, nj).lds <= kWfMaxLds;
+}
+
+template <int NJ>
+static void launch_wf(const GridDev& g, const Point* pts, int npts, TablesDev t, double* flux, double* flux_fla,
+                      hipStream_t s)
+{
+    const WfGeom w = wf_geom(g, NJ);
+    hipLaunchKernelGGL((k_cascade_wf<NJ>), dim3(npts), dim3(w.nthr), w.lds, s, g, pts, t, flux, flux_fla, w.K);
+}
+
 template <int NQ>
 static void launch_reg(const GridDev& g, const Point* pts, int npts, TablesDev t, double* flux, double* flux_fla,
                        hipStream_t s)
@@ -395,12 +599,23 @@ static bool dispatch_reg(int nq, const GridDev& g, const Point* pts, int npts, T
 using RegNQ = std::integer_sequence<int, 1, 2, 3, 4, 5, 6, 8, 10, 12, 16, 20>;
 
 hipError_t launch_cascade(const GridDev& g, const Point* pts, int npts, TablesDev t, double* flux, double* flux_fla,
-                          hipStream_t s)
+                          hipStream_t s, int kind)
 {
     const int nq = (g.N + 63) / 64;
-    static const bool force_lds = getenv("NUSI_CASCADE_LDS") != nullptr;   // A/B switch
-    if (!force_lds &&
-        dispatch_reg(nq, g, pts, npts, t, flux, flux_fla, s, RegNQ{}))
+    if (kind == NUSI_CASCADE_AUTO) {
+        static const char* env = getenv("NUSI_CASCADE");   // A/B switch: wf | reg | lds
+        kind = !env ? NUSI_CASCADE_AUTO
+                    : (env[0] == 'w' ? NUSI_CASCADE_WAVEFRONT : env[0] == 'r' ? NUSI_CASCADE_REG : NUSI_CASCADE_LDS);
+    }
+    if ((kind == NUSI_CASCADE_AUTO || kind == NUSI_CASCADE_WAVEFRONT) && wf_fits(g)) {
+        switch (wf_nj(g)) {
+        case 16: launch_wf<16>(g, pts, npts, t, flux, flux_fla, s); break;
+        case 32: launch_wf<32>(g, pts, npts, t, flux, flux_fla, s); break;
+        default: launch_wf<48>(g, pts, npts, t, flux, flux_fla, s); break;
+        }
+        return hipGetLastError();
+    }
+    if (kind != NUSI_CASCADE_LDS && dispatch_reg(nq, g, pts, npts, t, flux, flux_fla, s, RegNQ{}))
         return hipGetLastError();
     const size_t lds = cascade_lds_bytes(g.N);
     hipLaunchKernelGGL(k_cascade, dim3(npts), dim3(64), lds, s, g, pts, t, flux, flux_fla);

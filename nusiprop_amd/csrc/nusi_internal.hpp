@@ -3,6 +3,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include "nusi.h"
 #include "nusi_physics.hpp"
 
 namespace nusi {
@@ -48,7 +49,8 @@ hipError_t launch_gamma_alphat(const GridDev& g, const Point* pts, int npts, con
                                int* warn, hipStream_t s);
 hipError_t launch_alpha(const GridDev& g, const Point* pts, int npts, const SplineSet& spl, const AlphaTilesDev& tiles,
                         TablesDev t, int* warn, hipStream_t s);
+// kind: NUSI_CASCADE_* (include/nusi.h); NUSI_CASCADE_AUTO also honours $NUSI_CASCADE = wf|reg|lds
 hipError_t launch_cascade(const GridDev& g, const Point* pts, int npts, TablesDev t, double* flux, double* flux_fla,
-                          hipStream_t s);
+                          hipStream_t s, int kind);
 
 }  // namespace nusi

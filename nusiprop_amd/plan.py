@@ -81,6 +81,10 @@ class Plan:
                                                 ctypes.c_void_p(d_fla_ptr),
                                                 ctypes.c_void_p(stream_ptr) if stream_ptr else None))
 
+    def set_cascade(self, kind):
+        """Cascade kernel of later calls: _lib.CASCADE_{AUTO,WAVEFRONT,REG,LDS} (same fluxes bit for bit)."""
+        _lib.check(_lib.load().nusi_plan_set_cascade(self._h, int(kind)))
+
     def profile_begin(self, max_calls):
         _lib.check(_lib.load().nusi_plan_profile_begin(self._h, int(max_calls)))
 

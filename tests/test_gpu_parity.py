@@ -151,3 +151,28 @@ def test_gamma_batches_share_tables(nusi, oracle_mod):
         o = oracle_mod.Oracle(**cases.oracle_kwargs(p))
         _, fla_ref = o.evolve()
         assert cases.rel_err(fla[i], fla_ref) <= FLUX_RTOL
+
+
+@pytest.mark.parametrize("N,nonres", [(37, True), (64, False), (130, True), (200, True), (300, True), (300, False),
+                                      (700, True)])
+def test_cascade_kernels_agree(nusi, N, nonres):
+    """The wavefront cascade (all redshift steps in flight, N_z - 1 <= 48) and the register-
+    resident one give the same fluxes bit for bit (same fma()s in the same order); the LDS
+    kernel (separate multiply and add) agrees to 1e-12; N = 700 exceeds the wavefront
+    kernel's limits and checks its fallback."""
+    from nusiprop_amd import _lib
+    pts = [dict(cases.C2B_100, N_bins_E=N, non_resonant=nonres, majorana=maj, mphi=m, g=gg)
+           for maj, m, gg in ((True, 6e5, 0.01), (False, 2e6, 0.1), (True, 1e6, 0.3))]
+    plan = nusi.Plan(N, pts[0]["lEmin"], pts[0]["lEmax"], pts[0]["zmax"], max_points=len(pts))
+    out = {}
+    for kind in (_lib.CASCADE_WAVEFRONT, _lib.CASCADE_REG, _lib.CASCADE_LDS, _lib.CASCADE_AUTO):
+        plan.set_cascade(kind)
+        out[kind] = plan.evolve(pts)
+    ref = out[_lib.CASCADE_REG]
+    assert np.all(np.isfinite(ref[1])) and np.any(ref[1] > 0)
+    for kind, (f, fl) in out.items():
+        if kind == _lib.CASCADE_LDS:
+            assert cases.rel_err(f, ref[0]) <= 1e-12 and cases.rel_err(fl, ref[1]) <= 1e-12
+            continue
+        assert np.array_equal(f, ref[0]), "kind %d flux differs in %d entries" % (kind, np.sum(f != ref[0]))
+        assert np.array_equal(fl, ref[1])
