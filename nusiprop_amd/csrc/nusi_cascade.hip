@@ -55,25 +55,61 @@ NUSI_FN void lu3_factor(double A[3][3], int perm[3])
     }
 }
 
+// Per-point tables shared by the records of every (step, bin) (LDS; cascade_aux_init):
+//   rdE[b] = 1 / dE_b                                                           [N]
+//   pw[e]  = pow(E_e / E0 * (1 + z_i), -si) on table edge e = b + i (lower edge of bin b at
+//            step i; the upper edge is e + 1), power-law source only            [T + 2]
+// Along e the argument depends on b + i only (E_b (1 + z_i) = E_{b+i}, the index-shift
+// identity), so 2 (Nz-1) N pow() calls per point become T + 1.  pw[e] is evaluated at one
+// (b, i) of its edge; the other pairs' arguments differ from it by rounding only (<= 2 ulp).
+constexpr int kAuxDoubles = 2;   // cascade_aux_doubles(N, T) = N + T + kAuxDoubles
+NUSI_FN int cascade_aux_doubles(int N, int T) { return N + T + kAuxDoubles; }
+__device__ inline void cascade_aux_init(const GridDev& g, const Point& P, double* rdE, double* pw, int tid, int nthr)
+{
+    const int N = g.N, Nz = g.Nz, T = g.T;
+    for (int b = tid; b < N; b += nthr) rdE[b] = 1.0 / (g.Emax[b] - g.Emin[b]);
+    if (P.source == 1)
+        for (int e = tid + 1; e <= T + 1; e += nthr) {
+            const int i = min(Nz - 1, max(1, e - N + 1)), b = e - i;
+            const double E = (b < N) ? g.Emin[b] : g.Emax[N - 1];
+            pw[e] = nm::pow(E / 1e14 * (1 + g.z[i]), -P.si);
+        }
+}
+
+// the DSNB source, out of line: it is not the scans' source and inlined it would cost every
+// record's caller registers
+__device__ __attribute__((noinline)) double lum_out(const Point& P, double z, double sfr_z, double Em, double Ep)
+{
+    return lum(P, z, sfr_z, Em, Ep);
+}
+
 // flux-independent fields of bin b at step i (every PR_* field, the LU permutation in R[kPreFields]):
-// Zdr, M = I + offdiag and its LU (nuSIprop.hpp:289-310) and the source term c_i Lum (:283)
+// Zdr, M = I + offdiag and its LU (nuSIprop.hpp:289-310) and the source term c_i Lum (:283).
+// 1/dE_b and 1/Zdr are multiplied in (the reference divides; M's off-diagonals are ~1e-22 of
+// the diagonal), the power-law source reads pw[]; the DSNB source is evaluated in full.
 NUSI_FN void cascade_record(const GridDev& g, const Point& P, const double* __restrict__ Gt,
-                            const double* __restrict__ At, int i, int b, double* R, int stride)
+                            const double* __restrict__ At, const double* rdE, const double* pw, int i, int b,
+                            double* R, int stride)
 {
     const double c = g.step_c[i], s = g.step_s[i];
     const double uk[3] = {P.u[0], P.u[1], P.u[2]};
-    const double dEb = g.Emax[b] - g.Emin[b];
+    const double rd = rdE[b];
     const double Gw = s * Gt[b + i - 1], Aw = s * At[b + i - 1];
-    double Zd[3], M[3][3];
-    for (int k = 0; k < 3; ++k) Zd[k] = 1.0 + c * (Gw * uk[k] - Aw * (uk[k] * uk[k])) / dEb;
+    double rz[3], M[3][3];
+    for (int k = 0; k < 3; ++k) rz[k] = 1.0 / (1.0 + c * (Gw * uk[k] - Aw * (uk[k] * uk[k])) * rd);
     for (int k = 0; k < 3; ++k)
-        for (int l = 0; l < 3; ++l) M[k][l] = (k == l) ? 1.0 : (Aw * uk[k] * uk[l] / dEb) / Zd[k];
+        for (int l = 0; l < 3; ++l) M[k][l] = (k == l) ? 1.0 : Aw * uk[k] * uk[l] * rd * rz[k];
     int pm[3];
     lu3_factor(M, pm);
-    R[PR_RZ0 * stride] = 1.0 / Zd[0];
-    R[PR_RZ1 * stride] = 1.0 / Zd[1];
-    R[PR_RZ2 * stride] = 1.0 / Zd[2];
-    R[PR_SRC * stride] = c * lum(P, g.z[i], g.sfr[i], g.Emin[b], g.Emax[b]);
+    double src;
+    if (P.source == 1)   // nuSIprop.hpp:656
+        src = P.norm_total / 3.0 * g.sfr[i] * (g.Emax[b] * pw[b + i + 1] - g.Emin[b] * pw[b + i]) / (1 - P.si);
+    else
+        src = lum_out(P, g.z[i], g.sfr[i], g.Emin[b], g.Emax[b]);
+    R[PR_RZ0 * stride] = rz[0];
+    R[PR_RZ1 * stride] = rz[1];
+    R[PR_RZ2 * stride] = rz[2];
+    R[PR_SRC * stride] = c * src;
     R[PR_L10 * stride] = M[1][0];
     R[PR_L20 * stride] = M[2][0];
     R[PR_L21 * stride] = M[2][1];
@@ -83,7 +119,7 @@ NUSI_FN void cascade_record(const GridDev& g, const Point& P, const double* __re
     R[PR_RU00 * stride] = 1.0 / M[0][0];
     R[PR_RU11 * stride] = 1.0 / M[1][1];
     R[PR_RU22 * stride] = 1.0 / M[2][2];
-    R[PR_SDE * stride] = P.non_resonant ? s / dEb : dEb;
+    R[PR_SDE * stride] = P.non_resonant ? s * rd : (g.Emax[b] - g.Emin[b]);
     R[kPreFields * stride] = (double)(pm[0] | (pm[1] << 2) | (pm[2] << 4));
 }
 
@@ -279,8 +315,10 @@ template <int NQ, int D>
 __global__ __launch_bounds__(64) void k_cascade_reg(GridDev g, const Point* __restrict__ pts, TablesDev t,
                                                     double* __restrict__ flux, double* __restrict__ flux_fla)
 {
-    extern __shared__ __attribute__((aligned(16))) double sdiag[];   // resonant-only: alpha(b+i-1, b+i)
+    extern __shared__ __attribute__((aligned(16))) double sdiag[];   // resonant-only: alpha(b+i-1, b+i) [N]
     __shared__ __attribute__((aligned(16))) double rec[64 * kRec];
+    double* rdE = sdiag + g.N;       // cascade_aux_init tables
+    double* pw = rdE + g.N;
     const int N = g.N, Nz = g.Nz, T = g.T;
     const int p = blockIdx.x, lane = threadIdx.x;
     const Point& P = pts[p];
@@ -293,6 +331,7 @@ __global__ __launch_bounds__(64) void k_cascade_reg(GridDev g, const Point* __re
     double F0[NQ], F1[NQ], F2[NQ];
 #pragma unroll
     for (int q = 0; q < NQ; ++q) F0[q] = F1[q] = F2[q] = 0.0;
+    cascade_aux_init(g, P, rdE, pw, lane, 64);
 
     for (int i = Nz - 1; i > 0; --i) {
         const double c = g.step_c[i], s = g.step_s[i];
@@ -316,7 +355,7 @@ __global__ __launch_bounds__(64) void k_cascade_reg(GridDev g, const Point* __re
                 const int b = base + lane;
                 double* R = rec + lane * kRec;
                 if (b < N) {
-                    cascade_record(g, P, Gt, At, i, b, R, 1);
+                    cascade_record(g, P, Gt, At, rdE, pw, i, b, R, 1);
                     R[RC_F0] = F0[qc];
                     R[RC_F1] = F1[qc];
                     R[RC_F2] = F2[qc];
@@ -407,9 +446,9 @@ __global__ __launch_bounds__(64) void k_cascade_reg(GridDev g, const Point* __re
 // index-shift identity, nuSIprop.hpp:262-275), so each column of the packed
 // alpha table is read from HBM once per point instead of once per step.
 //
-// Workgroup of ceil((T-1)/64) waves, thread rho owns table row rho: it holds
-// acc_j(rho) for every step j in registers and, per stage, pushes column r
-// into them (acc_j(rho) += alpha(rho, r) T_j, rho < r).  Per stage:
+// A workgroup holds acc_j(rho) for every table row rho < T-1 and step j in
+// registers: thread = (group of 4 rows, quarter of the steps), so each T_j
+// broadcast read from LDS feeds 4 fma()s.  Per stage:
 //   P1  wave 0, lane j: the 3x3 solve of its (step, bin) from LDS records and
 //       the accumulator of row r (published by its owner), T_j -> LDS
 //   P2  every row: the push of column r; the owner of row r-1 publishes its
@@ -426,6 +465,7 @@ constexpr int kWfFields = kPreFields + 1;   // PR_* and the permutation
 #define NUSI_WF_AB 0   // timing experiments only: 1 skip records, 2 skip push, 4 skip solve
 #endif
 constexpr int kWfMaxThreads = 512;
+constexpr int kWfRows = 4, kWfQuarters = 4;   // push: rows per thread, step groups per row group
 
 template <int NJ>
 __global__ __launch_bounds__(kWfMaxThreads) void k_cascade_wf(GridDev g, const Point* __restrict__ pts, TablesDev t,
@@ -440,6 +480,8 @@ __global__ __launch_bounds__(kWfMaxThreads) void k_cascade_wf(GridDev g, const P
     double* rec = F + 3 * N;                 // [kWfFields][K][NJ]
     double* Tp = rec + kWfFields * KR;       // [NJ]  T_j of this stage
     double* AX = Tp + NJ;                    // [NJ]  accumulators of the row the chain solves next
+    double* rdE = AX + NJ;                   // cascade_aux_init tables
+    double* pw = rdE + N;
     const Point& P = pts[blockIdx.x];
     const double u0 = P.u[0], u1 = P.u[1], u2 = P.u[2];
     const double* __restrict__ Gt = t.G + (size_t)P.tslot * T;
@@ -449,15 +491,25 @@ __global__ __launch_bounds__(kWfMaxThreads) void k_cascade_wf(GridDev g, const P
 
     for (int b = tid; b < 3 * N; b += nthr) F[b] = 0.0;
     for (int j = tid; j < NJ; j += nthr) AX[j] = Tp[j] = 0.0;
-    double acc[NJ];
+    cascade_aux_init(g, P, rdE, pw, tid, nthr);
+    // push geometry: thread = (row group, step quarter); kWfRows rows x JG steps of accumulators
+    constexpr int JG = NJ / kWfQuarters;
+    const int h = tid & (kWfQuarters - 1), row0 = (tid / kWfQuarters) * kWfRows;
+    double acc[kWfRows][JG];
 #pragma unroll
-    for (int j = 0; j < NJ; ++j) acc[j] = 0.0;
-    const int rho = tid;
+    for (int c = 0; c < kWfRows; ++c)
+#pragma unroll
+        for (int jj = 0; jj < JG; ++jj) acc[c][jj] = 0.0;
     // chain lane state (wave 0, lane = step slot j)
     const int ist = Nz - 1 - tid;
     const double cj = (tid < nst) ? g.step_c[ist] : 0.0, sj = (tid < nst) ? g.step_s[ist] : 0.0;
     double racc = 0.0, px0 = 0.0, px1 = 0.0, px2 = 0.0;
-    double a_cur = (nonres && rho < T - 1) ? Al[(size_t)(T - 1) * (T - 2) / 2 + rho] : 0.0;
+    double a_cur[kWfRows];   // alpha(row, r) of this stage's column, rows clamped into the column
+#pragma unroll
+    for (int c = 0; c < kWfRows; ++c) {
+        const int row = row0 + c;
+        a_cur[c] = (nonres && T >= 2) ? Al[(size_t)(T - 1) * (T - 2) / 2 + (row < T - 2 ? row : T - 2)] : 0.0;
+    }
 
     for (int sg = 0; sg < T; ++sg) {
         const int r = T - 1 - sg;
@@ -467,7 +519,7 @@ __global__ __launch_bounds__(kWfMaxThreads) void k_cascade_wf(GridDev g, const P
             const int q = tid / NJ, jj = tid - q * NJ, s2 = sg + q;
             if (q < K && jj < nst && s2 < T) {
                 const int b = N - 1 - s2 + jj;
-                if (b >= 0 && b < N && !(NUSI_WF_AB & 1)) cascade_record(g, P, Gt, At, Nz - 1 - jj, b, rec + q * NJ + jj, KR);
+                if (b >= 0 && b < N && !(NUSI_WF_AB & 1)) cascade_record(g, P, Gt, At, rdE, pw, Nz - 1 - jj, b, rec + q * NJ + jj, KR);
             }
             __syncthreads();
         }
@@ -503,34 +555,34 @@ __global__ __launch_bounds__(kWfMaxThreads) void k_cascade_wf(GridDev g, const P
             Tp[tid] = T_j;
         }
         __syncthreads();
-        // ---- P2: push column r into rows rho < r (steps that have not started keep acc = 0)
-        if (nonres) {
-            const double a_next = (rho < r - 1) ? Al[(size_t)(r - 1) * (r - 2) / 2 + rho] : 0.0;
-            if (rho < r && !(NUSI_WF_AB & 2)) {
-                // T_j in groups of 8 (a fence per group keeps the compiler from holding all NJ
-                // broadcasts in registers next to the NJ accumulators)
-                if (sg >= NJ - 1) {
+        // ---- P2: push column r into rows < r.  Rows >= r were consumed already and steps that
+        // have not started have T_j = 0 (their accumulators stay exactly 0), so nothing is masked.
+        if (nonres && r >= 1 && !(NUSI_WF_AB & 2)) {
+            double a_next[kWfRows];
+            const size_t cn = (size_t)(r - 1) * (r - 2) / 2;
 #pragma unroll
-                    for (int j0 = 0; j0 < NJ; j0 += 8) {
-#pragma unroll
-                        for (int j = j0; j < j0 + 8; ++j) acc[j] = fma(a_cur, Tp[j], acc[j]);
-                        NUSI_PHASE();
-                    }
-                } else {
-#pragma unroll
-                    for (int j0 = 0; j0 < NJ; j0 += 8) {
-#pragma unroll
-                        for (int j = j0; j < j0 + 8; ++j)
-                            if (j <= sg) acc[j] = fma(a_cur, Tp[j], acc[j]);
-                        NUSI_PHASE();
-                    }
-                }
-                if (rho == r - 1) {
-#pragma unroll
-                    for (int j = 0; j < NJ; ++j) AX[j] = acc[j];
-                }
+            for (int c = 0; c < kWfRows; ++c) {
+                const int row = row0 + c;
+                a_next[c] = (r >= 2) ? Al[cn + (row < r - 2 ? row : r - 2)] : 0.0;
             }
-            a_cur = a_next;
+            const double* Th = Tp + h * JG;
+#pragma unroll
+            for (int jj = 0; jj < JG; ++jj) {
+                const double tj = Th[jj];
+#pragma unroll
+                for (int c = 0; c < kWfRows; ++c) acc[c][jj] = fma(a_cur[c], tj, acc[c][jj]);
+            }
+            if (r - 1 >= row0 && r - 1 < row0 + kWfRows) {   // publish row r-1 for the next chain
+                const int cp = r - 1 - row0;
+#pragma unroll
+                for (int c = 0; c < kWfRows; ++c)
+                    if (c == cp) {
+#pragma unroll
+                        for (int jj = 0; jj < JG; ++jj) AX[h * JG + jj] = acc[c][jj];
+                    }
+            }
+#pragma unroll
+            for (int c = 0; c < kWfRows; ++c) a_cur[c] = a_next[c];
         }
         __syncthreads();
     }
@@ -554,9 +606,11 @@ struct WfGeom { int nthr, K; size_t lds; };
 static WfGeom wf_geom(const GridDev& g, int NJ)
 {
     WfGeom w;
-    w.nthr = ((g.T - 1 + 63) / 64) * 64;
+    w.nthr = ((((g.T - 1 + kWfRows - 1) / kWfRows) * kWfQuarters + 63) / 64) * 64;
     w.K = w.nthr / NJ;
-    auto bytes = [&](int K) { return sizeof(double) * (3 * (size_t)g.N + (size_t)kWfFields * K * NJ + 2 * NJ); };
+    auto bytes = [&](int K) {
+        return sizeof(double) * (3 * (size_t)g.N + (size_t)kWfFields * K * NJ + 2 * NJ + cascade_aux_doubles(g.N, g.T));
+    };
     while (w.K > 1 && bytes(w.K) > kWfMaxLds) --w.K;
     w.lds = bytes(w.K);
     return w;
@@ -566,8 +620,10 @@ static int wf_nj(const GridDev& g) { const int n = g.Nz - 1; return n <= 16 ? 16
 static bool wf_fits(const GridDev& g)
 {
     const int nj = wf_nj(g);
-    if (!nj || g.T - 1 > kWfMaxThreads || g.T < 2) return false;
-    return wf_geom(g, nj).lds <= kWfMaxLds;
+    if (!nj || g.T < 2) return false;
+    const WfGeom w = wf_geom(g, nj);
+    if (w.nthr > kWfMaxThreads) return false;
+    return w.lds <= kWfMaxLds;
 }
 
 template <int NJ>
@@ -583,8 +639,8 @@ static void launch_reg(const GridDev& g, const Point* pts, int npts, TablesDev t
                        hipStream_t s)
 {
     constexpr int D = NQ <= 5 ? 8 : (NQ <= 10 ? 4 : 2);
-    hipLaunchKernelGGL((k_cascade_reg<NQ, D>), dim3(npts), dim3(64), sizeof(double) * (size_t)g.N, s, g, pts, t, flux,
-                       flux_fla);
+    const size_t lds = sizeof(double) * ((size_t)g.N + cascade_aux_doubles(g.N, g.T));
+    hipLaunchKernelGGL((k_cascade_reg<NQ, D>), dim3(npts), dim3(64), lds, s, g, pts, t, flux, flux_fla);
 }
 
 // instantiated chunk counts; a kernel built for NQ serves every N <= 64 NQ
