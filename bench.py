@@ -12,7 +12,8 @@ collective on the data path.
   python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c4|c5|c2] [--points P]
 Multi-GPU: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 
-Prints one JSON line (rank 0) with roofline (cascade kernel, HBM) and the
+Prints one JSON line (rank 0) with roofline (the dominant alpha-table kernel, fp64 VALU),
+roofline_cascade (the metric's cascade HBM GB/s) and the
 cpu_baseline (the C oracle, single thread, bounded sample).
 """
 import argparse
@@ -149,6 +150,8 @@ def main():
         traffic = pmc.get("k_cascade_bytes_per_launch")
         tsrc = os.path.relpath(tj, ROOT)
     achieved = casc_bytes / casc_s / 1e9
+    casc_min = scan.cascade_min_bytes_per_point(N, Nz) * P
+    step_ms = sum(sum_ms) / max(ncalls, 1)
     out = {
         "metric": METRIC,
         "value": value,
@@ -164,23 +167,35 @@ def main():
         "data": "synthetic (deterministic scan grid; power-law source)",
         "config": {"workload": desc, "N_E": N, "N_z": Nz, "points_per_gpu": P, "lEmin": p0["lEmin"],
                    "lEmax": p0["lEmax"], "parallelism": "independent points, %d GPU(s), no collective" % world},
-        "roofline": {"bound": "hbm", "kernel": "k_cascade_reg", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": tsrc,
-                     "algorithmic_bytes_per_launch": casc_bytes, "avg_launch_ms": casc_s * 1e3},
         "stage_ms_per_step": {"gamma_alphatilde": sum_ms[0] / max(ncalls, 1), "alpha": sum_ms[1] / max(ncalls, 1),
                               "cascade": sum_ms[2] / max(ncalls, 1)},
         "alpha_table": {"kernel": "k_alpha_tile", "bound": "fp64 VALU (transcendental)",
                         "entries_per_s": scan.alpha_entries_per_point(N, Nz) * P / alpha_s,
-                        "avg_step_ms": alpha_s * 1e3},
+                        "avg_step_ms": alpha_s * 1e3, "share_of_step": alpha_s * 1e3 / step_ms},
+        # the metric's "achieved HBM GB/s on the cascade kernel".  The wavefront kernel reads each alpha column
+        # once per point, so its algorithmic bytes are cascade_min_bytes_per_point (PMC traffic agrees);
+        # SURVEY.md sec. 8d's figure (every step re-reading its alpha window, the reference's access pattern)
+        # over the same time is reported beside it as reference_pattern_gbs
+        "roofline_cascade": {"bound": "hbm", "kernel": "k_cascade_wf", "achieved": casc_min / casc_s / 1e9,
+                             "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": casc_min / casc_s / 1e9 / HBM_PEAK_GBS,
+                             "traffic": traffic, "traffic_source": tsrc, "algorithmic_bytes_per_launch": casc_min,
+                             "reference_pattern_bytes_per_launch": casc_bytes, "reference_pattern_gbs": achieved,
+                             "avg_launch_ms": casc_s * 1e3,
+                             "note": "not HBM-bound: T = N+Nz-2 dependent stages per point (LDS/barrier latency)"},
         "invalid_outputs": bad,
     }
     fl = pmc.get("k_alpha_fp64_flops_per_step")
     if fl:   # the dominant kernel: executed fp64 VALU flops (PMC counts) per second vs the fp64 vector peak
         ach = fl / alpha_s / 1e12
-        out["roofline_dominant"] = {"bound": "valu", "kernel": "k_alpha_tile", "achieved": ach, "peak": FP64_PEAK_TFLOPS,
-                                    "unit": "TFLOP/s", "frac": ach / FP64_PEAK_TFLOPS,
-                                    "traffic": pmc.get("k_alpha_hbm_bytes_per_step"), "traffic_source": tsrc,
-                                    "flops": "executed fp64 VALU (SQ_INSTS_VALU_{ADD,MUL,TRANS}_F64 + 2 FMA) x 64 lanes"}
+        out["roofline"] = {"bound": "valu", "kernel": "k_alpha_tile", "achieved": ach, "peak": FP64_PEAK_TFLOPS,
+                           "unit": "TFLOP/s", "frac": ach / FP64_PEAK_TFLOPS,
+                           "traffic": pmc.get("k_alpha_hbm_bytes_per_step"), "traffic_source": tsrc,
+                           "flops": "executed fp64 VALU (SQ_INSTS_VALU_{ADD,MUL,TRANS}_F64 + 2 FMA) x 64 lanes, "
+                                    "from the PMC pass; time = the kernel's HIP events in this run",
+                           "note": "dominant kernel (alpha_table.share_of_step); fp64 vector-ALU bound "
+                                   "(transcendental leaves), neither HBM nor MFMA"}
+    else:
+        out["roofline"] = dict(out["roofline_cascade"])
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(pts, args.cpu_seconds)
     if rank == 0:

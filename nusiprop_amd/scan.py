@@ -40,6 +40,13 @@ def cascade_bytes_per_point(N, Nz):
     return 8 * ((Nz - 1) * N * (N - 1) // 2 + 6 * N * (Nz - 1) + Nz * N)
 
 
+def cascade_min_bytes_per_point(N, Nz):
+    """HBM bytes the wavefront cascade must move per propagation: each alpha column of the
+    packed table once (T(T-1)/2), Gamma and alphaTilde (2T), both flux outputs (6N)."""
+    T = N + Nz - 2
+    return 8 * (T * (T - 1) // 2 + 2 * T + 6 * N)
+
+
 def alpha_entries_per_point(N, Nz):
     """Stage-A alpha entries per propagation, T(T-1)/2 with T = N + Nz - 2 (each summed over 3 mass states)."""
     T = N + Nz - 2
