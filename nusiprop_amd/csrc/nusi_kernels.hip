@@ -122,7 +122,11 @@ __global__ __launch_bounds__(kTileThreads) NUSI_TILE_ATTR void k_alpha_tile(Grid
 #ifndef NUSI_AB_NO_CORNERS   // timing experiments only (scripts/build_variant.sh)
         if (nonres && maj) {
             for (int j = tid; j < cc; j += kTileThreads) alpha_tile_corner_job(P, k, j, tE, ct, sE, cc, cor);
+#ifndef NUSI_AB_NO_MIXED
             for (int j = tid; j < kAlphaTile * (cs + ct); j += kTileThreads)
+#else
+            for (int j = tid; j < 0; j += kTileThreads)
+#endif
                 alpha_tile_mixed_job(P, k, j, tE, ct, sE, cs, tl, th, sl, sh, n0, m0, T, cor);
         }
 #endif

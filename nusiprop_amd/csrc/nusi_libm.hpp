@@ -31,6 +31,8 @@
 #define NUSI_LM NUSI_FN
 #endif
 
+#include "nusi_logtab.hpp"
+
 namespace nusi {
 namespace nm {
 
@@ -45,123 +47,70 @@ NUSI_FN double with_hi(double x, int hi)
 
 constexpr double ln2_hi = 6.93147180369123816490e-01, ln2_lo = 1.90821492927058770002e-10;
 constexpr double two54 = 1.80143985094819840000e+16;
-constexpr double Lg1 = 6.666666666666735130e-01, Lg2 = 3.999999999940941908e-01, Lg3 = 2.857142874366239149e-01,
-                 Lg4 = 2.222219843214978396e-01, Lg5 = 1.818357216161805012e-01, Lg6 = 1.531383769920937332e-01,
-                 Lg7 = 1.479819860511658591e-01;
 
-// e_log.c
-NUSI_FN double log_i(double x)
+// log / log1p: table-driven, division-free (nusi_logtab.hpp, gen_logtab.py).  x = 2^k z,
+// z in [0x1.6p-1, 0x1.6p+0), c ~ the centre of z's 1/128 subinterval (c = 1 next to 1.0):
+//   log(x) = k ln2 + log(c) + log1p(r),  r = z/c - 1 = fma(z, invc, -1),  |r| < 2^-7,
+// k ln2 + log(c) + r summed with exact (Fast2Sum) error terms, log1p(r) - r by its Taylor
+// series to r^9.  Error < 0.52 ulp; replaces fdlibm e_log.c / s_log1p.c (one division and
+// ~20 integer / branch instructions each) with one table load and ~25 fp64 operations.
+constexpr double kLn2hi = 0x1.62e42fefa3800p-1, kLn2lo = 0x1.ef35793c76730p-45;   // k * kLn2hi exact
+// log(2^kadj * x) + c / x for a normal positive double x = from_bits(ix); c: log1p's rounding
+// correction of 1 + x (0 for log)
+NUSI_FN double log_kernel(unsigned long long ix, double c, int kadj)
 {
-    int hx = hiw(x);
-    const unsigned lx = low(x);
-    int k = 0;
-    if (hx < 0x00100000) {                       // x < 2^-1022
-        if (((hx & 0x7fffffff) | lx) == 0) return -1.0 / 0.0;
-        if (hx < 0) return (x - x) / 0.0;
-        k -= 54;
-        x *= two54;
-        hx = hiw(x);
-    }
-    if (hx >= 0x7ff00000) return x + x;
-    k += (hx >> 20) - 1023;
-    hx &= 0x000fffff;
-    int i = (hx + 0x95f64) & 0x100000;
-    x = with_hi(x, hx | (i ^ 0x3ff00000));       // normalise x or x/2
-    k += (i >> 20);
-    const double f = x - 1.0;
-    if ((0x000fffff & (2 + hx)) < 3) {           // |f| < 2^-20
-        if (f == 0.0) {
-            if (k == 0) return 0.0;
-            const double dk = (double)k;
-            return dk * ln2_hi + dk * ln2_lo;
-        }
-        const double R = f * f * (0.5 - 0.33333333333333333 * f);
-        if (k == 0) return f - R;
-        const double dk = (double)k;
-        return dk * ln2_hi - ((R - dk * ln2_lo) - f);
-    }
-    const double s = f / (2.0 + f);
-    const double dk = (double)k;
-    const double z = s * s;
-    i = hx - 0x6147a;
-    const double w = z * z;
-    const int j = 0x6b851 - hx;
-    const double t1 = w * (Lg2 + w * (Lg4 + w * Lg6));
-    const double t2 = z * (Lg1 + w * (Lg3 + w * (Lg5 + w * Lg7)));
-    i |= j;
-    const double R = t2 + t1;
-    if (i > 0) {
-        const double hfsq = 0.5 * f * f;
-        if (k == 0) return f - (hfsq - s * (hfsq + R));
-        return dk * ln2_hi - ((hfsq - (s * (hfsq + R) + dk * ln2_lo)) - f);
-    }
-    if (k == 0) return f - s * (f - R);
-    return dk * ln2_hi - ((s * (f - R) - dk * ln2_lo) - f);
+    const unsigned long long tmp = ix - 0x3fe6000000000000ULL;
+    const int i = (int)((tmp >> (52 - kLogTabBits)) & ((1u << kLogTabBits) - 1));
+    const int k = (int)((long long)tmp >> 52);
+    const double z = from_bits(ix - (tmp & (0xfffULL << 52)));
+    const double invc = kLogTab[i][0], lch = kLogTab[i][1], lcl = kLogTab[i][2];
+    const double r = fma(z, invc, -1.0);
+    const double kd = (double)(k + kadj);
+    const double t = kd * kLn2hi;
+    const double s1 = t + lch, e1 = (t - s1) + lch;   // |t| >= |lch| or t == 0
+    const double s2 = s1 + r, e2 = (s1 - s2) + r;     // |s1| >= |r| or s1 == 0
+    double q = fma(r, 1.0 / 9, -1.0 / 8);
+    q = fma(r, q, 1.0 / 7);
+    q = fma(r, q, -1.0 / 6);
+    q = fma(r, q, 1.0 / 5);
+    q = fma(r, q, -0.25);
+    q = fma(r, q, 1.0 / 3);
+    q = fma(r, q, -0.5);
+    const double p = (r * r) * q;
+    // c / x = c invc 2^-k / (1 + r) ~ sc (1 - r); 2^-k = 0 past the normal range (c / x negligible)
+    const double sc = c * (invc * ((k < 1023) ? from_bits((unsigned long long)(1023 - k) << 52) : 0.0));
+    return s2 + (((fma(kd, kLn2lo, lcl) + (e1 + e2)) + p) + fma(-sc, r, sc));
 }
 
-// s_log1p.c
+NUSI_FN double log_i(double x)
+{
+#ifdef NUSI_AB_STUB_LOG   // timing experiments only (scripts/build_variant.sh)
+    return (x - 1.0) * 0.9;
+#endif
+    const unsigned long long ix = bits(x);
+    if (ix - 0x0010000000000000ULL >= 0x7fe0000000000000ULL) {   // not a normal positive double
+        if (x != x || x == 1.0 / 0.0) return x + x;
+        if (x == 0.0) return -1.0 / 0.0;
+        if (x < 0.0) return (x - x) / 0.0;
+        return log_kernel(bits(x * 0x1p52), 0.0, -52);           // subnormal
+    }
+    return log_kernel(ix, 0.0, 0);
+}
+
+// log1p(x) = log(u) + c / u, u = 1 + x rounded, c its exact rounding error (Fast2Sum)
 NUSI_FN double log1p_i(double x)
 {
-    const int hx = hiw(x);
-    const int ax = hx & 0x7fffffff;
-    int k = 1, hu = 0;
-    double f = 0.0, c = 0.0;
-    if (hx < 0x3FDA827A) {                       // x < 0.41422
-        if (ax >= 0x3ff00000) {                  // x <= -1
-            if (x == -1.0) return -1.0 / 0.0;
-            return (x - x) / (x - x);
-        }
-        if (ax < 0x3e200000) {                   // |x| < 2^-29
-            if (ax < 0x3c900000) return x;       // |x| < 2^-54
-            return x - x * x * 0.5;
-        }
-        if (hx > 0 || hx <= (int)0xbfd2bec3) {   // -0.2929 < x < 0.41422
-            k = 0;
-            f = x;
-            hu = 1;
-        }
+#ifdef NUSI_AB_STUB_LOG
+    return x * 0.9;
+#endif
+    if (!(x > -1.0) || x == 1.0 / 0.0) {
+        if (x == -1.0) return -1.0 / 0.0;
+        if (x != x || x > 0.0) return x + x;
+        return (x - x) / (x - x);
     }
-    if (hx >= 0x7ff00000) return x + x;
-    if (k != 0) {
-        double u;
-        if (hx < 0x43400000) {
-            u = 1.0 + x;
-            hu = hiw(u);
-            k = (hu >> 20) - 1023;
-            c = (k > 0) ? 1.0 - (u - x) : x - (u - 1.0);   // correction term
-            c /= u;
-        } else {
-            u = x;
-            hu = hiw(u);
-            k = (hu >> 20) - 1023;
-            c = 0;
-        }
-        hu &= 0x000fffff;
-        if (hu < 0x6a09e) {
-            u = with_hi(u, hu | 0x3ff00000);     // normalise u
-        } else {
-            k += 1;
-            u = with_hi(u, hu | 0x3fe00000);     // normalise u/2
-            hu = (0x00100000 - hu) >> 2;
-        }
-        f = u - 1.0;
-    }
-    const double hfsq = 0.5 * f * f;
-    if (hu == 0) {                               // |f| < 2^-20
-        if (f == 0.0) {
-            if (k == 0) return 0.0;
-            c += k * ln2_lo;
-            return k * ln2_hi + c;
-        }
-        const double R = hfsq * (1.0 - 0.66666666666666666 * f);
-        if (k == 0) return f - R;
-        return k * ln2_hi - ((R - (k * ln2_lo + c)) - f);
-    }
-    const double s = f / (2.0 + f);
-    const double z = s * s;
-    const double R = z * (Lg1 + z * (Lg2 + z * (Lg3 + z * (Lg4 + z * (Lg5 + z * (Lg6 + z * Lg7))))));
-    if (k == 0) return f - (hfsq - s * (hfsq + R));
-    return k * ln2_hi - ((hfsq - (s * (hfsq + R) + (k * ln2_lo + c))) - f);
+    const double u = 1.0 + x;
+    const double c = (x >= 1.0) ? 1.0 - (u - x) : x - (u - 1.0);
+    return log_kernel(bits(u), c, 0);
 }
 
 // e_exp.c
@@ -212,6 +161,9 @@ NUSI_FN double exp_i(double x)
 // s_atan.c
 NUSI_FN double atan_i(double x)
 {
+#ifdef NUSI_AB_STUB_ATAN
+    return x * 0.9;
+#endif
     constexpr double atanhi[4] = {4.63647609000806093515e-01, 7.85398163397448278999e-01, 9.82793723247329054082e-01,
                                   1.57079632679489655800e+00};
     constexpr double atanlo[4] = {2.26987774529616870924e-17, 3.06161699786838301793e-17, 1.39033110312309984516e-17,
@@ -270,6 +222,9 @@ NUSI_FN double atan_i(double x)
 // e_atan2.c
 NUSI_FN double atan2_i(double y, double x)
 {
+#ifdef NUSI_AB_STUB_ATAN
+    return y * 0.9 + x * 0.1;
+#endif
     constexpr double pi_o_2 = 1.5707963267948965580E+00, pi = 3.1415926535897931160E+00,
                      pi_lo = 1.2246467991473531772E-16, pi_o_4 = 7.8539816339744827900E-01;
     const int hx = hiw(x), hy = hiw(y);

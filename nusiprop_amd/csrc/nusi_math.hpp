@@ -109,6 +109,9 @@ NUSI_FN double li2_useries(double u)
 // Re Li2(x) for real x (gsl_sf_dilog semantics)
 NUSI_FN_OUT double li2(double x)
 {
+#ifdef NUSI_AB_STUB_LI2   // timing experiments only (scripts/build_variant.sh)
+    return 0.5 * x;
+#endif
     double add = 0.0, sgn = 1.0;
     if (fabs(x) > 1.0) {   // x > 1: 2 zeta2 - log^2(x)/2 ; x < -1: -zeta2 - log^2(-x)/2 (one log for both)
         const double L = NUSI_PLOG(fabs(x));
@@ -130,6 +133,9 @@ NUSI_FN_OUT double li2(double x)
 NUSI_FN_OUT cd cli2(double x, double y)
 {
     if (y == 0.0) return cd{li2(x), (x >= 1.0) ? -kPi * NUSI_PLOG(x) : 0.0};
+#ifdef NUSI_AB_STUB_CLI2   // timing experiments only
+    return C(0.5 * x, 0.5 * y);
+#endif
     cd z = C(x, y), add = C(0.0);
     double sgn = 1.0;
     if (x * x + y * y > 1.0) {
