@@ -87,40 +87,65 @@ __device__ __attribute__((noinline)) double lum_out(const Point& P, double z, do
 // Zdr, M = I + offdiag and its LU (nuSIprop.hpp:289-310) and the source term c_i Lum (:283).
 // 1/dE_b and 1/Zdr are multiplied in (the reference divides; M's off-diagonals are ~1e-22 of
 // the diagonal), the power-law source reads pw[]; the DSNB source is evaluated in full.
+__device__ __attribute__((noinline)) void lu3_factor_out(double (&A)[3][3], int (&perm)[3]) { lu3_factor(A, perm); }
+
 NUSI_FN void cascade_record(const GridDev& g, const Point& P, const double* __restrict__ Gt,
                             const double* __restrict__ At, const double* rdE, const double* pw, int i, int b,
                             double* R, int stride)
 {
     const double c = g.step_c[i], s = g.step_s[i];
-    const double uk[3] = {P.u[0], P.u[1], P.u[2]};
+    const double u0 = P.u[0], u1 = P.u[1], u2 = P.u[2];
     const double rd = rdE[b];
     const double Gw = s * Gt[b + i - 1], Aw = s * At[b + i - 1];
-    double rz[3], M[3][3];
-    for (int k = 0; k < 3; ++k) rz[k] = 1.0 / (1.0 + c * (Gw * uk[k] - Aw * (uk[k] * uk[k])) * rd);
-    for (int k = 0; k < 3; ++k)
-        for (int l = 0; l < 3; ++l) M[k][l] = (k == l) ? 1.0 : Aw * uk[k] * uk[l] * rd * rz[k];
-    int pm[3];
-    lu3_factor(M, pm);
+    const double rz0 = 1.0 / (1.0 + c * (Gw * u0 - Aw * (u0 * u0)) * rd);
+    const double rz1 = 1.0 / (1.0 + c * (Gw * u1 - Aw * (u1 * u1)) * rd);
+    const double rz2 = 1.0 / (1.0 + c * (Gw * u2 - Aw * (u2 * u2)) * rd);
+    R[PR_RZ0 * stride] = rz0;
+    R[PR_RZ1 * stride] = rz1;
+    R[PR_RZ2 * stride] = rz2;
+    // M = I + offdiag, M[k][l] = Aw u_k u_l / dE_b / Zdr_k
+    const double m01 = Aw * u0 * u1 * rd * rz0, m02 = Aw * u0 * u2 * rd * rz0;
+    const double m10 = Aw * u1 * u0 * rd * rz1, m12 = Aw * u1 * u2 * rd * rz1;
+    const double m20 = Aw * u2 * u0 * rd * rz2, m21 = Aw * u2 * u1 * rd * rz2;
+    // LU without row exchanges when partial pivoting would not exchange (M ~ I: always, in
+    // practice); the same operations as lu3_factor on that path (a / 1.0 == a), else lu3_factor
+    const double a11 = 1.0 - m10 * m01, a12 = m12 - m10 * m02;
+    const double a21 = m21 - m20 * m01, a22 = 1.0 - m20 * m02;
+    if (fabs(m10) <= 1.0 && fabs(m20) <= 1.0 && fabs(a21) <= fabs(a11) && a11 != 0.0) {
+        const double l21 = a21 / a11;
+        const double u22 = a22 - l21 * a12;
+        R[PR_L10 * stride] = m10;
+        R[PR_L20 * stride] = m20;
+        R[PR_L21 * stride] = l21;
+        R[PR_U01 * stride] = m01;
+        R[PR_U02 * stride] = m02;
+        R[PR_U12 * stride] = a12;
+        R[PR_RU00 * stride] = 1.0;
+        R[PR_RU11 * stride] = 1.0 / a11;
+        R[PR_RU22 * stride] = 1.0 / u22;
+        R[kPreFields * stride] = (double)(0 | (1 << 2) | (2 << 4));
+    } else {
+        double M[3][3] = {{1.0, m01, m02}, {m10, 1.0, m12}, {m20, m21, 1.0}};
+        int pm[3];
+        lu3_factor_out(M, pm);
+        R[PR_L10 * stride] = M[1][0];
+        R[PR_L20 * stride] = M[2][0];
+        R[PR_L21 * stride] = M[2][1];
+        R[PR_U01 * stride] = M[0][1];
+        R[PR_U02 * stride] = M[0][2];
+        R[PR_U12 * stride] = M[1][2];
+        R[PR_RU00 * stride] = 1.0 / M[0][0];
+        R[PR_RU11 * stride] = 1.0 / M[1][1];
+        R[PR_RU22 * stride] = 1.0 / M[2][2];
+        R[kPreFields * stride] = (double)(pm[0] | (pm[1] << 2) | (pm[2] << 4));
+    }
     double src;
     if (P.source == 1)   // nuSIprop.hpp:656
         src = P.norm_total / 3.0 * g.sfr[i] * (g.Emax[b] * pw[b + i + 1] - g.Emin[b] * pw[b + i]) / (1 - P.si);
     else
         src = lum_out(P, g.z[i], g.sfr[i], g.Emin[b], g.Emax[b]);
-    R[PR_RZ0 * stride] = rz[0];
-    R[PR_RZ1 * stride] = rz[1];
-    R[PR_RZ2 * stride] = rz[2];
     R[PR_SRC * stride] = c * src;
-    R[PR_L10 * stride] = M[1][0];
-    R[PR_L20 * stride] = M[2][0];
-    R[PR_L21 * stride] = M[2][1];
-    R[PR_U01 * stride] = M[0][1];
-    R[PR_U02 * stride] = M[0][2];
-    R[PR_U12 * stride] = M[1][2];
-    R[PR_RU00 * stride] = 1.0 / M[0][0];
-    R[PR_RU11 * stride] = 1.0 / M[1][1];
-    R[PR_RU22 * stride] = 1.0 / M[2][2];
     R[PR_SDE * stride] = P.non_resonant ? s * rd : (g.Emax[b] - g.Emin[b]);
-    R[kPreFields * stride] = (double)(pm[0] | (pm[1] << 2) | (pm[2] << 4));
 }
 
 // the 3x3 solve of one bin (nuSIprop.hpp:289-313) from its fields and the coupling `add` to the
@@ -462,10 +487,14 @@ __global__ __launch_bounds__(64) void k_cascade_reg(GridDev g, const Point* __re
 // ---------------------------------------------------------------------------
 constexpr int kWfFields = kPreFields + 1;   // PR_* and the permutation
 #ifndef NUSI_WF_AB
-#define NUSI_WF_AB 0   // timing experiments only: 1 skip records, 2 skip push, 4 skip solve
+#define NUSI_WF_AB 0   // timing experiments only: 1 skip records, 2 skip push, 4 skip solve, 8 no alpha loads
 #endif
 constexpr int kWfMaxThreads = 512;
 constexpr int kWfRows = 4, kWfQuarters = 4;   // push: rows per thread, step groups per row group
+#ifndef NUSI_WF_PRE
+#define NUSI_WF_PRE 2
+#endif
+constexpr int kWfPre = NUSI_WF_PRE;           // alpha columns in flight (stages of prefetch)
 
 template <int NJ>
 __global__ __launch_bounds__(kWfMaxThreads) void k_cascade_wf(GridDev g, const Point* __restrict__ pts, TablesDev t,
@@ -504,13 +533,20 @@ __global__ __launch_bounds__(kWfMaxThreads) void k_cascade_wf(GridDev g, const P
     const int ist = Nz - 1 - tid;
     const double cj = (tid < nst) ? g.step_c[ist] : 0.0, sj = (tid < nst) ? g.step_s[ist] : 0.0;
     double racc = 0.0, px0 = 0.0, px1 = 0.0, px2 = 0.0;
-    double a_cur[kWfRows];   // alpha(row, r) of this stage's column, rows clamped into the column
+    // alpha(row, column) of the next kWfPre stages' columns (ring, [0] = this stage's), rows clamped
+    // into the column; each load is issued kWfPre stages before its use (HBM latency > a stage)
+    auto load_col = [&](int col, double (&dst)[kWfRows]) {
+        const size_t cb = (size_t)col * (col - 1) / 2;
 #pragma unroll
-    for (int c = 0; c < kWfRows; ++c) {
-        const int row = row0 + c;
-        a_cur[c] = (nonres && T >= 2) ? Al[(size_t)(T - 1) * (T - 2) / 2 + (row < T - 2 ? row : T - 2)] : 0.0;
-    }
-
+        for (int c = 0; c < kWfRows; ++c) {
+            const int row = row0 + c;
+            dst[c] = (nonres && col >= 1) ? ((NUSI_WF_AB & 8) ? 1e-300 * row : Al[cb + (row < col - 1 ? row : col - 1)])
+                                          : 0.0;
+        }
+    };
+    double a_ring[kWfPre][kWfRows];
+#pragma unroll
+    for (int d = 0; d < kWfPre; ++d) load_col(T - 1 - d, a_ring[d]);
     for (int sg = 0; sg < T; ++sg) {
         const int r = T - 1 - sg;
         const int ks = sg % K;
@@ -558,19 +594,12 @@ __global__ __launch_bounds__(kWfMaxThreads) void k_cascade_wf(GridDev g, const P
         // ---- P2: push column r into rows < r.  Rows >= r were consumed already and steps that
         // have not started have T_j = 0 (their accumulators stay exactly 0), so nothing is masked.
         if (nonres && r >= 1 && !(NUSI_WF_AB & 2)) {
-            double a_next[kWfRows];
-            const size_t cn = (size_t)(r - 1) * (r - 2) / 2;
-#pragma unroll
-            for (int c = 0; c < kWfRows; ++c) {
-                const int row = row0 + c;
-                a_next[c] = (r >= 2) ? Al[cn + (row < r - 2 ? row : r - 2)] : 0.0;
-            }
             const double* Th = Tp + h * JG;
 #pragma unroll
             for (int jj = 0; jj < JG; ++jj) {
                 const double tj = Th[jj];
 #pragma unroll
-                for (int c = 0; c < kWfRows; ++c) acc[c][jj] = fma(a_cur[c], tj, acc[c][jj]);
+                for (int c = 0; c < kWfRows; ++c) acc[c][jj] = fma(a_ring[0][c], tj, acc[c][jj]);
             }
             if (r - 1 >= row0 && r - 1 < row0 + kWfRows) {   // publish row r-1 for the next chain
                 const int cp = r - 1 - row0;
@@ -582,7 +611,10 @@ __global__ __launch_bounds__(kWfMaxThreads) void k_cascade_wf(GridDev g, const P
                     }
             }
 #pragma unroll
-            for (int c = 0; c < kWfRows; ++c) a_cur[c] = a_next[c];
+            for (int d = 0; d + 1 < kWfPre; ++d)
+#pragma unroll
+                for (int c = 0; c < kWfRows; ++c) a_ring[d][c] = a_ring[d + 1][c];
+            load_col(r - kWfPre, a_ring[kWfPre - 1]);
         }
         __syncthreads();
     }
