@@ -40,6 +40,7 @@ struct AlphaTilesDev {
     int* tiles = nullptr;   // device [ncore + nmixed + nfull]
     int ncls[3] = {0, 0, 0};
     int cs_max[3] = {0, 0, 0}, ct_max[3] = {0, 0, 0};
+    int ext_lo = 0;          // bins [ext_lo, T) x [ext_lo, T) are built by the per-entry kernel
 };
 // Classify the tiles of a grid on the host; `shared[n]` = (hi[n] == lo[n+1]) bitwise.
 hipError_t alpha_tiles_create(int T, const unsigned char* shared, AlphaTilesDev* out);

@@ -31,23 +31,27 @@ __global__ __launch_bounds__(64) void k_gamma_alphat(GridDev g, const Point* __r
     if (w) atomicOr(&warn[p], w);
 }
 
-__global__ __launch_bounds__(256) void k_alpha(GridDev g, const Point* __restrict__ pts, SplineSet spl,
+// one entry per work-item over the bins [nlo, T) x [nlo, T), n < m (nlo = 0: the whole table)
+__global__ __launch_bounds__(256) void k_alpha(GridDev g, const Point* __restrict__ pts, SplineSet spl, int nlo,
                                                double* __restrict__ A, int* __restrict__ warn)
 {
     const int p = blockIdx.y;
+    const long long L = g.T - nlo;
     const long long e = (long long)blockIdx.x * 256 + threadIdx.x;
-    if (e >= g.PT) return;
-    // packed transposed index e = m(m-1)/2 + n, n < m
+    if (e >= L * (L - 1) / 2) return;
+    // packed transposed index e = m'(m'-1)/2 + n', n' < m', within the sub-triangle
     int m = (int)((1.0 + sqrt(1.0 + 8.0 * (double)e)) * 0.5);
     while ((long long)m * (m - 1) / 2 > e) --m;
     while ((long long)(m + 1) * m / 2 <= e) ++m;
-    const int n = (int)(e - (long long)m * (m - 1) / 2);
+    int n = (int)(e - (long long)m * (m - 1) / 2);
+    n += nlo;
+    m += nlo;
     const Point& P = pts[p];
     int w = 0;
     double v = 0.0;
     // without non-s channels the cascade reads only alpha(n, n+1) (nuSIprop.hpp:273-275)
     if (P.non_resonant || m == n + 1) v = alpha_entry(P, spl, g.lo[n], g.hi[n], g.lo[m], g.hi[m], w);
-    A[(size_t)p * g.PT + e] = v;
+    A[(size_t)p * g.PT + (size_t)m * (m - 1) / 2 + n] = v;
     if (w) atomicOr(&warn[p], w);
 }
 
@@ -152,12 +156,22 @@ hipError_t alpha_tiles_create(int T, const unsigned char* shared, AlphaTilesDev*
     for (int t = 0; t < nt; ++t)
         for (int j = t * kAlphaTile; j < (t + 1) * kAlphaTile && j < T; ++j)
             ne[t] += (j > t * kAlphaTile && shared[j - 1]) ? 1 : 2;
-    // class 0: both sides <= 16 edges; 1: t side <= 16, S' side <= 30; 2: both <= 30
+    // class 0: both sides <= 16 edges; 1: t side <= 16, S' side <= 30; 2: both <= 30.  From the
+    // first tile t0 whose bins do not share edges (the redshift-extended bins) on, tiles of class 2
+    // save no corner (4 per entry, like the per-entry path) and their 80-KB LDS footprint halves the
+    // occupancy: the bins [15 t0, T) x [15 t0, T) go to the per-entry kernel instead (ext_lo).
     const int cap_core = kAlphaTile + 1, cap_ext = 2 * kAlphaTile;
+    int t0 = nt;
+    for (int t = 0; t < nt; ++t)
+        if (ne[t] > cap_core) { t0 = t; break; }
+    bool tail_ext = true;   // no bin from tile t0 on shares an edge with its neighbour
+    for (int n = t0 * kAlphaTile; n + 1 < T; ++n) tail_ext = tail_ext && !shared[n];
+    out->ext_lo = (tail_ext && t0 < nt) ? t0 * kAlphaTile : T;
     std::vector<int> cls[3];
     for (int tm = 0; tm < nt; ++tm)
         for (int tn = 0; tn <= tm; ++tn) {
             const int c = (ne[tn] <= cap_core && ne[tm] <= cap_core) ? 0 : (ne[tn] <= cap_core) ? 1 : 2;
+            if (tn * kAlphaTile >= out->ext_lo) continue;   // per-entry region
             cls[c].push_back(tn | (tm << 16));
         }
     const int csm[3] = {cap_core, cap_ext, cap_ext}, ctm[3] = {cap_core, cap_core, cap_ext};
@@ -183,11 +197,17 @@ hipError_t launch_alpha(const GridDev& g, const Point* pts, int npts, const Spli
                         TablesDev t, int* warn, hipStream_t s)
 {
     static const bool per_entry = getenv("NUSI_ALPHA_PER_ENTRY") != nullptr;   // A/B switch
+    auto per_entry_region = [&](int nlo) {
+        const long long L = g.T - nlo, ne = L * (L - 1) / 2;
+        if (ne <= 0) return;
+        dim3 grid((unsigned)((ne + 255) / 256), npts);
+        hipLaunchKernelGGL(k_alpha, grid, dim3(256), 0, s, g, pts, spl, nlo, t.A, warn);
+    };
     if (per_entry) {
-        dim3 grid((unsigned)((g.PT + 255) / 256), npts);
-        hipLaunchKernelGGL(k_alpha, grid, dim3(256), 0, s, g, pts, spl, t.A, warn);
+        per_entry_region(0);
         return hipGetLastError();
     }
+    per_entry_region(at.ext_lo);
     int off = 0;
     for (int c = 0; c < 3; ++c) {
         if (at.ncls[c] == 0) continue;
