@@ -120,10 +120,10 @@ NUSI_FN_OUT double li2(double x)
         x = 1.0 / x;
     }
     if (x == 1.0) return add + sgn * kZeta2;
-    if (x > 0.5) {
-        add += sgn * (kZeta2 - NUSI_PLOG(x) * NUSI_PLOG1P(-x));
-        sgn = -sgn;
-        x = 1.0 - x;
+    if (x > 0.5) {   // Li2(x) = zeta2 - log(x) log(1-x) - Li2(1-x); the series of Li2(1-x) takes u = -log(x)
+        const double lx = NUSI_PLOG(x);
+        add += sgn * (kZeta2 - lx * NUSI_PLOG1P(-x));
+        return add - sgn * li2_useries(-lx);
     }
     if (x == 0.0) return add;
     return add + sgn * li2_useries(-NUSI_PLOG1P(-x));
@@ -144,14 +144,16 @@ NUSI_FN_OUT cd cli2(double x, double y)
         sgn = -1.0;
         z = 1.0 / z;
     }
-    if (z.r > 0.5) {
-        add = add + sgn * (kZeta2 - clog_p(z) * clog_p(1.0 - z));
+    cd u;   // u = -log(1 - z) of the series' argument
+    if (z.r > 0.5) {   // Li2(z) = zeta2 - log(z) log(1-z) - Li2(1-z); for Li2(1-z), u = -log(z)
+        const cd lz = clog_p(z);
+        add = add + sgn * (kZeta2 - lz * clog_p(1.0 - z));
         sgn = -sgn;
-        z = 1.0 - z;
+        u = C(-lz.r, -lz.i);
+    } else {   // formed without the cancellation of 1 - z for small z
+        const double a = -z.r, b = -z.i;
+        u = C(-0.5 * NUSI_PLOG1P(2.0 * a + (a * a + b * b)), -NUSI_PATAN2(b, 1.0 + a));
     }
-    // u = -log(1 - z), formed without the cancellation of 1 - z for small z
-    const double a = -z.r, b = -z.i;
-    const cd u = C(-0.5 * NUSI_PLOG1P(2.0 * a + (a * a + b * b)), -NUSI_PATAN2(b, 1.0 + a));
     const cd u2 = u * u;
     cd p = C(kLi2Bern[kLi2Terms - 1]);
 #pragma unroll

@@ -46,10 +46,10 @@ double ora_dilog(double x)
         x = 1.0 / x;
     }
     if (x == 1.0) return add + sgn * ZETA2;
-    if (x > 0.5) {
-        add += sgn * (ZETA2 - ora_log(x) * ora_log1p(-x));
-        sgn = -sgn;
-        x = 1.0 - x;
+    if (x > 0.5) {   /* Li2(x) = zeta2 - log(x) log(1-x) - Li2(1-x); the series of Li2(1-x) takes u = -log(x) */
+        const double lx = ora_log(x);
+        add += sgn * (ZETA2 - lx * ora_log1p(-x));
+        return add - sgn * li2_useries(-lx);
     }
     if (x == 0.0) return add;
     return add + sgn * li2_useries(-ora_log1p(-x));
@@ -74,14 +74,17 @@ void ora_complex_dilog_xy(double x, double y, double *re, double *im)
         sgn = -1.0;
         z = zrdiv(1.0, z);
     }
-    if (z.r > 0.5) {
-        const zc P = zmul(zlog(z), zlog(zmk(1.0 - z.r, -z.i)));
+    zc u;   /* u = -log(1 - z) of the series' argument */
+    if (z.r > 0.5) {   /* Li2(z) = zeta2 - log(z) log(1-z) - Li2(1-z); for Li2(1-z), u = -log(z) */
+        const zc lz = zlog(z);
+        const zc P = zmul(lz, zlog(zmk(1.0 - z.r, -z.i)));
         add = zadd(add, zscale(sgn, zmk(ZETA2 - P.r, -P.i)));
         sgn = -sgn;
-        z = zmk(1.0 - z.r, -z.i);
+        u = zmk(-lz.r, -lz.i);
+    } else {
+        const double a = -z.r, b = -z.i;
+        u = zmk(-0.5 * ora_log1p(2.0 * a + (a * a + b * b)), -ora_atan2(b, 1.0 + a));
     }
-    const double a = -z.r, b = -z.i;
-    const zc u = zmk(-0.5 * ora_log1p(2.0 * a + (a * a + b * b)), -ora_atan2(b, 1.0 + a));
     const zc u2 = zmul(u, u);
     zc p = zmk(ora_li2_bern_d[ORA_LI2D_N - 1], 0.0);
     for (int k = ORA_LI2D_N - 2; k >= 0; --k) {
