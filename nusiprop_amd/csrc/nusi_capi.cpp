@@ -435,6 +435,7 @@ int build_point(nusi_plan* pl, const nusi_params& p, nusi::Point& P)
     P.non_resonant = p.non_resonant ? 1 : 0;
     P.phiphi = p.phiphi ? 1 : 0;
     P.source = p.source_model;
+    nusi::point_derive(P);
     if (P.non_resonant && P.phiphi && !pl->spl)
         return fail(NUSI_ETABLE, "phiphi requested but the phi-phi tables are not loaded (nusi_plan_load_phiphi)");
     return NUSI_OK;

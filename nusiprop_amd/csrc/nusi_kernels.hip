@@ -98,12 +98,18 @@ __global__ __launch_bounds__(kTileThreads) NUSI_TILE_ATTR void k_alpha_tile(Grid
     __shared__ double tE[2 * kAlphaTile], sE[2 * kAlphaTile];
     __shared__ int tl[kAlphaTile], th[kAlphaTile], sl[kAlphaTile], sh[kAlphaTile];
     __shared__ int cnt[2];
+    __shared__ double elo[2][kAlphaTile], ehi[2][kAlphaTile];   // bin edges of both sides, staged in parallel
     const int p = blockIdx.y, tid = threadIdx.x, T = g.T;
     const int tw = tiles[blockIdx.x];
     const int n0 = (tw & 0xffff) * kAlphaTile, m0 = (tw >> 16) * kAlphaTile;
     const Point& P = pts[p];
-    if (tid == 0) cnt[0] = alpha_edge_list(g.lo, g.hi, n0, T, tE, tl, th);
-    if (tid == 64) cnt[1] = alpha_edge_list(g.lo, g.hi, m0, T, sE, sl, sh);
+    if (tid < 2 * kAlphaTile) {
+        const int side = tid / kAlphaTile, j = tid - side * kAlphaTile, b = (side ? m0 : n0) + j;
+        if (b < T) { elo[side][j] = g.lo[b]; ehi[side][j] = g.hi[b]; }
+    }
+    __syncthreads();
+    if (tid == 0) cnt[0] = alpha_edge_list(elo[0], ehi[0], 0, T - n0, tE, tl, th);
+    if (tid == 64) cnt[1] = alpha_edge_list(elo[1], ehi[1], 0, T - m0, sE, sl, sh);
     __syncthreads();
     const int ct = cnt[0], cs = cnt[1], cc = cs * ct;
     const int ln = tid % kAlphaTile, lm = tid / kAlphaTile;
@@ -125,13 +131,14 @@ __global__ __launch_bounds__(kTileThreads) NUSI_TILE_ATTR void k_alpha_tile(Grid
         __syncthreads();   // edge leaves written / previous k's corners consumed
 #ifndef NUSI_AB_NO_CORNERS   // timing experiments only (scripts/build_variant.sh)
         if (nonres && maj) {
-            for (int j = tid; j < cc; j += kTileThreads) alpha_tile_corner_job(P, k, j, tE, ct, sE, cc, cor);
+            const double* edgk = edg + k * alpha_tile_edge_stride(cs, ct);
+            for (int j = tid; j < cc; j += kTileThreads) alpha_tile_corner_job(P, j, edgk, ct, cs, cor);
 #ifndef NUSI_AB_NO_MIXED
             for (int j = tid; j < kAlphaTile * (cs + ct); j += kTileThreads)
 #else
             for (int j = tid; j < 0; j += kTileThreads)
 #endif
-                alpha_tile_mixed_job(P, k, j, tE, ct, sE, cs, tl, th, sl, sh, n0, m0, T, cor);
+                alpha_tile_mixed_job(j, edgk, ct, cs, tl, th, sl, sh, n0, m0, T, cor);
         }
 #endif
         __syncthreads();

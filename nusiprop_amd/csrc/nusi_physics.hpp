@@ -38,7 +38,25 @@ struct Point {
     int majorana, non_resonant, phiphi, source;
     int tslot;           // Stage-A table slot of this point (points that differ only in si / norm /
                          // source share their tables: nuSIprop.hpp:217-253 read none of them)
+    // alpha()'s entry-independent factors (point_derive), each the exact subexpression the
+    // reference evaluates per entry (nuSIprop.hpp:1243-1275, 1430, 1505)
+    double a_wgt[3];     // m_phi^4 / (2 m_k)
+    double a_s;          // g^4 / (8 pi Ga m_phi^3)
+    double a_st;         // g^4 / (32 pi (1 + gr^2) m_phi^4)
+    double a_nrm;        // (g / m_phi)^4
+    double a_gr;         // Ga / m_phi
 };
+NUSI_FN void point_derive(Point& P)
+{
+    const double g = P.g, mphi = P.mphi, Ga = P.Ga;
+    const double g4 = (g * g) * (g * g), m4 = (mphi * mphi) * (mphi * mphi);
+    const double gr = Ga / mphi, gr2 = gr * gr;
+    for (int k = 0; k < 3; ++k) P.a_wgt[k] = m4 / (2 * P.mn[k]);
+    P.a_s = g4 / (8 * kPi * Ga * (mphi * mphi * mphi));
+    P.a_st = g4 / (32 * kPi * (1 + gr2) * m4);
+    P.a_nrm = (g / mphi) * (g / mphi) * ((g / mphi) * (g / mphi));
+    P.a_gr = gr;
+}
 
 enum { kWarnGamma = 1, kWarnAlphaTilde = 2, kWarnAlpha = 4, kWarnSplineOOB = 8 };
 
@@ -389,7 +407,7 @@ NUSI_FN double alphat_entry(const Point& P, const SplineSet& spl, double Em, dou
         }
         tot += wgt * app;
 
-        const double nrm = (g / mphi) * (g / mphi) * ((g / mphi) * (g / mphi));
+        const double nrm = P.a_nrm;
         if (as < 0 || at < 0 || au < 0 || atu / nrm < -1e-11 || (ast + at + as) / nrm < -1e-11 || (asu + au + as) / nrm < -1e-11)
             warn |= kWarnAlphaTilde;
     }
@@ -491,9 +509,14 @@ NUSI_FN void alpha_mbin(double Sm, double Sp, double mphi, double Ga, AlphaMBin&
     b.atd = (Sp < 1e-5) ? 0.0 : atandiff(mphi * (Sp - 1) / Ga, mphi * (Sm - 1) / Ga);
 }
 
+constexpr int kCornerFields = 10, kTEdgeFields = 6, kSEdgeFields = 6, kMBinFields = 3;
+constexpr int kTEdgeVal = 5, kSEdgeVal = 5;   // edge field holding t resp. S' itself (alpha_t / alpha_S)
+
 // leaves evaluated on the spot (per-entry path, host checks)
 struct DirectLeaves {
     double gr, gr2, mphi, Ga;
+    NUSI_FN double tval(int, double mk, double E, double m2) const { return alpha_t(mk, E, m2); }
+    NUSI_FN double Sval(int, double mk, double E, double m2) const { return alpha_S(mk, E, m2); }
     NUSI_FN AlphaCorner corner(int, int, double S, double t) const { AlphaCorner c; alpha_corner(S, t, gr, c); return c; }
     NUSI_FN AlphaTEdge tedge(int, double t) const { AlphaTEdge e; alpha_tedge(t, gr2, e); return e; }
     NUSI_FN AlphaSEdge sedge(int, double S) const { AlphaSEdge e; alpha_sedge(S, gr, gr2, e); return e; }
@@ -529,10 +552,11 @@ struct TileLeaves {
     {
         return AlphaMBin{mbv[mb], mbv[kAlphaTile + mb], mbv[2 * kAlphaTile + mb]};
     }
+    NUSI_FN double tval(int ti, double, double, double) const { return ted[kTEdgeVal * ct + tidx[ti]]; }
+    NUSI_FN double Sval(int si, double, double, double) const { return sed[kSEdgeVal * cs + sidx[si]]; }
     NUSI_FN double xlog(int si, double, double, double) const { return xl[sidx[si] * kAlphaTile + nb]; }
     NUSI_FN double ylog(int ti, double, double, double) const { return yl[mb * ct + tidx[ti]]; }
 };
-constexpr int kCornerFields = 10, kTEdgeFields = 5, kSEdgeFields = 5, kMBinFields = 3;
 // per-k leaf block of the corner phase: corners, then xlog [cs][kAlphaTile], then ylog [kAlphaTile][ct]
 NUSI_FN int alpha_tile_corner_block(int cs, int ct) { return kCornerFields * cs * ct + kAlphaTile * (cs + ct); }
 
@@ -567,15 +591,19 @@ NUSI_FN void alpha_tile_edge_job(const Point& P, int job, const double* tE, int 
     double* sed = ted + kTEdgeFields * ct;
     double* mbv = sed + kSEdgeFields * cs;
     if (j < ct) {
+        const double t = alpha_t(mk, tE[j], m2);
+        ted[kTEdgeVal * ct + j] = t;
         if (!P.non_resonant) return;
         AlphaTEdge e;
-        alpha_tedge(alpha_t(mk, tE[j], m2), gr2, e);
+        alpha_tedge(t, gr2, e);
         ted[j] = e.Lm1; ted[ct + j] = e.la; ted[2 * ct + j] = e.cm; ted[3 * ct + j] = e.L2; ted[4 * ct + j] = e.am;
     } else if (j < ct + cs) {
-        if (!P.non_resonant) return;
         const int q = j - ct;
+        const double S = alpha_S(mk, sE[q], m2);
+        sed[kSEdgeVal * cs + q] = S;
+        if (!P.non_resonant) return;
         AlphaSEdge e;
-        alpha_sedge(alpha_S(mk, sE[q], m2), gr, gr2, e);
+        alpha_sedge(S, gr, gr2, e);
         sed[q] = e.lS; sed[cs + q] = e.l2; sed[2 * cs + q] = e.Ls; sed[3 * cs + q] = e.cS; sed[4 * cs + q] = e.lS2;
     } else {
         const int q = j - ct - cs;
@@ -585,34 +613,34 @@ NUSI_FN void alpha_tile_edge_job(const Point& P, int job, const double* tE, int 
         mbv[q] = b.lr; mbv[kAlphaTile + q] = b.lr2; mbv[2 * kAlphaTile + q] = b.atd;
     }
 }
-// job j in [0, cs ct): corner (S' slot j / ct, t slot j % ct) of mass state k
-NUSI_FN void alpha_tile_corner_job(const Point& P, int k, int j, const double* tE, int ct, const double* sE, int cc,
-                                   double* cor)
+// job j in [0, cs ct): corner (S' slot j / ct, t slot j % ct) of mass state k; edgk = the edge
+// block of mass state k (its t and S' values)
+NUSI_FN void alpha_tile_corner_job(const Point& P, int j, const double* edgk, int ct, int cs, double* cor)
 {
-    const double mphi = P.mphi, m2 = mphi * mphi, gr = P.Ga / mphi, mk = P.mn[k];
+    const int cc = cs * ct;
     const int si = j / ct, ti = j - si * ct;
     AlphaCorner c;
-    alpha_corner(alpha_S(mk, sE[si], m2), alpha_t(mk, tE[ti], m2), gr, c);
+    alpha_corner(edgk[kTEdgeFields * ct + kSEdgeVal * cs + si], edgk[kTEdgeVal * ct + ti], P.a_gr, c);
     cor[j] = c.L; cor[cc + j] = c.LL; cor[2 * cc + j] = c.TU1; cor[3 * cc + j] = c.TU2; cor[4 * cc + j] = c.G;
     cor[5 * cc + j] = c.Drr; cor[6 * cc + j] = c.Dri; cor[7 * cc + j] = c.Dcr; cor[8 * cc + j] = c.Dci; cor[9 * cc + j] = c.A;
 }
 // job j in [0, kAlphaTile (cs + ct)): the xlog leaf (S' slot, n bin) or the ylog leaf (m bin, t slot)
 // of mass state k, into the block after the corners; bins past the table are skipped
-NUSI_FN void alpha_tile_mixed_job(const Point& P, int k, int j, const double* tE, int ct, const double* sE, int cs,
-                                  const int* tl, const int* th, const int* sl, const int* sh, int n0, int m0, int T,
-                                  double* cor)
+NUSI_FN void alpha_tile_mixed_job(int j, const double* edgk, int ct, int cs, const int* tl, const int* th,
+                                  const int* sl, const int* sh, int n0, int m0, int T, double* cor)
 {
-    const double mphi = P.mphi, m2 = mphi * mphi, mk = P.mn[k];
+    const double* tv = edgk + kTEdgeVal * ct;                           // t of each t slot
+    const double* sv = edgk + kTEdgeFields * ct + kSEdgeVal * cs;       // S' of each S' slot
     double* xl = cor + kCornerFields * cs * ct;
     double* yl = xl + kAlphaTile * cs;
     if (j < kAlphaTile * cs) {
         const int s = j / kAlphaTile, ln = j - s * kAlphaTile;
         if (n0 + ln >= T) return;
-        xl[j] = alpha_xlog(alpha_S(mk, sE[s], m2), alpha_t(mk, tE[tl[ln]], m2), alpha_t(mk, tE[th[ln]], m2));
+        xl[j] = alpha_xlog(sv[s], tv[tl[ln]], tv[th[ln]]);
     } else {
         const int q = j - kAlphaTile * cs, lm = q / ct, t = q - lm * ct;
         if (m0 + lm >= T) return;
-        yl[q] = alpha_ylog(alpha_S(mk, sE[sl[lm]], m2), alpha_S(mk, sE[sh[lm]], m2), alpha_t(mk, tE[t], m2));
+        yl[q] = alpha_ylog(sv[sl[lm]], sv[sh[lm]], tv[t]);
     }
 }
 // leaves of entry (n0 + ln, m0 + lm) of a tile for mass state k
@@ -697,22 +725,22 @@ template <class Lv>
 NUSI_FN void alpha_k(const Point& P, const SplineSet& spl, int k, double Em, double Ep, double Emp, double Epp,
                      const Lv& lv, double& tot, int& warn)
 {
-    const double g = P.g, mphi = P.mphi, Ga = P.Ga;
+    const double g = P.g, mphi = P.mphi;
     const double g4 = (g * g) * (g * g), m2 = mphi * mphi, m4 = (mphi * mphi) * (mphi * mphi);
-    const double gr = Ga / mphi, gr2 = gr * gr;
+    const double gr = P.a_gr, gr2 = gr * gr;
     const bool maj = P.majorana;
     const double mk = P.mn[k], uk = P.u[k];
-    const double tp = alpha_t(mk, Ep, m2), tm = alpha_t(mk, Em, m2);
-    const double Sp = alpha_S(mk, Epp, m2), Sm = alpha_S(mk, Emp, m2);
-    const double wgt = m4 / (2 * mk);
+    const double tp = lv.tval(1, mk, Ep, m2), tm = lv.tval(0, mk, Em, m2);
+    const double Sp = lv.Sval(1, mk, Epp, m2), Sm = lv.Sval(0, mk, Emp, m2);
+    const double wgt = P.a_wgt[k];
     const AlphaMBin mb = lv.mbin(Sm, Sp);
 
     double as;
     if (Sp < 1e-5)
-        as = g4 / (8 * kPi * Ga * (mphi * mphi * mphi)) * (tm - tp) *
+        as = P.a_s * (tm - tp) *
              ((gr * (1 + gr2 + 2 * Sm)) / ((1 + gr2) * (1 + gr2)) * (Sp - Sm) + gr / ((1 + gr2) * (1 + gr2)) * ((Sp - Sm) * (Sp - Sm)));
     else
-        as = g4 / (8 * kPi * Ga * (mphi * mphi * mphi)) * (tm - tp) * mb.atd;
+        as = P.a_s * (tm - tp) * mb.atd;
     as *= uk;
     if (!maj) as /= 2.;
     tot += wgt * as;
@@ -801,7 +829,7 @@ NUSI_FN void alpha_k(const Point& P, const SplineSet& spl, int k, double Em, dou
             const double cm = fTm.cm, cp = fTp.cm;
             const double L2m = fTm.L2, L2p = fTp.L2;
             const double am = fTm.am, ap = fTp.am;
-            ast = g4 / (32 * kPi * (1 + gr2) * m4) *
+            ast = P.a_st *
                   (2 * gr * (cmm.Dri - cmm.Dci - cpm.Dri + cpm.Dci - cmq.Dri + cmq.Dci + cpq.Dri - cpq.Dci)
                    - 2 * (cmm.Drr - cmm.Dcr - cpm.Drr + cpm.Dcr - cmq.Drr + cmq.Dcr + cpq.Drr - cpq.Dcr)
                    + 2 * gr * (cm - cmm.A) * Lmm
@@ -825,7 +853,7 @@ NUSI_FN void alpha_k(const Point& P, const SplineSet& spl, int k, double Em, dou
         tot += wgt * au;
         tot += wgt * atu;   // alpha_tu = 0 for Dirac
         const double Lsm = eSm.Ls, Lsp = eSp.Ls;
-        ast = g4 / (32 * kPi * (1 + gr2) * m4) *
+        ast = P.a_st *
               ((2 * gr * eSm.cS - 2 * gr * eSp.cS + 2 * lSm - 2 * lSp + Lsp - Lsm) * (tm - tp + Lmt - Lmp));
     }
     ast *= uk;
@@ -836,7 +864,7 @@ NUSI_FN void alpha_k(const Point& P, const SplineSet& spl, int k, double Em, dou
     const double app = (Sm > 4 && P.phiphi) ? alpha_phiphi(P, spl, uk, Sm, Sp, tm, tp, lSm, lSp, warn) : 0.0;
     tot += wgt * app;
 
-    const double nrm = (g / mphi) * (g / mphi) * ((g / mphi) * (g / mphi));
+    const double nrm = P.a_nrm;
     // the reference's roundoff checks (:1505); every quotient needs a negative numerator (nrm > 0),
     // so the divisions are only evaluated when one is
     const double sst = ast + as + at;

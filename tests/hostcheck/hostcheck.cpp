@@ -15,6 +15,7 @@ static nusi::Point mk(const double* pt, const int* flags)
     P.mphi = pt[0]; P.g = pt[1]; P.mntot = pt[2]; P.si = pt[3]; P.norm = pt[4]; P.norm_total = pt[5]; P.Ga = pt[6];
     for (int k = 0; k < 3; ++k) { P.mn[k] = pt[7 + k]; P.u[k] = pt[10 + k]; }
     P.majorana = flags[0]; P.non_resonant = flags[1]; P.phiphi = flags[2]; P.source = flags[3];
+    nusi::point_derive(P);
     return P;
 }
 
@@ -57,9 +58,10 @@ int hc_alpha_tiled(const double* pt, const int* flags, int T, const double* lo, 
             double tot[kAlphaTile * kAlphaTile] = {};
             for (int k = 0; k < 3; ++k) {
                 if (P.non_resonant && P.majorana) {
-                    for (int j = 0; j < cc; ++j) alpha_tile_corner_job(P, k, j, tE, ct, sE, cc, cor);
+                    const double* edgk = edg + k * alpha_tile_edge_stride(cs, ct);
+                    for (int j = 0; j < cc; ++j) alpha_tile_corner_job(P, j, edgk, ct, cs, cor);
                     for (int j = 0; j < kAlphaTile * (cs + ct); ++j)
-                        alpha_tile_mixed_job(P, k, j, tE, ct, sE, cs, tl, th, sl, sh, n0, m0, T, cor);
+                        alpha_tile_mixed_job(j, edgk, ct, cs, tl, th, sl, sh, n0, m0, T, cor);
                 }
                 for (int e = 0; e < kAlphaTile * kAlphaTile; ++e) {
                     const int ln = e % kAlphaTile, lm = e / kAlphaTile, n = n0 + ln, m = m0 + lm;
