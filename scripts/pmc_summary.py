@@ -67,16 +67,16 @@ def main():
     casc = [v for k, v in out["kernels"].items() if "k_cascade" in k]
     if casc:
         out["k_cascade_bytes_per_launch"] = casc[0]["hbm_bytes_per_launch"]
-    fk, ng = per_step(fetch_dir, "FETCH_SIZE", "k_alpha_tile")
-    wk, _ = per_step(write_dir, "WRITE_SIZE", "k_alpha_tile")
+    fk, ng = per_step(fetch_dir, "FETCH_SIZE", "nusi::k_alpha")   # tiles + the per-entry region
+    wk, _ = per_step(write_dir, "WRITE_SIZE", "nusi::k_alpha")
     if ng:
         out["k_alpha_launches_per_step"] = ng
         out["k_alpha_hbm_bytes_per_step"] = fk * 1024.0 * fac64 + wk * 1024.0
         if len(sys.argv) > 4:
-            add = per_step(sys.argv[4], "SQ_INSTS_VALU_ADD_F64", "k_alpha_tile")[0]
-            mul = per_step(sys.argv[4], "SQ_INSTS_VALU_MUL_F64", "k_alpha_tile")[0]
-            fma = per_step(sys.argv[4], "SQ_INSTS_VALU_FMA_F64", "k_alpha_tile")[0]
-            trn = per_step(sys.argv[4], "SQ_INSTS_VALU_TRANS_F64", "k_alpha_tile")[0]
+            add = per_step(sys.argv[4], "SQ_INSTS_VALU_ADD_F64", "nusi::k_alpha")[0]
+            mul = per_step(sys.argv[4], "SQ_INSTS_VALU_MUL_F64", "nusi::k_alpha")[0]
+            fma = per_step(sys.argv[4], "SQ_INSTS_VALU_FMA_F64", "nusi::k_alpha")[0]
+            trn = per_step(sys.argv[4], "SQ_INSTS_VALU_TRANS_F64", "nusi::k_alpha")[0]
             out["k_alpha_fp64_flops_per_step"] = 64.0 * (add + mul + 2.0 * fma + trn)
     json.dump(out, sys.stdout, indent=1)
 
