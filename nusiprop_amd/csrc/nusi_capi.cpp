@@ -638,7 +638,9 @@ int nusi_plan_evolve(nusi_plan* pl, const nusi_params* pts, int n, double* d_flu
     HIPCHECK(hipEventRecord(ev[1], s));
     HIPCHECK(nusi::launch_alpha(pl->gd, pl->d_tpts, ntab, spl, pl->atiles, pl->tabs, pl->d_warn, s));
     HIPCHECK(hipEventRecord(ev[2], s));
-    HIPCHECK(nusi::launch_cascade(pl->gd, pl->d_pts, n, pl->tabs, d_flux, d_fla, s, pl->cascade_kind));
+    bool all_pl = true;
+    for (int i = 0; i < n; ++i) all_pl = all_pl && pl->h_pts[i].source == NUSI_SOURCE_POWER_LAW;
+    HIPCHECK(nusi::launch_cascade(pl->gd, pl->d_pts, n, pl->tabs, d_flux, d_fla, s, pl->cascade_kind, all_pl));
     HIPCHECK(hipEventRecord(ev[3], s));
     pl->last_ev = ev;   // stage_ms / warnings / tables refer to the latest call
     pl->ran = true;

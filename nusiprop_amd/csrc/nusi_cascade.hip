@@ -89,6 +89,10 @@ __device__ __attribute__((noinline)) double lum_out(const Point& P, double z, do
 // the diagonal), the power-law source reads pw[]; the DSNB source is evaluated in full.
 __device__ __attribute__((noinline)) void lu3_factor_out(double (&A)[3][3], int (&perm)[3]) { lu3_factor(A, perm); }
 
+// kCallFree: the caller's points all use the power-law source and the pivoting LU is inlined, so
+// the record code makes no calls (a call inside the wavefront kernel's stage loop makes the
+// compiler drain every outstanding alpha prefetch, vmcnt(0), after it)
+template <bool kCallFree>
 NUSI_FN void cascade_record(const GridDev& g, const Point& P, const double* __restrict__ Gt,
                             const double* __restrict__ At, const double* rdE, const double* pw, int i, int b,
                             double* R, int stride)
@@ -127,7 +131,8 @@ NUSI_FN void cascade_record(const GridDev& g, const Point& P, const double* __re
     } else {
         double M[3][3] = {{1.0, m01, m02}, {m10, 1.0, m12}, {m20, m21, 1.0}};
         int pm[3];
-        lu3_factor_out(M, pm);
+        if (kCallFree) lu3_factor(M, pm);
+        else lu3_factor_out(M, pm);
         R[PR_L10 * stride] = M[1][0];
         R[PR_L20 * stride] = M[2][0];
         R[PR_L21 * stride] = M[2][1];
@@ -140,7 +145,7 @@ NUSI_FN void cascade_record(const GridDev& g, const Point& P, const double* __re
         R[kPreFields * stride] = (double)(pm[0] | (pm[1] << 2) | (pm[2] << 4));
     }
     double src;
-    if (P.source == 1)   // nuSIprop.hpp:656
+    if (kCallFree || P.source == 1)   // nuSIprop.hpp:656
         src = P.norm_total / 3.0 * g.sfr[i] * (g.Emax[b] * pw[b + i + 1] - g.Emin[b] * pw[b + i]) / (1 - P.si);
     else
         src = lum_out(P, g.z[i], g.sfr[i], g.Emin[b], g.Emax[b]);
@@ -380,7 +385,7 @@ __global__ __launch_bounds__(64) void k_cascade_reg(GridDev g, const Point* __re
                 const int b = base + lane;
                 double* R = rec + lane * kRec;
                 if (b < N) {
-                    cascade_record(g, P, Gt, At, rdE, pw, i, b, R, 1);
+                    cascade_record<false>(g, P, Gt, At, rdE, pw, i, b, R, 1);
                     R[RC_F0] = F0[qc];
                     R[RC_F1] = F1[qc];
                     R[RC_F2] = F2[qc];
@@ -496,7 +501,7 @@ constexpr int kWfRows = 4, kWfQuarters = 4;   // push: rows per thread, step gro
 #endif
 constexpr int kWfPre = NUSI_WF_PRE;           // alpha columns in flight (stages of prefetch)
 
-template <int NJ>
+template <int NJ, bool kPowerLaw>
 __global__ __launch_bounds__(kWfMaxThreads) void k_cascade_wf(GridDev g, const Point* __restrict__ pts, TablesDev t,
                                                               double* __restrict__ flux, double* __restrict__ flux_fla,
                                                               int K)
@@ -511,6 +516,21 @@ __global__ __launch_bounds__(kWfMaxThreads) void k_cascade_wf(GridDev g, const P
     double* AX = Tp + NJ;                    // [NJ]  accumulators of the row the chain solves next
     double* rdE = AX + NJ;                   // cascade_aux_init tables
     double* pw = rdE + N;
+    // per-point and grid arrays the stage loop reads, staged in LDS: the loop's only global loads
+    // are then the alpha-column prefetches, whose waits the compiler can count exactly
+    double* sGt = pw + (T + 2);
+    double* sAt = sGt + T;
+    double* sdg = sAt + T;                   // alpha(r, r+1) (resonant-only chain)
+    double* sEmin = sdg + T;
+    double* sEmax = sEmin + N;
+    double* sgz = sEmax + N;                 // z, step_c, step_s, sfr [Nz each]
+    GridDev gl = g;
+    gl.Emin = sEmin;
+    gl.Emax = sEmax;
+    gl.z = sgz;
+    gl.step_c = sgz + Nz;
+    gl.step_s = sgz + 2 * Nz;
+    gl.sfr = sgz + 3 * Nz;
     const Point& P = pts[blockIdx.x];
     const double u0 = P.u[0], u1 = P.u[1], u2 = P.u[2];
     const double* __restrict__ Gt = t.G + (size_t)P.tslot * T;
@@ -520,6 +540,18 @@ __global__ __launch_bounds__(kWfMaxThreads) void k_cascade_wf(GridDev g, const P
 
     for (int b = tid; b < 3 * N; b += nthr) F[b] = 0.0;
     for (int j = tid; j < NJ; j += nthr) AX[j] = Tp[j] = 0.0;
+    for (int n = tid; n < T; n += nthr) {
+        sGt[n] = Gt[n];
+        sAt[n] = At[n];
+        sdg[n] = (!nonres && n + 1 < T) ? Al[(size_t)(n + 1) * n / 2 + n] : 0.0;
+    }
+    for (int b = tid; b < N; b += nthr) { sEmin[b] = g.Emin[b]; sEmax[b] = g.Emax[b]; }
+    for (int i = tid; i < Nz; i += nthr) {
+        sgz[i] = g.z[i];
+        sgz[Nz + i] = g.step_c[i];
+        sgz[2 * Nz + i] = g.step_s[i];
+        sgz[3 * Nz + i] = g.sfr[i];
+    }
     cascade_aux_init(g, P, rdE, pw, tid, nthr);
     // push geometry: thread = (row group, step quarter); kWfRows rows x JG steps of accumulators
     constexpr int JG = NJ / kWfQuarters;
@@ -531,23 +563,39 @@ __global__ __launch_bounds__(kWfMaxThreads) void k_cascade_wf(GridDev g, const P
         for (int jj = 0; jj < JG; ++jj) acc[c][jj] = 0.0;
     // chain lane state (wave 0, lane = step slot j)
     const int ist = Nz - 1 - tid;
-    const double cj = (tid < nst) ? g.step_c[ist] : 0.0, sj = (tid < nst) ? g.step_s[ist] : 0.0;
+    __syncthreads();   // staged arrays visible; the chain reads its step's c_i, s_i from LDS (a global load
+                       // here would be waited for with vmcnt(0) inside the loop, draining the prefetches)
+    const double cj = (tid < nst) ? gl.step_c[ist] : 0.0, sj = (tid < nst) ? gl.step_s[ist] : 0.0;
     double racc = 0.0, px0 = 0.0, px1 = 0.0, px2 = 0.0;
     // alpha(row, column) of the next kWfPre stages' columns (ring, [0] = this stage's), rows clamped
     // into the column; each load is issued kWfPre stages before its use (HBM latency > a stage)
+    // The loads are unconditional (column clamped to >= 1, rows into the column; resonant-only
+    // tables are allocated in full): a load skipped on some path would make the compiler wait for
+    // every outstanding load (vmcnt(0)) at the next use.  Columns < 1 are never pushed.
     auto load_col = [&](int col, double (&dst)[kWfRows]) {
-        const size_t cb = (size_t)col * (col - 1) / 2;
+        const int cl = col < 1 ? 1 : col;
+        const size_t cb = (size_t)cl * (cl - 1) / 2;
 #pragma unroll
         for (int c = 0; c < kWfRows; ++c) {
             const int row = row0 + c;
-            dst[c] = (nonres && col >= 1) ? ((NUSI_WF_AB & 8) ? 1e-300 * row : Al[cb + (row < col - 1 ? row : col - 1)])
-                                          : 0.0;
+            dst[c] = (NUSI_WF_AB & 8) ? 1e-300 * row : Al[cb + (row < cl - 1 ? row : cl - 1)];
         }
     };
     double a_ring[kWfPre][kWfRows];
 #pragma unroll
-    for (int d = 0; d < kWfPre; ++d) load_col(T - 1 - d, a_ring[d]);
-    for (int sg = 0; sg < T; ++sg) {
+    for (int d = 0; d < kWfPre; ++d) {   // issued in slot order (the loop's waits count on it)
+        load_col(T - 1 - d, a_ring[d]);
+        NUSI_PHASE();
+    }
+    // stage sg; ac = its alpha column (ring slot sg % kWfPre), reloaded with the column kWfPre
+    // stages ahead after its use (the stage loop is unrolled by kWfPre, so the ring needs no
+    // register moves, which would wait for the newest loads)
+    for (int sg0 = 0; sg0 < T; sg0 += kWfPre)
+#pragma unroll
+    for (int d = 0; d < kWfPre; ++d) {
+        const int sg = sg0 + d;
+        if (sg >= T) break;
+        double (&ac)[kWfRows] = a_ring[d];
         const int r = T - 1 - sg;
         const int ks = sg % K;
         if (ks == 0) {   // ---- records of stages sg .. sg+K-1, one (stage, step) per thread
@@ -555,7 +603,7 @@ __global__ __launch_bounds__(kWfMaxThreads) void k_cascade_wf(GridDev g, const P
             const int q = tid / NJ, jj = tid - q * NJ, s2 = sg + q;
             if (q < K && jj < nst && s2 < T) {
                 const int b = N - 1 - s2 + jj;
-                if (b >= 0 && b < N && !(NUSI_WF_AB & 1)) cascade_record(g, P, Gt, At, rdE, pw, Nz - 1 - jj, b, rec + q * NJ + jj, KR);
+                if (b >= 0 && b < N && !(NUSI_WF_AB & 1)) cascade_record<kPowerLaw>(gl, P, sGt, sAt, rdE, pw, Nz - 1 - jj, b, rec + q * NJ + jj, KR);
             }
             __syncthreads();
         }
@@ -571,8 +619,8 @@ __global__ __launch_bounds__(kWfMaxThreads) void k_cascade_wf(GridDev g, const P
                 } else {
                     if (b != N - 1) {
                         const double Sres = u0 * px0 + u1 * px1 + u2 * px2;
-                        const double sd = Al[(size_t)(r + 1) * r / 2 + r];   // alpha(b+i-1, b+i)
-                        racc += Sres * (sj * sd) / (g.Emax[b + 1] - g.Emin[b + 1]) / R[PR_SDE * KR];
+                        const double sd = sdg[r];   // alpha(b+i-1, b+i)
+                        racc += Sres * (sj * sd) / (sEmax[b + 1] - sEmin[b + 1]) / R[PR_SDE * KR];
                     }
                     add = cj * racc * R[PR_SDE * KR];
                 }
@@ -599,7 +647,7 @@ __global__ __launch_bounds__(kWfMaxThreads) void k_cascade_wf(GridDev g, const P
             for (int jj = 0; jj < JG; ++jj) {
                 const double tj = Th[jj];
 #pragma unroll
-                for (int c = 0; c < kWfRows; ++c) acc[c][jj] = fma(a_ring[0][c], tj, acc[c][jj]);
+                for (int c = 0; c < kWfRows; ++c) acc[c][jj] = fma(ac[c], tj, acc[c][jj]);
             }
             if (r - 1 >= row0 && r - 1 < row0 + kWfRows) {   // publish row r-1 for the next chain
                 const int cp = r - 1 - row0;
@@ -610,12 +658,8 @@ __global__ __launch_bounds__(kWfMaxThreads) void k_cascade_wf(GridDev g, const P
                         for (int jj = 0; jj < JG; ++jj) AX[h * JG + jj] = acc[c][jj];
                     }
             }
-#pragma unroll
-            for (int d = 0; d + 1 < kWfPre; ++d)
-#pragma unroll
-                for (int c = 0; c < kWfRows; ++c) a_ring[d][c] = a_ring[d + 1][c];
-            load_col(r - kWfPre, a_ring[kWfPre - 1]);
         }
+        load_col(r - kWfPre, ac);
         __syncthreads();
     }
     // finalise (nuSIprop.hpp:328-336)
@@ -641,7 +685,8 @@ static WfGeom wf_geom(const GridDev& g, int NJ)
     w.nthr = ((((g.T - 1 + kWfRows - 1) / kWfRows) * kWfQuarters + 63) / 64) * 64;
     w.K = w.nthr / NJ;
     auto bytes = [&](int K) {
-        return sizeof(double) * (3 * (size_t)g.N + (size_t)kWfFields * K * NJ + 2 * NJ + cascade_aux_doubles(g.N, g.T));
+        return sizeof(double) * (3 * (size_t)g.N + (size_t)kWfFields * K * NJ + 2 * NJ + cascade_aux_doubles(g.N, g.T) +
+                                 3 * (size_t)g.T + 2 * (size_t)g.N + 4 * (size_t)g.Nz);
     };
     while (w.K > 1 && bytes(w.K) > kWfMaxLds) --w.K;
     w.lds = bytes(w.K);
@@ -660,10 +705,13 @@ static bool wf_fits(const GridDev& g)
 
 template <int NJ>
 static void launch_wf(const GridDev& g, const Point* pts, int npts, TablesDev t, double* flux, double* flux_fla,
-                      hipStream_t s)
+                      hipStream_t s, bool power_law)
 {
     const WfGeom w = wf_geom(g, NJ);
-    hipLaunchKernelGGL((k_cascade_wf<NJ>), dim3(npts), dim3(w.nthr), w.lds, s, g, pts, t, flux, flux_fla, w.K);
+    if (power_law)
+        hipLaunchKernelGGL((k_cascade_wf<NJ, true>), dim3(npts), dim3(w.nthr), w.lds, s, g, pts, t, flux, flux_fla, w.K);
+    else
+        hipLaunchKernelGGL((k_cascade_wf<NJ, false>), dim3(npts), dim3(w.nthr), w.lds, s, g, pts, t, flux, flux_fla, w.K);
 }
 
 template <int NQ>
@@ -687,7 +735,7 @@ static bool dispatch_reg(int nq, const GridDev& g, const Point* pts, int npts, T
 using RegNQ = std::integer_sequence<int, 1, 2, 3, 4, 5, 6, 8, 10, 12, 16, 20>;
 
 hipError_t launch_cascade(const GridDev& g, const Point* pts, int npts, TablesDev t, double* flux, double* flux_fla,
-                          hipStream_t s, int kind)
+                          hipStream_t s, int kind, bool all_power_law)
 {
     const int nq = (g.N + 63) / 64;
     if (kind == NUSI_CASCADE_AUTO) {
@@ -697,9 +745,9 @@ hipError_t launch_cascade(const GridDev& g, const Point* pts, int npts, TablesDe
     }
     if ((kind == NUSI_CASCADE_AUTO || kind == NUSI_CASCADE_WAVEFRONT) && wf_fits(g)) {
         switch (wf_nj(g)) {
-        case 16: launch_wf<16>(g, pts, npts, t, flux, flux_fla, s); break;
-        case 32: launch_wf<32>(g, pts, npts, t, flux, flux_fla, s); break;
-        default: launch_wf<48>(g, pts, npts, t, flux, flux_fla, s); break;
+        case 16: launch_wf<16>(g, pts, npts, t, flux, flux_fla, s, all_power_law); break;
+        case 32: launch_wf<32>(g, pts, npts, t, flux, flux_fla, s, all_power_law); break;
+        default: launch_wf<48>(g, pts, npts, t, flux, flux_fla, s, all_power_law); break;
         }
         return hipGetLastError();
     }

@@ -51,7 +51,8 @@ hipError_t launch_gamma_alphat(const GridDev& g, const Point* pts, int npts, con
 hipError_t launch_alpha(const GridDev& g, const Point* pts, int npts, const SplineSet& spl, const AlphaTilesDev& tiles,
                         TablesDev t, int* warn, hipStream_t s);
 // kind: NUSI_CASCADE_* (include/nusi.h); NUSI_CASCADE_AUTO also honours $NUSI_CASCADE = wf|reg|lds
+// all_power_law: every point uses the power-law source (selects the call-free wavefront kernel)
 hipError_t launch_cascade(const GridDev& g, const Point* pts, int npts, TablesDev t, double* flux, double* flux_fla,
-                          hipStream_t s, int kind);
+                          hipStream_t s, int kind, bool all_power_law);
 
 }  // namespace nusi
