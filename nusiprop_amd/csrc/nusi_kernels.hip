@@ -124,7 +124,20 @@ __global__ __launch_bounds__(kTileThreads) NUSI_TILE_ATTR void k_alpha_tile(Grid
     double* cor = sm;
     double* edg = sm + alpha_tile_corner_block(cs, ct);
     // ---- 2. edge and m-bin leaves, all k: 3 (ct + cs + kAlphaTile) <= 225 jobs, one round
-    if (tid < 3 * (ct + cs + kAlphaTile)) alpha_tile_edge_job(P, tid, tE, ct, sE, cs, g.lo, g.hi, m0, T, edg);
+    {
+        // one job kind per wave (t edges: wave 0, S' edges: waves 1-2, m bins: wave 3), so no wave runs
+        // two kinds' code one after the other; other tile shapes take the jobs in order
+        const int per = ct + cs + kAlphaTile, w = tid >> 6, l = tid & 63;
+        int job = -1;
+        if (3 * ct <= 64 && 3 * cs <= 128) {
+            if (w == 0) { if (l < 3 * ct) job = (l / ct) * per + l % ct; }
+            else if (w <= 2) { const int q = tid - 64; if (q < 3 * cs) job = (q / cs) * per + ct + q % cs; }
+            else if (l < 3 * kAlphaTile) job = (l / kAlphaTile) * per + ct + cs + l % kAlphaTile;
+        } else if (tid < 3 * per) {
+            job = tid;
+        }
+        if (job >= 0) alpha_tile_edge_job(P, job, tE, ct, sE, cs, g.lo, g.hi, m0, T, edg);
+    }
     double tot = 0;
     int w = 0;
     for (int k = 0; k < 3; ++k) {
