@@ -16,7 +16,10 @@ namespace nusi {
 // ---------------------------------------------------------------------------
 // Stage A
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(64) void k_gamma_alphat(GridDev g, const Point* __restrict__ pts, SplineSet spl,
+#ifndef NUSI_GA_WAVES   // Gamma / alphaTilde kernel waves per SIMD (A/B)
+#define NUSI_GA_WAVES 3   // 3: 0.57 vs 0.65 ms
+#endif
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NUSI_GA_WAVES, NUSI_GA_WAVES))) void k_gamma_alphat(GridDev g, const Point* __restrict__ pts, SplineSet spl,
                                                      double* __restrict__ G, double* __restrict__ At,
                                                      int* __restrict__ warn)
 {
@@ -32,7 +35,11 @@ __global__ __launch_bounds__(64) void k_gamma_alphat(GridDev g, const Point* __r
 }
 
 // one entry per work-item over the bins [nlo, T) x [nlo, T), n < m (nlo = 0: the whole table)
-__global__ __launch_bounds__(256) void k_alpha(GridDev g, const Point* __restrict__ pts, SplineSet spl, int nlo,
+#ifndef NUSI_PE_WAVES   // per-entry kernel waves per SIMD (A/B)
+#define NUSI_PE_WAVES 3   // 3: 20.05 vs 20.24 ms alpha stage (profiles/r1i/ab_occ_*)
+#endif
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NUSI_PE_WAVES, NUSI_PE_WAVES)))
+void k_alpha(GridDev g, const Point* __restrict__ pts, SplineSet spl, int nlo,
                                                double* __restrict__ A, int* __restrict__ warn)
 {
     const int p = blockIdx.y;
