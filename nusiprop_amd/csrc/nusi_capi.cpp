@@ -10,6 +10,8 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <algorithm>
+#include <tuple>
 #include <array>
 #include <map>
 #include <memory>
@@ -353,6 +355,9 @@ struct nusi_plan {
     nusi::Point* h_pts = nullptr;  // pinned
     nusi::Point* d_tpts = nullptr;  // one representative per distinct table (table kernels)
     nusi::Point* h_tpts = nullptr;  // pinned
+    int* d_batches = nullptr;       // alpha-table batches (nusi::launch_alpha): first table | count << 24
+    int* h_batches = nullptr;       // pinned
+    int alpha_batch = 3;            // tables per batch: 3 measured best (4 drops to 2 workgroups/CU on LDS); NUSI_ALPHA_BATCH overrides
     std::vector<int> slot_of;       // table slot of each point of the last call
     int last_ntab = 0;
     int* d_warn = nullptr;
@@ -488,6 +493,8 @@ void nusi_plan_destroy(nusi_plan* pl)
     hipFree(pl->d_pts);
     hipFree(pl->d_tpts);
     if (pl->h_tpts) hipHostFree(pl->h_tpts);
+    hipFree(pl->d_batches);
+    if (pl->h_batches) hipHostFree(pl->h_batches);
     hipFree(pl->d_warn);
     hipFree(pl->tabs.G);
     hipFree(pl->tabs.At);
@@ -560,6 +567,9 @@ int nusi_plan_create(int device, int N_bins_E, double lEmin, double lEmax, doubl
     HIPCHECK(hipHostMalloc((void**)&pl->h_pts, sizeof(nusi::Point) * max_points, hipHostMallocDefault));
     HIPCHECK(hipMalloc(&pl->d_tpts, sizeof(nusi::Point) * max_points));
     HIPCHECK(hipHostMalloc((void**)&pl->h_tpts, sizeof(nusi::Point) * max_points, hipHostMallocDefault));
+    HIPCHECK(hipMalloc(&pl->d_batches, sizeof(int) * max_points));
+    HIPCHECK(hipHostMalloc((void**)&pl->h_batches, sizeof(int) * max_points, hipHostMallocDefault));
+    if (const char* e = getenv("NUSI_ALPHA_BATCH")) pl->alpha_batch = std::max(1, std::min(8, atoi(e)));
     HIPCHECK(hipMalloc(&pl->d_warn, sizeof(int) * max_points));
     HIPCHECK(hipMalloc(&pl->tabs.G, sizeof(double) * (size_t)G.T * max_points));
     HIPCHECK(hipMalloc(&pl->tabs.At, sizeof(double) * (size_t)G.T * max_points));
@@ -619,7 +629,31 @@ int nusi_plan_evolve(nusi_plan* pl, const nusi_params* pts, int n, double* d_flu
         P.tslot = it->second;
         pl->slot_of[i] = it->second;
     }
+    // order the tables so that those sharing m_phi, the masses and the flags -- whose alpha tables
+    // share every leaf of (S', t) alone -- are neighbours, and cut them into batches
+    std::vector<int> order(ntab), perm(ntab);
+    for (int j = 0; j < ntab; ++j) order[j] = j;
+    auto bkey = [&](int j) {
+        const nusi::Point& P = pl->h_tpts[j];
+        return std::make_tuple(P.mphi, P.mn[0], P.mn[1], P.mn[2], P.majorana, P.non_resonant, P.phiphi);
+    };
+    std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return bkey(a) < bkey(b); });
+    {
+        std::vector<nusi::Point> tmp(pl->h_tpts, pl->h_tpts + ntab);
+        for (int j = 0; j < ntab; ++j) {
+            pl->h_tpts[j] = tmp[order[j]];
+            perm[order[j]] = j;
+        }
+    }
+    for (int i = 0; i < n; ++i) pl->h_pts[i].tslot = pl->slot_of[i] = perm[pl->slot_of[i]];
     for (int j = 0; j < ntab; ++j) pl->h_tpts[j].tslot = j;
+    int nbatch = 0;
+    for (int j = 0; j < ntab;) {
+        int c = 1;
+        while (c < pl->alpha_batch && j + c < ntab && bkey(j + c) == bkey(j)) ++c;
+        pl->h_batches[nbatch++] = j | (c << 24);
+        j += c;
+    }
     const size_t N3 = (size_t)3 * pl->grid.N;
     if (!d_flux || !d_fla) {
         if (!pl->d_scratch) HIPCHECK(hipMalloc(&pl->d_scratch, sizeof(double) * 2 * N3 * pl->max_points));
@@ -628,6 +662,7 @@ int nusi_plan_evolve(nusi_plan* pl, const nusi_params* pts, int n, double* d_flu
     }
     HIPCHECK(hipMemcpyAsync(pl->d_pts, pl->h_pts, sizeof(nusi::Point) * n, hipMemcpyHostToDevice, s));
     HIPCHECK(hipMemcpyAsync(pl->d_tpts, pl->h_tpts, sizeof(nusi::Point) * ntab, hipMemcpyHostToDevice, s));
+    HIPCHECK(hipMemcpyAsync(pl->d_batches, pl->h_batches, sizeof(int) * nbatch, hipMemcpyHostToDevice, s));
     HIPCHECK(hipEventRecord(pl->ev_copy, s));
     HIPCHECK(hipMemsetAsync(pl->d_warn, 0, sizeof(int) * ntab, s));
     const nusi::SplineSet spl = pl->spl ? pl->spl->set : nusi::SplineSet{};
@@ -636,7 +671,8 @@ int nusi_plan_evolve(nusi_plan* pl, const nusi_params* pts, int n, double* d_flu
     HIPCHECK(hipEventRecord(ev[0], s));
     HIPCHECK(nusi::launch_gamma_alphat(pl->gd, pl->d_tpts, ntab, spl, pl->tabs, pl->d_warn, s));
     HIPCHECK(hipEventRecord(ev[1], s));
-    HIPCHECK(nusi::launch_alpha(pl->gd, pl->d_tpts, ntab, spl, pl->atiles, pl->tabs, pl->d_warn, s));
+    HIPCHECK(nusi::launch_alpha(pl->gd, pl->d_tpts, ntab, spl, pl->atiles, pl->tabs, pl->d_warn, s, pl->d_batches,
+                                nbatch, pl->alpha_batch));
     HIPCHECK(hipEventRecord(ev[2], s));
     bool all_pl = true;
     for (int i = 0; i < n; ++i) all_pl = all_pl && pl->h_pts[i].source == NUSI_SOURCE_POWER_LAW;

@@ -48,8 +48,10 @@ void alpha_tiles_destroy(AlphaTilesDev* t);
 
 hipError_t launch_gamma_alphat(const GridDev& g, const Point* pts, int npts, const SplineSet& spl, TablesDev t,
                                int* warn, hipStream_t s);
+// batches: device [nbatches] of first table | count << 24 (count <= gmax), tables of a batch sharing
+// m_phi, the masses and the channel flags (nullptr: every table alone)
 hipError_t launch_alpha(const GridDev& g, const Point* pts, int npts, const SplineSet& spl, const AlphaTilesDev& tiles,
-                        TablesDev t, int* warn, hipStream_t s);
+                        TablesDev t, int* warn, hipStream_t s, const int* batches, int nbatches, int gmax);
 // kind: NUSI_CASCADE_* (include/nusi.h); NUSI_CASCADE_AUTO also honours $NUSI_CASCADE = wf|reg|lds
 // all_power_law: every point uses the power-law source (selects the call-free wavefront kernel)
 hipError_t launch_cascade(const GridDev& g, const Point* pts, int npts, TablesDev t, double* flux, double* flux_fla,

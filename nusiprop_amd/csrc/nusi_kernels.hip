@@ -86,9 +86,10 @@ hipError_t launch_gamma_alphat(const GridDev& g, const Point* pts, int npts, con
 constexpr int kTileThreads = 256;
 static_assert(kAlphaTile * kAlphaTile <= kTileThreads, "one entry per work-item");
 
-__host__ __device__ constexpr int alpha_tile_lds_doubles(int cs, int ct)
+// dynamic LDS of a tile for batches of up to G points: corner block, edge blocks, per-point sums
+__host__ __device__ constexpr int alpha_tile_lds_doubles(int cs, int ct, int G)
 {
-    return alpha_tile_corner_block(cs, ct) + 3 * alpha_tile_edge_stride(cs, ct);
+    return alpha_tile_corner_block(cs, ct, G) + alpha_tile_edge_doubles(cs, ct, G) + (G > 1 ? G * kTileThreads : 0);
 }
 
 // 3 waves per SIMD (<= 168 VGPRs): measured 38.5 ms vs 42.0 (2 waves, 222 VGPRs) and 42.4 (4 waves,
@@ -97,8 +98,13 @@ __host__ __device__ constexpr int alpha_tile_lds_doubles(int cs, int ct)
 #define NUSI_TILE_WAVES 3
 #endif
 #define NUSI_TILE_ATTR __attribute__((amdgpu_waves_per_eu(NUSI_TILE_WAVES, NUSI_TILE_WAVES)))
+// One workgroup per (tile, batch).  A batch is 1..G tables whose points share m_phi, the masses and
+// the channel flags (nusi_capi.cpp orders the tables so): the leaves of (S', t) alone -- the real
+// dilogarithms and most logarithms -- are evaluated once for the batch, the leaves that read
+// gr = Gamma_phi / m_phi once per point.  batches[y] = first table | count << 24 (nullptr: table y alone).
 __global__ __launch_bounds__(kTileThreads) NUSI_TILE_ATTR void k_alpha_tile(GridDev g, const Point* __restrict__ pts, SplineSet spl,
                                                            const int* __restrict__ tiles, int cs_max, int ct_max,
+                                                           const int* __restrict__ batches, int G,
                                                            double* __restrict__ A, int* __restrict__ warn)
 {
     extern __shared__ __attribute__((aligned(16))) double sm[];
@@ -106,10 +112,12 @@ __global__ __launch_bounds__(kTileThreads) NUSI_TILE_ATTR void k_alpha_tile(Grid
     __shared__ int tl[kAlphaTile], th[kAlphaTile], sl[kAlphaTile], sh[kAlphaTile];
     __shared__ int cnt[2];
     __shared__ double elo[2][kAlphaTile], ehi[2][kAlphaTile];   // bin edges of both sides, staged in parallel
-    const int p = blockIdx.y, tid = threadIdx.x, T = g.T;
+    const int tid = threadIdx.x, T = g.T;
+    const int bw = batches ? batches[blockIdx.y] : (int)blockIdx.y | (1 << 24);
+    const int p0 = bw & 0xffffff, nb = bw >> 24;   // tables p0 .. p0 + nb - 1 (nb <= G)
     const int tw = tiles[blockIdx.x];
     const int n0 = (tw & 0xffff) * kAlphaTile, m0 = (tw >> 16) * kAlphaTile;
-    const Point& P = pts[p];
+    const Point& P = pts[p0];   // the batch's shared fields (m_phi, masses, flags)
     if (tid < 2 * kAlphaTile) {
         const int side = tid / kAlphaTile, j = tid - side * kAlphaTile, b = (side ? m0 : n0) + j;
         if (b < T) { elo[side][j] = g.lo[b]; ehi[side][j] = g.hi[b]; }
@@ -122,15 +130,18 @@ __global__ __launch_bounds__(kTileThreads) NUSI_TILE_ATTR void k_alpha_tile(Grid
     const int ln = tid % kAlphaTile, lm = tid / kAlphaTile;
     const int n = n0 + ln, m = m0 + lm;
     const bool valid = tid < kAlphaTile * kAlphaTile && n < m && m < T;
-    if (cs > cs_max || ct > ct_max) {   // host classification guarantees this never happens
-        if (valid) A[(size_t)p * g.PT + (size_t)m * (m - 1) / 2 + n] = __builtin_nan("");
+    if (cs > cs_max || ct > ct_max || nb > G) {   // host classification guarantees this never happens
+        if (valid)
+            for (int q = 0; q < nb; ++q) A[(size_t)(p0 + q) * g.PT + (size_t)m * (m - 1) / 2 + n] = __builtin_nan("");
         return;
     }
     const bool nonres = P.non_resonant, maj = P.majorana;
     const bool needed = valid && (nonres || m == n + 1);
     double* cor = sm;
-    double* edg = sm + alpha_tile_corner_block(cs, ct);
-    // ---- 2. edge and m-bin leaves, all k: 3 (ct + cs + kAlphaTile) <= 225 jobs, one round
+    double* edg = sm + alpha_tile_corner_block(cs, ct, G);
+    double* tsum = edg + alpha_tile_edge_doubles(cs, ct, G);   // [G][kTileThreads] per-point sums (G > 1)
+    double tot1 = 0.0;                                          // the sum of a batch of one
+    // ---- 2. edge and m-bin leaves, all k: shared jobs, one round
     {
         // one job kind per wave (t edges: wave 0, S' edges: waves 1-2, m bins: wave 3), so no wave runs
         // two kinds' code one after the other; other tile shapes take the jobs in order
@@ -143,36 +154,51 @@ __global__ __launch_bounds__(kTileThreads) NUSI_TILE_ATTR void k_alpha_tile(Grid
         } else if (tid < 3 * per) {
             job = tid;
         }
-        if (job >= 0) alpha_tile_edge_job(P, job, tE, ct, sE, cs, g.lo, g.hi, m0, T, edg);
+        if (job >= 0) {   // the shared leaves, then the same edge's member leaves of every batch point
+            alpha_tile_edge_job(P, job, tE, ct, sE, cs, g.lo, g.hi, m0, T, edg);
+#pragma unroll 1
+            for (int q = 0; q < nb; ++q)
+                alpha_tile_edge_member_job(pts[p0 + q], q, G, job, tE, ct, sE, cs, g.lo, g.hi, m0, T, edg);
+        }
+        if (G > 1)
+            for (int q = 0; q < nb; ++q) tsum[q * kTileThreads + tid] = 0.0;
     }
-    double tot = 0;
-    int w = 0;
     for (int k = 0; k < 3; ++k) {
         __syncthreads();   // edge leaves written / previous k's corners consumed
 #ifndef NUSI_AB_NO_CORNERS   // timing experiments only (scripts/build_variant.sh)
         if (nonres && maj) {
             const double* edgk = edg + k * alpha_tile_edge_stride(cs, ct);
-            for (int j = tid; j < cc; j += kTileThreads) alpha_tile_corner_job(P, j, edgk, ct, cs, cor);
-#ifndef NUSI_AB_NO_MIXED
+            for (int j = tid; j < cc; j += kTileThreads) {   // corner j: shared leaves, then each point's
+                alpha_tile_corner_job(j, edgk, ct, cs, cor);
+#pragma unroll 1
+                for (int q = 0; q < nb; ++q) alpha_tile_corner_member_job(pts[p0 + q], q, j, edgk, ct, cs, cor);
+            }
             for (int j = tid; j < kAlphaTile * (cs + ct); j += kTileThreads)
-#else
-            for (int j = tid; j < 0; j += kTileThreads)
-#endif
-                alpha_tile_mixed_job(j, edgk, ct, cs, tl, th, sl, sh, n0, m0, T, cor);
+                alpha_tile_mixed_job(j, edgk, ct, cs, G, tl, th, sl, sh, n0, m0, T, cor);
         }
 #endif
         __syncthreads();
-#ifdef NUSI_AB_NO_COMBINE
-        if (needed) tot += cor[(tid * 7) % cc] + edg[tid % 64];
-        else
-#endif
         if (needed) {
-            const TileLeaves lv = alpha_tile_leaves(cor, edg, k, cs, ct, lm, sl, sh, tl, th, ln);
-            alpha_k(P, spl, k, g.lo[n], g.hi[n], g.lo[m], g.hi[m], lv, tot, w);
+#pragma unroll 1
+            for (int q = 0; q < nb; ++q) {
+                double tot = (G > 1) ? tsum[q * kTileThreads + tid] : tot1;
+                int w = 0;
+#ifdef NUSI_AB_NO_COMBINE
+                tot += cor[(tid * 7) % cc] + edg[tid % 64];
+#else
+                const TileLeaves lv = alpha_tile_leaves(cor, edg, k, q, G, cs, ct, lm, sl, sh, tl, th, ln);
+                alpha_k(pts[p0 + q], spl, k, g.lo[n], g.hi[n], g.lo[m], g.hi[m], lv, tot, w);
+#endif
+                if (G > 1) tsum[q * kTileThreads + tid] = tot;
+                else tot1 = tot;
+                if (w) atomicOr(&warn[p0 + q], w);
+            }
         }
     }
-    if (valid) A[(size_t)p * g.PT + (size_t)m * (m - 1) / 2 + n] = needed ? tot : 0.0;
-    if (w) atomicOr(&warn[p], w);
+    if (valid)
+        for (int q = 0; q < nb; ++q)
+            A[(size_t)(p0 + q) * g.PT + (size_t)m * (m - 1) / 2 + n] =
+                needed ? ((G > 1) ? tsum[q * kTileThreads + tid] : tot1) : 0.0;
 }
 
 hipError_t alpha_tiles_create(int T, const unsigned char* shared, AlphaTilesDev* out)
@@ -221,7 +247,7 @@ void alpha_tiles_destroy(AlphaTilesDev* t)
 }
 
 hipError_t launch_alpha(const GridDev& g, const Point* pts, int npts, const SplineSet& spl, const AlphaTilesDev& at,
-                        TablesDev t, int* warn, hipStream_t s)
+                        TablesDev t, int* warn, hipStream_t s, const int* batches, int nbatches, int gmax)
 {
     static const bool per_entry = getenv("NUSI_ALPHA_PER_ENTRY") != nullptr;   // A/B switch
     auto per_entry_region = [&](int nlo) {
@@ -239,9 +265,12 @@ hipError_t launch_alpha(const GridDev& g, const Point* pts, int npts, const Spli
     for (int c = 0; c < 3; ++c) {
         if (at.ncls[c] == 0) continue;
         const int cs = at.cs_max[c], ct = at.ct_max[c];
-        const size_t lds = sizeof(double) * (size_t)alpha_tile_lds_doubles(cs, ct);
-        hipLaunchKernelGGL(k_alpha_tile, dim3(at.ncls[c], npts), dim3(kTileThreads), lds, s, g, pts, spl,
-                           at.tiles + off, cs, ct, t.A, warn);
+        // class 0 (core tiles) runs on batches of tables sharing their (S', t) leaves; the others per table
+        const bool batched = c == 0 && batches && gmax > 1;
+        const int G = batched ? gmax : 1;
+        const size_t lds = sizeof(double) * (size_t)alpha_tile_lds_doubles(cs, ct, G);
+        hipLaunchKernelGGL(k_alpha_tile, dim3(at.ncls[c], batched ? nbatches : npts), dim3(kTileThreads), lds, s, g,
+                           pts, spl, at.tiles + off, cs, ct, batched ? batches : nullptr, G, t.A, warn);
         off += at.ncls[c];
     }
     return hipGetLastError();

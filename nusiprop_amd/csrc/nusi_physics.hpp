@@ -455,7 +455,9 @@ struct AlphaCorner {
 #define NUSI_CLOG1P nm::log1p_i
 #define NUSI_CARG carg_i
 #endif
-NUSI_FN void alpha_corner(double S, double t, double gr, AlphaCorner& c)
+// The leaves split into those of (S', t) alone ("shared": every point with the same m_phi and
+// masses has them, bit for bit) and those that also read gr = Gamma_phi / m_phi ("member").
+NUSI_FN void alpha_corner_shared(double S, double t, AlphaCorner& c)
 {
     c.L = NUSI_CLOG1P(S + t);
     c.LL = NUSI_CLOG(1 + S + t);
@@ -468,33 +470,54 @@ NUSI_FN void alpha_corner(double S, double t, double gr, AlphaCorner& c)
     }
     c.G = li2((1 + S + t) / (2 + S));
     const cd Dr = cli2((1 + S + t) / (1 + t), 0.0);
-    const cd dt = C(2 + t, -gr);
-    const cd Dc = cli2((1 + S + t) / dt);
     c.Drr = Dr.r;
     c.Dri = Dr.i;
+}
+NUSI_FN void alpha_corner_member(double S, double t, double gr, AlphaCorner& c)
+{
+    const cd dt = C(2 + t, -gr);
+    const cd Dc = cli2((1 + S + t) / dt);
     c.Dcr = Dc.r;
     c.Dci = Dc.i;
     c.A = NUSI_CARG(-(C(-1 + S, gr) / dt));
 }
-// t-edge leaves
+NUSI_FN void alpha_corner(double S, double t, double gr, AlphaCorner& c)
+{
+    alpha_corner_shared(S, t, c);
+    alpha_corner_member(S, t, gr, c);
+}
+// t-edge leaves (L2 is the member leaf)
 struct AlphaTEdge { double Lm1, la, cm, L2, am; };
-NUSI_FN void alpha_tedge(double t, double gr2, AlphaTEdge& e)
+NUSI_FN void alpha_tedge_shared(double t, AlphaTEdge& e)
 {
     e.Lm1 = nm::log1p(-t);
     e.la = (t > -1) ? nm::log1p(t) : nm::log(-1 - t);
     e.cm = carg_real(-(1 / (1 + t)));
-    e.L2 = nm::log1p(((2 + t) * (2 + t)) / gr2);
     e.am = nm::log(fabs(1 + t));
 }
-// S'-edge leaves
+NUSI_FN double alpha_tedge_L2(double t, double gr2) { return nm::log1p(((2 + t) * (2 + t)) / gr2); }
+NUSI_FN void alpha_tedge(double t, double gr2, AlphaTEdge& e)
+{
+    alpha_tedge_shared(t, e);
+    e.L2 = alpha_tedge_L2(t, gr2);
+}
+// S'-edge leaves (Ls, cS are member leaves)
 struct AlphaSEdge { double lS, l2, Ls, cS, lS2; };
-NUSI_FN void alpha_sedge(double S, double gr, double gr2, AlphaSEdge& e)
+NUSI_FN void alpha_sedge_shared(double S, AlphaSEdge& e)
 {
     e.lS = nm::log(S);
     e.l2 = nm::log((2 + S) / S);
+    e.lS2 = nm::log(S / (2 + S));
+}
+NUSI_FN void alpha_sedge_member(double S, double gr, double gr2, AlphaSEdge& e)
+{
     e.Ls = nm::log1p(((-1 + S) * (-1 + S)) / gr2);
     e.cS = carg(C(-1 + S, gr));
-    e.lS2 = nm::log(S / (2 + S));
+}
+NUSI_FN void alpha_sedge(double S, double gr, double gr2, AlphaSEdge& e)
+{
+    alpha_sedge_shared(S, e);
+    alpha_sedge_member(S, gr, gr2, e);
 }
 // mixed leaves of the Majorana t channel (nuSIprop.hpp:1284): each of its four logarithms
 // depends on one S' edge and the n bin (xlog) or on the m bin and one t edge (ylog)
@@ -502,15 +525,20 @@ NUSI_FN double alpha_xlog(double S, double tm, double tp) { return nm::log(((1 +
 NUSI_FN double alpha_ylog(double Sm, double Sp, double t) { return nm::log((Sm * (1 + Sp + t)) / (Sp * (1 + Sm + t))); }
 // m-bin leaves
 struct AlphaMBin { double lr, lr2, atd; };
+NUSI_FN double alpha_mbin_atd(double Sm, double Sp, double mphi, double Ga)   // the member leaf
+{
+    return (Sp < 1e-5) ? 0.0 : atandiff(mphi * (Sp - 1) / Ga, mphi * (Sm - 1) / Ga);
+}
 NUSI_FN void alpha_mbin(double Sm, double Sp, double mphi, double Ga, AlphaMBin& b)
 {
     b.lr = nm::log(Sm / Sp);
     b.lr2 = nm::log(Sp / Sm);
-    b.atd = (Sp < 1e-5) ? 0.0 : atandiff(mphi * (Sp - 1) / Ga, mphi * (Sm - 1) / Ga);
+    b.atd = alpha_mbin_atd(Sm, Sp, mphi, Ga);
 }
 
-constexpr int kCornerFields = 10, kTEdgeFields = 6, kSEdgeFields = 6, kMBinFields = 3;
-constexpr int kTEdgeVal = 5, kSEdgeVal = 5;   // edge field holding t resp. S' itself (alpha_t / alpha_S)
+// shared edge-block fields: t edges Lm1 la cm am t, S' edges lS l2 lS2 S, m bins lr lr2
+constexpr int kCornerFields = 10, kTEdgeFields = 5, kSEdgeFields = 4, kMBinFields = 2;
+constexpr int kTEdgeVal = 4, kSEdgeVal = 3;   // edge field holding t resp. S' itself (alpha_t / alpha_S)
 
 // leaves evaluated on the spot (per-entry path, host checks)
 struct DirectLeaves {
@@ -526,39 +554,48 @@ struct DirectLeaves {
 };
 
 // leaves read from a tile's precomputed arrays (structure of arrays):
-//   cor[v * cc + s * ct + t]  (v = field of AlphaCorner, cc = cs * ct), ted[v * ct + t],
-//   sed[v * cs + s], mbv[v * kAlphaTile + j], xl[s * kAlphaTile + n bin], yl[m bin * ct + t]
+//   cor[v * cc + s * ct + t]  (v = shared field of AlphaCorner, cc = cs * ct),
+//   corm[v * cc + s * ct + t] (v = member field Dcr, Dci, A of this point),
+//   ted[v * ct + t], sed[v * cs + s], mbv[v * kAlphaTile + j] (shared edge / m-bin fields),
+//   tedm[t] = L2, sedm[s] = Ls, sedm[cs + s] = cS, mbm[j] = atd (this point's member fields),
+//   xl[s * kAlphaTile + n bin], yl[m bin * ct + t]
 constexpr int kAlphaTile = 15;
+constexpr int kCornerShared = 7, kCornerMember = 3;   // L LL TU1 TU2 G Drr Dri | Dcr Dci A
 struct TileLeaves {
-    const double *cor, *ted, *sed, *mbv, *xl, *yl;
+    const double *cor, *corm, *ted, *sed, *mbv, *tedm, *sedm, *mbm, *xl, *yl;
     int cc, ct, cs, mb, nb;
     int sidx[2], tidx[2];   // slots of (Sm, Sp) and (tm, tp)
     NUSI_FN AlphaCorner corner(int si, int ti, double, double) const
     {
-        const double* c = cor + sidx[si] * ct + tidx[ti];
-        return AlphaCorner{c[0], c[cc], c[2 * cc], c[3 * cc], c[4 * cc], c[5 * cc], c[6 * cc], c[7 * cc], c[8 * cc], c[9 * cc]};
+        const int o = sidx[si] * ct + tidx[ti];
+        const double *c = cor + o, *d = corm + o;
+        return AlphaCorner{c[0], c[cc], c[2 * cc], c[3 * cc], c[4 * cc], c[5 * cc], c[6 * cc], d[0], d[cc], d[2 * cc]};
     }
     NUSI_FN AlphaTEdge tedge(int ti, double) const
     {
         const double* e = ted + tidx[ti];
-        return AlphaTEdge{e[0], e[ct], e[2 * ct], e[3 * ct], e[4 * ct]};
+        return AlphaTEdge{e[0], e[ct], e[2 * ct], tedm[tidx[ti]], e[3 * ct]};
     }
     NUSI_FN AlphaSEdge sedge(int si, double) const
     {
         const double* e = sed + sidx[si];
-        return AlphaSEdge{e[0], e[cs], e[2 * cs], e[3 * cs], e[4 * cs]};
+        return AlphaSEdge{e[0], e[cs], sedm[sidx[si]], sedm[cs + sidx[si]], e[2 * cs]};
     }
     NUSI_FN AlphaMBin mbin(double, double) const
     {
-        return AlphaMBin{mbv[mb], mbv[kAlphaTile + mb], mbv[2 * kAlphaTile + mb]};
+        return AlphaMBin{mbv[mb], mbv[kAlphaTile + mb], mbm[mb]};
     }
     NUSI_FN double tval(int ti, double, double, double) const { return ted[kTEdgeVal * ct + tidx[ti]]; }
     NUSI_FN double Sval(int si, double, double, double) const { return sed[kSEdgeVal * cs + sidx[si]]; }
     NUSI_FN double xlog(int si, double, double, double) const { return xl[sidx[si] * kAlphaTile + nb]; }
     NUSI_FN double ylog(int ti, double, double, double) const { return yl[mb * ct + tidx[ti]]; }
 };
-// per-k leaf block of the corner phase: corners, then xlog [cs][kAlphaTile], then ylog [kAlphaTile][ct]
-NUSI_FN int alpha_tile_corner_block(int cs, int ct) { return kCornerFields * cs * ct + kAlphaTile * (cs + ct); }
+// per-k leaf block of the corner phase for G points: shared corners, G member corner blocks, then
+// xlog [cs][kAlphaTile], then ylog [kAlphaTile][ct]
+NUSI_FN int alpha_tile_corner_block(int cs, int ct, int G)
+{
+    return (kCornerShared + kCornerMember * G) * cs * ct + kAlphaTile * (cs + ct);
+}
 
 // Unique edge energies of bins b0 .. b0+kAlphaTile-1 (< T): E[0..count), il/ih = slot of each bin's
 // lower/upper edge.  Bins of the first N share edges bitwise (Emax[n] == Emin[n+1], same pow()
@@ -577,13 +614,25 @@ NUSI_FN int alpha_edge_list(const double* lo, const double* hi, int b0, int T, d
 }
 
 // Tile precomputation jobs (k_alpha_tile; emulated on the host by tests/hostcheck).
-// Edge-leaf block of mass state k: [5][ct] t edges, [5][cs] S' edges, [3][kAlphaTile] m bins.
+// Edge-leaf block of mass state k: [5][ct] t edges, [4][cs] S' edges, [2][kAlphaTile] m bins (the
+// shared fields), then after the 3 blocks the member blocks of (k, point m): [ct] L2, [cs] Ls,
+// [cs] cS, [kAlphaTile] atd.
 NUSI_FN int alpha_tile_edge_stride(int cs, int ct) { return kTEdgeFields * ct + kSEdgeFields * cs + kMBinFields * kAlphaTile; }
-// job in [0, 3 (ct + cs + kAlphaTile)): one edge / m-bin leaf set of one mass state
+NUSI_FN int alpha_tile_member_stride(int cs, int ct) { return ct + 2 * cs + kAlphaTile; }
+NUSI_FN int alpha_tile_edge_doubles(int cs, int ct, int G)
+{
+    return 3 * (alpha_tile_edge_stride(cs, ct) + G * alpha_tile_member_stride(cs, ct));
+}
+NUSI_FN double* alpha_tile_member_block(double* edg, int cs, int ct, int G, int k, int m)
+{
+    return edg + 3 * alpha_tile_edge_stride(cs, ct) + (k * G + m) * alpha_tile_member_stride(cs, ct);
+}
+// job in [0, 3 (ct + cs + kAlphaTile)): the shared edge / m-bin leaves of one mass state (P: any
+// point of the tile's batch -- they read m_phi and the masses only)
 NUSI_FN void alpha_tile_edge_job(const Point& P, int job, const double* tE, int ct, const double* sE, int cs,
                                  const double* lo, const double* hi, int m0, int T, double* edg)
 {
-    const double mphi = P.mphi, Ga = P.Ga, m2 = mphi * mphi, gr = Ga / mphi, gr2 = gr * gr;
+    const double mphi = P.mphi, m2 = mphi * mphi;
     const int per = ct + cs + kAlphaTile;
     const int k = job / per, j = job - k * per;
     const double mk = P.mn[k];
@@ -595,43 +644,80 @@ NUSI_FN void alpha_tile_edge_job(const Point& P, int job, const double* tE, int 
         ted[kTEdgeVal * ct + j] = t;
         if (!P.non_resonant) return;
         AlphaTEdge e;
-        alpha_tedge(t, gr2, e);
-        ted[j] = e.Lm1; ted[ct + j] = e.la; ted[2 * ct + j] = e.cm; ted[3 * ct + j] = e.L2; ted[4 * ct + j] = e.am;
+        alpha_tedge_shared(t, e);
+        ted[j] = e.Lm1; ted[ct + j] = e.la; ted[2 * ct + j] = e.cm; ted[3 * ct + j] = e.am;
     } else if (j < ct + cs) {
         const int q = j - ct;
         const double S = alpha_S(mk, sE[q], m2);
         sed[kSEdgeVal * cs + q] = S;
         if (!P.non_resonant) return;
         AlphaSEdge e;
-        alpha_sedge(S, gr, gr2, e);
-        sed[q] = e.lS; sed[cs + q] = e.l2; sed[2 * cs + q] = e.Ls; sed[3 * cs + q] = e.cS; sed[4 * cs + q] = e.lS2;
+        alpha_sedge_shared(S, e);
+        sed[q] = e.lS; sed[cs + q] = e.l2; sed[2 * cs + q] = e.lS2;
     } else {
         const int q = j - ct - cs;
         if (m0 + q >= T) return;
-        AlphaMBin b;
-        alpha_mbin(alpha_S(mk, lo[m0 + q], m2), alpha_S(mk, hi[m0 + q], m2), mphi, Ga, b);
-        mbv[q] = b.lr; mbv[kAlphaTile + q] = b.lr2; mbv[2 * kAlphaTile + q] = b.atd;
+        const double Sm = alpha_S(mk, lo[m0 + q], m2), Sp = alpha_S(mk, hi[m0 + q], m2);
+        mbv[q] = nm::log(Sm / Sp);
+        mbv[kAlphaTile + q] = nm::log(Sp / Sm);
     }
 }
-// job j in [0, cs ct): corner (S' slot j / ct, t slot j % ct) of mass state k; edgk = the edge
-// block of mass state k (its t and S' values)
-NUSI_FN void alpha_tile_corner_job(const Point& P, int j, const double* edgk, int ct, int cs, double* cor)
+// job in [0, 3 (ct + cs + kAlphaTile)): the member edge / m-bin leaves of point P (slot m of the
+// batch); t and S' are recomputed (the same expression), so no barrier orders it after the shared jobs
+NUSI_FN void alpha_tile_edge_member_job(const Point& P, int m, int G, int job, const double* tE, int ct,
+                                        const double* sE, int cs, const double* lo, const double* hi, int m0, int T,
+                                        double* edg)
+{
+    const double mphi = P.mphi, Ga = P.Ga, m2 = mphi * mphi, gr = P.a_gr, gr2 = gr * gr;
+    const int per = ct + cs + kAlphaTile;
+    const int k = job / per, j = job - k * per;
+    const double mk = P.mn[k];
+    double* mbk = alpha_tile_member_block(edg, cs, ct, G, k, m);
+    if (j < ct) {
+        if (!P.non_resonant) return;
+        mbk[j] = alpha_tedge_L2(alpha_t(mk, tE[j], m2), gr2);
+    } else if (j < ct + cs) {
+        if (!P.non_resonant) return;
+        const int q = j - ct;
+        AlphaSEdge e;
+        alpha_sedge_member(alpha_S(mk, sE[q], m2), gr, gr2, e);
+        mbk[ct + q] = e.Ls;
+        mbk[ct + cs + q] = e.cS;
+    } else {
+        const int q = j - ct - cs;
+        if (m0 + q >= T) return;
+        mbk[ct + 2 * cs + q] = alpha_mbin_atd(alpha_S(mk, lo[m0 + q], m2), alpha_S(mk, hi[m0 + q], m2), mphi, Ga);
+    }
+}
+// job j in [0, cs ct): the shared leaves of corner (S' slot j / ct, t slot j % ct) of mass state k;
+// edgk = the edge block of mass state k (its t and S' values)
+NUSI_FN void alpha_tile_corner_job(int j, const double* edgk, int ct, int cs, double* cor)
 {
     const int cc = cs * ct;
     const int si = j / ct, ti = j - si * ct;
     AlphaCorner c;
-    alpha_corner(edgk[kTEdgeFields * ct + kSEdgeVal * cs + si], edgk[kTEdgeVal * ct + ti], P.a_gr, c);
+    alpha_corner_shared(edgk[kTEdgeFields * ct + kSEdgeVal * cs + si], edgk[kTEdgeVal * ct + ti], c);
     cor[j] = c.L; cor[cc + j] = c.LL; cor[2 * cc + j] = c.TU1; cor[3 * cc + j] = c.TU2; cor[4 * cc + j] = c.G;
-    cor[5 * cc + j] = c.Drr; cor[6 * cc + j] = c.Dri; cor[7 * cc + j] = c.Dcr; cor[8 * cc + j] = c.Dci; cor[9 * cc + j] = c.A;
+    cor[5 * cc + j] = c.Drr; cor[6 * cc + j] = c.Dri;
+}
+// job j in [0, cs ct): the member leaves of corner j for point P (slot m of the batch)
+NUSI_FN void alpha_tile_corner_member_job(const Point& P, int m, int j, const double* edgk, int ct, int cs, double* cor)
+{
+    const int cc = cs * ct;
+    const int si = j / ct, ti = j - si * ct;
+    AlphaCorner c;
+    alpha_corner_member(edgk[kTEdgeFields * ct + kSEdgeVal * cs + si], edgk[kTEdgeVal * ct + ti], P.a_gr, c);
+    double* d = cor + (kCornerShared + kCornerMember * m) * cc;
+    d[j] = c.Dcr; d[cc + j] = c.Dci; d[2 * cc + j] = c.A;
 }
 // job j in [0, kAlphaTile (cs + ct)): the xlog leaf (S' slot, n bin) or the ylog leaf (m bin, t slot)
-// of mass state k, into the block after the corners; bins past the table are skipped
-NUSI_FN void alpha_tile_mixed_job(int j, const double* edgk, int ct, int cs, const int* tl, const int* th,
+// of mass state k (shared), into the block after the corners; bins past the table are skipped
+NUSI_FN void alpha_tile_mixed_job(int j, const double* edgk, int ct, int cs, int G, const int* tl, const int* th,
                                   const int* sl, const int* sh, int n0, int m0, int T, double* cor)
 {
     const double* tv = edgk + kTEdgeVal * ct;                           // t of each t slot
     const double* sv = edgk + kTEdgeFields * ct + kSEdgeVal * cs;       // S' of each S' slot
-    double* xl = cor + kCornerFields * cs * ct;
+    double* xl = cor + (kCornerShared + kCornerMember * G) * cs * ct;
     double* yl = xl + kAlphaTile * cs;
     if (j < kAlphaTile * cs) {
         const int s = j / kAlphaTile, ln = j - s * kAlphaTile;
@@ -643,18 +729,19 @@ NUSI_FN void alpha_tile_mixed_job(int j, const double* edgk, int ct, int cs, con
         yl[q] = alpha_ylog(sv[sl[lm]], sv[sh[lm]], tv[t]);
     }
 }
-// leaves of entry (n0 + ln, m0 + lm) of a tile for mass state k
-NUSI_FN TileLeaves alpha_tile_leaves(const double* cor, const double* edg, int k, int cs, int ct, int lm,
+// leaves of entry (n0 + ln, m0 + lm) of a tile for mass state k and batch point m (of G)
+NUSI_FN TileLeaves alpha_tile_leaves(const double* cor, const double* edg, int k, int m, int G, int cs, int ct, int lm,
                                      const int* sl, const int* sh, const int* tl, const int* th, int ln)
 {
     TileLeaves lv;
-    lv.cor = cor;
     lv.cc = cs * ct;
+    lv.cor = cor;
+    lv.corm = cor + (kCornerShared + kCornerMember * m) * lv.cc;
     lv.ct = ct;
     lv.cs = cs;
     lv.mb = lm;
     lv.nb = ln;
-    lv.xl = cor + kCornerFields * lv.cc;
+    lv.xl = cor + (kCornerShared + kCornerMember * G) * lv.cc;
     lv.yl = lv.xl + kAlphaTile * cs;
     lv.sidx[0] = sl[lm];
     lv.sidx[1] = sh[lm];
@@ -663,6 +750,10 @@ NUSI_FN TileLeaves alpha_tile_leaves(const double* cor, const double* edg, int k
     lv.ted = edg + k * alpha_tile_edge_stride(cs, ct);
     lv.sed = lv.ted + kTEdgeFields * ct;
     lv.mbv = lv.sed + kSEdgeFields * cs;
+    const double* mbk = alpha_tile_member_block(const_cast<double*>(edg), cs, ct, G, k, m);
+    lv.tedm = mbk;
+    lv.sedm = mbk + ct;
+    lv.mbm = mbk + ct + 2 * cs;
     return lv;
 }
 

@@ -41,7 +41,9 @@ int hc_alpha_tiled(const double* pt, const int* flags, int T, const double* lo, 
     const Point P = mk(pt, flags);
     SplineSet spl{};
     const int nt = (T + kAlphaTile - 1) / kAlphaTile;
-    std::vector<double> sm(kCornerFields * 4 * kAlphaTile * kAlphaTile + 4 * 4 * kAlphaTile * kAlphaTile + 3 * 1000);
+    constexpr int G = 1;   // a batch of one point (the tile kernel's per-table path)
+    std::vector<double> sm(alpha_tile_corner_block(2 * kAlphaTile, 2 * kAlphaTile, G) +
+                           alpha_tile_edge_doubles(2 * kAlphaTile, 2 * kAlphaTile, G));
     int warn = 0;
     for (int tm = 0; tm < nt; ++tm)
         for (int tn = 0; tn <= tm; ++tn) {
@@ -52,21 +54,26 @@ int hc_alpha_tiled(const double* pt, const int* flags, int T, const double* lo, 
             const int cs = alpha_edge_list(lo, hi, m0, T, sE, sl, sh);
             const int cc = cs * ct;
             double* cor = sm.data();
-            double* edg = cor + alpha_tile_corner_block(cs, ct);
-            for (int job = 0; job < 3 * (ct + cs + kAlphaTile); ++job)
+            double* edg = cor + alpha_tile_corner_block(cs, ct, G);
+            for (int job = 0; job < 3 * (ct + cs + kAlphaTile); ++job) {
                 alpha_tile_edge_job(P, job, tE, ct, sE, cs, lo, hi, m0, T, edg);
+                alpha_tile_edge_member_job(P, 0, G, job, tE, ct, sE, cs, lo, hi, m0, T, edg);
+            }
             double tot[kAlphaTile * kAlphaTile] = {};
             for (int k = 0; k < 3; ++k) {
                 if (P.non_resonant && P.majorana) {
                     const double* edgk = edg + k * alpha_tile_edge_stride(cs, ct);
-                    for (int j = 0; j < cc; ++j) alpha_tile_corner_job(P, j, edgk, ct, cs, cor);
+                    for (int j = 0; j < cc; ++j) {
+                        alpha_tile_corner_job(j, edgk, ct, cs, cor);
+                        alpha_tile_corner_member_job(P, 0, j, edgk, ct, cs, cor);
+                    }
                     for (int j = 0; j < kAlphaTile * (cs + ct); ++j)
-                        alpha_tile_mixed_job(j, edgk, ct, cs, tl, th, sl, sh, n0, m0, T, cor);
+                        alpha_tile_mixed_job(j, edgk, ct, cs, G, tl, th, sl, sh, n0, m0, T, cor);
                 }
                 for (int e = 0; e < kAlphaTile * kAlphaTile; ++e) {
                     const int ln = e % kAlphaTile, lm = e / kAlphaTile, n = n0 + ln, m = m0 + lm;
                     if (!(n < m && m < T) || !(P.non_resonant || m == n + 1)) continue;
-                    const TileLeaves lv = alpha_tile_leaves(cor, edg, k, cs, ct, lm, sl, sh, tl, th, ln);
+                    const TileLeaves lv = alpha_tile_leaves(cor, edg, k, 0, G, cs, ct, lm, sl, sh, tl, th, ln);
                     alpha_k(P, spl, k, lo[n], hi[n], lo[m], hi[m], lv, tot[e], warn);
                 }
             }

@@ -176,3 +176,21 @@ def test_cascade_kernels_agree(nusi, N, nonres):
             continue
         assert np.array_equal(f, ref[0]), "kind %d flux differs in %d entries" % (kind, np.sum(f != ref[0]))
         assert np.array_equal(fl, ref[1])
+
+
+def test_alpha_batches_bitexact(nusi, oracle_mod):
+    """Tables of points that share m_phi and the masses are built in batches (k_alpha_tile shares
+    the leaves of (S', t) alone): interleaved points of two m_phi values, four couplings each
+    (batches of 3 + 1), every table bit-exact against the oracle and every flux equal to its
+    single-point evolve."""
+    pts = [dict(cases.C2B_100, mphi=m, g=g) for g in (0.01, 0.03, 0.1, 0.3) for m in (6e5, 2e6)]
+    plan, flux, fla, tabs, _ = _gpu(nusi, pts)
+    for k, kw in enumerate(pts):
+        o = oracle_mod.Oracle(**cases.oracle_kwargs(kw))
+        G, aT, al = o.tables()
+        assert np.array_equal(tabs[k][0], G) and np.array_equal(tabs[k][1], aT)
+        iu = np.triu_indices(o.T, 1)
+        Ad = nusi.unpack_alpha(tabs[k][2], o.T)
+        assert np.array_equal(Ad[iu], al[iu]), "point %d: alpha differs in %d entries" % (k, np.sum(Ad[iu] != al[iu]))
+        _, f1, fl1, _, _ = _gpu(nusi, [kw])
+        assert np.array_equal(f1[0], flux[k]) and np.array_equal(fl1[0], fla[k])
