@@ -569,7 +569,7 @@ int nusi_plan_create(int device, int N_bins_E, double lEmin, double lEmax, doubl
     HIPCHECK(hipHostMalloc((void**)&pl->h_tpts, sizeof(nusi::Point) * max_points, hipHostMallocDefault));
     HIPCHECK(hipMalloc(&pl->d_batches, sizeof(int) * max_points));
     HIPCHECK(hipHostMalloc((void**)&pl->h_batches, sizeof(int) * max_points, hipHostMallocDefault));
-    if (const char* e = getenv("NUSI_ALPHA_BATCH")) pl->alpha_batch = std::max(1, std::min(8, atoi(e)));
+    if (const char* e = getenv("NUSI_ALPHA_BATCH")) pl->alpha_batch = std::max(1, std::min(4, atoi(e)));
     HIPCHECK(hipMalloc(&pl->d_warn, sizeof(int) * max_points));
     HIPCHECK(hipMalloc(&pl->tabs.G, sizeof(double) * (size_t)G.T * max_points));
     HIPCHECK(hipMalloc(&pl->tabs.At, sizeof(double) * (size_t)G.T * max_points));

@@ -102,9 +102,10 @@ __host__ __device__ constexpr int alpha_tile_lds_doubles(int cs, int ct, int G)
 // the channel flags (nusi_capi.cpp orders the tables so): the leaves of (S', t) alone -- the real
 // dilogarithms and most logarithms -- are evaluated once for the batch, the leaves that read
 // gr = Gamma_phi / m_phi once per point.  batches[y] = first table | count << 24 (nullptr: table y alone).
+template <int G>   // batch capacity (compile time, so that G = 1 keeps its sum in a register)
 __global__ __launch_bounds__(kTileThreads) NUSI_TILE_ATTR void k_alpha_tile(GridDev g, const Point* __restrict__ pts, SplineSet spl,
                                                            const int* __restrict__ tiles, int cs_max, int ct_max,
-                                                           const int* __restrict__ batches, int G,
+                                                           const int* __restrict__ batches,
                                                            double* __restrict__ A, int* __restrict__ warn)
 {
     extern __shared__ __attribute__((aligned(16))) double sm[];
@@ -114,7 +115,7 @@ __global__ __launch_bounds__(kTileThreads) NUSI_TILE_ATTR void k_alpha_tile(Grid
     __shared__ double elo[2][kAlphaTile], ehi[2][kAlphaTile];   // bin edges of both sides, staged in parallel
     const int tid = threadIdx.x, T = g.T;
     const int bw = batches ? batches[blockIdx.y] : (int)blockIdx.y | (1 << 24);
-    const int p0 = bw & 0xffffff, nb = bw >> 24;   // tables p0 .. p0 + nb - 1 (nb <= G)
+    const int p0 = bw & 0xffffff, nb = (G == 1) ? 1 : bw >> 24;   // tables p0 .. p0 + nb - 1 (nb <= G)
     const int tw = tiles[blockIdx.x];
     const int n0 = (tw & 0xffff) * kAlphaTile, m0 = (tw >> 16) * kAlphaTile;
     const Point& P = pts[p0];   // the batch's shared fields (m_phi, masses, flags)
@@ -266,11 +267,18 @@ hipError_t launch_alpha(const GridDev& g, const Point* pts, int npts, const Spli
         if (at.ncls[c] == 0) continue;
         const int cs = at.cs_max[c], ct = at.ct_max[c];
         // class 0 (core tiles) runs on batches of tables sharing their (S', t) leaves; the others per table
+        // (batching class 1 too measured slower: its LDS then allows 2 workgroups/CU, profiles/r1l)
         const bool batched = c == 0 && batches && gmax > 1;
-        const int G = batched ? gmax : 1;
+        const int G = batched ? (gmax < 4 ? gmax : 4) : 1;
         const size_t lds = sizeof(double) * (size_t)alpha_tile_lds_doubles(cs, ct, G);
-        hipLaunchKernelGGL(k_alpha_tile, dim3(at.ncls[c], batched ? nbatches : npts), dim3(kTileThreads), lds, s, g,
-                           pts, spl, at.tiles + off, cs, ct, batched ? batches : nullptr, G, t.A, warn);
+        const dim3 grid(at.ncls[c], batched ? nbatches : npts), blk(kTileThreads);
+        const int* bt = batched ? batches : nullptr;
+        switch (G) {
+        case 1: hipLaunchKernelGGL(k_alpha_tile<1>, grid, blk, lds, s, g, pts, spl, at.tiles + off, cs, ct, bt, t.A, warn); break;
+        case 2: hipLaunchKernelGGL(k_alpha_tile<2>, grid, blk, lds, s, g, pts, spl, at.tiles + off, cs, ct, bt, t.A, warn); break;
+        case 3: hipLaunchKernelGGL(k_alpha_tile<3>, grid, blk, lds, s, g, pts, spl, at.tiles + off, cs, ct, bt, t.A, warn); break;
+        default: hipLaunchKernelGGL(k_alpha_tile<4>, grid, blk, lds, s, g, pts, spl, at.tiles + off, cs, ct, bt, t.A, warn); break;
+        }
         off += at.ncls[c];
     }
     return hipGetLastError();
