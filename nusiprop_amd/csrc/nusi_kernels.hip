@@ -117,20 +117,25 @@ __global__ __launch_bounds__(kTileThreads) NUSI_TILE_ATTR void k_alpha_tile(Grid
     const int bw = batches ? batches[blockIdx.y] : (int)blockIdx.y | (1 << 24);
     const int p0 = bw & 0xffffff, nb = (G == 1) ? 1 : bw >> 24;   // tables p0 .. p0 + nb - 1 (nb <= G)
     const int tw = tiles[blockIdx.x];
-    const int n0 = (tw & 0xffff) * kAlphaTile, m0 = (tw >> 16) * kAlphaTile;
+    // tile word: tn | tm << 14 | half << 28; half 1 / 2 = the first 8 / last 7 m bins of the tile only
+    // (the redshift-extended m tiles are split so that their 16 S' edges fit the core tiles' LDS)
+    const int half = (tw >> 28) & 3;
+    const int n0 = (tw & 0x3fff) * kAlphaTile, m0 = ((tw >> 14) & 0x3fff) * kAlphaTile + (half == 2 ? 8 : 0);
+    const int mcnt = half == 0 ? kAlphaTile : (half == 1 ? 8 : kAlphaTile - 8);
+    const int Tm = (m0 + mcnt < T) ? m0 + mcnt : T;   // bins of the m side: [m0, Tm)
     const Point& P = pts[p0];   // the batch's shared fields (m_phi, masses, flags)
     if (tid < 2 * kAlphaTile) {
         const int side = tid / kAlphaTile, j = tid - side * kAlphaTile, b = (side ? m0 : n0) + j;
-        if (b < T) { elo[side][j] = g.lo[b]; ehi[side][j] = g.hi[b]; }
+        if (b < (side ? Tm : T)) { elo[side][j] = g.lo[b]; ehi[side][j] = g.hi[b]; }
     }
     __syncthreads();
     if (tid == 0) cnt[0] = alpha_edge_list(elo[0], ehi[0], 0, T - n0, tE, tl, th);
-    if (tid == 64) cnt[1] = alpha_edge_list(elo[1], ehi[1], 0, T - m0, sE, sl, sh);
+    if (tid == 64) cnt[1] = alpha_edge_list(elo[1], ehi[1], 0, Tm - m0, sE, sl, sh);
     __syncthreads();
     const int ct = cnt[0], cs = cnt[1], cc = cs * ct;
     const int ln = tid % kAlphaTile, lm = tid / kAlphaTile;
     const int n = n0 + ln, m = m0 + lm;
-    const bool valid = tid < kAlphaTile * kAlphaTile && n < m && m < T;
+    const bool valid = tid < kAlphaTile * kAlphaTile && n < m && m < Tm;
     if (cs > cs_max || ct > ct_max || nb > G) {   // host classification guarantees this never happens
         if (valid)
             for (int q = 0; q < nb; ++q) A[(size_t)(p0 + q) * g.PT + (size_t)m * (m - 1) / 2 + n] = __builtin_nan("");
@@ -156,10 +161,10 @@ __global__ __launch_bounds__(kTileThreads) NUSI_TILE_ATTR void k_alpha_tile(Grid
             job = tid;
         }
         if (job >= 0) {   // the shared leaves, then the same edge's member leaves of every batch point
-            alpha_tile_edge_job(P, job, tE, ct, sE, cs, g.lo, g.hi, m0, T, edg);
+            alpha_tile_edge_job(P, job, tE, ct, sE, cs, g.lo, g.hi, m0, Tm, edg);
 #pragma unroll 1
             for (int q = 0; q < nb; ++q)
-                alpha_tile_edge_member_job(pts[p0 + q], q, G, job, tE, ct, sE, cs, g.lo, g.hi, m0, T, edg);
+                alpha_tile_edge_member_job(pts[p0 + q], q, G, job, tE, ct, sE, cs, g.lo, g.hi, m0, Tm, edg);
         }
         if (G > 1)
             for (int q = 0; q < nb; ++q) tsum[q * kTileThreads + tid] = 0.0;
@@ -175,7 +180,7 @@ __global__ __launch_bounds__(kTileThreads) NUSI_TILE_ATTR void k_alpha_tile(Grid
                 for (int q = 0; q < nb; ++q) alpha_tile_corner_member_job(pts[p0 + q], q, j, edgk, ct, cs, cor);
             }
             for (int j = tid; j < kAlphaTile * (cs + ct); j += kTileThreads)
-                alpha_tile_mixed_job(j, edgk, ct, cs, G, tl, th, sl, sh, n0, m0, T, cor);
+                alpha_tile_mixed_job(j, edgk, ct, cs, G, tl, th, sl, sh, n0, m0, T, Tm, cor);
         }
 #endif
         __syncthreads();
@@ -221,12 +226,22 @@ hipError_t alpha_tiles_create(int T, const unsigned char* shared, AlphaTilesDev*
     bool tail_ext = true;   // no bin from tile t0 on shares an edge with its neighbour
     for (int n = t0 * kAlphaTile; n + 1 < T; ++n) tail_ext = tail_ext && !shared[n];
     out->ext_lo = (tail_ext && t0 < nt) ? t0 * kAlphaTile : T;
+    // Class-1 tiles (t side core, S' side extended: 30 S' edges) are split into their first 8 and last
+    // 7 m bins (16 / 14 S' edges): the halves fit the core tiles' LDS footprint and join class 0,
+    // whose launch builds batches of tables (NUSI_ALPHA_SPLIT_EXT=0 keeps them whole, A/B).
+    static const bool split_ext = !(getenv("NUSI_ALPHA_SPLIT_EXT") && atoi(getenv("NUSI_ALPHA_SPLIT_EXT")) == 0);
     std::vector<int> cls[3];
     for (int tm = 0; tm < nt; ++tm)
         for (int tn = 0; tn <= tm; ++tn) {
             const int c = (ne[tn] <= cap_core && ne[tm] <= cap_core) ? 0 : (ne[tn] <= cap_core) ? 1 : 2;
             if (tn * kAlphaTile >= out->ext_lo) continue;   // per-entry region
-            cls[c].push_back(tn | (tm << 16));
+            const int w = tn | (tm << 14);
+            if (c == 1 && split_ext && tn < tm) {
+                cls[0].push_back(w | (1 << 28));
+                if (tm * kAlphaTile + 8 < T) cls[0].push_back(w | (2 << 28));
+            } else {
+                cls[c].push_back(w);
+            }
         }
     const int csm[3] = {cap_core, cap_ext, cap_ext}, ctm[3] = {cap_core, cap_core, cap_ext};
     std::vector<int> all;

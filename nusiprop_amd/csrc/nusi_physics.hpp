@@ -713,7 +713,7 @@ NUSI_FN void alpha_tile_corner_member_job(const Point& P, int m, int j, const do
 // job j in [0, kAlphaTile (cs + ct)): the xlog leaf (S' slot, n bin) or the ylog leaf (m bin, t slot)
 // of mass state k (shared), into the block after the corners; bins past the table are skipped
 NUSI_FN void alpha_tile_mixed_job(int j, const double* edgk, int ct, int cs, int G, const int* tl, const int* th,
-                                  const int* sl, const int* sh, int n0, int m0, int T, double* cor)
+                                  const int* sl, const int* sh, int n0, int m0, int T, int Tm, double* cor)
 {
     const double* tv = edgk + kTEdgeVal * ct;                           // t of each t slot
     const double* sv = edgk + kTEdgeFields * ct + kSEdgeVal * cs;       // S' of each S' slot
@@ -725,7 +725,7 @@ NUSI_FN void alpha_tile_mixed_job(int j, const double* edgk, int ct, int cs, int
         xl[j] = alpha_xlog(sv[s], tv[tl[ln]], tv[th[ln]]);
     } else {
         const int q = j - kAlphaTile * cs, lm = q / ct, t = q - lm * ct;
-        if (m0 + lm >= T) return;
+        if (m0 + lm >= Tm) return;   // Tm: end of the tile's m bins
         yl[q] = alpha_ylog(sv[sl[lm]], sv[sh[lm]], tv[t]);
     }
 }

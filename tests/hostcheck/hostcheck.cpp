@@ -68,7 +68,7 @@ int hc_alpha_tiled(const double* pt, const int* flags, int T, const double* lo, 
                         alpha_tile_corner_member_job(P, 0, j, edgk, ct, cs, cor);
                     }
                     for (int j = 0; j < kAlphaTile * (cs + ct); ++j)
-                        alpha_tile_mixed_job(j, edgk, ct, cs, G, tl, th, sl, sh, n0, m0, T, cor);
+                        alpha_tile_mixed_job(j, edgk, ct, cs, G, tl, th, sl, sh, n0, m0, T, T, cor);
                 }
                 for (int e = 0; e < kAlphaTile * kAlphaTile; ++e) {
                     const int ln = e % kAlphaTile, lm = e / kAlphaTile, n = n0 + ln, m = m0 + lm;
