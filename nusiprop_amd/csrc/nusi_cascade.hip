@@ -512,9 +512,9 @@ __global__ __launch_bounds__(kWfMaxThreads) void k_cascade_wf(GridDev g, const P
     const int KR = K * NJ;                   // records per batch (field stride)
     double* F = lds;                         // [3][N]
     double* rec = F + 3 * N;                 // [kWfFields][K][NJ]
-    double* Tp = rec + kWfFields * KR;       // [NJ]  T_j of this stage
-    double* AX = Tp + NJ;                    // [NJ]  accumulators of the row the chain solves next
-    double* rdE = AX + NJ;                   // cascade_aux_init tables
+    double* Tp = rec + kWfFields * KR;       // [2][NJ]  T_j of the stage (double-buffered by stage parity)
+    double* AX = Tp + 2 * NJ;                // [2][NJ]  accumulators B_j of the row the chain solves next
+    double* rdE = AX + 2 * NJ;               // cascade_aux_init tables
     double* pw = rdE + N;
     // per-point and grid arrays the stage loop reads, staged in LDS: the loop's only global loads
     // are then the alpha-column prefetches, whose waits the compiler can count exactly
@@ -539,11 +539,11 @@ __global__ __launch_bounds__(kWfMaxThreads) void k_cascade_wf(GridDev g, const P
     const bool nonres = P.non_resonant;
 
     for (int b = tid; b < 3 * N; b += nthr) F[b] = 0.0;
-    for (int j = tid; j < NJ; j += nthr) AX[j] = Tp[j] = 0.0;
+    for (int j = tid; j < 2 * NJ; j += nthr) AX[j] = Tp[j] = 0.0;
     for (int n = tid; n < T; n += nthr) {
         sGt[n] = Gt[n];
         sAt[n] = At[n];
-        sdg[n] = (!nonres && n + 1 < T) ? Al[(size_t)(n + 1) * n / 2 + n] : 0.0;
+        sdg[n] = (n + 1 < T) ? Al[(size_t)(n + 1) * n / 2 + n] : 0.0;
     }
     for (int b = tid; b < N; b += nthr) { sEmin[b] = g.Emin[b]; sEmax[b] = g.Emax[b]; }
     for (int i = tid; i < Nz; i += nthr) {
@@ -561,19 +561,22 @@ __global__ __launch_bounds__(kWfMaxThreads) void k_cascade_wf(GridDev g, const P
     for (int c = 0; c < kWfRows; ++c)
 #pragma unroll
         for (int jj = 0; jj < JG; ++jj) acc[c][jj] = 0.0;
-    // chain lane state (wave 0, lane = step slot j)
-    const int ist = Nz - 1 - tid;
+    // chain lane state (the last wave, lane = step slot j)
+    const int cbase = nthr - 64, cj_lane = tid - cbase;
+    const bool chain = cj_lane >= 0 && cj_lane < nst;
+    const int ist = Nz - 1 - cj_lane;
     __syncthreads();   // staged arrays visible; the chain reads its step's c_i, s_i from LDS (a global load
                        // here would be waited for with vmcnt(0) inside the loop, draining the prefetches)
-    const double cj = (tid < nst) ? gl.step_c[ist] : 0.0, sj = (tid < nst) ? gl.step_s[ist] : 0.0;
+    const double cj = chain ? gl.step_c[ist] : 0.0, sj = chain ? gl.step_s[ist] : 0.0;
     double racc = 0.0, px0 = 0.0, px1 = 0.0, px2 = 0.0;
+    double Tprev = 0.0;   // the lane's T_j of the previous stage
     // alpha(row, column) of the next kWfPre stages' columns (ring, [0] = this stage's), rows clamped
     // into the column; each load is issued kWfPre stages before its use (HBM latency > a stage)
     // The loads are unconditional (column clamped to >= 1, rows into the column; resonant-only
     // tables are allocated in full): a load skipped on some path would make the compiler wait for
     // every outstanding load (vmcnt(0)) at the next use.  Columns < 1 are never pushed.
     auto load_col = [&](int col, double (&dst)[kWfRows]) {
-        const int cl = col < 1 ? 1 : col;
+        const int cl = col < 1 ? 1 : (col > T - 1 ? T - 1 : col);
         const size_t cb = (size_t)cl * (cl - 1) / 2;
 #pragma unroll
         for (int c = 0; c < kWfRows; ++c) {
@@ -584,7 +587,7 @@ __global__ __launch_bounds__(kWfMaxThreads) void k_cascade_wf(GridDev g, const P
     double a_ring[kWfPre][kWfRows];
 #pragma unroll
     for (int d = 0; d < kWfPre; ++d) {   // issued in slot order (the loop's waits count on it)
-        load_col(T - 1 - d, a_ring[d]);
+        load_col(T - d, a_ring[d]);      // stage d pushes column T - d (none at stage 0)
         NUSI_PHASE();
     }
     // stage sg; ac = its alpha column (ring slot sg % kWfPre), reloaded with the column kWfPre
@@ -607,15 +610,22 @@ __global__ __launch_bounds__(kWfMaxThreads) void k_cascade_wf(GridDev g, const P
             }
             __syncthreads();
         }
-        // ---- P1: the chain, one lane per active step
-        if (tid < nst) {
+        // ---- one phase per stage (one barrier):
+        //   the chain (last wave) solves column r: its row's accumulator is the published B_j(r)
+        //   (columns >= r+2) plus column r+1, which the lane adds itself from its own T_j(sg-1);
+        //   the bulk push (other waves) adds column r+1 (T of stage sg-1) to the rows < r and
+        //   publishes B(r-1) (columns >= r+1) for the next stage.  Every accumulator receives the
+        //   same fma()s in the same descending-column order as before.
+        const int cur = sg & 1, prv = cur ^ 1;
+        if (chain) {
+            const int tid = cj_lane;
             const int b = N - 1 - sg + tid;
             double T_j = 0.0;
             if (b >= 0 && b < N) {
                 const double* R = rec + ks * NJ + tid;
                 double add;
                 if (nonres) {
-                    add = cj * AX[tid];
+                    add = cj * fma(sdg[r], Tprev, AX[prv * NJ + tid]);
                 } else {
                     if (b != N - 1) {
                         const double Sres = u0 * px0 + u1 * px1 + u2 * px2;
@@ -636,30 +646,29 @@ __global__ __launch_bounds__(kWfMaxThreads) void k_cascade_wf(GridDev g, const P
                 px0 = x0; px1 = x1; px2 = x2;
                 if (nonres && b > 0) T_j = (u0 * x0 + u1 * x1 + u2 * x2) * R[PR_SDE * KR];
             }
-            Tp[tid] = T_j;
-        }
-        __syncthreads();
-        // ---- P2: push column r into rows < r.  Rows >= r were consumed already and steps that
-        // have not started have T_j = 0 (their accumulators stay exactly 0), so nothing is masked.
-        if (nonres && r >= 1 && !(NUSI_WF_AB & 2)) {
-            const double* Th = Tp + h * JG;
+            Tp[cur * NJ + tid] = T_j;
+            Tprev = T_j;
+        } else if (tid < cbase && nonres && r >= 1 && r + 1 <= T - 1 && !(NUSI_WF_AB & 2)) {
+            // push column r+1 (T of stage sg-1) into rows < r; rows >= r are consumed (row r through
+            // the published copy) and steps that have not started have T_j = 0, so nothing is masked
+            const double* Th = Tp + prv * NJ + h * JG;
 #pragma unroll
             for (int jj = 0; jj < JG; ++jj) {
                 const double tj = Th[jj];
 #pragma unroll
                 for (int c = 0; c < kWfRows; ++c) acc[c][jj] = fma(ac[c], tj, acc[c][jj]);
             }
-            if (r - 1 >= row0 && r - 1 < row0 + kWfRows) {   // publish row r-1 for the next chain
+            if (r - 1 >= row0 && r - 1 < row0 + kWfRows) {   // publish B(r-1) for the next stage's chain
                 const int cp = r - 1 - row0;
 #pragma unroll
                 for (int c = 0; c < kWfRows; ++c)
                     if (c == cp) {
 #pragma unroll
-                        for (int jj = 0; jj < JG; ++jj) AX[h * JG + jj] = acc[c][jj];
+                        for (int jj = 0; jj < JG; ++jj) AX[cur * NJ + h * JG + jj] = acc[c][jj];
                     }
             }
         }
-        load_col(r - kWfPre, ac);
+        load_col(r + 1 - kWfPre, ac);
         __syncthreads();
     }
     // finalise (nuSIprop.hpp:328-336)
@@ -682,10 +691,10 @@ struct WfGeom { int nthr, K; size_t lds; };
 static WfGeom wf_geom(const GridDev& g, int NJ)
 {
     WfGeom w;
-    w.nthr = ((((g.T - 1 + kWfRows - 1) / kWfRows) * kWfQuarters + 63) / 64) * 64;
+    w.nthr = ((((g.T - 1 + kWfRows - 1) / kWfRows) * kWfQuarters + 63) / 64) * 64 + 64;   // rows + the chain wave
     w.K = w.nthr / NJ;
     auto bytes = [&](int K) {
-        return sizeof(double) * (3 * (size_t)g.N + (size_t)kWfFields * K * NJ + 2 * NJ + cascade_aux_doubles(g.N, g.T) +
+        return sizeof(double) * (3 * (size_t)g.N + (size_t)kWfFields * K * NJ + 4 * NJ + cascade_aux_doubles(g.N, g.T) +
                                  3 * (size_t)g.T + 2 * (size_t)g.N + 4 * (size_t)g.Nz);
     };
     while (w.K > 1 && bytes(w.K) > kWfMaxLds) --w.K;
