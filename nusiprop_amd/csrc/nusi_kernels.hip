@@ -6,6 +6,7 @@
 //   (Stage B, the cascade, is in nusi_cascade.hip)
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdlib>
 #include <vector>
 
@@ -117,25 +118,30 @@ __global__ __launch_bounds__(kTileThreads) NUSI_TILE_ATTR void k_alpha_tile(Grid
     const int bw = batches ? batches[blockIdx.y] : (int)blockIdx.y | (1 << 24);
     const int p0 = bw & 0xffffff, nb = (G == 1) ? 1 : bw >> 24;   // tables p0 .. p0 + nb - 1 (nb <= G)
     const int tw = tiles[blockIdx.x];
-    // tile word: tn | tm << 14 | half << 28; half 1 / 2 = the first 8 / last 7 m bins of the tile only
-    // (the redshift-extended m tiles are split so that their 16 S' edges fit the core tiles' LDS)
-    const int half = (tw >> 28) & 3;
-    const int n0 = (tw & 0x3fff) * kAlphaTile, m0 = ((tw >> 14) & 0x3fff) * kAlphaTile + (half == 2 ? 8 : 0);
+    // tile word: tn | tm << 14 | mhalf << 28 | nhalf << 30; half 1 / 2 = the first 8 / last 7 bins of
+    // that side of the tile only (redshift-extended sides are split so that their at most 16 edges fit
+    // the core tiles' LDS)
+    const unsigned tu = (unsigned)tw;
+    const int half = (tu >> 28) & 3, nhalf = (tu >> 30) & 3;
+    const int n0 = (tu & 0x3fff) * kAlphaTile + (nhalf == 2 ? 8 : 0);
+    const int m0 = ((tu >> 14) & 0x3fff) * kAlphaTile + (half == 2 ? 8 : 0);
     const int mcnt = half == 0 ? kAlphaTile : (half == 1 ? 8 : kAlphaTile - 8);
+    const int ncnt = nhalf == 0 ? kAlphaTile : (nhalf == 1 ? 8 : kAlphaTile - 8);
     const int Tm = (m0 + mcnt < T) ? m0 + mcnt : T;   // bins of the m side: [m0, Tm)
+    const int Tn = (n0 + ncnt < T) ? n0 + ncnt : T;   // bins of the n side: [n0, Tn)
     const Point& P = pts[p0];   // the batch's shared fields (m_phi, masses, flags)
     if (tid < 2 * kAlphaTile) {
         const int side = tid / kAlphaTile, j = tid - side * kAlphaTile, b = (side ? m0 : n0) + j;
-        if (b < (side ? Tm : T)) { elo[side][j] = g.lo[b]; ehi[side][j] = g.hi[b]; }
+        if (b < (side ? Tm : Tn)) { elo[side][j] = g.lo[b]; ehi[side][j] = g.hi[b]; }
     }
     __syncthreads();
-    if (tid == 0) cnt[0] = alpha_edge_list(elo[0], ehi[0], 0, T - n0, tE, tl, th);
+    if (tid == 0) cnt[0] = alpha_edge_list(elo[0], ehi[0], 0, Tn - n0, tE, tl, th);
     if (tid == 64) cnt[1] = alpha_edge_list(elo[1], ehi[1], 0, Tm - m0, sE, sl, sh);
     __syncthreads();
     const int ct = cnt[0], cs = cnt[1], cc = cs * ct;
     const int ln = tid % kAlphaTile, lm = tid / kAlphaTile;
     const int n = n0 + ln, m = m0 + lm;
-    const bool valid = tid < kAlphaTile * kAlphaTile && n < m && m < Tm;
+    const bool valid = tid < kAlphaTile * kAlphaTile && n < m && m < Tm && n < Tn;
     if (cs > cs_max || ct > ct_max || nb > G) {   // host classification guarantees this never happens
         if (valid)
             for (int q = 0; q < nb; ++q) A[(size_t)(p0 + q) * g.PT + (size_t)m * (m - 1) / 2 + n] = __builtin_nan("");
@@ -180,7 +186,7 @@ __global__ __launch_bounds__(kTileThreads) NUSI_TILE_ATTR void k_alpha_tile(Grid
                 for (int q = 0; q < nb; ++q) alpha_tile_corner_member_job(pts[p0 + q], q, j, edgk, ct, cs, cor);
             }
             for (int j = tid; j < kAlphaTile * (cs + ct); j += kTileThreads)
-                alpha_tile_mixed_job(j, edgk, ct, cs, G, tl, th, sl, sh, n0, m0, T, Tm, cor);
+                alpha_tile_mixed_job(j, edgk, ct, cs, G, tl, th, sl, sh, n0, m0, Tn, Tm, cor);
         }
 #endif
         __syncthreads();
@@ -225,7 +231,11 @@ hipError_t alpha_tiles_create(int T, const unsigned char* shared, AlphaTilesDev*
         if (ne[t] > cap_core) { t0 = t; break; }
     bool tail_ext = true;   // no bin from tile t0 on shares an edge with its neighbour
     for (int n = t0 * kAlphaTile; n + 1 < T; ++n) tail_ext = tail_ext && !shared[n];
-    out->ext_lo = (tail_ext && t0 < nt) ? t0 * kAlphaTile : T;
+    // NUSI_ALPHA_EXT_TILES=0 (A/B): the extended triangle runs on the per-entry kernel instead of
+    // quarter tiles (8 x 8 bins, batched with the core tiles)
+    static const bool ext_tiles = !(getenv("NUSI_ALPHA_EXT_TILES") && atoi(getenv("NUSI_ALPHA_EXT_TILES")) == 0);
+    out->ext_lo = (tail_ext && t0 < nt && !ext_tiles) ? t0 * kAlphaTile : T;
+    const int qlo = (tail_ext && t0 < nt && ext_tiles) ? t0 : nt;   // tiles from qlo on: split on both sides
     // Class-1 tiles (t side core, S' side extended: 30 S' edges) are split into their first 8 and last
     // 7 m bins (16 / 14 S' edges): the halves fit the core tiles' LDS footprint and join class 0,
     // whose launch builds batches of tables (NUSI_ALPHA_SPLIT_EXT=0 keeps them whole, A/B).
@@ -236,7 +246,15 @@ hipError_t alpha_tiles_create(int T, const unsigned char* shared, AlphaTilesDev*
             const int c = (ne[tn] <= cap_core && ne[tm] <= cap_core) ? 0 : (ne[tn] <= cap_core) ? 1 : 2;
             if (tn * kAlphaTile >= out->ext_lo) continue;   // per-entry region
             const int w = tn | (tm << 14);
-            if (c == 1 && split_ext && tn < tm) {
+            if (tn >= qlo) {   // both sides extended: up to 4 quarter tiles (n half, m half)
+                for (int nh = 1; nh <= 2; ++nh)
+                    for (int mh = 1; mh <= 2; ++mh) {
+                        const int nb0 = tn * kAlphaTile + (nh == 2 ? 8 : 0), mb0 = tm * kAlphaTile + (mh == 2 ? 8 : 0);
+                        const int mb1 = std::min(T, tm * kAlphaTile + (mh == 1 ? 8 : kAlphaTile));
+                        if (nb0 >= T || mb0 >= T || nb0 >= mb1 - 1) continue;   // no entry n < m
+                        cls[0].push_back((int)((unsigned)w | ((unsigned)mh << 28) | ((unsigned)nh << 30)));
+                    }
+            } else if (c == 1 && split_ext && tn < tm) {
                 cls[0].push_back(w | (1 << 28));
                 if (tm * kAlphaTile + 8 < T) cls[0].push_back(w | (2 << 28));
             } else {
