@@ -191,6 +191,13 @@ __global__ __launch_bounds__(kTileThreads) NUSI_TILE_ATTR void k_alpha_tile(Grid
 #endif
         __syncthreads();
         if (needed) {
+            // the t and tu channels' brackets depend on the shared leaves only: once per entry
+            AlphaPre pre;
+            const bool share = G > 1 && nb > 1 && nonres && maj;
+            if (share) {
+                const TileLeaves lv0 = alpha_tile_leaves(cor, edg, k, 0, G, cs, ct, lm, sl, sh, tl, th, ln);
+                alpha_k_pre(P, k, g.lo[n], g.hi[n], g.lo[m], g.hi[m], lv0, pre);
+            }
 #pragma unroll 1
             for (int q = 0; q < nb; ++q) {
                 double tot = (G > 1) ? tsum[q * kTileThreads + tid] : tot1;
@@ -199,7 +206,7 @@ __global__ __launch_bounds__(kTileThreads) NUSI_TILE_ATTR void k_alpha_tile(Grid
                 tot += cor[(tid * 7) % cc] + edg[tid % 64];
 #else
                 const TileLeaves lv = alpha_tile_leaves(cor, edg, k, q, G, cs, ct, lm, sl, sh, tl, th, ln);
-                alpha_k(pts[p0 + q], spl, k, g.lo[n], g.hi[n], g.lo[m], g.hi[m], lv, tot, w);
+                alpha_k(pts[p0 + q], spl, k, g.lo[n], g.hi[n], g.lo[m], g.hi[m], lv, tot, w, share ? &pre : nullptr);
 #endif
                 if (G > 1) tsum[q * kTileThreads + tid] = tot;
                 else tot1 = tot;

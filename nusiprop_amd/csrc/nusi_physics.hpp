@@ -811,10 +811,84 @@ NUSI_FN_OUT double alpha_phiphi(const Point& P, const SplineSet& spl, double uk,
 #else
 #define NUSI_PHASE() do { } while (0)
 #endif
-// one mass state k of alpha(Em, Ep, Em', Ep'): tot += wgt * (every channel)
+// The Majorana t (:1281-1333) and tu (:1370-1425) channels are g^4 / D * B with D and the bracket B
+// functions of the (S', t) leaves alone: points of a batch (same m_phi, masses, flags) share them.
+struct AlphaPre { double Dt, Bt, Dtu, Btu; };
+template <class Lv>
+NUSI_FN void alpha_bracket_t(const Lv& lv, double Sm, double Sp, double tm, double tp, double m4, double& D, double& B)
+{
+    const AlphaSEdge eSm = lv.sedge(0, Sm), eSp = lv.sedge(1, Sp);
+    const double lSm = eSm.lS, lSp = eSp.lS;
+    const double SS = Sm * Sp;
+    const AlphaCorner cmm = lv.corner(0, 0, Sm, tm), cpm = lv.corner(1, 0, Sp, tm);
+    const AlphaCorner cmq = lv.corner(0, 1, Sm, tp), cpq = lv.corner(1, 1, Sp, tp);
+    const double Lmm = cmm.L, Lpm = cpm.L, Lmq = cmq.L, Lpq = cpq.L;
+    const double LA = lv.xlog(0, Sm, tm, tp), LB = lv.xlog(1, Sp, tm, tp);
+    const double inner = SS * (-tm + tp) * lSm + SS * (tm - tp) * lSp - SS * Lmm - SS * tp * Lmm + SS * Lpm + SS * tp * Lpm
+                         - Sp * LA - Sp * tm * LA - Sp * tp * LA - Sp * tm * tp * LA
+                         + SS * cmq.LL + SS * tm * Lmq
+                         + Sm * LB + Sm * tm * LB + Sm * tp * LB + Sm * tm * tp * LB
+                         - SS * cpq.LL - SS * tm * Lpq;
+    D = Sm * Sp * 16 * kPi * m4;
+    B = (-((Sm - Sp) * (3 + 2 * tm * (-1 + tp) - 2 * tp) * (tm - tp)) / ((-1 + tm) * (-1 + tp))
+         + 2 * inner / ((1 + tm) * (1 + tp))
+         - ((SS * lv.ylog(0, Sm, Sp, tm)) / ((1 + tm) * (1 + tm))
+            + (((Sm - Sp) * (tm - tp) * (1 + tp)) / (1 + tm) - SS * lv.ylog(1, Sm, Sp, tp)) / ((1 + tp) * (1 + tp))));
+}
+template <class Lv>
+NUSI_FN void alpha_bracket_tu(const Lv& lv, double Sm, double Sp, double tm, double tp, double m4, double& D, double& B)
+{
+    const double SS = Sm * Sp;
+    const AlphaCorner cmm = lv.corner(0, 0, Sm, tm), cpm = lv.corner(1, 0, Sp, tm);
+    const AlphaCorner cmq = lv.corner(0, 1, Sm, tp), cpq = lv.corner(1, 1, Sp, tp);
+    const AlphaSEdge fSm = lv.sedge(0, Sm), fSp = lv.sedge(1, Sp);
+    const AlphaTEdge fTm = lv.tedge(0, tm), fTp = lv.tedge(1, tp);
+    const AlphaMBin mc = lv.mbin(Sm, Sp);
+    const double Lmm = cmm.L, Lpm = cpm.L, Lmq = cmq.L, Lpq = cpq.L;
+    double Fp, Fm;
+    if (tp < -1) Fp = cmq.TU1 - cpq.TU1;
+    else {
+        const double a = cmq.TU2, b = cpq.TU2;
+        Fp = -cmq.TU1 + cpq.TU1 - 0.5 * (a * a - b * b);
+    }
+    if (tm < -1) Fm = -cmm.TU1 + cpm.TU1;
+    else {
+        const double a = cmm.TU2, b = cpm.TU2;
+        Fm = cmm.TU1 - cpm.TU1 + 0.5 * (a * a - b * b);
+    }
+    const double lap = fTp.la, lam = fTm.la;
+    const double Pq = (1 + tm) * (1 + tp);
+    const double l2m = fSm.l2, l2p = fSp.l2;
+    const double SSP = SS * (1 + tm) * (1 + tp);
+    const double lSm = fSm.lS, lSp = fSp.lS, Lmt = fTm.Lm1, Lmp = fTp.Lm1;
+    D = 32 * kPi * m4 * Sm * Sp * (1 + tm) * (1 + tp);
+    B = (-4 * (Sm - Sp) * (1 + tm) * (tm - tp) * (1 + tp)
+         + 2 * SS * tp * (mc.lr - Lmm + Lpm)
+         + 2 * Sp * (1 + tm) * (1 + tp) * (Lmt - Lmm - Lmp + Lmq)
+         - 2 * Sm * (1 + tm) * (1 + tp) * (Lmt - Lpm - Lmp + Lpq)
+         + 2 * SS * (-Lmm + Lpm + Lmq - Lpq)
+         + SSP * (l2m * (lSp + Lmq) - l2p * (lSm + Lpq) + Lmp * (mc.lr - Lmq + Lpq))
+         + SSP * ((lSp + Lmm) * (fSm.lS2 + Lmt - lam) + (lSm + Lpm) * (l2p - Lmt + lam))
+         + SS * (mc.lr2 + Lmq - Lpq) * (2 * tm + Pq * lap)
+         + SSP * (cmm.G - cpm.G - cmq.G + cpq.G)
+         + SSP * (Fp + Fm));
+}
+// the shared brackets of entry (Em, Ep, Em', Ep') and mass state k (Majorana, non-resonant)
+template <class Lv>
+NUSI_FN void alpha_k_pre(const Point& P, int k, double Em, double Ep, double Emp, double Epp, const Lv& lv, AlphaPre& pre)
+{
+    const double mphi = P.mphi, m2 = mphi * mphi, m4 = (mphi * mphi) * (mphi * mphi), mk = P.mn[k];
+    const double tp = lv.tval(1, mk, Ep, m2), tm = lv.tval(0, mk, Em, m2);
+    const double Sp = lv.Sval(1, mk, Epp, m2), Sm = lv.Sval(0, mk, Emp, m2);
+    alpha_bracket_t(lv, Sm, Sp, tm, tp, m4, pre.Dt, pre.Bt);
+    alpha_bracket_tu(lv, Sm, Sp, tm, tp, m4, pre.Dtu, pre.Btu);
+}
+
+// one mass state k of alpha(Em, Ep, Em', Ep'): tot += wgt * (every channel); pre: the shared brackets
+// of a batch (alpha_k_pre with another point of it), nullptr = evaluate them here
 template <class Lv>
 NUSI_FN void alpha_k(const Point& P, const SplineSet& spl, int k, double Em, double Ep, double Emp, double Epp,
-                     const Lv& lv, double& tot, int& warn)
+                     const Lv& lv, double& tot, int& warn, const AlphaPre* pre = nullptr)
 {
     const double g = P.g, mphi = P.mphi;
     const double g4 = (g * g) * (g * g), m2 = mphi * mphi, m4 = (mphi * mphi) * (mphi * mphi);
@@ -844,24 +918,13 @@ NUSI_FN void alpha_k(const Point& P, const SplineSet& spl, int k, double Em, dou
     const AlphaSEdge eSm = lv.sedge(0, Sm), eSp = lv.sedge(1, Sp);
     const double Lmt = eTm.Lm1, Lmp = eTp.Lm1;
     const double lSm = eSm.lS, lSp = eSp.lS;
-    const double SS = Sm * Sp;
     double at, au, atu = 0., ast;
     if (maj) {
         {
-            const AlphaCorner cmm = lv.corner(0, 0, Sm, tm), cpm = lv.corner(1, 0, Sp, tm);
-            const AlphaCorner cmq = lv.corner(0, 1, Sm, tp), cpq = lv.corner(1, 1, Sp, tp);
-            const double Lmm = cmm.L, Lpm = cpm.L, Lmq = cmq.L, Lpq = cpq.L;
-            const double LA = lv.xlog(0, Sm, tm, tp), LB = lv.xlog(1, Sp, tm, tp);
-            const double inner = SS * (-tm + tp) * lSm + SS * (tm - tp) * lSp - SS * Lmm - SS * tp * Lmm + SS * Lpm + SS * tp * Lpm
-                                 - Sp * LA - Sp * tm * LA - Sp * tp * LA - Sp * tm * tp * LA
-                                 + SS * cmq.LL + SS * tm * Lmq
-                                 + Sm * LB + Sm * tm * LB + Sm * tp * LB + Sm * tm * tp * LB
-                                 - SS * cpq.LL - SS * tm * Lpq;
-            at = g4 / (Sm * Sp * 16 * kPi * m4) *
-                 (-((Sm - Sp) * (3 + 2 * tm * (-1 + tp) - 2 * tp) * (tm - tp)) / ((-1 + tm) * (-1 + tp))
-                  + 2 * inner / ((1 + tm) * (1 + tp))
-                  - ((SS * lv.ylog(0, Sm, Sp, tm)) / ((1 + tm) * (1 + tm))
-                     + (((Sm - Sp) * (tm - tp) * (1 + tp)) / (1 + tm) - SS * lv.ylog(1, Sm, Sp, tp)) / ((1 + tp) * (1 + tp))));
+            double D, B;
+            if (pre) { D = pre->Dt; B = pre->Bt; }
+            else alpha_bracket_t(lv, Sm, Sp, tm, tp, m4, D, B);
+            at = g4 / D * B;
             if (at < 0) at = gl33_rect(0, tp, tm, Sm, Sp) * (g4 / (16 * kPi * m4));
             at *= uk;
             tot += wgt * at;
@@ -870,39 +933,10 @@ NUSI_FN void alpha_k(const Point& P, const SplineSet& spl, int k, double Em, dou
         }
         NUSI_PHASE();
         {
-            const AlphaCorner cmm = lv.corner(0, 0, Sm, tm), cpm = lv.corner(1, 0, Sp, tm);
-            const AlphaCorner cmq = lv.corner(0, 1, Sm, tp), cpq = lv.corner(1, 1, Sp, tp);
-            const AlphaSEdge fSm = lv.sedge(0, Sm), fSp = lv.sedge(1, Sp);
-            const AlphaTEdge fTm = lv.tedge(0, tm), fTp = lv.tedge(1, tp);
-            const AlphaMBin mc = lv.mbin(Sm, Sp);
-            const double Lmm = cmm.L, Lpm = cpm.L, Lmq = cmq.L, Lpq = cpq.L;
-            double Fp, Fm;
-            if (tp < -1) Fp = cmq.TU1 - cpq.TU1;
-            else {
-                const double a = cmq.TU2, b = cpq.TU2;
-                Fp = -cmq.TU1 + cpq.TU1 - 0.5 * (a * a - b * b);
-            }
-            if (tm < -1) Fm = -cmm.TU1 + cpm.TU1;
-            else {
-                const double a = cmm.TU2, b = cpm.TU2;
-                Fm = cmm.TU1 - cpm.TU1 + 0.5 * (a * a - b * b);
-            }
-            const double lap = fTp.la, lam = fTm.la;
-            const double Pq = (1 + tm) * (1 + tp);
-            const double l2m = fSm.l2, l2p = fSp.l2;
-            const double SSP = SS * (1 + tm) * (1 + tp);
-            const double lSm = fSm.lS, lSp = fSp.lS, Lmt = fTm.Lm1, Lmp = fTp.Lm1;
-            atu = g4 / (32 * kPi * m4 * Sm * Sp * (1 + tm) * (1 + tp)) *
-                  (-4 * (Sm - Sp) * (1 + tm) * (tm - tp) * (1 + tp)
-                   + 2 * SS * tp * (mc.lr - Lmm + Lpm)
-                   + 2 * Sp * (1 + tm) * (1 + tp) * (Lmt - Lmm - Lmp + Lmq)
-                   - 2 * Sm * (1 + tm) * (1 + tp) * (Lmt - Lpm - Lmp + Lpq)
-                   + 2 * SS * (-Lmm + Lpm + Lmq - Lpq)
-                   + SSP * (l2m * (lSp + Lmq) - l2p * (lSm + Lpq) + Lmp * (mc.lr - Lmq + Lpq))
-                   + SSP * ((lSp + Lmm) * (fSm.lS2 + Lmt - lam) + (lSm + Lpm) * (l2p - Lmt + lam))
-                   + SS * (mc.lr2 + Lmq - Lpq) * (2 * tm + Pq * lap)
-                   + SSP * (cmm.G - cpm.G - cmq.G + cpq.G)
-                   + SSP * (Fp + Fm));
+            double D, B;
+            if (pre) { D = pre->Dtu; B = pre->Btu; }
+            else alpha_bracket_tu(lv, Sm, Sp, tm, tp, m4, D, B);
+            atu = g4 / D * B;
             // nuSIprop.hpp:1401-1418: the fallback assigns a shadowing local; a negative alpha_tu stays.
             atu *= uk;
             tot += wgt * atu;
