@@ -136,17 +136,29 @@ NUSI_FN_OUT cd cli2(double x, double y)
 #ifdef NUSI_AB_STUB_CLI2   // timing experiments only
     return C(0.5 * x, 0.5 * y);
 #endif
-    cd z = C(x, y), add = C(0.0);
+    cd z = C(x, y), add = C(0.0), lz;
     double sgn = 1.0;
-    if (x * x + y * y > 1.0) {
-        const cd l = clog_p(-z);
-        add = -kZeta2 - 0.5 * (l * l);
+    bool have_lz = false;
+    const double n2 = x * x + y * y;
+    if (n2 > 1.0) {   // Li2(z) = -zeta2 - log^2(-z)/2 - Li2(1/z)
+        const double hl = 0.5 * NUSI_PLOG(n2);
+        double am;   // arg(-z); for x > 0 it comes from arg z (no cancellation: |arg z| < pi/2),
+        if (x > 0.0) {   // which then also gives log(1/z) = -log z for the reflection below
+            const double t = NUSI_PATAN2(y, x);
+            am = t - copysign(kPi, y);
+            lz = C(-hl, -t);
+            have_lz = true;
+        } else {
+            am = NUSI_PATAN2(-y, -x);
+        }
+        add = C(-kZeta2 - 0.5 * (hl * hl - am * am), -(hl * am));
         sgn = -1.0;
-        z = 1.0 / z;
+        const double ri = 1.0 / n2;   // 1/z = conj(z)/|z|^2
+        z = C(x * ri, -(y * ri));
     }
     cd u;   // u = -log(1 - z) of the series' argument
     if (z.r > 0.5) {   // Li2(z) = zeta2 - log(z) log(1-z) - Li2(1-z); for Li2(1-z), u = -log(z)
-        const cd lz = clog_p(z);
+        if (!have_lz) lz = clog_p(z);
         add = add + sgn * (kZeta2 - lz * clog_p(1.0 - z));
         sgn = -sgn;
         u = C(-lz.r, -lz.i);

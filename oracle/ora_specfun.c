@@ -65,18 +65,29 @@ void ora_complex_dilog_xy(double x, double y, double *re, double *im)
         *im = (x >= 1.0) ? -PI_D * ora_log(x) : 0.0;
         return;
     }
-    zc z = zmk(x, y), add = zmk(0.0, 0.0);
+    zc z = zmk(x, y), add = zmk(0.0, 0.0), lz = zmk(0.0, 0.0);
     double sgn = 1.0;
-    if (x * x + y * y > 1.0) {
-        const zc l = zlog(zmk(-z.r, -z.i));
-        const zc h = zscale(0.5, zmul(l, l));
-        add = zmk(-ZETA2 - h.r, -h.i);
+    int have_lz = 0;
+    const double n2 = x * x + y * y;
+    if (n2 > 1.0) {   /* Li2(z) = -zeta2 - log^2(-z)/2 - Li2(1/z) */
+        const double hl = 0.5 * ora_log(n2);
+        double am;   /* arg(-z): for x > 0 from arg z (|arg z| < pi/2, no cancellation), */
+        if (x > 0.0) {   /* which also gives log(1/z) = -log z for the reflection below */
+            const double t = ora_atan2(y, x);
+            am = t - copysign(PI_D, y);
+            lz = zmk(-hl, -t);
+            have_lz = 1;
+        } else {
+            am = ora_atan2(-y, -x);
+        }
+        add = zmk(-ZETA2 - 0.5 * (hl * hl - am * am), -(hl * am));
         sgn = -1.0;
-        z = zrdiv(1.0, z);
+        const double ri = 1.0 / n2;   /* 1/z = conj(z)/|z|^2 */
+        z = zmk(x * ri, -(y * ri));
     }
     zc u;   /* u = -log(1 - z) of the series' argument */
     if (z.r > 0.5) {   /* Li2(z) = zeta2 - log(z) log(1-z) - Li2(1-z); for Li2(1-z), u = -log(z) */
-        const zc lz = zlog(z);
+        if (!have_lz) lz = zlog(z);
         const zc P = zmul(lz, zlog(zmk(1.0 - z.r, -z.i)));
         add = zadd(add, zscale(sgn, zmk(ZETA2 - P.r, -P.i)));
         sgn = -sgn;
