@@ -648,9 +648,10 @@ __global__ __launch_bounds__(kWfMaxThreads) void k_cascade_wf(GridDev g, const P
             }
             Tp[cur * NJ + tid] = T_j;
             Tprev = T_j;
-        } else if (tid < cbase && nonres && r >= 1 && r + 1 <= T - 1 && !(NUSI_WF_AB & 2)) {
+        } else if (tid < cbase && nonres && r >= 1 && r + 1 <= T - 1 && row0 < r && !(NUSI_WF_AB & 2)) {
             // push column r+1 (T of stage sg-1) into rows < r; rows >= r are consumed (row r through
-            // the published copy) and steps that have not started have T_j = 0, so nothing is masked
+            // the published copy), so a row group wholly at or above r stops pushing (whole waves drop
+            // out as r falls); steps that have not started have T_j = 0, so nothing else is masked
             const double* Th = Tp + prv * NJ + h * JG;
 #pragma unroll
             for (int jj = 0; jj < JG; ++jj) {
