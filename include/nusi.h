@@ -139,8 +139,9 @@ int nusi_plan_stage_ms(nusi_plan *plan, float *ms3);
  * summed ms per stage and the number of calls recorded. */
 int nusi_plan_profile_begin(nusi_plan *plan, int max_calls);
 int nusi_plan_profile_end(nusi_plan *plan, double *sum_ms3, int *ncalls);
-/* Cascade kernel of the plan's later calls (every kernel gives the same
- * fluxes bit for bit; the choice is a performance / A-B knob):
+/* Cascade kernel of the plan's later calls (WAVEFRONT, REG and LDS give the
+ * same fluxes bit for bit, MFMA the same to rounding; the choice is a
+ * performance / A-B knob):
  * AUTO = wavefront when the grid fits it (Nz-1 <= 48, T-1 <= 512), else
  * register-resident (N <= 1280), else LDS.  A kind that does not fit the
  * grid falls back the same way.  NUSI_EPARAM for an unknown kind. */
@@ -148,6 +149,7 @@ int nusi_plan_profile_end(nusi_plan *plan, double *sum_ms3, int *ncalls);
 #define NUSI_CASCADE_WAVEFRONT 1
 #define NUSI_CASCADE_REG 2
 #define NUSI_CASCADE_LDS 3
+#define NUSI_CASCADE_MFMA 4   /* wavefront with the push as fp64 MFMA rank-4 updates (fluxes to rounding) */
 int nusi_plan_set_cascade(nusi_plan *plan, int kind);
 /* per-point NUSI_WARN_* bits of the last call */
 int nusi_plan_warnings(nusi_plan *plan, int *out, int n);

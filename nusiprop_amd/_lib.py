@@ -54,7 +54,7 @@ EXPORTS = [
 ]
 
 # nusi_plan_set_cascade kinds (include/nusi.h)
-CASCADE_AUTO, CASCADE_WAVEFRONT, CASCADE_REG, CASCADE_LDS = 0, 1, 2, 3
+CASCADE_AUTO, CASCADE_WAVEFRONT, CASCADE_REG, CASCADE_LDS, CASCADE_MFMA = 0, 1, 2, 3, 4
 
 _lib = None
 

@@ -730,7 +730,7 @@ int nusi_plan_stage_ms(nusi_plan* pl, float* ms3)
 int nusi_plan_set_cascade(nusi_plan* pl, int kind)
 {
     if (!pl) return fail(NUSI_EPARAM, "plan is NULL");
-    if (kind < NUSI_CASCADE_AUTO || kind > NUSI_CASCADE_LDS) return fail(NUSI_EPARAM, "unknown cascade kind");
+    if (kind < NUSI_CASCADE_AUTO || kind > NUSI_CASCADE_MFMA) return fail(NUSI_EPARAM, "unknown cascade kind");
     pl->cascade_kind = kind;
     return NUSI_OK;
 }

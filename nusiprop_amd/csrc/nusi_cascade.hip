@@ -685,6 +685,203 @@ __global__ __launch_bounds__(kWfMaxThreads) void k_cascade_wf(GridDev g, const P
     }
 }
 
+// ---------------------------------------------------------------------------
+// Wavefront cascade with the push on the fp64 matrix cores (NUSI_CASCADE_MFMA).
+//
+// The push of k_cascade_wf adds one column per stage: ACC[rows, steps] += alpha[rows, r+1] T[r+1, steps],
+// a rank-1 update.  Here the columns are pushed in blocks of four, once every four stages, as
+// ACC[rows, steps] += alpha[rows, 4 columns] . T[4 columns, steps] -- the transfer-matrix x
+// flux-batch GEMM, whose batch is the set of redshift steps in flight -- with
+// v_mfma_f64_16x16x4f64 on 16 x 16 tiles (row tile x step tile).  Push wave w owns rows
+// [64w, 64w+64) = 4 row tiles, each with NJ/16 step tiles in its accumulator registers
+// (C/D layout: step = lane & 15, row = (lane >> 4) + 4 reg).
+//
+// Block q runs at stage 4q and pushes columns T-4q .. T-4q+3 (the T_j of stages 4q-1 .. 4q-4)
+// into the rows below T-1-4q, then publishes the four rows the chain solves at stages
+// 4q+1 .. 4q+4.  At stage sg the published row therefore lacks the columns r+1 .. r+n_u,
+// n_u = sg - 4 ((sg-1) >> 2) in [1, 4]: the chain lane adds them itself from its last four T_j
+// and alpha(r, r+k) (staged in LDS), in descending column order.  The MFMA sums each block of
+// four columns in its own order, so the fluxes agree with k_cascade_wf to rounding (the tests'
+// 1e-11 relative bound vs the oracle), not bit for bit.  Records, solves and the resonant-only
+// chain are k_cascade_wf's.
+// ---------------------------------------------------------------------------
+typedef double nusi_f64x4 __attribute__((ext_vector_type(4)));
+constexpr int kMfRowTiles = 4;   // 16-row tiles per push wave
+
+template <int NJ, bool kPowerLaw>
+__global__ __launch_bounds__(kWfMaxThreads) void k_cascade_wf_mfma(GridDev g, const Point* __restrict__ pts,
+                                                                   TablesDev t, double* __restrict__ flux,
+                                                                   double* __restrict__ flux_fla, int K)
+{
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    constexpr int NST = NJ / 16;             // step tiles
+    const int N = g.N, Nz = g.Nz, T = g.T, nst = Nz - 1;
+    const int tid = threadIdx.x, nthr = blockDim.x;
+    const int KR = K * NJ;
+    double* F = lds;                         // [3][N]
+    double* rec = F + 3 * N;                 // [kWfFields][K][NJ]
+    double* Tp = rec + kWfFields * KR;       // [8][NJ]  T_j by stage (ring of 8)
+    double* AX = Tp + 8 * NJ;                // [2][4][NJ]  published rows of block q (parity q & 1)
+    double* rdE = AX + 8 * NJ;
+    double* pw = rdE + N;
+    double* sGt = pw + (T + 2);
+    double* sAt = sGt + T;
+    double* sdg = sAt + T;                   // [4][T]: alpha(n, n+k), k = 1..4 (0 past the table)
+    double* sEmin = sdg + 4 * T;
+    double* sEmax = sEmin + N;
+    double* sgz = sEmax + N;
+    GridDev gl = g;
+    gl.Emin = sEmin;
+    gl.Emax = sEmax;
+    gl.z = sgz;
+    gl.step_c = sgz + Nz;
+    gl.step_s = sgz + 2 * Nz;
+    gl.sfr = sgz + 3 * Nz;
+    const Point& P = pts[blockIdx.x];
+    const double u0 = P.u[0], u1 = P.u[1], u2 = P.u[2];
+    const double* __restrict__ Gt = t.G + (size_t)P.tslot * T;
+    const double* __restrict__ At = t.At + (size_t)P.tslot * T;
+    const double* __restrict__ Al = t.A + (size_t)P.tslot * g.PT;
+    const bool nonres = P.non_resonant;
+
+    for (int b = tid; b < 3 * N; b += nthr) F[b] = 0.0;
+    for (int j = tid; j < 16 * NJ; j += nthr) Tp[j] = 0.0;   // Tp and AX
+    for (int n = tid; n < T; n += nthr) {
+        sGt[n] = Gt[n];
+        sAt[n] = At[n];
+#pragma unroll
+        for (int k = 1; k <= 4; ++k) sdg[(k - 1) * T + n] = (n + k < T) ? Al[(size_t)(n + k) * (n + k - 1) / 2 + n] : 0.0;
+    }
+    for (int b = tid; b < N; b += nthr) { sEmin[b] = g.Emin[b]; sEmax[b] = g.Emax[b]; }
+    for (int i = tid; i < Nz; i += nthr) {
+        sgz[i] = g.z[i];
+        sgz[Nz + i] = g.step_c[i];
+        sgz[2 * Nz + i] = g.step_s[i];
+        sgz[3 * Nz + i] = g.sfr[i];
+    }
+    cascade_aux_init(g, P, rdE, pw, tid, nthr);
+    const int lane = tid & 63, wave = tid >> 6;
+    const int cbase = nthr - 64, cj_lane = tid - cbase;
+    const bool chain = cj_lane >= 0 && cj_lane < nst;
+    const int ist = Nz - 1 - cj_lane;
+    const int rw0 = wave * 64;               // first row of this push wave
+    nusi_f64x4 acc[kMfRowTiles][NST];
+#pragma unroll
+    for (int a = 0; a < kMfRowTiles; ++a)
+#pragma unroll
+        for (int s = 0; s < NST; ++s) acc[a][s] = nusi_f64x4{0.0, 0.0, 0.0, 0.0};
+    // A operands of the next block: alpha(row, column) with row = tile row + (lane & 15),
+    // column = first block column + (lane >> 4); rows clamped into the column (those rows are consumed)
+    auto load_blk = [&](int q, double (&dst)[kMfRowTiles]) {
+        int c = T - 4 * q + (lane >> 4);
+        c = c < 1 ? 1 : (c > T - 1 ? T - 1 : c);
+        const size_t cb = (size_t)c * (c - 1) / 2;
+#pragma unroll
+        for (int a = 0; a < kMfRowTiles; ++a) {
+            const int row = rw0 + 16 * a + (lane & 15);
+            dst[a] = Al[cb + (row < c - 1 ? row : c - 1)];
+        }
+    };
+    double ablk[kMfRowTiles];
+    if (tid < cbase) load_blk(1, ablk);
+    __syncthreads();
+    const double cj = chain ? gl.step_c[ist] : 0.0, sj = chain ? gl.step_s[ist] : 0.0;
+    double racc = 0.0, px0 = 0.0, px1 = 0.0, px2 = 0.0;
+    double Th[4] = {0.0, 0.0, 0.0, 0.0};     // the lane's T_j of stages sg-1 .. sg-4
+    for (int sg0 = 0; sg0 < T; sg0 += 4)
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+        const int sg = sg0 + d;
+        if (sg >= T) break;
+        const int r = T - 1 - sg;
+        const int ks = sg % K;
+        if (ks == 0) {   // records of stages sg .. sg+K-1, one (stage, step) per thread
+            __syncthreads();
+            const int q = tid / NJ, jj = tid - q * NJ, s2 = sg + q;
+            if (q < K && jj < nst && s2 < T) {
+                const int b = N - 1 - s2 + jj;
+                if (b >= 0 && b < N) cascade_record<kPowerLaw>(gl, P, sGt, sAt, rdE, pw, Nz - 1 - jj, b, rec + q * NJ + jj, KR);
+            }
+            __syncthreads();
+        }
+        if (chain) {
+            const int tid = cj_lane;
+            const int b = N - 1 - sg + tid;
+            double T_j = 0.0;
+            if (b >= 0 && b < N) {
+                const double* R = rec + ks * NJ + tid;
+                double add;
+                if (nonres) {
+                    const int qq = (sg - 1) >> 2;              // block whose publication serves stage sg
+                    const int nu = (d == 0) ? 4 : d;           // columns r+1 .. r+nu not yet pushed
+                    double s = AX[((qq & 1) * 4 + (sg - 1 - 4 * qq)) * NJ + tid];
+#pragma unroll
+                    for (int k = 4; k >= 1; --k)
+                        if (k <= nu) s = fma(sdg[(k - 1) * T + r], Th[k - 1], s);
+                    add = cj * s;
+                } else {
+                    if (b != N - 1) {
+                        const double Sres = u0 * px0 + u1 * px1 + u2 * px2;
+                        const double sd = sdg[r];
+                        racc += Sres * (sj * sd) / (sEmax[b + 1] - sEmin[b + 1]) / R[PR_SDE * KR];
+                    }
+                    add = cj * racc * R[PR_SDE * KR];
+                }
+                double x0 = add, x1 = add, x2 = add;
+                cascade_solve(F[b], F[N + b], F[2 * N + b], add, R[PR_SRC * KR], u0, u1, u2, R[PR_RZ0 * KR],
+                              R[PR_RZ1 * KR], R[PR_RZ2 * KR], (int)R[kPreFields * KR], R[PR_L10 * KR], R[PR_L20 * KR],
+                              R[PR_L21 * KR], R[PR_U01 * KR], R[PR_U02 * KR], R[PR_U12 * KR], R[PR_RU00 * KR],
+                              R[PR_RU11 * KR], R[PR_RU22 * KR], x0, x1, x2);
+                F[b] = x0;
+                F[N + b] = x1;
+                F[2 * N + b] = x2;
+                px0 = x0; px1 = x1; px2 = x2;
+                if (nonres && b > 0) T_j = (u0 * x0 + u1 * x1 + u2 * x2) * R[PR_SDE * KR];
+            }
+            Tp[(sg & 7) * NJ + tid] = T_j;
+            Th[3] = Th[2]; Th[2] = Th[1]; Th[1] = Th[0]; Th[0] = T_j;
+        } else if (d == 0 && tid < cbase && nonres) {
+            // block q = sg / 4: columns c_k = T-4q+k, k = 0..3, carry the T of stage 4q-1-k
+            const int q = sg >> 2;
+            if (q >= 1) {
+#pragma unroll
+                for (int s = 0; s < NST; ++s) {
+                    const double bop = Tp[((sg - 1 - (lane >> 4)) & 7) * NJ + 16 * s + (lane & 15)];
+#pragma unroll
+                    for (int a = 0; a < kMfRowTiles; ++a)
+                        if (rw0 + 16 * a < r)   // tiles wholly at or above r hold consumed rows only
+                            acc[a][s] = __builtin_amdgcn_mfma_f64_16x16x4f64(ablk[a], bop, acc[a][s], 0, 0, 0);
+                }
+                load_blk(q + 1, ablk);
+            }
+            // publish rows r-1 .. r-4 (the rows of stages sg+1 .. sg+4) into AX[q & 1][0..3]
+            const int hi = r - 1;
+#pragma unroll
+            for (int a = 0; a < kMfRowTiles; ++a)
+                if (rw0 + 16 * a <= hi && rw0 + 16 * a + 15 >= hi - 3)   // uniform: tiles holding those rows
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const int row = rw0 + 16 * a + (lane >> 4) + 4 * e;
+                    const int slot = hi - row;
+                    if (slot >= 0 && slot < 4)
+#pragma unroll
+                        for (int s = 0; s < NST; ++s) AX[((q & 1) * 4 + slot) * NJ + 16 * s + (lane & 15)] = acc[a][s][e];
+                }
+        }
+        __syncthreads();
+    }
+    double* fo = flux + (size_t)blockIdx.x * 3 * N;
+    double* fl = flux_fla + (size_t)blockIdx.x * 3 * N;
+    for (int b = tid; b < N; b += nthr) {
+        const double dE = g.Emax[b] - g.Emin[b];
+        const double f0 = F[b] / dE, f1 = F[N + b] / dE, f2 = F[2 * N + b] / dE;
+        fo[b] = f0;
+        fo[N + b] = f1;
+        fo[2 * N + b] = f2;
+        for (int f = 0; f < 3; ++f) fl[f * N + b] = P.U2[3 * f + 0] * f0 + P.U2[3 * f + 1] * f1 + P.U2[3 * f + 2] * f2;
+    }
+}
+
 // launch geometry of the wavefront kernel: one thread per pushed row (T-1), whole waves; K stages
 // of records per batch, as many as the threads cover and kWfMaxLds allows
 constexpr size_t kWfMaxLds = 64 * 1024;
@@ -711,6 +908,40 @@ static bool wf_fits(const GridDev& g)
     const WfGeom w = wf_geom(g, nj);
     if (w.nthr > kWfMaxThreads) return false;
     return w.lds <= kWfMaxLds;
+}
+
+// the MFMA variant: one push wave per 64 rows + the chain wave; T_j ring of 8 stages, 2 x 4 published
+// rows, alpha(n, n+k) for k = 1..4
+static WfGeom mf_geom(const GridDev& g, int NJ)
+{
+    WfGeom w;
+    w.nthr = ((g.T - 1 + 63) / 64) * 64 + 64;
+    w.K = w.nthr / NJ;
+    auto bytes = [&](int K) {
+        return sizeof(double) * (3 * (size_t)g.N + (size_t)kWfFields * K * NJ + 16 * NJ + cascade_aux_doubles(g.N, g.T) +
+                                 6 * (size_t)g.T + 2 * (size_t)g.N + 4 * (size_t)g.Nz);
+    };
+    while (w.K > 1 && bytes(w.K) > kWfMaxLds) --w.K;
+    w.lds = bytes(w.K);
+    return w;
+}
+static bool mf_fits(const GridDev& g)
+{
+    const int nj = wf_nj(g);
+    if (!nj || g.T < 2) return false;
+    const WfGeom w = mf_geom(g, nj);
+    return w.nthr <= kWfMaxThreads && w.K >= 1 && w.lds <= kWfMaxLds;
+}
+
+template <int NJ>
+static void launch_mf(const GridDev& g, const Point* pts, int npts, TablesDev t, double* flux, double* flux_fla,
+                      hipStream_t s, bool power_law)
+{
+    const WfGeom w = mf_geom(g, NJ);
+    if (power_law)
+        hipLaunchKernelGGL((k_cascade_wf_mfma<NJ, true>), dim3(npts), dim3(w.nthr), w.lds, s, g, pts, t, flux, flux_fla, w.K);
+    else
+        hipLaunchKernelGGL((k_cascade_wf_mfma<NJ, false>), dim3(npts), dim3(w.nthr), w.lds, s, g, pts, t, flux, flux_fla, w.K);
 }
 
 template <int NJ>
@@ -749,11 +980,20 @@ hipError_t launch_cascade(const GridDev& g, const Point* pts, int npts, TablesDe
 {
     const int nq = (g.N + 63) / 64;
     if (kind == NUSI_CASCADE_AUTO) {
-        static const char* env = getenv("NUSI_CASCADE");   // A/B switch: wf | reg | lds
+        static const char* env = getenv("NUSI_CASCADE");   // A/B switch: wf | mfma | reg | lds
         kind = !env ? NUSI_CASCADE_AUTO
-                    : (env[0] == 'w' ? NUSI_CASCADE_WAVEFRONT : env[0] == 'r' ? NUSI_CASCADE_REG : NUSI_CASCADE_LDS);
+                    : (env[0] == 'w' ? NUSI_CASCADE_WAVEFRONT : env[0] == 'm' ? NUSI_CASCADE_MFMA
+                       : env[0] == 'r' ? NUSI_CASCADE_REG : NUSI_CASCADE_LDS);
     }
-    if ((kind == NUSI_CASCADE_AUTO || kind == NUSI_CASCADE_WAVEFRONT) && wf_fits(g)) {
+    if (kind == NUSI_CASCADE_MFMA && mf_fits(g)) {
+        switch (wf_nj(g)) {
+        case 16: launch_mf<16>(g, pts, npts, t, flux, flux_fla, s, all_power_law); break;
+        case 32: launch_mf<32>(g, pts, npts, t, flux, flux_fla, s, all_power_law); break;
+        default: launch_mf<48>(g, pts, npts, t, flux, flux_fla, s, all_power_law); break;
+        }
+        return hipGetLastError();
+    }
+    if ((kind == NUSI_CASCADE_AUTO || kind == NUSI_CASCADE_WAVEFRONT || kind == NUSI_CASCADE_MFMA) && wf_fits(g)) {
         switch (wf_nj(g)) {
         case 16: launch_wf<16>(g, pts, npts, t, flux, flux_fla, s, all_power_law); break;
         case 32: launch_wf<32>(g, pts, npts, t, flux, flux_fla, s, all_power_law); break;

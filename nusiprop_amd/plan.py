@@ -82,7 +82,8 @@ class Plan:
                                                 ctypes.c_void_p(stream_ptr) if stream_ptr else None))
 
     def set_cascade(self, kind):
-        """Cascade kernel of later calls: _lib.CASCADE_{AUTO,WAVEFRONT,REG,LDS} (same fluxes bit for bit)."""
+        """Cascade kernel of later calls: _lib.CASCADE_{AUTO,WAVEFRONT,REG,LDS} (same fluxes bit for bit) or
+        CASCADE_MFMA (the wavefront with its push on the fp64 matrix cores; fluxes to rounding)."""
         _lib.check(_lib.load().nusi_plan_set_cascade(self._h, int(kind)))
 
     def profile_begin(self, max_calls):

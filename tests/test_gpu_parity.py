@@ -83,6 +83,21 @@ def test_full_size_flux(nusi, oracle_mod, kw):
     assert cases.rel_err(fla[0], fla_ref) <= FLUX_RTOL
 
 
+@pytest.mark.parametrize("kw", [cases.C2A, cases.C2B], ids=["C2a_N300", "C2b_N300"])
+def test_mfma_cascade_vs_oracle(nusi, oracle_mod, kw):
+    """The MFMA-push cascade (fp64 matrix cores, rank-4 blocks) at BASELINE config 2 vs the oracle."""
+    from nusiprop_amd import _lib
+    o = oracle_mod.Oracle(**cases.oracle_kwargs(kw))
+    f_ref, fla_ref = o.evolve()
+    plan = nusi.Plan(kw["N_bins_E"], kw["lEmin"], kw["lEmax"], kw["zmax"], max_points=3)
+    plan.set_cascade(_lib.CASCADE_MFMA)
+    flux, fla = plan.evolve([kw, kw, kw])
+    for i in range(3):
+        assert cases.rel_err(flux[i], f_ref) <= FLUX_RTOL
+        assert cases.rel_err(fla[i], fla_ref) <= FLUX_RTOL
+        assert np.array_equal(flux[i] == 0, f_ref == 0)
+
+
 def test_data_massless_through_pyprop(nusi):
     """The reference's golden output (output/data_massless.txt, written by test.py)
     reproduced through the drop-in pyprop API on the GPU, to its printed precision."""
@@ -159,20 +174,22 @@ def test_cascade_kernels_agree(nusi, N, nonres):
     """The wavefront cascade (all redshift steps in flight, N_z - 1 <= 48) and the register-
     resident one give the same fluxes bit for bit (same fma()s in the same order); the LDS
     kernel (separate multiply and add, the reference's record arithmetic) agrees to FLUX_RTOL; N = 700 exceeds the wavefront
-    kernel's limits and checks its fallback."""
+    kernel's limits and checks its fallback.  The MFMA-push variant sums each block of four
+    columns in the matrix core's order: FLUX_RTOL, and the same exact zeros."""
     from nusiprop_amd import _lib
     pts = [dict(cases.C2B_100, N_bins_E=N, non_resonant=nonres, majorana=maj, mphi=m, g=gg)
            for maj, m, gg in ((True, 6e5, 0.01), (False, 2e6, 0.1), (True, 1e6, 0.3))]
     plan = nusi.Plan(N, pts[0]["lEmin"], pts[0]["lEmax"], pts[0]["zmax"], max_points=len(pts))
     out = {}
-    for kind in (_lib.CASCADE_WAVEFRONT, _lib.CASCADE_REG, _lib.CASCADE_LDS, _lib.CASCADE_AUTO):
+    for kind in (_lib.CASCADE_WAVEFRONT, _lib.CASCADE_REG, _lib.CASCADE_LDS, _lib.CASCADE_AUTO, _lib.CASCADE_MFMA):
         plan.set_cascade(kind)
         out[kind] = plan.evolve(pts)
     ref = out[_lib.CASCADE_REG]
     assert np.all(np.isfinite(ref[1])) and np.any(ref[1] > 0)
     for kind, (f, fl) in out.items():
-        if kind == _lib.CASCADE_LDS:
+        if kind in (_lib.CASCADE_LDS, _lib.CASCADE_MFMA):   # MFMA: blocks of 4 columns summed in its own order
             assert cases.rel_err(f, ref[0]) <= FLUX_RTOL and cases.rel_err(fl, ref[1]) <= FLUX_RTOL
+            assert np.array_equal(f == 0, ref[0] == 0)
             continue
         assert np.array_equal(f, ref[0]), "kind %d flux differs in %d entries" % (kind, np.sum(f != ref[0]))
         assert np.array_equal(fl, ref[1])
