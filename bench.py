@@ -39,6 +39,9 @@ def parse():
     ap.add_argument("--points", type=int, default=0, help="points per GPU (default: 1024 for c4, 8192 for c5, 1 for c2)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="budget of the oracle CPU baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cascade", default="mfma", choices=["mfma", "wf", "auto"],
+                    help="cascade kernel: mfma = wavefront with the push on the fp64 matrix cores (default, "
+                         "fastest measured), wf = the bit-exact wavefront kernel, auto = the library's choice")
     ap.add_argument("--traffic-json", default="",
                     help="per-launch HBM bytes / fp64 VALU work from rocprofv3 --pmc passes (scripts/pmc_summary.py); "
                          "default for the default workload: the committed profiles/pmc_traffic_latest.json")
@@ -105,6 +108,9 @@ def main():
     p0 = pts[0]
     plan = nu.Plan(p0["N_bins_E"], p0["lEmin"], p0["lEmax"], p0["zmax"], max_points=P, device=local)
     arr = plan.params_array(pts)
+    from nusiprop_amd import _lib
+    plan.set_cascade({"mfma": _lib.CASCADE_MFMA, "wf": _lib.CASCADE_WAVEFRONT, "auto": _lib.CASCADE_AUTO}[args.cascade])
+    casc_kernel = {"mfma": "k_cascade_wf_mfma", "wf": "k_cascade_wf", "auto": "k_cascade_wf"}[args.cascade]
     dev = torch.device("cuda", local)
     flux = torch.empty((P, 3, plan.N), dtype=torch.float64, device=dev)
     fla = torch.empty((P, 3, plan.N), dtype=torch.float64, device=dev)
@@ -176,7 +182,7 @@ def main():
         # once per point, so its algorithmic bytes are cascade_min_bytes_per_point (PMC traffic agrees);
         # SURVEY.md sec. 8d's figure (every step re-reading its alpha window, the reference's access pattern)
         # over the same time is reported beside it as reference_pattern_gbs
-        "roofline_cascade": {"bound": "hbm", "kernel": "k_cascade_wf", "achieved": casc_min / casc_s / 1e9,
+        "roofline_cascade": {"bound": "hbm", "kernel": casc_kernel, "achieved": casc_min / casc_s / 1e9,
                              "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": casc_min / casc_s / 1e9 / HBM_PEAK_GBS,
                              "traffic": traffic, "traffic_source": tsrc, "algorithmic_bytes_per_launch": casc_min,
                              "reference_pattern_bytes_per_launch": casc_bytes, "reference_pattern_gbs": achieved,
@@ -184,6 +190,12 @@ def main():
                              "note": "not HBM-bound: T = N+Nz-2 dependent stages per point (LDS/barrier latency)"},
         "invalid_outputs": bad,
     }
+    if args.cascade == "mfma":   # the push on the fp64 matrix cores: issued MFMA flops over the kernel's time
+        mf = scan.cascade_mfma_flops_per_point(N, Nz) * P
+        out["roofline_cascade"]["mfma"] = {"flops_per_launch": mf, "achieved": mf / casc_s / 1e12,
+                                           "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                                           "frac": mf / casc_s / 1e12 / FP64_PEAK_TFLOPS,
+                                           "note": "v_mfma_f64_16x16x4f64 rank-4 pushes (scan.cascade_mfma_flops_per_point)"}
     fl = pmc.get("k_alpha_fp64_flops_per_step")
     if fl:   # the dominant kernel: executed fp64 VALU flops (PMC counts) per second vs the fp64 vector peak
         ach = fl / alpha_s / 1e12

@@ -782,6 +782,10 @@ __global__ __launch_bounds__(kWfMaxThreads) void k_cascade_wf_mfma(GridDev g, co
             dst[a] = Al[cb + (row < c - 1 ? row : c - 1)];
         }
     };
+#ifndef NUSI_MF_PRIO
+#define NUSI_MF_PRIO 0
+#endif
+    if (NUSI_MF_PRIO && tid >= cbase) __builtin_amdgcn_s_setprio(NUSI_MF_PRIO);   // the chain is the critical path
     double ablk[kMfRowTiles];
     if (tid < cbase) load_blk(1, ablk);
     __syncthreads();

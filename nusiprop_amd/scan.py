@@ -47,6 +47,20 @@ def cascade_min_bytes_per_point(N, Nz):
     return 8 * (T * (T - 1) // 2 + 2 * T + 6 * N)
 
 
+def cascade_mfma_flops_per_point(N, Nz):
+    """fp64 matrix-core flops the MFMA-push cascade (k_cascade_wf_mfma) issues per propagation: block q
+    (stage 4q, q >= 1) runs one v_mfma_f64_16x16x4f64 (2*16*16*4 flops) per 16-row tile starting below
+    r = T-1-4q, per 16-step tile (NJ/16 of them, NJ = Nz-1 rounded up to 16/32/48); 0 if the grid does
+    not fit that kernel."""
+    T, n = N + Nz - 2, Nz - 1
+    NJ = 16 if n <= 16 else 32 if n <= 32 else 48 if n <= 48 else 0
+    waves = (T - 1 + 63) // 64
+    if not NJ or T < 2 or waves * 64 + 64 > 512:
+        return 0
+    tiles = sum(min(4 * waves, -(-(T - 1 - 4 * q) // 16)) for q in range(1, (T - 1) // 4 + 1) if T - 1 - 4 * q > 0)
+    return tiles * (NJ // 16) * 2 * 16 * 16 * 4
+
+
 def alpha_entries_per_point(N, Nz):
     """Stage-A alpha entries per propagation, T(T-1)/2 with T = N + Nz - 2 (each summed over 3 mass states)."""
     T = N + Nz - 2
