@@ -35,7 +35,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--workload", default="c4", choices=["c4", "c5", "c2"])
+    ap.add_argument("--workload", default="c4", choices=["c4", "c5", "c2", "c3"])
     ap.add_argument("--points", type=int, default=0, help="points per GPU (default: 1024 for c4, 8192 for c5, 1 for c2)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="budget of the oracle CPU baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -53,6 +53,13 @@ def rank_points(args, rank, world):
     if args.workload == "c2":
         pts = [dict(scan.BASE, mphi=6e5, g=0.01, si=2.5, norm=6.0)]
         return pts * max(1, args.points or 1), "C2b: single propagation, N_E=300, lE 12->17, power-law source, test.cpp physics"
+    import numpy as np
+    if args.workload == "c3":   # BASELINE config 3: N_E = 1200, lE 10 -> 17, phi-phi on (synthetic tables)
+        P = args.points or 256
+        base = dict(scan.BASE, mphi=1e5, g=0.05, N_bins_E=1200, lEmin=10.0, lEmax=17.0, phiphi=True)
+        pts = [dict(base, g=float(g), si=2.5 + 0.05 * rank) for g in np.logspace(-2.0, -0.5, P)]
+        return pts, ("C3: %d-point g scan per GPU at m_phi=1e5, N_E=1200, lE 10->17, phi-phi on (synthetic tables "
+                     "in the reference layout, tests/phiphi_synth.py), power-law source" % P)
     if args.workload == "c4":
         P = args.points or 1024
         pts = scan.c4_points(si=2.5 + 0.05 * rank)
@@ -107,6 +114,11 @@ def main():
     P = len(pts)
     p0 = pts[0]
     plan = nu.Plan(p0["N_bins_E"], p0["lEmin"], p0["lEmax"], p0["zmax"], max_points=P, device=local)
+    if any(p.get("phiphi") for p in pts):
+        import tempfile
+        from tests.phiphi_synth import make_tables
+        at, atd, a, ad = make_tables(tempfile.mkdtemp(prefix="nusi_phiphi_"), a_dims=(40, 1400, 6), x1_max=1400.0)
+        plan.load_phiphi(at, a, atd, ad)
     arr = plan.params_array(pts)
     from nusiprop_amd import _lib
     plan.set_cascade({"mfma": _lib.CASCADE_MFMA, "wf": _lib.CASCADE_WAVEFRONT, "auto": _lib.CASCADE_AUTO}[args.cascade])
@@ -141,6 +153,8 @@ def main():
     bad = int(torch.isnan(fla).sum().item()) + int((fla < 0).sum().item())
 
     N, Nz = plan.N, plan.Nz
+    if not scan.cascade_mfma_flops_per_point(N, Nz):   # grid beyond the wavefront kernels (Nz-1 > 48): per-step chain
+        casc_kernel, args.cascade = "k_cascade_reg", "reg"
     props = world * P * args.steps
     value = props / dt
     casc_bytes = scan.cascade_bytes_per_point(N, Nz) * P
