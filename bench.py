@@ -36,7 +36,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--workload", default="c4", choices=["c4", "c5", "c2", "c3"])
-    ap.add_argument("--points", type=int, default=0, help="points per GPU (default: 1024 for c4, 8192 for c5, 1 for c2)")
+    ap.add_argument("--points", type=int, default=0, help="points per GPU (default: 1024 for c4 and c3, 8192 for c5, 1 for c2)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="budget of the oracle CPU baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cascade", default="mfma", choices=["mfma", "wf", "auto"],
@@ -55,7 +55,7 @@ def rank_points(args, rank, world):
         return pts * max(1, args.points or 1), "C2b: single propagation, N_E=300, lE 12->17, power-law source, test.cpp physics"
     import numpy as np
     if args.workload == "c3":   # BASELINE config 3: N_E = 1200, lE 10 -> 17, phi-phi on (synthetic tables)
-        P = args.points or 256
+        P = args.points or 1024
         base = dict(scan.BASE, mphi=1e5, g=0.05, N_bins_E=1200, lEmin=10.0, lEmax=17.0, phiphi=True)
         pts = [dict(base, g=float(g), si=2.5 + 0.05 * rank) for g in np.logspace(-2.0, -0.5, P)]
         return pts, ("C3: %d-point g scan per GPU at m_phi=1e5, N_E=1200, lE 10->17, phi-phi on (synthetic tables "
