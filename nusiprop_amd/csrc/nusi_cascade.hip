@@ -920,7 +920,10 @@ static WfGeom mf_geom(const GridDev& g, int NJ)
 {
     WfGeom w;
     w.nthr = ((g.T - 1 + 63) / 64) * 64 + 64;
-    w.K = w.nthr / NJ;
+#ifndef NUSI_MF_KMAX   // cap on the record batch (stages per records phase), A/B
+#define NUSI_MF_KMAX 64
+#endif
+    w.K = std::min(w.nthr / NJ, NUSI_MF_KMAX);
     auto bytes = [&](int K) {
         return sizeof(double) * (3 * (size_t)g.N + (size_t)kWfFields * K * NJ + 16 * NJ + cascade_aux_doubles(g.N, g.T) +
                                  6 * (size_t)g.T + 2 * (size_t)g.N + 4 * (size_t)g.Nz);
