@@ -30,6 +30,7 @@
 
 #define SQ(a) ((a) * (a))
 #define CU(a) ((a) * (a) * (a))
+#define CH(S, bit) ((S)->chan & (bit))
 
 struct ora_state {
     ora_params p;
@@ -43,6 +44,7 @@ struct ora_state {
     ora_spline spl_at, spl_a;
     int err;
     int warn;
+    int chan;                           /* ORA_CH_* mask of the channels summed (test hook; all by default) */
 };
 
 static const double E0 = 1e14;          /* nuSIprop.hpp:549 */
@@ -151,7 +153,7 @@ static double f_Gpp(double z)                                                   
 }
 
 /* the double-scalar analytic absorption piece, nuSIprop.hpp:885 (a = max(s-,4)) */
-static double Gpp_analytic(double a, double b)
+double ora_Gpp_bracket(double a, double b)
 {
     const double ra4 = sqrt(-4 + a), ra = sqrt(a), rb4 = sqrt(-4 + b), rb = sqrt(b);
     const double qa = sqrt((-4 + a) * a), qb = sqrt((-4 + b) * b);
@@ -185,7 +187,7 @@ double ora_Gamma(ora_state *S, double Em, double Ep)       /* nuSIprop.hpp:759-9
             Gs = g4 / (32 * M_PI * m2 * Ga) * (2 * mphi * ora_atandiff(mphi * (sp - 1) / Ga, mphi * (sm - 1) / Ga) + lg);
         Gs *= uj;
         const double wgt = m2 / (2 * mj);
-        tot += wgt * Gs;
+        if (CH(S, ORA_CH_S)) tot += wgt * Gs;
         if (!S->p.non_resonant) continue;
 
         const double L1p = ora_log1p(sp), L1m = ora_log1p(sm);
@@ -193,7 +195,7 @@ double ora_Gamma(ora_state *S, double Em, double Ep)       /* nuSIprop.hpp:759-9
         double Gtu0 = g4 / (16 * M_PI * m2) * (2 * L1p / sp - 2 * L1m / sm + L1p - L1m);
         if (Gtu0 < 0) Gtu0 = g4 / (16 * M_PI * m2) * (sp - sm) / 2. * gl3(sm, sp, f_Gtu_nores);
         Gtu0 *= 2 * uj;
-        tot += wgt * Gtu0;
+        if (CH(S, ORA_CH_T)) tot += wgt * Gtu0;
 
         /* t-u interference */
         double Gint = g4 / (32 * M_PI * m2 * sm * sp) *
@@ -201,7 +203,7 @@ double ora_Gamma(ora_state *S, double Em, double Ep)       /* nuSIprop.hpp:759-9
                        + sm * sp * (ora_dilog1mdiff(sp, sm) + ora_dilogdiff(sp, sm)));
         if (Gint < 0) Gint = g4 / (16 * M_PI * m2) * (sp - sm) / 2. * gl3(sm, sp, f_Gtu_int);
         Gint *= S->p.majorana ? uj : 0.5 * uj;
-        tot += wgt * Gint;
+        if (CH(S, ORA_CH_TU)) tot += wgt * Gint;
 
         /* s-t interference */
         /* z1 = I(1+s)/(2I+gr), z2 = conj(z1)  (nuSIprop.hpp:846-849) */
@@ -226,15 +228,15 @@ double ora_Gamma(ora_state *S, double Em, double Ep)       /* nuSIprop.hpp:759-9
                       - 2 * gr * zarg(zrsub(1, z2m)) * L1m +ora_log1p(4 / SQ(gr)) * (L1m - L1p) + Lgp * L1p - Lgm * L1m
                       + (1 + SQ(gr)) * (Lgm - Lgp) + 2 * ora_dilogdiff(sp, sm));
         Gst *= uj;
-        tot += wgt * Gst;
+        if (CH(S, ORA_CH_ST)) tot += wgt * Gst;
         const double Gsu = S->p.majorana ? Gst : 0;
-        tot += wgt * Gsu;
+        if (CH(S, ORA_CH_SU)) tot += wgt * Gsu;
 
         /* double scalar production */
         double Gpp = 0;
         if (sp > 4 && S->p.phiphi) {
             const double a = (sm > 4) ? sm : 4.0;
-            Gpp = g4 / (128. * M_PI * m2) * Gpp_analytic(a, sp);
+            Gpp = g4 / (128. * M_PI * m2) * ora_Gpp_bracket(a, sp);
             if (Gpp < 0) {
                 const double aa = (sm < 4) ? 4 : sm;
                 Gpp = g4 / (64 * M_PI * m2) * (sp - aa) / 2. * gl3(aa, sp, f_Gpp);
@@ -242,7 +244,7 @@ double ora_Gamma(ora_state *S, double Em, double Ep)       /* nuSIprop.hpp:759-9
             Gpp *= uj;
             if (S->p.majorana) Gpp *= 2;
         }
-        tot += wgt * Gpp;
+        if (CH(S, ORA_CH_PP)) tot += wgt * Gpp;
 
         if (Gs < 0 || Gtu0 < 0 || Gint < 0 || (Gs + Gtu0 + Gst + Gsu) < 0) S->warn |= 1;
     }
@@ -315,7 +317,7 @@ double ora_alphaTilde(ora_state *S, double Em, double Ep)   /* nuSIprop.hpp:924-
             as = g4 / (16 * M_PI * Ga * m4) * (2 * mphi * (1 + tm) * ora_atandiff(mphi * (1 + tm) / Ga, mphi * (1 + tp) / Ga) + lg);
         as *= uk;
         if (!maj) as /= 2.;
-        tot += wgt * as;
+        if (CH(S, ORA_CH_S)) tot += wgt * as;
         if (!S->p.non_resonant) continue;
 
         const double Lmt = ora_log1p(-tm), Lmp = ora_log1p(-tp), Ld = ora_log1p(tm - tp);
@@ -332,7 +334,7 @@ double ora_alphaTilde(ora_state *S, double Em, double Ep)   /* nuSIprop.hpp:924-
             if (at < 0) at = gl33_tri(tp, tm, F_t_dir) * (3. / 2. * g4 / (32 * M_PI * m4));
         }
         at *= uk;
-        tot += wgt * at;
+        if (CH(S, ORA_CH_T)) tot += wgt * at;
 
         /* u channel */
         double au;
@@ -342,7 +344,7 @@ double ora_alphaTilde(ora_state *S, double Em, double Ep)   /* nuSIprop.hpp:924-
             if (au < 0) au = gl33_tri(tp, tm, F_t_dir) * (1. / 2. * g4 / (32 * M_PI * m4));
             au *= uk;
         }
-        tot += wgt * au;
+        if (CH(S, ORA_CH_U)) tot += wgt * au;
 
         /* t-u interference */
         double atu;
@@ -372,7 +374,7 @@ double ora_alphaTilde(ora_state *S, double Em, double Ep)   /* nuSIprop.hpp:924-
         } else
             atu = 0;
         atu *= uk;
-        tot += wgt * atu;
+        if (CH(S, ORA_CH_TU)) tot += wgt * atu;
 
         /* s-t interference */
         /* nuSIprop.hpp:1137-1144 */
@@ -439,9 +441,9 @@ double ora_alphaTilde(ora_state *S, double Em, double Ep)   /* nuSIprop.hpp:924-
                    + 2 * Bp * (M_PI + gr * Lmp) - 2 * Lmt * ora_log(-tp) + 2 * tm * ora_log(tm / tp) + 2 * Lmp * ora_log(-tp)
                    + (Lmp - Lmt) * (ora_log(4 + SQ(gr)) - 2 * ora_log(gr) - Lgp) + (1 + tm + SQ(gr)) * (Lgp - Lgm));
         ast *= uk;
-        tot += wgt * ast;
+        if (CH(S, ORA_CH_ST)) tot += wgt * ast;
         const double asu = maj ? ast : 0;
-        tot += wgt * asu;
+        if (CH(S, ORA_CH_SU)) tot += wgt * asu;
 
         /* double scalar production */
         double app = 0;
@@ -460,7 +462,7 @@ double ora_alphaTilde(ora_state *S, double Em, double Ep)   /* nuSIprop.hpp:924-
             app *= 2;
             if (maj) app *= 2;
         }
-        tot += wgt * app;
+        if (CH(S, ORA_CH_PP)) tot += wgt * app;
 
         const double nrm = SQ(SQ(g / mphi));
         if (as < 0 || at < 0 || au < 0 || atu / nrm < -1e-11 || (ast + at + as) / nrm < -1e-11 || (asu + au + as) / nrm < -1e-11)
@@ -494,7 +496,7 @@ double ora_alpha(ora_state *S, double Em, double Ep, double Emp, double Epp)   /
             as = g4 / (8 * M_PI * Ga * CU(mphi)) * (tm - tp) * ora_atandiff(mphi * (Sp - 1) / Ga, mphi * (Sm - 1) / Ga);
         as *= uk;
         if (!maj) as /= 2.;
-        tot += wgt * as;
+        if (CH(S, ORA_CH_S)) tot += wgt * as;
         if (!S->p.non_resonant) continue;
 
         const double Lmt = ora_log1p(-tm), Lmp = ora_log1p(-tp);
@@ -523,7 +525,7 @@ double ora_alpha(ora_state *S, double Em, double Ep, double Emp, double Epp)   /
             if (at < 0) at = gl33_rect(tp, tm, Sm, Sp, F_t_dir) * (3. / 2. * g4 / (32 * M_PI * m4));
         }
         at *= uk;
-        tot += wgt * at;
+        if (CH(S, ORA_CH_T)) tot += wgt * at;
 
         /* u channel */
         double au;
@@ -534,7 +536,7 @@ double ora_alpha(ora_state *S, double Em, double Ep, double Emp, double Epp)   /
             if (au < 0) au = gl33_rect(tp, tm, Sm, Sp, F_t_dir) * (1. / 2. * g4 / (32 * M_PI * m4));
             au *= uk;
         }
-        tot += wgt * au;
+        if (CH(S, ORA_CH_U)) tot += wgt * au;
 
         /* t-u interference */
         double atu;
@@ -567,7 +569,7 @@ double ora_alpha(ora_state *S, double Em, double Ep, double Emp, double Epp)   /
         } else
             atu = 0.;
         atu *= uk;
-        tot += wgt * atu;
+        if (CH(S, ORA_CH_TU)) tot += wgt * atu;
 
         /* s-t interference: 8 GSL complex dilogs (nuSIprop.hpp:1431-1451) */
         const double z1 = (1 + Sm + tm) / (1 + tm);
@@ -609,9 +611,9 @@ double ora_alpha(ora_state *S, double Em, double Ep, double Emp, double Epp)   /
             ast = g4 / (32 * M_PI * (1 + SQ(gr)) * m4) *
                   ((2 * gr * zarg(zmk(-1 + Sm, gr)) - 2 * gr * zarg(zmk(-1 + Sp, gr)) + 2 * lSm - 2 * lSp + Lsp - Lsm) * (tm - tp + Lmt - Lmp));
         ast *= uk;
-        tot += wgt * ast;
+        if (CH(S, ORA_CH_ST)) tot += wgt * ast;
         const double asu = maj ? ast : 0.;
-        tot += wgt * asu;
+        if (CH(S, ORA_CH_SU)) tot += wgt * asu;
 
         /* double scalar production */
         double app = 0;
@@ -653,7 +655,7 @@ double ora_alpha(ora_state *S, double Em, double Ep, double Emp, double Epp)   /
             app *= 2;
             if (maj) app *= 2;
         }
-        tot += wgt * app;
+        if (CH(S, ORA_CH_PP)) tot += wgt * app;
 
         const double nrm = SQ(SQ(g / mphi));
         if (as < 0 || at / nrm < -1e-11 || au / nrm < -1e-11 || atu / nrm < -1e-11 || (ast + as + at) / nrm < -1e-11)
@@ -720,6 +722,7 @@ ora_state *ora_create(const ora_params *p, int *err)
     S->T = N + S->Nz - 2;
     build_pmns(S);
     S->norm_total = 0;   /* uninitialised in the reference until the first evolve() */
+    S->chan = ORA_CH_ALL;
     if (err) *err = 0;
     return S;
 }
@@ -930,3 +933,7 @@ double ora_check_energy_conservation(ora_state *S, double *flux, double *flux_fl
         for (int k = 0; k < 3; ++k) E_int += (log(S->Emax[i]) - log(S->Emin[i])) * SQ(S->Enu[i]) * flux[k * N + i];
     return (E_int - E_FS) / E_FS;
 }
+
+/* test hooks: sum only the ORA_CH_* channels in Gamma / alphaTilde / alpha (quadrature and
+ * additivity KATs, tests/test_oracle_quadrature.py) */
+void ora_set_channels(ora_state *S, int mask) { S->chan = mask; }

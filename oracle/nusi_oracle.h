@@ -66,6 +66,23 @@ double ora_check_energy_conservation(ora_state *S, double *flux, double *flux_fl
 /* warnings emitted (negative cross sections), bitmask 1=Gamma 2=alphaTilde 4=alpha */
 int ora_warnings(const ora_state *S);
 
+/* Test hooks for the closed-form KATs (tests/test_oracle_quadrature.py).
+ * ora_set_channels: Gamma / alphaTilde / alpha sum only the masked channels
+ * (default ORA_CH_ALL).  Gamma's combined t+u term (nuSIprop.hpp:797) follows
+ * ORA_CH_T; ORA_CH_U selects the separate u terms of alphaTilde / alpha. */
+#define ORA_CH_S 1
+#define ORA_CH_T 2
+#define ORA_CH_U 4
+#define ORA_CH_TU 8
+#define ORA_CH_ST 16
+#define ORA_CH_SU 32
+#define ORA_CH_PP 64
+#define ORA_CH_ALL 127
+void ora_set_channels(ora_state *S, int mask);
+/* the bracket of the analytic double-scalar absorption, nuSIprop.hpp:885 (a = max(s-, 4)):
+ * Gamma_pp = g^4 / (128 pi mphi^2) * ora_Gpp_bracket(a, s+) per mass state */
+double ora_Gpp_bracket(double a, double b);
+
 #ifdef __cplusplus
 }
 #endif

@@ -83,6 +83,9 @@ def lib():
         L.ora_complex_dilog_xy.argtypes = [d, d, dp, dp]
         L.ora_getmL.restype = i
         L.ora_getmL.argtypes = [d, d, d, dp]
+        L.ora_set_channels.argtypes = [p, i]
+        L.ora_Gpp_bracket.restype = d
+        L.ora_Gpp_bracket.argtypes = [d, d]
         _lib = L
     return _lib
 
@@ -103,6 +106,15 @@ def complex_dilog(x, y):
     re, im = ctypes.c_double(), ctypes.c_double()
     lib().ora_complex_dilog_xy(float(x), float(y), ctypes.byref(re), ctypes.byref(im))
     return complex(re.value, im.value)
+
+
+# channel bits of Oracle.set_channels (nusi_oracle.h ORA_CH_*)
+CH_S, CH_T, CH_U, CH_TU, CH_ST, CH_SU, CH_PP, CH_ALL = 1, 2, 4, 8, 16, 32, 64, 127
+
+
+def Gpp_bracket(a, b):
+    """The bracket of the analytic phi-phi absorption (nuSIprop.hpp:885), a = max(s-, 4)."""
+    return lib().ora_Gpp_bracket(float(a), float(b))
 
 
 def getmL(msum, dm21, dmAT):
@@ -192,6 +204,10 @@ class Oracle:
 
     def warnings(self):
         return lib().ora_warnings(self.h)
+
+    def set_channels(self, mask):
+        """Gamma / alphaTilde / alpha sum only the CH_* channels in `mask` (KAT test hook)."""
+        lib().ora_set_channels(self.h, int(mask))
 
     def Gamma(self, Em, Ep):
         return lib().ora_Gamma(self.h, Em, Ep)
