@@ -21,7 +21,9 @@
 // warning on stderr and continue, as in the reference (:909-918, :1215-1231,
 // :1505-1516).  Deliberate difference: the reference's getters read one past
 // the end for j == N_bins_E (:374, :398, :422: the test is j > N_bins_E);
-// here that index returns 0 without reading out of bounds.
+// here that index returns 0 without reading out of bounds.  check_energy_conservation()
+// before any evolve() returns NaN with a message (the reference reads an uninitialised
+// norm_total there, nuSIprop.hpp:341).
 #ifndef NUSIPROP_MI355X_HPP
 #define NUSIPROP_MI355X_HPP
 
@@ -102,7 +104,11 @@ public:
     {
         double r = 0;
         check(nusi_set_params(h_, mphi, g, mntot, si, norm));
-        check(nusi_check_energy_conservation(h_, &r));
+        const int e = nusi_check_energy_conservation(h_, &r);
+        if (e == NUSI_ESTATE)   // before any evolve(): the reference reads norm_total uninitialised; NaN + message
+            std::cerr << nusi_last_error() << std::endl;
+        else
+            check(e);
         fetch();
         return r;
     }

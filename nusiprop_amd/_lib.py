@@ -109,6 +109,10 @@ def load():
     return L
 
 
+def last_error():
+    return load().nusi_last_error().decode(errors="replace")
+
+
 def check(code):
     if code != NUSI_OK:
         raise NusiError(code, load().nusi_last_error().decode(errors="replace"))

@@ -367,10 +367,11 @@ struct nusi_plan {
     std::shared_ptr<SplineStore> spl;
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
     hipEvent_t ev_copy = nullptr;
+    hipEvent_t ev_done = nullptr;      // end of the latest call's kernels (the next call waits for it)
     bool ran = false;
     int last_n = 0;
     std::vector<hipEvent_t> prof_ev;   // 4 per recorded call
-    hipEvent_t* last_ev = nullptr;
+    hipEvent_t last_ev[4] = {nullptr, nullptr, nullptr, nullptr};   // the latest call's stage events (handles)
     int prof_max = 0, prof_n = 0;
     int cascade_kind = NUSI_CASCADE_AUTO;
     double U2[2][9];
@@ -488,6 +489,7 @@ void nusi_plan_destroy(nusi_plan* pl)
     for (auto& e : pl->ev)
         if (e) hipEventDestroy(e);
     if (pl->ev_copy) hipEventDestroy(pl->ev_copy);
+    if (pl->ev_done) hipEventDestroy(pl->ev_done);
     for (auto& e : pl->prof_ev) hipEventDestroy(e);
     hipFree(pl->d_grid);
     hipFree(pl->d_pts);
@@ -528,6 +530,7 @@ int nusi_plan_create(int device, int N_bins_E, double lEmin, double lEmax, doubl
     HIPCHECK(hipStreamCreateWithFlags(&pl->stream, hipStreamNonBlocking));
     for (auto& e : pl->ev) HIPCHECK(hipEventCreate(&e));
     HIPCHECK(hipEventCreateWithFlags(&pl->ev_copy, hipEventDisableTiming));
+    HIPCHECK(hipEventCreateWithFlags(&pl->ev_done, hipEventDisableTiming));
     // grid arrays in one allocation
     const size_t ng = 2 * (size_t)G.N + 2 * (size_t)G.T + 4 * (size_t)G.Nz;
     HIPCHECK(hipMalloc(&pl->d_grid, sizeof(double) * ng));
@@ -608,7 +611,10 @@ int nusi_plan_evolve(nusi_plan* pl, const nusi_params* pts, int n, double* d_flu
     if (n < 1 || n > pl->max_points) return fail(NUSI_EPARAM, "number of points outside [1, max_points]");
     HIPCHECK(hipSetDevice(pl->device));
     hipStream_t s = stream ? (hipStream_t)stream : pl->stream;
-    if (pl->ran) HIPCHECK(hipEventSynchronize(pl->ev_copy));   // h_pts is reused
+    if (pl->ran) {
+        HIPCHECK(hipEventSynchronize(pl->ev_copy));          // the pinned h_pts / h_tpts / h_batches are reused
+        HIPCHECK(hipStreamWaitEvent(s, pl->ev_done, 0));     // so are d_pts, the tables and the warnings: one plan
+    }                                                        // serialises its calls, whatever streams they use
     for (int i = 0; i < n; ++i) {
         const int r = build_point(pl, pts[i], pl->h_pts[i]);
         if (r) return r;
@@ -678,7 +684,8 @@ int nusi_plan_evolve(nusi_plan* pl, const nusi_params* pts, int n, double* d_flu
     for (int i = 0; i < n; ++i) all_pl = all_pl && pl->h_pts[i].source == NUSI_SOURCE_POWER_LAW;
     HIPCHECK(nusi::launch_cascade(pl->gd, pl->d_pts, n, pl->tabs, d_flux, d_fla, s, pl->cascade_kind, all_pl));
     HIPCHECK(hipEventRecord(ev[3], s));
-    pl->last_ev = ev;   // stage_ms / warnings / tables refer to the latest call
+    HIPCHECK(hipEventRecord(pl->ev_done, s));
+    for (int k = 0; k < 4; ++k) pl->last_ev[k] = ev[k];   // stage_ms / warnings / tables refer to the latest call
     pl->ran = true;
     pl->last_n = n;
     pl->last_ntab = ntab;
@@ -797,6 +804,7 @@ struct nusi_handle {
     nusi_plan* plan = nullptr;
     std::vector<double> flux, fla;
     double norm_total = 0.0;   // of the last evolve() (stale in check_energy_conservation)
+    bool evolved = false;      // an evolve() has run (norm_total is set)
     int warn = 0;
     ~nusi_handle() { nusi_plan_destroy(plan); }
 };
@@ -838,6 +846,7 @@ int nusi_copy(const nusi_handle* src, nusi_handle** out)
     (*out)->flux = src->flux;
     (*out)->fla = src->fla;
     (*out)->norm_total = src->norm_total;
+    (*out)->evolved = src->evolved;
     (*out)->warn = src->warn;
     return NUSI_OK;
 }
@@ -869,6 +878,7 @@ int nusi_evolve(nusi_handle* h)
     int r = nusi_plan_evolve_host(h->plan, &h->p, 1, h->flux.data(), h->fla.data());
     if (r) return r;
     h->norm_total = h->plan->h_pts[0].norm_total;
+    h->evolved = true;
     int w = 0;
     r = nusi_plan_warnings(h->plan, &w, 1);
     h->warn = w & (NUSI_WARN_GAMMA | NUSI_WARN_ALPHATILDE | NUSI_WARN_ALPHA);
@@ -878,9 +888,16 @@ int nusi_evolve(nusi_handle* h)
 int nusi_check_energy_conservation(nusi_handle* h, double* out)
 {
     const HostGrid& G = h->plan->grid;
+    // the reference evaluates E_FS with the previous evolve()'s norm_total (nuSIprop.hpp:341-343)
+    const bool unset = !h->evolved;
     const double E_FS = energy_fs(h->p.si, h->norm_total, G.zmax_eff, G.lEmin, G.lEmax);
     int r = nusi_evolve(h);
     if (r) return r;
+    if (unset) {   // deliberate difference: the reference reads an uninitialised member here (inf / garbage)
+        *out = NAN;
+        return fail(NUSI_ESTATE, "check_energy_conservation before any evolve(): norm_total is not set "
+                                 "(the reference reads it uninitialised); evolved now, result NaN");
+    }
     double E_int = 0;
     const int N = G.N;
     for (int i = 0; i < N; ++i)

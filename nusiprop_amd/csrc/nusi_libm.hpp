@@ -232,7 +232,7 @@ NUSI_FN double atan2_i(double y, double x)
     const int ix = hx & 0x7fffffff, iy = hy & 0x7fffffff;
     if (((unsigned)ix | ((lx | (0u - lx)) >> 31)) > 0x7ff00000u || ((unsigned)iy | ((ly | (0u - ly)) >> 31)) > 0x7ff00000u)
         return x + y;                            // NaN
-    if (((hx - 0x3ff00000) | (int)lx) == 0) return atan_i(y);   // x = 1.0
+    if (hx == 0x3ff00000 && lx == 0u) return atan_i(y);   // x = 1.0 (fdlibm subtracts, overflowing int)
     const int m = ((hy >> 31) & 1) | ((hx >> 30) & 2);         // 2*sign(x)+sign(y)
     if ((iy | (int)ly) == 0) {                   // y = 0
         switch (m) {

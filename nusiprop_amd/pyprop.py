@@ -55,8 +55,9 @@ class pyprop:  # noqa: N801  (name of the reference class)
 
     def evolve(self):
         """Evolve the neutrino flux (nuSIprop.pyx:87-90)."""
-        self.evolved = True
+        self.evolved = False          # stays False if the call raises (no stale flux behind an "evolved" flag)
         _lib.check(_lib.load().nusi_evolve(self._h))
+        self.evolved = True
         w = _lib.load().nusi_get_warnings(self._h)
         if w:
             kinds = [n for b, n in ((1, "Gamma"), (2, "alphaTilde"), (4, "alpha")) if w & b]
@@ -108,5 +109,9 @@ class pyprop:  # noqa: N801  (name of the reference class)
         """(E_int - E_FS)/E_FS (nuSIprop.pyx:140-144).  Evolves the C++ object, but -- as in the
         reference -- does not set the Python-side evolved flag."""
         out = ctypes.c_double()
-        _lib.check(_lib.load().nusi_check_energy_conservation(self._h, ctypes.byref(out)))
+        r = _lib.load().nusi_check_energy_conservation(self._h, ctypes.byref(out))
+        if r == _lib.NUSI_ESTATE:   # before any evolve: the reference reads norm_total uninitialised
+            warnings.warn(_lib.last_error())
+            return out.value        # NaN
+        _lib.check(r)
         return out.value

@@ -5,7 +5,7 @@ so a multi-GPU scan is a pure partition: contiguous blocks of the flattened
 grid per rank, no collective on the data path; results are gathered on the
 host at the end.  Points that share (mphi, g, mntot, flags,
 grid) also share their Stage-A tables (nuSIprop.hpp:217-253 do not depend on
-si or norm), so the partition keeps such groups whole when it can.
+si or norm), so the partition keeps such groups whole (shard_aligned).
 """
 import numpy as np
 
@@ -32,6 +32,47 @@ def shard(n_points, world, rank):
     q, r = divmod(n_points, world)
     lo = rank * q + min(rank, r)
     return lo, lo + q + (1 if rank < r else 0)
+
+
+TABLE_KEYS = ("mphi", "g", "mntot", "majorana", "non_resonant", "normal_ordering", "flav", "phiphi",
+              "N_bins_E", "lEmin", "lEmax", "zmax")
+
+
+def table_key(p):
+    """The fields a point's Stage-A tables depend on (nuSIprop.hpp:217-253 read neither si, norm nor the
+    source): points with equal keys share one table on a GPU (nusi_plan_evolve deduplicates them)."""
+    return tuple(p.get(k) for k in TABLE_KEYS)
+
+
+def group_bounds(points):
+    """Start index of every maximal run of consecutive points sharing a table key, plus len(points)."""
+    b = [0]
+    for i in range(1, len(points)):
+        if table_key(points[i]) != table_key(points[i - 1]):
+            b.append(i)
+    if points:
+        b.append(len(points))
+    return b
+
+
+def shard_aligned(points, world, rank):
+    """Contiguous block [lo, hi) of rank `rank` whose ends fall on table-group boundaries (runs of points
+    sharing a table stay on one GPU), each end the group boundary nearest to the even
+    split r * n / world.  Ranks may get empty blocks when there are fewer groups than ranks."""
+    n = len(points)
+    if n == 0:
+        return 0, 0
+    b = group_bounds(points)
+
+    def cut(r):
+        if r <= 0:
+            return 0
+        if r >= world:
+            return n
+        ideal = r * n / world
+        return min(b, key=lambda x: (abs(x - ideal), x))
+
+    return cut(rank), max(cut(rank), cut(rank + 1))
 
 
 def cascade_bytes_per_point(N, Nz):

@@ -211,3 +211,28 @@ def test_alpha_batches_bitexact(nusi, oracle_mod):
         assert np.array_equal(Ad[iu], al[iu]), "point %d: alpha differs in %d entries" % (k, np.sum(Ad[iu] != al[iu]))
         _, f1, fl1, _, _ = _gpu(nusi, [kw])
         assert np.array_equal(f1[0], flux[k]) and np.array_equal(fl1[0], fla[k])
+
+
+def test_plan_serialises_calls_across_streams(nusi):
+    """One plan's device buffers (point records, tables, warnings) are reused by every call: a call on
+    another stream waits for the previous call's kernels (nusi_plan_evolve's done event).  An async
+    evolve on a second torch stream, immediately followed by a host evolve of other points on the plan's
+    own stream, gives each batch its single-call result bit for bit."""
+    import torch
+    a = [dict(cases.C2B_100, mphi=m, g=g) for m, g in ((6e5, 0.01), (2e6, 0.1), (1e7, 0.5))]
+    b = [dict(cases.C2B_100, mphi=m, g=g, majorana=False) for m, g in ((3e5, 0.3), (8e5, 0.05), (4e6, 0.02))]
+    plan = nusi.Plan(100, 12.0, 17.0, 5.0, max_points=3)
+    ref_a = plan.evolve(a)
+    ref_b = plan.evolve(b)
+    dev = torch.device("cuda", 0)
+    s2 = torch.cuda.Stream(device=dev)
+    fa = torch.empty((3, 3, 100), dtype=torch.float64, device=dev)
+    la = torch.empty_like(fa)
+    arr = plan.params_array(a)
+    for _ in range(3):
+        with torch.cuda.stream(s2):
+            plan.evolve_device(arr, fa.data_ptr(), la.data_ptr(), s2.cuda_stream)
+        got_b = plan.evolve(b)                     # plan's own stream, right behind the async call
+        s2.synchronize()
+        assert np.array_equal(fa.cpu().numpy(), ref_a[0]) and np.array_equal(la.cpu().numpy(), ref_a[1])
+        assert np.array_equal(got_b[0], ref_b[0]) and np.array_equal(got_b[1], ref_b[1])

@@ -1,15 +1,26 @@
 """The phi-phi (double-scalar production) path: interp::spline_ND tables
 (interp.hpp:13-638) in the alphaTilde (nuSIprop.hpp:1195-1213) and alpha
 (:1477-1503) channels.  Synthetic tables in the reference layout
-(tests/phiphi_synth.py); GPU tables bit-exact against the oracle, fluxes to
-cases.FLUX_RTOL.  BASELINE config C3 (N_E = 1200, lE 10 -> 17, phi-phi on) is checked
-on a sample of alpha entries (the oracle's full N=1200 table would take
-minutes) plus every Gamma / alphaTilde entry and the full cascade."""
+(nusiprop_amd.phiphi_tables.write_synthetic_tables); GPU tables bit-exact against the
+oracle, fluxes to cases.FLUX_RTOL.  BASELINE config C3 (N_E = 1200, lE 10 -> 17, phi-phi
+on) runs on tables with the reference's exact axes and record counts ({5000, 100},
+{1000, 1000, 100}, xsec/tables_phiphi.py:21-22, 39-41; 1.6 GB on disk, 400 MB on the
+GPU): every Gamma / alphaTilde / alpha entry bit-exact, no lookup outside the nodes,
+and the full cascade."""
+import os
+
 import numpy as np
 import pytest
 
 from tests import cases
-from tests.phiphi_synth import make_tables
+from nusiprop_amd.phiphi_tables import write_synthetic_tables
+
+
+def make_tables(d, at_dims=(120, 10), a_dims=(40, 110, 6), x0_range=(1.0, 2e4)):
+    """Small stand-in tables (x0 log-spaced over x0_range, x1 = 0 .. a_dims[1] - 1, log10 delta in
+    [0.003, 0.06]) for the small-grid tests."""
+    return write_synthetic_tables(d, at_dims=at_dims, a_dims=a_dims, at_x0=x0_range, a_x0=x0_range,
+                                  a_x1=(0.0, a_dims[1] - 1.0), delta=(0.003, 0.06))
 
 PP_SMALL = dict(mphi=1e4, g=0.05, mntot=0.1, si=2.5, norm=1.0, majorana=True, non_resonant=True,
                 normal_ordering=True, N_bins_E=60, lEmin=10.0, lEmax=12.0, zmax=5.0, flav=2, phiphi=True,
@@ -72,29 +83,54 @@ def test_phiphi_out_of_range_is_an_error(tmp_path):
     assert e.value.code == nusi._lib.NUSI_EINTERP
 
 
-@pytest.mark.gpu
-def test_c3_n1200_phiphi(tmp_path, oracle_mod):
-    import nusiprop_amd as nusi
-    tabs = make_tables(str(tmp_path), a_dims=(40, 1400, 6), x1_max=1400.0)
+def test_reference_geometry_tables(tmp_path):
+    """write_synthetic_tables() defaults: the reference's axes and record counts, float32 records with the
+    last index fastest (interp.hpp:249-291) -- the files nusi_plan_load_phiphi reads with dims = NULL."""
+    at, atd, a, ad = write_synthetic_tables(str(tmp_path))
+    assert (atd, ad) == ([5000, 100], [1000, 1000, 100])
+    assert os.path.getsize(at) == 5000 * 100 * 3 * 4 and os.path.getsize(a) == 1000 * 1000 * 100 * 4 * 4
+    r = np.memmap(a, dtype=np.float32, mode="r").reshape(-1, 4)
+    assert r[0, 0] == np.float32(4.0) and r[-1, 0] == np.float32(1e4)
+    assert r[0, 1] == 1 and r[100 * 999, 1] == 1000 and r[99, 2] == np.float32(0.05)
+    assert r[1, 2] > r[0, 2] and r[1, 0] == r[0, 0] and r[100, 1] == 2
+    t = np.fromfile(at, dtype=np.float32).reshape(-1, 3)
+    assert t[0, 0] == np.float32(4.0) and t[-1, 0] == np.float32(1e4) and np.all(t[:, 2] > 0)
+
+
+@pytest.fixture(scope="module")
+def ref_tables(tmp_path_factory):
+    d = str(tmp_path_factory.mktemp("pp_ref"))
+    return write_synthetic_tables(d)
+
+
+def test_c3_oracle_stays_inside_reference_nodes(ref_tables, oracle_mod):
+    """BASELINE C3 (m_phi = 1e5, N_E = 1200, lE 10 -> 17): every phi-phi lookup of the full table build
+    falls inside the reference's table nodes (x1 = (m - n) * 1.0001 <= 1000, log10 delta = 7/1200), so
+    the reference would not exit(1) on this configuration."""
     o = oracle_mod.Oracle(**cases.oracle_kwargs(C3))
-    o.load_phiphi(*tabs)
-    o.prepare()
-    p = _plan(nusi, C3, tabs)
-    flux, fla = p.evolve([C3])
+    o.load_phiphi(*ref_tables)
+    G, aT, al = o.tables()     # raises on an out-of-range lookup
+    assert np.all(np.isfinite(al)) and np.all(np.isfinite(aT))
+
+
+@pytest.mark.gpu
+def test_c3_n1200_phiphi(ref_tables, oracle_mod):
+    import nusiprop_amd as nusi
+    at, atd, a, ad = ref_tables
+    o = oracle_mod.Oracle(**cases.oracle_kwargs(C3))
+    o.load_phiphi(at, atd, a, ad)
+    G, aT, al = o.tables()
+    p = nusi.Plan(C3["N_bins_E"], C3["lEmin"], C3["lEmax"], C3["zmax"], max_points=1)
+    p.load_phiphi(at, a)                       # dims = NULL: the reference's {5000,100}, {1000,1000,100}
+    flux, fla = p.evolve([C3])                 # raises NUSI_EINTERP on an out-of-range lookup
+    assert p.warnings(1)[0] & 8 == 0
     Gg, aTg, Ag = p.tables(0)
     T = o.T
     assert (p.N, p.T) == (1200, 1333)
-    Emin, Emax, _, z = o.grid()
-    N = o.N
-    lo = np.concatenate([Emin, Emin[-1] * (1 + z[1:T - N + 1])])
-    hi = np.concatenate([Emax, Emax[-1] * (1 + z[1:T - N + 1])])
-    for n in range(0, T, 97):   # Gamma / alphaTilde entries (every 97th: each is an O(1) oracle call)
-        assert Gg[n] == o.Gamma(lo[n], hi[n]) and aTg[n] == o.alphaTilde(lo[n], hi[n])
-    rng = np.random.default_rng(20250213)
-    m = rng.integers(1, T, 400)
-    n = (rng.random(400) * m).astype(int)
-    for mm, nn in zip(m, n):
-        assert Ag[mm * (mm - 1) // 2 + nn] == o.alpha(lo[nn], hi[nn], lo[mm], hi[mm]), (nn, mm)
+    assert np.array_equal(Gg, G) and np.array_equal(aTg, aT)
     A = nusi.unpack_alpha(Ag, T)
-    f_ref, fla_ref = o.cascade(Gg, aTg, A)
+    iu = np.triu_indices(T, 1)
+    assert np.array_equal(A[iu], al[iu]), "alpha differs in %d of %d entries" % (np.sum(A[iu] != al[iu]), len(iu[0]))
+    f_ref, fla_ref = o.cascade(G, aT, al)
+    assert cases.rel_err(flux[0], f_ref) <= cases.FLUX_RTOL
     assert cases.rel_err(fla[0], fla_ref) <= cases.FLUX_RTOL

@@ -8,7 +8,7 @@ import numpy as np
 import pytest
 
 from nusiprop_amd import phiphi_tables as pt
-from tests.phiphi_synth import make_tables
+from tests.test_phiphi import make_tables
 
 pytestmark = pytest.mark.skipif(not os.path.exists(pt.TOOL), reason="converter not built (make -C nusiprop_amd/csrc)")
 

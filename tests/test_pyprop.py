@@ -71,10 +71,29 @@ def test_check_energy_conservation_matches_oracle(nusi, oracle_mod):
     o.evolve()
     r, r_ref = ev.check_energy_conservation(), o.check_energy_conservation()
     assert abs(r - r_ref) <= cases.FLUX_RTOL * abs(r_ref)
-    with pytest.warns(UserWarning):      # the Python evolved flag is untouched (as in the reference)
-        ev2 = nusi.pyprop(**_kw(cases.C2B_100))
-        ev2.check_energy_conservation()
+    # before any evolve the reference reads norm_total uninitialised: here a warning and NaN (deliberate
+    # difference); the Python evolved flag is untouched (as in the reference)
+    ev2 = nusi.pyprop(**_kw(cases.C2B_100))
+    with pytest.warns(UserWarning, match="before any evolve"):
+        assert np.isnan(ev2.check_energy_conservation())
+    with pytest.warns(UserWarning, match="not evolved"):
         ev2.get_flux()
+    assert np.isfinite(ev2.check_energy_conservation())   # the call above evolved the C++ object
+
+
+def test_failed_evolve_leaves_not_evolved(nusi, monkeypatch):
+    """An evolve that fails (an error the reference ends with exit(1), e.g. EINTERP for a phi-phi lookup
+    outside the table) raises NusiError and leaves pyprop not evolved: get_flux then warns and returns
+    zeros instead of a stale flux behind an "evolved" flag."""
+    ev = nusi.pyprop(**_kw(cases.C2B_100))
+    ev.evolve()
+    assert ev.get_flux_fla().any()
+    L = nusi._lib.load()
+    monkeypatch.setattr(L, "nusi_evolve", lambda h: nusi._lib.NUSI_EINTERP)
+    with pytest.raises(nusi.NusiError):
+        ev.evolve()
+    with pytest.warns(UserWarning, match="not evolved"):
+        assert not ev.get_flux_fla().any()
 
 
 def test_default_phiphi_needs_tables(nusi, tmp_path, monkeypatch):

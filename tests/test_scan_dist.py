@@ -80,34 +80,91 @@ def _oracle_block(pts):
     return np.array(out_f), np.array(out_l)
 
 
-def _worker(rank, world, port, pts, q):
+def _worker(rank, world, port, pts, q, sub=None):
     import torch.distributed as dist
     from nusiprop_amd import dist as ndist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        lo, hi = ndist.local_block(len(pts))
-        flux, fla = ndist.evolve_sharded(pts, _oracle_block)
+        group = dist.new_group(sub) if sub else None
+        if sub and rank not in sub:
+            q.put((rank, None, None, "outside"))
+            return
+        lo, hi = ndist.local_block(pts, group)
+        flux, fla = ndist.evolve_sharded(pts, _oracle_block, group=group)
         q.put((rank, lo, hi, None if flux is None else (flux, fla)))
     finally:
         dist.destroy_process_group()
 
 
-def test_sharded_evolve_gloo_world2(oracle_mod):
+def _run(world, pts, sub=None):
     import torch.multiprocessing as mp
-    pts = scan.c4_points(n_mphi=3, n_g=2, N_bins_E=24)           # 6 small points
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, pts, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, pts, q, sub)) for r in range(world)]
     for p in procs:
         p.start()
-    res = sorted([q.get(timeout=300) for _ in range(2)])
+    res = sorted([q.get(timeout=300) for _ in range(world)], key=lambda r: r[0])
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
+    return res
+
+
+def test_sharded_evolve_gloo_world2(oracle_mod):
+    pts = scan.c4_points(n_mphi=3, n_g=2, N_bins_E=24)           # 6 small points, 6 tables
+    res = _run(2, pts)
     assert [(r[1], r[2]) for r in res] == [(0, 3), (3, 6)]
     flux, fla = res[0][3]
     assert res[1][3] is None
+    ref_f, ref_l = _oracle_block(pts)
+    assert np.array_equal(flux, ref_f) and np.array_equal(fla, ref_l)
+
+
+def _gamma_groups(sizes, N=20):
+    """Consecutive gamma-batches (points sharing one table) of the given sizes."""
+    pts = []
+    for j, n in enumerate(sizes):
+        pts += [dict(scan.BASE, N_bins_E=N, mphi=6e5 * (1 + j), g=0.02, si=2.0 + 0.1 * s) for s in range(n)]
+    return pts
+
+
+@pytest.mark.parametrize("sizes,world", [((5, 5, 5, 5), 3), ((16,) * 3 + (7,), 3), ((3, 1, 4, 1, 5), 4), ((2,), 3)])
+def test_shard_aligned_keeps_table_groups(sizes, world):
+    pts = _gamma_groups(sizes)
+    blocks = [scan.shard_aligned(pts, world, r) for r in range(world)]
+    assert blocks[0][0] == 0 and blocks[-1][1] == len(pts)
+    assert all(blocks[r][1] == blocks[r + 1][0] for r in range(world - 1))
+    bounds = set(scan.group_bounds(pts))
+    for lo, hi in blocks:
+        assert lo in bounds and hi in bounds           # no table group is split
+    # each cut is the group boundary nearest to the even split
+    for r in range(1, world):
+        ideal = r * len(pts) / world
+        assert abs(blocks[r][0] - ideal) == min(abs(b - ideal) for b in bounds)
+
+
+def test_sharded_evolve_gloo_world3_uneven_groups(oracle_mod):
+    """World 3 over 4 gamma-batches of 5 (20 points, no multiple of 3): groups stay whole, the gather
+    (padded float64 blocks) returns every flux bit-exact in input order."""
+    pts = _gamma_groups((5, 5, 5, 5))
+    res = _run(3, pts)
+    assert [(r[1], r[2]) for r in res] == [(0, 5), (5, 15), (15, 20)]
+    flux, fla = res[0][3]
+    assert res[1][3] is None and res[2][3] is None
+    ref_f, ref_l = _oracle_block(pts)
+    assert np.array_equal(flux, ref_f) and np.array_equal(fla, ref_l)
+
+
+def test_sharded_evolve_subgroup_of_world4(oracle_mod):
+    """A 2-rank subgroup {1, 2} of a 4-rank world: the gather goes to the subgroup's first rank
+    (global rank 1), which gets the full result."""
+    pts = scan.c4_points(n_mphi=2, n_g=2, N_bins_E=20)
+    res = _run(4, pts, sub=[1, 2])
+    assert res[0][3] == "outside" and res[3][3] == "outside"
+    assert [(r[1], r[2]) for r in res[1:3]] == [(0, 2), (2, 4)]
+    flux, fla = res[1][3]
+    assert res[2][3] is None
     ref_f, ref_l = _oracle_block(pts)
     assert np.array_equal(flux, ref_f) and np.array_equal(fla, ref_l)
