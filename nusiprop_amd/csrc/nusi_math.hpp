@@ -129,10 +129,59 @@ NUSI_FN_OUT double li2(double x)
     return add + sgn * li2_useries(-NUSI_PLOG1P(-x));
 }
 
+// Li2(x + iy) close to the real axis, |y| <= kLi2AxisRatio min(|x|, |1 - x|): the Taylor series in iy
+// about the real point x + i0 sign(y) (radius |1 - x|, the distance to the branch point),
+//   Li2(x + iy) = sum_n c_n (iy)^n,  c_n = Li2^(n)(x) / n!,
+//   c_0 = Li2(x) + i pi sign(y) log(x) [x > 1],  c_1 = -log(1 - z) / z (log(1 - z) = log(x - 1) - i pi sign(y)
+//   for x > 1), c_{n+1} = (g^n / (n (n + 1)) - c_n n / (n + 1)) / x with g = 1 / (1 - x)
+// (from z Li2'(z) = -log(1 - z)), summed by Horner in iy.  Truncated after kLi2AxisTerms: the remainder is
+// below (kLi2AxisRatio)^7 ~ 1e-18 relative.  One real Li2, one log and two divisions instead of the general
+// path's three complex logarithms; this is the regime of the alpha table's member leaves (arguments with
+// Im ~ Gamma_phi / m_phi).  Same algorithm as the oracle (ora_specfun.c ora_complex_dilog_xy).
+constexpr int kLi2AxisTerms = 6;
+constexpr double kLi2AxisRatio = 2.5e-3;
+NUSI_FN cd cli2_axis(double x, double y)
+{
+    constexpr double kA[kLi2AxisTerms] = {0.0, 1.0 / 2, 1.0 / 6, 1.0 / 12, 1.0 / 20, 1.0 / 30};   // 1 / (n (n + 1))
+    constexpr double kB[kLi2AxisTerms] = {0.0, 1.0 / 2, 2.0 / 3, 3.0 / 4, 4.0 / 5, 5.0 / 6};     // n / (n + 1)
+    double ar[kLi2AxisTerms + 1], ai[kLi2AxisTerms + 1];
+    const double r = 1.0 / x, g = 1.0 / (1.0 - x);
+    ar[0] = li2(x);
+    if (x < 1.0) {
+        ai[0] = 0.0;
+        ar[1] = -NUSI_PLOG1P(-x) * r;
+        ai[1] = 0.0;
+    } else {
+        const double sp = copysign(kPi, y);
+        ai[0] = sp * NUSI_PLOG(x);
+        ar[1] = -NUSI_PLOG(x - 1.0) * r;
+        ai[1] = sp * r;
+    }
+    double gn = g;
+#pragma unroll
+    for (int n = 1; n < kLi2AxisTerms; ++n) {
+        ar[n + 1] = (gn * kA[n] - kB[n] * ar[n]) * r;
+        ai[n + 1] = -(kB[n] * ai[n]) * r;
+        gn = gn * g;
+    }
+    double sr = ar[kLi2AxisTerms], si = ai[kLi2AxisTerms];
+#pragma unroll
+    for (int n = kLi2AxisTerms - 1; n >= 0; --n) {
+        const double tr = ar[n] - si * y, ti = ai[n] + sr * y;
+        sr = tr;
+        si = ti;
+    }
+    return cd{sr, si};
+}
+
 // principal-branch Li2(x+iy); y == 0 follows gsl_sf_complex_dilog_xy_e
 NUSI_FN_OUT cd cli2(double x, double y)
 {
     if (y == 0.0) return cd{li2(x), (x >= 1.0) ? -kPi * NUSI_PLOG(x) : 0.0};
+    {
+        const double ax = fabs(x), a1 = fabs(1.0 - x);
+        if (fabs(y) <= kLi2AxisRatio * (ax < a1 ? ax : a1)) return cli2_axis(x, y);
+    }
 #ifdef NUSI_AB_STUB_CLI2   // timing experiments only
     return C(0.5 * x, 0.5 * y);
 #endif

@@ -57,6 +57,46 @@ double ora_dilog(double x)
 
 double ora_li2(double x) { return ora_dilog(x); }
 
+/* Li2(x + iy) for |y| <= AXIS_RATIO min(|x|, |1 - x|): Taylor series in iy about x + i0 sign(y)
+ * (radius |1 - x|): c_0 = Li2(x) + i pi sign(y) log x [x > 1], c_1 = -log(1 - z)/z, c_{n+1} =
+ * (g^n/(n(n+1)) - c_n n/(n+1))/x with g = 1/(1 - x) (from z Li2'(z) = -log(1 - z)), Horner in iy,
+ * AXIS_TERMS + 1 terms (remainder < AXIS_RATIO^7 ~ 1e-18 relative).  The GPU runs the same sequence
+ * (nusi_math.hpp cli2_axis); pinned by the mpmath KATs (tests/test_specfun.py). */
+#define AXIS_TERMS 6
+static const double AXIS_RATIO = 2.5e-3;
+static void cdilog_axis(double x, double y, double *re, double *im)
+{
+    static const double kA[AXIS_TERMS] = {0.0, 1.0 / 2, 1.0 / 6, 1.0 / 12, 1.0 / 20, 1.0 / 30};
+    static const double kB[AXIS_TERMS] = {0.0, 1.0 / 2, 2.0 / 3, 3.0 / 4, 4.0 / 5, 5.0 / 6};
+    double ar[AXIS_TERMS + 1], ai[AXIS_TERMS + 1];
+    const double r = 1.0 / x, g = 1.0 / (1.0 - x);
+    ar[0] = ora_dilog(x);
+    if (x < 1.0) {
+        ai[0] = 0.0;
+        ar[1] = -ora_log1p(-x) * r;
+        ai[1] = 0.0;
+    } else {
+        const double sp = copysign(PI_D, y);
+        ai[0] = sp * ora_log(x);
+        ar[1] = -ora_log(x - 1.0) * r;
+        ai[1] = sp * r;
+    }
+    double gn = g;
+    for (int n = 1; n < AXIS_TERMS; ++n) {
+        ar[n + 1] = (gn * kA[n] - kB[n] * ar[n]) * r;
+        ai[n + 1] = -(kB[n] * ai[n]) * r;
+        gn = gn * g;
+    }
+    double sr = ar[AXIS_TERMS], si = ai[AXIS_TERMS];
+    for (int n = AXIS_TERMS - 1; n >= 0; --n) {
+        const double tr = ar[n] - si * y, ti = ai[n] + sr * y;
+        sr = tr;
+        si = ti;
+    }
+    *re = sr;
+    *im = si;
+}
+
 void ora_complex_dilog_xy(double x, double y, double *re, double *im)
 {
     if (y == 0.0) {
@@ -64,6 +104,13 @@ void ora_complex_dilog_xy(double x, double y, double *re, double *im)
         *re = ora_dilog(x);
         *im = (x >= 1.0) ? -PI_D * ora_log(x) : 0.0;
         return;
+    }
+    {
+        const double ax = fabs(x), a1 = fabs(1.0 - x);
+        if (fabs(y) <= AXIS_RATIO * (ax < a1 ? ax : a1)) {
+            cdilog_axis(x, y, re, im);
+            return;
+        }
     }
     zc z = zmk(x, y), add = zmk(0.0, 0.0), lz = zmk(0.0, 0.0);
     double sgn = 1.0;

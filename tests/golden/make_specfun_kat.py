@@ -56,6 +56,23 @@ def main():
         out["atan2"].append([p, q, f(mp.atan2(p, q))])
         h = random.uniform(-0.999999, 0.999999)
         out["atanh"].append([h, f(mp.atanh(h))])
+    # near the real axis (the Taylor path of the complex dilog, |y| <= 2.5e-3 min(|x|, |1 - x|)), both sides
+    # of the cut x > 1, next to the branch point and next to 0; drawn after every set above
+    out["li2_complex_axis"] = []
+    for _ in range(400):
+        r = random.random()
+        if r < 0.4:
+            x = random.choice([-1, 1]) * 10 ** random.uniform(-5, 4)
+        elif r < 0.7:
+            x = 1 + random.choice([-1, 1]) * 10 ** random.uniform(-7, 0)
+        else:
+            x = 1 + 10 ** random.uniform(-7, 3)
+        d = min(abs(x), abs(1 - x))
+        y = random.choice([-1, 1]) * d * 2.5e-3 * random.random()
+        if y == 0:
+            continue
+        v = mp.polylog(2, mp.mpc(x, y))
+        out["li2_complex_axis"].append([x, y, f(mp.re(v)), f(mp.im(v))])
     with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "specfun_kat.json"), "w") as fh:
         json.dump(out, fh)
 

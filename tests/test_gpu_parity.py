@@ -213,26 +213,48 @@ def test_alpha_batches_bitexact(nusi, oracle_mod):
         assert np.array_equal(f1[0], flux[k]) and np.array_equal(fl1[0], fla[k])
 
 
+def _hip():
+    """The HIP runtime libnusi.so itself links (ctypes), for streams and device buffers in tests that must not
+    initialise torch's separately bundled runtime after libnusi's."""
+    import ctypes
+    H = ctypes.CDLL("/opt/rocm/lib/libamdhip64.so.7")
+    vp = ctypes.c_void_p
+    H.hipStreamCreate.argtypes = [ctypes.POINTER(vp)]
+    H.hipStreamDestroy.argtypes = [vp]
+    H.hipStreamSynchronize.argtypes = [vp]
+    H.hipMalloc.argtypes = [ctypes.POINTER(vp), ctypes.c_size_t]
+    H.hipFree.argtypes = [vp]
+    H.hipMemcpy.argtypes = [vp, vp, ctypes.c_size_t, ctypes.c_int]
+    return H
+
+
 def test_plan_serialises_calls_across_streams(nusi):
     """One plan's device buffers (point records, tables, warnings) are reused by every call: a call on
     another stream waits for the previous call's kernels (nusi_plan_evolve's done event).  An async
-    evolve on a second torch stream, immediately followed by a host evolve of other points on the plan's
-    own stream, gives each batch its single-call result bit for bit."""
-    import torch
+    evolve on a second stream, immediately followed by a host evolve of other points on the plan's own
+    stream, gives each batch its single-call result bit for bit."""
+    import ctypes
+    H = _hip()
     a = [dict(cases.C2B_100, mphi=m, g=g) for m, g in ((6e5, 0.01), (2e6, 0.1), (1e7, 0.5))]
     b = [dict(cases.C2B_100, mphi=m, g=g, majorana=False) for m, g in ((3e5, 0.3), (8e5, 0.05), (4e6, 0.02))]
     plan = nusi.Plan(100, 12.0, 17.0, 5.0, max_points=3)
     ref_a = plan.evolve(a)
     ref_b = plan.evolve(b)
-    dev = torch.device("cuda", 0)
-    s2 = torch.cuda.Stream(device=dev)
-    fa = torch.empty((3, 3, 100), dtype=torch.float64, device=dev)
-    la = torch.empty_like(fa)
+    nbytes = 3 * 3 * 100 * 8
+    s2, fa, la = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p()
+    assert H.hipStreamCreate(ctypes.byref(s2)) == 0
+    assert H.hipMalloc(ctypes.byref(fa), nbytes) == 0 and H.hipMalloc(ctypes.byref(la), nbytes) == 0
     arr = plan.params_array(a)
-    for _ in range(3):
-        with torch.cuda.stream(s2):
-            plan.evolve_device(arr, fa.data_ptr(), la.data_ptr(), s2.cuda_stream)
-        got_b = plan.evolve(b)                     # plan's own stream, right behind the async call
-        s2.synchronize()
-        assert np.array_equal(fa.cpu().numpy(), ref_a[0]) and np.array_equal(la.cpu().numpy(), ref_a[1])
-        assert np.array_equal(got_b[0], ref_b[0]) and np.array_equal(got_b[1], ref_b[1])
+    try:
+        for _ in range(3):
+            plan.evolve_device(arr, fa.value, la.value, s2.value)
+            got_b = plan.evolve(b)                     # plan's own stream, right behind the async call
+            assert H.hipStreamSynchronize(s2) == 0
+            ha, hl = np.zeros((3, 3, 100)), np.zeros((3, 3, 100))
+            assert H.hipMemcpy(ha.ctypes.data, fa, nbytes, 2) == 0 and H.hipMemcpy(hl.ctypes.data, la, nbytes, 2) == 0
+            assert np.array_equal(ha, ref_a[0]) and np.array_equal(hl, ref_a[1])
+            assert np.array_equal(got_b[0], ref_b[0]) and np.array_equal(got_b[1], ref_b[1])
+    finally:
+        H.hipFree(fa)
+        H.hipFree(la)
+        H.hipStreamDestroy(s2)

@@ -83,6 +83,16 @@ def test_complex_dilog_vs_mpmath(oracle_mod):
         assert abs(z - complex(re, im)) <= 1e-15 * max(1.0, abs(complex(re, im))), (x, y, z, re, im)
 
 
+def test_complex_dilog_near_axis_vs_mpmath(oracle_mod):
+    """The Taylor path in iy about the real axis (|y| <= 2.5e-3 min(|x|, |1 - x|)), both sides of the
+    cut x > 1, next to the branch point 1 and next to 0: modulus-relative error <= 1e-15."""
+    assert len(KAT["li2_complex_axis"]) >= 390
+    for x, y, re, im in KAT["li2_complex_axis"]:
+        z = oracle_mod.complex_dilog(x, y)
+        ref = complex(re, im)
+        assert abs(z - ref) <= 1e-15 * abs(ref), (x, y, z, re, im)
+
+
 def test_li3_vs_mpmath(oracle_mod):
     for x, y in KAT["li3"]:
         v = oracle_mod.li3(x)
@@ -93,7 +103,7 @@ def test_device_specfun_bit_identical_to_oracle(oracle_mod, hlib):
     re, im = D(), D()
     for x, _ in KAT["li2_real"]:
         assert hlib.hc_li2(x) == oracle_mod.dilog(x), x
-    for x, y, _, _ in KAT["li2_complex"]:
+    for x, y, _, _ in KAT["li2_complex"] + KAT["li2_complex_axis"]:
         hlib.hc_cli2(x, y, ctypes.byref(re), ctypes.byref(im))
         z = oracle_mod.complex_dilog(x, y)
         assert (re.value, im.value) == (z.real, z.imag), (x, y)
