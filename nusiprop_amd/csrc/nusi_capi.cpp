@@ -357,7 +357,8 @@ struct nusi_plan {
     nusi::Point* h_tpts = nullptr;  // pinned
     int* d_batches = nullptr;       // alpha-table batches (nusi::launch_alpha): first table | count << 24
     int* h_batches = nullptr;       // pinned
-    int alpha_batch = 3;            // tables per batch: 3 measured best (4 drops to 2 workgroups/CU on LDS); NUSI_ALPHA_BATCH overrides
+    int alpha_batch = 0;            // max tables per batch; 0 = auto (alpha_batch_cap); NUSI_ALPHA_BATCH overrides
+    bool alpha_tile_kernel = false; // NUSI_ALPHA_KERNEL=tile: k_alpha_tile<G> batches of <= 4 (A/B)
     std::vector<int> slot_of;       // table slot of each point of the last call
     int last_ntab = 0;
     int* d_warn = nullptr;
@@ -572,7 +573,8 @@ int nusi_plan_create(int device, int N_bins_E, double lEmin, double lEmax, doubl
     HIPCHECK(hipHostMalloc((void**)&pl->h_tpts, sizeof(nusi::Point) * max_points, hipHostMallocDefault));
     HIPCHECK(hipMalloc(&pl->d_batches, sizeof(int) * max_points));
     HIPCHECK(hipHostMalloc((void**)&pl->h_batches, sizeof(int) * max_points, hipHostMallocDefault));
-    if (const char* e = getenv("NUSI_ALPHA_BATCH")) pl->alpha_batch = std::max(1, std::min(4, atoi(e)));
+    if (const char* e = getenv("NUSI_ALPHA_KERNEL")) pl->alpha_tile_kernel = e[0] == 't';
+    if (const char* e = getenv("NUSI_ALPHA_BATCH")) pl->alpha_batch = std::max(1, std::min(pl->alpha_tile_kernel ? 4 : 255, atoi(e)));
     HIPCHECK(hipMalloc(&pl->d_warn, sizeof(int) * max_points));
     HIPCHECK(hipMalloc(&pl->tabs.G, sizeof(double) * (size_t)G.T * max_points));
     HIPCHECK(hipMalloc(&pl->tabs.At, sizeof(double) * (size_t)G.T * max_points));
@@ -641,7 +643,9 @@ int nusi_plan_evolve(nusi_plan* pl, const nusi_params* pts, int n, double* d_flu
     for (int j = 0; j < ntab; ++j) order[j] = j;
     auto bkey = [&](int j) {
         const nusi::Point& P = pl->h_tpts[j];
-        return std::make_tuple(P.mphi, P.mn[0], P.mn[1], P.mn[2], P.majorana, P.non_resonant, P.phiphi);
+        // phi-phi first: the tables with the channel come last (their batches run on their own launch)
+        return std::make_tuple(P.phiphi && P.non_resonant, P.mphi, P.mn[0], P.mn[1], P.mn[2], P.majorana, P.non_resonant,
+                               P.phiphi);
     };
     std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return bkey(a) < bkey(b); });
     {
@@ -653,12 +657,33 @@ int nusi_plan_evolve(nusi_plan* pl, const nusi_params* pts, int n, double* d_flu
     }
     for (int i = 0; i < n; ++i) pl->h_pts[i].tslot = pl->slot_of[i] = perm[pl->slot_of[i]];
     for (int j = 0; j < ntab; ++j) pl->h_tpts[j].tslot = j;
+    // batch cap: the tile kernel's LDS holds <= 4 (3 measured best); the big-batch kernel shares the leaves of
+    // any number, but one workgroup runs a batch's points one after the other, so the cap keeps ~2 rounds of
+    // workgroups per CU slot (256 CUs x 3) in the grid: ntab x class-0 tiles / cap >= 1536
+    int cap = pl->alpha_batch;
+    if (cap <= 0) {
+        if (pl->alpha_tile_kernel) cap = 3;
+        else {
+            const long long work = (long long)ntab * std::max(1, pl->atiles.ncls[0]);
+            cap = (int)std::max(1LL, std::min(64LL, (work + 1535) / 1536));
+        }
+    }
     int nbatch = 0;
     for (int j = 0; j < ntab;) {
-        int c = 1;
-        while (c < pl->alpha_batch && j + c < ntab && bkey(j + c) == bkey(j)) ++c;
-        pl->h_batches[nbatch++] = j | (c << 24);
-        j += c;
+        int run = 1;   // the group of tables sharing bkey, split into near-equal batches of <= cap
+        while (j + run < ntab && bkey(j + run) == bkey(j)) ++run;
+        const int nb = (run + cap - 1) / cap;
+        for (int b = 0; b < nb; ++b) {
+            const int lo = j + (int)((long long)run * b / nb), hi = j + (int)((long long)run * (b + 1) / nb);
+            pl->h_batches[nbatch++] = lo | ((hi - lo) << 24);
+        }
+        j += run;
+    }
+    int nb_plain = 0;   // batches without the phi-phi channel (sorted first by bkey)
+    while (nb_plain < nbatch) {
+        const nusi::Point& F = pl->h_tpts[pl->h_batches[nb_plain] & 0xffffff];
+        if (F.phiphi && F.non_resonant) break;
+        ++nb_plain;
     }
     const size_t N3 = (size_t)3 * pl->grid.N;
     if (!d_flux || !d_fla) {
@@ -678,7 +703,8 @@ int nusi_plan_evolve(nusi_plan* pl, const nusi_params* pts, int n, double* d_flu
     HIPCHECK(nusi::launch_gamma_alphat(pl->gd, pl->d_tpts, ntab, spl, pl->tabs, pl->d_warn, s));
     HIPCHECK(hipEventRecord(ev[1], s));
     HIPCHECK(nusi::launch_alpha(pl->gd, pl->d_tpts, ntab, spl, pl->atiles, pl->tabs, pl->d_warn, s, pl->d_batches,
-                                nbatch, pl->alpha_batch));
+                                nbatch, pl->alpha_tile_kernel ? std::min(cap, 4) : cap, pl->alpha_tile_kernel,
+                                nb_plain));
     HIPCHECK(hipEventRecord(ev[2], s));
     bool all_pl = true;
     for (int i = 0; i < n; ++i) all_pl = all_pl && pl->h_pts[i].source == NUSI_SOURCE_POWER_LAW;

@@ -49,9 +49,12 @@ void alpha_tiles_destroy(AlphaTilesDev* t);
 hipError_t launch_gamma_alphat(const GridDev& g, const Point* pts, int npts, const SplineSet& spl, TablesDev t,
                                int* warn, hipStream_t s);
 // batches: device [nbatches] of first table | count << 24 (count <= gmax), tables of a batch sharing
-// m_phi, the masses and the channel flags (nullptr: every table alone)
+// m_phi, the masses and the channel flags (nullptr: every table alone).  Core tiles run on the big-batch
+// kernel k_alpha_batch (any count < 256; the first nb_plain batches without the phi-phi channel, the rest
+// with it), or with tile_kernel on k_alpha_tile<G> (count <= 4; A/B)
 hipError_t launch_alpha(const GridDev& g, const Point* pts, int npts, const SplineSet& spl, const AlphaTilesDev& tiles,
-                        TablesDev t, int* warn, hipStream_t s, const int* batches, int nbatches, int gmax);
+                        TablesDev t, int* warn, hipStream_t s, const int* batches, int nbatches, int gmax,
+                        bool tile_kernel, int nb_plain);
 // kind: NUSI_CASCADE_* (include/nusi.h); NUSI_CASCADE_AUTO also honours $NUSI_CASCADE = wf|reg|lds
 // all_power_law: every point uses the power-law source (selects the call-free wavefront kernel)
 hipError_t launch_cascade(const GridDev& g, const Point* pts, int npts, TablesDev t, double* flux, double* flux_fla,

@@ -222,6 +222,158 @@ __global__ __launch_bounds__(kTileThreads) NUSI_TILE_ATTR void k_alpha_tile(Grid
                 needed ? ((G > 1) ? tsum[q * kTileThreads + tid] : tot1) : 0.0;
 }
 
+// ---------------------------------------------------------------------------
+// k_alpha_batch: one workgroup per (class-0 tile, batch of up to 255 tables sharing m_phi, the masses
+// and the channel flags).  The leaves of (S', t) alone and the brackets built from them alone (t,
+// t-u, phi-phi) are formed ONCE per batch; then the batch's points run one after the other through
+// their member leaves (those that read gr = Gamma_phi / m_phi: one complex dilogarithm and one arg per
+// corner, a few per edge) and the per-point combine.  So the batch size no longer costs LDS: the shared
+// work per table falls as 1/batch (C4: 32 couplings per m_phi, C5: 64) where k_alpha_tile<G> stopped at
+// G = 3.  Every entry is the same alpha_k expression on the same leaves as k_alpha_tile: bit-identical.
+//
+// LDS (doubles; cs, ct <= kAlphaTile + 1, cc = cs ct):
+//   per [3 k][3][cc]   L, Drr, Dri of every mass state (kept through the batch loop)
+//   tmp [4][cc]        LL, TU1, TU2, G of the current k (bracket phase); reused as mem [3][cc], the
+//                      member corner leaves of the current (point, k)
+//   mix [kAlphaTile (cs + ct)]  xlog / ylog of the current k (bracket phase)
+//   edg alpha_tile_edge_doubles(cs, ct, 1): shared edge / m-bin leaves of every k + one point's member ones
+// ---------------------------------------------------------------------------
+__host__ __device__ constexpr int alpha_batch_lds_doubles(int cs, int ct)
+{
+    return 3 * 3 * cs * ct + 4 * cs * ct + kAlphaTile * (cs + ct) + alpha_tile_edge_doubles(cs, ct, 1);
+}
+
+#ifndef NUSI_AB_BATCH   // timing experiments only: 1 skip the member corner leaves, 2 skip the combine, 4 skip brackets
+#define NUSI_AB_BATCH 0
+#endif
+#ifndef NUSI_BATCH_WAVES
+#define NUSI_BATCH_WAVES 4   // 4: 8.32-8.45 ms vs 3: 8.61-8.81 (C4 alpha stage; 43 VGPRs spill, profiles/r2/ab)
+#endif
+template <bool kPP>   // the batches' tables have the phi-phi channel (their shared terms are kept per k)
+__global__ __launch_bounds__(kTileThreads) __attribute__((amdgpu_waves_per_eu(NUSI_BATCH_WAVES, NUSI_BATCH_WAVES)))
+void k_alpha_batch(GridDev g, const Point* __restrict__ pts, SplineSet spl, const int* __restrict__ tiles,
+                   const int* __restrict__ batches, double* __restrict__ A, int* __restrict__ warn)
+{
+    extern __shared__ __attribute__((aligned(16))) double sm[];
+    __shared__ double tE[2 * kAlphaTile], sE[2 * kAlphaTile];
+    __shared__ int tl[kAlphaTile], th[kAlphaTile], sl[kAlphaTile], sh[kAlphaTile];
+    __shared__ int cnt[2];
+    __shared__ double elo[2][kAlphaTile], ehi[2][kAlphaTile];
+    const int tid = threadIdx.x, T = g.T;
+    const int bw = batches[blockIdx.y];
+    const int p0 = bw & 0xffffff, nb = (int)((unsigned)bw >> 24);   // tables p0 .. p0 + nb - 1
+    const unsigned tu = (unsigned)tiles[blockIdx.x];                 // tile word, as in k_alpha_tile
+    const int half = (tu >> 28) & 3, nhalf = (tu >> 30) & 3;
+    const int n0 = (tu & 0x3fff) * kAlphaTile + (nhalf == 2 ? 8 : 0);
+    const int m0 = ((tu >> 14) & 0x3fff) * kAlphaTile + (half == 2 ? 8 : 0);
+    const int mcnt = half == 0 ? kAlphaTile : (half == 1 ? 8 : kAlphaTile - 8);
+    const int ncnt = nhalf == 0 ? kAlphaTile : (nhalf == 1 ? 8 : kAlphaTile - 8);
+    const int Tm = (m0 + mcnt < T) ? m0 + mcnt : T;
+    const int Tn = (n0 + ncnt < T) ? n0 + ncnt : T;
+    const Point& P = pts[p0];
+    if (tid < 2 * kAlphaTile) {
+        const int side = tid / kAlphaTile, j = tid - side * kAlphaTile, b = (side ? m0 : n0) + j;
+        if (b < (side ? Tm : Tn)) { elo[side][j] = g.lo[b]; ehi[side][j] = g.hi[b]; }
+    }
+    __syncthreads();
+    if (tid == 0) cnt[0] = alpha_edge_list(elo[0], ehi[0], 0, Tn - n0, tE, tl, th);
+    if (tid == 64) cnt[1] = alpha_edge_list(elo[1], ehi[1], 0, Tm - m0, sE, sl, sh);
+    __syncthreads();
+    const int ct = cnt[0], cs = cnt[1], cc = cs * ct;
+    const int ln = tid % kAlphaTile, lm = tid / kAlphaTile;
+    const int n = n0 + ln, m = m0 + lm;
+    const bool valid = tid < kAlphaTile * kAlphaTile && n < m && m < Tm && n < Tn;
+    if (cs > kAlphaTile + 1 || ct > kAlphaTile + 1) {   // host classification guarantees this never happens
+        if (valid)
+            for (int q = 0; q < nb; ++q) A[(size_t)(p0 + q) * g.PT + (size_t)m * (m - 1) / 2 + n] = __builtin_nan("");
+        return;
+    }
+    const bool nonres = P.non_resonant, maj = P.majorana, cornered = nonres && maj;
+    const bool needed = valid && (nonres || m == n + 1);
+    double* per = sm;                          // [3][3][cc]
+    double* tmp = per + 9 * cc;                // [4][cc] | mem [3][cc]
+    double* mix = tmp + 4 * cc;                // xl [cs][kAlphaTile], yl [kAlphaTile][ct]
+    double* edg = mix + kAlphaTile * (cs + ct);
+    double* mem = tmp;
+    const int per_jobs = 3 * (ct + cs + kAlphaTile);
+    const int estride = alpha_tile_edge_stride(cs, ct);
+    double* memb = alpha_tile_member_block(edg, cs, ct, 1, 0, 0);   // member edge leaves, k-major
+    const int mstride = alpha_tile_member_stride(cs, ct);
+    // ---- shared edge / m-bin leaves of every k (one job per thread)
+    if (tid < per_jobs) alpha_tile_edge_job(P, tid, tE, ct, sE, cs, g.lo, g.hi, m0, Tm, edg);
+    __syncthreads();
+    // ---- shared corner leaves and brackets of the batch, one k at a time
+    AlphaPre pre[3];
+    PPTerm ppt[kPP ? 3 : 1];
+    int wsh = 0;
+    if (cornered) {
+#pragma unroll 1
+        for (int k = 0; k < 3; ++k) {
+            const double* edgk = edg + k * estride;
+            double* perk = per + 3 * k * cc;
+            for (int j = tid; j < cc; j += kTileThreads) alpha_batch_corner_job(j, edgk, ct, cs, perk, tmp);
+            for (int j = tid; j < kAlphaTile * (cs + ct); j += kTileThreads)
+                alpha_batch_mixed_job(j, edgk, ct, cs, tl, th, sl, sh, n0, m0, T, Tm, mix, mix + kAlphaTile * cs);
+            __syncthreads();
+            if (needed) {
+                SplitLeaves lv;
+                lv.cf[0] = perk; lv.cf[1] = tmp; lv.cf[2] = tmp + cc; lv.cf[3] = tmp + 2 * cc; lv.cf[4] = tmp + 3 * cc;
+                lv.cf[5] = perk + cc; lv.cf[6] = perk + 2 * cc;
+                lv.corm = perk;   // (no member corner is read by the brackets)
+                lv.cc = cc; lv.ct = ct; lv.cs = cs; lv.mb = lm; lv.nb = ln;
+                lv.sidx[0] = sl[lm]; lv.sidx[1] = sh[lm]; lv.tidx[0] = tl[ln]; lv.tidx[1] = th[ln];
+                lv.ted = edgk; lv.sed = edgk + kTEdgeFields * ct; lv.mbv = lv.sed + kSEdgeFields * cs;
+                lv.tedm = memb; lv.sedm = memb + ct; lv.mbm = memb + ct + 2 * cs;
+                lv.xl = mix; lv.yl = mix + kAlphaTile * cs;
+                if (NUSI_AB_BATCH & 4) pre[k] = AlphaPre{lv.cf[1][tid % cc], lv.cf[2][tid % cc], 1.0, 1.0};
+                else alpha_k_pre(P, k, g.lo[n], g.hi[n], g.lo[m], g.hi[m], lv, pre[k]);
+                if (kPP) ppt[k] = alpha_k_pp(P, spl, k, g.lo[n], g.hi[n], g.lo[m], g.hi[m], lv, wsh);
+            }
+            __syncthreads();   // tmp / mix are rewritten by the next k
+        }
+    }
+    if (wsh)
+        for (int q = 0; q < nb; ++q) atomicOr(&warn[p0 + q], wsh);
+    // ---- the batch's points, one after the other
+    const size_t eidx = (size_t)m * (m - 1) / 2 + n;
+#pragma unroll 1
+    for (int q = 0; q < nb; ++q) {
+        const Point& Q = pts[p0 + q];
+        if (q > 0) __syncthreads();   // the previous point's combine is done with memb / mem
+        if (tid < per_jobs) alpha_tile_edge_member_job(Q, 0, 1, tid, tE, ct, sE, cs, g.lo, g.hi, m0, Tm, edg);
+        double tot = 0.0;
+        int w = 0;
+#pragma unroll 1
+        for (int k = 0; k < 3; ++k) {
+            const double* edgk = edg + k * estride;
+            if (cornered) {
+                if (k > 0) __syncthreads();   // mem of the previous k consumed
+                if (!(NUSI_AB_BATCH & 1))
+                    for (int j = tid; j < cc; j += kTileThreads) alpha_batch_member_job(Q, j, edgk, ct, cs, mem);
+            }
+            __syncthreads();
+            if (needed) {
+                const double* perk = per + 3 * k * cc;
+                SplitLeaves lv;
+                lv.cf[0] = perk; lv.cf[1] = perk; lv.cf[2] = perk; lv.cf[3] = perk; lv.cf[4] = perk;
+                lv.cf[5] = perk + cc; lv.cf[6] = perk + 2 * cc;   // (LL, TU1, TU2, G are not read with pre)
+                lv.corm = mem;
+                lv.cc = cc; lv.ct = ct; lv.cs = cs; lv.mb = lm; lv.nb = ln;
+                lv.sidx[0] = sl[lm]; lv.sidx[1] = sh[lm]; lv.tidx[0] = tl[ln]; lv.tidx[1] = th[ln];
+                lv.ted = edgk; lv.sed = edgk + kTEdgeFields * ct; lv.mbv = lv.sed + kSEdgeFields * cs;
+                double* mbk = memb + k * mstride;
+                lv.tedm = mbk; lv.sedm = mbk + ct; lv.mbm = mbk + ct + 2 * cs;
+                lv.xl = mix; lv.yl = mix;   // (not read with pre)
+                if (NUSI_AB_BATCH & 2) tot += mem[(tid * 7) % cc] + lv.tedm[tid % ct] + pre[k].Bt;
+                else alpha_k(Q, spl, k, g.lo[n], g.hi[n], g.lo[m], g.hi[m], lv, tot, w, cornered ? &pre[k] : nullptr,
+                             kPP && cornered ? &ppt[k] : nullptr);
+            }
+        }
+        if (valid) A[(size_t)(p0 + q) * g.PT + eidx] = needed ? tot : 0.0;
+        if (w) atomicOr(&warn[p0 + q], w);
+    }
+}
+
 hipError_t alpha_tiles_create(int T, const unsigned char* shared, AlphaTilesDev* out)
 {
     const int nt = (T + kAlphaTile - 1) / kAlphaTile;
@@ -290,8 +442,37 @@ void alpha_tiles_destroy(AlphaTilesDev* t)
 }
 
 hipError_t launch_alpha(const GridDev& g, const Point* pts, int npts, const SplineSet& spl, const AlphaTilesDev& at,
-                        TablesDev t, int* warn, hipStream_t s, const int* batches, int nbatches, int gmax)
+                        TablesDev t, int* warn, hipStream_t s, const int* batches, int nbatches, int gmax,
+                        bool tile_kernel, int nb_plain)
 {
+    if (!tile_kernel && batches && getenv("NUSI_ALPHA_PER_ENTRY") == nullptr) {
+        // class 0 on the big-batch kernel (batches of up to gmax tables), classes 1 / 2 per table
+        if (at.ext_lo < g.T) {
+            const long long L = g.T - at.ext_lo, ne = L * (L - 1) / 2;
+            hipLaunchKernelGGL(k_alpha, dim3((unsigned)((ne + 255) / 256), npts), dim3(256), 0, s, g, pts, spl, at.ext_lo,
+                               t.A, warn);
+        }
+        int off = 0;
+        for (int c = 0; c < 3; ++c) {
+            if (at.ncls[c] == 0) continue;
+            const int cs = at.cs_max[c], ct = at.ct_max[c];
+            if (c == 0) {   // batches [0, nb_plain) without the phi-phi channel, then those with it
+                const size_t lds = sizeof(double) * (size_t)alpha_batch_lds_doubles(cs, ct);
+                if (nb_plain > 0)
+                    hipLaunchKernelGGL(k_alpha_batch<false>, dim3(at.ncls[0], nb_plain), dim3(kTileThreads), lds, s, g,
+                                       pts, spl, at.tiles, batches, t.A, warn);
+                if (nbatches > nb_plain)
+                    hipLaunchKernelGGL(k_alpha_batch<true>, dim3(at.ncls[0], nbatches - nb_plain), dim3(kTileThreads),
+                                       lds, s, g, pts, spl, at.tiles, batches + nb_plain, t.A, warn);
+            } else {
+                const size_t lds = sizeof(double) * (size_t)alpha_tile_lds_doubles(cs, ct, 1);
+                hipLaunchKernelGGL(k_alpha_tile<1>, dim3(at.ncls[c], npts), dim3(kTileThreads), lds, s, g, pts, spl,
+                                   at.tiles + off, cs, ct, nullptr, t.A, warn);
+            }
+            off += at.ncls[c];
+        }
+        return hipGetLastError();
+    }
     static const bool per_entry = getenv("NUSI_ALPHA_PER_ENTRY") != nullptr;   // A/B switch
     auto per_entry_region = [&](int nlo) {
         const long long L = g.T - nlo, ne = L * (L - 1) / 2;

@@ -129,14 +129,42 @@ NUSI_FN_OUT double li2(double x)
     return add + sgn * li2_useries(-NUSI_PLOG1P(-x));
 }
 
+// Re Li2(x) (li2's algorithm and bits) together with log|1 - x| and, for |x| > 1, log|x| -- the
+// logarithms li2 forms on its way (log1p(-x) of the series argument, or log|x| + log1p(-1/x) after the
+// x -> 1/x map), for the near-axis complex path below; x != 1
+NUSI_FN double li2_ext(double x, double& L1m, double& Lx)
+{
+    double add = 0.0, sgn = 1.0, L = 0.0;
+    if (fabs(x) > 1.0) {
+        L = NUSI_PLOG(fabs(x));
+        add = (x > 1.0 ? 2.0 * kZeta2 : -kZeta2) - 0.5 * L * L;
+        sgn = -1.0;
+        x = 1.0 / x;
+    }
+    Lx = L;
+    if (x > 0.5) {
+        const double lx = NUSI_PLOG(x), l1 = NUSI_PLOG1P(-x);
+        L1m = L + l1;
+        add += sgn * (kZeta2 - lx * l1);
+        return add - sgn * li2_useries(-lx);
+    }
+    if (x == 0.0) {
+        L1m = 0.0;
+        return add;
+    }
+    const double l1 = NUSI_PLOG1P(-x);
+    L1m = L + l1;
+    return add + sgn * li2_useries(-l1);
+}
+
 // Li2(x + iy) close to the real axis, |y| <= kLi2AxisRatio min(|x|, |1 - x|): the Taylor series in iy
 // about the real point x + i0 sign(y) (radius |1 - x|, the distance to the branch point),
 //   Li2(x + iy) = sum_n c_n (iy)^n,  c_n = Li2^(n)(x) / n!,
 //   c_0 = Li2(x) + i pi sign(y) log(x) [x > 1],  c_1 = -log(1 - z) / z (log(1 - z) = log(x - 1) - i pi sign(y)
 //   for x > 1), c_{n+1} = (g^n / (n (n + 1)) - c_n n / (n + 1)) / x with g = 1 / (1 - x)
 // (from z Li2'(z) = -log(1 - z)), summed by Horner in iy.  Truncated after kLi2AxisTerms: the remainder is
-// below (kLi2AxisRatio)^7 ~ 1e-18 relative.  One real Li2, one log and two divisions instead of the general
-// path's three complex logarithms; this is the regime of the alpha table's member leaves (arguments with
+// below (kLi2AxisRatio)^7 ~ 1e-18 relative.  One real Li2 (whose logarithms give log|1 - x| and log x) and
+// two divisions instead of the general path's three complex logarithms; this is the regime of the alpha table's member leaves (arguments with
 // Im ~ Gamma_phi / m_phi).  Same algorithm as the oracle (ora_specfun.c ora_complex_dilog_xy).
 constexpr int kLi2AxisTerms = 6;
 constexpr double kLi2AxisRatio = 2.5e-3;
@@ -146,15 +174,15 @@ NUSI_FN cd cli2_axis(double x, double y)
     constexpr double kB[kLi2AxisTerms] = {0.0, 1.0 / 2, 2.0 / 3, 3.0 / 4, 4.0 / 5, 5.0 / 6};     // n / (n + 1)
     double ar[kLi2AxisTerms + 1], ai[kLi2AxisTerms + 1];
     const double r = 1.0 / x, g = 1.0 / (1.0 - x);
-    ar[0] = li2(x);
+    double L1m, Lx;   // log|1 - x|, log x (x > 1)
+    ar[0] = li2_ext(x, L1m, Lx);
+    ar[1] = -L1m * r;
     if (x < 1.0) {
         ai[0] = 0.0;
-        ar[1] = -NUSI_PLOG1P(-x) * r;
         ai[1] = 0.0;
     } else {
         const double sp = copysign(kPi, y);
-        ai[0] = sp * NUSI_PLOG(x);
-        ar[1] = -NUSI_PLOG(x - 1.0) * r;
+        ai[0] = sp * Lx;
         ai[1] = sp * r;
     }
     double gn = g;
@@ -174,8 +202,9 @@ NUSI_FN cd cli2_axis(double x, double y)
     return cd{sr, si};
 }
 
-// principal-branch Li2(x+iy); y == 0 follows gsl_sf_complex_dilog_xy_e
-NUSI_FN_OUT cd cli2(double x, double y)
+// principal-branch Li2(x+iy); y == 0 follows gsl_sf_complex_dilog_xy_e.  cli2_body is the inline body
+// (one call site of the big-batch alpha kernel inlines it), cli2 the out-of-line entry point.
+NUSI_FN cd cli2_body(double x, double y)
 {
     if (y == 0.0) return cd{li2(x), (x >= 1.0) ? -kPi * NUSI_PLOG(x) : 0.0};
     {
@@ -222,6 +251,7 @@ NUSI_FN_OUT cd cli2(double x, double y)
     const cd s = (u - 0.25 * u2) + (u * u2) * p;
     return add + sgn * s;
 }
+NUSI_FN_OUT cd cli2(double x, double y) { return cli2_body(x, y); }
 NUSI_FN cd cli2(cd z) { return cli2(z.r, z.i); }
 
 // Li3(x), x in [-1, 1/2] (the DSNB source only reaches [-1, 0))

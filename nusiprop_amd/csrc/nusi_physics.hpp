@@ -473,13 +473,21 @@ NUSI_FN void alpha_corner_shared(double S, double t, AlphaCorner& c)
     c.Drr = Dr.r;
     c.Dri = Dr.i;
 }
+// The member leaves (nuSIprop.hpp:1444-1451, 1456-1459) for dt = 2 + t - i gr:
+//   Dc = Li2(w), w = (1 + S + t) / dt = a (c + i gr) / (c^2 + gr^2), a = 1 + S + t, c = 2 + t  (one division),
+//   A  = arg(-(-1 + i gr + S) / dt) = atan2 of -(S - 1 + i gr)(c + i gr) = (-((S - 1) c - gr^2), -gr a)
+//        (dividing by |dt|^2 > 0 does not change the argument: no division).
+// The oracle forms them the same way (nusi_oracle.c member_w / member_arg).
+template <bool kInlineCli2 = false>
 NUSI_FN void alpha_corner_member(double S, double t, double gr, AlphaCorner& c)
 {
-    const cd dt = C(2 + t, -gr);
-    const cd Dc = cli2((1 + S + t) / dt);
+    const double a = 1 + S + t, cr = 2 + t;
+    const double inv = 1.0 / (cr * cr + gr * gr);
+    const double wr = (a * cr) * inv, wi = (a * gr) * inv;
+    const cd Dc = kInlineCli2 ? cli2_body(wr, wi) : cli2(wr, wi);
     c.Dcr = Dc.r;
     c.Dci = Dc.i;
-    c.A = NUSI_CARG(-(C(-1 + S, gr) / dt));
+    c.A = nm::atan2_i(-(gr * a), -((S - 1) * cr - gr * gr));
 }
 NUSI_FN void alpha_corner(double S, double t, double gr, AlphaCorner& c)
 {
@@ -757,52 +765,132 @@ NUSI_FN TileLeaves alpha_tile_leaves(const double* cor, const double* edg, int k
     return lv;
 }
 
-// phi-phi double-scalar production term of alpha (nuSIprop.hpp:1477-1503); out of line: only
-// the phiphi configuration reaches it, and inlined it would cost every entry registers
-NUSI_FN_OUT double alpha_phiphi(const Point& P, const SplineSet& spl, double uk, double Sm, double Sp, double tm,
-                                double tp, double lSm, double lSp, int& warn)
+// phi-phi double-scalar production term of alpha (nuSIprop.hpp:1477-1503), split as
+//   alpha_pp = ((g^4 / m_phi^4 * f1) * f2) / den  (then * |U_fk|^2 and the Majorana / 2-neutrino factors),
+// the reference's association in each branch: f1 = |spline(S'-, ln(-S'-/t-)/ln d * 1.0001, log10 d)| below
+// S'- = 1e4 (f2 = den = 1), else its large-s expansion (branch 1: f1 = numerator, den = 256 pi S-^2 S+^2;
+// branch 2: f1 = the whole bracket; branch 3: f1 = t+ - t-, f2 = bracket, den = 128 pi S- S+).  The term
+// reads neither g nor Gamma_phi, so the points of a batch (same m_phi and masses) share it.  Out of line:
+// only the phiphi configuration reaches it, and inlined it would cost every entry registers.
+struct PPTerm { double f1, f2, den; };
+NUSI_FN_OUT PPTerm alpha_phiphi_core(const SplineSet& spl, double Sm, double Sp, double tm, double tp, double lSm,
+                                     double lSp, int& warn)
 {
-    const double g = P.g, mphi = P.mphi;
-    const double g4 = (g * g) * (g * g), m4 = (mphi * mphi) * (mphi * mphi);
-    const bool maj = P.majorana;
-    double app = 0;
     if (Sm < 1e4) {
         const double d = Sp / Sm;
         const double xx[3] = {Sm, nm::log(-Sm / tm) / nm::log(d) * 1.0001, nm::log10(d)};
         double v = 0;
         if (!spl.a.eval(xx, v)) warn |= kWarnSplineOOB;
-        app = g4 / m4 * fabs(v);
-    } else if (tm < -1) {
+        return PPTerm{fabs(v), 1.0, 1.0};
+    }
+    if (tm < -1) {
         const double l1m = nm::log(-1 - tm), l0m = nm::log(-tm), l1p = nm::log(-1 - tp), l0p = nm::log(-tp);
-        app = g4 / m4 *
-              ((-Sm + Sp) * ((tm - tp) * (Sp * (-2 + tm + tp) + Sm * (-2 - 24 * Sp + tm + tp))
-                             + 4 * (-(Sp * (1 + tm)) + Sm * (-1 + 2 * Sp + (-1 + Sp) * tm)) * l1m
-                             + 2 * (3 * Sp + Sm * (3 + 4 * Sp)) * tm * l0m
-                             + 4 * (Sp + Sp * tp + Sm * (1 + tp - Sp * (2 + tp))) * l1p
-                             - 2 * (3 * Sp + Sm * (3 + 4 * Sp)) * tp * l0p)
-               + 2 * (Sm * Sm) * lSp * ((3 + 2 * Sp) * (tm - tp) + 2 * (Sp * Sp) * ((-1 - tm) * l1m + tm * l0m + (1 + tp) * l1p - tp * l0p))
-               + 2 * (Sp * Sp) * lSm * ((-3 - 2 * Sm) * (tm - tp) + 2 * (Sm * Sm) * ((1 + tm) * l1m - tm * l0m - (1 + tp) * l1p + tp * l0p)))
-              / (256. * kPi * (Sm * Sm) * (Sp * Sp));
-    } else if (tp < -1) {
+        return PPTerm{((-Sm + Sp) * ((tm - tp) * (Sp * (-2 + tm + tp) + Sm * (-2 - 24 * Sp + tm + tp))
+                              + 4 * (-(Sp * (1 + tm)) + Sm * (-1 + 2 * Sp + (-1 + Sp) * tm)) * l1m
+                              + 2 * (3 * Sp + Sm * (3 + 4 * Sp)) * tm * l0m
+                              + 4 * (Sp + Sp * tp + Sm * (1 + tp - Sp * (2 + tp))) * l1p
+                              - 2 * (3 * Sp + Sm * (3 + 4 * Sp)) * tp * l0p)
+                + 2 * (Sm * Sm) * lSp * ((3 + 2 * Sp) * (tm - tp) + 2 * (Sp * Sp) * ((-1 - tm) * l1m + tm * l0m + (1 + tp) * l1p - tp * l0p))
+                + 2 * (Sp * Sp) * lSm * ((-3 - 2 * Sm) * (tm - tp) + 2 * (Sm * Sm) * ((1 + tm) * l1m - tm * l0m - (1 + tp) * l1p + tp * l0p))),
+                      1.0, 256. * kPi * (Sm * Sm) * (Sp * Sp)};
+    }
+    if (tp < -1) {
         const double l1p = nm::log(-1 - tp), l0p = nm::log(-tp);
-        app = g4 / m4 *
-              ((2 * (Sm * Sm) * lSp * ((1 + tp) * (-3 - 2 * Sp + 2 * (Sp * Sp) * l1p) - 2 * (Sp * Sp) * tp * l0p)
+        return PPTerm{(2 * (Sm * Sm) * lSp * ((1 + tp) * (-3 - 2 * Sp + 2 * (Sp * Sp) * l1p) - 2 * (Sp * Sp) * tp * l0p)
                 + (Sm - Sp) * ((1 + tp) * (-3 * (Sm + Sp + 8 * Sm * Sp) + (Sm + Sp) * tp)
                                + 4 * (-(Sp * (1 + tp)) + Sm * (-1 + 2 * Sp + (-1 + Sp) * tp)) * l1p
                                + 2 * (3 * Sp + Sm * (3 + 4 * Sp)) * tp * l0p)
                 + 2 * (Sp * Sp) * lSm * ((3 + 2 * Sm) * (1 + tp) + 2 * (Sm * Sm) * (-((1 + tp) * l1p) + tp * l0p)))
                    / (256. * kPi * (Sm * Sm) * (Sp * Sp))
                + (-1 - tm) * (-6 * Sm + 6 * Sp - 2 * (-2 + Sm) * Sp * lSm + Sm * Sp * (lSm * lSm) + 2 * Sm * (-2 + Sp) * lSp - Sm * Sp * (lSp * lSp))
-                     / (128. * kPi * Sm * Sp));
-    } else
-        app = g4 / m4 * (tp - tm) *
-              (-6 * Sm + 6 * Sp - 2 * (-2 + Sm) * Sp * lSm + Sm * Sp * (lSm * lSm) + 2 * Sm * (-2 + Sp) * lSp - Sm * Sp * (lSp * lSp))
-              / (128. * kPi * Sm * Sp);
+                     / (128. * kPi * Sm * Sp), 1.0, 1.0};
+    }
+    return PPTerm{tp - tm,
+                  -6 * Sm + 6 * Sp - 2 * (-2 + Sm) * Sp * lSm + Sm * Sp * (lSm * lSm) + 2 * Sm * (-2 + Sp) * lSp - Sm * Sp * (lSp * lSp),
+                  128. * kPi * Sm * Sp};
+}
+// alpha_pp of point P from its term (the reference's association: ((g^4/m^4 * f1) * f2) / den; f2 = den = 1
+// are exact)
+NUSI_FN double alpha_phiphi_scale(const Point& P, double uk, const PPTerm& X)
+{
+    const double g = P.g, mphi = P.mphi;
+    const double g4 = (g * g) * (g * g), m4 = (mphi * mphi) * (mphi * mphi);
+    double app = ((g4 / m4 * X.f1) * X.f2) / X.den;
     app *= uk;
-    if (maj) app *= 2;
+    if (P.majorana) app *= 2;
     app *= 2;
-    if (maj) app *= 2;
+    if (P.majorana) app *= 2;
     return app;
+}
+
+// Leaves of the big-batch tile kernel (k_alpha_batch): the shared corner fields live in separate blocks
+// (L, Drr, Dri persist for every mass state through the batch loop; LL, TU1, TU2, G and the mixed logs
+// only while the batch's shared brackets are formed), so each field has its own base pointer.
+struct SplitLeaves {
+    const double* cf[kCornerShared];   // L LL TU1 TU2 G Drr Dri, each [cc]
+    const double *corm, *ted, *sed, *mbv, *tedm, *sedm, *mbm, *xl, *yl;
+    int cc, ct, cs, mb, nb;
+    int sidx[2], tidx[2];
+    NUSI_FN AlphaCorner corner(int si, int ti, double, double) const
+    {
+        const int o = sidx[si] * ct + tidx[ti];
+        return AlphaCorner{cf[0][o], cf[1][o], cf[2][o], cf[3][o], cf[4][o], cf[5][o], cf[6][o],
+                           corm[o], corm[cc + o], corm[2 * cc + o]};
+    }
+    NUSI_FN AlphaTEdge tedge(int ti, double) const
+    {
+        const double* e = ted + tidx[ti];
+        return AlphaTEdge{e[0], e[ct], e[2 * ct], tedm[tidx[ti]], e[3 * ct]};
+    }
+    NUSI_FN AlphaSEdge sedge(int si, double) const
+    {
+        const double* e = sed + sidx[si];
+        return AlphaSEdge{e[0], e[cs], sedm[sidx[si]], sedm[cs + sidx[si]], e[2 * cs]};
+    }
+    NUSI_FN AlphaMBin mbin(double, double) const { return AlphaMBin{mbv[mb], mbv[kAlphaTile + mb], mbm[mb]}; }
+    NUSI_FN double tval(int ti, double, double, double) const { return ted[kTEdgeVal * ct + tidx[ti]]; }
+    NUSI_FN double Sval(int si, double, double, double) const { return sed[kSEdgeVal * cs + sidx[si]]; }
+    NUSI_FN double xlog(int si, double, double, double) const { return xl[sidx[si] * kAlphaTile + nb]; }
+    NUSI_FN double ylog(int ti, double, double, double) const { return yl[mb * ct + tidx[ti]]; }
+};
+// shared corner leaves of corner j: L, Drr, Dri -> per[0..2][cc] (kept), LL, TU1, TU2, G -> tmp[0..3][cc]
+NUSI_FN void alpha_batch_corner_job(int j, const double* edgk, int ct, int cs, double* per, double* tmp)
+{
+    const int cc = cs * ct;
+    const int si = j / ct, ti = j - si * ct;
+    AlphaCorner c;
+    alpha_corner_shared(edgk[kTEdgeFields * ct + kSEdgeVal * cs + si], edgk[kTEdgeVal * ct + ti], c);
+    per[j] = c.L; per[cc + j] = c.Drr; per[2 * cc + j] = c.Dri;
+    tmp[j] = c.LL; tmp[cc + j] = c.TU1; tmp[2 * cc + j] = c.TU2; tmp[3 * cc + j] = c.G;
+}
+#ifndef NUSI_BATCH_INLINE_CLI2   // 1: the big-batch kernel's member job inlines the complex dilogarithm
+#define NUSI_BATCH_INLINE_CLI2 0   // (A/B: 10.02 vs 9.96 ms alpha stage at C4, profiles/r2/ab4) -- kept out of line
+#endif
+// member corner leaves of corner j for point P -> mem[0..2][cc] (Dcr, Dci, A)
+NUSI_FN void alpha_batch_member_job(const Point& P, int j, const double* edgk, int ct, int cs, double* mem)
+{
+    const int cc = cs * ct;
+    const int si = j / ct, ti = j - si * ct;
+    AlphaCorner c;
+    alpha_corner_member<NUSI_BATCH_INLINE_CLI2>(edgk[kTEdgeFields * ct + kSEdgeVal * cs + si], edgk[kTEdgeVal * ct + ti],
+                                                P.a_gr, c);
+    mem[j] = c.Dcr; mem[cc + j] = c.Dci; mem[2 * cc + j] = c.A;
+}
+// xlog / ylog leaves of mass state k into xl [cs][kAlphaTile], yl [kAlphaTile][ct] (alpha_tile_mixed_job's jobs)
+NUSI_FN void alpha_batch_mixed_job(int j, const double* edgk, int ct, int cs, const int* tl, const int* th,
+                                   const int* sl, const int* sh, int n0, int m0, int T, int Tm, double* xl, double* yl)
+{
+    const double* tv = edgk + kTEdgeVal * ct;
+    const double* sv = edgk + kTEdgeFields * ct + kSEdgeVal * cs;
+    if (j < kAlphaTile * cs) {
+        const int s = j / kAlphaTile, ln = j - s * kAlphaTile;
+        if (n0 + ln >= T) return;
+        xl[j] = alpha_xlog(sv[s], tv[tl[ln]], tv[th[ln]]);
+    } else {
+        const int q = j - kAlphaTile * cs, lm = q / ct, t = q - lm * ct;
+        if (m0 + lm >= Tm) return;
+        yl[q] = alpha_ylog(sv[sl[lm]], sv[sh[lm]], tv[t]);
+    }
 }
 
 // compiler fence between the phases of alpha_k (device: no scheduling or LDS-load reuse across it)
@@ -883,12 +971,25 @@ NUSI_FN void alpha_k_pre(const Point& P, int k, double Em, double Ep, double Emp
     alpha_bracket_t(lv, Sm, Sp, tm, tp, m4, pre.Dt, pre.Bt);
     alpha_bracket_tu(lv, Sm, Sp, tm, tp, m4, pre.Dtu, pre.Btu);
 }
+// the phi-phi term of entry (Em, Ep, Em', Ep') and mass state k (shared by a batch); zero term where the
+// channel is closed (S'- <= 4)
+template <class Lv>
+NUSI_FN PPTerm alpha_k_pp(const Point& P, const SplineSet& spl, int k, double Em, double Ep, double Emp, double Epp,
+                          const Lv& lv, int& warn)
+{
+    const double mphi = P.mphi, m2 = mphi * mphi, mk = P.mn[k];
+    const double tp = lv.tval(1, mk, Ep, m2), tm = lv.tval(0, mk, Em, m2);
+    const double Sp = lv.Sval(1, mk, Epp, m2), Sm = lv.Sval(0, mk, Emp, m2);
+    if (!(Sm > 4 && P.phiphi)) return PPTerm{0.0, 1.0, 1.0};
+    const AlphaSEdge eSm = lv.sedge(0, Sm), eSp = lv.sedge(1, Sp);
+    return alpha_phiphi_core(spl, Sm, Sp, tm, tp, eSm.lS, eSp.lS, warn);
+}
 
 // one mass state k of alpha(Em, Ep, Em', Ep'): tot += wgt * (every channel); pre: the shared brackets
 // of a batch (alpha_k_pre with another point of it), nullptr = evaluate them here
 template <class Lv>
 NUSI_FN void alpha_k(const Point& P, const SplineSet& spl, int k, double Em, double Ep, double Emp, double Epp,
-                     const Lv& lv, double& tot, int& warn, const AlphaPre* pre = nullptr)
+                     const Lv& lv, double& tot, int& warn, const AlphaPre* pre = nullptr, const PPTerm* ppt = nullptr)
 {
     const double g = P.g, mphi = P.mphi;
     const double g4 = (g * g) * (g * g), m2 = mphi * mphi, m4 = (mphi * mphi) * (mphi * mphi);
@@ -986,7 +1087,9 @@ NUSI_FN void alpha_k(const Point& P, const SplineSet& spl, int k, double Em, dou
     const double asu = maj ? ast : 0.;
     tot += wgt * asu;
 
-    const double app = (Sm > 4 && P.phiphi) ? alpha_phiphi(P, spl, uk, Sm, Sp, tm, tp, lSm, lSp, warn) : 0.0;
+    double app = 0.0;
+    if (Sm > 4 && P.phiphi)   // ppt: the term shared by a batch (alpha_k_pp)
+        app = alpha_phiphi_scale(P, uk, ppt ? *ppt : alpha_phiphi_core(spl, Sm, Sp, tm, tp, lSm, lSp, warn));
     tot += wgt * app;
 
     const double nrm = P.a_nrm;

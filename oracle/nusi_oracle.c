@@ -471,6 +471,22 @@ double ora_alphaTilde(ora_state *S, double Em, double Ep)   /* nuSIprop.hpp:924-
     return tot;
 }
 
+/* The s-t interference's g-dependent pieces (nuSIprop.hpp:1440-1459) for dt = 2 + t - i gr:
+ * (1 + S + t) / dt = a (c + i gr) / (c^2 + gr^2) with a = 1 + S + t, c = 2 + t (one division), and
+ * arg(-(-1 + i gr + S) / dt) as the atan2 of -(S - 1 + i gr)(c + i gr) (the positive |dt|^2 dropped).
+ * The GPU forms them the same way (nusi_physics.hpp alpha_corner_member). */
+static zc member_w(double S, double t, double gr)
+{
+    const double a = 1 + S + t, c = 2 + t;
+    const double inv = 1.0 / (c * c + gr * gr);
+    return zmk((a * c) * inv, (a * gr) * inv);
+}
+static double member_arg(double S, double t, double gr)
+{
+    const double a = 1 + S + t, c = 2 + t;
+    return ora_atan2(-(gr * a), -((S - 1) * c - gr * gr));
+}
+
 double ora_alpha(ora_state *S, double Em, double Ep, double Emp, double Epp)   /* nuSIprop.hpp:1237-1520 */
 {
     const double g = S->p.g, mphi = S->p.mphi;
@@ -573,14 +589,13 @@ double ora_alpha(ora_state *S, double Em, double Ep, double Emp, double Epp)   /
 
         /* s-t interference: 8 GSL complex dilogs (nuSIprop.hpp:1431-1451) */
         const double z1 = (1 + Sm + tm) / (1 + tm);
-        const zc dtm = zmk(2 + tm, -gr), dtp = zmk(2 + tp, -gr);       /* 2 - I gr + t */
-        const zc z2 = zrdiv(1 + Sm + tm, dtm);
+        const zc z2 = member_w(Sm, tm, gr);
         const double z3 = (1 + Sp + tm) / (1 + tm);
-        const zc z4 = zrdiv(1 + Sp + tm, dtm);
+        const zc z4 = member_w(Sp, tm, gr);
         const double z5 = (1 + Sm + tp) / (1 + tp);
-        const zc z6 = zrdiv(1 + Sm + tp, dtp);
+        const zc z6 = member_w(Sm, tp, gr);
         const double z7 = (1 + Sp + tp) / (1 + tp);
-        const zc z8 = zrdiv(1 + Sp + tp, dtp);
+        const zc z8 = member_w(Sp, tp, gr);
         double R[9], J[9];
         ora_complex_dilog_xy(z1, 0, &R[1], &J[1]);
         ora_complex_dilog_xy(z2.r, z2.i, &R[2], &J[2]);
@@ -600,10 +615,10 @@ double ora_alpha(ora_state *S, double Em, double Ep, double Emp, double Epp)   /
             ast = g4 / (32 * M_PI * (1 + SQ(gr)) * m4) *
                   (2 * gr * (J[1] - J[2] - J[3] + J[4] - J[5] + J[6] + J[7] - J[8])
                    - 2 * (R[1] - R[2] - R[3] + R[4] - R[5] + R[6] + R[7] - R[8])
-                   + 2 * gr * (cm - zarg(zneg(zdiv(nm_, dtm)))) * Lmm
-                   - 2 * gr * (cm - zarg(zneg(zdiv(np_, dtm)))) * Lpm
-                   + 2 * gr * (cp - zarg(zneg(zdiv(np_, dtp)))) * Lpq
-                   - 2 * gr * (cp - zarg(zneg(zdiv(nm_, dtp)))) * Lmq
+                   + 2 * gr * (cm - member_arg(Sm, tm, gr)) * Lmm
+                   - 2 * gr * (cm - member_arg(Sp, tm, gr)) * Lpm
+                   + 2 * gr * (cp - member_arg(Sp, tp, gr)) * Lpq
+                   - 2 * gr * (cp - member_arg(Sm, tp, gr)) * Lmq
                    + 2 * (gr * zarg(nm_) - gr * zarg(np_) + Lsp / 2. - Lsm / 2. + lSm - lSp) * (2 * (tm - tp) + (Lmt - Lmp))
                    + Lmm * (Lsm - L2m - 2 * (lSm - am)) - Lpm * (Lsp - L2m - 2 * (lSp - am))
                    - Lmq * (Lsm - L2p - 2 * (lSm - ap)) + Lpq * (Lsp - L2p - 2 * (lSp - ap)));

@@ -57,6 +57,33 @@ double ora_dilog(double x)
 
 double ora_li2(double x) { return ora_dilog(x); }
 
+/* ora_dilog (same operations) with log|1 - x| and, for |x| > 1, log|x| (the logarithms it forms on its
+ * way: log1p(-x), or log|x| + log1p(-1/x) after the x -> 1/x map); x != 1 */
+static double dilog_ext(double x, double *L1m, double *Lx)
+{
+    double add = 0.0, sgn = 1.0, L = 0.0;
+    if (fabs(x) > 1.0) {
+        L = ora_log(fabs(x));
+        add = (x > 1.0 ? 2.0 * ZETA2 : -ZETA2) - 0.5 * L * L;
+        sgn = -1.0;
+        x = 1.0 / x;
+    }
+    *Lx = L;
+    if (x > 0.5) {
+        const double lx = ora_log(x), l1 = ora_log1p(-x);
+        *L1m = L + l1;
+        add += sgn * (ZETA2 - lx * l1);
+        return add - sgn * li2_useries(-lx);
+    }
+    if (x == 0.0) {
+        *L1m = 0.0;
+        return add;
+    }
+    const double l1 = ora_log1p(-x);
+    *L1m = L + l1;
+    return add + sgn * li2_useries(-l1);
+}
+
 /* Li2(x + iy) for |y| <= AXIS_RATIO min(|x|, |1 - x|): Taylor series in iy about x + i0 sign(y)
  * (radius |1 - x|): c_0 = Li2(x) + i pi sign(y) log x [x > 1], c_1 = -log(1 - z)/z, c_{n+1} =
  * (g^n/(n(n+1)) - c_n n/(n+1))/x with g = 1/(1 - x) (from z Li2'(z) = -log(1 - z)), Horner in iy,
@@ -70,15 +97,15 @@ static void cdilog_axis(double x, double y, double *re, double *im)
     static const double kB[AXIS_TERMS] = {0.0, 1.0 / 2, 2.0 / 3, 3.0 / 4, 4.0 / 5, 5.0 / 6};
     double ar[AXIS_TERMS + 1], ai[AXIS_TERMS + 1];
     const double r = 1.0 / x, g = 1.0 / (1.0 - x);
-    ar[0] = ora_dilog(x);
+    double L1m, Lx;
+    ar[0] = dilog_ext(x, &L1m, &Lx);
+    ar[1] = -L1m * r;
     if (x < 1.0) {
         ai[0] = 0.0;
-        ar[1] = -ora_log1p(-x) * r;
         ai[1] = 0.0;
     } else {
         const double sp = copysign(PI_D, y);
-        ai[0] = sp * ora_log(x);
-        ar[1] = -ora_log(x - 1.0) * r;
+        ai[0] = sp * Lx;
         ai[1] = sp * r;
     }
     double gn = g;

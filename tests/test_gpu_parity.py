@@ -258,3 +258,24 @@ def test_plan_serialises_calls_across_streams(nusi):
         H.hipFree(fa)
         H.hipFree(la)
         H.hipStreamDestroy(s2)
+
+
+def test_alpha_batch_kernel_equals_tile_kernel(nusi, monkeypatch):
+    """The big-batch alpha kernel (shared leaves once per batch of up to 64 tables, points one after the
+    other) and the k_alpha_tile<G> batches of 3 give the same tables and fluxes bit for bit: a C4-style
+    slice (2 m_phi x 8 couplings, Majorana) plus Dirac and resonant-only points, several batch caps."""
+    base = [dict(cases.C2B_100, mphi=m, g=g) for m in (6e5, 2e6) for g in np.logspace(-3, 0, 8)]
+    pts = base + [dict(cases.C2B_100, mphi=1e6, g=0.1, majorana=False), dict(cases.C2B_100, mphi=1e6, g=0.2,
+                                                                             non_resonant=False)]
+    monkeypatch.setenv("NUSI_ALPHA_KERNEL", "tile")
+    ref = _gpu(nusi, pts)
+    monkeypatch.delenv("NUSI_ALPHA_KERNEL")
+    for cap in ("", "1", "5", "64"):
+        if cap:
+            monkeypatch.setenv("NUSI_ALPHA_BATCH", cap)
+        got = _gpu(nusi, pts)
+        assert np.array_equal(got[1], ref[1]) and np.array_equal(got[2], ref[2]), cap
+        for a, b in zip(got[3], ref[3]):
+            for x, y in zip(a, b):
+                assert np.array_equal(x, y), cap
+        assert got[4] == ref[4]
