@@ -224,32 +224,64 @@ __global__ __launch_bounds__(kTileThreads) NUSI_TILE_ATTR void k_alpha_tile(Grid
 
 // ---------------------------------------------------------------------------
 // k_alpha_batch: one workgroup per (class-0 tile, batch of up to 255 tables sharing m_phi, the masses
-// and the channel flags).  The leaves of (S', t) alone and the brackets built from them alone (t,
-// t-u, phi-phi) are formed ONCE per batch; then the batch's points run one after the other through
-// their member leaves (those that read gr = Gamma_phi / m_phi: one complex dilogarithm and one arg per
-// corner, a few per edge) and the per-point combine.  So the batch size no longer costs LDS: the shared
-// work per table falls as 1/batch (C4: 32 couplings per m_phi, C5: 64) where k_alpha_tile<G> stopped at
-// G = 3.  Every entry is the same alpha_k expression on the same leaves as k_alpha_tile: bit-identical.
+// and the channel flags).  Mass state by mass state, the leaves of (S', t) alone -- and from them the
+// t / t-u / phi-phi brackets and the Taylor coefficients of the member complex dilogarithms about their
+// gr-free real points -- are formed ONCE per batch; then the batch's points run through their member
+// leaves (edge leaves for kBatchQC points at a time, one job per thread; per corner one Taylor
+// evaluation) and the per-point combine.  The shared work per table falls as 1 / batch (C4: 32
+// couplings per m_phi, C5: 64).  A point's entry accumulates over the mass states in the output array
+// (the reference's k order and term order: bit-identical to k_alpha_tile and to the oracle).
 //
-// LDS (doubles; cs, ct <= kAlphaTile + 1, cc = cs ct):
-//   per [3 k][3][cc]   L, Drr, Dri of every mass state (kept through the batch loop)
-//   tmp [4][cc]        LL, TU1, TU2, G of the current k (bracket phase); reused as mem [3][cc], the
-//                      member corner leaves of the current (point, k)
-//   mix [kAlphaTile (cs + ct)]  xlog / ylog of the current k (bracket phase)
-//   edg alpha_tile_edge_doubles(cs, ct, 1): shared edge / m-bin leaves of every k + one point's member ones
+// LDS (doubles; cs, ct <= kAlphaTile + 1, cc = cs ct; offsets for the largest tile):
+//   P3   [3][cc]   L, Drr, Dri of the current k
+//   X    [10][cc]  the current k's member coefficients (alpha_batch_xshared_job); while the brackets are
+//                  formed it holds LL, TU1, TU2, G [4][cc] and the mixed logs [kAlphaTile (cs + ct)]
+//   mem  [2][cc]   member corner leaves Dcr, Dci of the current (point, k)
+//   edg  [alpha_tile_edge_stride]  shared edge / m-bin leaves of the current k
+//   memb [kBatchQC][alpha_batch_memb_doubles]  member edge leaves of a chunk of points
 // ---------------------------------------------------------------------------
-__host__ __device__ constexpr int alpha_batch_lds_doubles(int cs, int ct)
+constexpr int kBatchQC = 4;   // points per member-edge round: kBatchQC (ct + cs + kAlphaTile) <= 252 jobs
+__host__ __device__ inline int alpha_batch_lds_doubles()
 {
-    return 3 * 3 * cs * ct + 4 * cs * ct + kAlphaTile * (cs + ct) + alpha_tile_edge_doubles(cs, ct, 1);
+    const int c1 = kAlphaTile + 1;
+    return (3 + kXFields + 2) * c1 * c1 + alpha_tile_edge_stride(c1, c1) + kBatchQC * alpha_batch_memb_doubles(c1, c1);
 }
+static_assert(kXFields * (kAlphaTile + 1) * (kAlphaTile + 1) >= 4 * (kAlphaTile + 1) * (kAlphaTile + 1) + kAlphaTile * 2 * (kAlphaTile + 1),
+              "the bracket phase's blocks fit X");
+static_assert(kBatchQC * (2 * (kAlphaTile + 1) + kAlphaTile) <= kTileThreads, "one member-edge round per chunk");
 
 #ifndef NUSI_AB_BATCH   // timing experiments only: 1 skip the member corner leaves, 2 skip the combine, 4 skip brackets
 #define NUSI_AB_BATCH 0
 #endif
 #ifndef NUSI_BATCH_WAVES
-#define NUSI_BATCH_WAVES 4   // 4: 8.32-8.45 ms vs 3: 8.61-8.81 (C4 alpha stage; 43 VGPRs spill, profiles/r2/ab)
+#define NUSI_BATCH_WAVES 4
 #endif
-template <bool kPP>   // the batches' tables have the phi-phi channel (their shared terms are kept per k)
+// the batch-shared phases out of line: they run once per batch, and inlined their working sets would
+// raise the register pressure of the per-point loop (NUSI_BATCH_OUTLINE=0: inline, A/B)
+#ifndef NUSI_BATCH_OUTLINE
+#define NUSI_BATCH_OUTLINE 1
+#endif
+#if NUSI_BATCH_OUTLINE
+#define NUSI_BCOLD __device__ __attribute__((noinline))
+#else
+#define NUSI_BCOLD __device__ inline
+#endif
+NUSI_BCOLD void b_corner(int j, const double* edgk, int ct, int cs, double* per, double* tmp)
+{
+    alpha_batch_corner_job(j, edgk, ct, cs, per, tmp);
+}
+NUSI_BCOLD void b_xshared(int j, const double* edgk, int ct, int cs, double* X) { alpha_batch_xshared_job(j, edgk, ct, cs, X); }
+NUSI_BCOLD void b_medge(const Point& P, int k, int job, const double* tE, int ct, const double* sE, int cs,
+                        const double* lo, const double* hi, int m0, int Tm, double* memb)
+{
+    alpha_batch_medge_job(P, k, job, tE, ct, sE, cs, lo, hi, m0, Tm, memb);
+}
+NUSI_BCOLD void b_pre(const Point& P, int k, double Em, double Ep, double Emp, double Epp, SplitLeaves lv, AlphaPre& pre)
+{
+    alpha_k_pre(P, k, Em, Ep, Emp, Epp, lv, pre);
+}
+
+template <bool kPP>   // the batches' tables have the phi-phi channel (its shared term per k)
 __global__ __launch_bounds__(kTileThreads) __attribute__((amdgpu_waves_per_eu(NUSI_BATCH_WAVES, NUSI_BATCH_WAVES)))
 void k_alpha_batch(GridDev g, const Point* __restrict__ pts, SplineSet spl, const int* __restrict__ tiles,
                    const int* __restrict__ batches, double* __restrict__ A, int* __restrict__ warn)
@@ -283,95 +315,98 @@ void k_alpha_batch(GridDev g, const Point* __restrict__ pts, SplineSet spl, cons
     const int ln = tid % kAlphaTile, lm = tid / kAlphaTile;
     const int n = n0 + ln, m = m0 + lm;
     const bool valid = tid < kAlphaTile * kAlphaTile && n < m && m < Tm && n < Tn;
+    const size_t eidx = (size_t)m * (m - 1) / 2 + n;
     if (cs > kAlphaTile + 1 || ct > kAlphaTile + 1) {   // host classification guarantees this never happens
         if (valid)
-            for (int q = 0; q < nb; ++q) A[(size_t)(p0 + q) * g.PT + (size_t)m * (m - 1) / 2 + n] = __builtin_nan("");
+            for (int q = 0; q < nb; ++q) A[(size_t)(p0 + q) * g.PT + eidx] = __builtin_nan("");
         return;
     }
     const bool nonres = P.non_resonant, maj = P.majorana, cornered = nonres && maj;
     const bool needed = valid && (nonres || m == n + 1);
-    double* per = sm;                          // [3][3][cc]
-    double* tmp = per + 9 * cc;                // [4][cc] | mem [3][cc]
-    double* mix = tmp + 4 * cc;                // xl [cs][kAlphaTile], yl [kAlphaTile][ct]
-    double* edg = mix + kAlphaTile * (cs + ct);
-    double* mem = tmp;
-    const int per_jobs = 3 * (ct + cs + kAlphaTile);
-    const int estride = alpha_tile_edge_stride(cs, ct);
-    double* memb = alpha_tile_member_block(edg, cs, ct, 1, 0, 0);   // member edge leaves, k-major
-    const int mstride = alpha_tile_member_stride(cs, ct);
-    // ---- shared edge / m-bin leaves of every k (one job per thread)
-    if (tid < per_jobs) alpha_tile_edge_job(P, tid, tE, ct, sE, cs, g.lo, g.hi, m0, Tm, edg);
-    __syncthreads();
-    // ---- shared corner leaves and brackets of the batch, one k at a time
-    AlphaPre pre[3];
-    PPTerm ppt[kPP ? 3 : 1];
+    constexpr int ccmax = (kAlphaTile + 1) * (kAlphaTile + 1);
+    double* P3 = sm;                           // [3][cc]
+    double* X = P3 + 3 * ccmax;                // [kXFields][cc] | LL TU1 TU2 G [4][cc] + mixed
+    double* mem = X + kXFields * ccmax;        // [2][cc]
+    double* edgk = mem + 2 * ccmax;            // [estride]
+    double* membq = edgk + alpha_tile_edge_stride(kAlphaTile + 1, kAlphaTile + 1);   // [kBatchQC][mbd]
+    const int mbd = alpha_batch_memb_doubles(cs, ct);
+    double* tmp = X;
+    double* mix = X + 4 * cc;
+    const int mjobs = ct + cs + kAlphaTile;
     int wsh = 0;
-    if (cornered) {
 #pragma unroll 1
-        for (int k = 0; k < 3; ++k) {
-            const double* edgk = edg + k * estride;
-            double* perk = per + 3 * k * cc;
-            for (int j = tid; j < cc; j += kTileThreads) alpha_batch_corner_job(j, edgk, ct, cs, perk, tmp);
+    for (int k = 0; k < 3; ++k) {
+        __syncthreads();   // the previous k's points are done with P3, X, mem, edgk, membq
+        if (tid < mjobs) alpha_tile_edge_job_k(P, k, tid, tE, ct, sE, cs, g.lo, g.hi, m0, Tm, edgk);
+        __syncthreads();
+        // ---- the batch's shared leaves and brackets of mass state k
+        AlphaPre pre{};
+        PPTerm ppt{0.0, 1.0, 1.0};
+        if (cornered) {
+            for (int j = tid; j < cc; j += kTileThreads) b_corner(j, edgk, ct, cs, P3, tmp);
             for (int j = tid; j < kAlphaTile * (cs + ct); j += kTileThreads)
                 alpha_batch_mixed_job(j, edgk, ct, cs, tl, th, sl, sh, n0, m0, T, Tm, mix, mix + kAlphaTile * cs);
             __syncthreads();
             if (needed) {
                 SplitLeaves lv;
-                lv.cf[0] = perk; lv.cf[1] = tmp; lv.cf[2] = tmp + cc; lv.cf[3] = tmp + 2 * cc; lv.cf[4] = tmp + 3 * cc;
-                lv.cf[5] = perk + cc; lv.cf[6] = perk + 2 * cc;
-                lv.corm = perk;   // (no member corner is read by the brackets)
+                lv.cf[0] = P3; lv.cf[1] = tmp; lv.cf[2] = tmp + cc; lv.cf[3] = tmp + 2 * cc; lv.cf[4] = tmp + 3 * cc;
+                lv.cf[5] = P3 + cc; lv.cf[6] = P3 + 2 * cc;
+                lv.corm = P3;   // (no member leaf is read by the brackets)
                 lv.cc = cc; lv.ct = ct; lv.cs = cs; lv.mb = lm; lv.nb = ln;
                 lv.sidx[0] = sl[lm]; lv.sidx[1] = sh[lm]; lv.tidx[0] = tl[ln]; lv.tidx[1] = th[ln];
                 lv.ted = edgk; lv.sed = edgk + kTEdgeFields * ct; lv.mbv = lv.sed + kSEdgeFields * cs;
-                lv.tedm = memb; lv.sedm = memb + ct; lv.mbm = memb + ct + 2 * cs;
+                lv.tedm = membq; lv.sedm = membq + ct; lv.mbm = membq + ct + 2 * cs; lv.marg = membq;   // (not read)
                 lv.xl = mix; lv.yl = mix + kAlphaTile * cs;
-                if (NUSI_AB_BATCH & 4) pre[k] = AlphaPre{lv.cf[1][tid % cc], lv.cf[2][tid % cc], 1.0, 1.0};
-                else alpha_k_pre(P, k, g.lo[n], g.hi[n], g.lo[m], g.hi[m], lv, pre[k]);
-                if (kPP) ppt[k] = alpha_k_pp(P, spl, k, g.lo[n], g.hi[n], g.lo[m], g.hi[m], lv, wsh);
+                if (NUSI_AB_BATCH & 4) pre = AlphaPre{lv.cf[1][tid % cc], lv.cf[2][tid % cc], 1.0, 1.0};
+                else b_pre(P, k, g.lo[n], g.hi[n], g.lo[m], g.hi[m], lv, pre);
+                if (kPP) ppt = alpha_k_pp(P, spl, k, g.lo[n], g.hi[n], g.lo[m], g.hi[m], lv, wsh);
             }
-            __syncthreads();   // tmp / mix are rewritten by the next k
+            __syncthreads();   // X is rewritten with the member coefficients
+            for (int j = tid; j < cc; j += kTileThreads) b_xshared(j, edgk, ct, cs, X);
+        }
+        // ---- the points, kBatchQC at a time: their member edge leaves in one round, then point by point
+#pragma unroll 1
+        for (int q0 = 0; q0 < nb; q0 += kBatchQC) {
+            const int nq = (nb - q0 < kBatchQC) ? nb - q0 : kBatchQC;
+            __syncthreads();   // the previous chunk is done with membq (and mem)
+            {
+                const int qq = tid / mjobs, job = tid - qq * mjobs;
+                if (qq < nq) b_medge(pts[p0 + q0 + qq], k, job, tE, ct, sE, cs, g.lo, g.hi, m0, Tm, membq + qq * mbd);
+            }
+#pragma unroll 1
+            for (int qq = 0; qq < nq; ++qq) {
+                const int q = q0 + qq;
+                const Point& Q = pts[p0 + q];
+                const double* memb = membq + qq * mbd;
+                double tot = 0.0;
+                if (k > 0 && needed && !(NUSI_AB_BATCH & 8)) tot = A[(size_t)(p0 + q) * g.PT + eidx];   // after states < k
+                __syncthreads();   // member edges written / the previous point's combine is done with mem
+                if (cornered && !(NUSI_AB_BATCH & 1))
+                    for (int j = tid; j < cc; j += kTileThreads) alpha_batch_mcorner_job(Q, j, edgk, ct, cs, X, memb, mem);
+                __syncthreads();   // mem of q written
+                int w = 0;
+                if (needed) {
+                    SplitLeaves lv;
+                    lv.cf[0] = P3; lv.cf[1] = P3; lv.cf[2] = P3; lv.cf[3] = P3; lv.cf[4] = P3;
+                    lv.cf[5] = P3 + cc; lv.cf[6] = P3 + 2 * cc;   // (LL, TU1, TU2, G are not read with pre)
+                    lv.corm = mem;
+                    lv.cc = cc; lv.ct = ct; lv.cs = cs; lv.mb = lm; lv.nb = ln;
+                    lv.sidx[0] = sl[lm]; lv.sidx[1] = sh[lm]; lv.tidx[0] = tl[ln]; lv.tidx[1] = th[ln];
+                    lv.ted = edgk; lv.sed = edgk + kTEdgeFields * ct; lv.mbv = lv.sed + kSEdgeFields * cs;
+                    lv.tedm = memb; lv.sedm = memb + ct; lv.mbm = memb + ct + 2 * cs;
+                    lv.marg = memb + ct + 2 * cs + kAlphaTile + 2 * ct;   // sT | fT | sS | fS
+                    lv.xl = mix; lv.yl = mix;   // (not read with pre)
+                    if (NUSI_AB_BATCH & 2) tot += mem[(tid * 7) % cc] + memb[tid % ct] + pre.Bt;
+                    else alpha_k(Q, spl, k, g.lo[n], g.hi[n], g.lo[m], g.hi[m], lv, tot, w, cornered ? &pre : nullptr,
+                                 kPP && cornered ? &ppt : nullptr);
+                }
+                if (valid && (!(NUSI_AB_BATCH & 8) || k == 2)) A[(size_t)(p0 + q) * g.PT + eidx] = needed ? tot : 0.0;
+                if (w) atomicOr(&warn[p0 + q], w);
+            }
         }
     }
     if (wsh)
         for (int q = 0; q < nb; ++q) atomicOr(&warn[p0 + q], wsh);
-    // ---- the batch's points, one after the other
-    const size_t eidx = (size_t)m * (m - 1) / 2 + n;
-#pragma unroll 1
-    for (int q = 0; q < nb; ++q) {
-        const Point& Q = pts[p0 + q];
-        if (q > 0) __syncthreads();   // the previous point's combine is done with memb / mem
-        if (tid < per_jobs) alpha_tile_edge_member_job(Q, 0, 1, tid, tE, ct, sE, cs, g.lo, g.hi, m0, Tm, edg);
-        double tot = 0.0;
-        int w = 0;
-#pragma unroll 1
-        for (int k = 0; k < 3; ++k) {
-            const double* edgk = edg + k * estride;
-            if (cornered) {
-                if (k > 0) __syncthreads();   // mem of the previous k consumed
-                if (!(NUSI_AB_BATCH & 1))
-                    for (int j = tid; j < cc; j += kTileThreads) alpha_batch_member_job(Q, j, edgk, ct, cs, mem);
-            }
-            __syncthreads();
-            if (needed) {
-                const double* perk = per + 3 * k * cc;
-                SplitLeaves lv;
-                lv.cf[0] = perk; lv.cf[1] = perk; lv.cf[2] = perk; lv.cf[3] = perk; lv.cf[4] = perk;
-                lv.cf[5] = perk + cc; lv.cf[6] = perk + 2 * cc;   // (LL, TU1, TU2, G are not read with pre)
-                lv.corm = mem;
-                lv.cc = cc; lv.ct = ct; lv.cs = cs; lv.mb = lm; lv.nb = ln;
-                lv.sidx[0] = sl[lm]; lv.sidx[1] = sh[lm]; lv.tidx[0] = tl[ln]; lv.tidx[1] = th[ln];
-                lv.ted = edgk; lv.sed = edgk + kTEdgeFields * ct; lv.mbv = lv.sed + kSEdgeFields * cs;
-                double* mbk = memb + k * mstride;
-                lv.tedm = mbk; lv.sedm = mbk + ct; lv.mbm = mbk + ct + 2 * cs;
-                lv.xl = mix; lv.yl = mix;   // (not read with pre)
-                if (NUSI_AB_BATCH & 2) tot += mem[(tid * 7) % cc] + lv.tedm[tid % ct] + pre[k].Bt;
-                else alpha_k(Q, spl, k, g.lo[n], g.hi[n], g.lo[m], g.hi[m], lv, tot, w, cornered ? &pre[k] : nullptr,
-                             kPP && cornered ? &ppt[k] : nullptr);
-            }
-        }
-        if (valid) A[(size_t)(p0 + q) * g.PT + eidx] = needed ? tot : 0.0;
-        if (w) atomicOr(&warn[p0 + q], w);
-    }
 }
 
 hipError_t alpha_tiles_create(int T, const unsigned char* shared, AlphaTilesDev* out)
@@ -457,7 +492,8 @@ hipError_t launch_alpha(const GridDev& g, const Point* pts, int npts, const Spli
             if (at.ncls[c] == 0) continue;
             const int cs = at.cs_max[c], ct = at.ct_max[c];
             if (c == 0) {   // batches [0, nb_plain) without the phi-phi channel, then those with it
-                const size_t lds = sizeof(double) * (size_t)alpha_batch_lds_doubles(cs, ct);
+                const size_t lds = sizeof(double) * (size_t)alpha_batch_lds_doubles();
+                if (cs > kAlphaTile + 1 || ct > kAlphaTile + 1) return hipErrorInvalidValue;
                 if (nb_plain > 0)
                     hipLaunchKernelGGL(k_alpha_batch<false>, dim3(at.ncls[0], nb_plain), dim3(kTileThreads), lds, s, g,
                                        pts, spl, at.tiles, batches, t.A, warn);

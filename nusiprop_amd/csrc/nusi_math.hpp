@@ -157,49 +157,65 @@ NUSI_FN double li2_ext(double x, double& L1m, double& Lx)
     return add + sgn * li2_useries(-l1);
 }
 
-// Li2(x + iy) close to the real axis, |y| <= kLi2AxisRatio min(|x|, |1 - x|): the Taylor series in iy
-// about the real point x + i0 sign(y) (radius |1 - x|, the distance to the branch point),
-//   Li2(x + iy) = sum_n c_n (iy)^n,  c_n = Li2^(n)(x) / n!,
-//   c_0 = Li2(x) + i pi sign(y) log(x) [x > 1],  c_1 = -log(1 - z) / z (log(1 - z) = log(x - 1) - i pi sign(y)
-//   for x > 1), c_{n+1} = (g^n / (n (n + 1)) - c_n n / (n + 1)) / x with g = 1 / (1 - x)
-// (from z Li2'(z) = -log(1 - z)), summed by Horner in iy.  Truncated after kLi2AxisTerms: the remainder is
-// below (kLi2AxisRatio)^7 ~ 1e-18 relative.  One real Li2 (whose logarithms give log|1 - x| and log x) and
-// two divisions instead of the general path's three complex logarithms; this is the regime of the alpha table's member leaves (arguments with
-// Im ~ Gamma_phi / m_phi).  Same algorithm as the oracle (ora_specfun.c ora_complex_dilog_xy).
+// Li2 about a real point x0 (x0 != 0, 1): the Taylor series in d = z - x0 (radius |1 - x0|, the distance to
+// the branch point),
+//   Li2(x0 + d) = sum_n c_n d^n,  c_n = Li2^(n)(x0) / n!,
+//   c_0 = Li2(x0) + i pi s log(x0) [x0 > 1],  c_1 = -log(1 - z) / z (log(1 - z) = log(x0 - 1) - i pi s for
+//   x0 > 1), c_{n+1} = (g^n / (n (n + 1)) - c_n n / (n + 1)) / x0 with g = 1 / (1 - x0)
+// (from z Li2'(z) = -log(1 - z)); s = +-1 is the side of the cut x0 > 1 the point x0 + d lies on.
+// Summed by Horner in d, truncated after kLi2AxisTerms: for |d| <= kLi2AxisRatio min(|x0|, |1 - x0|) the
+// remainder is below kLi2AxisRatio^7 ~ 1e-18 relative.  The coefficients are one real Li2 (whose
+// logarithms give log|1 - x0| and log x0) and two divisions; the evaluation is 6 complex fma steps.
+// Used (a) for arguments next to the real axis (cli2: x0 = Re z, d = i Im z), and (b) by the alpha table's
+// member leaves, whose arguments w = (1 + S + t) / (2 + t - i gr) all lie close to the real point
+// (1 + S + t) / (2 + t) that the points of a batch share: the coefficients are formed once per batch,
+// each point only evaluates.  Same algorithm as the oracle (ora_specfun.c ora_li2_taylor_*).
 constexpr int kLi2AxisTerms = 6;
 constexpr double kLi2AxisRatio = 2.5e-3;
-NUSI_FN cd cli2_axis(double x, double y)
+struct Li2Taylor {
+    double c[kLi2AxisTerms + 1];   // real parts of c_n
+    double r, b0;                  // 1 / x0 ; pi log(x0) for x0 > 1, else 0
+};
+NUSI_FN void li2_taylor_coeffs(double x0, Li2Taylor& T)
 {
     constexpr double kA[kLi2AxisTerms] = {0.0, 1.0 / 2, 1.0 / 6, 1.0 / 12, 1.0 / 20, 1.0 / 30};   // 1 / (n (n + 1))
     constexpr double kB[kLi2AxisTerms] = {0.0, 1.0 / 2, 2.0 / 3, 3.0 / 4, 4.0 / 5, 5.0 / 6};     // n / (n + 1)
-    double ar[kLi2AxisTerms + 1], ai[kLi2AxisTerms + 1];
-    const double r = 1.0 / x, g = 1.0 / (1.0 - x);
-    double L1m, Lx;   // log|1 - x|, log x (x > 1)
-    ar[0] = li2_ext(x, L1m, Lx);
-    ar[1] = -L1m * r;
-    if (x < 1.0) {
-        ai[0] = 0.0;
-        ai[1] = 0.0;
-    } else {
-        const double sp = copysign(kPi, y);
-        ai[0] = sp * Lx;
-        ai[1] = sp * r;
-    }
+    const double r = 1.0 / x0, g = 1.0 / (1.0 - x0);
+    double L1m, Lx;   // log|1 - x0|, log x0 (x0 > 1)
+    T.c[0] = li2_ext(x0, L1m, Lx);
+    T.c[1] = -L1m * r;
     double gn = g;
 #pragma unroll
     for (int n = 1; n < kLi2AxisTerms; ++n) {
-        ar[n + 1] = (gn * kA[n] - kB[n] * ar[n]) * r;
-        ai[n + 1] = -(kB[n] * ai[n]) * r;
+        T.c[n + 1] = (gn * kA[n] - kB[n] * T.c[n]) * r;
         gn = gn * g;
     }
-    double sr = ar[kLi2AxisTerms], si = ai[kLi2AxisTerms];
+    T.r = r;
+    T.b0 = (x0 > 1.0) ? kPi * Lx : 0.0;
+}
+NUSI_FN cd li2_taylor_eval(const Li2Taylor& T, double dr, double di, double side)
+{
+    constexpr double kB[kLi2AxisTerms] = {0.0, 1.0 / 2, 2.0 / 3, 3.0 / 4, 4.0 / 5, 5.0 / 6};
+    double b[kLi2AxisTerms + 1];   // imaginary parts of c_n (x0 > 1 only): b_1 = pi s / x0, b_{n+1} = -b_n n / (n + 1) / x0
+    b[0] = side * T.b0;
+    b[1] = (T.b0 != 0.0) ? side * kPi * T.r : 0.0;
+#pragma unroll
+    for (int n = 1; n < kLi2AxisTerms; ++n) b[n + 1] = -(kB[n] * b[n]) * T.r;
+    double sr = T.c[kLi2AxisTerms], si = b[kLi2AxisTerms];
 #pragma unroll
     for (int n = kLi2AxisTerms - 1; n >= 0; --n) {
-        const double tr = ar[n] - si * y, ti = ai[n] + sr * y;
+        const double tr = T.c[n] + (sr * dr - si * di), ti = b[n] + (sr * di + si * dr);
         sr = tr;
         si = ti;
     }
     return cd{sr, si};
+}
+// Li2(x + iy) close to the real axis, |y| <= kLi2AxisRatio min(|x|, |1 - x|)
+NUSI_FN cd cli2_axis(double x, double y)
+{
+    Li2Taylor T;
+    li2_taylor_coeffs(x, T);
+    return li2_taylor_eval(T, 0.0, y, y > 0.0 ? 1.0 : -1.0);
 }
 
 // principal-branch Li2(x+iy); y == 0 follows gsl_sf_complex_dilog_xy_e.  cli2_body is the inline body

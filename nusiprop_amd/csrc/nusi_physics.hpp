@@ -473,21 +473,73 @@ NUSI_FN void alpha_corner_shared(double S, double t, AlphaCorner& c)
     c.Drr = Dr.r;
     c.Dri = Dr.i;
 }
-// The member leaves (nuSIprop.hpp:1444-1451, 1456-1459) for dt = 2 + t - i gr:
-//   Dc = Li2(w), w = (1 + S + t) / dt = a (c + i gr) / (c^2 + gr^2), a = 1 + S + t, c = 2 + t  (one division),
-//   A  = arg(-(-1 + i gr + S) / dt) = atan2 of -(S - 1 + i gr)(c + i gr) = (-((S - 1) c - gr^2), -gr a)
-//        (dividing by |dt|^2 > 0 does not change the argument: no division).
-// The oracle forms them the same way (nusi_oracle.c member_w / member_arg).
+// The member leaves of the s-t interference (nuSIprop.hpp:1444-1451, 1456-1459), dt = 2 + t - i gr:
+//   Dc = Li2(w), w = (1 + S + t) / dt = a (c + i gr) / (c^2 + gr^2), a = 1 + S + t, c = 2 + t;
+//   A  = arg(-(-1 + i gr + S) / dt) = arg(S - 1 + i gr) + arg(c + i gr) - pi   (both arguments lie in
+//        (0, pi), and Im(-(S - 1 + i gr)(c + i gr)) = -gr a < 0 puts A in (-pi, 0): no wrap).
+// w lies within gr / |c| (relative) of the real point x0 = a / c, which does not depend on gr: the Taylor
+// coefficients of Li2 about x0 are formed once per corner for every point of a batch (alpha_member_shared),
+// and a point only evaluates them at d = w - x0 = i (gr / c) w (li2_taylor_eval); a w outside the
+// expansion's radius takes the general cli2.  Each argument is written as f pi + s with s the small angle
+// where the argument is near 0 or pi (edge leaves), so A = (sS + sT) + (fS + fT - 1) pi keeps full
+// relative accuracy where it is small.  The oracle forms them the same way (nusi_oracle.c member_*).
+struct MemberShared {
+    Li2Taylor T;
+    double m;   // kLi2AxisRatio min(|x0|, |1 - x0|): the radius used (0: no expansion)
+};
+NUSI_FN void alpha_member_shared(double S, double t, MemberShared& M)
+{
+    const double a = 1 + S + t, c = 2 + t;
+    const double x0 = a / c;
+    const double ax = fabs(x0), a1 = fabs(1.0 - x0);
+    if (c != 0.0 && a1 > 0.0 && ax < 1e300) {
+        li2_taylor_coeffs(x0, M.T);
+        M.m = kLi2AxisRatio * (ax < a1 ? ax : a1);
+    } else {
+        for (int n = 0; n <= kLi2AxisTerms; ++n) M.T.c[n] = 0.0;
+        M.T.r = M.T.b0 = 0.0;
+        M.m = 0.0;
+    }
+}
+// member t-edge leaves of coupling gr: inv = 1 / (c^2 + gr^2), q = gr / c, arg(c + i gr) = fT pi + sT
+struct MemberTEdge { double inv, q, sT, fT; };
+NUSI_FN MemberTEdge alpha_member_tedge(double t, double gr)
+{
+    const double c = 2 + t;
+    MemberTEdge e;
+    e.inv = 1.0 / (c * c + gr * gr);
+    e.q = gr / c;
+    if (c < 0.0) { e.sT = -nm::atan2_i(gr, -c); e.fT = 1.0; }
+    else { e.sT = nm::atan2_i(gr, c); e.fT = 0.0; }
+    return e;
+}
+// member S'-edge leaves: arg(S - 1 + i gr) = fS pi + sS
+NUSI_FN void alpha_member_sarg(double S, double gr, double& sS, double& fS)
+{
+    if (S < 1.0) { sS = -nm::atan2_i(gr, 1.0 - S); fS = 1.0; }
+    else { sS = nm::atan2_i(gr, S - 1.0); fS = 0.0; }
+}
+// Dc and A of corner (S, t) for coupling gr from the shared coefficients and the edge leaves
+NUSI_FN void alpha_member_corner(const MemberShared& M, double S, double t, double gr, const MemberTEdge& e, double sS,
+                                 double fS, double& Dcr, double& Dci, double& A)
+{
+    const double a = 1 + S + t, c = 2 + t;
+    const double wr = (a * c) * e.inv, wi = (a * gr) * e.inv;
+    const double dr = -(e.q * wi), di = e.q * wr;
+    const cd Dc = (dr * dr + di * di <= M.m * M.m) ? li2_taylor_eval(M.T, dr, di, 1.0) : cli2(wr, wi);
+    Dcr = Dc.r;
+    Dci = Dc.i;
+    A = (sS + e.sT) + (fS + e.fT - 1.0) * kPi;
+}
 template <bool kInlineCli2 = false>
 NUSI_FN void alpha_corner_member(double S, double t, double gr, AlphaCorner& c)
 {
-    const double a = 1 + S + t, cr = 2 + t;
-    const double inv = 1.0 / (cr * cr + gr * gr);
-    const double wr = (a * cr) * inv, wi = (a * gr) * inv;
-    const cd Dc = kInlineCli2 ? cli2_body(wr, wi) : cli2(wr, wi);
-    c.Dcr = Dc.r;
-    c.Dci = Dc.i;
-    c.A = nm::atan2_i(-(gr * a), -((S - 1) * cr - gr * gr));
+    MemberShared M;
+    alpha_member_shared(S, t, M);
+    const MemberTEdge e = alpha_member_tedge(t, gr);
+    double sS, fS;
+    alpha_member_sarg(S, gr, sS, fS);
+    alpha_member_corner(M, S, t, gr, e, sS, fS, c.Dcr, c.Dci, c.A);
 }
 NUSI_FN void alpha_corner(double S, double t, double gr, AlphaCorner& c)
 {
@@ -637,14 +689,13 @@ NUSI_FN double* alpha_tile_member_block(double* edg, int cs, int ct, int G, int 
 }
 // job in [0, 3 (ct + cs + kAlphaTile)): the shared edge / m-bin leaves of one mass state (P: any
 // point of the tile's batch -- they read m_phi and the masses only)
-NUSI_FN void alpha_tile_edge_job(const Point& P, int job, const double* tE, int ct, const double* sE, int cs,
-                                 const double* lo, const double* hi, int m0, int T, double* edg)
+// job j in [0, ct + cs + kAlphaTile) of mass state k into that state's edge block edgk
+NUSI_FN void alpha_tile_edge_job_k(const Point& P, int k, int j, const double* tE, int ct, const double* sE, int cs,
+                                   const double* lo, const double* hi, int m0, int T, double* edgk)
 {
     const double mphi = P.mphi, m2 = mphi * mphi;
-    const int per = ct + cs + kAlphaTile;
-    const int k = job / per, j = job - k * per;
     const double mk = P.mn[k];
-    double* ted = edg + k * alpha_tile_edge_stride(cs, ct);
+    double* ted = edgk;
     double* sed = ted + kTEdgeFields * ct;
     double* mbv = sed + kSEdgeFields * cs;
     if (j < ct) {
@@ -669,6 +720,13 @@ NUSI_FN void alpha_tile_edge_job(const Point& P, int job, const double* tE, int 
         mbv[q] = nm::log(Sm / Sp);
         mbv[kAlphaTile + q] = nm::log(Sp / Sm);
     }
+}
+NUSI_FN void alpha_tile_edge_job(const Point& P, int job, const double* tE, int ct, const double* sE, int cs,
+                                 const double* lo, const double* hi, int m0, int T, double* edg)
+{
+    const int per = ct + cs + kAlphaTile;
+    const int k = job / per;
+    alpha_tile_edge_job_k(P, k, job - k * per, tE, ct, sE, cs, lo, hi, m0, T, edg + k * alpha_tile_edge_stride(cs, ct));
 }
 // job in [0, 3 (ct + cs + kAlphaTile)): the member edge / m-bin leaves of point P (slot m of the
 // batch); t and S' are recomputed (the same expression), so no barrier orders it after the shared jobs
@@ -829,13 +887,17 @@ NUSI_FN double alpha_phiphi_scale(const Point& P, double uk, const PPTerm& X)
 struct SplitLeaves {
     const double* cf[kCornerShared];   // L LL TU1 TU2 G Drr Dri, each [cc]
     const double *corm, *ted, *sed, *mbv, *tedm, *sedm, *mbm, *xl, *yl;
+    const double* marg;                // sT [ct] | fT [ct] | sS [cs] | fS [cs]: A from the edge arguments
     int cc, ct, cs, mb, nb;
     int sidx[2], tidx[2];
     NUSI_FN AlphaCorner corner(int si, int ti, double, double) const
     {
         const int o = sidx[si] * ct + tidx[ti];
+        const int a = sidx[si], b = tidx[ti];
+        // A = arg(S - 1 + i gr) + arg(c + i gr) - pi, the expression of alpha_member_corner
+        const double A = (marg[2 * ct + a] + marg[b]) + (marg[2 * ct + cs + a] + marg[ct + b] - 1.0) * kPi;
         return AlphaCorner{cf[0][o], cf[1][o], cf[2][o], cf[3][o], cf[4][o], cf[5][o], cf[6][o],
-                           corm[o], corm[cc + o], corm[2 * cc + o]};
+                           corm[o], corm[cc + o], A};
     }
     NUSI_FN AlphaTEdge tedge(int ti, double) const
     {
@@ -863,18 +925,72 @@ NUSI_FN void alpha_batch_corner_job(int j, const double* edgk, int ct, int cs, d
     per[j] = c.L; per[cc + j] = c.Drr; per[2 * cc + j] = c.Dri;
     tmp[j] = c.LL; tmp[cc + j] = c.TU1; tmp[2 * cc + j] = c.TU2; tmp[3 * cc + j] = c.G;
 }
-#ifndef NUSI_BATCH_INLINE_CLI2   // 1: the big-batch kernel's member job inlines the complex dilogarithm
-#define NUSI_BATCH_INLINE_CLI2 0   // (A/B: 10.02 vs 9.96 ms alpha stage at C4, profiles/r2/ab4) -- kept out of line
-#endif
-// member corner leaves of corner j for point P -> mem[0..2][cc] (Dcr, Dci, A)
-NUSI_FN void alpha_batch_member_job(const Point& P, int j, const double* edgk, int ct, int cs, double* mem)
+// The big-batch kernel's member blocks, per (point, mass state):
+//   X    [10][cc]  shared across the batch: the Taylor coefficients of Li2 about x0 = (1+S+t)/(2+t) per corner
+//                  (c_0..c_6, 1/x0, pi log x0, the radius bound m), alpha_batch_xshared_job
+//   memb [5 ct + 4 cs + kAlphaTile]  the point's edge leaves: L2 [ct] | Ls [cs] | cS [cs] | atd [kAlphaTile] |
+//                  inv [ct] | q [ct] | sT [ct] | fT [ct] | sS [cs] | fS [cs]   (the first four as TileLeaves reads them)
+//   mem  [2][cc]   the point's corner leaves Dcr, Dci (A = sum of the edge arguments, formed where read)
+constexpr int kXFields = kLi2AxisTerms + 4;
+NUSI_FN int alpha_batch_memb_doubles(int cs, int ct) { return 5 * ct + 4 * cs + kAlphaTile; }
+NUSI_FN void alpha_batch_xshared_job(int j, const double* edgk, int ct, int cs, double* X)
 {
     const int cc = cs * ct;
     const int si = j / ct, ti = j - si * ct;
-    AlphaCorner c;
-    alpha_corner_member<NUSI_BATCH_INLINE_CLI2>(edgk[kTEdgeFields * ct + kSEdgeVal * cs + si], edgk[kTEdgeVal * ct + ti],
-                                                P.a_gr, c);
-    mem[j] = c.Dcr; mem[cc + j] = c.Dci; mem[2 * cc + j] = c.A;
+    MemberShared M;
+    alpha_member_shared(edgk[kTEdgeFields * ct + kSEdgeVal * cs + si], edgk[kTEdgeVal * ct + ti], M);
+#pragma unroll
+    for (int n = 0; n <= kLi2AxisTerms; ++n) X[n * cc + j] = M.T.c[n];
+    X[(kLi2AxisTerms + 1) * cc + j] = M.T.r;
+    X[(kLi2AxisTerms + 2) * cc + j] = M.T.b0;
+    X[(kLi2AxisTerms + 3) * cc + j] = M.m;
+}
+// job in [0, ct + cs + kAlphaTile): the member edge / m-bin leaves of point P for mass state k
+NUSI_FN void alpha_batch_medge_job(const Point& P, int k, int job, const double* tE, int ct, const double* sE, int cs,
+                                   const double* lo, const double* hi, int m0, int Tm, double* memb)
+{
+    const double mphi = P.mphi, Ga = P.Ga, m2 = mphi * mphi, gr = P.a_gr, gr2 = gr * gr, mk = P.mn[k];
+    double* ext = memb + ct + 2 * cs + kAlphaTile;   // inv | q | sT | fT | sS | fS
+    if (job < ct) {
+        if (!P.non_resonant) return;
+        const double t = alpha_t(mk, tE[job], m2);
+        memb[job] = alpha_tedge_L2(t, gr2);
+        const MemberTEdge e = alpha_member_tedge(t, gr);
+        ext[job] = e.inv; ext[ct + job] = e.q; ext[2 * ct + job] = e.sT; ext[3 * ct + job] = e.fT;
+    } else if (job < ct + cs) {
+        if (!P.non_resonant) return;
+        const int q = job - ct;
+        const double S = alpha_S(mk, sE[q], m2);
+        AlphaSEdge e;
+        alpha_sedge_member(S, gr, gr2, e);
+        memb[ct + q] = e.Ls;
+        memb[ct + cs + q] = e.cS;
+        alpha_member_sarg(S, gr, ext[4 * ct + q], ext[4 * ct + cs + q]);
+    } else {
+        const int q = job - ct - cs;
+        if (m0 + q >= Tm) return;
+        memb[ct + 2 * cs + q] = alpha_mbin_atd(alpha_S(mk, lo[m0 + q], m2), alpha_S(mk, hi[m0 + q], m2), mphi, Ga);
+    }
+}
+// member corner leaves of corner j for point P -> mem[0..2][cc] (Dcr, Dci, A); edgk: the shared edge block of
+// mass state k (its t and S' values)
+NUSI_FN void alpha_batch_mcorner_job(const Point& P, int j, const double* edgk, int ct, int cs, const double* X,
+                                     const double* memb, double* mem)
+{
+    const int cc = cs * ct;
+    const int si = j / ct, ti = j - si * ct;
+    MemberShared M;
+#pragma unroll
+    for (int n = 0; n <= kLi2AxisTerms; ++n) M.T.c[n] = X[n * cc + j];
+    M.T.r = X[(kLi2AxisTerms + 1) * cc + j];
+    M.T.b0 = X[(kLi2AxisTerms + 2) * cc + j];
+    M.m = X[(kLi2AxisTerms + 3) * cc + j];
+    const double* ext = memb + ct + 2 * cs + kAlphaTile;
+    const MemberTEdge e{ext[ti], ext[ct + ti], ext[2 * ct + ti], ext[3 * ct + ti]};
+    double Dcr, Dci, A;
+    alpha_member_corner(M, edgk[kTEdgeFields * ct + kSEdgeVal * cs + si], edgk[kTEdgeVal * ct + ti], P.a_gr, e,
+                        ext[4 * ct + si], ext[4 * ct + cs + si], Dcr, Dci, A);
+    mem[j] = Dcr; mem[cc + j] = Dci;   // (A: SplitLeaves forms it from the edge arguments)
 }
 // xlog / ylog leaves of mass state k into xl [cs][kAlphaTile], yl [kAlphaTile][ct] (alpha_tile_mixed_job's jobs)
 NUSI_FN void alpha_batch_mixed_job(int j, const double* edgk, int ct, int cs, const int* tl, const int* th,

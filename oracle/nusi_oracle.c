@@ -471,20 +471,35 @@ double ora_alphaTilde(ora_state *S, double Em, double Ep)   /* nuSIprop.hpp:924-
     return tot;
 }
 
-/* The s-t interference's g-dependent pieces (nuSIprop.hpp:1440-1459) for dt = 2 + t - i gr:
- * (1 + S + t) / dt = a (c + i gr) / (c^2 + gr^2) with a = 1 + S + t, c = 2 + t (one division), and
- * arg(-(-1 + i gr + S) / dt) as the atan2 of -(S - 1 + i gr)(c + i gr) (the positive |dt|^2 dropped).
- * The GPU forms them the same way (nusi_physics.hpp alpha_corner_member). */
-static zc member_w(double S, double t, double gr)
+/* The s-t interference's g-dependent pieces (nuSIprop.hpp:1440-1459), dt = 2 + t - i gr, a = 1 + S + t,
+ * c = 2 + t:  Li2(w), w = a / dt = a (c + i gr) / (c^2 + gr^2), by the Taylor series about the real point
+ * x0 = a / c at d = w - x0 = i (gr / c) w when |d| <= 2.5e-3 min(|x0|, |1 - x0|), else the general complex
+ * dilog; and arg(-(-1 + i gr + S) / dt) = arg(S - 1 + i gr) + arg(c + i gr) - pi, each argument written as
+ * f pi + s with s the small angle.  The GPU forms them the same way (nusi_physics.hpp alpha_member_*). */
+static void member_dc(double S, double t, double gr, double *re, double *im)
 {
     const double a = 1 + S + t, c = 2 + t;
-    const double inv = 1.0 / (c * c + gr * gr);
-    return zmk((a * c) * inv, (a * gr) * inv);
+    const double x0 = a / c;
+    const double ax = fabs(x0), a1 = fabs(1.0 - x0);
+    ora_li2t T;
+    double m = 0.0;
+    if (c != 0.0 && a1 > 0.0 && ax < 1e300) {
+        ora_li2_taylor_coeffs(x0, &T);
+        m = ORA_LI2T_RATIO * (ax < a1 ? ax : a1);
+    }
+    const double inv = 1.0 / (c * c + gr * gr), q = gr / c;
+    const double wr = (a * c) * inv, wi = (a * gr) * inv;
+    const double dr = -(q * wi), di = q * wr;
+    if (dr * dr + di * di <= m * m) ora_li2_taylor_eval(&T, dr, di, 1.0, re, im);
+    else ora_complex_dilog_xy(wr, wi, re, im);
 }
 static double member_arg(double S, double t, double gr)
 {
-    const double a = 1 + S + t, c = 2 + t;
-    return ora_atan2(-(gr * a), -((S - 1) * c - gr * gr));
+    const double c = 2 + t;
+    double sS, fS, sT, fT;
+    if (S < 1.0) { sS = -ora_atan2(gr, 1.0 - S); fS = 1.0; } else { sS = ora_atan2(gr, S - 1.0); fS = 0.0; }
+    if (c < 0.0) { sT = -ora_atan2(gr, -c); fT = 1.0; } else { sT = ora_atan2(gr, c); fT = 0.0; }
+    return (sS + sT) + (fS + fT - 1.0) * M_PI;
 }
 
 double ora_alpha(ora_state *S, double Em, double Ep, double Emp, double Epp)   /* nuSIprop.hpp:1237-1520 */
@@ -589,22 +604,18 @@ double ora_alpha(ora_state *S, double Em, double Ep, double Emp, double Epp)   /
 
         /* s-t interference: 8 GSL complex dilogs (nuSIprop.hpp:1431-1451) */
         const double z1 = (1 + Sm + tm) / (1 + tm);
-        const zc z2 = member_w(Sm, tm, gr);
         const double z3 = (1 + Sp + tm) / (1 + tm);
-        const zc z4 = member_w(Sp, tm, gr);
         const double z5 = (1 + Sm + tp) / (1 + tp);
-        const zc z6 = member_w(Sm, tp, gr);
         const double z7 = (1 + Sp + tp) / (1 + tp);
-        const zc z8 = member_w(Sp, tp, gr);
         double R[9], J[9];
         ora_complex_dilog_xy(z1, 0, &R[1], &J[1]);
-        ora_complex_dilog_xy(z2.r, z2.i, &R[2], &J[2]);
+        member_dc(Sm, tm, gr, &R[2], &J[2]);   /* (1+Sm+tm)/(2 - I gr + tm) */
         ora_complex_dilog_xy(z3, 0, &R[3], &J[3]);
-        ora_complex_dilog_xy(z4.r, z4.i, &R[4], &J[4]);
+        member_dc(Sp, tm, gr, &R[4], &J[4]);
         ora_complex_dilog_xy(z5, 0, &R[5], &J[5]);
-        ora_complex_dilog_xy(z6.r, z6.i, &R[6], &J[6]);
+        member_dc(Sm, tp, gr, &R[6], &J[6]);
         ora_complex_dilog_xy(z7, 0, &R[7], &J[7]);
-        ora_complex_dilog_xy(z8.r, z8.i, &R[8], &J[8]);
+        member_dc(Sp, tp, gr, &R[8], &J[8]);
         const double Lsm = ora_log1p(SQ(-1 + Sm) / SQ(gr)), Lsp = ora_log1p(SQ(-1 + Sp) / SQ(gr));
         double ast;
         if (maj) {

@@ -84,44 +84,53 @@ static double dilog_ext(double x, double *L1m, double *Lx)
     return add + sgn * li2_useries(-l1);
 }
 
-/* Li2(x + iy) for |y| <= AXIS_RATIO min(|x|, |1 - x|): Taylor series in iy about x + i0 sign(y)
- * (radius |1 - x|): c_0 = Li2(x) + i pi sign(y) log x [x > 1], c_1 = -log(1 - z)/z, c_{n+1} =
- * (g^n/(n(n+1)) - c_n n/(n+1))/x with g = 1/(1 - x) (from z Li2'(z) = -log(1 - z)), Horner in iy,
- * AXIS_TERMS + 1 terms (remainder < AXIS_RATIO^7 ~ 1e-18 relative).  The GPU runs the same sequence
- * (nusi_math.hpp cli2_axis); pinned by the mpmath KATs (tests/test_specfun.py). */
-#define AXIS_TERMS 6
-static const double AXIS_RATIO = 2.5e-3;
-static void cdilog_axis(double x, double y, double *re, double *im)
+/* Li2 about a real point x0 != 0, 1: Taylor series in d = z - x0 (radius |1 - x0|), c_0 = Li2(x0) +
+ * i pi s log x0 [x0 > 1], c_1 = -log(1 - z)/z, c_{n+1} = (g^n/(n(n+1)) - c_n n/(n+1))/x0 with g = 1/(1 - x0)
+ * (from z Li2'(z) = -log(1 - z)), s = +-1 the side of the cut x0 > 1, Horner in d, AXIS_TERMS + 1 terms
+ * (remainder < AXIS_RATIO^7 ~ 1e-18 relative for |d| <= AXIS_RATIO min(|x0|, |1 - x0|)).  Used near the
+ * real axis (d = i y) and for the alpha table's member leaves (nusi_oracle.c member_dc).  The GPU runs the
+ * same sequence (nusi_math.hpp li2_taylor_*); pinned by the mpmath KATs (tests/test_specfun.py). */
+#define AXIS_TERMS ORA_LI2T_TERMS
+static const double AXIS_RATIO = ORA_LI2T_RATIO;
+static const double kA_[AXIS_TERMS] = {0.0, 1.0 / 2, 1.0 / 6, 1.0 / 12, 1.0 / 20, 1.0 / 30};
+static const double kB_[AXIS_TERMS] = {0.0, 1.0 / 2, 2.0 / 3, 3.0 / 4, 4.0 / 5, 5.0 / 6};
+
+void ora_li2_taylor_coeffs(double x0, ora_li2t *T)
 {
-    static const double kA[AXIS_TERMS] = {0.0, 1.0 / 2, 1.0 / 6, 1.0 / 12, 1.0 / 20, 1.0 / 30};
-    static const double kB[AXIS_TERMS] = {0.0, 1.0 / 2, 2.0 / 3, 3.0 / 4, 4.0 / 5, 5.0 / 6};
-    double ar[AXIS_TERMS + 1], ai[AXIS_TERMS + 1];
-    const double r = 1.0 / x, g = 1.0 / (1.0 - x);
+    const double r = 1.0 / x0, g = 1.0 / (1.0 - x0);
     double L1m, Lx;
-    ar[0] = dilog_ext(x, &L1m, &Lx);
-    ar[1] = -L1m * r;
-    if (x < 1.0) {
-        ai[0] = 0.0;
-        ai[1] = 0.0;
-    } else {
-        const double sp = copysign(PI_D, y);
-        ai[0] = sp * Lx;
-        ai[1] = sp * r;
-    }
+    T->c[0] = dilog_ext(x0, &L1m, &Lx);
+    T->c[1] = -L1m * r;
     double gn = g;
     for (int n = 1; n < AXIS_TERMS; ++n) {
-        ar[n + 1] = (gn * kA[n] - kB[n] * ar[n]) * r;
-        ai[n + 1] = -(kB[n] * ai[n]) * r;
+        T->c[n + 1] = (gn * kA_[n] - kB_[n] * T->c[n]) * r;
         gn = gn * g;
     }
-    double sr = ar[AXIS_TERMS], si = ai[AXIS_TERMS];
+    T->r = r;
+    T->b0 = (x0 > 1.0) ? PI_D * Lx : 0.0;
+}
+
+void ora_li2_taylor_eval(const ora_li2t *T, double dr, double di, double side, double *re, double *im)
+{
+    double b[AXIS_TERMS + 1];
+    b[0] = side * T->b0;
+    b[1] = (T->b0 != 0.0) ? side * PI_D * T->r : 0.0;
+    for (int n = 1; n < AXIS_TERMS; ++n) b[n + 1] = -(kB_[n] * b[n]) * T->r;
+    double sr = T->c[AXIS_TERMS], si = b[AXIS_TERMS];
     for (int n = AXIS_TERMS - 1; n >= 0; --n) {
-        const double tr = ar[n] - si * y, ti = ai[n] + sr * y;
+        const double tr = T->c[n] + (sr * dr - si * di), ti = b[n] + (sr * di + si * dr);
         sr = tr;
         si = ti;
     }
     *re = sr;
     *im = si;
+}
+
+static void cdilog_axis(double x, double y, double *re, double *im)
+{
+    ora_li2t T;
+    ora_li2_taylor_coeffs(x, &T);
+    ora_li2_taylor_eval(&T, 0.0, y, y > 0.0 ? 1.0 : -1.0, re, im);
 }
 
 void ora_complex_dilog_xy(double x, double y, double *re, double *im)

@@ -32,6 +32,13 @@ extern "C" {
 
 double ora_dilog(double x);                                  /* gsl_sf_dilog */
 void ora_complex_dilog_xy(double x, double y, double *re, double *im);
+/* Li2 about a real point x0 (x0 != 0, 1): coefficients and evaluation at x0 + (dr + i di) on the side
+ * `side` (+-1) of the cut x0 > 1; |d| <= ORA_LI2T_RATIO min(|x0|, |1 - x0|) */
+#define ORA_LI2T_TERMS 6
+#define ORA_LI2T_RATIO 2.5e-3
+typedef struct { double c[ORA_LI2T_TERMS + 1]; double r, b0; } ora_li2t;
+void ora_li2_taylor_coeffs(double x0, ora_li2t *T);
+void ora_li2_taylor_eval(const ora_li2t *T, double dr, double di, double side, double *re, double *im);
 double ora_li2(double x);                                    /* polylogarithm::Li2 */
 double ora_li3(double x);                                    /* polylogarithm::Li3, x in [-1,0.5] */
 /* long-double yardsticks (tests only) */
