@@ -9,12 +9,14 @@ its own tables) per GPU; with N GPUs each rank evolves its own 1024 points
 (weak scaling, gamma shifted per rank so every rank's points are distinct), no
 collective on the data path.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c4|c5|c2] [--points P]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c4|c5|c3|c2|c1] [--points P]
 Multi-GPU: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 
 Prints one JSON line (rank 0) with roofline (the dominant alpha-table kernel, fp64 VALU),
-roofline_cascade (the metric's cascade HBM GB/s) and the
-cpu_baseline (the C oracle, single thread, bounded sample).
+roofline_cascade (the metric's cascade HBM GB/s) and the cpu_baseline (the C oracle on a
+thread pool over the host cores the job may use, bounded sample, Stage A / Stage B timed
+apart on one core).  c2 / c1 (single propagations) add the latency of one evolve() through
+the object API (nusi_evolve, host I/O included) beside the 1-point plan's device-resident rate.
 """
 import argparse
 import json
@@ -35,7 +37,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--workload", default="c4", choices=["c4", "c5", "c2", "c3"])
+    ap.add_argument("--workload", default="c4", choices=["c4", "c5", "c3", "c2", "c1"])
     ap.add_argument("--points", type=int, default=0, help="points per GPU (default: 1024 for c4 and c3, 8192 for c5, 1 for c2)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="budget of the oracle CPU baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -53,6 +55,9 @@ def rank_points(args, rank, world):
     if args.workload == "c2":
         pts = [dict(scan.BASE, mphi=6e5, g=0.01, si=2.5, norm=6.0)]
         return pts * max(1, args.points or 1), "C2b: single propagation, N_E=300, lE 12->17, power-law source, test.cpp physics"
+    if args.workload == "c1":   # test.cpp:6-23 verbatim (N_E = 100, lE 9 -> 14, DSNB source)
+        pts = [dict(scan.C1)]
+        return pts * max(1, args.points or 1), "C1: test.cpp single propagation (N_E=100, lE 9->14, DSNB source, phiphi off)"
     import numpy as np
     if args.workload == "c3":   # BASELINE config 3: N_E = 1200, lE 10 -> 17, phi-phi on (synthetic tables)
         P = args.points or 1024
@@ -77,22 +82,128 @@ def rank_points(args, rank, world):
     return pts[:P], desc
 
 
+def host_cores():
+    """Threads the job may use on this host: the affinity mask, capped by OMP_NUM_THREADS when it is set (the
+    GPU box sets it to its CPU share), plus what the machine reports."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = os.cpu_count() or 1
+    cap = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    model = ""
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return (min(aff, cap) if cap > 0 else aff), {"nproc": os.cpu_count(), "affinity": aff,
+                                                   "OMP_NUM_THREADS": cap or None, "cpu_model": model}
+
+
+def _oracle(p):
+    from oracle import oracle
+    kw = dict(p)
+    kw["source"] = kw.pop("source_model")
+    return oracle.Oracle(**kw)
+
+
 def cpu_baseline(pts, budget_s):
-    """The C oracle (single thread) on the first points of the same workload until the budget is spent."""
+    """The C oracle (test infrastructure, the reference's algorithm restated) on a bounded sample of the same
+    workload: Stage A (tables) and Stage B (cascade) timed apart on one core for a quarter of the budget, then
+    whole evolve()s on a thread pool over the host cores for the rest (ctypes releases the GIL, the oracle has
+    no global state).  value = the pool's propagations/s."""
+    import concurrent.futures as cf
+    import threading
     from oracle import oracle
     oracle.build()
-    n, t0 = 0, time.perf_counter()
+    threads, host = host_cores()
+    # one core, stages apart
+    ta = tb = 0.0
+    n1, t0 = 0, time.perf_counter()
     for p in pts:
-        kw = dict(p)
-        kw["source"] = kw.pop("source_model")
-        o = oracle.Oracle(**kw)
-        o.evolve()
-        n += 1
-        if time.perf_counter() - t0 > budget_s:
+        o = _oracle(p)
+        t1 = time.perf_counter()
+        G, At, A = o.tables()
+        t2 = time.perf_counter()
+        o.cascade(G, At, A)
+        t3 = time.perf_counter()
+        ta += t2 - t1
+        tb += t3 - t2
+        n1 += 1
+        if t3 - t0 > budget_s / 4:
             break
+    # the pool: worker k evolves points k, k + threads, ... until the deadline
+    deadline = time.perf_counter() + budget_s * 3 / 4
+    done = [0] * threads
+    lock = threading.Lock()
+
+    def work(k):
+        i = k
+        while time.perf_counter() < deadline:
+            _oracle(pts[i % len(pts)]).evolve()
+            with lock:
+                done[k] += 1
+            i += threads
+    t0 = time.perf_counter()
+    with cf.ThreadPoolExecutor(threads) as ex:
+        list(ex.map(work, range(threads)))
     dt = time.perf_counter() - t0
-    return {"value": n / dt, "unit": "propagations/s", "cores": 1, "kind": "port",
-            "sample": "%d full propagations (first points of the same workload), single-threaded C oracle, %.1f s" % (n, dt)}
+    n = sum(done)
+    return {"value": n / dt, "unit": "propagations/s", "cores": threads, "kind": "port",
+            "sample": "%d full propagations of the same workload (points cycled from the first) on a %d-thread pool "
+                      "of the single-threaded C oracle, %.1f s" % (n, threads, dt),
+            "host": host,
+            "single_core": {"propagations": n1, "value": n1 / (ta + tb), "stage_a_ms_per_prop": ta / n1 * 1e3,
+                            "stage_b_ms_per_prop": tb / n1 * 1e3,
+                            "note": "Stage A = Gamma/alphaTilde/alpha tables (nuSIprop.hpp:217-253), Stage B = "
+                                    "cascade + finalise (:255-336), first points of the workload, one thread"}}
+
+
+def c1_cpu_lines(budget_s):
+    """test.cpp (C1) on the oracle at its own N_E = 100 and at N_E = 300 (lE 9 -> 14), one core each."""
+    from nusiprop_amd import scan
+    out = {}
+    for N in (100, 300):
+        p = dict(scan.C1, N_bins_E=N)
+        n, t0 = 0, time.perf_counter()
+        while True:
+            _oracle(p).evolve()
+            n += 1
+            if time.perf_counter() - t0 > budget_s:
+                break
+        dt = time.perf_counter() - t0
+        out["N_E=%d" % N] = {"ms_per_prop": dt / n * 1e3, "propagations": n, "cores": 1}
+    return out
+
+
+def single_point_latency(pt, reps):
+    """One evolve() through the object API (nusi_create / nusi_evolve: host parameters in, tables and cascade
+    on the GPU, fluxes copied to the host) -- the reference's own usage, calculate_flux::evolve() per object."""
+    import ctypes
+    from nusiprop_amd import _lib
+    L = _lib.load()
+    p = dict(pt)
+    src = p.pop("source_model")
+    h = ctypes.c_void_p()
+    _lib.check(L.nusi_create(ctypes.byref(_lib.make_params(source_model=src, **p)), ctypes.byref(h)))
+    try:
+        out = (ctypes.c_double * (3 * p["N_bins_E"]))()
+        for _ in range(3):
+            _lib.check(L.nusi_evolve(h))
+        ts = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            _lib.check(L.nusi_evolve(h))
+            _lib.check(L.nusi_get_flux_fla(h, out))
+            ts.append(time.perf_counter() - t0)
+    finally:
+        L.nusi_destroy(h)
+    ts.sort()
+    return {"median_ms": ts[len(ts) // 2] * 1e3, "min_ms": ts[0] * 1e3, "reps": reps,
+            "path": "nusi_create + nusi_evolve + nusi_get_flux_fla (object API, host I/O and sync included)"}
 
 
 def main():
@@ -230,8 +341,13 @@ def main():
                                    "(transcendental leaves), neither HBM nor MFMA"}
     else:
         out["roofline"] = dict(out["roofline_cascade"])
+    if args.workload in ("c1", "c2") and rank == 0:
+        out["single_propagation"] = single_point_latency(pts[0], max(20, args.steps))
+        out["single_propagation"]["plan_ms_per_step"] = dt / args.steps * 1e3
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(pts, args.cpu_seconds)
+        if args.workload == "c1":
+            out["cpu_baseline"]["c1_test_cpp"] = c1_cpu_lines(min(5.0, args.cpu_seconds / 3))
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist is not None:

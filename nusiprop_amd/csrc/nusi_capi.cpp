@@ -355,6 +355,8 @@ struct nusi_plan {
     nusi::Point* h_pts = nullptr;  // pinned
     nusi::Point* d_tpts = nullptr;  // one representative per distinct table (table kernels)
     nusi::Point* h_tpts = nullptr;  // pinned
+    int2* d_groups = nullptr;       // multi-RHS cascade: pairs of points sharing a table slot
+    int2* h_groups = nullptr;       // pinned
     int* d_batches = nullptr;       // alpha-table batches (nusi::launch_alpha): first table | count << 24
     int* h_batches = nullptr;       // pinned
     int alpha_batch = 0;            // max tables per batch; 0 = auto (alpha_batch_cap); NUSI_ALPHA_BATCH overrides
@@ -497,6 +499,8 @@ void nusi_plan_destroy(nusi_plan* pl)
     hipFree(pl->d_tpts);
     if (pl->h_tpts) hipHostFree(pl->h_tpts);
     hipFree(pl->d_batches);
+    hipFree(pl->d_groups);
+    if (pl->h_groups) hipHostFree(pl->h_groups);
     if (pl->h_batches) hipHostFree(pl->h_batches);
     hipFree(pl->d_warn);
     hipFree(pl->tabs.G);
@@ -572,6 +576,8 @@ int nusi_plan_create(int device, int N_bins_E, double lEmin, double lEmax, doubl
     HIPCHECK(hipMalloc(&pl->d_tpts, sizeof(nusi::Point) * max_points));
     HIPCHECK(hipHostMalloc((void**)&pl->h_tpts, sizeof(nusi::Point) * max_points, hipHostMallocDefault));
     HIPCHECK(hipMalloc(&pl->d_batches, sizeof(int) * max_points));
+    HIPCHECK(hipMalloc(&pl->d_groups, sizeof(int2) * max_points));
+    HIPCHECK(hipHostMalloc((void**)&pl->h_groups, sizeof(int2) * max_points, hipHostMallocDefault));
     HIPCHECK(hipHostMalloc((void**)&pl->h_batches, sizeof(int) * max_points, hipHostMallocDefault));
     if (const char* e = getenv("NUSI_ALPHA_KERNEL")) pl->alpha_tile_kernel = e[0] == 't';
     if (const char* e = getenv("NUSI_ALPHA_BATCH")) pl->alpha_batch = std::max(1, std::min(pl->alpha_tile_kernel ? 4 : 255, atoi(e)));
@@ -691,6 +697,28 @@ int nusi_plan_evolve(nusi_plan* pl, const nusi_params* pts, int n, double* d_flu
         if (!d_flux) d_flux = pl->d_scratch;
         if (!d_fla) d_fla = pl->d_scratch + N3 * pl->max_points;
     }
+    // the cascade: points sharing a table slot run in pairs on the multi-RHS kernel (k_cascade_ws<R = 2>: one
+    // operator, two sources) when every point is non-resonant with the power-law source and most points pair up
+    bool all_pl = true, all_nr = true;
+    for (int i = 0; i < n; ++i) {
+        all_pl = all_pl && pl->h_pts[i].source == NUSI_SOURCE_POWER_LAW;
+        all_nr = all_nr && pl->h_pts[i].non_resonant;
+    }
+    int ngroups = 0;
+    const char* mrhs_env = getenv("NUSI_MRHS");     // A/B: 0 = one point per workgroup
+    if (pl->cascade_kind == NUSI_CASCADE_MFMA && all_pl && all_nr && !(mrhs_env && mrhs_env[0] == '0') &&
+        nusi::cascade_ws_fits(pl->gd, 2)) {
+        std::vector<int> open(ntab, -1);   // per table slot: a point waiting for its partner
+        for (int i = 0; i < n; ++i) {
+            int& o = open[pl->h_pts[i].tslot];
+            if (o < 0) o = i;
+            else { pl->h_groups[ngroups++] = make_int2(o, i); o = -1; }
+        }
+        for (int j = 0; j < ntab; ++j)
+            if (open[j] >= 0) pl->h_groups[ngroups++] = make_int2(open[j], -1);
+        if (4 * ngroups > 3 * n) ngroups = 0;   // too few pairs: one point per workgroup
+    }
+    if (ngroups) HIPCHECK(hipMemcpyAsync(pl->d_groups, pl->h_groups, sizeof(int2) * ngroups, hipMemcpyHostToDevice, s));
     HIPCHECK(hipMemcpyAsync(pl->d_pts, pl->h_pts, sizeof(nusi::Point) * n, hipMemcpyHostToDevice, s));
     HIPCHECK(hipMemcpyAsync(pl->d_tpts, pl->h_tpts, sizeof(nusi::Point) * ntab, hipMemcpyHostToDevice, s));
     HIPCHECK(hipMemcpyAsync(pl->d_batches, pl->h_batches, sizeof(int) * nbatch, hipMemcpyHostToDevice, s));
@@ -706,9 +734,10 @@ int nusi_plan_evolve(nusi_plan* pl, const nusi_params* pts, int n, double* d_flu
                                 nbatch, pl->alpha_tile_kernel ? std::min(cap, 4) : cap, pl->alpha_tile_kernel,
                                 nb_plain));
     HIPCHECK(hipEventRecord(ev[2], s));
-    bool all_pl = true;
-    for (int i = 0; i < n; ++i) all_pl = all_pl && pl->h_pts[i].source == NUSI_SOURCE_POWER_LAW;
-    HIPCHECK(nusi::launch_cascade(pl->gd, pl->d_pts, n, pl->tabs, d_flux, d_fla, s, pl->cascade_kind, all_pl));
+    if (ngroups)
+        HIPCHECK(nusi::launch_cascade_ws(pl->gd, pl->d_pts, 2, pl->d_groups, ngroups, pl->tabs, d_flux, d_fla, s));
+    else
+        HIPCHECK(nusi::launch_cascade(pl->gd, pl->d_pts, n, pl->tabs, d_flux, d_fla, s, pl->cascade_kind, all_pl, all_nr));
     HIPCHECK(hipEventRecord(ev[3], s));
     HIPCHECK(hipEventRecord(pl->ev_done, s));
     for (int k = 0; k < 4; ++k) pl->last_ev[k] = ev[k];   // stage_ms / warnings / tables refer to the latest call

@@ -886,6 +886,273 @@ __global__ __launch_bounds__(kWfMaxThreads) void k_cascade_wf_mfma(GridDev g, co
     }
 }
 
+// ---------------------------------------------------------------------------
+// Warp-specialised MFMA cascade, R right-hand sides per workgroup (NUSI_CASCADE_MFMA's kernel for
+// non-resonant points with the power-law source, the scans' case).
+//
+// The wavefront and the rank-4 MFMA push are k_cascade_wf_mfma's; the waves are specialised:
+//   * push waves (0 .. nw-3) hold the accumulators of 16 RT rows and run only the block pushes;
+//   * the record wave (nw-2) computes the flux-independent records (1/Z, LU of M, sources) of
+//     stage sg+1 while the chain solves stage sg (a 2-slot ring in LDS): no records phase, no
+//     extra barriers;
+//   * the chain wave (nw-1) solves, lane j = step slot j.
+// Each kind runs its own stage loop with one barrier per stage, so the registers of one kind's
+// code are not live in another's: the accumulators no longer share a budget with the records'
+// temporaries, and the kernel fits 128 VGPRs (4 waves per SIMD).
+//
+// R = 1 (RT = 4): one point per workgroup, two workgroups per CU -- two independent chains share
+//   a CU instead of one.
+// R = 2 (RT = 2): two points that share one Stage-A table (a gamma batch: same m_phi, g, masses
+//   and flags; nuSIprop.hpp:217-253 read neither si nor norm) in one workgroup -- the multi-RHS
+//   transfer-matrix x flux-batch GEMM.  For fixed tables the cascade is linear in the source (Lum
+//   enters only through src, nuSIprop.hpp:283): both points run the same triangular operator, so
+//   the records are computed once (one source field per point), each alpha block is loaded once
+//   and is the A operand of both points' MFMAs, and the chain lane solves both points' bins (two
+//   independent solves that interleave).  groups[k] = (p0, p1); p1 < 0: a single point.
+// Every accumulator, published row and solve receives the same operations on the same operands
+// as in k_cascade_wf_mfma, so the fluxes equal that kernel's bit for bit (test_cascade_ws_*).
+// ---------------------------------------------------------------------------
+
+// the power-law source term c_i Lum of bin b at step i (nuSIprop.hpp:283, :656), the expression
+// cascade_record stores in PR_SRC
+NUSI_FN double powerlaw_src(const GridDev& g, const Point& P, const double* pw, int i, int b)
+{
+    return g.step_c[i] * (P.norm_total / 3.0 * g.sfr[i] * (g.Emax[b] * pw[b + i + 1] - g.Emin[b] * pw[b + i]) / (1 - P.si));
+}
+
+template <int R> struct WsCfg;
+template <> struct WsCfg<1> { static constexpr int RT = 4, kMaxThreads = 512; };   // 6 push waves + 2
+template <> struct WsCfg<2> { static constexpr int RT = 2, kMaxThreads = 832; };   // 11 push waves + 2
+
+template <int NJ, int R>
+__global__ __launch_bounds__(WsCfg<R>::kMaxThreads) __attribute__((amdgpu_waves_per_eu(4, 4)))
+void k_cascade_ws(GridDev g, const Point* __restrict__ pts, const int2* __restrict__ groups, TablesDev t,
+                  double* __restrict__ flux, double* __restrict__ flux_fla)
+{
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    constexpr int RT = WsCfg<R>::RT, NST = NJ / 16, NF = kWfFields + R - 1;
+    const int N = g.N, Nz = g.Nz, T = g.T, nst = Nz - 1;
+    const int tid = threadIdx.x, nthr = blockDim.x, lane = tid & 63, wave = tid >> 6, nw = nthr >> 6;
+    int pid[R];
+    bool single = false;
+    if (R == 1) {
+        pid[0] = blockIdx.x;
+    } else {
+        const int2 gp = groups[blockIdx.x];
+        pid[0] = gp.x;
+        pid[R - 1] = gp.y >= 0 ? gp.y : gp.x;
+        single = gp.y < 0;
+    }
+    double* F = lds;                         // [R][3][N]
+    double* rec = F + 3 * R * N;             // [NF][2][NJ]  records of stage sg in slot sg & 1
+    double* Tp = rec + 2 * NF * NJ;          // [R][8][NJ]   T_j by stage (ring of 8)
+    double* AX = Tp + 8 * R * NJ;            // [R][2][4][NJ] rows published by block q (parity q & 1)
+    double* rdE = AX + 8 * R * NJ;           // [N]
+    double* pw = rdE + N;                    // [R][T + 2]
+    double* sGt = pw + R * (T + 2);
+    double* sAt = sGt + T;
+    double* sdg = sAt + T;                   // [4][T]: alpha(n, n+k), k = 1..4 (0 past the table)
+    double* sEmin = sdg + 4 * T;
+    double* sEmax = sEmin + N;
+    double* sgz = sEmax + N;                 // z, step_c, step_s, sfr [Nz each]
+    GridDev gl = g;
+    gl.Emin = sEmin;
+    gl.Emax = sEmax;
+    gl.z = sgz;
+    gl.step_c = sgz + Nz;
+    gl.step_s = sgz + 2 * Nz;
+    gl.sfr = sgz + 3 * Nz;
+    const Point& P = pts[pid[0]];
+    const double* __restrict__ Al = t.A + (size_t)P.tslot * g.PT;
+    {
+        const double* __restrict__ Gt = t.G + (size_t)P.tslot * T;
+        const double* __restrict__ At = t.At + (size_t)P.tslot * T;
+        for (int b = tid; b < 3 * R * N; b += nthr) F[b] = 0.0;
+        for (int j = tid; j < 16 * R * NJ; j += nthr) Tp[j] = 0.0;   // Tp and AX
+        for (int n = tid; n < T; n += nthr) {
+            sGt[n] = Gt[n];
+            sAt[n] = At[n];
+#pragma unroll
+            for (int k = 1; k <= 4; ++k) sdg[(k - 1) * T + n] = (n + k < T) ? Al[(size_t)(n + k) * (n + k - 1) / 2 + n] : 0.0;
+        }
+        for (int b = tid; b < N; b += nthr) { sEmin[b] = g.Emin[b]; sEmax[b] = g.Emax[b]; }
+        for (int i = tid; i < Nz; i += nthr) {
+            sgz[i] = g.z[i];
+            sgz[Nz + i] = g.step_c[i];
+            sgz[2 * Nz + i] = g.step_s[i];
+            sgz[3 * Nz + i] = g.sfr[i];
+        }
+        cascade_aux_init(g, P, rdE, pw, tid, nthr);
+#pragma unroll
+        for (int p = 1; p < R; ++p) {   // the other points' pw[] (cascade_aux_init's expression)
+            const double si = pts[pid[p]].si;
+            for (int e = tid + 1; e <= T + 1; e += nthr) {
+                const int i = min(Nz - 1, max(1, e - N + 1)), b = e - i;
+                const double E = (b < N) ? g.Emin[b] : g.Emax[N - 1];
+                pw[p * (T + 2) + e] = nm::pow(E / 1e14 * (1 + g.z[i]), -si);
+            }
+        }
+    }
+    __syncthreads();
+    // records of stage s2 for step slot jj (record wave): the fields of point 0, then the other sources
+    auto records = [&](int s2, int jj) {
+        const int b = N - 1 - s2 + jj;
+        if (jj < nst && b >= 0 && b < N) {
+            double* Rw = rec + (s2 & 1) * NJ + jj;
+            cascade_record<true>(gl, P, sGt, sAt, rdE, pw, Nz - 1 - jj, b, Rw, 2 * NJ);
+#pragma unroll
+            for (int p = 1; p < R; ++p)
+                Rw[(kWfFields + p - 1) * 2 * NJ] = powerlaw_src(gl, pts[pid[p]], pw + p * (T + 2), Nz - 1 - jj, b);
+        }
+    };
+    if (wave == nw - 2) records(0, lane);
+    __syncthreads();
+
+    if (wave == nw - 1) {
+        // ---- chain: lane j solves (step j, bin N-1-sg+j) of every point at stage sg
+        const int j = lane;
+        const bool act = j < nst;
+        const double u0 = P.u[0], u1 = P.u[1], u2 = P.u[2];
+        const double cj = act ? gl.step_c[Nz - 1 - j] : 0.0;
+        for (int sg0 = 0; sg0 < T; sg0 += 4)
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+            const int sg = sg0 + d;
+            if (sg >= T) break;
+            const int r = T - 1 - sg;
+            const int b = N - 1 - sg + j;
+            double Tn[R];
+#pragma unroll
+            for (int p = 0; p < R; ++p) Tn[p] = 0.0;
+            if (act && b >= 0 && b < N) {
+                const double* Rc = rec + (sg & 1) * NJ + j;
+                constexpr int S = 2 * NJ;
+                const int qq = (sg - 1) >> 2;              // block whose publication serves stage sg
+                const int nu = (d == 0) ? 4 : d;           // columns r+1 .. r+nu not yet pushed
+                const int ax = ((qq & 1) * 4 + (sg - 1 - 4 * qq)) * NJ + j;
+                double s[R];
+#pragma unroll
+                for (int p = 0; p < R; ++p) s[p] = AX[p * 8 * NJ + ax];
+#pragma unroll
+                for (int k = 4; k >= 1; --k)
+                    if (k <= nu) {
+                        const double a = sdg[(k - 1) * T + r];
+#pragma unroll
+                        for (int p = 0; p < R; ++p) s[p] = fma(a, Tp[(p * 8 + ((sg - k) & 7)) * NJ + j], s[p]);
+                    }
+                const double rz0 = Rc[PR_RZ0 * S], rz1 = Rc[PR_RZ1 * S], rz2 = Rc[PR_RZ2 * S];
+                const int pmb = (int)Rc[kPreFields * S];
+                const double l10 = Rc[PR_L10 * S], l20 = Rc[PR_L20 * S], l21 = Rc[PR_L21 * S];
+                const double u01 = Rc[PR_U01 * S], u02 = Rc[PR_U02 * S], u12 = Rc[PR_U12 * S];
+                const double ru00 = Rc[PR_RU00 * S], ru11 = Rc[PR_RU11 * S], ru22 = Rc[PR_RU22 * S];
+                const double sde = Rc[PR_SDE * S];
+#pragma unroll
+                for (int p = 0; p < R; ++p) {
+                    double* Fp = F + 3 * N * p;
+                    const double src = Rc[(p == 0 ? PR_SRC : kWfFields + p - 1) * S];
+                    double x0, x1, x2;
+                    cascade_solve(Fp[b], Fp[N + b], Fp[2 * N + b], cj * s[p], src, u0, u1, u2, rz0, rz1, rz2, pmb, l10,
+                                  l20, l21, u01, u02, u12, ru00, ru11, ru22, x0, x1, x2);
+                    Fp[b] = x0;
+                    Fp[N + b] = x1;
+                    Fp[2 * N + b] = x2;
+                    if (b > 0) Tn[p] = (u0 * x0 + u1 * x1 + u2 * x2) * sde;
+                }
+            }
+            if (act)
+#pragma unroll
+                for (int p = 0; p < R; ++p) Tp[(p * 8 + (sg & 7)) * NJ + j] = Tn[p];
+            __syncthreads();
+        }
+    } else if (wave == nw - 2) {
+        // ---- records of the next stage, while the chain solves this one
+        for (int sg = 0; sg < T; ++sg) {
+            if (sg + 1 < T) records(sg + 1, lane);
+            __syncthreads();
+        }
+    } else {
+        // ---- push: block q (stage 4q) adds columns T-4q .. T-4q+3 (the T of stages 4q-1 .. 4q-4) into the
+        // rows below r = T-1-4q, then publishes rows r-1 .. r-4 (the rows of stages 4q+1 .. 4q+4)
+        const int rw0 = wave * 16 * RT;
+        nusi_f64x4 acc[R][RT][NST];
+#pragma unroll
+        for (int p = 0; p < R; ++p)
+#pragma unroll
+            for (int a = 0; a < RT; ++a)
+#pragma unroll
+                for (int s = 0; s < NST; ++s) acc[p][a][s] = nusi_f64x4{0.0, 0.0, 0.0, 0.0};
+        // A operands: alpha(row, column), row = tile row + (lane & 15), column = first block column + (lane >> 4);
+        // rows clamped into the column (those rows are consumed)
+        auto load_blk = [&](int q, double (&dst)[RT]) {
+            int c = T - 4 * q + (lane >> 4);
+            c = c < 1 ? 1 : (c > T - 1 ? T - 1 : c);
+            const size_t cb = (size_t)c * (c - 1) / 2;
+#pragma unroll
+            for (int a = 0; a < RT; ++a) {
+                const int row = rw0 + 16 * a + (lane & 15);
+                dst[a] = Al[cb + (row < c - 1 ? row : c - 1)];
+            }
+        };
+        double ablk[RT];
+        load_blk(1, ablk);
+        for (int sg = 0; sg < T; ++sg) {
+            if ((sg & 3) == 0) {
+                const int q = sg >> 2, r = T - 1 - sg;
+                if (q >= 1) {
+#pragma unroll
+                    for (int s = 0; s < NST; ++s) {
+                        const int bi = ((sg - 1 - (lane >> 4)) & 7) * NJ + 16 * s + (lane & 15);
+                        double bop[R];
+#pragma unroll
+                        for (int p = 0; p < R; ++p) bop[p] = Tp[p * 8 * NJ + bi];
+#pragma unroll
+                        for (int a = 0; a < RT; ++a)
+                            if (rw0 + 16 * a < r)   // tiles wholly at or above r hold consumed rows only
+#pragma unroll
+                                for (int p = 0; p < R; ++p)
+                                    acc[p][a][s] = __builtin_amdgcn_mfma_f64_16x16x4f64(ablk[a], bop[p], acc[p][a][s], 0, 0, 0);
+                    }
+                    load_blk(q + 1, ablk);
+                }
+                const int hi = r - 1;
+#pragma unroll
+                for (int a = 0; a < RT; ++a)
+                    if (rw0 + 16 * a <= hi && rw0 + 16 * a + 15 >= hi - 3)   // uniform: tiles holding those rows
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) {
+                            const int row = rw0 + 16 * a + (lane >> 4) + 4 * e;
+                            const int slot = hi - row;
+                            if (slot >= 0 && slot < 4)
+#pragma unroll
+                                for (int s = 0; s < NST; ++s) {
+                                    const int o = ((q & 1) * 4 + slot) * NJ + 16 * s + (lane & 15);
+#pragma unroll
+                                    for (int p = 0; p < R; ++p) AX[p * 8 * NJ + o] = acc[p][a][s][e];
+                                }
+                        }
+            }
+            __syncthreads();
+        }
+    }
+    // finalise (nuSIprop.hpp:328-336)
+#pragma unroll
+    for (int p = 0; p < R; ++p) {
+        if (p > 0 && single) break;
+        const Point& Q = pts[pid[p]];
+        const double* Fp = F + 3 * N * p;
+        double* fo = flux + (size_t)pid[p] * 3 * N;
+        double* fl = flux_fla + (size_t)pid[p] * 3 * N;
+        for (int b = tid; b < N; b += nthr) {
+            const double dE = g.Emax[b] - g.Emin[b];
+            const double f0 = Fp[b] / dE, f1 = Fp[N + b] / dE, f2 = Fp[2 * N + b] / dE;
+            fo[b] = f0;
+            fo[N + b] = f1;
+            fo[2 * N + b] = f2;
+            for (int f = 0; f < 3; ++f) fl[f * N + b] = Q.U2[3 * f + 0] * f0 + Q.U2[3 * f + 1] * f1 + Q.U2[3 * f + 2] * f2;
+        }
+    }
+}
+
 // launch geometry of the wavefront kernel: one thread per pushed row (T-1), whole waves; K stages
 // of records per batch, as many as the threads cover and kWfMaxLds allows
 constexpr size_t kWfMaxLds = 64 * 1024;
@@ -940,6 +1207,51 @@ static bool mf_fits(const GridDev& g)
     return w.nthr <= kWfMaxThreads && w.K >= 1 && w.lds <= kWfMaxLds;
 }
 
+// the warp-specialised kernel: push waves of 16 RT rows each, then the record and chain waves
+constexpr size_t kWsMaxLds[3] = {0, 80 * 1024, 150 * 1024};   // R = 1: two workgroups per CU
+static WfGeom ws_geom(const GridDev& g, int NJ, int R)
+{
+    WfGeom w;
+    const int rows = R == 1 ? 64 : 32;
+    w.nthr = ((g.T - 1 + rows - 1) / rows) * 64 + 128;
+    w.K = 2;
+    w.lds = sizeof(double) * (3 * (size_t)R * g.N + 2 * (size_t)(kWfFields + R - 1) * NJ + 16 * (size_t)R * NJ + g.N +
+                              (size_t)R * (g.T + 2) + 6 * (size_t)g.T + 2 * (size_t)g.N + 4 * (size_t)g.Nz);
+    return w;
+}
+bool cascade_ws_fits(const GridDev& g, int R)
+{
+    const int nj = wf_nj(g);
+    if (!nj || g.T < 2 || R < 1 || R > 2) return false;
+    const WfGeom w = ws_geom(g, nj, R);
+    return w.nthr <= (R == 1 ? WsCfg<1>::kMaxThreads : WsCfg<2>::kMaxThreads) && w.lds <= kWsMaxLds[R];
+}
+
+template <int NJ, int R>
+static void launch_ws_nj(const GridDev& g, const Point* pts, const int2* groups, int nwg, TablesDev t, double* flux,
+                         double* flux_fla, hipStream_t s)
+{
+    const WfGeom w = ws_geom(g, NJ, R);
+    hipLaunchKernelGGL((k_cascade_ws<NJ, R>), dim3(nwg), dim3(w.nthr), w.lds, s, g, pts, groups, t, flux, flux_fla);
+}
+
+hipError_t launch_cascade_ws(const GridDev& g, const Point* pts, int R, const int2* groups, int nwg, TablesDev t,
+                             double* flux, double* flux_fla, hipStream_t s)
+{
+    if (!cascade_ws_fits(g, R)) return hipErrorInvalidValue;
+    const int nj = wf_nj(g);
+    if (R == 1) {
+        if (nj == 16) launch_ws_nj<16, 1>(g, pts, groups, nwg, t, flux, flux_fla, s);
+        else if (nj == 32) launch_ws_nj<32, 1>(g, pts, groups, nwg, t, flux, flux_fla, s);
+        else launch_ws_nj<48, 1>(g, pts, groups, nwg, t, flux, flux_fla, s);
+    } else {
+        if (nj == 16) launch_ws_nj<16, 2>(g, pts, groups, nwg, t, flux, flux_fla, s);
+        else if (nj == 32) launch_ws_nj<32, 2>(g, pts, groups, nwg, t, flux, flux_fla, s);
+        else launch_ws_nj<48, 2>(g, pts, groups, nwg, t, flux, flux_fla, s);
+    }
+    return hipGetLastError();
+}
+
 template <int NJ>
 static void launch_mf(const GridDev& g, const Point* pts, int npts, TablesDev t, double* flux, double* flux_fla,
                       hipStream_t s, bool power_law)
@@ -983,7 +1295,7 @@ static bool dispatch_reg(int nq, const GridDev& g, const Point* pts, int npts, T
 using RegNQ = std::integer_sequence<int, 1, 2, 3, 4, 5, 6, 8, 10, 12, 16, 20>;
 
 hipError_t launch_cascade(const GridDev& g, const Point* pts, int npts, TablesDev t, double* flux, double* flux_fla,
-                          hipStream_t s, int kind, bool all_power_law)
+                          hipStream_t s, int kind, bool all_power_law, bool all_nonres)
 {
     const int nq = (g.N + 63) / 64;
     if (kind == NUSI_CASCADE_AUTO) {
@@ -991,6 +1303,10 @@ hipError_t launch_cascade(const GridDev& g, const Point* pts, int npts, TablesDe
         kind = !env ? NUSI_CASCADE_AUTO
                     : (env[0] == 'w' ? NUSI_CASCADE_WAVEFRONT : env[0] == 'm' ? NUSI_CASCADE_MFMA
                        : env[0] == 'r' ? NUSI_CASCADE_REG : NUSI_CASCADE_LDS);
+    }
+    if (kind == NUSI_CASCADE_MFMA && all_power_law && all_nonres && cascade_ws_fits(g, 1)) {
+        const char* ws = getenv("NUSI_CASCADE_WS");   // A/B: 0 = k_cascade_wf_mfma
+        if (!ws || ws[0] != '0') return launch_cascade_ws(g, pts, 1, nullptr, npts, t, flux, flux_fla, s);
     }
     if (kind == NUSI_CASCADE_MFMA && mf_fits(g)) {
         switch (wf_nj(g)) {

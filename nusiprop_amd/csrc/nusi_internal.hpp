@@ -56,8 +56,15 @@ hipError_t launch_alpha(const GridDev& g, const Point* pts, int npts, const Spli
                         TablesDev t, int* warn, hipStream_t s, const int* batches, int nbatches, int gmax,
                         bool tile_kernel, int nb_plain);
 // kind: NUSI_CASCADE_* (include/nusi.h); NUSI_CASCADE_AUTO also honours $NUSI_CASCADE = wf|reg|lds
-// all_power_law: every point uses the power-law source (selects the call-free wavefront kernel)
+// all_power_law: every point uses the power-law source (selects the call-free wavefront kernel);
+// all_nonres: every point is non-resonant (with all_power_law and NUSI_CASCADE_MFMA: k_cascade_ws<R = 1>)
 hipError_t launch_cascade(const GridDev& g, const Point* pts, int npts, TablesDev t, double* flux, double* flux_fla,
-                          hipStream_t s, int kind, bool all_power_law);
+                          hipStream_t s, int kind, bool all_power_law, bool all_nonres);
+// the warp-specialised MFMA cascade (k_cascade_ws): R = 1, one point per workgroup (groups unused, nwg = points),
+// or R = 2, groups[k] = two points sharing one table slot (y < 0: one point); non-resonant points with the
+// power-law source only.  Fluxes equal k_cascade_wf_mfma's bit for bit.
+bool cascade_ws_fits(const GridDev& g, int R);
+hipError_t launch_cascade_ws(const GridDev& g, const Point* pts, int R, const int2* groups, int nwg, TablesDev t,
+                             double* flux, double* flux_fla, hipStream_t s);
 
 }  // namespace nusi

@@ -12,6 +12,10 @@ import numpy as np
 BASE = dict(mntot=0.1, norm=1.0, majorana=True, non_resonant=True, normal_ordering=True, flav=2, phiphi=False,
             source_model=1, N_bins_E=300, lEmin=12.0, lEmax=17.0, zmax=5.0)
 
+# BASELINE config 1: test.cpp:6-23 (N_E = 100, lE 9 -> 14, the fork's DSNB source, phi-phi off)
+C1 = dict(mphi=6e5, g=0.01, mntot=0.1, si=2.5, norm=6.0, majorana=True, non_resonant=True, normal_ordering=True,
+          N_bins_E=100, lEmin=9.0, lEmax=14.0, zmax=5.0, flav=2, phiphi=False, source_model=0)
+
 
 def c4_points(si=2.5, n_mphi=32, n_g=32, **over):
     """BASELINE config 4: mphi in logspace(5.5, 8, 32) x g in logspace(-3, 0, 32), gamma = 2.5, power law."""

@@ -279,3 +279,70 @@ def test_alpha_batch_kernel_equals_tile_kernel(nusi, monkeypatch):
             for x, y in zip(a, b):
                 assert np.array_equal(x, y), cap
         assert got[4] == ref[4]
+
+
+def _evolve_env(nusi, pts, monkeypatch, **env):
+    """evolve `pts` on the MFMA cascade with the A/B switches in `env` (NUSI_CASCADE_WS, NUSI_MRHS)."""
+    from nusiprop_amd import _lib
+    for k in ("NUSI_CASCADE_WS", "NUSI_MRHS"):
+        monkeypatch.delenv(k, raising=False)
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    p0 = pts[0]
+    plan = nusi.Plan(p0["N_bins_E"], p0["lEmin"], p0["lEmax"], p0["zmax"], max_points=len(pts))
+    plan.set_cascade(_lib.CASCADE_MFMA)
+    out = plan.evolve(pts)
+    plan.close()
+    return out
+
+
+@pytest.mark.parametrize("N", [37, 100, 130, 300])
+def test_cascade_ws_equals_mfma(nusi, monkeypatch, N):
+    """The warp-specialised cascade (push / record / chain waves in their own stage loops) gives
+    k_cascade_wf_mfma's fluxes bit for bit: one point per workgroup (distinct tables), and two points
+    per workgroup when they share a table (the multi-RHS kernel: gamma batches, one operator, two
+    sources), including a table slot with an odd number of points (a single in the pair list)."""
+    distinct = [dict(cases.C2B_100, N_bins_E=N, mphi=m, g=g, majorana=maj)
+                for m, g, maj in ((6e5, 0.01, True), (2e6, 0.1, False), (1e6, 0.3, True), (3e7, 0.8, True))]
+    ref = _evolve_env(nusi, distinct, monkeypatch, NUSI_CASCADE_WS="0")
+    got = _evolve_env(nusi, distinct, monkeypatch)
+    assert np.array_equal(got[0], ref[0]) and np.array_equal(got[1], ref[1])
+    gam = [dict(p, si=s, norm=nm) for p in distinct[:2] for s, nm in ((2.0, 1.0), (2.3, 3.0), (2.9, 0.5))]
+    gam.append(dict(distinct[2], si=2.7))
+    ref = _evolve_env(nusi, gam, monkeypatch, NUSI_CASCADE_WS="0", NUSI_MRHS="0")
+    one = _evolve_env(nusi, gam, monkeypatch, NUSI_MRHS="0")
+    two = _evolve_env(nusi, gam, monkeypatch)
+    for f in (one, two):
+        assert np.array_equal(f[0], ref[0]) and np.array_equal(f[1], ref[1])
+
+
+def test_c5_gamma_block_vs_oracle(nusi, oracle_mod, monkeypatch):
+    """BASELINE config 5: one full 16-gamma block of scan.c5_points() (N_E = 300, power law; one
+    Stage-A table, 8 pairs on the multi-RHS cascade) against the oracle -- its tables once, its
+    cascade per gamma -- to FLUX_RTOL with the same exact zeros; and the block through the
+    one-point-per-workgroup kernel bit for bit (A/B)."""
+    from nusiprop_amd import scan
+    allp = scan.c5_points()
+    blk = allp[16 * 1234:16 * 1235]
+    assert len({scan.table_key(p) for p in blk}) == 1 and len({p["si"] for p in blk}) == 16
+    flux, fla = _evolve_env(nusi, blk, monkeypatch)
+    ref1 = _evolve_env(nusi, blk, monkeypatch, NUSI_MRHS="0")
+    assert np.array_equal(flux, ref1[0]) and np.array_equal(fla, ref1[1])
+    o = oracle_mod.Oracle(**cases.oracle_kwargs(blk[0]))
+    G, aT, al = o.tables()
+    for k, p in enumerate(blk):
+        ok = oracle_mod.Oracle(**cases.oracle_kwargs(p))
+        ok.prepare()
+        f_ref, fla_ref = ok.cascade(G, aT, al)
+        assert cases.rel_err(flux[k], f_ref) <= FLUX_RTOL, k
+        assert cases.rel_err(fla[k], fla_ref) <= FLUX_RTOL, k
+
+
+def test_c1_test_cpp_n300(nusi, oracle_mod):
+    """BASELINE config 1 (test.cpp:6-23: DSNB source, lE 9 -> 14) at N_E = 300 end to end vs the oracle."""
+    kw = dict(cases.TEST_CPP, N_bins_E=300)
+    o = oracle_mod.Oracle(**cases.oracle_kwargs(kw))
+    f_ref, fla_ref = o.evolve()
+    _, flux, fla, _, _ = _gpu(nusi, [kw])
+    assert cases.rel_err(flux[0], f_ref) <= FLUX_RTOL
+    assert cases.rel_err(fla[0], fla_ref) <= FLUX_RTOL
