@@ -87,49 +87,69 @@ __device__ __attribute__((noinline)) double lum_out(const Point& P, double z, do
 // Zdr, M = I + offdiag and its LU (nuSIprop.hpp:289-310) and the source term c_i Lum (:283).
 // 1/dE_b and 1/Zdr are multiplied in (the reference divides; M's off-diagonals are ~1e-22 of
 // the diagonal), the power-law source reads pw[]; the DSNB source is evaluated in full.
-__device__ __attribute__((noinline)) void lu3_factor_out(double (&A)[3][3], int (&perm)[3]) { lu3_factor(A, perm); }
 
-// kCallFree: the caller's points all use the power-law source and the pivoting LU is inlined, so
-// the record code makes no calls (a call inside the wavefront kernel's stage loop makes the
-// compiler drain every outstanding alpha prefetch, vmcnt(0), after it)
-template <bool kCallFree>
-NUSI_FN void cascade_record(const GridDev& g, const Point& P, const double* __restrict__ Gt,
-                            const double* __restrict__ At, const double* rdE, const double* pw, int i, int b,
-                            double* R, int stride)
+// 1/x to about an ulp: the hardware reciprocal estimate (v_rcp_f64) refined by two Newton steps.  The
+// records' divisions use it (a correctly rounded fp64 division is a ~10-instruction dependent chain);
+// the reference divides, so the fluxes move by rounding only (tests: FLUX_RTOL against the oracle).
+NUSI_FN double rcp_nr(double x)
+{
+    double r = __builtin_amdgcn_rcp(x);
+    double e = fma(-x, r, 1.0);
+    r = fma(r, e, r);
+    e = fma(-x, r, 1.0);
+    return fma(r, e, r);
+}
+
+// The record of (step i, bin b) in two phases (k_cascade_ws runs them on different waves, one stage
+// apart; cascade_record runs them back to back -- the same operations either way):
+//   phase 1: 1/Zdr_k and the off-diagonals of M = I + offdiag (nuSIprop.hpp:289-300)
+//   phase 2: the LU of M (GSL's partial pivoting, :309) from those
+struct RecM { double rz0, rz1, rz2, m01, m02, m10, m12, m20, m21; };
+NUSI_FN RecM record_phase1(const GridDev& g, const Point& P, const double* __restrict__ Gt,
+                           const double* __restrict__ At, const double* rdE, int i, int b)
 {
     const double c = g.step_c[i], s = g.step_s[i];
     const double u0 = P.u[0], u1 = P.u[1], u2 = P.u[2];
     const double rd = rdE[b];
     const double Gw = s * Gt[b + i - 1], Aw = s * At[b + i - 1];
-    const double rz0 = 1.0 / (1.0 + c * (Gw * u0 - Aw * (u0 * u0)) * rd);
-    const double rz1 = 1.0 / (1.0 + c * (Gw * u1 - Aw * (u1 * u1)) * rd);
-    const double rz2 = 1.0 / (1.0 + c * (Gw * u2 - Aw * (u2 * u2)) * rd);
-    R[PR_RZ0 * stride] = rz0;
-    R[PR_RZ1 * stride] = rz1;
-    R[PR_RZ2 * stride] = rz2;
+    RecM m;
+    m.rz0 = rcp_nr(1.0 + c * (Gw * u0 - Aw * (u0 * u0)) * rd);
+    m.rz1 = rcp_nr(1.0 + c * (Gw * u1 - Aw * (u1 * u1)) * rd);
+    m.rz2 = rcp_nr(1.0 + c * (Gw * u2 - Aw * (u2 * u2)) * rd);
     // M = I + offdiag, M[k][l] = Aw u_k u_l / dE_b / Zdr_k
-    const double m01 = Aw * u0 * u1 * rd * rz0, m02 = Aw * u0 * u2 * rd * rz0;
-    const double m10 = Aw * u1 * u0 * rd * rz1, m12 = Aw * u1 * u2 * rd * rz1;
-    const double m20 = Aw * u2 * u0 * rd * rz2, m21 = Aw * u2 * u1 * rd * rz2;
+    m.m01 = Aw * u0 * u1 * rd * m.rz0;
+    m.m02 = Aw * u0 * u2 * rd * m.rz0;
+    m.m10 = Aw * u1 * u0 * rd * m.rz1;
+    m.m12 = Aw * u1 * u2 * rd * m.rz1;
+    m.m20 = Aw * u2 * u0 * rd * m.rz2;
+    m.m21 = Aw * u2 * u1 * rd * m.rz2;
+    return m;
+}
+__device__ __attribute__((noinline)) void lu3_factor_out(double (&A)[3][3], int (&perm)[3]) { lu3_factor(A, perm); }
+// the LU fields PR_L10 .. PR_RU22 and the permutation (R[kPreFields * stride])
+template <bool kCallFree>
+NUSI_FN void record_phase2(const RecM& m, double* R, int stride)
+{
     // LU without row exchanges when partial pivoting would not exchange (M ~ I: always, in
     // practice); the same operations as lu3_factor on that path (a / 1.0 == a), else lu3_factor
-    const double a11 = 1.0 - m10 * m01, a12 = m12 - m10 * m02;
-    const double a21 = m21 - m20 * m01, a22 = 1.0 - m20 * m02;
-    if (fabs(m10) <= 1.0 && fabs(m20) <= 1.0 && fabs(a21) <= fabs(a11) && a11 != 0.0) {
-        const double l21 = a21 / a11;
+    const double a11 = 1.0 - m.m10 * m.m01, a12 = m.m12 - m.m10 * m.m02;
+    const double a21 = m.m21 - m.m20 * m.m01, a22 = 1.0 - m.m20 * m.m02;
+    if (fabs(m.m10) <= 1.0 && fabs(m.m20) <= 1.0 && fabs(a21) <= fabs(a11) && a11 != 0.0) {
+        const double ra11 = rcp_nr(a11);
+        const double l21 = a21 * ra11;
         const double u22 = a22 - l21 * a12;
-        R[PR_L10 * stride] = m10;
-        R[PR_L20 * stride] = m20;
+        R[PR_L10 * stride] = m.m10;
+        R[PR_L20 * stride] = m.m20;
         R[PR_L21 * stride] = l21;
-        R[PR_U01 * stride] = m01;
-        R[PR_U02 * stride] = m02;
+        R[PR_U01 * stride] = m.m01;
+        R[PR_U02 * stride] = m.m02;
         R[PR_U12 * stride] = a12;
         R[PR_RU00 * stride] = 1.0;
-        R[PR_RU11 * stride] = 1.0 / a11;
-        R[PR_RU22 * stride] = 1.0 / u22;
+        R[PR_RU11 * stride] = ra11;
+        R[PR_RU22 * stride] = rcp_nr(u22);
         R[kPreFields * stride] = (double)(0 | (1 << 2) | (2 << 4));
     } else {
-        double M[3][3] = {{1.0, m01, m02}, {m10, 1.0, m12}, {m20, m21, 1.0}};
+        double M[3][3] = {{1.0, m.m01, m.m02}, {m.m10, 1.0, m.m12}, {m.m20, m.m21, 1.0}};
         int pm[3];
         if (kCallFree) lu3_factor(M, pm);
         else lu3_factor_out(M, pm);
@@ -144,9 +164,26 @@ NUSI_FN void cascade_record(const GridDev& g, const Point& P, const double* __re
         R[PR_RU22 * stride] = 1.0 / M[2][2];
         R[kPreFields * stride] = (double)(pm[0] | (pm[1] << 2) | (pm[2] << 4));
     }
+}
+
+// kCallFree: the caller's points all use the power-law source and the pivoting LU is inlined, so
+// the record code makes no calls (a call inside the wavefront kernel's stage loop makes the
+// compiler drain every outstanding alpha prefetch, vmcnt(0), after it)
+template <bool kCallFree>
+NUSI_FN void cascade_record(const GridDev& g, const Point& P, const double* __restrict__ Gt,
+                            const double* __restrict__ At, const double* rdE, const double* pw, int i, int b,
+                            double* R, int stride)
+{
+    const double c = g.step_c[i], s = g.step_s[i];
+    const double rd = rdE[b];
+    const RecM m = record_phase1(g, P, Gt, At, rdE, i, b);
+    R[PR_RZ0 * stride] = m.rz0;
+    R[PR_RZ1 * stride] = m.rz1;
+    R[PR_RZ2 * stride] = m.rz2;
+    record_phase2<kCallFree>(m, R, stride);
     double src;
     if (kCallFree || P.source == 1)   // nuSIprop.hpp:656
-        src = P.norm_total / 3.0 * g.sfr[i] * (g.Emax[b] * pw[b + i + 1] - g.Emin[b] * pw[b + i]) / (1 - P.si);
+        src = P.norm_total / 3.0 * g.sfr[i] * (g.Emax[b] * pw[b + i + 1] - g.Emin[b] * pw[b + i]) * rcp_nr(1 - P.si);
     else
         src = lum_out(P, g.z[i], g.sfr[i], g.Emin[b], g.Emax[b]);
     R[PR_SRC * stride] = c * src;
@@ -892,9 +929,10 @@ __global__ __launch_bounds__(kWfMaxThreads) void k_cascade_wf_mfma(GridDev g, co
 //
 // The wavefront and the rank-4 MFMA push are k_cascade_wf_mfma's; the waves are specialised:
 //   * push waves (0 .. nw-3) hold the accumulators of 16 RT rows and run only the block pushes;
-//   * the record wave (nw-2) computes the flux-independent records (1/Z, LU of M, sources) of
-//     stage sg+1 while the chain solves stage sg (a 2-slot ring in LDS): no records phase, no
-//     extra barriers;
+//   * the flux-independent records (1/Z, the LU of M, the sources) come from a 3-slot ring in LDS,
+//     two phases one stage apart: the record wave (nw-2) runs phase 1 (1/Z, M, sources) of stage
+//     sg+2, the chain wave runs phase 2 (the LU) of stage sg+1 beside its solves -- no records
+//     phase, no extra barriers, and neither wave carries a whole record per stage;
 //   * the chain wave (nw-1) solves, lane j = step slot j.
 // Each kind runs its own stage loop with one barrier per stage, so the registers of one kind's
 // code are not live in another's: the accumulators no longer share a budget with the records'
@@ -917,12 +955,18 @@ __global__ __launch_bounds__(kWfMaxThreads) void k_cascade_wf_mfma(GridDev g, co
 // cascade_record stores in PR_SRC
 NUSI_FN double powerlaw_src(const GridDev& g, const Point& P, const double* pw, int i, int b)
 {
-    return g.step_c[i] * (P.norm_total / 3.0 * g.sfr[i] * (g.Emax[b] * pw[b + i + 1] - g.Emin[b] * pw[b + i]) / (1 - P.si));
+    return g.step_c[i] * (P.norm_total / 3.0 * g.sfr[i] * (g.Emax[b] * pw[b + i + 1] - g.Emin[b] * pw[b + i]) * rcp_nr(1 - P.si));
 }
 
+#ifndef NUSI_WS_AB
+#define NUSI_WS_AB 0   // timing experiments only: 1 skip records, 2 skip pushes, 4 skip solves
+#endif
+#ifndef NUSI_WS_P2WAVE
+#define NUSI_WS_P2WAVE 1   // R = 2: the LU phase of the records on a wave of its own (nw-3), not the chain (A/B: C5 cascade 5.75 -> 4.49 ms)
+#endif
 template <int R> struct WsCfg;
 template <> struct WsCfg<1> { static constexpr int RT = 4, kMaxThreads = 512; };   // 6 push waves + 2
-template <> struct WsCfg<2> { static constexpr int RT = 2, kMaxThreads = 832; };   // 11 push waves + 2
+template <> struct WsCfg<2> { static constexpr int RT = 2, kMaxThreads = 832 + 64 * NUSI_WS_P2WAVE; };   // 11 push waves + 2 (3)
 
 template <int NJ, int R>
 __global__ __launch_bounds__(WsCfg<R>::kMaxThreads) __attribute__((amdgpu_waves_per_eu(4, 4)))
@@ -930,7 +974,9 @@ void k_cascade_ws(GridDev g, const Point* __restrict__ pts, const int2* __restri
                   double* __restrict__ flux, double* __restrict__ flux_fla)
 {
     extern __shared__ __attribute__((aligned(16))) double lds[];
-    constexpr int RT = WsCfg<R>::RT, NST = NJ / 16, NF = kWfFields + R - 1;
+    constexpr int RT = WsCfg<R>::RT, NST = NJ / 16;
+    constexpr bool kP2 = R == 2 && NUSI_WS_P2WAVE;   // phase 2 on wave nw-3
+    constexpr int FSRC = kWfFields, FM = kWfFields + R - 1, NF = FM + 6;   // other sources; phase-1 M entries
     const int N = g.N, Nz = g.Nz, T = g.T, nst = Nz - 1;
     const int tid = threadIdx.x, nthr = blockDim.x, lane = tid & 63, wave = tid >> 6, nw = nthr >> 6;
     int pid[R];
@@ -944,8 +990,8 @@ void k_cascade_ws(GridDev g, const Point* __restrict__ pts, const int2* __restri
         single = gp.y < 0;
     }
     double* F = lds;                         // [R][3][N]
-    double* rec = F + 3 * R * N;             // [NF][2][NJ]  records of stage sg in slot sg & 1
-    double* Tp = rec + 2 * NF * NJ;          // [R][8][NJ]   T_j by stage (ring of 8)
+    double* rec = F + 3 * R * N;             // [NF][3][NJ]  records of stage sg in slot sg % 3
+    double* Tp = rec + 3 * NF * NJ;          // [R][8][NJ]   T_j by stage (ring of 8)
     double* AX = Tp + 8 * R * NJ;            // [R][2][4][NJ] rows published by block q (parity q & 1)
     double* rdE = AX + 8 * R * NJ;           // [N]
     double* pw = rdE + N;                    // [R][T + 2]
@@ -994,18 +1040,50 @@ void k_cascade_ws(GridDev g, const Point* __restrict__ pts, const int2* __restri
         }
     }
     __syncthreads();
-    // records of stage s2 for step slot jj (record wave): the fields of point 0, then the other sources
-    auto records = [&](int s2, int jj) {
-        const int b = N - 1 - s2 + jj;
+    // records of stage s2 for step slot jj in ring slot s2 % 3 (fields spaced 3 NJ):
+    //   phase 1 (record wave): 1/Z, the M entries, the sources of every point, sde
+    //   phase 2 (chain wave, one stage later): the LU of M -- cascade_record's operations, split
+    constexpr int S3 = 3 * NJ;
+    auto phase1 = [&](int s2, int jj) {
+        const int b = N - 1 - s2 + jj, i = Nz - 1 - jj;
         if (jj < nst && b >= 0 && b < N) {
-            double* Rw = rec + (s2 & 1) * NJ + jj;
-            cascade_record<true>(gl, P, sGt, sAt, rdE, pw, Nz - 1 - jj, b, Rw, 2 * NJ);
+            double* Rw = rec + (s2 % 3) * NJ + jj;
+            const RecM m = record_phase1(gl, P, sGt, sAt, rdE, i, b);
+            Rw[PR_RZ0 * S3] = m.rz0;
+            Rw[PR_RZ1 * S3] = m.rz1;
+            Rw[PR_RZ2 * S3] = m.rz2;
+            Rw[(FM + 0) * S3] = m.m01;
+            Rw[(FM + 1) * S3] = m.m02;
+            Rw[(FM + 2) * S3] = m.m10;
+            Rw[(FM + 3) * S3] = m.m12;
+            Rw[(FM + 4) * S3] = m.m20;
+            Rw[(FM + 5) * S3] = m.m21;
+            Rw[PR_SDE * S3] = gl.step_s[i] * rdE[b];
 #pragma unroll
-            for (int p = 1; p < R; ++p)
-                Rw[(kWfFields + p - 1) * 2 * NJ] = powerlaw_src(gl, pts[pid[p]], pw + p * (T + 2), Nz - 1 - jj, b);
+            for (int p = 0; p < R; ++p)
+                Rw[(p == 0 ? PR_SRC : FSRC + p - 1) * S3] = powerlaw_src(gl, pts[pid[p]], pw + p * (T + 2), i, b);
         }
     };
-    if (wave == nw - 2) records(0, lane);
+    auto phase2 = [&](int s2, int jj) {
+        const int b = N - 1 - s2 + jj;
+        if (jj < nst && b >= 0 && b < N) {
+            double* Rw = rec + (s2 % 3) * NJ + jj;
+            RecM m;
+            m.m01 = Rw[(FM + 0) * S3];
+            m.m02 = Rw[(FM + 1) * S3];
+            m.m10 = Rw[(FM + 2) * S3];
+            m.m12 = Rw[(FM + 3) * S3];
+            m.m20 = Rw[(FM + 4) * S3];
+            m.m21 = Rw[(FM + 5) * S3];
+            record_phase2<true>(m, Rw, S3);
+        }
+    };
+    if (wave == nw - 2) {
+        phase1(0, lane);
+        if (1 < T) phase1(1, lane);
+    }
+    __syncthreads();
+    if (wave == (kP2 ? nw - 3 : nw - 1)) phase2(0, lane);
     __syncthreads();
 
     if (wave == nw - 1) {
@@ -1024,9 +1102,10 @@ void k_cascade_ws(GridDev g, const Point* __restrict__ pts, const int2* __restri
             double Tn[R];
 #pragma unroll
             for (int p = 0; p < R; ++p) Tn[p] = 0.0;
-            if (act && b >= 0 && b < N) {
-                const double* Rc = rec + (sg & 1) * NJ + j;
-                constexpr int S = 2 * NJ;
+            if (!kP2 && sg + 1 < T && !(NUSI_WS_AB & 1)) phase2(sg + 1, j);   // independent of this stage's solve
+            if (act && b >= 0 && b < N && !(NUSI_WS_AB & 4)) {
+                const double* Rc = rec + (sg % 3) * NJ + j;
+                constexpr int S = S3;
                 const int qq = (sg - 1) >> 2;              // block whose publication serves stage sg
                 const int nu = (d == 0) ? 4 : d;           // columns r+1 .. r+nu not yet pushed
                 const int ax = ((qq & 1) * 4 + (sg - 1 - 4 * qq)) * NJ + j;
@@ -1049,7 +1128,7 @@ void k_cascade_ws(GridDev g, const Point* __restrict__ pts, const int2* __restri
 #pragma unroll
                 for (int p = 0; p < R; ++p) {
                     double* Fp = F + 3 * N * p;
-                    const double src = Rc[(p == 0 ? PR_SRC : kWfFields + p - 1) * S];
+                    const double src = Rc[(p == 0 ? PR_SRC : FSRC + p - 1) * S];
                     double x0, x1, x2;
                     cascade_solve(Fp[b], Fp[N + b], Fp[2 * N + b], cj * s[p], src, u0, u1, u2, rz0, rz1, rz2, pmb, l10,
                                   l20, l21, u01, u02, u12, ru00, ru11, ru22, x0, x1, x2);
@@ -1064,10 +1143,15 @@ void k_cascade_ws(GridDev g, const Point* __restrict__ pts, const int2* __restri
                 for (int p = 0; p < R; ++p) Tp[(p * 8 + (sg & 7)) * NJ + j] = Tn[p];
             __syncthreads();
         }
-    } else if (wave == nw - 2) {
-        // ---- records of the next stage, while the chain solves this one
+    } else if (kP2 && wave == nw - 3) {
         for (int sg = 0; sg < T; ++sg) {
-            if (sg + 1 < T) records(sg + 1, lane);
+            if (sg + 1 < T && !(NUSI_WS_AB & 1)) phase2(sg + 1, lane);
+            __syncthreads();
+        }
+    } else if (wave == nw - 2) {
+        // ---- phase 1 of the records two stages ahead, while the chain solves this stage
+        for (int sg = 0; sg < T; ++sg) {
+            if (sg + 2 < T && !(NUSI_WS_AB & 1)) phase1(sg + 2, lane);
             __syncthreads();
         }
     } else {
@@ -1096,7 +1180,7 @@ void k_cascade_ws(GridDev g, const Point* __restrict__ pts, const int2* __restri
         double ablk[RT];
         load_blk(1, ablk);
         for (int sg = 0; sg < T; ++sg) {
-            if ((sg & 3) == 0) {
+            if ((sg & 3) == 0 && !(NUSI_WS_AB & 2)) {
                 const int q = sg >> 2, r = T - 1 - sg;
                 if (q >= 1) {
 #pragma unroll
@@ -1213,9 +1297,9 @@ static WfGeom ws_geom(const GridDev& g, int NJ, int R)
 {
     WfGeom w;
     const int rows = R == 1 ? 64 : 32;
-    w.nthr = ((g.T - 1 + rows - 1) / rows) * 64 + 128;
+    w.nthr = ((g.T - 1 + rows - 1) / rows) * 64 + 128 + (R == 2 ? 64 * NUSI_WS_P2WAVE : 0);
     w.K = 2;
-    w.lds = sizeof(double) * (3 * (size_t)R * g.N + 2 * (size_t)(kWfFields + R - 1) * NJ + 16 * (size_t)R * NJ + g.N +
+    w.lds = sizeof(double) * (3 * (size_t)R * g.N + 3 * (size_t)(kWfFields + R - 1 + 6) * NJ + 16 * (size_t)R * NJ + g.N +
                               (size_t)R * (g.T + 2) + 6 * (size_t)g.T + 2 * (size_t)g.N + 4 * (size_t)g.Nz);
     return w;
 }

@@ -1,0 +1,51 @@
+"""SURVEY sec. 8 f4 -- cross-point table reuse by index shift, measured on the oracle (CPU).
+
+alpha() sees the energies only through t = -2 m_k E / m_phi^2 and s' = 2 m_k E' / m_phi^2
+(nuSIprop.hpp:1253-1256), and at fixed g its prefactors reduce to functions of g alone
+(Gamma_phi / m_phi = g^2 / 16 pi): m_phi^4 / 2 m_k * g^4 / (8 pi Gamma_phi m_phi^3) = g^2 / m_k, etc.
+On the log-uniform table axis (bin ratio r) the tables of m_phi r^(k/2) are therefore those of m_phi
+shifted by k bins, in exact arithmetic.  In fp64 the bin edges and t, s' round differently, and the
+closed forms amplify that rounding in their small-|t| cancellations: alpha entries move by up to
+~1.5e-6 relative (median ~1e-11), Gamma/alphaTilde by ~1e-13, and the fluxes computed from shifted
+tables move by <= ~2e-11 relative (strong coupling g = 0.5), ~1e-12 at g = 0.1.  That is inside the
+north-star's 1e-9 flux bound but not inside the parity tests' FLUX_RTOL = 1e-11, so the solver does
+not reuse tables across m_phi.  These tests pin the measurement.
+"""
+import numpy as np
+import pytest
+
+from tests import cases
+
+
+def _shift_case(oracle_mod, g, k, N=100):
+    base = dict(cases.C2B_100, N_bins_E=N)
+    r = 10 ** ((base["lEmax"] - base["lEmin"]) / N)
+    o0 = oracle_mod.Oracle(**cases.oracle_kwargs(dict(base, mphi=6e5, g=g)))
+    o1 = oracle_mod.Oracle(**cases.oracle_kwargs(dict(base, mphi=6e5 * r ** (k / 2), g=g)))
+    G0, A0, al0 = o0.tables()
+    G1, A1, al1 = o1.tables()
+    iu = np.triu_indices(o0.T, 1)
+    sel = iu[0] >= k
+    n, m = iu[0][sel], iu[1][sel]
+    a1, a0 = al1[n, m], al0[n - k, m - k]
+    nz = a1 != 0
+    rel_alpha = np.abs(a1[nz] - a0[nz]) / np.abs(a1[nz])
+    rel_gamma = np.max(np.abs(G1[k:] - G0[:-k]) / np.abs(G1[k:]))
+    alS, GS, AS = al1.copy(), G1.copy(), A1.copy()
+    alS[n, m] = al0[n - k, m - k]
+    GS[k:] = G0[:-k]
+    AS[k:] = A0[:-k]
+    _, fl_own = o1.cascade(G1, A1, al1)
+    _, fl_shift = o1.cascade(GS, AS, alS)
+    return rel_alpha, rel_gamma, cases.rel_err(fl_shift, fl_own)
+
+
+@pytest.mark.parametrize("g,k", [(0.1, 2), (0.5, 1)])
+def test_index_shift_reuse_discrepancy(oracle_mod, g, k):
+    rel_alpha, rel_gamma, rel_flux = _shift_case(oracle_mod, g, k)
+    assert np.median(rel_alpha) < 1e-10          # the shift holds: most entries agree to rounding
+    assert 1e-8 < rel_alpha.max() < 1e-5          # ... but the ill-conditioned entries move by ~1e-6
+    assert rel_gamma < 1e-12
+    assert rel_flux < 1e-9                        # inside the north-star bound
+    if g >= 0.5:
+        assert rel_flux > 1e-12                   # measurably outside the cascade's own rounding
