@@ -237,12 +237,13 @@ struct SplineStore {
     }
 };
 
-// weights of interp.hpp:576-636 (the last node's weights are never read)
+// weights of interp.hpp:576-636 (the last node's weights are never read), node-major: the 16 weights
+// of node j at w[16 j + 4 a + b]
 void spline_weights(const std::vector<double>& x, std::vector<double>& w)
 {
     const int n = (int)x.size();
     w.assign((size_t)16 * n, 0.0);
-    auto W = [&](int a, int b, int j) -> double& { return w[(size_t)(a * 4 + b) * n + j]; };
+    auto W = [&](int a, int b, int j) -> double& { return w[(size_t)16 * j + 4 * a + b]; };
     for (int j = 0; j + 1 < n; ++j) {
         const double xm = (j > 0) ? x[j - 1] : 0.0, x0 = x[j], x1 = x[j + 1], x2 = (j + 2 < n) ? x[j + 2] : 0.0;
         if (j == 0) {
@@ -329,6 +330,26 @@ int load_spline(const char* path, int ndim, const int* dims, SplineStore& st, nu
         HIPCHECK(hipMemcpy(dw, w.data(), sizeof(double) * w.size(), hipMemcpyHostToDevice));
         sd.x[i] = dx;
         sd.w[i] = dw;
+        // guide table of the node search (nusi_spline.hpp): gd[u] = the last node <= the lower end of
+        // bucket u, 4 (n-1) buckets over [x[0], x[n-1]]
+        const std::vector<double>& xi = x[i];
+        const int n = dims[i], G = 4 * (n - 1);
+        const double h = (xi[n - 1] - xi[0]) / G;
+        if (n >= 2 && h > 0 && std::is_sorted(xi.begin(), xi.end())) {
+            std::vector<int> gd(G);
+            for (int u = 0; u < G; ++u) {
+                const double lo = xi[0] + u * h;
+                const int k = (int)(std::upper_bound(xi.begin(), xi.end(), lo) - xi.begin()) - 1;
+                gd[u] = std::max(0, std::min(n - 2, k));
+            }
+            int* dg = nullptr;
+            HIPCHECK(hipMalloc(&dg, sizeof(int) * G));
+            st.bufs.push_back(dg);
+            HIPCHECK(hipMemcpy(dg, gd.data(), sizeof(int) * G, hipMemcpyHostToDevice));
+            sd.gd[i] = dg;
+            sd.ng[i] = G;
+            sd.ginv[i] = 1.0 / h;
+        }
     }
     float* df = nullptr;
     HIPCHECK(hipMalloc(&df, sizeof(float) * nf));

@@ -8,8 +8,20 @@
 // the 4x4 Hermite weights (interp.hpp:576-636) are fp64, computed on the host.
 // eval() follows f_eval (interp.hpp:345-467): bounds check (the reference
 // exits on a miss -- here eval returns false and the caller raises a warning
-// bit that the host turns into an error), binary search per axis, 3- or
+// bit that the host turns into an error), node search per axis, 3- or
 // 4-point stencil, tensor product summed with axis 0 fastest.
+//
+// Node search.  The reference binary-searches every axis (isRegular = false,
+// nuSIprop.hpp:168-169): 10 + 10 + 7 dependent loads per lookup, which made
+// the phi-phi alpha table latency-bound at the real 1000x1000x100 geometry.
+// Here each axis carries a guide table over 4 (n-1) equal buckets of its
+// (log'd) range: gd[u] = the last node <= the bucket's lower end.  A query
+// starts from the guide of the bucket BELOW its own (a valid lower bound even
+// when the bucket index rounds up) and steps up while the next node is <= x0.
+// The result is the last node <= x0 -- exactly the index the binary search
+// returns on sorted nodes -- in one guide load and about two node loads.
+// The 16 weights of node k sit together (wt[16 k + 4 a + b], one 128-B line).
+// Without a guide (gd == nullptr) the reference's binary search runs.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -29,9 +41,35 @@ struct SplineDev {
     int ndim = 0;
     int n[kSplMaxDim] = {0, 0, 0};
     const double* x[kSplMaxDim] = {nullptr, nullptr, nullptr};  // nodes, log'd where islog
-    const double* w[kSplMaxDim] = {nullptr, nullptr, nullptr};  // w[i][(a*4+b)*n[i] + node]
+    const double* w[kSplMaxDim] = {nullptr, nullptr, nullptr};  // w[i][16 node + 4 a + b]
+    const int* gd[kSplMaxDim] = {nullptr, nullptr, nullptr};     // guide: gd[i][bucket], ng[i] buckets
+    int ng[kSplMaxDim] = {0, 0, 0};
+    double ginv[kSplMaxDim] = {0.0, 0.0, 0.0};                   // buckets per unit of the axis
     const float* f = nullptr;                                    // values, last index fastest
     int islog[kSplMaxDim + 1] = {0, 0, 0, 0};
+
+    // the last node <= x0 (x[0] < x0 < x[n-1])
+    NUSI_FN int search(int i, double x0) const
+    {
+        const double* xi = x[i];
+        if (gd[i]) {
+            int u = (int)((x0 - xi[0]) * ginv[i]) - 1;
+            u = u < 0 ? 0 : (u >= ng[i] ? ng[i] - 1 : u);
+            int kk = gd[i][u];
+            while (xi[kk + 1] <= x0) ++kk;
+            return kk;
+        }
+        int L = 0, R = n[i] - 1, kk = 0;
+        while (L <= R) {
+            const int m = (L + R) / 2;
+            if (x0 < xi[m]) R = m - 1;
+            else {
+                kk = m;
+                L = m + 1;
+            }
+        }
+        return kk;
+    }
 
     NUSI_FN bool eval(const double* x0in, double& out) const
     {
@@ -45,15 +83,7 @@ struct SplineDev {
                 out = 0.0;
                 return false;
             }
-            int L = 0, R = n[i] - 1, kk = 0;
-            while (L <= R) {
-                const int m = (L + R) / 2;
-                if (x0[i] < xi[m]) R = m - 1;
-                else {
-                    kk = m;
-                    L = m + 1;
-                }
-            }
+            const int kk = search(i, x0[i]);
             k[i] = kk;
             if (kk == 0) { lo[i] = 0; cnt[i] = 3; }
             else if (kk == n[i] - 2) { lo[i] = kk - 1; cnt[i] = 3; }
@@ -64,10 +94,8 @@ struct SplineDev {
         double fac[kSplMaxDim][4];
         for (int i = 0; i < ndim; ++i)
             for (int a = 0; a < cnt[i]; ++a) {
-                const double* wi = w[i];
-                const int ni = n[i], kk = k[i];
-                fac[i][a] = t[i] * t[i] * t[i] * wi[(a * 4 + 0) * ni + kk] + (t[i] * t[i]) * wi[(a * 4 + 1) * ni + kk]
-                            + t[i] * wi[(a * 4 + 2) * ni + kk] + wi[(a * 4 + 3) * ni + kk];
+                const double* wk = w[i] + 16 * k[i] + 4 * a;
+                fac[i][a] = t[i] * t[i] * t[i] * wk[0] + (t[i] * t[i]) * wk[1] + t[i] * wk[2] + wk[3];
             }
         int idx[kSplMaxDim] = {0, 0, 0};
         double res = 0;
