@@ -237,7 +237,6 @@ def main():
     arr = plan.params_array(pts)
     from nusiprop_amd import _lib
     plan.set_cascade({"mfma": _lib.CASCADE_MFMA, "wf": _lib.CASCADE_WAVEFRONT, "auto": _lib.CASCADE_AUTO}[args.cascade])
-    casc_kernel = {"mfma": "k_cascade_wf_mfma", "wf": "k_cascade_wf", "auto": "k_cascade_wf"}[args.cascade]
     dev = torch.device("cuda", local)
     flux = torch.empty((P, 3, plan.N), dtype=torch.float64, device=dev)
     fla = torch.empty((P, 3, plan.N), dtype=torch.float64, device=dev)
@@ -271,8 +270,7 @@ def main():
     oob = sum(1 for w in plan.warnings(P) if w & 8)
 
     N, Nz = plan.N, plan.Nz
-    if not scan.cascade_mfma_flops_per_point(N, Nz):   # grid beyond the wavefront kernels (Nz-1 > 48): per-step chain
-        casc_kernel, args.cascade = "k_cascade_reg", "reg"
+    alpha_kernel, casc_kernel = plan.kernels()   # what the library launched (nusi_plan_kernels)
     props = world * P * args.steps
     value = props / dt
     casc_bytes = scan.cascade_bytes_per_point(N, Nz) * P
@@ -288,7 +286,7 @@ def main():
         traffic = pmc.get("k_cascade_bytes_per_launch")
         tsrc = os.path.relpath(tj, ROOT)
     achieved = casc_bytes / casc_s / 1e9
-    casc_min = scan.cascade_min_bytes_per_point(N, Nz) * P
+    casc_min = scan.cascade_min_bytes_per_point(N, Nz, passes=casc_kernel == "k_cascade_ws_passes") * P
     step_ms = sum(sum_ms) / max(ncalls, 1)
     out = {
         "metric": METRIC,
@@ -307,7 +305,7 @@ def main():
                    "lEmax": p0["lEmax"], "parallelism": "independent points, %d GPU(s), no collective" % world},
         "stage_ms_per_step": {"gamma_alphatilde": sum_ms[0] / max(ncalls, 1), "alpha": sum_ms[1] / max(ncalls, 1),
                               "cascade": sum_ms[2] / max(ncalls, 1)},
-        "alpha_table": {"kernel": "k_alpha_tile", "bound": "fp64 VALU (transcendental)",
+        "alpha_table": {"kernel": alpha_kernel, "bound": "fp64 VALU (transcendental)",
                         "entries_per_s": scan.alpha_entries_per_point(N, Nz) * P / alpha_s,
                         "avg_step_ms": alpha_s * 1e3, "share_of_step": alpha_s * 1e3 / step_ms},
         # the metric's "achieved HBM GB/s on the cascade kernel".  The wavefront kernel reads each alpha column
@@ -323,7 +321,7 @@ def main():
         "invalid_outputs": bad,
         "phiphi_lookups_out_of_range": oob,
     }
-    if args.cascade == "mfma":   # the push on the fp64 matrix cores: issued MFMA flops over the kernel's time
+    if args.cascade == "mfma" and "ws" in casc_kernel or "mfma" in casc_kernel:   # the push on the matrix cores
         mf = scan.cascade_mfma_flops_per_point(N, Nz) * P
         out["roofline_cascade"]["mfma"] = {"flops_per_launch": mf, "achieved": mf / casc_s / 1e12,
                                            "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
@@ -332,7 +330,7 @@ def main():
     fl = pmc.get("k_alpha_fp64_flops_per_step")
     if fl:   # the dominant kernel: executed fp64 VALU flops (PMC counts) per second vs the fp64 vector peak
         ach = fl / alpha_s / 1e12
-        out["roofline"] = {"bound": "valu", "kernel": "k_alpha_tile", "achieved": ach, "peak": FP64_PEAK_TFLOPS,
+        out["roofline"] = {"bound": "valu", "kernel": alpha_kernel, "achieved": ach, "peak": FP64_PEAK_TFLOPS,
                            "unit": "TFLOP/s", "frac": ach / FP64_PEAK_TFLOPS,
                            "traffic": pmc.get("k_alpha_hbm_bytes_per_step"), "traffic_source": tsrc,
                            "flops": "executed fp64 VALU (SQ_INSTS_VALU_{ADD,MUL,TRANS}_F64 + 2 FMA) x 64 lanes, "

@@ -153,6 +153,10 @@ int nusi_plan_profile_end(nusi_plan *plan, double *sum_ms3, int *ncalls);
 int nusi_plan_set_cascade(nusi_plan *plan, int kind);
 /* per-point NUSI_WARN_* bits of the last call */
 int nusi_plan_warnings(nusi_plan *plan, int *out, int n);
+/* Names of the main alpha-table and cascade kernels the last call launched (static strings, e.g.
+ * "k_alpha_batch", "k_cascade_ws"); for reports -- bench.py's roofline lines.  No reference
+ * counterpart. */
+int nusi_plan_kernels(const nusi_plan *plan, const char **alpha, const char **cascade);
 /* Copy point `i`'s Stage-A tables of the last call to the host (parity
  * tests): Gamma[T], alphaTilde[T], alpha packed transposed [T(T-1)/2] with
  * alpha(n,m), n<m, at m(m-1)/2+n.  Any pointer may be NULL. */

@@ -51,6 +51,7 @@ EXPORTS = [
     "nusi_plan_create", "nusi_plan_destroy", "nusi_plan_load_phiphi", "nusi_plan_grid", "nusi_plan_evolve",
     "nusi_plan_evolve_host", "nusi_plan_stage_ms", "nusi_plan_profile_begin", "nusi_plan_profile_end",
     "nusi_plan_warnings", "nusi_plan_tables", "nusi_evolve_batch", "nusi_plan_set_cascade",
+    "nusi_plan_kernels",
 ]
 
 # nusi_plan_set_cascade kinds (include/nusi.h)
@@ -100,6 +101,7 @@ def load():
         "nusi_plan_tables": (i, [vp, i, dp, dp, dp]),
         "nusi_evolve_batch": (i, [i, pp, i, dp, dp]),
         "nusi_plan_set_cascade": (i, [vp, i]),
+        "nusi_plan_kernels": (i, [vp, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_char_p)]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)

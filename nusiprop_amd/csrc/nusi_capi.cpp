@@ -396,6 +396,8 @@ struct nusi_plan {
     int last_n = 0;
     std::vector<hipEvent_t> prof_ev;   // 4 per recorded call
     hipEvent_t last_ev[4] = {nullptr, nullptr, nullptr, nullptr};   // the latest call's stage events (handles)
+    const char* alpha_kernel = "";     // main kernels of the latest call (nusi_plan_kernels)
+    const char* cascade_kernel = "";
     int prof_max = 0, prof_n = 0;
     int cascade_kind = NUSI_CASCADE_AUTO;
     double U2[2][9];
@@ -761,6 +763,8 @@ int nusi_plan_evolve(nusi_plan* pl, const nusi_params* pts, int n, double* d_flu
         HIPCHECK(nusi::launch_cascade(pl->gd, pl->d_pts, n, pl->tabs, d_flux, d_fla, s, pl->cascade_kind, all_pl, all_nr));
     HIPCHECK(hipEventRecord(ev[3], s));
     HIPCHECK(hipEventRecord(pl->ev_done, s));
+    pl->alpha_kernel = nusi::last_alpha_kernel();
+    pl->cascade_kernel = nusi::last_cascade_kernel();
     for (int k = 0; k < 4; ++k) pl->last_ev[k] = ev[k];   // stage_ms / warnings / tables refer to the latest call
     pl->ran = true;
     pl->last_n = n;
@@ -827,6 +831,14 @@ int nusi_plan_warnings(nusi_plan* pl, int* out, int n)
     std::vector<int> w(pl->last_ntab);
     HIPCHECK(hipMemcpy(w.data(), pl->d_warn, sizeof(int) * w.size(), hipMemcpyDeviceToHost));
     for (int i = 0; i < n; ++i) out[i] = w[pl->slot_of[i]];
+    return NUSI_OK;
+}
+
+int nusi_plan_kernels(const nusi_plan* pl, const char** alpha, const char** cascade)
+{
+    if (!pl->ran) return fail(NUSI_ESTATE, "no evolve has run on this plan");
+    if (alpha) *alpha = pl->alpha_kernel;
+    if (cascade) *cascade = pl->cascade_kernel;
     return NUSI_OK;
 }
 

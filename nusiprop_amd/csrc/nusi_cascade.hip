@@ -1237,6 +1237,300 @@ void k_cascade_ws(GridDev g, const Point* __restrict__ pts, const int2* __restri
     }
 }
 
+// ---------------------------------------------------------------------------
+// Step passes: k_cascade_ws for grids with more redshift steps than the slots in flight (e.g.
+// BASELINE C3: N = 1200, 134 steps).
+//
+// The wavefront keeps every step in flight, and its accumulators (T-1 rows x steps) outgrow a CU's
+// registers.  The steps are therefore taken NJ = 16 at a time: pass p runs the wavefront of step
+// slots [16 p, 16 p + 16) over N + 15 stages, its local stage 0 reading table column T-1-16p (along
+// a stage b + i is constant within the pass as before).  F[3][N] stays in LDS from pass to pass --
+// the first step of pass p starts from the last step of pass p-1, as step i starts from step i+1 in
+// the reference's loop (nuSIprop.hpp:257-315) -- and the accumulators, the T_j ring and the
+// published rows restart from zero.  Each pass reads its columns once (the table is read
+// ceil(steps / 16) times).  Push waves own 16 RT = 128 rows; phase 2 of the records has a wave of
+// its own.  Everything else -- records, solves, the rank-4 MFMA push -- is k_cascade_ws<NJ, 1>'s code;
+// one pass (steps <= 16) gives that kernel's fluxes bit for bit (test_cascade_step_passes).  The body
+// is a separate kernel rather than a mode of k_cascade_ws because the 48-slot instantiation of that
+// kernel sits on the 128-VGPR edge and spills as soon as its code changes shape.
+// ---------------------------------------------------------------------------
+constexpr int kWsBigNJ = 16, kWsBigRT = 8;   // step slots per pass, 16-row tiles per push wave
+
+template <int NJ>
+__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4, 4)))
+void k_cascade_wsp(GridDev g, const Point* __restrict__ pts, TablesDev t, double* __restrict__ flux,
+                   double* __restrict__ flux_fla)
+{
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    constexpr int R = 1, RT = kWsBigRT, NST = NJ / 16;
+    constexpr bool kP2 = NUSI_WS_P2WAVE;   // phase 2 on wave nw-3
+    constexpr int FSRC = kWfFields, FM = kWfFields + R - 1, NF = FM + 6;   // other sources; phase-1 M entries
+    const int N = g.N, Nz = g.Nz, T = g.T, nst = Nz - 1;
+    const int tid = threadIdx.x, nthr = blockDim.x, lane = tid & 63, wave = tid >> 6, nw = nthr >> 6;
+    const int pid[R] = {(int)blockIdx.x};   // one point per workgroup
+    constexpr bool single = true;
+    double* F = lds;                         // [R][3][N]
+    double* rec = F + 3 * R * N;             // [NF][3][NJ]  records of stage sg in slot sg % 3
+    double* Tp = rec + 3 * NF * NJ;          // [R][8][NJ]   T_j by stage (ring of 8)
+    double* AX = Tp + 8 * R * NJ;            // [R][2][4][NJ] rows published by block q (parity q & 1)
+    double* rdE = AX + 8 * R * NJ;           // [N]
+    double* pw = rdE + N;                    // [R][T + 2]
+    double* sGt = pw + R * (T + 2);
+    double* sAt = sGt + T;
+    double* sdg = sAt + T;                   // [4][T]: alpha(n, n+k), k = 1..4 (0 past the table)
+    double* sEmin = sdg + 4 * T;
+    double* sEmax = sEmin + N;
+    double* sgz = sEmax + N;                 // z, step_c, step_s, sfr [Nz each]
+    GridDev gl = g;
+    gl.Emin = sEmin;
+    gl.Emax = sEmax;
+    gl.z = sgz;
+    gl.step_c = sgz + Nz;
+    gl.step_s = sgz + 2 * Nz;
+    gl.sfr = sgz + 3 * Nz;
+    const Point& P = pts[pid[0]];
+    const double* __restrict__ Al = t.A + (size_t)P.tslot * g.PT;
+    {
+        const double* __restrict__ Gt = t.G + (size_t)P.tslot * T;
+        const double* __restrict__ At = t.At + (size_t)P.tslot * T;
+        for (int b = tid; b < 3 * R * N; b += nthr) F[b] = 0.0;
+        for (int j = tid; j < 16 * R * NJ; j += nthr) Tp[j] = 0.0;   // Tp and AX
+        for (int n = tid; n < T; n += nthr) {
+            sGt[n] = Gt[n];
+            sAt[n] = At[n];
+#pragma unroll
+            for (int k = 1; k <= 4; ++k) sdg[(k - 1) * T + n] = (n + k < T) ? Al[(size_t)(n + k) * (n + k - 1) / 2 + n] : 0.0;
+        }
+        for (int b = tid; b < N; b += nthr) { sEmin[b] = g.Emin[b]; sEmax[b] = g.Emax[b]; }
+        for (int i = tid; i < Nz; i += nthr) {
+            sgz[i] = g.z[i];
+            sgz[Nz + i] = g.step_c[i];
+            sgz[2 * Nz + i] = g.step_s[i];
+            sgz[3 * Nz + i] = g.sfr[i];
+        }
+        cascade_aux_init(g, P, rdE, pw, tid, nthr);
+#pragma unroll
+        for (int p = 1; p < R; ++p) {   // the other points' pw[] (cascade_aux_init's expression)
+            const double si = pts[pid[p]].si;
+            for (int e = tid + 1; e <= T + 1; e += nthr) {
+                const int i = min(Nz - 1, max(1, e - N + 1)), b = e - i;
+                const double E = (b < N) ? g.Emin[b] : g.Emax[N - 1];
+                pw[p * (T + 2) + e] = nm::pow(E / 1e14 * (1 + g.z[i]), -si);
+            }
+        }
+    }
+    __syncthreads();
+    // records of stage s2 for step slot jj in ring slot s2 % 3 (fields spaced 3 NJ):
+    //   phase 1 (record wave): 1/Z, the M entries, the sources of every point, sde
+    //   phase 2 (chain wave, one stage later): the LU of M -- cascade_record's operations, split
+    constexpr int S3 = 3 * NJ;
+    int jb = 0;   // first step slot of the current pass (step i = Nz-1-jb-j for slot j)
+    auto phase1 = [&](int s2, int jj) {
+        const int b = N - 1 - s2 + jj, i = Nz - 1 - jb - jj;
+        if (jj < NJ && jb + jj < nst && b >= 0 && b < N) {
+            double* Rw = rec + (s2 % 3) * NJ + jj;
+            const RecM m = record_phase1(gl, P, sGt, sAt, rdE, i, b);
+            Rw[PR_RZ0 * S3] = m.rz0;
+            Rw[PR_RZ1 * S3] = m.rz1;
+            Rw[PR_RZ2 * S3] = m.rz2;
+            Rw[(FM + 0) * S3] = m.m01;
+            Rw[(FM + 1) * S3] = m.m02;
+            Rw[(FM + 2) * S3] = m.m10;
+            Rw[(FM + 3) * S3] = m.m12;
+            Rw[(FM + 4) * S3] = m.m20;
+            Rw[(FM + 5) * S3] = m.m21;
+            Rw[PR_SDE * S3] = gl.step_s[i] * rdE[b];
+#pragma unroll
+            for (int p = 0; p < R; ++p)
+                Rw[(p == 0 ? PR_SRC : FSRC + p - 1) * S3] = powerlaw_src(gl, pts[pid[p]], pw + p * (T + 2), i, b);
+        }
+    };
+    auto phase2 = [&](int s2, int jj) {
+        const int b = N - 1 - s2 + jj;
+        if (jj < NJ && jb + jj < nst && b >= 0 && b < N) {
+            double* Rw = rec + (s2 % 3) * NJ + jj;
+            RecM m;
+            m.m01 = Rw[(FM + 0) * S3];
+            m.m02 = Rw[(FM + 1) * S3];
+            m.m10 = Rw[(FM + 2) * S3];
+            m.m12 = Rw[(FM + 3) * S3];
+            m.m20 = Rw[(FM + 4) * S3];
+            m.m21 = Rw[(FM + 5) * S3];
+            record_phase2<true>(m, Rw, S3);
+        }
+    };
+    const int npass = (nst + NJ - 1) / NJ;
+#pragma unroll 1
+    for (int pass = 0; pass < npass; ++pass) {
+    jb = pass * NJ;
+    const int Ts = N - 1 + (nst - jb < NJ ? nst - jb : NJ);   // stages of this pass
+    const int c0 = T - 1 - jb;                                 // the table column of local stage 0
+    if (pass > 0) {   // accumulators, T_j ring and published rows restart; F carries over
+        __syncthreads();
+        for (int j = tid; j < 16 * R * NJ; j += nthr) Tp[j] = 0.0;
+        __syncthreads();
+    }
+    if (wave == nw - 2) {
+        phase1(0, lane);
+        if (1 < Ts) phase1(1, lane);
+    }
+    __syncthreads();
+    if (wave == (kP2 ? nw - 3 : nw - 1)) phase2(0, lane);
+    __syncthreads();
+
+    if (wave == nw - 1) {
+        // ---- chain: lane j solves (step jb+j, bin N-1-sg+j) of every point at stage sg
+        const int j = lane;
+        const bool act = j < NJ && jb + j < nst;
+        const double u0 = P.u[0], u1 = P.u[1], u2 = P.u[2];
+        const double cj = act ? gl.step_c[Nz - 1 - jb - j] : 0.0;
+        for (int sg0 = 0; sg0 < Ts; sg0 += 4)
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+            const int sg = sg0 + d;
+            if (sg >= Ts) break;
+            const int r = c0 - sg;
+            const int b = N - 1 - sg + j;
+            double Tn[R];
+#pragma unroll
+            for (int p = 0; p < R; ++p) Tn[p] = 0.0;
+            if (!kP2 && sg + 1 < Ts && !(NUSI_WS_AB & 1)) phase2(sg + 1, j);   // independent of this stage's solve
+            if (act && b >= 0 && b < N && !(NUSI_WS_AB & 4)) {
+                const double* Rc = rec + (sg % 3) * NJ + j;
+                constexpr int S = S3;
+                const int qq = (sg - 1) >> 2;              // block whose publication serves stage sg
+                const int nu = (d == 0) ? 4 : d;           // columns r+1 .. r+nu not yet pushed
+                const int ax = ((qq & 1) * 4 + (sg - 1 - 4 * qq)) * NJ + j;
+                double s[R];
+#pragma unroll
+                for (int p = 0; p < R; ++p) s[p] = AX[p * 8 * NJ + ax];
+#pragma unroll
+                for (int k = 4; k >= 1; --k)
+                    if (k <= nu) {
+                        const double a = sdg[(k - 1) * T + r];
+#pragma unroll
+                        for (int p = 0; p < R; ++p) s[p] = fma(a, Tp[(p * 8 + ((sg - k) & 7)) * NJ + j], s[p]);
+                    }
+                const double rz0 = Rc[PR_RZ0 * S], rz1 = Rc[PR_RZ1 * S], rz2 = Rc[PR_RZ2 * S];
+                const int pmb = (int)Rc[kPreFields * S];
+                const double l10 = Rc[PR_L10 * S], l20 = Rc[PR_L20 * S], l21 = Rc[PR_L21 * S];
+                const double u01 = Rc[PR_U01 * S], u02 = Rc[PR_U02 * S], u12 = Rc[PR_U12 * S];
+                const double ru00 = Rc[PR_RU00 * S], ru11 = Rc[PR_RU11 * S], ru22 = Rc[PR_RU22 * S];
+                const double sde = Rc[PR_SDE * S];
+#pragma unroll
+                for (int p = 0; p < R; ++p) {
+                    double* Fp = F + 3 * N * p;
+                    const double src = Rc[(p == 0 ? PR_SRC : FSRC + p - 1) * S];
+                    double x0, x1, x2;
+                    cascade_solve(Fp[b], Fp[N + b], Fp[2 * N + b], cj * s[p], src, u0, u1, u2, rz0, rz1, rz2, pmb, l10,
+                                  l20, l21, u01, u02, u12, ru00, ru11, ru22, x0, x1, x2);
+                    Fp[b] = x0;
+                    Fp[N + b] = x1;
+                    Fp[2 * N + b] = x2;
+                    if (b > 0) Tn[p] = (u0 * x0 + u1 * x1 + u2 * x2) * sde;
+                }
+            }
+            if (act)
+#pragma unroll
+                for (int p = 0; p < R; ++p) Tp[(p * 8 + (sg & 7)) * NJ + j] = Tn[p];
+            __syncthreads();
+        }
+    } else if (kP2 && wave == nw - 3) {
+        for (int sg = 0; sg < Ts; ++sg) {
+            if (sg + 1 < Ts && !(NUSI_WS_AB & 1)) phase2(sg + 1, lane);
+            __syncthreads();
+        }
+    } else if (wave == nw - 2) {
+        // ---- phase 1 of the records two stages ahead, while the chain solves this stage
+        for (int sg = 0; sg < Ts; ++sg) {
+            if (sg + 2 < Ts && !(NUSI_WS_AB & 1)) phase1(sg + 2, lane);
+            __syncthreads();
+        }
+    } else {
+        // ---- push: block q (stage 4q) adds columns c0+1-4q .. c0+4-4q (the T of stages 4q-1 .. 4q-4) into
+        // the rows below r = c0-4q, then publishes rows r-1 .. r-4 (the rows of stages 4q+1 .. 4q+4)
+        const int rw0 = wave * 16 * RT;
+        nusi_f64x4 acc[R][RT][NST];
+#pragma unroll
+        for (int p = 0; p < R; ++p)
+#pragma unroll
+            for (int a = 0; a < RT; ++a)
+#pragma unroll
+                for (int s = 0; s < NST; ++s) acc[p][a][s] = nusi_f64x4{0.0, 0.0, 0.0, 0.0};
+        // A operands: alpha(row, column), row = tile row + (lane & 15), column = first block column + (lane >> 4);
+        // rows clamped into the column (those rows are consumed)
+        auto load_blk = [&](int q, double (&dst)[RT]) {
+            int c = c0 + 1 - 4 * q + (lane >> 4);
+            c = c < 1 ? 1 : (c > T - 1 ? T - 1 : c);
+            const size_t cb = (size_t)c * (c - 1) / 2;
+#pragma unroll
+            for (int a = 0; a < RT; ++a) {
+                const int row = rw0 + 16 * a + (lane & 15);
+                dst[a] = Al[cb + (row < c - 1 ? row : c - 1)];
+            }
+        };
+        double ablk[RT];
+        load_blk(1, ablk);
+        for (int sg = 0; sg < Ts; ++sg) {
+            if ((sg & 3) == 0 && !(NUSI_WS_AB & 2)) {
+                const int q = sg >> 2, r = c0 - sg;
+                if (q >= 1) {
+#pragma unroll
+                    for (int s = 0; s < NST; ++s) {
+                        const int bi = ((sg - 1 - (lane >> 4)) & 7) * NJ + 16 * s + (lane & 15);
+                        double bop[R];
+#pragma unroll
+                        for (int p = 0; p < R; ++p) bop[p] = Tp[p * 8 * NJ + bi];
+#pragma unroll
+                        for (int a = 0; a < RT; ++a)
+                            if (rw0 + 16 * a < r)   // tiles wholly at or above r hold consumed rows only
+#pragma unroll
+                                for (int p = 0; p < R; ++p)
+                                    acc[p][a][s] = __builtin_amdgcn_mfma_f64_16x16x4f64(ablk[a], bop[p], acc[p][a][s], 0, 0, 0);
+                    }
+                    load_blk(q + 1, ablk);
+                }
+                const int hi = r - 1;
+#pragma unroll
+                for (int a = 0; a < RT; ++a)
+                    if (rw0 + 16 * a <= hi && rw0 + 16 * a + 15 >= hi - 3)   // uniform: tiles holding those rows
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) {
+                            const int row = rw0 + 16 * a + (lane >> 4) + 4 * e;
+                            const int slot = hi - row;
+                            if (slot >= 0 && slot < 4)
+#pragma unroll
+                                for (int s = 0; s < NST; ++s) {
+                                    const int o = ((q & 1) * 4 + slot) * NJ + 16 * s + (lane & 15);
+#pragma unroll
+                                    for (int p = 0; p < R; ++p) AX[p * 8 * NJ + o] = acc[p][a][s][e];
+                                }
+                        }
+            }
+            __syncthreads();
+        }
+    }
+    }   // passes
+    __syncthreads();   // the last pass's solves are in F
+    // finalise (nuSIprop.hpp:328-336)
+#pragma unroll
+    for (int p = 0; p < R; ++p) {
+        if (p > 0 && single) break;
+        const Point& Q = pts[pid[p]];
+        const double* Fp = F + 3 * N * p;
+        double* fo = flux + (size_t)pid[p] * 3 * N;
+        double* fl = flux_fla + (size_t)pid[p] * 3 * N;
+        for (int b = tid; b < N; b += nthr) {
+            const double dE = g.Emax[b] - g.Emin[b];
+            const double f0 = Fp[b] / dE, f1 = Fp[N + b] / dE, f2 = Fp[2 * N + b] / dE;
+            fo[b] = f0;
+            fo[N + b] = f1;
+            fo[2 * N + b] = f2;
+            for (int f = 0; f < 3; ++f) fl[f * N + b] = Q.U2[3 * f + 0] * f0 + Q.U2[3 * f + 1] * f1 + Q.U2[3 * f + 2] * f2;
+        }
+    }
+}
+
 // launch geometry of the wavefront kernel: one thread per pushed row (T-1), whole waves; K stages
 // of records per batch, as many as the threads cover and kWfMaxLds allows
 constexpr size_t kWfMaxLds = 64 * 1024;
@@ -1292,12 +1586,15 @@ static bool mf_fits(const GridDev& g)
 }
 
 // the warp-specialised kernel: push waves of 16 RT rows each, then the record and chain waves
-constexpr size_t kWsMaxLds[3] = {0, 80 * 1024, 150 * 1024};   // R = 1: two workgroups per CU
+// (R = 3 here: the step-pass kernel, one right-hand side, 128 rows per push wave)
+constexpr size_t kWsMaxLds[4] = {0, 80 * 1024, 150 * 1024, 160 * 1024};   // R = 1: two workgroups per CU
 static WfGeom ws_geom(const GridDev& g, int NJ, int R)
 {
     WfGeom w;
-    const int rows = R == 1 ? 64 : 32;
-    w.nthr = ((g.T - 1 + rows - 1) / rows) * 64 + 128 + (R == 2 ? 64 * NUSI_WS_P2WAVE : 0);
+    const bool big = R == 3;
+    if (big) R = 1;
+    const int rows = big ? 16 * kWsBigRT : R == 1 ? 64 : 32;
+    w.nthr = ((g.T - 1 + rows - 1) / rows) * 64 + 128 + ((R == 2 || big) ? 64 * NUSI_WS_P2WAVE : 0);
     w.K = 2;
     w.lds = sizeof(double) * (3 * (size_t)R * g.N + 3 * (size_t)(kWfFields + R - 1 + 6) * NJ + 16 * (size_t)R * NJ + g.N +
                               (size_t)R * (g.T + 2) + 6 * (size_t)g.T + 2 * (size_t)g.N + 4 * (size_t)g.Nz);
@@ -1310,6 +1607,16 @@ bool cascade_ws_fits(const GridDev& g, int R)
     const WfGeom w = ws_geom(g, nj, R);
     return w.nthr <= (R == 1 ? WsCfg<1>::kMaxThreads : WsCfg<2>::kMaxThreads) && w.lds <= kWsMaxLds[R];
 }
+// the step-pass kernel: any number of redshift steps, T - 1 <= 13 x 128 rows
+bool cascade_wsp_fits(const GridDev& g)
+{
+    if (g.T < 2 || g.Nz < 2) return false;
+    const WfGeom w = ws_geom(g, kWsBigNJ, 3);
+    return w.nthr <= 1024 && w.lds <= kWsMaxLds[3];
+}
+
+static thread_local const char* t_cascade_kernel = "";   // the kernel the latest launch on this thread chose
+const char* last_cascade_kernel() { return t_cascade_kernel; }
 
 template <int NJ, int R>
 static void launch_ws_nj(const GridDev& g, const Point* pts, const int2* groups, int nwg, TablesDev t, double* flux,
@@ -1323,6 +1630,7 @@ hipError_t launch_cascade_ws(const GridDev& g, const Point* pts, int R, const in
                              double* flux, double* flux_fla, hipStream_t s)
 {
     if (!cascade_ws_fits(g, R)) return hipErrorInvalidValue;
+    t_cascade_kernel = R == 2 ? "k_cascade_ws_mrhs" : "k_cascade_ws";
     const int nj = wf_nj(g);
     if (R == 1) {
         if (nj == 16) launch_ws_nj<16, 1>(g, pts, groups, nwg, t, flux, flux_fla, s);
@@ -1333,6 +1641,15 @@ hipError_t launch_cascade_ws(const GridDev& g, const Point* pts, int R, const in
         else if (nj == 32) launch_ws_nj<32, 2>(g, pts, groups, nwg, t, flux, flux_fla, s);
         else launch_ws_nj<48, 2>(g, pts, groups, nwg, t, flux, flux_fla, s);
     }
+    return hipGetLastError();
+}
+
+hipError_t launch_cascade_wsp(const GridDev& g, const Point* pts, int npts, TablesDev t, double* flux, double* flux_fla,
+                              hipStream_t s)
+{
+    if (!cascade_wsp_fits(g)) return hipErrorInvalidValue;
+    const WfGeom w = ws_geom(g, kWsBigNJ, 3);
+    hipLaunchKernelGGL((k_cascade_wsp<kWsBigNJ>), dim3(npts), dim3(w.nthr), w.lds, s, g, pts, t, flux, flux_fla);
     return hipGetLastError();
 }
 
@@ -1390,9 +1707,19 @@ hipError_t launch_cascade(const GridDev& g, const Point* pts, int npts, TablesDe
     }
     if (kind == NUSI_CASCADE_MFMA && all_power_law && all_nonres && cascade_ws_fits(g, 1)) {
         const char* ws = getenv("NUSI_CASCADE_WS");   // A/B: 0 = k_cascade_wf_mfma
-        if (!ws || ws[0] != '0') return launch_cascade_ws(g, pts, 1, nullptr, npts, t, flux, flux_fla, s);
+        if (!ws || ws[0] != '0') return launch_cascade_ws(g, pts, 1, nullptr, npts, t, flux, flux_fla, s);   // names itself
+    }
+    if (kind == NUSI_CASCADE_MFMA && all_power_law && all_nonres && cascade_wsp_fits(g)) {
+        // NUSI_CASCADE_WSP (A/B, tests): 0 = never the step-pass kernel, 1 = also where one pass fits
+        const char* wsp = getenv("NUSI_CASCADE_WSP");
+        if ((!wf_nj(g) && !(wsp && wsp[0] == '0')) || (wsp && wsp[0] == '1'))
+        {
+            t_cascade_kernel = "k_cascade_ws_passes";
+            return launch_cascade_wsp(g, pts, npts, t, flux, flux_fla, s);
+        }
     }
     if (kind == NUSI_CASCADE_MFMA && mf_fits(g)) {
+        t_cascade_kernel = "k_cascade_wf_mfma";
         switch (wf_nj(g)) {
         case 16: launch_mf<16>(g, pts, npts, t, flux, flux_fla, s, all_power_law); break;
         case 32: launch_mf<32>(g, pts, npts, t, flux, flux_fla, s, all_power_law); break;
@@ -1401,6 +1728,7 @@ hipError_t launch_cascade(const GridDev& g, const Point* pts, int npts, TablesDe
         return hipGetLastError();
     }
     if ((kind == NUSI_CASCADE_AUTO || kind == NUSI_CASCADE_WAVEFRONT || kind == NUSI_CASCADE_MFMA) && wf_fits(g)) {
+        t_cascade_kernel = "k_cascade_wf";
         switch (wf_nj(g)) {
         case 16: launch_wf<16>(g, pts, npts, t, flux, flux_fla, s, all_power_law); break;
         case 32: launch_wf<32>(g, pts, npts, t, flux, flux_fla, s, all_power_law); break;
@@ -1408,8 +1736,10 @@ hipError_t launch_cascade(const GridDev& g, const Point* pts, int npts, TablesDe
         }
         return hipGetLastError();
     }
+    t_cascade_kernel = "k_cascade_reg";
     if (kind != NUSI_CASCADE_LDS && dispatch_reg(nq, g, pts, npts, t, flux, flux_fla, s, RegNQ{}))
         return hipGetLastError();
+    t_cascade_kernel = "k_cascade";
     const size_t lds = cascade_lds_bytes(g.N);
     hipLaunchKernelGGL(k_cascade, dim3(npts), dim3(64), lds, s, g, pts, t, flux, flux_fla);
     return hipGetLastError();

@@ -64,7 +64,15 @@ hipError_t launch_cascade(const GridDev& g, const Point* pts, int npts, TablesDe
 // or R = 2, groups[k] = two points sharing one table slot (y < 0: one point); non-resonant points with the
 // power-law source only.  Fluxes equal k_cascade_wf_mfma's bit for bit.
 bool cascade_ws_fits(const GridDev& g, int R);
+bool cascade_wsp_fits(const GridDev& g);   // the step-pass kernel (any number of redshift steps)
+hipError_t launch_cascade_wsp(const GridDev& g, const Point* pts, int npts, TablesDev t, double* flux, double* flux_fla,
+                              hipStream_t s);
 hipError_t launch_cascade_ws(const GridDev& g, const Point* pts, int R, const int2* groups, int nwg, TablesDev t,
                              double* flux, double* flux_fla, hipStream_t s);
+
+// names of the main alpha-table / cascade kernels the latest launch_alpha / launch_cascade(_ws) on this
+// thread chose (static strings; nusi_plan_kernels)
+const char* last_alpha_kernel();
+const char* last_cascade_kernel();
 
 }  // namespace nusi

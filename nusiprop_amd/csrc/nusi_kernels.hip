@@ -476,11 +476,16 @@ void alpha_tiles_destroy(AlphaTilesDev* t)
     t->tiles = nullptr;
 }
 
+static thread_local const char* t_alpha_kernel = "";   // the main kernel of the latest launch on this thread
+const char* last_alpha_kernel() { return t_alpha_kernel; }
+
 hipError_t launch_alpha(const GridDev& g, const Point* pts, int npts, const SplineSet& spl, const AlphaTilesDev& at,
                         TablesDev t, int* warn, hipStream_t s, const int* batches, int nbatches, int gmax,
                         bool tile_kernel, int nb_plain)
 {
+    t_alpha_kernel = "k_alpha_tile";
     if (!tile_kernel && batches && getenv("NUSI_ALPHA_PER_ENTRY") == nullptr) {
+        t_alpha_kernel = "k_alpha_batch";
         // class 0 on the big-batch kernel (batches of up to gmax tables), classes 1 / 2 per table
         if (at.ext_lo < g.T) {
             const long long L = g.T - at.ext_lo, ne = L * (L - 1) / 2;
@@ -517,6 +522,7 @@ hipError_t launch_alpha(const GridDev& g, const Point* pts, int npts, const Spli
         hipLaunchKernelGGL(k_alpha, grid, dim3(256), 0, s, g, pts, spl, nlo, t.A, warn);
     };
     if (per_entry) {
+        t_alpha_kernel = "k_alpha";
         per_entry_region(0);
         return hipGetLastError();
     }

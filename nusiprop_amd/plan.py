@@ -106,6 +106,12 @@ class Plan:
         _lib.check(_lib.load().nusi_plan_warnings(self._h, out, n))
         return list(out)
 
+    def kernels(self):
+        """(alpha-table kernel, cascade kernel) the last call launched, e.g. ('k_alpha_batch', 'k_cascade_ws')."""
+        a, c = ctypes.c_char_p(), ctypes.c_char_p()
+        _lib.check(_lib.load().nusi_plan_kernels(self._h, ctypes.byref(a), ctypes.byref(c)))
+        return a.value.decode(), c.value.decode()
+
     def tables(self, i):
         """Point i's Stage-A tables of the last call: Gamma[T], alphaTilde[T], alpha packed [T(T-1)/2]."""
         G, At, A = np.zeros(self.T), np.zeros(self.T), np.zeros(self.PT)

@@ -85,21 +85,42 @@ def cascade_bytes_per_point(N, Nz):
     return 8 * ((Nz - 1) * N * (N - 1) // 2 + 6 * N * (Nz - 1) + Nz * N)
 
 
-def cascade_min_bytes_per_point(N, Nz):
+WSP_NJ, WSP_RT = 16, 8   # the step-pass cascade (k_cascade_wsp): step slots per pass, 16-row tiles per push wave
+
+
+def cascade_passes(N, Nz):
+    """The step-pass cascade's passes: (first step slot jb, stages Ts, column of local stage 0 c0)."""
+    T, nst = N + Nz - 2, Nz - 1
+    return [(jb, N - 1 + min(WSP_NJ, nst - jb), T - 1 - jb) for jb in range(0, nst, WSP_NJ)]
+
+
+def cascade_min_bytes_per_point(N, Nz, passes=False):
     """HBM bytes the wavefront cascade must move per propagation: each alpha column of the
-    packed table once (T(T-1)/2), Gamma and alphaTilde (2T), both flux outputs (6N)."""
+    packed table once (T(T-1)/2), Gamma and alphaTilde (2T), both flux outputs (6N).  With step
+    passes (Nz - 1 > 48) every pass reads the columns its stages visit (column c holds c entries)."""
     T = N + Nz - 2
-    return 8 * (T * (T - 1) // 2 + 2 * T + 6 * N)
+    if not passes:
+        return 8 * (T * (T - 1) // 2 + 2 * T + 6 * N)
+    cols = 0
+    for jb, Ts, c0 in cascade_passes(N, Nz):
+        lo = max(1, c0 + 1 - 4 * ((Ts - 1) // 4))
+        cols += sum(range(lo, min(c0 + 1, T - 1) + 1))
+    return 8 * (cols + 2 * T + 6 * N)
 
 
 def cascade_mfma_flops_per_point(N, Nz):
     """fp64 matrix-core flops the MFMA-push cascade (k_cascade_wf_mfma) issues per propagation: block q
     (stage 4q, q >= 1) runs one v_mfma_f64_16x16x4f64 (2*16*16*4 flops) per 16-row tile starting below
-    r = T-1-4q, per 16-step tile (NJ/16 of them, NJ = Nz-1 rounded up to 16/32/48); 0 if the grid does
-    not fit that kernel."""
+    r = T-1-4q, per 16-step tile (NJ/16 of them, NJ = Nz-1 rounded up to 16/32/48).  Grids with more
+    steps run the step-pass kernel (k_cascade_wsp): the same count per pass, one step tile."""
     T, n = N + Nz - 2, Nz - 1
     NJ = 16 if n <= 16 else 32 if n <= 32 else 48 if n <= 48 else 0
     waves = (T - 1 + 63) // 64
+    if not NJ and T >= 2:   # the step-pass kernel: one 16-step tile, RT row tiles per push wave
+        ntile = -(-(T - 1) // (16 * WSP_RT)) * WSP_RT
+        tiles = sum(min(ntile, -(-(c0 - 4 * q) // 16)) for jb, Ts, c0 in cascade_passes(N, Nz)
+                    for q in range(1, (Ts - 1) // 4 + 1) if c0 - 4 * q > 0)
+        return tiles * 2 * 16 * 16 * 4
     if not NJ or T < 2 or waves * 64 + 64 > 512:
         return 0
     tiles = sum(min(4 * waves, -(-(T - 1 - 4 * q) // 16)) for q in range(1, (T - 1) // 4 + 1) if T - 1 - 4 * q > 0)

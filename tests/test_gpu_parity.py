@@ -282,9 +282,10 @@ def test_alpha_batch_kernel_equals_tile_kernel(nusi, monkeypatch):
 
 
 def _evolve_env(nusi, pts, monkeypatch, **env):
-    """evolve `pts` on the MFMA cascade with the A/B switches in `env` (NUSI_CASCADE_WS, NUSI_MRHS)."""
+    """evolve `pts` on the MFMA cascade with the A/B switches in `env` (NUSI_CASCADE_WS, NUSI_MRHS,
+    NUSI_CASCADE_WSP)."""
     from nusiprop_amd import _lib
-    for k in ("NUSI_CASCADE_WS", "NUSI_MRHS"):
+    for k in ("NUSI_CASCADE_WS", "NUSI_MRHS", "NUSI_CASCADE_WSP"):
         monkeypatch.delenv(k, raising=False)
     for k, v in env.items():
         monkeypatch.setenv(k, v)
@@ -314,6 +315,35 @@ def test_cascade_ws_equals_mfma(nusi, monkeypatch, N):
     two = _evolve_env(nusi, gam, monkeypatch)
     for f in (one, two):
         assert np.array_equal(f[0], ref[0]) and np.array_equal(f[1], ref[1])
+
+
+@pytest.mark.parametrize("N,lEmin", [(100, 12.0), (200, 12.0), (700, 12.0), (1200, 10.0)])
+def test_cascade_step_passes(nusi, oracle_mod, monkeypatch, N, lEmin):
+    """The step-pass cascade (k_cascade_ws<16, 1, true>: 16 redshift steps in flight per pass, F carried
+    in LDS from pass to pass; nuSIprop.hpp:257-315): N = 100 (16 steps, one pass) equals the one-pass
+    kernel k_cascade_ws<16, 1> bit for bit; N = 200 (32 steps, 2 passes, forced), 700 (109 steps, 7 passes) and
+    BASELINE C3's grid (N = 1200, lE 10 -> 17: 134 steps, 9 passes) against the oracle's cascade on the
+    GPU's own tables to FLUX_RTOL, with the per-step register kernel's exact zeros."""
+    from nusiprop_amd import _lib
+    pts = [dict(cases.C2B_100, N_bins_E=N, lEmin=lEmin, mphi=m, g=g, majorana=maj)
+           for m, g, maj in ((6e5, 0.01, True), (1e5, 0.05, True), (2e6, 0.3, False))]
+    got = _evolve_env(nusi, pts, monkeypatch, NUSI_CASCADE_WSP="1")
+    if N == 100:
+        one = _evolve_env(nusi, pts, monkeypatch, NUSI_CASCADE_WSP="0")
+        assert np.array_equal(got[0], one[0]) and np.array_equal(got[1], one[1])
+    plan = nusi.Plan(N, lEmin, pts[0]["lEmax"], pts[0]["zmax"], max_points=len(pts))
+    plan.set_cascade(_lib.CASCADE_REG)
+    reg = plan.evolve(pts)
+    assert plan.Nz - 1 == {100: 16, 200: 32, 700: 109, 1200: 134}[N]
+    for k, p in enumerate(pts):
+        G, aT, A = plan.tables(k)
+        o = oracle_mod.Oracle(**cases.oracle_kwargs(p))
+        o.prepare()
+        f_ref, fla_ref = o.cascade(G, aT, nusi.unpack_alpha(A, plan.T))
+        assert cases.rel_err(got[0][k], f_ref) <= FLUX_RTOL, k
+        assert cases.rel_err(got[1][k], fla_ref) <= FLUX_RTOL, k
+        assert np.array_equal(got[0][k] == 0, reg[0][k] == 0)
+    plan.close()
 
 
 def test_c5_gamma_block_vs_oracle(nusi, oracle_mod, monkeypatch):
