@@ -529,6 +529,7 @@ void nusi_plan_destroy(nusi_plan* pl)
     hipFree(pl->tabs.G);
     hipFree(pl->tabs.At);
     hipFree(pl->tabs.A);
+    hipFree(pl->tabs.Med);
     nusi::alpha_tiles_destroy(&pl->atiles);
     hipFree(pl->d_scratch);
     if (pl->h_pts) hipHostFree(pl->h_pts);
@@ -608,6 +609,7 @@ int nusi_plan_create(int device, int N_bins_E, double lEmin, double lEmax, doubl
     HIPCHECK(hipMalloc(&pl->tabs.G, sizeof(double) * (size_t)G.T * max_points));
     HIPCHECK(hipMalloc(&pl->tabs.At, sizeof(double) * (size_t)G.T * max_points));
     HIPCHECK(hipMalloc(&pl->tabs.A, sizeof(double) * (size_t)gd.PT * max_points));
+    HIPCHECK(hipMalloc(&pl->tabs.Med, sizeof(double) * 3 * nusi::kMedFields * (size_t)G.T * max_points));
     std::vector<unsigned char> shared(G.T, 0);   // bin edges shared bitwise with the next bin
     for (int n = 0; n + 1 < G.T; ++n) shared[n] = (G.hi[n] == G.lo[n + 1]);
     HIPCHECK(nusi::alpha_tiles_create(G.T, shared.data(), &pl->atiles));

@@ -961,6 +961,14 @@ NUSI_FN double powerlaw_src(const GridDev& g, const Point& P, const double* pw, 
 #ifndef NUSI_WS_AB
 #define NUSI_WS_AB 0   // timing experiments only: 1 skip records, 2 skip pushes, 4 skip solves
 #endif
+// push waves not publishing spread their block MFMAs over the block's stages: k_cascade_wsp yes (C3 cascade
+// 37.3 -> 36.0 ms), k_cascade_ws no (C4 0.698 -> 0.728, C5 4.58 -> 4.93 ms; profiles/r2q)
+#ifndef NUSI_WS_STAGGER
+#define NUSI_WS_STAGGER 0
+#endif
+#ifndef NUSI_WSP_STAGGER
+#define NUSI_WSP_STAGGER 1
+#endif
 #ifndef NUSI_WS_P2WAVE
 #define NUSI_WS_P2WAVE 1   // R = 2: the LU phase of the records on a wave of its own (nw-3), not the chain (A/B: C5 cascade 5.75 -> 4.49 ms)
 #endif
@@ -1180,12 +1188,17 @@ void k_cascade_ws(GridDev g, const Point* __restrict__ pts, const int2* __restri
         double ablk[RT];
         load_blk(1, ablk);
         for (int sg = 0; sg < T; ++sg) {
-            if ((sg & 3) == 0 && !(NUSI_WS_AB & 2)) {
-                const int q = sg >> 2, r = T - 1 - sg;
+            // block q is pushed at stage 4q by the waves holding the rows it publishes, and one to three
+            // stages later by the others (their rows are needed >= 5 stages on; the T_j ring keeps 8):
+            // the matrix-core work of a block is spread over its four stages (NUSI_WS_STAGGER)
+            const int q = sg >> 2, r = T - 1 - 4 * q, hi = r - 1;
+            const bool crit = rw0 <= hi && rw0 + 16 * RT - 1 >= hi - 3;
+            const int dw = (!NUSI_WS_STAGGER || crit) ? 0 : 1 + wave % 3;
+            if ((sg & 3) == dw && !(NUSI_WS_AB & 2)) {
                 if (q >= 1) {
 #pragma unroll
                     for (int s = 0; s < NST; ++s) {
-                        const int bi = ((sg - 1 - (lane >> 4)) & 7) * NJ + 16 * s + (lane & 15);
+                        const int bi = ((4 * q - 1 - (lane >> 4)) & 7) * NJ + 16 * s + (lane & 15);
                         double bop[R];
 #pragma unroll
                         for (int p = 0; p < R; ++p) bop[p] = Tp[p * 8 * NJ + bi];
@@ -1198,7 +1211,8 @@ void k_cascade_ws(GridDev g, const Point* __restrict__ pts, const int2* __restri
                     }
                     load_blk(q + 1, ablk);
                 }
-                const int hi = r - 1;
+            }
+            if ((sg & 3) == 0 && !(NUSI_WS_AB & 2)) {
 #pragma unroll
                 for (int a = 0; a < RT; ++a)
                     if (rw0 + 16 * a <= hi && rw0 + 16 * a + 15 >= hi - 3)   // uniform: tiles holding those rows
@@ -1472,12 +1486,17 @@ void k_cascade_wsp(GridDev g, const Point* __restrict__ pts, TablesDev t, double
         double ablk[RT];
         load_blk(1, ablk);
         for (int sg = 0; sg < Ts; ++sg) {
-            if ((sg & 3) == 0 && !(NUSI_WS_AB & 2)) {
-                const int q = sg >> 2, r = c0 - sg;
+            // block q is pushed at stage 4q by the waves holding the rows it publishes, and one to three
+            // stages later by the others (their rows are needed >= 5 stages on; the T_j ring keeps 8):
+            // the matrix-core work of a block is spread over its four stages (NUSI_WSP_STAGGER)
+            const int q = sg >> 2, r = c0 - 4 * q, hi = r - 1;
+            const bool crit = rw0 <= hi && rw0 + 16 * RT - 1 >= hi - 3;
+            const int dw = (!NUSI_WSP_STAGGER || crit) ? 0 : 1 + wave % 3;
+            if ((sg & 3) == dw && !(NUSI_WS_AB & 2)) {
                 if (q >= 1) {
 #pragma unroll
                     for (int s = 0; s < NST; ++s) {
-                        const int bi = ((sg - 1 - (lane >> 4)) & 7) * NJ + 16 * s + (lane & 15);
+                        const int bi = ((4 * q - 1 - (lane >> 4)) & 7) * NJ + 16 * s + (lane & 15);
                         double bop[R];
 #pragma unroll
                         for (int p = 0; p < R; ++p) bop[p] = Tp[p * 8 * NJ + bi];
@@ -1490,7 +1509,8 @@ void k_cascade_wsp(GridDev g, const Point* __restrict__ pts, TablesDev t, double
                     }
                     load_blk(q + 1, ablk);
                 }
-                const int hi = r - 1;
+            }
+            if ((sg & 3) == 0 && !(NUSI_WS_AB & 2)) {
 #pragma unroll
                 for (int a = 0; a < RT; ++a)
                     if (rw0 + 16 * a <= hi && rw0 + 16 * a + 15 >= hi - 3)   // uniform: tiles holding those rows

@@ -30,6 +30,7 @@ struct TablesDev {
     double* G;    // [npts][T]
     double* At;   // [npts][T]
     double* A;    // [npts][PT]
+    double* Med;  // [npts][3][kMedFields T]: member edge leaves of every bin edge (k_alpha_medge)
 };
 
 // Tiles of the alpha table for k_alpha_tile: kAlphaTile x kAlphaTile (n, m) bin blocks with

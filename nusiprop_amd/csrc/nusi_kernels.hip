@@ -240,7 +240,10 @@ __global__ __launch_bounds__(kTileThreads) NUSI_TILE_ATTR void k_alpha_tile(Grid
 //   edg  [alpha_tile_edge_stride]  shared edge / m-bin leaves of the current k
 //   memb [kBatchQC][alpha_batch_memb_doubles]  member edge leaves of a chunk of points
 // ---------------------------------------------------------------------------
-constexpr int kBatchQC = 4;   // points per member-edge round: kBatchQC (ct + cs + kAlphaTile) <= 252 jobs
+#ifndef NUSI_BATCH_QC   // points per member-edge round (5: C4 alpha 6.05 -> 5.95 ms vs 4, profiles/r2q)
+#define NUSI_BATCH_QC 5
+#endif
+constexpr int kBatchQC = NUSI_BATCH_QC;   // kBatchQC (ct + cs + kAlphaTile) <= 256 jobs
 __host__ __device__ inline int alpha_batch_lds_doubles()
 {
     const int c1 = kAlphaTile + 1;
@@ -250,7 +253,8 @@ static_assert(kXFields * (kAlphaTile + 1) * (kAlphaTile + 1) >= 4 * (kAlphaTile 
               "the bracket phase's blocks fit X");
 static_assert(kBatchQC * (2 * (kAlphaTile + 1) + kAlphaTile) <= kTileThreads, "one member-edge round per chunk");
 
-#ifndef NUSI_AB_BATCH   // timing experiments only: 1 skip the member corner leaves, 2 skip the combine, 4 skip brackets
+#ifndef NUSI_AB_BATCH   // timing experiments only: 1 skip the member corner leaves, 2 skip the combine, 4 skip brackets,
+                        // 16 skip the member edges, 32 skip the shared corner / mixed / member-coefficient phases
 #define NUSI_AB_BATCH 0
 #endif
 #ifndef NUSI_BATCH_WAVES
@@ -281,10 +285,23 @@ NUSI_BCOLD void b_pre(const Point& P, int k, double Em, double Ep, double Emp, d
     alpha_k_pre(P, k, Em, Ep, Emp, Epp, lv, pre);
 }
 
+// member edge leaves of every (table, k, bin edge) -> t.Med (alpha_medge_job); grid (jobs / 256, tables, 3)
+__global__ __launch_bounds__(256) void k_alpha_medge(GridDev g, const Point* __restrict__ pts, double* __restrict__ med)
+{
+    const int j = blockIdx.x * 256 + threadIdx.x, p = blockIdx.y, k = blockIdx.z, T = g.T;
+    if (j >= 5 * T) return;
+    alpha_medge_job(pts[p], k, j, T, g.lo, g.hi, med + ((size_t)p * 3 + k) * kMedFields * T);
+}
+
+#ifndef NUSI_MEDGE_GLOBAL   // 1: member edges copied from k_alpha_medge's table; 0: evaluated per tile (A/B)
+#define NUSI_MEDGE_GLOBAL 1
+#endif
+
 template <bool kPP>   // the batches' tables have the phi-phi channel (its shared term per k)
 __global__ __launch_bounds__(kTileThreads) __attribute__((amdgpu_waves_per_eu(NUSI_BATCH_WAVES, NUSI_BATCH_WAVES)))
 void k_alpha_batch(GridDev g, const Point* __restrict__ pts, SplineSet spl, const int* __restrict__ tiles,
-                   const int* __restrict__ batches, double* __restrict__ A, int* __restrict__ warn)
+                   const int* __restrict__ batches, double* __restrict__ A, const double* __restrict__ med,
+                   int* __restrict__ warn)
 {
     extern __shared__ __attribute__((aligned(16))) double sm[];
     __shared__ double tE[2 * kAlphaTile], sE[2 * kAlphaTile];
@@ -312,6 +329,17 @@ void k_alpha_batch(GridDev g, const Point* __restrict__ pts, SplineSet spl, cons
     if (tid == 64) cnt[1] = alpha_edge_list(elo[1], ehi[1], 0, Tm - m0, sE, sl, sh);
     __syncthreads();
     const int ct = cnt[0], cs = cnt[1], cc = cs * ct;
+    __shared__ int tsrc[2 * kAlphaTile], ssrc[2 * kAlphaTile];   // bin edge (2 b + side) behind each list slot
+    if (NUSI_MEDGE_GLOBAL && tid < 2 * kAlphaTile) {
+        const int side = tid / kAlphaTile, j = tid - side * kAlphaTile, b0 = side ? m0 : n0;
+        const int* il = side ? sl : tl;
+        const int* ih = side ? sh : th;
+        int* src = side ? ssrc : tsrc;
+        if (b0 + j < (side ? Tm : Tn)) {
+            src[ih[j]] = 2 * (b0 + j) + 1;
+            if (j == 0 || il[j] != ih[j - 1]) src[il[j]] = 2 * (b0 + j);   // else the previous bin's upper edge
+        }
+    }
     const int ln = tid % kAlphaTile, lm = tid / kAlphaTile;
     const int n = n0 + ln, m = m0 + lm;
     const bool valid = tid < kAlphaTile * kAlphaTile && n < m && m < Tm && n < Tn;
@@ -343,9 +371,11 @@ void k_alpha_batch(GridDev g, const Point* __restrict__ pts, SplineSet spl, cons
         AlphaPre pre{};
         PPTerm ppt{0.0, 1.0, 1.0};
         if (cornered) {
-            for (int j = tid; j < cc; j += kTileThreads) b_corner(j, edgk, ct, cs, P3, tmp);
-            for (int j = tid; j < kAlphaTile * (cs + ct); j += kTileThreads)
-                alpha_batch_mixed_job(j, edgk, ct, cs, tl, th, sl, sh, n0, m0, T, Tm, mix, mix + kAlphaTile * cs);
+            if (!(NUSI_AB_BATCH & 32)) {
+                for (int j = tid; j < cc; j += kTileThreads) b_corner(j, edgk, ct, cs, P3, tmp);
+                for (int j = tid; j < kAlphaTile * (cs + ct); j += kTileThreads)
+                    alpha_batch_mixed_job(j, edgk, ct, cs, tl, th, sl, sh, n0, m0, T, Tm, mix, mix + kAlphaTile * cs);
+            }
             __syncthreads();
             if (needed) {
                 SplitLeaves lv;
@@ -362,24 +392,38 @@ void k_alpha_batch(GridDev g, const Point* __restrict__ pts, SplineSet spl, cons
                 if (kPP) ppt = alpha_k_pp(P, spl, k, g.lo[n], g.hi[n], g.lo[m], g.hi[m], lv, wsh);
             }
             __syncthreads();   // X is rewritten with the member coefficients
-            for (int j = tid; j < cc; j += kTileThreads) b_xshared(j, edgk, ct, cs, X);
+            if (!(NUSI_AB_BATCH & 32))
+                for (int j = tid; j < cc; j += kTileThreads) b_xshared(j, edgk, ct, cs, X);
         }
-        // ---- the points, kBatchQC at a time: their member edge leaves in one round, then point by point
+        // ---- the points, kBatchQC at a time: their member edge leaves in one round, then point by point.
+        // A point's entry accumulates over the mass states in A; the sum of the states < k is loaded one
+        // point ahead, so its latency (the line left L2 since state k-1) hides behind a point's work.
+        const bool reload = k > 0 && needed && !(NUSI_AB_BATCH & 8);
+        double tnext = reload ? A[(size_t)p0 * g.PT + eidx] : 0.0;
+        // member edges: thread (mq, mjob) copies job mjob of point mq of each chunk (loading the next chunk's
+        // values a chunk ahead measured slower: their registers stay live through the combine)
+        const int mq = tid / mjobs, mjob = tid - mq * mjobs;
 #pragma unroll 1
         for (int q0 = 0; q0 < nb; q0 += kBatchQC) {
             const int nq = (nb - q0 < kBatchQC) ? nb - q0 : kBatchQC;
             __syncthreads();   // the previous chunk is done with membq (and mem)
-            {
-                const int qq = tid / mjobs, job = tid - qq * mjobs;
-                if (qq < nq) b_medge(pts[p0 + q0 + qq], k, job, tE, ct, sE, cs, g.lo, g.hi, m0, Tm, membq + qq * mbd);
+            if (mq < nq && !(NUSI_AB_BATCH & 16)) {
+                if (NUSI_MEDGE_GLOBAL) {
+                    MedVals mv{};
+                    alpha_batch_medge_load(nonres, mjob, tsrc, ct, ssrc, cs, m0, Tm, T,
+                                           med + ((size_t)(p0 + q0 + mq) * 3 + k) * kMedFields * T, mv);
+                    alpha_batch_medge_store(nonres, mjob, ct, cs, m0, Tm, mv, membq + mq * mbd);
+                } else {
+                    b_medge(pts[p0 + q0 + mq], k, mjob, tE, ct, sE, cs, g.lo, g.hi, m0, Tm, membq + mq * mbd);
+                }
             }
 #pragma unroll 1
             for (int qq = 0; qq < nq; ++qq) {
                 const int q = q0 + qq;
                 const Point& Q = pts[p0 + q];
                 const double* memb = membq + qq * mbd;
-                double tot = 0.0;
-                if (k > 0 && needed && !(NUSI_AB_BATCH & 8)) tot = A[(size_t)(p0 + q) * g.PT + eidx];   // after states < k
+                double tot = tnext;   // after states < k
+                if (reload && q + 1 < nb) tnext = A[(size_t)(p0 + q + 1) * g.PT + eidx];
                 __syncthreads();   // member edges written / the previous point's combine is done with mem
                 if (cornered && !(NUSI_AB_BATCH & 1))
                     for (int j = tid; j < cc; j += kTileThreads) alpha_batch_mcorner_job(Q, j, edgk, ct, cs, X, memb, mem);
@@ -499,12 +543,17 @@ hipError_t launch_alpha(const GridDev& g, const Point* pts, int npts, const Spli
             if (c == 0) {   // batches [0, nb_plain) without the phi-phi channel, then those with it
                 const size_t lds = sizeof(double) * (size_t)alpha_batch_lds_doubles();
                 if (cs > kAlphaTile + 1 || ct > kAlphaTile + 1) return hipErrorInvalidValue;
+                if (NUSI_MEDGE_GLOBAL) {
+                    if (!t.Med) return hipErrorInvalidValue;
+                    hipLaunchKernelGGL(k_alpha_medge, dim3((unsigned)((5 * g.T + 255) / 256), npts, 3), dim3(256), 0, s,
+                                       g, pts, t.Med);
+                }
                 if (nb_plain > 0)
                     hipLaunchKernelGGL(k_alpha_batch<false>, dim3(at.ncls[0], nb_plain), dim3(kTileThreads), lds, s, g,
-                                       pts, spl, at.tiles, batches, t.A, warn);
+                                       pts, spl, at.tiles, batches, t.A, t.Med, warn);
                 if (nbatches > nb_plain)
                     hipLaunchKernelGGL(k_alpha_batch<true>, dim3(at.ncls[0], nbatches - nb_plain), dim3(kTileThreads),
-                                       lds, s, g, pts, spl, at.tiles, batches + nb_plain, t.A, warn);
+                                       lds, s, g, pts, spl, at.tiles, batches + nb_plain, t.A, t.Med, warn);
             } else {
                 const size_t lds = sizeof(double) * (size_t)alpha_tile_lds_doubles(cs, ct, 1);
                 hipLaunchKernelGGL(k_alpha_tile<1>, dim3(at.ncls[c], npts), dim3(kTileThreads), lds, s, g, pts, spl,

@@ -972,6 +972,81 @@ NUSI_FN void alpha_batch_medge_job(const Point& P, int k, int job, const double*
         memb[ct + 2 * cs + q] = alpha_mbin_atd(alpha_S(mk, lo[m0 + q], m2), alpha_S(mk, hi[m0 + q], m2), mphi, Ga);
     }
 }
+// The member edge leaves of a table point are functions of one bin edge energy (t side, S' side) or of
+// one bin (atd), not of the tile: k_alpha_medge evaluates them once per (point, k, bin edge) into
+// global memory -- layout per (point, k), with e = 2 b + (0: lo[b], 1: hi[b]):
+//   L2 inv q sT fT [5][2T] | Ls cS sS fS [4][2T] | atd [T]
+// -- and the batch kernel copies its tile's edges from there (alpha_batch_medge_copy), instead of every
+// tile of a row re-evaluating the same edges.  Same functions, same arguments: the same bits as
+// alpha_batch_medge_job.
+constexpr int kMedFields = 19;   // doubles per bin per (point, k): 2 (5 + 4) + 1
+NUSI_FN void alpha_medge_job(const Point& P, int k, int j, int T, const double* lo, const double* hi, double* med)
+{
+    const double mphi = P.mphi, Ga = P.Ga, m2 = mphi * mphi, gr = P.a_gr, gr2 = gr * gr, mk = P.mn[k];
+    const int E2 = 2 * T;
+    if (j < E2) {
+        if (!P.non_resonant) return;
+        const double t = alpha_t(mk, (j & 1) ? hi[j >> 1] : lo[j >> 1], m2);
+        med[j] = alpha_tedge_L2(t, gr2);
+        const MemberTEdge e = alpha_member_tedge(t, gr);
+        med[E2 + j] = e.inv; med[2 * E2 + j] = e.q; med[3 * E2 + j] = e.sT; med[4 * E2 + j] = e.fT;
+    } else if (j < 2 * E2) {
+        if (!P.non_resonant) return;
+        const int q = j - E2;
+        const double S = alpha_S(mk, (q & 1) ? hi[q >> 1] : lo[q >> 1], m2);
+        AlphaSEdge e;
+        alpha_sedge_member(S, gr, gr2, e);
+        double* ms = med + 5 * E2;
+        ms[q] = e.Ls;
+        ms[E2 + q] = e.cS;
+        alpha_member_sarg(S, gr, ms[2 * E2 + q], ms[3 * E2 + q]);
+    } else if (j < 2 * E2 + T) {
+        const int b = j - 2 * E2;
+        med[9 * E2 + b] = alpha_mbin_atd(alpha_S(mk, lo[b], m2), alpha_S(mk, hi[b], m2), mphi, Ga);
+    }
+}
+// alpha_batch_medge_job's outputs, copied from k_alpha_medge's block med (point, k): medge_load reads
+// job's values (tsrc / ssrc: the bin edge, 2 b + side, each slot of the tile's t / S' edge list was
+// taken from), medge_store puts them where alpha_batch_medge_job would have written them.
+struct MedVals { double v[5]; };
+NUSI_FN void alpha_batch_medge_load(bool nonres, int job, const int* tsrc, int ct, const int* ssrc, int cs, int m0,
+                                    int Tm, int T, const double* __restrict__ med, MedVals& o)
+{
+    const int E2 = 2 * T;
+    if (job < ct) {
+        if (!nonres) return;
+        const int e = tsrc[job];
+#pragma unroll
+        for (int f = 0; f < 5; ++f) o.v[f] = med[f * E2 + e];
+    } else if (job < ct + cs) {
+        if (!nonres) return;
+        const int e = ssrc[job - ct];
+#pragma unroll
+        for (int f = 0; f < 4; ++f) o.v[f] = med[(5 + f) * E2 + e];
+    } else {
+        const int q = job - ct - cs;
+        if (m0 + q < Tm) o.v[0] = med[9 * E2 + m0 + q];
+    }
+}
+NUSI_FN void alpha_batch_medge_store(bool nonres, int job, int ct, int cs, int m0, int Tm, const MedVals& o, double* memb)
+{
+    double* ext = memb + ct + 2 * cs + kAlphaTile;   // inv | q | sT | fT | sS | fS
+    if (job < ct) {
+        if (!nonres) return;
+        memb[job] = o.v[0];
+        ext[job] = o.v[1]; ext[ct + job] = o.v[2]; ext[2 * ct + job] = o.v[3]; ext[3 * ct + job] = o.v[4];
+    } else if (job < ct + cs) {
+        if (!nonres) return;
+        const int q = job - ct;
+        memb[ct + q] = o.v[0];
+        memb[ct + cs + q] = o.v[1];
+        ext[4 * ct + q] = o.v[2];
+        ext[4 * ct + cs + q] = o.v[3];
+    } else {
+        const int q = job - ct - cs;
+        if (m0 + q < Tm) memb[ct + 2 * cs + q] = o.v[0];
+    }
+}
 // member corner leaves of corner j for point P -> mem[0..2][cc] (Dcr, Dci, A); edgk: the shared edge block of
 // mass state k (its t and S' values)
 NUSI_FN void alpha_batch_mcorner_job(const Point& P, int j, const double* edgk, int ct, int cs, const double* X,
