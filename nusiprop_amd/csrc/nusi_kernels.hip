@@ -293,6 +293,9 @@ __global__ __launch_bounds__(256) void k_alpha_medge(GridDev g, const Point* __r
     alpha_medge_job(pts[p], k, j, T, g.lo, g.hi, med + ((size_t)p * 3 + k) * kMedFields * T);
 }
 
+#ifndef NUSI_ALPHA_XCD   // 1: k_alpha_batch's blocks remapped so that each XCD runs contiguous (batch, tile) ranges
+#define NUSI_ALPHA_XCD 0    // (A/B, profiles/r2s: C4 alpha 5.97 -> 6.09 ms, C3 90.7 -> 94.4 ms; the dealt order wins)
+#endif
 #ifndef NUSI_MEDGE_GLOBAL   // 1: member edges copied from k_alpha_medge's table; 0: evaluated per tile (A/B)
 #define NUSI_MEDGE_GLOBAL 1
 #endif
@@ -309,9 +312,20 @@ void k_alpha_batch(GridDev g, const Point* __restrict__ pts, SplineSet spl, cons
     __shared__ int cnt[2];
     __shared__ double elo[2][kAlphaTile], ehi[2][kAlphaTile];
     const int tid = threadIdx.x, T = g.T;
-    const int bw = batches[blockIdx.y];
+    // XCD-aware order: blocks are dealt round-robin over the 8 XCDs (b and b + 8 share one), so the
+    // linear block id is remapped to make each XCD run a contiguous range of (batch, tile) -- the tiles
+    // of one batch read the same member-edge blocks (k_alpha_medge) and share them in that XCD's L2
+    int bx = blockIdx.x, by = blockIdx.y;
+    if (NUSI_ALPHA_XCD) {
+        const int nbk = gridDim.x * gridDim.y, L = by * gridDim.x + bx;
+        const int xcd = L & 7, slot = L >> 3, q8 = nbk >> 3, rem = nbk & 7;
+        const int M = xcd < rem ? xcd * (q8 + 1) + slot : rem * (q8 + 1) + (xcd - rem) * q8 + slot;
+        by = M / gridDim.x;
+        bx = M - by * gridDim.x;
+    }
+    const int bw = batches[by];
     const int p0 = bw & 0xffffff, nb = (int)((unsigned)bw >> 24);   // tables p0 .. p0 + nb - 1
-    const unsigned tu = (unsigned)tiles[blockIdx.x];                 // tile word, as in k_alpha_tile
+    const unsigned tu = (unsigned)tiles[bx];                         // tile word, as in k_alpha_tile
     const int half = (tu >> 28) & 3, nhalf = (tu >> 30) & 3;
     const int n0 = (tu & 0x3fff) * kAlphaTile + (nhalf == 2 ? 8 : 0);
     const int m0 = ((tu >> 14) & 0x3fff) * kAlphaTile + (half == 2 ? 8 : 0);
