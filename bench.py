@@ -286,7 +286,13 @@ def main():
         traffic = pmc.get("k_cascade_bytes_per_launch")
         tsrc = os.path.relpath(tj, ROOT)
     achieved = casc_bytes / casc_s / 1e9
-    casc_min = scan.cascade_min_bytes_per_point(N, Nz, passes=casc_kernel == "k_cascade_ws_passes") * P
+    # workgroups that read a table: one per point, or one per pair of points sharing a table on the multi-RHS
+    # kernel (the pair reads its alpha table once)
+    readers = P
+    if casc_kernel == "k_cascade_ws_mrhs":
+        from collections import Counter
+        readers = sum((c + 1) // 2 for c in Counter(scan.table_key(p) for p in pts).values())
+    casc_min = scan.cascade_min_bytes_per_point(N, Nz, passes=casc_kernel == "k_cascade_ws_passes") * readers
     step_ms = sum(sum_ms) / max(ncalls, 1)
     out = {
         "metric": METRIC,
@@ -315,6 +321,7 @@ def main():
         "roofline_cascade": {"bound": "hbm", "kernel": casc_kernel, "achieved": casc_min / casc_s / 1e9,
                              "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": casc_min / casc_s / 1e9 / HBM_PEAK_GBS,
                              "traffic": traffic, "traffic_source": tsrc, "algorithmic_bytes_per_launch": casc_min,
+                             "table_readers": readers,
                              "reference_pattern_bytes_per_launch": casc_bytes, "reference_pattern_gbs": achieved,
                              "avg_launch_ms": casc_s * 1e3,
                              "note": "not HBM-bound: T = N+Nz-2 dependent stages per point (LDS/barrier latency)"},

@@ -356,6 +356,13 @@ int load_spline(const char* path, int ndim, const int* dims, SplineStore& st, nu
     st.bufs.push_back(df);
     HIPCHECK(hipMemcpy(df, f.data(), sizeof(float) * nf, hipMemcpyHostToDevice));
     sd.f = df;
+    if (ndim == 3 && !(getenv("NUSI_SPLINE_WINDOWS") && getenv("NUSI_SPLINE_WINDOWS")[0] == '0')) {
+        float* dw = nullptr;   // 16 x the table: the 4 x 4 windows of nusi_spline.hpp
+        HIPCHECK(hipMalloc(&dw, sizeof(float) * 16 * nf));
+        st.bufs.push_back(dw);
+        HIPCHECK(nusi::spline_windows_build(df, dims[0], dims[1], dims[2], dw));
+        sd.fw = dw;
+    }
     out = sd;
     return NUSI_OK;
 }

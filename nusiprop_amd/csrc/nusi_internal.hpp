@@ -71,6 +71,9 @@ hipError_t launch_cascade_wsp(const GridDev& g, const Point* pts, int npts, Tabl
 hipError_t launch_cascade_ws(const GridDev& g, const Point* pts, int R, const int2* groups, int nwg, TablesDev t,
                              double* flux, double* flux_fla, hipStream_t s);
 
+// 4 x 4 windows of a 3-D spline table f [n0][n1][n2] into fw [n0 n1 n2][16] (synchronous)
+hipError_t spline_windows_build(const float* f, int n0, int n1, int n2, float* fw);
+
 // names of the main alpha-table / cascade kernels the latest launch_alpha / launch_cascade(_ws) on this
 // thread chose (static strings; nusi_plan_kernels)
 const char* last_alpha_kernel();

@@ -37,6 +37,34 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NUSI_GA_WAVE
     if (w) atomicOr(&warn[p], w);
 }
 
+// 4 x 4 windows of a 3-D spline table (nusi_spline.hpp): fw[16 node + 4 a1 + a2] = f[i0][i1 + a1][i2 + a2]
+__global__ __launch_bounds__(256) void k_spline_windows(const float* __restrict__ f, int n0, int n1, int n2,
+                                                        float* __restrict__ fw)
+{
+    const size_t node = (size_t)blockIdx.x * 256 + threadIdx.x, nn = (size_t)n0 * n1 * n2;
+    if (node >= nn) return;
+    const int i2 = (int)(node % n2), i1 = (int)((node / n2) % n1);
+    const size_t row = node - (size_t)i1 * n2 - i2;   // (i0, 0, 0)
+    float4 out[4];
+#pragma unroll
+    for (int a1 = 0; a1 < 4; ++a1) {
+        const size_t r = row + (size_t)min(i1 + a1, n1 - 1) * n2;
+        out[a1] = make_float4(f[r + min(i2, n2 - 1)], f[r + min(i2 + 1, n2 - 1)], f[r + min(i2 + 2, n2 - 1)],
+                              f[r + min(i2 + 3, n2 - 1)]);
+    }
+    float4* dst = reinterpret_cast<float4*>(fw + 16 * node);
+#pragma unroll
+    for (int a1 = 0; a1 < 4; ++a1) dst[a1] = out[a1];
+}
+
+hipError_t spline_windows_build(const float* f, int n0, int n1, int n2, float* fw)
+{
+    const size_t nn = (size_t)n0 * n1 * n2;
+    hipLaunchKernelGGL(k_spline_windows, dim3((unsigned)((nn + 255) / 256)), dim3(256), 0, 0, f, n0, n1, n2, fw);
+    hipError_t e = hipGetLastError();
+    return e != hipSuccess ? e : hipDeviceSynchronize();
+}
+
 // one entry per work-item over the bins [nlo, T) x [nlo, T), n < m (nlo = 0: the whole table)
 #ifndef NUSI_PE_WAVES   // per-entry kernel waves per SIMD (A/B)
 #define NUSI_PE_WAVES 3   // 3: 20.05 vs 20.24 ms alpha stage (profiles/r1i/ab_occ_*)

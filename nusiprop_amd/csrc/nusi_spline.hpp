@@ -22,6 +22,16 @@
 // returns on sorted nodes -- in one guide load and about two node loads.
 // The 16 weights of node k sit together (wt[16 k + 4 a + b], one 128-B line).
 // Without a guide (gd == nullptr) the reference's binary search runs.
+//
+// Windows (3-D table).  A lookup reads a 4 x 4 x 4 stencil: with the values
+// in the file's order (last index fastest) that is 16 runs of 16 B, each in
+// its own cache line, and at C3 these gathers were ~80 % of the alpha
+// kernel's HBM traffic.  The plan therefore keeps, for every node
+// (i0, i1, i2), the 4 x 4 window fw[16 node + 4 a1 + a2] = f[i0][i1 + a1][i2 + a2]
+// (indices clamped at the table's end; those entries are never read): a
+// lookup reads 4 aligned 64-B windows.  16 x the table (6.4 GB at
+// {1000,1000,100}), built on the GPU from f at load.  The same floats are
+// summed in the same order (axis 0 fastest), so the value is unchanged.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -46,6 +56,7 @@ struct SplineDev {
     int ng[kSplMaxDim] = {0, 0, 0};
     double ginv[kSplMaxDim] = {0.0, 0.0, 0.0};                   // buckets per unit of the axis
     const float* f = nullptr;                                    // values, last index fastest
+    const float* fw = nullptr;                                   // 3-D: 4 x 4 windows per node (or nullptr)
     int islog[kSplMaxDim + 1] = {0, 0, 0, 0};
 
     // the last node <= x0 (x[0] < x0 < x[n-1])
@@ -97,6 +108,33 @@ struct SplineDev {
                 const double* wk = w[i] + 16 * k[i] + 4 * a;
                 fac[i][a] = t[i] * t[i] * t[i] * wk[0] + (t[i] * t[i]) * wk[1] + t[i] * wk[2] + wk[3];
             }
+        if (ndim == 3 && fw) {
+            struct alignas(16) F4 { float v[4]; };
+            F4 win[4][4];   // win[idx0][a1].v[a2] = f[lo0 + idx0][lo1 + a1][lo2 + a2]
+#pragma unroll
+            for (int i0 = 0; i0 < 4; ++i0) {
+                const int r0 = lo[0] + (i0 < cnt[0] ? i0 : 0);
+                const F4* src = reinterpret_cast<const F4*>(fw + 16 * (((size_t)r0 * n[1] + lo[1]) * n[2] + lo[2]));
+#pragma unroll
+                for (int a1 = 0; a1 < 4; ++a1) win[i0][a1] = src[a1];
+            }
+            double res = 0;   // the reference's order: axis 0 fastest (loops of 4 with guards: static indices)
+#pragma unroll
+            for (int i2 = 0; i2 < 4; ++i2)
+#pragma unroll
+                for (int i1 = 0; i1 < 4; ++i1)
+#pragma unroll
+                    for (int i0 = 0; i0 < 4; ++i0)
+                        if (i2 < cnt[2] && i1 < cnt[1] && i0 < cnt[0]) {
+                            double v = (double)win[i0][i1].v[i2];
+                            v *= fac[0][i0];
+                            v *= fac[1][i1];
+                            v *= fac[2][i2];
+                            res += v;
+                        }
+            out = islog[ndim] ? nm::exp(res) : res;
+            return true;
+        }
         int idx[kSplMaxDim] = {0, 0, 0};
         double res = 0;
         for (;;) {

@@ -346,6 +346,26 @@ def test_cascade_step_passes(nusi, oracle_mod, monkeypatch, N, lEmin):
     plan.close()
 
 
+def test_plan_kernels_names(nusi):
+    """nusi_plan_kernels reports what the last call launched: the batch alpha kernel, and per grid and
+    cascade kind the one-pass warp-specialised kernel, its multi-RHS form (gamma pairs sharing a table),
+    the step-pass kernel (N_z - 1 > 48) or the bit-exact wavefront (AUTO)."""
+    from nusiprop_amd import _lib
+    def run(N, lEmin, pts_kw, kind):
+        pts = [dict(cases.C2B_100, N_bins_E=N, lEmin=lEmin, **kw) for kw in pts_kw]
+        plan = nusi.Plan(N, lEmin, pts[0]["lEmax"], pts[0]["zmax"], max_points=len(pts))
+        plan.set_cascade(kind)
+        plan.evolve(pts)
+        k = plan.kernels()
+        plan.close()
+        return k
+    two = [dict(mphi=6e5, g=0.01), dict(mphi=2e6, g=0.1)]
+    assert run(100, 12.0, two, _lib.CASCADE_MFMA) == ("k_alpha_batch", "k_cascade_ws")
+    assert run(100, 12.0, [dict(mphi=6e5, g=0.01, si=s) for s in (2.0, 2.5)], _lib.CASCADE_MFMA)[1] == "k_cascade_ws_mrhs"
+    assert run(700, 12.0, two, _lib.CASCADE_MFMA)[1] == "k_cascade_ws_passes"
+    assert run(100, 12.0, two, _lib.CASCADE_AUTO)[1] == "k_cascade_wf"
+
+
 def test_c5_gamma_block_vs_oracle(nusi, oracle_mod, monkeypatch):
     """BASELINE config 5: one full 16-gamma block of scan.c5_points() (N_E = 300, power law; one
     Stage-A table, 8 pairs on the multi-RHS cascade) against the oracle -- its tables once, its
