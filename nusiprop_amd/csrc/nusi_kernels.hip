@@ -308,9 +308,13 @@ NUSI_BCOLD void b_medge(const Point& P, int k, int job, const double* tE, int ct
 {
     alpha_batch_medge_job(P, k, job, tE, ct, sE, cs, lo, hi, m0, Tm, memb);
 }
-NUSI_BCOLD void b_pre(const Point& P, int k, double Em, double Ep, double Emp, double Epp, SplitLeaves lv, AlphaPre& pre)
+// (returned by value: an out parameter's address would keep the caller's copy in scratch, reloaded by every
+// point's combine)
+NUSI_BCOLD AlphaPre b_pre(const Point& P, int k, double Em, double Ep, double Emp, double Epp, SplitLeaves lv)
 {
+    AlphaPre pre;
     alpha_k_pre(P, k, Em, Ep, Emp, Epp, lv, pre);
+    return pre;
 }
 
 // member edge leaves of every (table, k, bin edge) -> t.Med (alpha_medge_job); grid (jobs / 256, tables, 3)
@@ -430,7 +434,7 @@ void k_alpha_batch(GridDev g, const Point* __restrict__ pts, SplineSet spl, cons
                 lv.tedm = membq; lv.sedm = membq + ct; lv.mbm = membq + ct + 2 * cs; lv.marg = membq;   // (not read)
                 lv.xl = mix; lv.yl = mix + kAlphaTile * cs;
                 if (NUSI_AB_BATCH & 4) pre = AlphaPre{lv.cf[1][tid % cc], lv.cf[2][tid % cc], 1.0, 1.0};
-                else b_pre(P, k, g.lo[n], g.hi[n], g.lo[m], g.hi[m], lv, pre);
+                else pre = b_pre(P, k, g.lo[n], g.hi[n], g.lo[m], g.hi[m], lv);
                 if (kPP) ppt = alpha_k_pp(P, spl, k, g.lo[n], g.hi[n], g.lo[m], g.hi[m], lv, wsh);
             }
             __syncthreads();   // X is rewritten with the member coefficients

@@ -829,17 +829,19 @@ NUSI_FN TileLeaves alpha_tile_leaves(const double* cor, const double* edg, int k
 // S'- = 1e4 (f2 = den = 1), else its large-s expansion (branch 1: f1 = numerator, den = 256 pi S-^2 S+^2;
 // branch 2: f1 = the whole bracket; branch 3: f1 = t+ - t-, f2 = bracket, den = 128 pi S- S+).  The term
 // reads neither g nor Gamma_phi, so the points of a batch (same m_phi and masses) share it.  Out of line:
-// only the phiphi configuration reaches it, and inlined it would cost every entry registers.
-struct PPTerm { double f1, f2, den; };
+// only the phiphi configuration reaches it, and inlined it would cost every entry registers.  The
+// out-of-range warning comes back in the result (oob), not through a reference: a caller's warning word
+// whose address escaped into a call would live in scratch, stored and reloaded every entry.
+struct PPTerm { double f1, f2, den; int oob = 0; };
 NUSI_FN_OUT PPTerm alpha_phiphi_core(const SplineSet& spl, double Sm, double Sp, double tm, double tp, double lSm,
-                                     double lSp, int& warn)
+                                     double lSp)
 {
     if (Sm < 1e4) {
         const double d = Sp / Sm;
         const double xx[3] = {Sm, nm::log(-Sm / tm) / nm::log(d) * 1.0001, nm::log10(d)};
         double v = 0;
-        if (!spl.a.eval(xx, v)) warn |= kWarnSplineOOB;
-        return PPTerm{fabs(v), 1.0, 1.0};
+        const bool in = spl.a.eval(xx, v);
+        return PPTerm{fabs(v), 1.0, 1.0, in ? 0 : kWarnSplineOOB};
     }
     if (tm < -1) {
         const double l1m = nm::log(-1 - tm), l0m = nm::log(-tm), l1p = nm::log(-1 - tp), l0p = nm::log(-tp);
@@ -1173,7 +1175,9 @@ NUSI_FN PPTerm alpha_k_pp(const Point& P, const SplineSet& spl, int k, double Em
     const double Sp = lv.Sval(1, mk, Epp, m2), Sm = lv.Sval(0, mk, Emp, m2);
     if (!(Sm > 4 && P.phiphi)) return PPTerm{0.0, 1.0, 1.0};
     const AlphaSEdge eSm = lv.sedge(0, Sm), eSp = lv.sedge(1, Sp);
-    return alpha_phiphi_core(spl, Sm, Sp, tm, tp, eSm.lS, eSp.lS, warn);
+    const PPTerm X = alpha_phiphi_core(spl, Sm, Sp, tm, tp, eSm.lS, eSp.lS);
+    warn |= X.oob;
+    return X;
 }
 
 // one mass state k of alpha(Em, Ep, Em', Ep'): tot += wgt * (every channel); pre: the shared brackets
@@ -1280,7 +1284,15 @@ NUSI_FN void alpha_k(const Point& P, const SplineSet& spl, int k, double Em, dou
 
     double app = 0.0;
     if (Sm > 4 && P.phiphi)   // ppt: the term shared by a batch (alpha_k_pp)
-        app = alpha_phiphi_scale(P, uk, ppt ? *ppt : alpha_phiphi_core(spl, Sm, Sp, tm, tp, lSm, lSp, warn));
+    {
+        PPTerm X;
+        if (ppt) X = *ppt;
+        else {
+            X = alpha_phiphi_core(spl, Sm, Sp, tm, tp, lSm, lSp);
+            warn |= X.oob;
+        }
+        app = alpha_phiphi_scale(P, uk, X);
+    }
     tot += wgt * app;
 
     const double nrm = P.a_nrm;
