@@ -1,1 +1,3 @@
-bash scripts/ab_libs.sh r2x "c4 c5" base sedge ga2 ga3 bw3 && timeout -k 10 500 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/r2x/pytest.log 2>&1
+mkdir -p gpurun_out/r2z
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/r2z/smoke.log 2>&1 && \
+timeout -k 10 600 python bench.py > gpurun_out/r2z/bench_default.json 2> gpurun_out/r2z/bench_default.err
