@@ -443,7 +443,7 @@ void k_alpha_batch(GridDev g, const Point* __restrict__ pts, SplineSet spl, cons
         }
         // ---- the points, kBatchQC at a time: their member edge leaves in one round, then point by point.
         // A point's entry accumulates over the mass states in A; the sum of the states < k is loaded one
-        // point ahead, so its latency (the line left L2 since state k-1) hides behind a point's work.
+        // point ahead (timed equal to loading it in place, profiles/r2m: four blocks per CU already hide it).
         const bool reload = k > 0 && needed && !(NUSI_AB_BATCH & 8);
         double tnext = reload ? A[(size_t)p0 * g.PT + eidx] : 0.0;
         // member edges: thread (mq, mjob) copies job mjob of point mq of each chunk (loading the next chunk's
