@@ -15,6 +15,9 @@
 #include <array>
 #include <map>
 #include <memory>
+#include <mutex>
+#include <string>
+#include <sys/stat.h>
 #include <string>
 #include <utility>
 #include <vector>
@@ -278,6 +281,16 @@ void spline_weights(const std::vector<double>& x, std::vector<double>& w)
         }
     }
 }
+
+// file identity for the table-set cache of nusi_plan_load_phiphi
+std::string file_stamp(const char* path)
+{
+    struct stat sb;
+    if (stat(path, &sb) != 0) return std::string(path) + "|?";
+    return std::string(path) + "|" + std::to_string((long long)sb.st_size) + "|" + std::to_string((long long)sb.st_mtime);
+}
+std::mutex g_spl_mu;
+std::map<std::string, std::weak_ptr<SplineStore>> g_spl_cache;
 
 int load_spline(const char* path, int ndim, const int* dims, SplineStore& st, nusi::SplineDev& out)
 {
@@ -624,16 +637,31 @@ int nusi_plan_create(int device, int N_bins_E, double lEmin, double lEmax, doubl
     return NUSI_OK;
 }
 
+// Loaded table sets are shared by every plan / object on the same device that loads the same files
+// (path, dims, size and mtime): the reference reads the tables in every constructor
+// (nuSIprop.hpp:166-170); here a set costs 400 MB + its 6.4 GB of windows in HBM, so a second
+// calculate_flux object reuses the first one's while it is alive.
 int nusi_plan_load_phiphi(nusi_plan* pl, const char* at_path, const int* at_dims, const char* a_path, const int* a_dims)
 {
     static const int def2[2] = {5000, 100}, def3[3] = {1000, 1000, 100};
     HIPCHECK(hipSetDevice(pl->device));
+    const int* d2 = at_dims ? at_dims : def2;
+    const int* d3 = a_dims ? a_dims : def3;
+    const std::string key = std::to_string(pl->device) + "|" + file_stamp(at_path) + "|" + std::to_string(d2[0]) + "x" +
+                            std::to_string(d2[1]) + "|" + file_stamp(a_path) + "|" + std::to_string(d3[0]) + "x" +
+                            std::to_string(d3[1]) + "x" + std::to_string(d3[2]);
+    std::lock_guard<std::mutex> lock(g_spl_mu);
+    if (auto hit = g_spl_cache[key].lock()) {
+        pl->spl = hit;
+        return NUSI_OK;
+    }
     auto st = std::make_shared<SplineStore>();
     st->device = pl->device;
-    int r = load_spline(at_path, 2, at_dims ? at_dims : def2, *st, st->set.at);
+    int r = load_spline(at_path, 2, d2, *st, st->set.at);
     if (r) return r;
-    r = load_spline(a_path, 3, a_dims ? a_dims : def3, *st, st->set.a);
+    r = load_spline(a_path, 3, d3, *st, st->set.a);
     if (r) return r;
+    g_spl_cache[key] = st;
     pl->spl = st;
     return NUSI_OK;
 }

@@ -1,1 +1,3 @@
-bash scripts/ab_libs.sh r2aa "c4 c3" base xin
+mkdir -p gpurun_out/r2ab
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/r2ab/pytest.log 2>&1 && \
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/r2ab/smoke.log 2>&1
