@@ -10,7 +10,9 @@ its own tables) per GPU; with N GPUs each rank evolves its own 1024 points
 collective on the data path.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c4|c5|c3|c2|c1] [--points P]
-Multi-GPU: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+Multi-GPU: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N, or plain
+`python bench.py --gpus N`, which starts that launcher itself (N fresh rank processes, before any GPU
+call here) and exits with its status; a rank count that differs from --gpus is an error.
 
 Prints one JSON line (rank 0) with roofline (the dominant alpha-table kernel, fp64 VALU),
 roofline_cascade (the metric's cascade HBM GB/s) and the cpu_baseline (the C oracle on a
@@ -34,19 +36,22 @@ FP64_PEAK_TFLOPS = 78.6        # MI355X fp64 vector spec
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None, help="GPUs = ranks (default: WORLD_SIZE, else 1)")
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--workload", default="c4", choices=["c4", "c5", "c3", "c2", "c1"])
     ap.add_argument("--points", type=int, default=0, help="points per GPU (default: 1024 for c4 and c3, 8192 for c5, 1 for c2)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="budget of the oracle CPU baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cascade", default="mfma", choices=["mfma", "wf", "auto"],
-                    help="cascade kernel: mfma = wavefront with the push on the fp64 matrix cores (default, "
-                         "fastest measured), wf = the bit-exact wavefront kernel, auto = the library's choice")
+    ap.add_argument("--cascade", default="auto", choices=["auto", "mfma", "wf"],
+                    help="cascade kernel: auto = the library default (= mfma: the warp-specialised wavefront with "
+                         "the push on the fp64 matrix cores), wf = the bit-exact scalar wavefront")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launch / rank / reduction plumbing only, no GPU work (gloo; CPU tests): prints the JSON "
+                         "line with value null")
     ap.add_argument("--traffic-json", default="",
                     help="per-launch HBM bytes / fp64 VALU work from rocprofv3 --pmc passes (scripts/pmc_summary.py); "
-                         "default for the default workload: the committed profiles/pmc_traffic_latest.json")
+                         "default: the committed profiles/pmc_traffic_<workload>.json, used only if its libnusi_sha256 matches the loaded library")
     return ap.parse_args()
 
 
@@ -99,8 +104,11 @@ def host_cores():
                     break
     except OSError:
         pass
-    return (min(aff, cap) if cap > 0 else aff), {"nproc": os.cpu_count(), "affinity": aff,
-                                                   "OMP_NUM_THREADS": cap or None, "cpu_model": model}
+    used = min(aff, cap) if cap > 0 else aff
+    note = ("capped by OMP_NUM_THREADS=%d (the GPU box's CPU share) of %d CPUs in the affinity mask, nproc %s"
+            % (cap, aff, os.cpu_count())) if 0 < cap < aff else "the whole affinity mask (%d CPUs)" % aff
+    return used, {"nproc": os.cpu_count(), "affinity": aff, "OMP_NUM_THREADS": cap or None, "cpu_model": model,
+                  "cores_note": note}
 
 
 def _oracle(p):
@@ -152,7 +160,8 @@ def cpu_baseline(pts, budget_s):
         list(ex.map(work, range(threads)))
     dt = time.perf_counter() - t0
     n = sum(done)
-    return {"value": n / dt, "unit": "propagations/s", "cores": threads, "kind": "port",
+    return {"value": n / dt, "unit": "propagations/s", "cores": threads, "cores_note": host["cores_note"],
+            "kind": "port",
             "sample": "%d full propagations of the same workload (points cycled from the first) on a %d-thread pool "
                       "of the single-threaded C oracle, %.1f s" % (n, threads, dt),
             "host": host,
@@ -206,12 +215,85 @@ def single_point_latency(pt, reps):
             "path": "nusi_create + nusi_evolve + nusi_get_flux_fla (object API, host I/O and sync included)"}
 
 
+def free_port():
+    import socket
+    sk = socket.socket()
+    sk.bind(("127.0.0.1", 0))
+    port = sk.getsockname()[1]
+    sk.close()
+    return port
+
+
+def launch_ranks(args):
+    """--gpus N > 1 without a launcher: start N rank processes with torch.distributed.run (one per GPU, RCCL
+    rendezvous on 127.0.0.1) -- before anything here has touched the GPU -- and return their exit status.  A
+    rank count that differs from --gpus is an error, never an N-GPU label on a different run."""
+    world_env = os.environ.get("WORLD_SIZE")
+    if world_env is not None:
+        if args.gpus is not None and int(world_env) != args.gpus:
+            sys.exit("bench.py: --gpus %d but WORLD_SIZE=%s ranks were launched" % (args.gpus, world_env))
+        return None
+    if not args.gpus or args.gpus == 1:
+        return None
+    if args.gpus < 1:
+        sys.exit("bench.py: --gpus must be >= 1")
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(args.gpus),
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    print("bench.py: launching %d ranks: %s" % (args.gpus, " ".join(cmd)), file=sys.stderr, flush=True)
+    return subprocess.call(cmd)
+
+
+def file_sha256(path):
+    import hashlib
+    h = hashlib.sha256()
+    with open(path, "rb") as fh:
+        for chunk in iter(lambda: fh.read(1 << 20), b""):
+            h.update(chunk)
+    return h.hexdigest()
+
+
+def dry_run(args, world, rank):
+    """The launch / rank / reduction path without GPU work (gloo): each rank 'steps' for 1 ms; the line carries
+    n_gpus = the ranks that ran and value null."""
+    import torch
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("gloo")
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        time.sleep(0.001)
+    dt = time.perf_counter() - t0
+    ranks = 1
+    if dist is not None:
+        tt = torch.tensor([dt, 1.0], dtype=torch.float64)
+        dist.all_reduce(tt[:1], op=dist.ReduceOp.MAX)
+        one = torch.ones(1, dtype=torch.float64)
+        dist.all_reduce(one, op=dist.ReduceOp.SUM)
+        dt, ranks = float(tt[0]), int(one.item())
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": None, "unit": "propagations/s", "n_gpus": world,
+                          "ranks_reporting": ranks, "steps": args.steps, "warmup": args.warmup,
+                          "ms_per_step": dt / max(args.steps, 1) * 1e3, "dry_run": True}), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
 def main():
     args = parse()
+    rc = launch_ranks(args)
+    if rc is not None:
+        sys.exit(rc)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.dry_run:
+        return dry_run(args, world, rank)
     import torch
+    ndev = torch.cuda.device_count()   # (does not initialise the GPU)
+    if local >= ndev:
+        sys.exit("bench.py: rank %d needs GPU %d but %d device(s) are visible" % (rank, local, ndev))
     dist = None
     if world > 1:
         import torch.distributed as dist
@@ -220,7 +302,7 @@ def main():
     else:
         torch.cuda.set_device(local)
     import nusiprop_amd as nu
-    from nusiprop_amd import scan
+    from nusiprop_amd import _lib, scan
 
     pts, desc = rank_points(args, rank, world)
     P = len(pts)
@@ -235,7 +317,6 @@ def main():
         plan.load_phiphi(at, a)                           # dims = NULL: {5000,100}, {1000,1000,100}
         shutil.rmtree(tdir, ignore_errors=True)
     arr = plan.params_array(pts)
-    from nusiprop_amd import _lib
     plan.set_cascade({"mfma": _lib.CASCADE_MFMA, "wf": _lib.CASCADE_WAVEFRONT, "auto": _lib.CASCADE_AUTO}[args.cascade])
     dev = torch.device("cuda", local)
     flux = torch.empty((P, 3, plan.N), dtype=torch.float64, device=dev)
@@ -277,14 +358,20 @@ def main():
     casc_s = sum_ms[2] / max(ncalls, 1) / 1e3
     alpha_s = sum_ms[1] / max(ncalls, 1) / 1e3
     traffic, tsrc, pmc = None, None, {}
+    lib_sha = file_sha256(_lib.LIB_PATH)
     tj = args.traffic_json
-    if not tj and args.workload == "c4" and not args.points:
-        tj = os.path.join(ROOT, "profiles", "pmc_traffic_latest.json")
+    if not tj and not args.points:
+        tj = os.path.join(ROOT, "profiles", "pmc_traffic_%s.json" % args.workload)
+    pmc_note = None
     if tj and os.path.exists(tj):
         with open(tj) as fh:
             pmc = json.load(fh)
-        traffic = pmc.get("k_cascade_bytes_per_launch")
         tsrc = os.path.relpath(tj, ROOT)
+        if pmc.get("libnusi_sha256") != lib_sha:   # counters of another binary: not this kernel's traffic
+            pmc_note = "%s was collected on libnusi.so %s, not the loaded %s: traffic / flops dropped" % (
+                tsrc, str(pmc.get("libnusi_sha256"))[:12], lib_sha[:12])
+            pmc = {}
+        traffic = pmc.get("k_cascade_bytes_per_launch")
     achieved = casc_bytes / casc_s / 1e9
     # workgroups that read a table: one per point, or one per pair of points sharing a table on the multi-RHS
     # kernel (the pair reads its alpha table once)
@@ -308,7 +395,10 @@ def main():
         "dtype": "f64",
         "data": "synthetic (deterministic scan grid; power-law source)",
         "config": {"workload": desc, "N_E": N, "N_z": Nz, "points_per_gpu": P, "lEmin": p0["lEmin"],
-                   "lEmax": p0["lEmax"], "parallelism": "independent points, %d GPU(s), no collective" % world},
+                   "lEmax": p0["lEmax"], "parallelism": "independent points, %d GPU(s), no collective" % world,
+                   "alpha_kernel": alpha_kernel, "cascade_kernel": casc_kernel, "cascade_kind": args.cascade},
+        "libnusi": {"path": os.path.relpath(_lib.LIB_PATH, ROOT), "sha256": lib_sha, "pmc_source": tsrc,
+                    "pmc_note": pmc_note},
         "stage_ms_per_step": {"gamma_alphatilde": sum_ms[0] / max(ncalls, 1), "alpha": sum_ms[1] / max(ncalls, 1),
                               "cascade": sum_ms[2] / max(ncalls, 1)},
         "alpha_table": {"kernel": alpha_kernel, "bound": "fp64 VALU (transcendental)",
@@ -328,7 +418,7 @@ def main():
         "invalid_outputs": bad,
         "phiphi_lookups_out_of_range": oob,
     }
-    if args.cascade == "mfma" and "ws" in casc_kernel or "mfma" in casc_kernel:   # the push on the matrix cores
+    if "ws" in casc_kernel:   # the push on the matrix cores
         mf = scan.cascade_mfma_flops_per_point(N, Nz) * P
         out["roofline_cascade"]["mfma"] = {"flops_per_launch": mf, "achieved": mf / casc_s / 1e12,
                                            "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",

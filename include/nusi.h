@@ -86,7 +86,8 @@ typedef struct nusi_handle nusi_handle;
  * non_resonant && phiphi the phi-phi tables are loaded like the reference,
  * from xsec/alphatilde_phiphi.bin and xsec/alpha_phiphi.bin relative to the
  * current directory (or $NUSI_XSEC_DIR), -> NUSI_ETABLE if missing.
- * The object evolves on GPU `$NUSI_DEVICE` (default 0). */
+ * The object evolves on GPU `$NUSI_DEVICE` (default 0) with the default
+ * (NUSI_CASCADE_AUTO) kernels. */
 int nusi_create(const nusi_params *p, nusi_handle **out);
 /* copy constructor / operator=  (nuSIprop.hpp:434-525) */
 int nusi_copy(const nusi_handle *src, nusi_handle **out);
@@ -105,6 +106,9 @@ int nusi_get_energies(const nusi_handle *h, double *out_N);    /* get_energy(i) 
 int nusi_get_N_bins_E(const nusi_handle *h);                   /* get_N_bins_E()    :407-410 */
 int nusi_get_N_steps_z(const nusi_handle *h);
 int nusi_get_warnings(const nusi_handle *h);                   /* NUSI_WARN_* of the last evolve */
+/* names of the alpha-table and cascade kernels the last evolve() launched (static strings; no reference
+ * counterpart -- reports and tests) */
+int nusi_get_kernels(const nusi_handle *h, const char **alpha, const char **cascade);
 
 /* ---------------------------------------------------------------------------
  * 2. plan API -- batched parameter scans on one GPU
@@ -139,18 +143,42 @@ int nusi_plan_stage_ms(nusi_plan *plan, float *ms3);
  * summed ms per stage and the number of calls recorded. */
 int nusi_plan_profile_begin(nusi_plan *plan, int max_calls);
 int nusi_plan_profile_end(nusi_plan *plan, double *sum_ms3, int *ncalls);
-/* Cascade kernel of the plan's later calls (WAVEFRONT, REG and LDS give the
- * same fluxes bit for bit, MFMA the same to rounding; the choice is a
- * performance / A-B knob):
- * AUTO = wavefront when the grid fits it (Nz-1 <= 48, T-1 <= 512), else
- * register-resident (N <= 1280), else LDS.  A kind that does not fit the
- * grid falls back the same way.  NUSI_EPARAM for an unknown kind. */
+/* Cascade kernel of the plan's later calls.  Every kind meets the same flux
+ * tolerance against the reference algorithm (<= 1e-11 relative, the same
+ * exact zeros); the choice is a performance / cross-check knob:
+ * AUTO (default, also for the object API) = MFMA.
+ * MFMA = the warp-specialised wavefront with the push on the fp64 matrix
+ *   cores (k_cascade_ws, one pass, Nz-1 <= 48; k_cascade_ws_passes beyond),
+ *   for both sources and both scattering modes; points sharing a Stage-A
+ *   table share one workgroup (multi-RHS).  Grids beyond its limits fall back
+ *   to REG / LDS.
+ * WAVEFRONT, REG, LDS = the bit-exact scalar kernels (right-looking fma()s in
+ *   one fixed order: WAVEFRONT and REG agree bit for bit): wavefront when
+ *   the grid fits it (Nz-1 <= 48, T-1 <= 512), else register-resident
+ *   (N <= 1280), else LDS.
+ * NUSI_EPARAM for an unknown kind. */
 #define NUSI_CASCADE_AUTO 0
 #define NUSI_CASCADE_WAVEFRONT 1
 #define NUSI_CASCADE_REG 2
 #define NUSI_CASCADE_LDS 3
-#define NUSI_CASCADE_MFMA 4   /* wavefront with the push as fp64 MFMA rank-4 updates (fluxes to rounding) */
+#define NUSI_CASCADE_MFMA 4
 int nusi_plan_set_cascade(nusi_plan *plan, int kind);
+/* Explicit A/B and test options of a plan (no reference counterpart).  The
+ * defaults are the production choices, and nothing in the library reads the
+ * environment to select kernels.  NUSI_EPARAM for an unknown option or value.
+ *   NUSI_OPT_ALPHA_BATCH   max tables per alpha batch (tables sharing m_phi,
+ *                          masses and flags), 1..255; 0 = automatic
+ *   NUSI_OPT_ALPHA_KERNEL  0 = k_alpha_batch (default), 1 = k_alpha_tile
+ *                          batches of <= 4, 2 = one entry per work-item
+ *   NUSI_OPT_CASCADE_RHS   max points sharing a table per MFMA-cascade
+ *                          workgroup: 0 = automatic, 1 = one point each
+ *   NUSI_OPT_STEP_PASSES   0 = automatic (step passes beyond 48 redshift
+ *                          steps), 1 = always the step-pass kernel */
+#define NUSI_OPT_ALPHA_BATCH 1
+#define NUSI_OPT_ALPHA_KERNEL 2
+#define NUSI_OPT_CASCADE_RHS 3
+#define NUSI_OPT_STEP_PASSES 4
+int nusi_plan_set_option(nusi_plan *plan, int option, int value);
 /* per-point NUSI_WARN_* bits of the last call */
 int nusi_plan_warnings(nusi_plan *plan, int *out, int n);
 /* Names of the main alpha-table and cascade kernels the last call launched (static strings, e.g.

@@ -282,15 +282,24 @@ void spline_weights(const std::vector<double>& x, std::vector<double>& w)
     }
 }
 
-// file identity for the table-set cache of nusi_plan_load_phiphi
+// file identity for the table-set cache of nusi_plan_load_phiphi: path, device and inode, size and the
+// modification time to the nanosecond (a file rewritten in place gets a new mtime)
 std::string file_stamp(const char* path)
 {
     struct stat sb;
     if (stat(path, &sb) != 0) return std::string(path) + "|?";
-    return std::string(path) + "|" + std::to_string((long long)sb.st_size) + "|" + std::to_string((long long)sb.st_mtime);
+    return std::string(path) + "|" + std::to_string((unsigned long long)sb.st_dev) + ":" +
+           std::to_string((unsigned long long)sb.st_ino) + "|" + std::to_string((long long)sb.st_size) + "|" +
+           std::to_string((long long)sb.st_mtim.tv_sec) + "." + std::to_string((long long)sb.st_mtim.tv_nsec);
 }
-std::mutex g_spl_mu;
-std::map<std::string, std::weak_ptr<SplineStore>> g_spl_cache;
+// the cache: one entry per key; its mutex is held while that key loads (1.6 GB read + upload + windows), so
+// loads of other keys (e.g. the same files on another device) run concurrently
+struct SplineSlot {
+    std::mutex mu;
+    std::weak_ptr<SplineStore> set;
+};
+std::mutex g_spl_mu;   // guards the map only
+std::map<std::string, std::shared_ptr<SplineSlot>> g_spl_cache;
 
 int load_spline(const char* path, int ndim, const int* dims, SplineStore& st, nusi::SplineDev& out)
 {
@@ -369,7 +378,7 @@ int load_spline(const char* path, int ndim, const int* dims, SplineStore& st, nu
     st.bufs.push_back(df);
     HIPCHECK(hipMemcpy(df, f.data(), sizeof(float) * nf, hipMemcpyHostToDevice));
     sd.f = df;
-    if (ndim == 3 && !(getenv("NUSI_SPLINE_WINDOWS") && getenv("NUSI_SPLINE_WINDOWS")[0] == '0')) {
+    if (ndim == 3) {
         float* dw = nullptr;   // 16 x the table: the 4 x 4 windows of nusi_spline.hpp
         HIPCHECK(hipMalloc(&dw, sizeof(float) * 16 * nf));
         st.bufs.push_back(dw);
@@ -400,8 +409,12 @@ struct nusi_plan {
     int2* h_groups = nullptr;       // pinned
     int* d_batches = nullptr;       // alpha-table batches (nusi::launch_alpha): first table | count << 24
     int* h_batches = nullptr;       // pinned
-    int alpha_batch = 0;            // max tables per batch; 0 = auto (alpha_batch_cap); NUSI_ALPHA_BATCH overrides
-    bool alpha_tile_kernel = false; // NUSI_ALPHA_KERNEL=tile: k_alpha_tile<G> batches of <= 4 (A/B)
+    int alpha_batch = 0;            // NUSI_OPT_ALPHA_BATCH: max tables per batch; 0 = auto
+    int alpha_kind = 0;             // NUSI_OPT_ALPHA_KERNEL: 0 k_alpha_batch, 1 k_alpha_tile<G> (<= 4), 2 per entry
+    int cascade_rhs = 0;            // NUSI_OPT_CASCADE_RHS: 0 = auto, 1 = one point per MFMA-cascade workgroup
+    int step_passes = 0;            // NUSI_OPT_STEP_PASSES: 1 = the step-pass cascade also where one pass fits
+    double* d_src = nullptr;        // DSNB source terms of the MFMA cascade [src_cap][cascade_src_doubles]
+    int src_cap = 0;
     std::vector<int> slot_of;       // table slot of each point of the last call
     int last_ntab = 0;
     int* d_warn = nullptr;
@@ -550,6 +563,7 @@ void nusi_plan_destroy(nusi_plan* pl)
     hipFree(pl->tabs.At);
     hipFree(pl->tabs.A);
     hipFree(pl->tabs.Med);
+    hipFree(pl->d_src);
     nusi::alpha_tiles_destroy(&pl->atiles);
     hipFree(pl->d_scratch);
     if (pl->h_pts) hipHostFree(pl->h_pts);
@@ -623,8 +637,6 @@ int nusi_plan_create(int device, int N_bins_E, double lEmin, double lEmax, doubl
     HIPCHECK(hipMalloc(&pl->d_groups, sizeof(int2) * max_points));
     HIPCHECK(hipHostMalloc((void**)&pl->h_groups, sizeof(int2) * max_points, hipHostMallocDefault));
     HIPCHECK(hipHostMalloc((void**)&pl->h_batches, sizeof(int) * max_points, hipHostMallocDefault));
-    if (const char* e = getenv("NUSI_ALPHA_KERNEL")) pl->alpha_tile_kernel = e[0] == 't';
-    if (const char* e = getenv("NUSI_ALPHA_BATCH")) pl->alpha_batch = std::max(1, std::min(pl->alpha_tile_kernel ? 4 : 255, atoi(e)));
     HIPCHECK(hipMalloc(&pl->d_warn, sizeof(int) * max_points));
     HIPCHECK(hipMalloc(&pl->tabs.G, sizeof(double) * (size_t)G.T * max_points));
     HIPCHECK(hipMalloc(&pl->tabs.At, sizeof(double) * (size_t)G.T * max_points));
@@ -644,14 +656,23 @@ int nusi_plan_create(int device, int N_bins_E, double lEmin, double lEmax, doubl
 int nusi_plan_load_phiphi(nusi_plan* pl, const char* at_path, const int* at_dims, const char* a_path, const int* a_dims)
 {
     static const int def2[2] = {5000, 100}, def3[3] = {1000, 1000, 100};
+    if (!pl) return fail(NUSI_EPARAM, "plan is NULL");
+    if (!at_path || !a_path) return fail(NUSI_EPARAM, "phi-phi table path is NULL");
     HIPCHECK(hipSetDevice(pl->device));
     const int* d2 = at_dims ? at_dims : def2;
     const int* d3 = a_dims ? a_dims : def3;
     const std::string key = std::to_string(pl->device) + "|" + file_stamp(at_path) + "|" + std::to_string(d2[0]) + "x" +
                             std::to_string(d2[1]) + "|" + file_stamp(a_path) + "|" + std::to_string(d3[0]) + "x" +
                             std::to_string(d3[1]) + "x" + std::to_string(d3[2]);
-    std::lock_guard<std::mutex> lock(g_spl_mu);
-    if (auto hit = g_spl_cache[key].lock()) {
+    std::shared_ptr<SplineSlot> slot;
+    {
+        std::lock_guard<std::mutex> lock(g_spl_mu);
+        auto& e = g_spl_cache[key];
+        if (!e) e = std::make_shared<SplineSlot>();
+        slot = e;
+    }
+    std::lock_guard<std::mutex> lock(slot->mu);
+    if (auto hit = slot->set.lock()) {
         pl->spl = hit;
         return NUSI_OK;
     }
@@ -661,7 +682,7 @@ int nusi_plan_load_phiphi(nusi_plan* pl, const char* at_path, const int* at_dims
     if (r) return r;
     r = load_spline(a_path, 3, d3, *st, st->set.a);
     if (r) return r;
-    g_spl_cache[key] = st;
+    slot->set = st;
     pl->spl = st;
     return NUSI_OK;
 }
@@ -726,9 +747,9 @@ int nusi_plan_evolve(nusi_plan* pl, const nusi_params* pts, int n, double* d_flu
     // batch cap: the tile kernel's LDS holds <= 4 (3 measured best); the big-batch kernel shares the leaves of
     // any number, but one workgroup runs a batch's points one after the other, so the cap keeps ~2 rounds of
     // workgroups per CU slot (256 CUs x 3) in the grid: ntab x class-0 tiles / cap >= 1536
-    int cap = pl->alpha_batch;
+    int cap = pl->alpha_kind == 1 ? std::min(pl->alpha_batch, 4) : pl->alpha_batch;
     if (cap <= 0) {
-        if (pl->alpha_tile_kernel) cap = 3;
+        if (pl->alpha_kind == 1) cap = 3;
         else {
             const long long work = (long long)ntab * std::max(1, pl->atiles.ncls[0]);
             cap = (int)std::max(1LL, std::min(64LL, (work + 1535) / 1536));
@@ -757,17 +778,19 @@ int nusi_plan_evolve(nusi_plan* pl, const nusi_params* pts, int n, double* d_flu
         if (!d_flux) d_flux = pl->d_scratch;
         if (!d_fla) d_fla = pl->d_scratch + N3 * pl->max_points;
     }
-    // the cascade: points sharing a table slot run in pairs on the multi-RHS kernel (k_cascade_ws<R = 2>: one
-    // operator, two sources) when every point is non-resonant with the power-law source and most points pair up
-    bool all_pl = true, all_nr = true;
+    // the cascade.  AUTO / MFMA: the warp-specialised MFMA kernels for every point kind, points sharing a table
+    // slot in pairs on the multi-RHS form (k_cascade_ws<R = 2>: one operator, two sources) when most points pair
+    // up; the step-pass kernel beyond 48 redshift steps.  WAVEFRONT / REG / LDS: the bit-exact scalar kernels.
+    const int kind = pl->cascade_kind == NUSI_CASCADE_AUTO ? NUSI_CASCADE_MFMA : pl->cascade_kind;
+    bool all_pl = true, any_dsnb = false;
     for (int i = 0; i < n; ++i) {
         all_pl = all_pl && pl->h_pts[i].source == NUSI_SOURCE_POWER_LAW;
-        all_nr = all_nr && pl->h_pts[i].non_resonant;
+        any_dsnb = any_dsnb || pl->h_pts[i].source == NUSI_SOURCE_DSNB;
     }
+    const bool one_pass = nusi::cascade_ws_fits(pl->gd, 1) && pl->step_passes != 1;
+    const bool fast = kind == NUSI_CASCADE_MFMA && (one_pass || nusi::cascade_wsp_fits(pl->gd));
     int ngroups = 0;
-    const char* mrhs_env = getenv("NUSI_MRHS");     // A/B: 0 = one point per workgroup
-    if (pl->cascade_kind == NUSI_CASCADE_MFMA && all_pl && all_nr && !(mrhs_env && mrhs_env[0] == '0') &&
-        nusi::cascade_ws_fits(pl->gd, 2)) {
+    if (fast && one_pass && pl->cascade_rhs != 1 && nusi::cascade_ws_fits(pl->gd, 2)) {
         std::vector<int> open(ntab, -1);   // per table slot: a point waiting for its partner
         for (int i = 0; i < n; ++i) {
             int& o = open[pl->h_pts[i].tslot];
@@ -777,6 +800,14 @@ int nusi_plan_evolve(nusi_plan* pl, const nusi_params* pts, int n, double* d_flu
         for (int j = 0; j < ntab; ++j)
             if (open[j] >= 0) pl->h_groups[ngroups++] = make_int2(open[j], -1);
         if (4 * ngroups > 3 * n) ngroups = 0;   // too few pairs: one point per workgroup
+    }
+    if (fast && any_dsnb && pl->src_cap < pl->max_points) {
+        hipFree(pl->d_src);
+        pl->d_src = nullptr;
+        pl->src_cap = 0;
+        HIPCHECK(hipMalloc(&pl->d_src, sizeof(double) * nusi::cascade_src_doubles(pl->gd) * pl->max_points));
+        pl->src_cap = pl->max_points;
+        pl->tabs.Src = pl->d_src;
     }
     if (ngroups) HIPCHECK(hipMemcpyAsync(pl->d_groups, pl->h_groups, sizeof(int2) * ngroups, hipMemcpyHostToDevice, s));
     HIPCHECK(hipMemcpyAsync(pl->d_pts, pl->h_pts, sizeof(nusi::Point) * n, hipMemcpyHostToDevice, s));
@@ -791,13 +822,18 @@ int nusi_plan_evolve(nusi_plan* pl, const nusi_params* pts, int n, double* d_flu
     HIPCHECK(nusi::launch_gamma_alphat(pl->gd, pl->d_tpts, ntab, spl, pl->tabs, pl->d_warn, s));
     HIPCHECK(hipEventRecord(ev[1], s));
     HIPCHECK(nusi::launch_alpha(pl->gd, pl->d_tpts, ntab, spl, pl->atiles, pl->tabs, pl->d_warn, s, pl->d_batches,
-                                nbatch, pl->alpha_tile_kernel ? std::min(cap, 4) : cap, pl->alpha_tile_kernel,
-                                nb_plain));
+                                nbatch, cap, pl->alpha_kind, nb_plain));
     HIPCHECK(hipEventRecord(ev[2], s));
-    if (ngroups)
+    if (fast && any_dsnb) HIPCHECK(nusi::launch_source_dsnb(pl->gd, pl->d_pts, n, pl->d_src, s));
+    if (fast && ngroups)
         HIPCHECK(nusi::launch_cascade_ws(pl->gd, pl->d_pts, 2, pl->d_groups, ngroups, pl->tabs, d_flux, d_fla, s));
+    else if (fast && one_pass)
+        HIPCHECK(nusi::launch_cascade_ws(pl->gd, pl->d_pts, 1, nullptr, n, pl->tabs, d_flux, d_fla, s));
+    else if (fast)
+        HIPCHECK(nusi::launch_cascade_wsp(pl->gd, pl->d_pts, n, pl->tabs, d_flux, d_fla, s));
     else
-        HIPCHECK(nusi::launch_cascade(pl->gd, pl->d_pts, n, pl->tabs, d_flux, d_fla, s, pl->cascade_kind, all_pl, all_nr));
+        HIPCHECK(nusi::launch_cascade_exact(pl->gd, pl->d_pts, n, pl->tabs, d_flux, d_fla, s,
+                                            kind == NUSI_CASCADE_MFMA ? NUSI_CASCADE_WAVEFRONT : kind, all_pl));
     HIPCHECK(hipEventRecord(ev[3], s));
     HIPCHECK(hipEventRecord(pl->ev_done, s));
     pl->alpha_kernel = nusi::last_alpha_kernel();
@@ -857,6 +893,31 @@ int nusi_plan_set_cascade(nusi_plan* pl, int kind)
     if (kind < NUSI_CASCADE_AUTO || kind > NUSI_CASCADE_MFMA) return fail(NUSI_EPARAM, "unknown cascade kind");
     pl->cascade_kind = kind;
     return NUSI_OK;
+}
+
+int nusi_plan_set_option(nusi_plan* pl, int option, int value)
+{
+    if (!pl) return fail(NUSI_EPARAM, "plan is NULL");
+    switch (option) {
+    case NUSI_OPT_ALPHA_BATCH:
+        if (value < 0 || value > 255) return fail(NUSI_EPARAM, "NUSI_OPT_ALPHA_BATCH outside [0, 255]");
+        pl->alpha_batch = value;
+        return NUSI_OK;
+    case NUSI_OPT_ALPHA_KERNEL:
+        if (value < 0 || value > 2) return fail(NUSI_EPARAM, "NUSI_OPT_ALPHA_KERNEL outside [0, 2]");
+        pl->alpha_kind = value;
+        return NUSI_OK;
+    case NUSI_OPT_CASCADE_RHS:
+        if (value < 0 || value > 2) return fail(NUSI_EPARAM, "NUSI_OPT_CASCADE_RHS outside [0, 2]");
+        pl->cascade_rhs = value;
+        return NUSI_OK;
+    case NUSI_OPT_STEP_PASSES:
+        if (value < 0 || value > 1) return fail(NUSI_EPARAM, "NUSI_OPT_STEP_PASSES outside [0, 1]");
+        pl->step_passes = value;
+        return NUSI_OK;
+    default:
+        return fail(NUSI_EPARAM, "unknown plan option");
+    }
 }
 
 int nusi_plan_warnings(nusi_plan* pl, int* out, int n)
@@ -1049,5 +1110,10 @@ int nusi_get_energies(const nusi_handle* h, double* out)
 int nusi_get_N_bins_E(const nusi_handle* h) { return h->plan->grid.N; }
 int nusi_get_N_steps_z(const nusi_handle* h) { return h->plan->grid.Nz; }
 int nusi_get_warnings(const nusi_handle* h) { return h->warn; }
+int nusi_get_kernels(const nusi_handle* h, const char** alpha, const char** cascade)
+{
+    if (!h->evolved) return fail(NUSI_ESTATE, "no evolve has run on this object");
+    return nusi_plan_kernels(h->plan, alpha, cascade);
+}
 
 }  // extern "C"

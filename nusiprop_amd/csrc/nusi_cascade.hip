@@ -1,11 +1,15 @@
 // nuSIprop MI355X -- Stage B: the implicit redshift cascade + finalisation
-// (calculate_flux::evolve, nuSIprop.hpp:255-336), one wavefront per point.
+// (calculate_flux::evolve, nuSIprop.hpp:255-336).
 //
-//   k_cascade_reg<NQ, D>  register-resident chain, N <= 64 NQ (default path)
-//   k_cascade             LDS-resident generic path (any N; NUSI_CASCADE_LDS=1)
+//   k_cascade_ws<NJ, R>   warp-specialised wavefront, push on the fp64 matrix cores, R points sharing a
+//                         table per workgroup (NUSI_CASCADE_AUTO / MFMA, Nz-1 <= 48)
+//   k_cascade_wsp<NJ>     the same in passes of 16 redshift steps (Nz-1 > 48)
+//   k_source_dsnb         the DSNB source terms those two read
+//   k_cascade_wf<NJ>      bit-exact scalar wavefront (NUSI_CASCADE_WAVEFRONT)
+//   k_cascade_reg<NQ, D>  bit-exact per-step chain in registers, N <= 64 NQ (NUSI_CASCADE_REG, fallback)
+//   k_cascade             LDS-resident generic path, any N (NUSI_CASCADE_LDS, last fallback)
 #include <hip/hip_runtime.h>
 
-#include <cstdlib>
 #include <utility>
 
 #include "nusi_internal.hpp"
@@ -528,15 +532,9 @@ __global__ __launch_bounds__(64) void k_cascade_reg(GridDev g, const Point* __re
 // never feed a solve.
 // ---------------------------------------------------------------------------
 constexpr int kWfFields = kPreFields + 1;   // PR_* and the permutation
-#ifndef NUSI_WF_AB
-#define NUSI_WF_AB 0   // timing experiments only: 1 skip records, 2 skip push, 4 skip solve, 8 no alpha loads
-#endif
 constexpr int kWfMaxThreads = 512;
 constexpr int kWfRows = 4, kWfQuarters = 4;   // push: rows per thread, step groups per row group
-#ifndef NUSI_WF_PRE
-#define NUSI_WF_PRE 2
-#endif
-constexpr int kWfPre = NUSI_WF_PRE;           // alpha columns in flight (stages of prefetch)
+constexpr int kWfPre = 2;           // alpha columns in flight (stages of prefetch)
 
 template <int NJ, bool kPowerLaw>
 __global__ __launch_bounds__(kWfMaxThreads) void k_cascade_wf(GridDev g, const Point* __restrict__ pts, TablesDev t,
@@ -618,7 +616,7 @@ __global__ __launch_bounds__(kWfMaxThreads) void k_cascade_wf(GridDev g, const P
 #pragma unroll
         for (int c = 0; c < kWfRows; ++c) {
             const int row = row0 + c;
-            dst[c] = (NUSI_WF_AB & 8) ? 1e-300 * row : Al[cb + (row < cl - 1 ? row : cl - 1)];
+            dst[c] = Al[cb + (row < cl - 1 ? row : cl - 1)];
         }
     };
     double a_ring[kWfPre][kWfRows];
@@ -643,7 +641,7 @@ __global__ __launch_bounds__(kWfMaxThreads) void k_cascade_wf(GridDev g, const P
             const int q = tid / NJ, jj = tid - q * NJ, s2 = sg + q;
             if (q < K && jj < nst && s2 < T) {
                 const int b = N - 1 - s2 + jj;
-                if (b >= 0 && b < N && !(NUSI_WF_AB & 1)) cascade_record<kPowerLaw>(gl, P, sGt, sAt, rdE, pw, Nz - 1 - jj, b, rec + q * NJ + jj, KR);
+                if (b >= 0 && b < N) cascade_record<kPowerLaw>(gl, P, sGt, sAt, rdE, pw, Nz - 1 - jj, b, rec + q * NJ + jj, KR);
             }
             __syncthreads();
         }
@@ -672,7 +670,6 @@ __global__ __launch_bounds__(kWfMaxThreads) void k_cascade_wf(GridDev g, const P
                     add = cj * racc * R[PR_SDE * KR];
                 }
                 double x0 = add, x1 = add, x2 = add;
-                if (!(NUSI_WF_AB & 4))
                 cascade_solve(F[b], F[N + b], F[2 * N + b], add, R[PR_SRC * KR], u0, u1, u2, R[PR_RZ0 * KR],
                               R[PR_RZ1 * KR], R[PR_RZ2 * KR], (int)R[kPreFields * KR], R[PR_L10 * KR], R[PR_L20 * KR],
                               R[PR_L21 * KR], R[PR_U01 * KR], R[PR_U02 * KR], R[PR_U12 * KR], R[PR_RU00 * KR],
@@ -685,7 +682,7 @@ __global__ __launch_bounds__(kWfMaxThreads) void k_cascade_wf(GridDev g, const P
             }
             Tp[cur * NJ + tid] = T_j;
             Tprev = T_j;
-        } else if (tid < cbase && nonres && r >= 1 && r + 1 <= T - 1 && row0 < r && !(NUSI_WF_AB & 2)) {
+        } else if (tid < cbase && nonres && r >= 1 && r + 1 <= T - 1 && row0 < r) {
             // push column r+1 (T of stage sg-1) into rows < r; rows >= r are consumed (row r through
             // the published copy), so a row group wholly at or above r stops pushing (whole waves drop
             // out as r falls); steps that have not started have T_j = 0, so nothing else is masked
@@ -722,221 +719,37 @@ __global__ __launch_bounds__(kWfMaxThreads) void k_cascade_wf(GridDev g, const P
     }
 }
 
-// ---------------------------------------------------------------------------
-// Wavefront cascade with the push on the fp64 matrix cores (NUSI_CASCADE_MFMA).
-//
-// The push of k_cascade_wf adds one column per stage: ACC[rows, steps] += alpha[rows, r+1] T[r+1, steps],
-// a rank-1 update.  Here the columns are pushed in blocks of four, once every four stages, as
-// ACC[rows, steps] += alpha[rows, 4 columns] . T[4 columns, steps] -- the transfer-matrix x
-// flux-batch GEMM, whose batch is the set of redshift steps in flight -- with
-// v_mfma_f64_16x16x4f64 on 16 x 16 tiles (row tile x step tile).  Push wave w owns rows
-// [64w, 64w+64) = 4 row tiles, each with NJ/16 step tiles in its accumulator registers
-// (C/D layout: step = lane & 15, row = (lane >> 4) + 4 reg).
-//
-// Block q runs at stage 4q and pushes columns T-4q .. T-4q+3 (the T_j of stages 4q-1 .. 4q-4)
-// into the rows below T-1-4q, then publishes the four rows the chain solves at stages
-// 4q+1 .. 4q+4.  At stage sg the published row therefore lacks the columns r+1 .. r+n_u,
-// n_u = sg - 4 ((sg-1) >> 2) in [1, 4]: the chain lane adds them itself from its last four T_j
-// and alpha(r, r+k) (staged in LDS), in descending column order.  The MFMA sums each block of
-// four columns in its own order, so the fluxes agree with k_cascade_wf to rounding (the tests'
-// 1e-11 relative bound vs the oracle), not bit for bit.  Records, solves and the resonant-only
-// chain are k_cascade_wf's.
-// ---------------------------------------------------------------------------
 typedef double nusi_f64x4 __attribute__((ext_vector_type(4)));
-constexpr int kMfRowTiles = 4;   // 16-row tiles per push wave
-
-template <int NJ, bool kPowerLaw>
-__global__ __launch_bounds__(kWfMaxThreads) void k_cascade_wf_mfma(GridDev g, const Point* __restrict__ pts,
-                                                                   TablesDev t, double* __restrict__ flux,
-                                                                   double* __restrict__ flux_fla, int K)
-{
-    extern __shared__ __attribute__((aligned(16))) double lds[];
-    constexpr int NST = NJ / 16;             // step tiles
-    const int N = g.N, Nz = g.Nz, T = g.T, nst = Nz - 1;
-    const int tid = threadIdx.x, nthr = blockDim.x;
-    const int KR = K * NJ;
-    double* F = lds;                         // [3][N]
-    double* rec = F + 3 * N;                 // [kWfFields][K][NJ]
-    double* Tp = rec + kWfFields * KR;       // [8][NJ]  T_j by stage (ring of 8)
-    double* AX = Tp + 8 * NJ;                // [2][4][NJ]  published rows of block q (parity q & 1)
-    double* rdE = AX + 8 * NJ;
-    double* pw = rdE + N;
-    double* sGt = pw + (T + 2);
-    double* sAt = sGt + T;
-    double* sdg = sAt + T;                   // [4][T]: alpha(n, n+k), k = 1..4 (0 past the table)
-    double* sEmin = sdg + 4 * T;
-    double* sEmax = sEmin + N;
-    double* sgz = sEmax + N;
-    GridDev gl = g;
-    gl.Emin = sEmin;
-    gl.Emax = sEmax;
-    gl.z = sgz;
-    gl.step_c = sgz + Nz;
-    gl.step_s = sgz + 2 * Nz;
-    gl.sfr = sgz + 3 * Nz;
-    const Point& P = pts[blockIdx.x];
-    const double u0 = P.u[0], u1 = P.u[1], u2 = P.u[2];
-    const double* __restrict__ Gt = t.G + (size_t)P.tslot * T;
-    const double* __restrict__ At = t.At + (size_t)P.tslot * T;
-    const double* __restrict__ Al = t.A + (size_t)P.tslot * g.PT;
-    const bool nonres = P.non_resonant;
-
-    for (int b = tid; b < 3 * N; b += nthr) F[b] = 0.0;
-    for (int j = tid; j < 16 * NJ; j += nthr) Tp[j] = 0.0;   // Tp and AX
-    for (int n = tid; n < T; n += nthr) {
-        sGt[n] = Gt[n];
-        sAt[n] = At[n];
-#pragma unroll
-        for (int k = 1; k <= 4; ++k) sdg[(k - 1) * T + n] = (n + k < T) ? Al[(size_t)(n + k) * (n + k - 1) / 2 + n] : 0.0;
-    }
-    for (int b = tid; b < N; b += nthr) { sEmin[b] = g.Emin[b]; sEmax[b] = g.Emax[b]; }
-    for (int i = tid; i < Nz; i += nthr) {
-        sgz[i] = g.z[i];
-        sgz[Nz + i] = g.step_c[i];
-        sgz[2 * Nz + i] = g.step_s[i];
-        sgz[3 * Nz + i] = g.sfr[i];
-    }
-    cascade_aux_init(g, P, rdE, pw, tid, nthr);
-    const int lane = tid & 63, wave = tid >> 6;
-    const int cbase = nthr - 64, cj_lane = tid - cbase;
-    const bool chain = cj_lane >= 0 && cj_lane < nst;
-    const int ist = Nz - 1 - cj_lane;
-    const int rw0 = wave * 64;               // first row of this push wave
-    nusi_f64x4 acc[kMfRowTiles][NST];
-#pragma unroll
-    for (int a = 0; a < kMfRowTiles; ++a)
-#pragma unroll
-        for (int s = 0; s < NST; ++s) acc[a][s] = nusi_f64x4{0.0, 0.0, 0.0, 0.0};
-    // A operands of the next block: alpha(row, column) with row = tile row + (lane & 15),
-    // column = first block column + (lane >> 4); rows clamped into the column (those rows are consumed)
-    auto load_blk = [&](int q, double (&dst)[kMfRowTiles]) {
-        int c = T - 4 * q + (lane >> 4);
-        c = c < 1 ? 1 : (c > T - 1 ? T - 1 : c);
-        const size_t cb = (size_t)c * (c - 1) / 2;
-#pragma unroll
-        for (int a = 0; a < kMfRowTiles; ++a) {
-            const int row = rw0 + 16 * a + (lane & 15);
-            dst[a] = Al[cb + (row < c - 1 ? row : c - 1)];
-        }
-    };
-#ifndef NUSI_MF_PRIO
-#define NUSI_MF_PRIO 0
-#endif
-    if (NUSI_MF_PRIO && tid >= cbase) __builtin_amdgcn_s_setprio(NUSI_MF_PRIO);   // the chain is the critical path
-    double ablk[kMfRowTiles];
-    if (tid < cbase) load_blk(1, ablk);
-    __syncthreads();
-    const double cj = chain ? gl.step_c[ist] : 0.0, sj = chain ? gl.step_s[ist] : 0.0;
-    double racc = 0.0, px0 = 0.0, px1 = 0.0, px2 = 0.0;
-    double Th[4] = {0.0, 0.0, 0.0, 0.0};     // the lane's T_j of stages sg-1 .. sg-4
-    for (int sg0 = 0; sg0 < T; sg0 += 4)
-#pragma unroll
-    for (int d = 0; d < 4; ++d) {
-        const int sg = sg0 + d;
-        if (sg >= T) break;
-        const int r = T - 1 - sg;
-        const int ks = sg % K;
-        if (ks == 0) {   // records of stages sg .. sg+K-1, one (stage, step) per thread
-            __syncthreads();
-            const int q = tid / NJ, jj = tid - q * NJ, s2 = sg + q;
-            if (q < K && jj < nst && s2 < T) {
-                const int b = N - 1 - s2 + jj;
-                if (b >= 0 && b < N) cascade_record<kPowerLaw>(gl, P, sGt, sAt, rdE, pw, Nz - 1 - jj, b, rec + q * NJ + jj, KR);
-            }
-            __syncthreads();
-        }
-        if (chain) {
-            const int tid = cj_lane;
-            const int b = N - 1 - sg + tid;
-            double T_j = 0.0;
-            if (b >= 0 && b < N) {
-                const double* R = rec + ks * NJ + tid;
-                double add;
-                if (nonres) {
-                    const int qq = (sg - 1) >> 2;              // block whose publication serves stage sg
-                    const int nu = (d == 0) ? 4 : d;           // columns r+1 .. r+nu not yet pushed
-                    double s = AX[((qq & 1) * 4 + (sg - 1 - 4 * qq)) * NJ + tid];
-#pragma unroll
-                    for (int k = 4; k >= 1; --k)
-                        if (k <= nu) s = fma(sdg[(k - 1) * T + r], Th[k - 1], s);
-                    add = cj * s;
-                } else {
-                    if (b != N - 1) {
-                        const double Sres = u0 * px0 + u1 * px1 + u2 * px2;
-                        const double sd = sdg[r];
-                        racc += Sres * (sj * sd) / (sEmax[b + 1] - sEmin[b + 1]) / R[PR_SDE * KR];
-                    }
-                    add = cj * racc * R[PR_SDE * KR];
-                }
-                double x0 = add, x1 = add, x2 = add;
-                cascade_solve(F[b], F[N + b], F[2 * N + b], add, R[PR_SRC * KR], u0, u1, u2, R[PR_RZ0 * KR],
-                              R[PR_RZ1 * KR], R[PR_RZ2 * KR], (int)R[kPreFields * KR], R[PR_L10 * KR], R[PR_L20 * KR],
-                              R[PR_L21 * KR], R[PR_U01 * KR], R[PR_U02 * KR], R[PR_U12 * KR], R[PR_RU00 * KR],
-                              R[PR_RU11 * KR], R[PR_RU22 * KR], x0, x1, x2);
-                F[b] = x0;
-                F[N + b] = x1;
-                F[2 * N + b] = x2;
-                px0 = x0; px1 = x1; px2 = x2;
-                if (nonres && b > 0) T_j = (u0 * x0 + u1 * x1 + u2 * x2) * R[PR_SDE * KR];
-            }
-            Tp[(sg & 7) * NJ + tid] = T_j;
-            Th[3] = Th[2]; Th[2] = Th[1]; Th[1] = Th[0]; Th[0] = T_j;
-        } else if (d == 0 && tid < cbase && nonres) {
-            // block q = sg / 4: columns c_k = T-4q+k, k = 0..3, carry the T of stage 4q-1-k
-            const int q = sg >> 2;
-            if (q >= 1) {
-#pragma unroll
-                for (int s = 0; s < NST; ++s) {
-                    const double bop = Tp[((sg - 1 - (lane >> 4)) & 7) * NJ + 16 * s + (lane & 15)];
-#pragma unroll
-                    for (int a = 0; a < kMfRowTiles; ++a)
-                        if (rw0 + 16 * a < r)   // tiles wholly at or above r hold consumed rows only
-                            acc[a][s] = __builtin_amdgcn_mfma_f64_16x16x4f64(ablk[a], bop, acc[a][s], 0, 0, 0);
-                }
-                load_blk(q + 1, ablk);
-            }
-            // publish rows r-1 .. r-4 (the rows of stages sg+1 .. sg+4) into AX[q & 1][0..3]
-            const int hi = r - 1;
-#pragma unroll
-            for (int a = 0; a < kMfRowTiles; ++a)
-                if (rw0 + 16 * a <= hi && rw0 + 16 * a + 15 >= hi - 3)   // uniform: tiles holding those rows
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    const int row = rw0 + 16 * a + (lane >> 4) + 4 * e;
-                    const int slot = hi - row;
-                    if (slot >= 0 && slot < 4)
-#pragma unroll
-                        for (int s = 0; s < NST; ++s) AX[((q & 1) * 4 + slot) * NJ + 16 * s + (lane & 15)] = acc[a][s][e];
-                }
-        }
-        __syncthreads();
-    }
-    double* fo = flux + (size_t)blockIdx.x * 3 * N;
-    double* fl = flux_fla + (size_t)blockIdx.x * 3 * N;
-    for (int b = tid; b < N; b += nthr) {
-        const double dE = g.Emax[b] - g.Emin[b];
-        const double f0 = F[b] / dE, f1 = F[N + b] / dE, f2 = F[2 * N + b] / dE;
-        fo[b] = f0;
-        fo[N + b] = f1;
-        fo[2 * N + b] = f2;
-        for (int f = 0; f < 3; ++f) fl[f * N + b] = P.U2[3 * f + 0] * f0 + P.U2[3 * f + 1] * f1 + P.U2[3 * f + 2] * f2;
-    }
-}
 
 // ---------------------------------------------------------------------------
-// Warp-specialised MFMA cascade, R right-hand sides per workgroup (NUSI_CASCADE_MFMA's kernel for
-// non-resonant points with the power-law source, the scans' case).
+// Warp-specialised MFMA cascade, R right-hand sides per workgroup (NUSI_CASCADE_MFMA / AUTO: every
+// point kind -- power-law or DSNB source, non-resonant or resonant-only).
 //
-// The wavefront and the rank-4 MFMA push are k_cascade_wf_mfma's; the waves are specialised:
+// The wavefront of k_cascade_wf (stage sg: step slot j solves bin N-1-sg+j, and every active step
+// reads the same table column r = T-1-sg) with its push on the fp64 matrix cores.  k_cascade_wf adds
+// one column per stage, ACC[rows, steps] += alpha[rows, r+1] T[r+1, steps], a rank-1 update; here the
+// columns are pushed in blocks of four, once every four stages, as ACC[rows, steps] += alpha[rows, 4
+// columns] . T[4 columns, steps] -- the transfer-matrix x flux-batch GEMM, whose batch is the set of
+// redshift steps in flight -- with v_mfma_f64_16x16x4f64 on 16 x 16 tiles (row tile x step tile; C/D
+// layout: step = lane & 15, row = (lane >> 4) + 4 reg).  Block q runs at stage 4q and pushes columns
+// T-4q .. T-4q+3 (the T_j of stages 4q-1 .. 4q-4) into the rows below T-1-4q, then publishes the four
+// rows the chain solves at stages 4q+1 .. 4q+4.  At stage sg the published row therefore lacks the
+// columns r+1 .. r+n_u, n_u = sg - 4 ((sg-1) >> 2) in [1, 4]: the chain lane adds them itself from its
+// last four T_j and alpha(r, r+k) (staged in LDS), in descending column order.  The matrix core sums
+// each block of four columns in its own order, so the fluxes agree with k_cascade_wf to rounding (the
+// tests' 1e-11 relative bound vs the oracle, the same exact zeros), not bit for bit.
+//
+// The waves are specialised, each kind in its own stage loop with one barrier per stage:
 //   * push waves (0 .. nw-3) hold the accumulators of 16 RT rows and run only the block pushes;
 //   * the flux-independent records (1/Z, the LU of M, the sources) come from a 3-slot ring in LDS,
 //     two phases one stage apart: the record wave (nw-2) runs phase 1 (1/Z, M, sources) of stage
-//     sg+2, the chain wave runs phase 2 (the LU) of stage sg+1 beside its solves -- no records
-//     phase, no extra barriers, and neither wave carries a whole record per stage;
+//     sg+2, the chain wave (or, R = 2, a wave of its own) phase 2 (the LU) of stage sg+1;
 //   * the chain wave (nw-1) solves, lane j = step slot j.
-// Each kind runs its own stage loop with one barrier per stage, so the registers of one kind's
-// code are not live in another's: the accumulators no longer share a budget with the records'
-// temporaries, and the kernel fits 128 VGPRs (4 waves per SIMD).
+// The registers of one kind's code are not live in another's, so the accumulators do not share a
+// budget with the records' temporaries, and the kernel fits 128 VGPRs (4 waves per SIMD).
+// Resonant-only points (non_resonant = false) read only alpha(b+i-1, b+i): their chain keeps the
+// reference's running sum (nuSIprop.hpp:273-278, 285-287) and the push waves idle.  The DSNB source
+// comes from k_source_dsnb's table, the power law is evaluated in the record wave.
 //
 // R = 1 (RT = 4): one point per workgroup, two workgroups per CU -- two independent chains share
 //   a CU instead of one.
@@ -947,8 +760,8 @@ __global__ __launch_bounds__(kWfMaxThreads) void k_cascade_wf_mfma(GridDev g, co
 //   the records are computed once (one source field per point), each alpha block is loaded once
 //   and is the A operand of both points' MFMAs, and the chain lane solves both points' bins (two
 //   independent solves that interleave).  groups[k] = (p0, p1); p1 < 0: a single point.
-// Every accumulator, published row and solve receives the same operations on the same operands
-// as in k_cascade_wf_mfma, so the fluxes equal that kernel's bit for bit (test_cascade_ws_*).
+// Every accumulator, published row and solve of a point receives the same operations on the same
+// operands whether it runs alone or paired (test_cascade_ws_*: R = 2 equals R = 1 bit for bit).
 // ---------------------------------------------------------------------------
 
 // the power-law source term c_i Lum of bin b at step i (nuSIprop.hpp:283, :656), the expression
@@ -958,23 +771,44 @@ NUSI_FN double powerlaw_src(const GridDev& g, const Point& P, const double* pw, 
     return g.step_c[i] * (P.norm_total / 3.0 * g.sfr[i] * (g.Emax[b] * pw[b + i + 1] - g.Emin[b] * pw[b + i]) * rcp_nr(1 - P.si));
 }
 
-#ifndef NUSI_WS_AB
-#define NUSI_WS_AB 0   // timing experiments only: 1 skip records, 2 skip pushes, 4 skip solves
-#endif
+// The DSNB source term c_i Lum(z_i, Emin_b, Emax_b) (nuSIprop.hpp:283, :659-662) of every (step slot J, bin b)
+// of a point, computed before the MFMA cascade (it costs two Li2 / Li3 pairs per record, far more than a
+// wavefront stage) in the diagonal layout src[(b - J + Nz - 2) (Nz - 1) + J]: the lanes of one stage (b - J
+// constant) read consecutive doubles.  The expression is cascade_record's, so the records are the same bits.
+NUSI_FN size_t src_index(int Nz, int J, int b) { return (size_t)(b - J + Nz - 2) * (Nz - 1) + J; }
+__global__ __launch_bounds__(256) void k_source_dsnb(GridDev g, const Point* __restrict__ pts, double* __restrict__ src)
+{
+    const int p = blockIdx.y, N = g.N, Nz = g.Nz, nst = Nz - 1;
+    const Point& P = pts[p];
+    const int e = blockIdx.x * 256 + threadIdx.x;
+    if (P.source != NUSI_SOURCE_DSNB || e >= nst * N) return;
+    const int J = e / N, b = e - J * N, i = Nz - 1 - J;
+    src[(size_t)p * g.T * nst + src_index(Nz, J, b)] = g.step_c[i] * lum(P, g.z[i], g.sfr[i], g.Emin[b], g.Emax[b]);
+}
+size_t cascade_src_doubles(const GridDev& g) { return (size_t)g.T * (g.Nz - 1); }
+hipError_t launch_source_dsnb(const GridDev& g, const Point* pts, int npts, double* src, hipStream_t s)
+{
+    const int ne = (g.Nz - 1) * g.N;
+    hipLaunchKernelGGL(k_source_dsnb, dim3((ne + 255) / 256, npts), dim3(256), 0, s, g, pts, src);
+    return hipGetLastError();
+}
+
+// The resonant-only chain (nuSIprop.hpp:261-278, 285-287): the running sum of the bins above, from the
+// lane's own solve of bin b+1 (x = F[:, b+1] of this step) -- k_cascade_wf's expression.  sde = dE_b.
+NUSI_FN double resonant_add(double& racc, double u0, double u1, double u2, double px0, double px1, double px2,
+                            double sj, double sd, double dEb1, double sde, double cj, bool top)
+{
+    if (!top) racc += (u0 * px0 + u1 * px1 + u2 * px2) * (sj * sd) / dEb1 / sde;
+    return cj * racc * sde;
+}
+
 // push waves not publishing spread their block MFMAs over the block's stages: k_cascade_wsp yes (C3 cascade
 // 37.3 -> 36.0 ms), k_cascade_ws no (C4 0.698 -> 0.728, C5 4.58 -> 4.93 ms; profiles/r2q)
-#ifndef NUSI_WS_STAGGER
-#define NUSI_WS_STAGGER 0
-#endif
-#ifndef NUSI_WSP_STAGGER
-#define NUSI_WSP_STAGGER 1
-#endif
-#ifndef NUSI_WS_P2WAVE
-#define NUSI_WS_P2WAVE 1   // R = 2: the LU phase of the records on a wave of its own (nw-3), not the chain (A/B: C5 cascade 5.75 -> 4.49 ms)
-#endif
+constexpr bool kWsStagger = false, kWspStagger = true;
+constexpr int kWsP2Wave = 1;   // R = 2: the LU phase of the records on a wave of its own (nw-3), not the chain (A/B: C5 cascade 5.75 -> 4.49 ms)
 template <int R> struct WsCfg;
 template <> struct WsCfg<1> { static constexpr int RT = 4, kMaxThreads = 512; };   // 6 push waves + 2
-template <> struct WsCfg<2> { static constexpr int RT = 2, kMaxThreads = 832 + 64 * NUSI_WS_P2WAVE; };   // 11 push waves + 2 (3)
+template <> struct WsCfg<2> { static constexpr int RT = 2, kMaxThreads = 832 + 64 * kWsP2Wave; };   // 11 push waves + 2 (3)
 
 template <int NJ, int R>
 __global__ __launch_bounds__(WsCfg<R>::kMaxThreads) __attribute__((amdgpu_waves_per_eu(4, 4)))
@@ -983,7 +817,7 @@ void k_cascade_ws(GridDev g, const Point* __restrict__ pts, const int2* __restri
 {
     extern __shared__ __attribute__((aligned(16))) double lds[];
     constexpr int RT = WsCfg<R>::RT, NST = NJ / 16;
-    constexpr bool kP2 = R == 2 && NUSI_WS_P2WAVE;   // phase 2 on wave nw-3
+    constexpr bool kP2 = R == 2 && kWsP2Wave;   // phase 2 on wave nw-3
     constexpr int FSRC = kWfFields, FM = kWfFields + R - 1, NF = FM + 6;   // other sources; phase-1 M entries
     const int N = g.N, Nz = g.Nz, T = g.T, nst = Nz - 1;
     const int tid = threadIdx.x, nthr = blockDim.x, lane = tid & 63, wave = tid >> 6, nw = nthr >> 6;
@@ -1052,6 +886,7 @@ void k_cascade_ws(GridDev g, const Point* __restrict__ pts, const int2* __restri
     //   phase 1 (record wave): 1/Z, the M entries, the sources of every point, sde
     //   phase 2 (chain wave, one stage later): the LU of M -- cascade_record's operations, split
     constexpr int S3 = 3 * NJ;
+    const bool nonres = P.non_resonant;   // the points of a workgroup share a table, hence the flags
     auto phase1 = [&](int s2, int jj) {
         const int b = N - 1 - s2 + jj, i = Nz - 1 - jj;
         if (jj < nst && b >= 0 && b < N) {
@@ -1066,10 +901,14 @@ void k_cascade_ws(GridDev g, const Point* __restrict__ pts, const int2* __restri
             Rw[(FM + 3) * S3] = m.m12;
             Rw[(FM + 4) * S3] = m.m20;
             Rw[(FM + 5) * S3] = m.m21;
-            Rw[PR_SDE * S3] = gl.step_s[i] * rdE[b];
+            Rw[PR_SDE * S3] = nonres ? gl.step_s[i] * rdE[b] : (gl.Emax[b] - gl.Emin[b]);
 #pragma unroll
-            for (int p = 0; p < R; ++p)
-                Rw[(p == 0 ? PR_SRC : FSRC + p - 1) * S3] = powerlaw_src(gl, pts[pid[p]], pw + p * (T + 2), i, b);
+            for (int p = 0; p < R; ++p) {
+                const Point& Q = pts[pid[p]];
+                Rw[(p == 0 ? PR_SRC : FSRC + p - 1) * S3] =
+                    Q.source == NUSI_SOURCE_POWER_LAW ? powerlaw_src(gl, Q, pw + p * (T + 2), i, b)
+                                                      : t.Src[(size_t)pid[p] * T * nst + src_index(Nz, jj, b)];
+            }
         }
     };
     auto phase2 = [&](int s2, int jj) {
@@ -1099,7 +938,10 @@ void k_cascade_ws(GridDev g, const Point* __restrict__ pts, const int2* __restri
         const int j = lane;
         const bool act = j < nst;
         const double u0 = P.u[0], u1 = P.u[1], u2 = P.u[2];
-        const double cj = act ? gl.step_c[Nz - 1 - j] : 0.0;
+        const double cj = act ? gl.step_c[Nz - 1 - j] : 0.0, sj = act ? gl.step_s[Nz - 1 - j] : 0.0;
+        double racc[R], px0[R], px1[R], px2[R];   // resonant-only chain state of each point
+#pragma unroll
+        for (int p = 0; p < R; ++p) racc[p] = px0[p] = px1[p] = px2[p] = 0.0;
         for (int sg0 = 0; sg0 < T; sg0 += 4)
 #pragma unroll
         for (int d = 0; d < 4; ++d) {
@@ -1110,40 +952,52 @@ void k_cascade_ws(GridDev g, const Point* __restrict__ pts, const int2* __restri
             double Tn[R];
 #pragma unroll
             for (int p = 0; p < R; ++p) Tn[p] = 0.0;
-            if (!kP2 && sg + 1 < T && !(NUSI_WS_AB & 1)) phase2(sg + 1, j);   // independent of this stage's solve
-            if (act && b >= 0 && b < N && !(NUSI_WS_AB & 4)) {
+            if (!kP2 && sg + 1 < T) phase2(sg + 1, j);   // independent of this stage's solve
+            if (act && b >= 0 && b < N) {
                 const double* Rc = rec + (sg % 3) * NJ + j;
                 constexpr int S = S3;
-                const int qq = (sg - 1) >> 2;              // block whose publication serves stage sg
-                const int nu = (d == 0) ? 4 : d;           // columns r+1 .. r+nu not yet pushed
-                const int ax = ((qq & 1) * 4 + (sg - 1 - 4 * qq)) * NJ + j;
-                double s[R];
-#pragma unroll
-                for (int p = 0; p < R; ++p) s[p] = AX[p * 8 * NJ + ax];
-#pragma unroll
-                for (int k = 4; k >= 1; --k)
-                    if (k <= nu) {
-                        const double a = sdg[(k - 1) * T + r];
-#pragma unroll
-                        for (int p = 0; p < R; ++p) s[p] = fma(a, Tp[(p * 8 + ((sg - k) & 7)) * NJ + j], s[p]);
-                    }
                 const double rz0 = Rc[PR_RZ0 * S], rz1 = Rc[PR_RZ1 * S], rz2 = Rc[PR_RZ2 * S];
                 const int pmb = (int)Rc[kPreFields * S];
                 const double l10 = Rc[PR_L10 * S], l20 = Rc[PR_L20 * S], l21 = Rc[PR_L21 * S];
                 const double u01 = Rc[PR_U01 * S], u02 = Rc[PR_U02 * S], u12 = Rc[PR_U12 * S];
                 const double ru00 = Rc[PR_RU00 * S], ru11 = Rc[PR_RU11 * S], ru22 = Rc[PR_RU22 * S];
                 const double sde = Rc[PR_SDE * S];
+                double add[R];   // c_i x (coupling of the bin to the bins above)
+                if (nonres) {
+                    const int qq = (sg - 1) >> 2;              // block whose publication serves stage sg
+                    const int nu = (d == 0) ? 4 : d;           // columns r+1 .. r+nu not yet pushed
+                    const int ax = ((qq & 1) * 4 + (sg - 1 - 4 * qq)) * NJ + j;
+                    double s[R];
+#pragma unroll
+                    for (int p = 0; p < R; ++p) s[p] = AX[p * 8 * NJ + ax];
+#pragma unroll
+                    for (int k = 4; k >= 1; --k)
+                        if (k <= nu) {
+                            const double a = sdg[(k - 1) * T + r];
+#pragma unroll
+                            for (int p = 0; p < R; ++p) s[p] = fma(a, Tp[(p * 8 + ((sg - k) & 7)) * NJ + j], s[p]);
+                        }
+#pragma unroll
+                    for (int p = 0; p < R; ++p) add[p] = cj * s[p];
+                } else {
+                    const double dEb1 = (b + 1 < N) ? sEmax[b + 1] - sEmin[b + 1] : 1.0;
+#pragma unroll
+                    for (int p = 0; p < R; ++p)
+                        add[p] = resonant_add(racc[p], u0, u1, u2, px0[p], px1[p], px2[p], sj, sdg[r], dEb1, sde, cj,
+                                              b == N - 1);
+                }
 #pragma unroll
                 for (int p = 0; p < R; ++p) {
                     double* Fp = F + 3 * N * p;
                     const double src = Rc[(p == 0 ? PR_SRC : FSRC + p - 1) * S];
                     double x0, x1, x2;
-                    cascade_solve(Fp[b], Fp[N + b], Fp[2 * N + b], cj * s[p], src, u0, u1, u2, rz0, rz1, rz2, pmb, l10,
+                    cascade_solve(Fp[b], Fp[N + b], Fp[2 * N + b], add[p], src, u0, u1, u2, rz0, rz1, rz2, pmb, l10,
                                   l20, l21, u01, u02, u12, ru00, ru11, ru22, x0, x1, x2);
                     Fp[b] = x0;
                     Fp[N + b] = x1;
                     Fp[2 * N + b] = x2;
-                    if (b > 0) Tn[p] = (u0 * x0 + u1 * x1 + u2 * x2) * sde;
+                    px0[p] = x0; px1[p] = x1; px2[p] = x2;
+                    if (nonres && b > 0) Tn[p] = (u0 * x0 + u1 * x1 + u2 * x2) * sde;
                 }
             }
             if (act)
@@ -1153,13 +1007,13 @@ void k_cascade_ws(GridDev g, const Point* __restrict__ pts, const int2* __restri
         }
     } else if (kP2 && wave == nw - 3) {
         for (int sg = 0; sg < T; ++sg) {
-            if (sg + 1 < T && !(NUSI_WS_AB & 1)) phase2(sg + 1, lane);
+            if (sg + 1 < T) phase2(sg + 1, lane);
             __syncthreads();
         }
     } else if (wave == nw - 2) {
         // ---- phase 1 of the records two stages ahead, while the chain solves this stage
         for (int sg = 0; sg < T; ++sg) {
-            if (sg + 2 < T && !(NUSI_WS_AB & 1)) phase1(sg + 2, lane);
+            if (sg + 2 < T) phase1(sg + 2, lane);
             __syncthreads();
         }
     } else {
@@ -1190,11 +1044,11 @@ void k_cascade_ws(GridDev g, const Point* __restrict__ pts, const int2* __restri
         for (int sg = 0; sg < T; ++sg) {
             // block q is pushed at stage 4q by the waves holding the rows it publishes, and one to three
             // stages later by the others (their rows are needed >= 5 stages on; the T_j ring keeps 8):
-            // the matrix-core work of a block is spread over its four stages (NUSI_WS_STAGGER)
+            // the matrix-core work of a block is spread over its four stages (kWsStagger)
             const int q = sg >> 2, r = T - 1 - 4 * q, hi = r - 1;
             const bool crit = rw0 <= hi && rw0 + 16 * RT - 1 >= hi - 3;
-            const int dw = (!NUSI_WS_STAGGER || crit) ? 0 : 1 + wave % 3;
-            if ((sg & 3) == dw && !(NUSI_WS_AB & 2)) {
+            const int dw = (!kWsStagger || crit) ? 0 : 1 + wave % 3;
+            if ((sg & 3) == dw && nonres) {
                 if (q >= 1) {
 #pragma unroll
                     for (int s = 0; s < NST; ++s) {
@@ -1212,7 +1066,7 @@ void k_cascade_ws(GridDev g, const Point* __restrict__ pts, const int2* __restri
                     load_blk(q + 1, ablk);
                 }
             }
-            if ((sg & 3) == 0 && !(NUSI_WS_AB & 2)) {
+            if ((sg & 3) == 0 && nonres) {
 #pragma unroll
                 for (int a = 0; a < RT; ++a)
                     if (rw0 + 16 * a <= hi && rw0 + 16 * a + 15 >= hi - 3)   // uniform: tiles holding those rows
@@ -1277,7 +1131,7 @@ void k_cascade_wsp(GridDev g, const Point* __restrict__ pts, TablesDev t, double
 {
     extern __shared__ __attribute__((aligned(16))) double lds[];
     constexpr int R = 1, RT = kWsBigRT, NST = NJ / 16;
-    constexpr bool kP2 = NUSI_WS_P2WAVE;   // phase 2 on wave nw-3
+    constexpr bool kP2 = kWsP2Wave;   // phase 2 on wave nw-3
     constexpr int FSRC = kWfFields, FM = kWfFields + R - 1, NF = FM + 6;   // other sources; phase-1 M entries
     const int N = g.N, Nz = g.Nz, T = g.T, nst = Nz - 1;
     const int tid = threadIdx.x, nthr = blockDim.x, lane = tid & 63, wave = tid >> 6, nw = nthr >> 6;
@@ -1339,6 +1193,7 @@ void k_cascade_wsp(GridDev g, const Point* __restrict__ pts, TablesDev t, double
     //   phase 2 (chain wave, one stage later): the LU of M -- cascade_record's operations, split
     constexpr int S3 = 3 * NJ;
     int jb = 0;   // first step slot of the current pass (step i = Nz-1-jb-j for slot j)
+    const bool nonres = P.non_resonant;
     auto phase1 = [&](int s2, int jj) {
         const int b = N - 1 - s2 + jj, i = Nz - 1 - jb - jj;
         if (jj < NJ && jb + jj < nst && b >= 0 && b < N) {
@@ -1353,10 +1208,14 @@ void k_cascade_wsp(GridDev g, const Point* __restrict__ pts, TablesDev t, double
             Rw[(FM + 3) * S3] = m.m12;
             Rw[(FM + 4) * S3] = m.m20;
             Rw[(FM + 5) * S3] = m.m21;
-            Rw[PR_SDE * S3] = gl.step_s[i] * rdE[b];
+            Rw[PR_SDE * S3] = nonres ? gl.step_s[i] * rdE[b] : (gl.Emax[b] - gl.Emin[b]);
 #pragma unroll
-            for (int p = 0; p < R; ++p)
-                Rw[(p == 0 ? PR_SRC : FSRC + p - 1) * S3] = powerlaw_src(gl, pts[pid[p]], pw + p * (T + 2), i, b);
+            for (int p = 0; p < R; ++p) {
+                const Point& Q = pts[pid[p]];
+                Rw[(p == 0 ? PR_SRC : FSRC + p - 1) * S3] =
+                    Q.source == NUSI_SOURCE_POWER_LAW ? powerlaw_src(gl, Q, pw + p * (T + 2), i, b)
+                                                      : t.Src[(size_t)pid[p] * T * nst + src_index(Nz, jb + jj, b)];
+            }
         }
     };
     auto phase2 = [&](int s2, int jj) {
@@ -1397,7 +1256,10 @@ void k_cascade_wsp(GridDev g, const Point* __restrict__ pts, TablesDev t, double
         const int j = lane;
         const bool act = j < NJ && jb + j < nst;
         const double u0 = P.u[0], u1 = P.u[1], u2 = P.u[2];
-        const double cj = act ? gl.step_c[Nz - 1 - jb - j] : 0.0;
+        const double cj = act ? gl.step_c[Nz - 1 - jb - j] : 0.0, sj = act ? gl.step_s[Nz - 1 - jb - j] : 0.0;
+        double racc[R], px0[R], px1[R], px2[R];   // resonant-only chain state (per step: restarts every pass)
+#pragma unroll
+        for (int p = 0; p < R; ++p) racc[p] = px0[p] = px1[p] = px2[p] = 0.0;
         for (int sg0 = 0; sg0 < Ts; sg0 += 4)
 #pragma unroll
         for (int d = 0; d < 4; ++d) {
@@ -1408,40 +1270,52 @@ void k_cascade_wsp(GridDev g, const Point* __restrict__ pts, TablesDev t, double
             double Tn[R];
 #pragma unroll
             for (int p = 0; p < R; ++p) Tn[p] = 0.0;
-            if (!kP2 && sg + 1 < Ts && !(NUSI_WS_AB & 1)) phase2(sg + 1, j);   // independent of this stage's solve
-            if (act && b >= 0 && b < N && !(NUSI_WS_AB & 4)) {
+            if (!kP2 && sg + 1 < Ts) phase2(sg + 1, j);   // independent of this stage's solve
+            if (act && b >= 0 && b < N) {
                 const double* Rc = rec + (sg % 3) * NJ + j;
                 constexpr int S = S3;
-                const int qq = (sg - 1) >> 2;              // block whose publication serves stage sg
-                const int nu = (d == 0) ? 4 : d;           // columns r+1 .. r+nu not yet pushed
-                const int ax = ((qq & 1) * 4 + (sg - 1 - 4 * qq)) * NJ + j;
-                double s[R];
-#pragma unroll
-                for (int p = 0; p < R; ++p) s[p] = AX[p * 8 * NJ + ax];
-#pragma unroll
-                for (int k = 4; k >= 1; --k)
-                    if (k <= nu) {
-                        const double a = sdg[(k - 1) * T + r];
-#pragma unroll
-                        for (int p = 0; p < R; ++p) s[p] = fma(a, Tp[(p * 8 + ((sg - k) & 7)) * NJ + j], s[p]);
-                    }
                 const double rz0 = Rc[PR_RZ0 * S], rz1 = Rc[PR_RZ1 * S], rz2 = Rc[PR_RZ2 * S];
                 const int pmb = (int)Rc[kPreFields * S];
                 const double l10 = Rc[PR_L10 * S], l20 = Rc[PR_L20 * S], l21 = Rc[PR_L21 * S];
                 const double u01 = Rc[PR_U01 * S], u02 = Rc[PR_U02 * S], u12 = Rc[PR_U12 * S];
                 const double ru00 = Rc[PR_RU00 * S], ru11 = Rc[PR_RU11 * S], ru22 = Rc[PR_RU22 * S];
                 const double sde = Rc[PR_SDE * S];
+                double add[R];
+                if (nonres) {
+                    const int qq = (sg - 1) >> 2;              // block whose publication serves stage sg
+                    const int nu = (d == 0) ? 4 : d;           // columns r+1 .. r+nu not yet pushed
+                    const int ax = ((qq & 1) * 4 + (sg - 1 - 4 * qq)) * NJ + j;
+                    double s[R];
+#pragma unroll
+                    for (int p = 0; p < R; ++p) s[p] = AX[p * 8 * NJ + ax];
+#pragma unroll
+                    for (int k = 4; k >= 1; --k)
+                        if (k <= nu) {
+                            const double a = sdg[(k - 1) * T + r];
+#pragma unroll
+                            for (int p = 0; p < R; ++p) s[p] = fma(a, Tp[(p * 8 + ((sg - k) & 7)) * NJ + j], s[p]);
+                        }
+#pragma unroll
+                    for (int p = 0; p < R; ++p) add[p] = cj * s[p];
+                } else {
+                    const double dEb1 = (b + 1 < N) ? sEmax[b + 1] - sEmin[b + 1] : 1.0;
+#pragma unroll
+                    for (int p = 0; p < R; ++p)
+                        add[p] = resonant_add(racc[p], u0, u1, u2, px0[p], px1[p], px2[p], sj, sdg[r], dEb1, sde, cj,
+                                              b == N - 1);
+                }
 #pragma unroll
                 for (int p = 0; p < R; ++p) {
                     double* Fp = F + 3 * N * p;
                     const double src = Rc[(p == 0 ? PR_SRC : FSRC + p - 1) * S];
                     double x0, x1, x2;
-                    cascade_solve(Fp[b], Fp[N + b], Fp[2 * N + b], cj * s[p], src, u0, u1, u2, rz0, rz1, rz2, pmb, l10,
+                    cascade_solve(Fp[b], Fp[N + b], Fp[2 * N + b], add[p], src, u0, u1, u2, rz0, rz1, rz2, pmb, l10,
                                   l20, l21, u01, u02, u12, ru00, ru11, ru22, x0, x1, x2);
                     Fp[b] = x0;
                     Fp[N + b] = x1;
                     Fp[2 * N + b] = x2;
-                    if (b > 0) Tn[p] = (u0 * x0 + u1 * x1 + u2 * x2) * sde;
+                    px0[p] = x0; px1[p] = x1; px2[p] = x2;
+                    if (nonres && b > 0) Tn[p] = (u0 * x0 + u1 * x1 + u2 * x2) * sde;
                 }
             }
             if (act)
@@ -1451,13 +1325,13 @@ void k_cascade_wsp(GridDev g, const Point* __restrict__ pts, TablesDev t, double
         }
     } else if (kP2 && wave == nw - 3) {
         for (int sg = 0; sg < Ts; ++sg) {
-            if (sg + 1 < Ts && !(NUSI_WS_AB & 1)) phase2(sg + 1, lane);
+            if (sg + 1 < Ts) phase2(sg + 1, lane);
             __syncthreads();
         }
     } else if (wave == nw - 2) {
         // ---- phase 1 of the records two stages ahead, while the chain solves this stage
         for (int sg = 0; sg < Ts; ++sg) {
-            if (sg + 2 < Ts && !(NUSI_WS_AB & 1)) phase1(sg + 2, lane);
+            if (sg + 2 < Ts) phase1(sg + 2, lane);
             __syncthreads();
         }
     } else {
@@ -1488,11 +1362,11 @@ void k_cascade_wsp(GridDev g, const Point* __restrict__ pts, TablesDev t, double
         for (int sg = 0; sg < Ts; ++sg) {
             // block q is pushed at stage 4q by the waves holding the rows it publishes, and one to three
             // stages later by the others (their rows are needed >= 5 stages on; the T_j ring keeps 8):
-            // the matrix-core work of a block is spread over its four stages (NUSI_WSP_STAGGER)
+            // the matrix-core work of a block is spread over its four stages (kWspStagger)
             const int q = sg >> 2, r = c0 - 4 * q, hi = r - 1;
             const bool crit = rw0 <= hi && rw0 + 16 * RT - 1 >= hi - 3;
-            const int dw = (!NUSI_WSP_STAGGER || crit) ? 0 : 1 + wave % 3;
-            if ((sg & 3) == dw && !(NUSI_WS_AB & 2)) {
+            const int dw = (!kWspStagger || crit) ? 0 : 1 + wave % 3;
+            if ((sg & 3) == dw && nonres) {
                 if (q >= 1) {
 #pragma unroll
                     for (int s = 0; s < NST; ++s) {
@@ -1510,7 +1384,7 @@ void k_cascade_wsp(GridDev g, const Point* __restrict__ pts, TablesDev t, double
                     load_blk(q + 1, ablk);
                 }
             }
-            if ((sg & 3) == 0 && !(NUSI_WS_AB & 2)) {
+            if ((sg & 3) == 0 && nonres) {
 #pragma unroll
                 for (int a = 0; a < RT; ++a)
                     if (rw0 + 16 * a <= hi && rw0 + 16 * a + 15 >= hi - 3)   // uniform: tiles holding those rows
@@ -1579,32 +1453,6 @@ static bool wf_fits(const GridDev& g)
     return w.lds <= kWfMaxLds;
 }
 
-// the MFMA variant: one push wave per 64 rows + the chain wave; T_j ring of 8 stages, 2 x 4 published
-// rows, alpha(n, n+k) for k = 1..4
-static WfGeom mf_geom(const GridDev& g, int NJ)
-{
-    WfGeom w;
-    w.nthr = ((g.T - 1 + 63) / 64) * 64 + 64;
-#ifndef NUSI_MF_KMAX   // cap on the record batch (stages per records phase), A/B
-#define NUSI_MF_KMAX 64
-#endif
-    w.K = std::min(w.nthr / NJ, NUSI_MF_KMAX);
-    auto bytes = [&](int K) {
-        return sizeof(double) * (3 * (size_t)g.N + (size_t)kWfFields * K * NJ + 16 * NJ + cascade_aux_doubles(g.N, g.T) +
-                                 6 * (size_t)g.T + 2 * (size_t)g.N + 4 * (size_t)g.Nz);
-    };
-    while (w.K > 1 && bytes(w.K) > kWfMaxLds) --w.K;
-    w.lds = bytes(w.K);
-    return w;
-}
-static bool mf_fits(const GridDev& g)
-{
-    const int nj = wf_nj(g);
-    if (!nj || g.T < 2) return false;
-    const WfGeom w = mf_geom(g, nj);
-    return w.nthr <= kWfMaxThreads && w.K >= 1 && w.lds <= kWfMaxLds;
-}
-
 // the warp-specialised kernel: push waves of 16 RT rows each, then the record and chain waves
 // (R = 3 here: the step-pass kernel, one right-hand side, 128 rows per push wave)
 constexpr size_t kWsMaxLds[4] = {0, 80 * 1024, 150 * 1024, 160 * 1024};   // R = 1: two workgroups per CU
@@ -1614,7 +1462,7 @@ static WfGeom ws_geom(const GridDev& g, int NJ, int R)
     const bool big = R == 3;
     if (big) R = 1;
     const int rows = big ? 16 * kWsBigRT : R == 1 ? 64 : 32;
-    w.nthr = ((g.T - 1 + rows - 1) / rows) * 64 + 128 + ((R == 2 || big) ? 64 * NUSI_WS_P2WAVE : 0);
+    w.nthr = ((g.T - 1 + rows - 1) / rows) * 64 + 128 + ((R == 2 || big) ? 64 * kWsP2Wave : 0);
     w.K = 2;
     w.lds = sizeof(double) * (3 * (size_t)R * g.N + 3 * (size_t)(kWfFields + R - 1 + 6) * NJ + 16 * (size_t)R * NJ + g.N +
                               (size_t)R * (g.T + 2) + 6 * (size_t)g.T + 2 * (size_t)g.N + 4 * (size_t)g.Nz);
@@ -1668,20 +1516,10 @@ hipError_t launch_cascade_wsp(const GridDev& g, const Point* pts, int npts, Tabl
                               hipStream_t s)
 {
     if (!cascade_wsp_fits(g)) return hipErrorInvalidValue;
+    t_cascade_kernel = "k_cascade_ws_passes";
     const WfGeom w = ws_geom(g, kWsBigNJ, 3);
     hipLaunchKernelGGL((k_cascade_wsp<kWsBigNJ>), dim3(npts), dim3(w.nthr), w.lds, s, g, pts, t, flux, flux_fla);
     return hipGetLastError();
-}
-
-template <int NJ>
-static void launch_mf(const GridDev& g, const Point* pts, int npts, TablesDev t, double* flux, double* flux_fla,
-                      hipStream_t s, bool power_law)
-{
-    const WfGeom w = mf_geom(g, NJ);
-    if (power_law)
-        hipLaunchKernelGGL((k_cascade_wf_mfma<NJ, true>), dim3(npts), dim3(w.nthr), w.lds, s, g, pts, t, flux, flux_fla, w.K);
-    else
-        hipLaunchKernelGGL((k_cascade_wf_mfma<NJ, false>), dim3(npts), dim3(w.nthr), w.lds, s, g, pts, t, flux, flux_fla, w.K);
 }
 
 template <int NJ>
@@ -1715,39 +1553,13 @@ static bool dispatch_reg(int nq, const GridDev& g, const Point* pts, int npts, T
 }
 using RegNQ = std::integer_sequence<int, 1, 2, 3, 4, 5, 6, 8, 10, 12, 16, 20>;
 
-hipError_t launch_cascade(const GridDev& g, const Point* pts, int npts, TablesDev t, double* flux, double* flux_fla,
-                          hipStream_t s, int kind, bool all_power_law, bool all_nonres)
+// the bit-exact scalar kernels (NUSI_CASCADE_WAVEFRONT / REG / LDS): k_cascade_wf where the grid fits it,
+// else k_cascade_reg (N <= 1280), else k_cascade; a kind that does not fit falls back the same way
+hipError_t launch_cascade_exact(const GridDev& g, const Point* pts, int npts, TablesDev t, double* flux,
+                                double* flux_fla, hipStream_t s, int kind, bool all_power_law)
 {
     const int nq = (g.N + 63) / 64;
-    if (kind == NUSI_CASCADE_AUTO) {
-        static const char* env = getenv("NUSI_CASCADE");   // A/B switch: wf | mfma | reg | lds
-        kind = !env ? NUSI_CASCADE_AUTO
-                    : (env[0] == 'w' ? NUSI_CASCADE_WAVEFRONT : env[0] == 'm' ? NUSI_CASCADE_MFMA
-                       : env[0] == 'r' ? NUSI_CASCADE_REG : NUSI_CASCADE_LDS);
-    }
-    if (kind == NUSI_CASCADE_MFMA && all_power_law && all_nonres && cascade_ws_fits(g, 1)) {
-        const char* ws = getenv("NUSI_CASCADE_WS");   // A/B: 0 = k_cascade_wf_mfma
-        if (!ws || ws[0] != '0') return launch_cascade_ws(g, pts, 1, nullptr, npts, t, flux, flux_fla, s);   // names itself
-    }
-    if (kind == NUSI_CASCADE_MFMA && all_power_law && all_nonres && cascade_wsp_fits(g)) {
-        // NUSI_CASCADE_WSP (A/B, tests): 0 = never the step-pass kernel, 1 = also where one pass fits
-        const char* wsp = getenv("NUSI_CASCADE_WSP");
-        if ((!wf_nj(g) && !(wsp && wsp[0] == '0')) || (wsp && wsp[0] == '1'))
-        {
-            t_cascade_kernel = "k_cascade_ws_passes";
-            return launch_cascade_wsp(g, pts, npts, t, flux, flux_fla, s);
-        }
-    }
-    if (kind == NUSI_CASCADE_MFMA && mf_fits(g)) {
-        t_cascade_kernel = "k_cascade_wf_mfma";
-        switch (wf_nj(g)) {
-        case 16: launch_mf<16>(g, pts, npts, t, flux, flux_fla, s, all_power_law); break;
-        case 32: launch_mf<32>(g, pts, npts, t, flux, flux_fla, s, all_power_law); break;
-        default: launch_mf<48>(g, pts, npts, t, flux, flux_fla, s, all_power_law); break;
-        }
-        return hipGetLastError();
-    }
-    if ((kind == NUSI_CASCADE_AUTO || kind == NUSI_CASCADE_WAVEFRONT || kind == NUSI_CASCADE_MFMA) && wf_fits(g)) {
+    if (kind == NUSI_CASCADE_WAVEFRONT && wf_fits(g)) {
         t_cascade_kernel = "k_cascade_wf";
         switch (wf_nj(g)) {
         case 16: launch_wf<16>(g, pts, npts, t, flux, flux_fla, s, all_power_law); break;

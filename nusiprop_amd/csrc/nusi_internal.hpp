@@ -31,6 +31,7 @@ struct TablesDev {
     double* At;   // [npts][T]
     double* A;    // [npts][PT]
     double* Med;  // [npts][3][kMedFields T]: member edge leaves of every bin edge (k_alpha_medge)
+    double* Src;  // [npts][T (Nz-1)]: DSNB source terms c_i Lum (k_source_dsnb, diagonal layout), or nullptr
 };
 
 // Tiles of the alpha table for k_alpha_tile: kAlphaTile x kAlphaTile (n, m) bin blocks with
@@ -50,26 +51,29 @@ void alpha_tiles_destroy(AlphaTilesDev* t);
 hipError_t launch_gamma_alphat(const GridDev& g, const Point* pts, int npts, const SplineSet& spl, TablesDev t,
                                int* warn, hipStream_t s);
 // batches: device [nbatches] of first table | count << 24 (count <= gmax), tables of a batch sharing
-// m_phi, the masses and the channel flags (nullptr: every table alone).  Core tiles run on the big-batch
-// kernel k_alpha_batch (any count < 256; the first nb_plain batches without the phi-phi channel, the rest
-// with it), or with tile_kernel on k_alpha_tile<G> (count <= 4; A/B)
+// m_phi, the masses and the channel flags (nullptr: every table alone).  kernel = NUSI_OPT_ALPHA_KERNEL:
+// 0 -- core tiles on the big-batch kernel k_alpha_batch (any count < 256; the first nb_plain batches without
+// the phi-phi channel, the rest with it); 1 -- k_alpha_tile<G> batches (count <= 4); 2 -- one entry per
+// work-item (k_alpha)
 hipError_t launch_alpha(const GridDev& g, const Point* pts, int npts, const SplineSet& spl, const AlphaTilesDev& tiles,
                         TablesDev t, int* warn, hipStream_t s, const int* batches, int nbatches, int gmax,
-                        bool tile_kernel, int nb_plain);
-// kind: NUSI_CASCADE_* (include/nusi.h); NUSI_CASCADE_AUTO also honours $NUSI_CASCADE = wf|reg|lds
-// all_power_law: every point uses the power-law source (selects the call-free wavefront kernel);
-// all_nonres: every point is non-resonant (with all_power_law and NUSI_CASCADE_MFMA: k_cascade_ws<R = 1>)
-hipError_t launch_cascade(const GridDev& g, const Point* pts, int npts, TablesDev t, double* flux, double* flux_fla,
-                          hipStream_t s, int kind, bool all_power_law, bool all_nonres);
-// the warp-specialised MFMA cascade (k_cascade_ws): R = 1, one point per workgroup (groups unused, nwg = points),
-// or R = 2, groups[k] = two points sharing one table slot (y < 0: one point); non-resonant points with the
-// power-law source only.  Fluxes equal k_cascade_wf_mfma's bit for bit.
+                        int kernel, int nb_plain);
+// The MFMA cascade (NUSI_CASCADE_AUTO / MFMA): k_cascade_ws -- R = 1, one point per workgroup (groups
+// unused, nwg = points), or R = 2, groups[k] = two points sharing one table slot (y < 0: one point) -- for
+// Nz - 1 <= 48, k_cascade_wsp (step passes) for any number of steps.  Every point kind: the DSNB points'
+// source terms come from t.Src (launch_source_dsnb first), the power law is evaluated in the kernel.
 bool cascade_ws_fits(const GridDev& g, int R);
 bool cascade_wsp_fits(const GridDev& g);   // the step-pass kernel (any number of redshift steps)
-hipError_t launch_cascade_wsp(const GridDev& g, const Point* pts, int npts, TablesDev t, double* flux, double* flux_fla,
-                              hipStream_t s);
 hipError_t launch_cascade_ws(const GridDev& g, const Point* pts, int R, const int2* groups, int nwg, TablesDev t,
                              double* flux, double* flux_fla, hipStream_t s);
+hipError_t launch_cascade_wsp(const GridDev& g, const Point* pts, int npts, TablesDev t, double* flux, double* flux_fla,
+                              hipStream_t s);
+size_t cascade_src_doubles(const GridDev& g);   // t.Src doubles per point
+hipError_t launch_source_dsnb(const GridDev& g, const Point* pts, int npts, double* src, hipStream_t s);
+// The bit-exact scalar cascades (NUSI_CASCADE_WAVEFRONT / REG / LDS; a kind that does not fit the grid falls
+// back wavefront -> register-resident -> LDS).  all_power_law selects the call-free wavefront variant.
+hipError_t launch_cascade_exact(const GridDev& g, const Point* pts, int npts, TablesDev t, double* flux,
+                                double* flux_fla, hipStream_t s, int kind, bool all_power_law);
 
 // 4 x 4 windows of a 3-D spline table f [n0][n1][n2] into fw [n0 n1 n2][16] (synchronous)
 hipError_t spline_windows_build(const float* f, int n0, int n1, int n2, float* fw);

@@ -517,15 +517,15 @@ hipError_t alpha_tiles_create(int T, const unsigned char* shared, AlphaTilesDev*
         if (ne[t] > cap_core) { t0 = t; break; }
     bool tail_ext = true;   // no bin from tile t0 on shares an edge with its neighbour
     for (int n = t0 * kAlphaTile; n + 1 < T; ++n) tail_ext = tail_ext && !shared[n];
-    // NUSI_ALPHA_EXT_TILES=0 (A/B): the extended triangle runs on the per-entry kernel instead of
-    // quarter tiles (8 x 8 bins, batched with the core tiles)
-    static const bool ext_tiles = !(getenv("NUSI_ALPHA_EXT_TILES") && atoi(getenv("NUSI_ALPHA_EXT_TILES")) == 0);
+    // the extended triangle runs as quarter tiles (8 x 8 bins, batched with the core tiles; round 1: alpha
+    // stage 14.68 -> 14.55 ms per 1024 points against the per-entry kernel)
+    constexpr bool ext_tiles = true;
     out->ext_lo = (tail_ext && t0 < nt && !ext_tiles) ? t0 * kAlphaTile : T;
     const int qlo = (tail_ext && t0 < nt && ext_tiles) ? t0 : nt;   // tiles from qlo on: split on both sides
     // Class-1 tiles (t side core, S' side extended: 30 S' edges) are split into their first 8 and last
     // 7 m bins (16 / 14 S' edges): the halves fit the core tiles' LDS footprint and join class 0,
-    // whose launch builds batches of tables (NUSI_ALPHA_SPLIT_EXT=0 keeps them whole, A/B).
-    static const bool split_ext = !(getenv("NUSI_ALPHA_SPLIT_EXT") && atoi(getenv("NUSI_ALPHA_SPLIT_EXT")) == 0);
+    // whose launch builds batches of tables (16.0 -> 14.8 ms when introduced).
+    constexpr bool split_ext = true;
     std::vector<int> cls[3];
     for (int tm = 0; tm < nt; ++tm)
         for (int tn = 0; tn <= tm; ++tn) {
@@ -571,10 +571,10 @@ const char* last_alpha_kernel() { return t_alpha_kernel; }
 
 hipError_t launch_alpha(const GridDev& g, const Point* pts, int npts, const SplineSet& spl, const AlphaTilesDev& at,
                         TablesDev t, int* warn, hipStream_t s, const int* batches, int nbatches, int gmax,
-                        bool tile_kernel, int nb_plain)
+                        int kernel, int nb_plain)
 {
     t_alpha_kernel = "k_alpha_tile";
-    if (!tile_kernel && batches && getenv("NUSI_ALPHA_PER_ENTRY") == nullptr) {
+    if (kernel == 0 && batches) {
         t_alpha_kernel = "k_alpha_batch";
         // class 0 on the big-batch kernel (batches of up to gmax tables), classes 1 / 2 per table
         if (at.ext_lo < g.T) {
@@ -609,7 +609,7 @@ hipError_t launch_alpha(const GridDev& g, const Point* pts, int npts, const Spli
         }
         return hipGetLastError();
     }
-    static const bool per_entry = getenv("NUSI_ALPHA_PER_ENTRY") != nullptr;   // A/B switch
+    const bool per_entry = kernel == 2;
     auto per_entry_region = [&](int nlo) {
         const long long L = g.T - nlo, ne = L * (L - 1) / 2;
         if (ne <= 0) return;

@@ -82,9 +82,16 @@ class Plan:
                                                 ctypes.c_void_p(stream_ptr) if stream_ptr else None))
 
     def set_cascade(self, kind):
-        """Cascade kernel of later calls: _lib.CASCADE_{AUTO,WAVEFRONT,REG,LDS} (same fluxes bit for bit) or
-        CASCADE_MFMA (the wavefront with its push on the fp64 matrix cores; fluxes to rounding)."""
+        """Cascade kernel of later calls: _lib.CASCADE_AUTO (default) = CASCADE_MFMA (the warp-specialised
+        wavefront with its push on the fp64 matrix cores), or the bit-exact scalar kernels
+        CASCADE_{WAVEFRONT,REG,LDS} (WAVEFRONT and REG agree bit for bit)."""
         _lib.check(_lib.load().nusi_plan_set_cascade(self._h, int(kind)))
+
+    def set_option(self, option, value):
+        """A/B and test options (nusi_plan_set_option): _lib.OPT_ALPHA_BATCH (max tables per alpha batch, 0 =
+        auto), OPT_ALPHA_KERNEL (0 batch, 1 tile, 2 per entry), OPT_CASCADE_RHS (1 = one point per cascade
+        workgroup), OPT_STEP_PASSES (1 = the step-pass cascade also where one pass fits)."""
+        _lib.check(_lib.load().nusi_plan_set_option(self._h, int(option), int(value)))
 
     def profile_begin(self, max_calls):
         _lib.check(_lib.load().nusi_plan_profile_begin(self._h, int(max_calls)))

@@ -105,6 +105,13 @@ class pyprop:  # noqa: N801  (name of the reference class)
         _lib.load().nusi_get_energies(self._h, E.ctypes.data_as(ctypes.POINTER(ctypes.c_double)))
         return E
 
+    def kernels(self):
+        """Extension (no reference counterpart): names of the alpha-table and cascade kernels the last
+        evolve() launched, e.g. ('k_alpha_batch', 'k_cascade_ws')."""
+        a, c = ctypes.c_char_p(), ctypes.c_char_p()
+        _lib.check(_lib.load().nusi_get_kernels(self._h, ctypes.byref(a), ctypes.byref(c)))
+        return a.value.decode(), c.value.decode()
+
     def check_energy_conservation(self):
         """(E_int - E_FS)/E_FS (nuSIprop.pyx:140-144).  Evolves the C++ object, but -- as in the
         reference -- does not set the Python-side evolved flag."""

@@ -60,13 +60,17 @@ def group_bounds(points):
 
 
 def shard_aligned(points, world, rank):
-    """Contiguous block [lo, hi) of rank `rank` whose ends fall on table-group boundaries (runs of points
-    sharing a table stay on one GPU), each end the group boundary nearest to the even
-    split r * n / world.  Ranks may get empty blocks when there are fewer groups than ranks."""
+    """Contiguous block [lo, hi) of rank `rank` whose ends fall on table-group boundaries where that costs
+    little balance (runs of points sharing a table stay on one GPU): each end is the group
+    boundary nearest to the even split r * n / world, unless that boundary is more than half a block away
+    -- a group much larger than n / world (e.g. a pure spectral-index scan: one table) -- in which case the
+    cut is the even split itself and the group's table is built on both ranks (one Stage-A table per GPU is
+    cheaper than idle GPUs)."""
     n = len(points)
     if n == 0:
         return 0, 0
     b = group_bounds(points)
+    tol = n / world / 2.0
 
     def cut(r):
         if r <= 0:
@@ -74,7 +78,8 @@ def shard_aligned(points, world, rank):
         if r >= world:
             return n
         ideal = r * n / world
-        return min(b, key=lambda x: (abs(x - ideal), x))
+        near = min(b, key=lambda x: (abs(x - ideal), x))
+        return near if abs(near - ideal) <= tol else int(round(ideal))
 
     return cut(rank), max(cut(rank), cut(rank + 1))
 

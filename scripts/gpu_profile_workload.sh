@@ -10,5 +10,5 @@ timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/kt -o kt --output-for
 timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $OUT/pmc_fetch -o fetch --output-format csv -- python3 bench.py $BARGS > $OUT/pmc_fetch.log 2>&1 && \
 timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d $OUT/pmc_write -o write --output-format csv -- python3 bench.py $BARGS > $OUT/pmc_write.log 2>&1 && \
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $OUT/pmc_calib -o calib --output-format csv -- ./scripts/calib/pmc_calib > $OUT/pmc_calib.log 2>&1 && \
-python scripts/pmc_summary.py $OUT/pmc_fetch $OUT/pmc_write $OUT/pmc_calib > $OUT/pmc_traffic_summary.json && \
+python scripts/pmc_summary.py $OUT/pmc_fetch $OUT/pmc_write $OUT/pmc_calib --lib nusiprop_amd/libnusi.so > $OUT/pmc_traffic_summary.json && \
 timeout -k 10 600 python bench.py $BARGS --traffic-json $OUT/pmc_traffic_summary.json > $OUT/bench.json 2> $OUT/bench.err

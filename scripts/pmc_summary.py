@@ -9,7 +9,10 @@ fp64 VALU work per launch (for the table kernel's VALU roofline) comes from an
 optional fourth pass with SQ_INSTS_VALU_{ADD,MUL,FMA,TRANS}_F64: per-wave
 instruction counts, x 64 lanes, FMA counted as 2 flops.
 
-  python scripts/pmc_summary.py <fetch_dir> <write_dir> <calib_dir> [<valu_dir>] > traffic.json
+  python scripts/pmc_summary.py <fetch_dir> <write_dir> <calib_dir> [<valu_dir>] [--lib libnusi.so] > traffic.json
+
+--lib records the sha256 of the library the passes ran (bench.py drops traffic / flops taken from a
+summary whose hash differs from the library it loads).
 """
 import csv
 import glob
@@ -40,6 +43,13 @@ def per_step(d, counter, name_part):
 
 
 def main():
+    argv = list(sys.argv[1:])
+    lib = None
+    if "--lib" in argv:
+        k = argv.index("--lib")
+        lib = argv[k + 1]
+        del argv[k:k + 2]
+    sys.argv[1:] = argv
     fetch_dir, write_dir, calib_dir = sys.argv[1:4]
     calib_bytes = 2 << 30
     cal = per_kernel(calib_dir, "FETCH_SIZE")
@@ -78,6 +88,10 @@ def main():
             fma = per_step(sys.argv[4], "SQ_INSTS_VALU_FMA_F64", "nusi::k_alpha")[0]
             trn = per_step(sys.argv[4], "SQ_INSTS_VALU_TRANS_F64", "nusi::k_alpha")[0]
             out["k_alpha_fp64_flops_per_step"] = 64.0 * (add + mul + 2.0 * fma + trn)
+    if lib:
+        import hashlib
+        with open(lib, "rb") as fh:
+            out["libnusi_sha256"] = hashlib.sha256(fh.read()).hexdigest()
     json.dump(out, sys.stdout, indent=1)
 
 

@@ -1,0 +1,47 @@
+"""bench.py's multi-GPU launch path (the driver's N = 1, 2, 4, 8 scaling runs): `--gpus N` without a launcher
+starts N rank processes itself (torch.distributed.run, before any GPU call) and the line reports the ranks that
+actually ran; a rank count that differs from --gpus is an error.  --dry-run exercises the launch, rendezvous and
+max-over-ranks reduction on CPU (gloo) without GPU work."""
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _bench(args, env=None, timeout=300):
+    e = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        e.pop(k, None)
+    e.update(env or {})
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, cwd=ROOT, env=e,
+                          capture_output=True, text=True, timeout=timeout)
+
+
+def _line(out):
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout + out.stderr
+    return json.loads(lines[0])
+
+
+def test_gpus2_launches_two_ranks():
+    out = _bench(["--gpus", "2", "--dry-run", "--steps", "3", "--warmup", "0"])
+    assert out.returncode == 0, out.stderr
+    j = _line(out)
+    assert j["n_gpus"] == 2 and j["ranks_reporting"] == 2 and j["dry_run"] and j["value"] is None
+    assert "launching 2 ranks" in out.stderr
+
+
+def test_single_gpu_runs_in_process():
+    out = _bench(["--dry-run", "--steps", "2", "--warmup", "0"])
+    assert out.returncode == 0, out.stderr
+    j = _line(out)
+    assert j["n_gpus"] == 1 and j["ranks_reporting"] == 1
+    assert "launching" not in out.stderr
+
+
+def test_rank_count_mismatch_is_an_error():
+    out = _bench(["--gpus", "4", "--dry-run"], env={"WORLD_SIZE": "2", "RANK": "0", "LOCAL_RANK": "0"})
+    assert out.returncode != 0 and "WORLD_SIZE=2" in out.stderr
+    assert not [l for l in out.stdout.splitlines() if l.startswith("{")]

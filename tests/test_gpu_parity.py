@@ -28,9 +28,12 @@ def nusi():
     return nusiprop_amd
 
 
-def _gpu(nusi, pts):
+def _gpu(nusi, pts, **opts):
+    from nusiprop_amd import _lib
     p0 = pts[0]
     plan = nusi.Plan(p0["N_bins_E"], p0["lEmin"], p0["lEmax"], p0["zmax"], max_points=len(pts))
+    for k, v in opts.items():
+        plan.set_option(getattr(_lib, "OPT_" + k.upper()), v)
     flux, fla = plan.evolve(pts)
     tabs = [plan.tables(i) for i in range(len(pts))]
     warn = plan.warnings(len(pts))
@@ -43,6 +46,7 @@ def test_tables_bitexact_and_flux(nusi, oracle_mod, name):
     o = oracle_mod.Oracle(**cases.oracle_kwargs(kw))
     G, aT, al = o.tables()
     plan, flux, fla, tabs, warn = _gpu(nusi, [kw])
+    assert plan.kernels()[1] == "k_cascade_ws"   # the default (AUTO) cascade, for every source and mode
     Gg, aTg, Ag = tabs[0]
     T = o.T
     assert plan.T == T and plan.N == o.N and plan.Nz == o.Nz
@@ -171,11 +175,12 @@ def test_gamma_batches_share_tables(nusi, oracle_mod):
 @pytest.mark.parametrize("N,nonres", [(37, True), (64, False), (130, True), (200, True), (300, True), (300, False),
                                       (700, True)])
 def test_cascade_kernels_agree(nusi, N, nonres):
-    """The wavefront cascade (all redshift steps in flight, N_z - 1 <= 48) and the register-
-    resident one give the same fluxes bit for bit (same fma()s in the same order); the LDS
-    kernel (separate multiply and add, the reference's record arithmetic) agrees to FLUX_RTOL; N = 700 exceeds the wavefront
-    kernel's limits and checks its fallback.  The MFMA-push variant sums each block of four
-    columns in the matrix core's order: FLUX_RTOL, and the same exact zeros."""
+    """The bit-exact scalar cascades -- the wavefront (all redshift steps in flight, N_z - 1 <= 48) and the
+    register-resident per-step chain -- give the same fluxes bit for bit (same fma()s in the same order); the
+    LDS kernel (separate multiply and add, the reference's record arithmetic) and the default MFMA kernels
+    (AUTO = MFMA: blocks of four columns summed in the matrix core's order) agree to FLUX_RTOL with the same
+    exact zeros.  N = 700 exceeds the one-pass kernels' limits: the wavefront falls back to the register
+    kernel, the MFMA kind runs in step passes."""
     from nusiprop_amd import _lib
     pts = [dict(cases.C2B_100, N_bins_E=N, non_resonant=nonres, majorana=maj, mphi=m, g=gg)
            for maj, m, gg in ((True, 6e5, 0.01), (False, 2e6, 0.1), (True, 1e6, 0.3))]
@@ -187,12 +192,13 @@ def test_cascade_kernels_agree(nusi, N, nonres):
     ref = out[_lib.CASCADE_REG]
     assert np.all(np.isfinite(ref[1])) and np.any(ref[1] > 0)
     for kind, (f, fl) in out.items():
-        if kind in (_lib.CASCADE_LDS, _lib.CASCADE_MFMA):   # MFMA: blocks of 4 columns summed in its own order
+        if kind in (_lib.CASCADE_LDS, _lib.CASCADE_MFMA, _lib.CASCADE_AUTO):
             assert cases.rel_err(f, ref[0]) <= FLUX_RTOL and cases.rel_err(fl, ref[1]) <= FLUX_RTOL
             assert np.array_equal(f == 0, ref[0] == 0)
             continue
         assert np.array_equal(f, ref[0]), "kind %d flux differs in %d entries" % (kind, np.sum(f != ref[0]))
         assert np.array_equal(fl, ref[1])
+    assert np.array_equal(out[_lib.CASCADE_AUTO][0], out[_lib.CASCADE_MFMA][0])
 
 
 def test_alpha_batches_bitexact(nusi, oracle_mod):
@@ -260,20 +266,16 @@ def test_plan_serialises_calls_across_streams(nusi):
         H.hipStreamDestroy(s2)
 
 
-def test_alpha_batch_kernel_equals_tile_kernel(nusi, monkeypatch):
+def test_alpha_batch_kernel_equals_tile_kernel(nusi):
     """The big-batch alpha kernel (shared leaves once per batch of up to 64 tables, points one after the
     other) and the k_alpha_tile<G> batches of 3 give the same tables and fluxes bit for bit: a C4-style
     slice (2 m_phi x 8 couplings, Majorana) plus Dirac and resonant-only points, several batch caps."""
     base = [dict(cases.C2B_100, mphi=m, g=g) for m in (6e5, 2e6) for g in np.logspace(-3, 0, 8)]
     pts = base + [dict(cases.C2B_100, mphi=1e6, g=0.1, majorana=False), dict(cases.C2B_100, mphi=1e6, g=0.2,
                                                                              non_resonant=False)]
-    monkeypatch.setenv("NUSI_ALPHA_KERNEL", "tile")
-    ref = _gpu(nusi, pts)
-    monkeypatch.delenv("NUSI_ALPHA_KERNEL")
-    for cap in ("", "1", "5", "64"):
-        if cap:
-            monkeypatch.setenv("NUSI_ALPHA_BATCH", cap)
-        got = _gpu(nusi, pts)
+    ref = _gpu(nusi, pts, alpha_kernel=1)
+    for cap in (0, 1, 5, 64):
+        got = _gpu(nusi, pts, alpha_batch=cap)
         assert np.array_equal(got[1], ref[1]) and np.array_equal(got[2], ref[2]), cap
         for a, b in zip(got[3], ref[3]):
             for x, y in zip(a, b):
@@ -281,44 +283,55 @@ def test_alpha_batch_kernel_equals_tile_kernel(nusi, monkeypatch):
         assert got[4] == ref[4]
 
 
-def _evolve_env(nusi, pts, monkeypatch, **env):
-    """evolve `pts` on the MFMA cascade with the A/B switches in `env` (NUSI_CASCADE_WS, NUSI_MRHS,
-    NUSI_CASCADE_WSP)."""
+def _evolve_opts(nusi, pts, kind=None, **opts):
+    """evolve `pts` on the default (AUTO = MFMA) cascade, or `kind`, with plan options (nusi_plan_set_option:
+    cascade_rhs, step_passes, ...)."""
     from nusiprop_amd import _lib
-    for k in ("NUSI_CASCADE_WS", "NUSI_MRHS", "NUSI_CASCADE_WSP"):
-        monkeypatch.delenv(k, raising=False)
-    for k, v in env.items():
-        monkeypatch.setenv(k, v)
     p0 = pts[0]
     plan = nusi.Plan(p0["N_bins_E"], p0["lEmin"], p0["lEmax"], p0["zmax"], max_points=len(pts))
-    plan.set_cascade(_lib.CASCADE_MFMA)
+    if kind is not None:
+        plan.set_cascade(kind)
+    for k, v in opts.items():
+        plan.set_option(getattr(_lib, "OPT_" + k.upper()), v)
     out = plan.evolve(pts)
+    names = plan.kernels()
     plan.close()
-    return out
+    return out + (names,)
 
 
 @pytest.mark.parametrize("N", [37, 100, 130, 300])
-def test_cascade_ws_equals_mfma(nusi, monkeypatch, N):
-    """The warp-specialised cascade (push / record / chain waves in their own stage loops) gives
-    k_cascade_wf_mfma's fluxes bit for bit: one point per workgroup (distinct tables), and two points
-    per workgroup when they share a table (the multi-RHS kernel: gamma batches, one operator, two
-    sources), including a table slot with an odd number of points (a single in the pair list)."""
-    distinct = [dict(cases.C2B_100, N_bins_E=N, mphi=m, g=g, majorana=maj)
-                for m, g, maj in ((6e5, 0.01, True), (2e6, 0.1, False), (1e6, 0.3, True), (3e7, 0.8, True))]
-    ref = _evolve_env(nusi, distinct, monkeypatch, NUSI_CASCADE_WS="0")
-    got = _evolve_env(nusi, distinct, monkeypatch)
-    assert np.array_equal(got[0], ref[0]) and np.array_equal(got[1], ref[1])
-    gam = [dict(p, si=s, norm=nm) for p in distinct[:2] for s, nm in ((2.0, 1.0), (2.3, 3.0), (2.9, 0.5))]
-    gam.append(dict(distinct[2], si=2.7))
-    ref = _evolve_env(nusi, gam, monkeypatch, NUSI_CASCADE_WS="0", NUSI_MRHS="0")
-    one = _evolve_env(nusi, gam, monkeypatch, NUSI_MRHS="0")
-    two = _evolve_env(nusi, gam, monkeypatch)
-    for f in (one, two):
-        assert np.array_equal(f[0], ref[0]) and np.array_equal(f[1], ref[1])
+def test_cascade_ws_multi_rhs(nusi, N):
+    """The warp-specialised MFMA cascade on every point kind -- power-law and DSNB sources, non-resonant and
+    resonant-only, Majorana and Dirac: one point per workgroup (distinct tables) and two per workgroup when
+    they share a table (the multi-RHS kernel: gamma / norm / source batches, one operator, two sources, mixed
+    sources in one pair, a table slot with an odd number of points).  The pairs give the one-point-per-workgroup
+    fluxes bit for bit; both agree with the bit-exact wavefront to FLUX_RTOL with the same exact zeros."""
+    from nusiprop_amd import _lib
+    distinct = [dict(cases.C2B_100, N_bins_E=N, mphi=m, g=g, majorana=maj, non_resonant=nr, source_model=src)
+                for m, g, maj, nr, src in ((6e5, 0.01, True, True, 1), (2e6, 0.1, False, True, 1), (1e6, 0.3, True, True, 0),
+                                           (3e7, 0.8, True, False, 1), (8e5, 0.05, True, False, 0))]
+    # DSNB points at lE 12 -> 17 have a zero source (the Fermi-Dirac tail underflows): move them to lE 4 -> 9
+    lo = [dict(p, lEmin=4.0, lEmax=9.0, mphi=p["mphi"] / 200.0) for p in distinct]
+    for grid in (distinct, lo):
+        one = _evolve_opts(nusi, grid, cascade_rhs=1)
+        wf = _evolve_opts(nusi, grid, kind=_lib.CASCADE_WAVEFRONT)
+        assert one[2][1] == "k_cascade_ws"
+        for a, b in zip(one[:2], wf[:2]):
+            assert cases.rel_err(a, b) <= FLUX_RTOL and np.array_equal(a == 0, b == 0)
+        gam = [dict(p, si=s, norm=nm, source_model=src) for p in grid[:4]
+               for s, nm, src in ((2.0, 1.0, 1), (2.3, 3.0, 0), (2.9, 0.5, 1))]
+        gam.append(dict(grid[4], si=2.7))
+        ref = _evolve_opts(nusi, gam, cascade_rhs=1)
+        two = _evolve_opts(nusi, gam)
+        assert two[2][1] == "k_cascade_ws_mrhs"
+        assert np.array_equal(two[0], ref[0]) and np.array_equal(two[1], ref[1])
+        wf = _evolve_opts(nusi, gam, kind=_lib.CASCADE_WAVEFRONT)
+        assert cases.rel_err(two[1], wf[1]) <= FLUX_RTOL and np.array_equal(two[1] == 0, wf[1] == 0)
+        assert np.any(two[1] > 0)
 
 
 @pytest.mark.parametrize("N,lEmin", [(100, 12.0), (200, 12.0), (700, 12.0), (1200, 10.0)])
-def test_cascade_step_passes(nusi, oracle_mod, monkeypatch, N, lEmin):
+def test_cascade_step_passes(nusi, oracle_mod, N, lEmin):
     """The step-pass cascade (k_cascade_ws<16, 1, true>: 16 redshift steps in flight per pass, F carried
     in LDS from pass to pass; nuSIprop.hpp:257-315): N = 100 (16 steps, one pass) equals the one-pass
     kernel k_cascade_ws<16, 1> bit for bit; N = 200 (32 steps, 2 passes, forced), 700 (109 steps, 7 passes) and
@@ -327,9 +340,11 @@ def test_cascade_step_passes(nusi, oracle_mod, monkeypatch, N, lEmin):
     from nusiprop_amd import _lib
     pts = [dict(cases.C2B_100, N_bins_E=N, lEmin=lEmin, mphi=m, g=g, majorana=maj)
            for m, g, maj in ((6e5, 0.01, True), (1e5, 0.05, True), (2e6, 0.3, False))]
-    got = _evolve_env(nusi, pts, monkeypatch, NUSI_CASCADE_WSP="1")
+    got = _evolve_opts(nusi, pts, step_passes=1)
+    assert got[2][1] == "k_cascade_ws_passes"
     if N == 100:
-        one = _evolve_env(nusi, pts, monkeypatch, NUSI_CASCADE_WSP="0")
+        one = _evolve_opts(nusi, pts)
+        assert one[2][1] == "k_cascade_ws"
         assert np.array_equal(got[0], one[0]) and np.array_equal(got[1], one[1])
     plan = nusi.Plan(N, lEmin, pts[0]["lEmax"], pts[0]["zmax"], max_points=len(pts))
     plan.set_cascade(_lib.CASCADE_REG)
@@ -360,13 +375,17 @@ def test_plan_kernels_names(nusi):
         plan.close()
         return k
     two = [dict(mphi=6e5, g=0.01), dict(mphi=2e6, g=0.1)]
-    assert run(100, 12.0, two, _lib.CASCADE_MFMA) == ("k_alpha_batch", "k_cascade_ws")
-    assert run(100, 12.0, [dict(mphi=6e5, g=0.01, si=s) for s in (2.0, 2.5)], _lib.CASCADE_MFMA)[1] == "k_cascade_ws_mrhs"
-    assert run(700, 12.0, two, _lib.CASCADE_MFMA)[1] == "k_cascade_ws_passes"
-    assert run(100, 12.0, two, _lib.CASCADE_AUTO)[1] == "k_cascade_wf"
+    for kind in (_lib.CASCADE_AUTO, _lib.CASCADE_MFMA):
+        assert run(100, 12.0, two, kind) == ("k_alpha_batch", "k_cascade_ws")
+        assert run(100, 12.0, [dict(mphi=6e5, g=0.01, si=s) for s in (2.0, 2.5)], kind)[1] == "k_cascade_ws_mrhs"
+        assert run(700, 12.0, two, kind)[1] == "k_cascade_ws_passes"
+        assert run(100, 12.0, [dict(mphi=6e5, g=0.01, source_model=0, non_resonant=False)], kind)[1] == "k_cascade_ws"
+    assert run(100, 12.0, two, _lib.CASCADE_WAVEFRONT)[1] == "k_cascade_wf"
+    assert run(700, 12.0, two, _lib.CASCADE_WAVEFRONT)[1] == "k_cascade_reg"
+    assert run(100, 12.0, two, _lib.CASCADE_LDS)[1] == "k_cascade"
 
 
-def test_c5_gamma_block_vs_oracle(nusi, oracle_mod, monkeypatch):
+def test_c5_gamma_block_vs_oracle(nusi, oracle_mod):
     """BASELINE config 5: one full 16-gamma block of scan.c5_points() (N_E = 300, power law; one
     Stage-A table, 8 pairs on the multi-RHS cascade) against the oracle -- its tables once, its
     cascade per gamma -- to FLUX_RTOL with the same exact zeros; and the block through the
@@ -375,8 +394,9 @@ def test_c5_gamma_block_vs_oracle(nusi, oracle_mod, monkeypatch):
     allp = scan.c5_points()
     blk = allp[16 * 1234:16 * 1235]
     assert len({scan.table_key(p) for p in blk}) == 1 and len({p["si"] for p in blk}) == 16
-    flux, fla = _evolve_env(nusi, blk, monkeypatch)
-    ref1 = _evolve_env(nusi, blk, monkeypatch, NUSI_MRHS="0")
+    flux, fla, names = _evolve_opts(nusi, blk)
+    assert names[1] == "k_cascade_ws_mrhs"
+    ref1 = _evolve_opts(nusi, blk, cascade_rhs=1)
     assert np.array_equal(flux, ref1[0]) and np.array_equal(fla, ref1[1])
     o = oracle_mod.Oracle(**cases.oracle_kwargs(blk[0]))
     G, aT, al = o.tables()

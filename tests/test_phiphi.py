@@ -73,6 +73,50 @@ def test_phiphi_small_bitexact(tmp_path, oracle_mod):
 
 
 @pytest.mark.gpu
+def test_phiphi_multi_table_batches(tmp_path, oracle_mod):
+    """Several couplings per m_phi with phi-phi on share one k_alpha_batch<true> batch: the phi-phi core of a
+    mass state depends on (S', t) alone (m_phi, masses, bin edges) and is evaluated once per batch, each point
+    applies its own g^4 scale (alpha_phiphi_scale).  Plain points in the same call run on the other launch (the
+    batches without the channel), Dirac and resonant-only points on theirs.  Every table of every point is
+    bit-exact against the oracle -- automatic batches, caps of 1 and 64, and the tile kernel -- and the fluxes
+    agree to FLUX_RTOL."""
+    import nusiprop_amd as nusi
+    from nusiprop_amd import _lib
+    tabs = make_tables(str(tmp_path))
+    pts = [dict(PP_SMALL, g=g) for g in (0.01, 0.02, 0.05, 0.1, 0.3)]
+    pts += [dict(PP_SMALL, g=0.05, majorana=False), dict(PP_SMALL, g=0.08, majorana=False),
+            dict(PP_SMALL, g=0.05, phiphi=False), dict(PP_SMALL, g=0.2, phiphi=False),
+            dict(PP_SMALL, g=0.05, non_resonant=False), dict(PP_SMALL, g=0.02, si=2.2)]
+    refs = []
+    for kw in pts:
+        o = oracle_mod.Oracle(**cases.oracle_kwargs(kw))
+        if kw["phiphi"] and kw["non_resonant"]:
+            o.load_phiphi(*tabs)
+        G, aT, al = o.tables()
+        refs.append((o, G, aT, al))
+    T = refs[0][0].T
+    iu = np.triu_indices(T, 1)
+    for opt, val in ((None, 0), (_lib.OPT_ALPHA_BATCH, 1), (_lib.OPT_ALPHA_BATCH, 64), (_lib.OPT_ALPHA_KERNEL, 1)):
+        p = nusi.Plan(PP_SMALL["N_bins_E"], PP_SMALL["lEmin"], PP_SMALL["lEmax"], PP_SMALL["zmax"], max_points=len(pts))
+        p.load_phiphi(tabs[0], tabs[2], tabs[1], tabs[3])
+        if opt is not None:
+            p.set_option(opt, val)
+        flux, fla = p.evolve(pts)
+        for k, (o, G, aT, al) in enumerate(refs):
+            Gg, aTg, Ag = p.tables(k)
+            assert np.array_equal(Gg, G) and np.array_equal(aTg, aT), (opt, val, k)
+            A = nusi.unpack_alpha(Ag, T)
+            if pts[k]["non_resonant"]:
+                assert np.array_equal(A[iu], al[iu]), (opt, val, k, int(np.sum(A[iu] != al[iu])))
+            else:
+                d = np.arange(T - 1)
+                assert np.array_equal(A[d, d + 1], al[d, d + 1]), (opt, val, k)
+            f_ref, fla_ref = o.cascade(G, aT, al)
+            assert cases.rel_err(fla[k], fla_ref) <= cases.FLUX_RTOL, (opt, val, k)
+        p.close()
+
+
+@pytest.mark.gpu
 def test_phiphi_out_of_range_is_an_error(tmp_path):
     """A lookup outside the table nodes ends the reference (interp.hpp:355-361); here NUSI_EINTERP."""
     import nusiprop_amd as nusi

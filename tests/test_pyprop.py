@@ -105,3 +105,24 @@ def test_default_phiphi_needs_tables(nusi, tmp_path, monkeypatch):
         nusi.pyprop(6e5, 0.01, 0.1, 2.5, N_bins_E=50)
     assert e.value.code == nusi._lib.NUSI_ETABLE
     assert "does not exist" in str(e.value)
+
+
+@pytest.mark.parametrize("kw,kernel", [
+    (dict(cases.TEST_CPP, N_bins_E=300, phiphi=False), "k_cascade_ws"),                      # C1 at N_E = 300 (DSNB)
+    (dict(cases.C2A, phiphi=False), "k_cascade_ws"),                                         # C2a (DSNB, resonance in range)
+    (dict(cases.TEST_PY, phiphi=False), "k_cascade_ws"),                                     # resonant-only, DSNB
+    (dict(cases.TEST_CPP, N_bins_E=1200, lEmin=10.0, lEmax=17.0, phiphi=False, source_model=1),
+     "k_cascade_ws_passes"),                                                                 # the C3 grid (134 steps)
+], ids=["C1_N300", "C2a_N300", "test_py", "C3_grid"])
+def test_drop_in_object_gets_the_fast_cascade(nusi, oracle_mod, kw, kernel):
+    """The drop-in object (calculate_flux / pyprop: one point, default kernels) runs the MFMA cascade for the
+    reference's own DSNB source and resonant-only mode and, beyond 48 redshift steps, its step-pass form --
+    fluxes against the oracle's evolve() to FLUX_RTOL with the same exact zeros."""
+    ev = nusi.pyprop(**_kw(kw))
+    ev.evolve()
+    assert ev.kernels()[1] == kernel
+    o = oracle_mod.Oracle(**cases.oracle_kwargs(kw))
+    f_ref, fla_ref = o.evolve()
+    assert cases.rel_err(ev.get_flux(), f_ref) <= cases.FLUX_RTOL
+    assert cases.rel_err(ev.get_flux_fla(), fla_ref) <= cases.FLUX_RTOL
+    assert np.any(fla_ref > 0)

@@ -130,8 +130,9 @@ def _gamma_groups(sizes, N=20):
     return pts
 
 
-@pytest.mark.parametrize("sizes,world", [((5, 5, 5, 5), 3), ((16,) * 3 + (7,), 3), ((3, 1, 4, 1, 5), 4), ((2,), 3)])
+@pytest.mark.parametrize("sizes,world", [((5, 5, 5, 5), 3), ((16,) * 3 + (7,), 3), ((3, 1, 4, 1, 5), 4), ((2, 2, 1, 3), 3)])
 def test_shard_aligned_keeps_table_groups(sizes, world):
+    """Groups no larger than half a block stay whole, each cut at the group boundary nearest the even split."""
     pts = _gamma_groups(sizes)
     blocks = [scan.shard_aligned(pts, world, r) for r in range(world)]
     assert blocks[0][0] == 0 and blocks[-1][1] == len(pts)
@@ -143,6 +144,21 @@ def test_shard_aligned_keeps_table_groups(sizes, world):
     for r in range(1, world):
         ideal = r * len(pts) / world
         assert abs(blocks[r][0] - ideal) == min(abs(b - ideal) for b in bounds)
+
+
+@pytest.mark.parametrize("sizes,world", [((64,), 4), ((64,), 8), ((2,), 3), ((40, 2, 2), 4), ((100, 3), 2)])
+def test_shard_aligned_splits_large_groups(sizes, world):
+    """A group much larger than a block (a pure spectral-index scan shares one table) is split at the even
+    cuts, so no GPU idles: every block is within half a block of n / world, and the blocks tile the scan."""
+    pts = _gamma_groups(sizes)
+    n = len(pts)
+    blocks = [scan.shard_aligned(pts, world, r) for r in range(world)]
+    assert blocks[0][0] == 0 and blocks[-1][1] == n
+    assert all(blocks[r][1] == blocks[r + 1][0] for r in range(world - 1))
+    for lo, hi in blocks:
+        assert abs((hi - lo) - n / world) <= n / world / 2.0 + 1
+    if sizes == (64,):
+        assert all(hi - lo == 64 // world for lo, hi in blocks)
 
 
 def test_sharded_evolve_gloo_world3_uneven_groups(oracle_mod):
