@@ -471,13 +471,19 @@ double ora_alphaTilde(ora_state *S, double Em, double Ep)   /* nuSIprop.hpp:924-
     return tot;
 }
 
+static int g_ref_order;
 /* The s-t interference's g-dependent pieces (nuSIprop.hpp:1440-1459), dt = 2 + t - i gr, a = 1 + S + t,
  * c = 2 + t:  Li2(w), w = a / dt = a (c + i gr) / (c^2 + gr^2), by the Taylor series about the real point
  * x0 = a / c at d = w - x0 = i (gr / c) w when |d| <= 2.5e-3 min(|x0|, |1 - x0|), else the general complex
  * dilog; and arg(-(-1 + i gr + S) / dt) = arg(S - 1 + i gr) + arg(c + i gr) - pi, each argument written as
  * f pi + s with s the small angle.  The GPU forms them the same way (nusi_physics.hpp alpha_member_*). */
+static void member_dc_ref(double S, double t, double gr, double *re, double *im);
 static void member_dc(double S, double t, double gr, double *re, double *im)
 {
+    if (g_ref_order) {
+        member_dc_ref(S, t, gr, re, im);
+        return;
+    }
     const double a = 1 + S + t, c = 2 + t;
     const double x0 = a / c;
     const double ax = fabs(x0), a1 = fabs(1.0 - x0);
@@ -493,8 +499,29 @@ static void member_dc(double S, double t, double gr, double *re, double *im)
     if (dr * dr + di * di <= m * m) ora_li2_taylor_eval(&T, dr, di, 1.0, re, im);
     else ora_complex_dilog_xy(wr, wi, re, im);
 }
+/* Reference-order arithmetic (ora_set_reference_order, test infrastructure): the s-t interference's
+ * member dilogs are the general complex dilogarithm of the reference's quotient z = (1+S+t)/(2 - i gr + t)
+ * (C99 complex division, nuSIprop.hpp:1432-1438 -> gsl_sf_complex_dilog_xy_e, :1444-1451) and its arguments
+ * carg(-((-1 + i gr + S)/(2 - i gr + t))) (:1456), instead of member_dc's Taylor evaluation and member_arg's sum of
+ * edge arguments; every complex dilogarithm skips the near-axis Taylor path.  Measures how far the
+ * shared-algorithm tables sit from the reference's own operation order (tests/test_oracle_reference_order.py). */
+void ora_set_reference_order(int level)
+{
+    g_ref_order = level != 0;
+    ora_cdilog_set_general(level);
+}
+static void member_dc_ref(double S, double t, double gr, double *re, double *im)
+{
+    const zc z = zrdiv(1 + S + t, zmk(2 + t, -gr));
+    ora_complex_dilog_xy(z.r, z.i, re, im);
+}
+static double member_arg_ref(double S, double t, double gr)
+{
+    return zarg(zneg(zdiv(zmk(-1 + S, gr), zmk(2 + t, -gr))));
+}
 static double member_arg(double S, double t, double gr)
 {
+    if (g_ref_order) return member_arg_ref(S, t, gr);
     const double c = 2 + t;
     double sS, fS, sT, fT;
     if (S < 1.0) { sS = -ora_atan2(gr, 1.0 - S); fS = 1.0; } else { sS = ora_atan2(gr, S - 1.0); fS = 0.0; }

@@ -37,6 +37,12 @@ int ora_load_phiphi(ora_state *S, const char *alphatilde_path, const char *alpha
 /* same with caller-chosen node counts (synthetic tables in the reference layout) */
 int ora_load_phiphi_dims(ora_state *S, const char *at_path, const int *n2, const char *a_path, const int *n3);
 
+/* Test hook (process-wide, not thread-safe; 0 by default): 1 = reference-order arithmetic in the alpha
+ * table's s-t interference -- the general complex dilog of the reference's quotient and carg of its
+ * expression (nuSIprop.hpp:1431-1456), no member Taylor path, no near-axis shortcut in any complex dilog;
+ * 2 = the same with every complex dilog evaluated in long double (precision probe) */
+void ora_set_reference_order(int level);
+
 int ora_N(const ora_state *S);
 int ora_Nz(const ora_state *S);
 int ora_T(const ora_state *S);

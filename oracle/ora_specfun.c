@@ -133,6 +133,12 @@ static void cdilog_axis(double x, double y, double *re, double *im)
     ora_li2_taylor_eval(&T, 0.0, y, y > 0.0 ? 1.0 : -1.0, re, im);
 }
 
+/* reference-order arithmetic (ora_set_reference_order): 1 = the complex dilogarithm without the near-axis
+ * Taylor shortcut, 2 = its long-double evaluation (precision probe) -- test infrastructure, read-only while
+ * tables are built */
+static int g_cdilog_general = 0;
+void ora_cdilog_set_general(int on) { g_cdilog_general = on; }
+
 void ora_complex_dilog_xy(double x, double y, double *re, double *im)
 {
     if (y == 0.0) {
@@ -141,7 +147,11 @@ void ora_complex_dilog_xy(double x, double y, double *re, double *im)
         *im = (x >= 1.0) ? -PI_D * ora_log(x) : 0.0;
         return;
     }
-    {
+    if (g_cdilog_general == 2) {   /* (precision probe: the long-double evaluation) */
+        ora_complex_dilog_xy_ld(x, y, re, im);
+        return;
+    }
+    if (!g_cdilog_general) {
         const double ax = fabs(x), a1 = fabs(1.0 - x);
         if (fabs(y) <= AXIS_RATIO * (ax < a1 ? ax : a1)) {
             cdilog_axis(x, y, re, im);

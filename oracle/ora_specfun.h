@@ -32,6 +32,8 @@ extern "C" {
 
 double ora_dilog(double x);                                  /* gsl_sf_dilog */
 void ora_complex_dilog_xy(double x, double y, double *re, double *im);
+/* 1: ora_complex_dilog_xy skips its near-axis Taylor path (the general series everywhere) */
+void ora_cdilog_set_general(int on);
 /* Li2 about a real point x0 (x0 != 0, 1): coefficients and evaluation at x0 + (dr + i di) on the side
  * `side` (+-1) of the cut x0 > 1; |d| <= ORA_LI2T_RATIO min(|x0|, |1 - x0|) */
 #define ORA_LI2T_TERMS 6

@@ -84,6 +84,7 @@ def lib():
         L.ora_getmL.restype = i
         L.ora_getmL.argtypes = [d, d, d, dp]
         L.ora_set_channels.argtypes = [p, i]
+        L.ora_set_reference_order.argtypes = [i]
         L.ora_Gpp_bracket.restype = d
         L.ora_Gpp_bracket.argtypes = [d, d]
         _lib = L
@@ -115,6 +116,24 @@ CH_S, CH_T, CH_U, CH_TU, CH_ST, CH_SU, CH_PP, CH_ALL = 1, 2, 4, 8, 16, 32, 64, 1
 def Gpp_bracket(a, b):
     """The bracket of the analytic phi-phi absorption (nuSIprop.hpp:885), a = max(s-, 4)."""
     return lib().ora_Gpp_bracket(float(a), float(b))
+
+
+class reference_order:
+    """Context: the oracle in reference-order arithmetic (nusi_oracle.h ora_set_reference_order) -- the alpha
+    table's s-t member dilogs as the general complex dilogarithm of the reference's own quotient and carg of
+    its expression (nuSIprop.hpp:1431-1456), no near-axis Taylor shortcut (level 1); level 2 evaluates every
+    complex dilogarithm in long double (a precision probe).  Process-wide: tests only."""
+
+    def __init__(self, level=1):
+        self.level = int(level)
+
+    def __enter__(self):
+        lib().ora_set_reference_order(self.level)
+        return self
+
+    def __exit__(self, *exc):
+        lib().ora_set_reference_order(0)
+        return False
 
 
 def getmL(msum, dm21, dmAT):

@@ -141,12 +141,6 @@ def test_reference_geometry_tables(tmp_path):
     assert t[0, 0] == np.float32(4.0) and t[-1, 0] == np.float32(1e4) and np.all(t[:, 2] > 0)
 
 
-@pytest.fixture(scope="module")
-def ref_tables(tmp_path_factory):
-    d = str(tmp_path_factory.mktemp("pp_ref"))
-    return write_synthetic_tables(d)
-
-
 def test_c3_oracle_stays_inside_reference_nodes(ref_tables, oracle_mod):
     """BASELINE C3 (m_phi = 1e5, N_E = 1200, lE 10 -> 17): every phi-phi lookup of the full table build
     falls inside the reference's table nodes (x1 = (m - n) * 1.0001 <= 1000, log10 delta = 7/1200), so
