@@ -168,9 +168,9 @@ int nusi_plan_set_cascade(nusi_plan *plan, int kind);
  * environment to select kernels.  NUSI_EPARAM for an unknown option or value.
  *   NUSI_OPT_ALPHA_BATCH   max tables per alpha batch (tables sharing m_phi,
  *                          masses and flags), 1..255; 0 = automatic
- *   NUSI_OPT_ALPHA_KERNEL  0 = k_alpha_wave (default), 1 = k_alpha_tile
- *                          batches of <= 4, 2 = one entry per work-item,
- *                          3 = k_alpha_batch (all tables bit-identical)
+ *   NUSI_OPT_ALPHA_KERNEL  0 = k_alpha_batch (default), 1 = k_alpha_tile
+ *                          batches of <= 4, 2 = one entry per work-item
+ *                          (all three give the same tables bit for bit)
  *   NUSI_OPT_CASCADE_RHS   max points sharing a table per MFMA-cascade
  *                          workgroup: 0 = automatic, 1 = one point each
  *   NUSI_OPT_STEP_PASSES   0 = automatic (step passes beyond 48 redshift

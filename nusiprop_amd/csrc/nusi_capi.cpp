@@ -410,7 +410,7 @@ struct nusi_plan {
     int* d_batches = nullptr;       // alpha-table batches (nusi::launch_alpha): first table | count << 24
     int* h_batches = nullptr;       // pinned
     int alpha_batch = 0;            // NUSI_OPT_ALPHA_BATCH: max tables per batch; 0 = auto
-    int alpha_kind = 0;             // NUSI_OPT_ALPHA_KERNEL: 0 k_alpha_wave, 1 k_alpha_tile<G> (<= 4), 2 per entry, 3 k_alpha_batch
+    int alpha_kind = 0;             // NUSI_OPT_ALPHA_KERNEL: 0 k_alpha_batch, 1 k_alpha_tile<G> (<= 4), 2 per entry
     int cascade_rhs = 0;            // NUSI_OPT_CASCADE_RHS: 0 = auto, 1 = one point per MFMA-cascade workgroup
     int step_passes = 0;            // NUSI_OPT_STEP_PASSES: 1 = the step-pass cascade also where one pass fits
     double* d_src = nullptr;        // DSNB source terms of the MFMA cascade [src_cap][cascade_src_doubles]
@@ -904,7 +904,7 @@ int nusi_plan_set_option(nusi_plan* pl, int option, int value)
         pl->alpha_batch = value;
         return NUSI_OK;
     case NUSI_OPT_ALPHA_KERNEL:
-        if (value < 0 || value > 3) return fail(NUSI_EPARAM, "NUSI_OPT_ALPHA_KERNEL outside [0, 3]");
+        if (value < 0 || value > 2) return fail(NUSI_EPARAM, "NUSI_OPT_ALPHA_KERNEL outside [0, 2]");
         pl->alpha_kind = value;
         return NUSI_OK;
     case NUSI_OPT_CASCADE_RHS:

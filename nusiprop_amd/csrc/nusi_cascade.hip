@@ -770,6 +770,14 @@ NUSI_FN double powerlaw_src(const GridDev& g, const Point& P, const double* pw, 
 {
     return g.step_c[i] * (P.norm_total / 3.0 * g.sfr[i] * (g.Emax[b] * pw[b + i + 1] - g.Emin[b] * pw[b + i]) * rcp_nr(1 - P.si));
 }
+// the same with the point's factors hoisted: a3 = norm_total / 3.0, rs = rcp_nr(1 - si) (the same operations,
+// once per point instead of once per record)
+struct SrcFactors { double a3, rs; };
+NUSI_FN SrcFactors src_factors(const Point& P) { return SrcFactors{P.norm_total / 3.0, rcp_nr(1 - P.si)}; }
+NUSI_FN double powerlaw_src_h(const GridDev& g, const SrcFactors& f, const double* pw, int i, int b)
+{
+    return g.step_c[i] * (f.a3 * g.sfr[i] * (g.Emax[b] * pw[b + i + 1] - g.Emin[b] * pw[b + i]) * f.rs);
+}
 
 // The DSNB source term c_i Lum(z_i, Emin_b, Emax_b) (nuSIprop.hpp:283, :659-662) of every (step slot J, bin b)
 // of a point, computed before the MFMA cascade (it costs two Li2 / Li3 pairs per record, far more than a
@@ -793,6 +801,18 @@ hipError_t launch_source_dsnb(const GridDev& g, const Point* pts, int npts, doub
     return hipGetLastError();
 }
 
+// The chain's hand-off between steps: step slot j solves bin b at stage sg, right after slot j-1 solved the same
+// bin at stage sg-1 (nuSIprop.hpp:257-315: step i starts from step i+1's F[:, b]).  wave_shr1 moves each lane's
+// value to the next lane (DPP wave_shr:1, a register move across the wave); lane 0 receives `fill`.  It must run
+// with every lane of the wave active (a disabled source lane would leave its neighbour's old value).
+__device__ __forceinline__ double wave_shr1(double v, double fill)
+{
+    const long long x = __double_as_longlong(v), f = __double_as_longlong(fill);
+    const int lo = __builtin_amdgcn_update_dpp((int)f, (int)x, 0x138, 0xf, 0xf, false);
+    const int hi = __builtin_amdgcn_update_dpp((int)(f >> 32), (int)(x >> 32), 0x138, 0xf, 0xf, false);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
 // The resonant-only chain (nuSIprop.hpp:261-278, 285-287): the running sum of the bins above, from the
 // lane's own solve of bin b+1 (x = F[:, b+1] of this step) -- k_cascade_wf's expression.  sde = dE_b.
 NUSI_FN double resonant_add(double& racc, double u0, double u1, double u2, double px0, double px1, double px2,
@@ -809,6 +829,28 @@ constexpr int kWsP2Wave = 1;   // R = 2: the LU phase of the records on a wave o
 template <int R> struct WsCfg;
 template <> struct WsCfg<1> { static constexpr int RT = 4, kMaxThreads = 512; };   // 6 push waves + 2
 template <> struct WsCfg<2> { static constexpr int RT = 2, kMaxThreads = 832 + 64 * kWsP2Wave; };   // 11 push waves + 2 (3)
+
+// Diagnostic build only (-DNUSI_WS_TRACE, scripts/build_variant.sh): s_memtime stamps of workgroup 0's waves
+// at the start of each stage's work and at its barrier (read the shares, not the length: the stamps cost
+// cycles).  nusi_debug_ws_trace() copies them out.  Compiled out of the product.
+#ifdef NUSI_WS_TRACE
+constexpr int kTrWaves = 16, kTrStages = 512, kTrBlocks = 8192;
+__device__ unsigned long long g_ws_trace[kTrWaves * kTrStages * 2];
+__device__ unsigned int g_ws_hwid[kTrBlocks * kTrWaves];   // HW_ID (SE, CU, SIMD, wave slot) of every wave
+#define NUSI_WS_HWID()                                                                                             \
+    do {                                                                                                           \
+        if ((threadIdx.x & 63) == 0 && blockIdx.x < kTrBlocks)                                                     \
+            g_ws_hwid[blockIdx.x * kTrWaves + (threadIdx.x >> 6)] = __builtin_amdgcn_s_getreg(4 | (31 << 11));     \
+    } while (0)
+#define NUSI_WS_STAMP(sg, which)                                                                                   \
+    do {                                                                                                           \
+        if (blockIdx.x == 0 && (threadIdx.x & 63) == 0 && (sg) < kTrStages)                                        \
+            g_ws_trace[((threadIdx.x >> 6) * kTrStages + (sg)) * 2 + (which)] = __builtin_amdgcn_s_memtime();        \
+    } while (0)
+#else
+#define NUSI_WS_STAMP(sg, which) do { } while (0)
+#define NUSI_WS_HWID() do { } while (0)
+#endif
 
 template <int NJ, int R>
 __global__ __launch_bounds__(WsCfg<R>::kMaxThreads) __attribute__((amdgpu_waves_per_eu(4, 4)))
@@ -831,6 +873,7 @@ void k_cascade_ws(GridDev g, const Point* __restrict__ pts, const int2* __restri
         pid[R - 1] = gp.y >= 0 ? gp.y : gp.x;
         single = gp.y < 0;
     }
+    NUSI_WS_HWID();
     double* F = lds;                         // [R][3][N]
     double* rec = F + 3 * R * N;             // [NF][3][NJ]  records of stage sg in slot sg % 3
     double* Tp = rec + 3 * NF * NJ;          // [R][8][NJ]   T_j by stage (ring of 8)
@@ -887,6 +930,13 @@ void k_cascade_ws(GridDev g, const Point* __restrict__ pts, const int2* __restri
     //   phase 2 (chain wave, one stage later): the LU of M -- cascade_record's operations, split
     constexpr int S3 = 3 * NJ;
     const bool nonres = P.non_resonant;   // the points of a workgroup share a table, hence the flags
+    SrcFactors sf[R];   // each point's source factors and kind (the record wave's)
+    bool pl[R];
+#pragma unroll
+    for (int p = 0; p < R; ++p) {
+        sf[p] = src_factors(pts[pid[p]]);
+        pl[p] = pts[pid[p]].source == NUSI_SOURCE_POWER_LAW;
+    }
     auto phase1 = [&](int s2, int jj) {
         const int b = N - 1 - s2 + jj, i = Nz - 1 - jj;
         if (jj < nst && b >= 0 && b < N) {
@@ -903,12 +953,10 @@ void k_cascade_ws(GridDev g, const Point* __restrict__ pts, const int2* __restri
             Rw[(FM + 5) * S3] = m.m21;
             Rw[PR_SDE * S3] = nonres ? gl.step_s[i] * rdE[b] : (gl.Emax[b] - gl.Emin[b]);
 #pragma unroll
-            for (int p = 0; p < R; ++p) {
-                const Point& Q = pts[pid[p]];
+            for (int p = 0; p < R; ++p)
                 Rw[(p == 0 ? PR_SRC : FSRC + p - 1) * S3] =
-                    Q.source == NUSI_SOURCE_POWER_LAW ? powerlaw_src(gl, Q, pw + p * (T + 2), i, b)
-                                                      : t.Src[(size_t)pid[p] * T * nst + src_index(Nz, jj, b)];
-            }
+                    pl[p] ? powerlaw_src_h(gl, sf[p], pw + p * (T + 2), i, b)
+                          : t.Src[(size_t)pid[p] * T * nst + src_index(Nz, jj, b)];
         }
     };
     auto phase2 = [&](int s2, int jj) {
@@ -933,26 +981,46 @@ void k_cascade_ws(GridDev g, const Point* __restrict__ pts, const int2* __restri
     if (wave == (kP2 ? nw - 3 : nw - 1)) phase2(0, lane);
     __syncthreads();
 
+    // R = 1: phase 2 of stage sg+1 runs on the chain wave until the top push wave (nw-3) has no rows left to push
+    // or publish (its rows all >= the block's column r = T-1-4q), then on that wave
+    const int top_rw0 = (nw - 3) * 16 * RT;
+    auto p2_on_top = [&](int sg) { return !kP2 && top_rw0 >= T - 1 - 4 * (sg >> 2); };
     if (wave == nw - 1) {
         // ---- chain: lane j solves (step j, bin N-1-sg+j) of every point at stage sg
         const int j = lane;
         const bool act = j < nst;
         const double u0 = P.u[0], u1 = P.u[1], u2 = P.u[2];
         const double cj = act ? gl.step_c[Nz - 1 - j] : 0.0, sj = act ? gl.step_s[Nz - 1 - j] : 0.0;
-        double racc[R], px0[R], px1[R], px2[R];   // resonant-only chain state of each point
+        // chain state in registers: px = the lane's last solve (F[:, b+1] of its step, which slot j+1 needs at
+        // the next stage and the resonant-only sum reads), Th = its T_j of the last four stages (the columns the
+        // published rows still lack); racc = the resonant-only running sum
+        double racc[R], px0[R], px1[R], px2[R], Th[R][4];
 #pragma unroll
-        for (int p = 0; p < R; ++p) racc[p] = px0[p] = px1[p] = px2[p] = 0.0;
+        for (int p = 0; p < R; ++p) {
+            racc[p] = px0[p] = px1[p] = px2[p] = 0.0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) Th[p][k] = 0.0;
+        }
         for (int sg0 = 0; sg0 < T; sg0 += 4)
 #pragma unroll
         for (int d = 0; d < 4; ++d) {
             const int sg = sg0 + d;
             if (sg >= T) break;
+            NUSI_WS_STAMP(sg, 0);
             const int r = T - 1 - sg;
             const int b = N - 1 - sg + j;
+            // F[:, b] of this step = slot j-1's solve of bin b at stage sg-1 (slot 0: the initial flux, 0)
+            double f0[R], f1[R], f2[R];
+#pragma unroll
+            for (int p = 0; p < R; ++p) {
+                f0[p] = wave_shr1(px0[p], 0.0);
+                f1[p] = wave_shr1(px1[p], 0.0);
+                f2[p] = wave_shr1(px2[p], 0.0);
+            }
             double Tn[R];
 #pragma unroll
             for (int p = 0; p < R; ++p) Tn[p] = 0.0;
-            if (!kP2 && sg + 1 < T) phase2(sg + 1, j);   // independent of this stage's solve
+            if (!kP2 && sg + 1 < T && !p2_on_top(sg)) phase2(sg + 1, j);   // independent of this stage's solve
             if (act && b >= 0 && b < N) {
                 const double* Rc = rec + (sg % 3) * NJ + j;
                 constexpr int S = S3;
@@ -962,6 +1030,9 @@ void k_cascade_ws(GridDev g, const Point* __restrict__ pts, const int2* __restri
                 const double u01 = Rc[PR_U01 * S], u02 = Rc[PR_U02 * S], u12 = Rc[PR_U12 * S];
                 const double ru00 = Rc[PR_RU00 * S], ru11 = Rc[PR_RU11 * S], ru22 = Rc[PR_RU22 * S];
                 const double sde = Rc[PR_SDE * S];
+                double srcv[R];
+#pragma unroll
+                for (int p = 0; p < R; ++p) srcv[p] = Rc[(p == 0 ? PR_SRC : FSRC + p - 1) * S];
                 double add[R];   // c_i x (coupling of the bin to the bins above)
                 if (nonres) {
                     const int qq = (sg - 1) >> 2;              // block whose publication serves stage sg
@@ -975,7 +1046,7 @@ void k_cascade_ws(GridDev g, const Point* __restrict__ pts, const int2* __restri
                         if (k <= nu) {
                             const double a = sdg[(k - 1) * T + r];
 #pragma unroll
-                            for (int p = 0; p < R; ++p) s[p] = fma(a, Tp[(p * 8 + ((sg - k) & 7)) * NJ + j], s[p]);
+                            for (int p = 0; p < R; ++p) s[p] = fma(a, Th[p][k - 1], s[p]);
                         }
 #pragma unroll
                     for (int p = 0; p < R; ++p) add[p] = cj * s[p];
@@ -989,31 +1060,41 @@ void k_cascade_ws(GridDev g, const Point* __restrict__ pts, const int2* __restri
 #pragma unroll
                 for (int p = 0; p < R; ++p) {
                     double* Fp = F + 3 * N * p;
-                    const double src = Rc[(p == 0 ? PR_SRC : FSRC + p - 1) * S];
                     double x0, x1, x2;
-                    cascade_solve(Fp[b], Fp[N + b], Fp[2 * N + b], add[p], src, u0, u1, u2, rz0, rz1, rz2, pmb, l10,
-                                  l20, l21, u01, u02, u12, ru00, ru11, ru22, x0, x1, x2);
-                    Fp[b] = x0;
-                    Fp[N + b] = x1;
-                    Fp[2 * N + b] = x2;
+                    cascade_solve(f0[p], f1[p], f2[p], add[p], srcv[p], u0, u1, u2, rz0, rz1, rz2, pmb, l10, l20, l21, u01,
+                                  u02, u12, ru00, ru11, ru22, x0, x1, x2);
+                    if (j == nst - 1) {   // the last step's flux (finalisation)
+                        Fp[b] = x0;
+                        Fp[N + b] = x1;
+                        Fp[2 * N + b] = x2;
+                    }
                     px0[p] = x0; px1[p] = x1; px2[p] = x2;
                     if (nonres && b > 0) Tn[p] = (u0 * x0 + u1 * x1 + u2 * x2) * sde;
                 }
             }
+#pragma unroll
+            for (int p = 0; p < R; ++p) {
+                Th[p][3] = Th[p][2]; Th[p][2] = Th[p][1]; Th[p][1] = Th[p][0]; Th[p][0] = Tn[p];
+            }
             if (act)
 #pragma unroll
                 for (int p = 0; p < R; ++p) Tp[(p * 8 + (sg & 7)) * NJ + j] = Tn[p];
+            NUSI_WS_STAMP(sg, 1);
             __syncthreads();
         }
     } else if (kP2 && wave == nw - 3) {
         for (int sg = 0; sg < T; ++sg) {
+            NUSI_WS_STAMP(sg, 0);
             if (sg + 1 < T) phase2(sg + 1, lane);
+            NUSI_WS_STAMP(sg, 1);
             __syncthreads();
         }
     } else if (wave == nw - 2) {
         // ---- phase 1 of the records two stages ahead, while the chain solves this stage
         for (int sg = 0; sg < T; ++sg) {
+            NUSI_WS_STAMP(sg, 0);
             if (sg + 2 < T) phase1(sg + 2, lane);
+            NUSI_WS_STAMP(sg, 1);
             __syncthreads();
         }
     } else {
@@ -1042,10 +1123,17 @@ void k_cascade_ws(GridDev g, const Point* __restrict__ pts, const int2* __restri
         double ablk[RT];
         load_blk(1, ablk);
         for (int sg = 0; sg < T; ++sg) {
+            NUSI_WS_STAMP(sg, 0);
             // block q is pushed at stage 4q by the waves holding the rows it publishes, and one to three
             // stages later by the others (their rows are needed >= 5 stages on; the T_j ring keeps 8):
             // the matrix-core work of a block is spread over its four stages (kWsStagger)
             const int q = sg >> 2, r = T - 1 - 4 * q, hi = r - 1;
+            if (wave == nw - 3 && p2_on_top(sg)) {   // (uniform: this wave's rows are all consumed)
+                if (sg + 1 < T) phase2(sg + 1, lane);
+                NUSI_WS_STAMP(sg, 1);
+                __syncthreads();
+                continue;
+            }
             const bool crit = rw0 <= hi && rw0 + 16 * RT - 1 >= hi - 3;
             const int dw = (!kWsStagger || crit) ? 0 : 1 + wave % 3;
             if ((sg & 3) == dw && nonres) {
@@ -1083,6 +1171,7 @@ void k_cascade_ws(GridDev g, const Point* __restrict__ pts, const int2* __restri
                                 }
                         }
             }
+            NUSI_WS_STAMP(sg, 1);
             __syncthreads();
         }
     }
@@ -1194,6 +1283,13 @@ void k_cascade_wsp(GridDev g, const Point* __restrict__ pts, TablesDev t, double
     constexpr int S3 = 3 * NJ;
     int jb = 0;   // first step slot of the current pass (step i = Nz-1-jb-j for slot j)
     const bool nonres = P.non_resonant;
+    SrcFactors sf[R];   // each point's source factors and kind (the record wave's)
+    bool pl[R];
+#pragma unroll
+    for (int p = 0; p < R; ++p) {
+        sf[p] = src_factors(pts[pid[p]]);
+        pl[p] = pts[pid[p]].source == NUSI_SOURCE_POWER_LAW;
+    }
     auto phase1 = [&](int s2, int jj) {
         const int b = N - 1 - s2 + jj, i = Nz - 1 - jb - jj;
         if (jj < NJ && jb + jj < nst && b >= 0 && b < N) {
@@ -1210,12 +1306,10 @@ void k_cascade_wsp(GridDev g, const Point* __restrict__ pts, TablesDev t, double
             Rw[(FM + 5) * S3] = m.m21;
             Rw[PR_SDE * S3] = nonres ? gl.step_s[i] * rdE[b] : (gl.Emax[b] - gl.Emin[b]);
 #pragma unroll
-            for (int p = 0; p < R; ++p) {
-                const Point& Q = pts[pid[p]];
+            for (int p = 0; p < R; ++p)
                 Rw[(p == 0 ? PR_SRC : FSRC + p - 1) * S3] =
-                    Q.source == NUSI_SOURCE_POWER_LAW ? powerlaw_src(gl, Q, pw + p * (T + 2), i, b)
-                                                      : t.Src[(size_t)pid[p] * T * nst + src_index(Nz, jb + jj, b)];
-            }
+                    pl[p] ? powerlaw_src_h(gl, sf[p], pw + p * (T + 2), i, b)
+                          : t.Src[(size_t)pid[p] * T * nst + src_index(Nz, jb + jj, b)];
         }
     };
     auto phase2 = [&](int s2, int jj) {
@@ -1257,9 +1351,15 @@ void k_cascade_wsp(GridDev g, const Point* __restrict__ pts, TablesDev t, double
         const bool act = j < NJ && jb + j < nst;
         const double u0 = P.u[0], u1 = P.u[1], u2 = P.u[2];
         const double cj = act ? gl.step_c[Nz - 1 - jb - j] : 0.0, sj = act ? gl.step_s[Nz - 1 - jb - j] : 0.0;
-        double racc[R], px0[R], px1[R], px2[R];   // resonant-only chain state (per step: restarts every pass)
+        // chain state in registers (k_cascade_ws's; it restarts every pass with the pass's steps)
+        double racc[R], px0[R], px1[R], px2[R], Th[R][4];
 #pragma unroll
-        for (int p = 0; p < R; ++p) racc[p] = px0[p] = px1[p] = px2[p] = 0.0;
+        for (int p = 0; p < R; ++p) {
+            racc[p] = px0[p] = px1[p] = px2[p] = 0.0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) Th[p][k] = 0.0;
+        }
+        const int jl = (nst - jb < NJ ? nst - jb : NJ) - 1;   // the pass's last step slot
         for (int sg0 = 0; sg0 < Ts; sg0 += 4)
 #pragma unroll
         for (int d = 0; d < 4; ++d) {
@@ -1267,6 +1367,17 @@ void k_cascade_wsp(GridDev g, const Point* __restrict__ pts, TablesDev t, double
             if (sg >= Ts) break;
             const int r = c0 - sg;
             const int b = N - 1 - sg + j;
+            // F[:, b] of this step: slot j-1's solve of bin b at stage sg-1; slot 0 reads the previous pass's
+            // last step from LDS (0 in the first pass)
+            double f0[R], f1[R], f2[R];
+#pragma unroll
+            for (int p = 0; p < R; ++p) {
+                const double* Fp = F + 3 * N * p;
+                const bool from_lds = j == 0 && b >= 0 && b < N;
+                f0[p] = wave_shr1(px0[p], from_lds ? Fp[b] : 0.0);
+                f1[p] = wave_shr1(px1[p], from_lds ? Fp[N + b] : 0.0);
+                f2[p] = wave_shr1(px2[p], from_lds ? Fp[2 * N + b] : 0.0);
+            }
             double Tn[R];
 #pragma unroll
             for (int p = 0; p < R; ++p) Tn[p] = 0.0;
@@ -1293,7 +1404,7 @@ void k_cascade_wsp(GridDev g, const Point* __restrict__ pts, TablesDev t, double
                         if (k <= nu) {
                             const double a = sdg[(k - 1) * T + r];
 #pragma unroll
-                            for (int p = 0; p < R; ++p) s[p] = fma(a, Tp[(p * 8 + ((sg - k) & 7)) * NJ + j], s[p]);
+                            for (int p = 0; p < R; ++p) s[p] = fma(a, Th[p][k - 1], s[p]);
                         }
 #pragma unroll
                     for (int p = 0; p < R; ++p) add[p] = cj * s[p];
@@ -1309,14 +1420,20 @@ void k_cascade_wsp(GridDev g, const Point* __restrict__ pts, TablesDev t, double
                     double* Fp = F + 3 * N * p;
                     const double src = Rc[(p == 0 ? PR_SRC : FSRC + p - 1) * S];
                     double x0, x1, x2;
-                    cascade_solve(Fp[b], Fp[N + b], Fp[2 * N + b], add[p], src, u0, u1, u2, rz0, rz1, rz2, pmb, l10,
-                                  l20, l21, u01, u02, u12, ru00, ru11, ru22, x0, x1, x2);
-                    Fp[b] = x0;
-                    Fp[N + b] = x1;
-                    Fp[2 * N + b] = x2;
+                    cascade_solve(f0[p], f1[p], f2[p], add[p], src, u0, u1, u2, rz0, rz1, rz2, pmb, l10, l20, l21, u01,
+                                  u02, u12, ru00, ru11, ru22, x0, x1, x2);
+                    if (j == jl) {   // the pass's last step: the next pass's (or the finalisation's) flux
+                        Fp[b] = x0;
+                        Fp[N + b] = x1;
+                        Fp[2 * N + b] = x2;
+                    }
                     px0[p] = x0; px1[p] = x1; px2[p] = x2;
                     if (nonres && b > 0) Tn[p] = (u0 * x0 + u1 * x1 + u2 * x2) * sde;
                 }
+            }
+#pragma unroll
+            for (int p = 0; p < R; ++p) {
+                Th[p][3] = Th[p][2]; Th[p][2] = Th[p][1]; Th[p][1] = Th[p][0]; Th[p][0] = Tn[p];
             }
             if (act)
 #pragma unroll
@@ -1578,3 +1695,18 @@ hipError_t launch_cascade_exact(const GridDev& g, const Point* pts, int npts, Ta
 }
 
 }  // namespace nusi
+
+#ifdef NUSI_WS_TRACE
+// diagnostic build: workgroup 0's stage stamps of the latest k_cascade_ws launch, [wave][stage][start, barrier]
+extern "C" int nusi_debug_ws_trace(unsigned long long* out, int n)
+{
+    const int m = n < nusi::kTrWaves * nusi::kTrStages * 2 ? n : nusi::kTrWaves * nusi::kTrStages * 2;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(nusi::g_ws_trace), sizeof(unsigned long long) * m) == hipSuccess ? 0 : -5;
+}
+// HW_ID of every wave of the first kTrBlocks workgroups, [block][wave]
+extern "C" int nusi_debug_ws_hwid(unsigned int* out, int n)
+{
+    const int m = n < nusi::kTrBlocks * nusi::kTrWaves ? n : nusi::kTrBlocks * nusi::kTrWaves;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(nusi::g_ws_hwid), sizeof(unsigned int) * m) == hipSuccess ? 0 : -5;
+}
+#endif

@@ -52,9 +52,9 @@ hipError_t launch_gamma_alphat(const GridDev& g, const Point* pts, int npts, con
                                int* warn, hipStream_t s);
 // batches: device [nbatches] of first table | count << 24 (count <= gmax), tables of a batch sharing
 // m_phi, the masses and the channel flags (nullptr: every table alone).  kernel = NUSI_OPT_ALPHA_KERNEL:
-// 0 -- core tiles on the wave-per-point batch kernel k_alpha_wave (any count < 256; the first nb_plain batches
-// without the phi-phi channel, the rest with it); 3 -- the same on k_alpha_batch; 1 -- k_alpha_tile<G> batches
-// (count <= 4); 2 -- one entry per work-item (k_alpha)
+// 0 -- core tiles on the big-batch kernel k_alpha_batch (any count < 256; the first nb_plain batches without
+// the phi-phi channel, the rest with it); 1 -- k_alpha_tile<G> batches (count <= 4); 2 -- one entry per
+// work-item (k_alpha)
 hipError_t launch_alpha(const GridDev& g, const Point* pts, int npts, const SplineSet& spl, const AlphaTilesDev& tiles,
                         TablesDev t, int* warn, hipStream_t s, const int* batches, int nbatches, int gmax,
                         int kernel, int nb_plain);

@@ -499,198 +499,6 @@ void k_alpha_batch(GridDev g, const Point* __restrict__ pts, SplineSet spl, cons
         for (int q = 0; q < nb; ++q) atomicOr(&warn[p0 + q], wsh);
 }
 
-// ---------------------------------------------------------------------------
-// k_alpha_wave: k_alpha_batch with the batch's points dealt to waves.  One workgroup of kAwWaves waves per
-// (class-0 tile, batch of tables sharing m_phi, the masses and the flags).  Mass state by mass state the whole
-// workgroup forms the batch's shared leaves and brackets (k_alpha_batch's phases, the brackets of each entry
-// now kept in LDS); then wave w runs points w, w + kAwWaves, ... on its own, with no workgroup barrier: it
-// copies the point's member edge leaves (k_alpha_medge's table) into its LDS slice, evaluates the point's member
-// corners (four corners per lane) and combines the tile's entries (four per lane), each entry accumulating the
-// mass states in the output array.  k_alpha_batch ran every point through the whole workgroup with two
-// barriers per point, where the slowest wave of each phase (a corner off the Taylor radius, an entry on a
-// quadrature fallback) held the other three.  Same functions on the same LDS leaves in the same order: the
-// tables are k_alpha_batch's bit for bit.
-// LDS (doubles): P3 [3][ccm] | X [kXFields][ccm] | edgk [estride] | pre [4][225] | ppt [3][225] (kPP) |
-// per wave: mem [2][ccm] | memb [mbd]
-// ---------------------------------------------------------------------------
-template <bool kPP> struct AwCfg { static constexpr int W = kPP ? 6 : 8; };
-constexpr int kAwCcm = (kAlphaTile + 1) * (kAlphaTile + 1), kAwEntries = kAlphaTile * kAlphaTile;
-__host__ __device__ constexpr int alpha_wave_mbd() { return 5 * (kAlphaTile + 1) + 4 * (kAlphaTile + 1) + kAlphaTile; }
-__host__ __device__ constexpr int alpha_wave_lds_doubles(bool pp, int W)
-{
-    return (3 + kXFields) * kAwCcm + (kTEdgeFields + kSEdgeFields) * (kAlphaTile + 1) + kMBinFields * kAlphaTile +
-           4 * kAwEntries + (pp ? 3 * kAwEntries : 0) + W * (2 * kAwCcm + alpha_wave_mbd());
-}
-// LDS visibility within one wave: the wave's DS operations complete in order; this keeps the compiler from
-// moving memory operations across the point's phases
-__device__ __forceinline__ void wave_lds_sync()
-{
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-}
-
-template <bool kPP>
-__global__ __launch_bounds__(64 * AwCfg<kPP>::W) __attribute__((amdgpu_waves_per_eu(4, 4)))
-void k_alpha_wave(GridDev g, const Point* __restrict__ pts, SplineSet spl, const int* __restrict__ tiles,
-                  const int* __restrict__ batches, double* __restrict__ A, const double* __restrict__ med,
-                  int* __restrict__ warn)
-{
-    constexpr int W = AwCfg<kPP>::W, NT = 64 * W;
-    extern __shared__ __attribute__((aligned(16))) double sm[];
-    __shared__ double tE[2 * kAlphaTile], sE[2 * kAlphaTile];
-    __shared__ int tl[kAlphaTile], th[kAlphaTile], sl[kAlphaTile], sh[kAlphaTile];
-    __shared__ int cnt[2];
-    __shared__ double elo[2][kAlphaTile], ehi[2][kAlphaTile];
-    __shared__ int tsrc[2 * kAlphaTile], ssrc[2 * kAlphaTile];   // bin edge (2 b + side) behind each list slot
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, T = g.T;
-    const int bw = batches[blockIdx.y];
-    const int p0 = bw & 0xffffff, nb = (int)((unsigned)bw >> 24);   // tables p0 .. p0 + nb - 1
-    const unsigned tu = (unsigned)tiles[blockIdx.x];                 // tile word, as in k_alpha_tile
-    const int half = (tu >> 28) & 3, nhalf = (tu >> 30) & 3;
-    const int n0 = (tu & 0x3fff) * kAlphaTile + (nhalf == 2 ? 8 : 0);
-    const int m0 = ((tu >> 14) & 0x3fff) * kAlphaTile + (half == 2 ? 8 : 0);
-    const int mcnt = half == 0 ? kAlphaTile : (half == 1 ? 8 : kAlphaTile - 8);
-    const int ncnt = nhalf == 0 ? kAlphaTile : (nhalf == 1 ? 8 : kAlphaTile - 8);
-    const int Tm = (m0 + mcnt < T) ? m0 + mcnt : T;
-    const int Tn = (n0 + ncnt < T) ? n0 + ncnt : T;
-    const Point& P = pts[p0];
-    if (tid < 2 * kAlphaTile) {
-        const int side = tid / kAlphaTile, j = tid - side * kAlphaTile, b = (side ? m0 : n0) + j;
-        if (b < (side ? Tm : Tn)) { elo[side][j] = g.lo[b]; ehi[side][j] = g.hi[b]; }
-    }
-    __syncthreads();
-    if (tid == 0) cnt[0] = alpha_edge_list(elo[0], ehi[0], 0, Tn - n0, tE, tl, th);
-    if (tid == 64) cnt[1] = alpha_edge_list(elo[1], ehi[1], 0, Tm - m0, sE, sl, sh);
-    __syncthreads();
-    const int ct = cnt[0], cs = cnt[1], cc = cs * ct;
-    if (tid < 2 * kAlphaTile) {
-        const int side = tid / kAlphaTile, j = tid - side * kAlphaTile, b0 = side ? m0 : n0;
-        const int* il = side ? sl : tl;
-        const int* ih = side ? sh : th;
-        int* src = side ? ssrc : tsrc;
-        if (b0 + j < (side ? Tm : Tn)) {
-            src[ih[j]] = 2 * (b0 + j) + 1;
-            if (j == 0 || il[j] != ih[j - 1]) src[il[j]] = 2 * (b0 + j);   // else the previous bin's upper edge
-        }
-    }
-    if (cs > kAlphaTile + 1 || ct > kAlphaTile + 1) {   // host classification guarantees this never happens
-        for (int e = tid; e < kAwEntries; e += NT) {
-            const int n = n0 + e % kAlphaTile, m = m0 + e / kAlphaTile;
-            if (n < m && m < Tm && n < Tn)
-                for (int q = 0; q < nb; ++q) A[(size_t)(p0 + q) * g.PT + (size_t)m * (m - 1) / 2 + n] = __builtin_nan("");
-        }
-        return;
-    }
-    const bool nonres = P.non_resonant, maj = P.majorana, cornered = nonres && maj;
-    double* P3 = sm;                                   // [3][cc]
-    double* X = P3 + 3 * kAwCcm;                       // [kXFields][cc] | LL TU1 TU2 G [4][cc] + mixed
-    double* edgk = X + kXFields * kAwCcm;              // [estride]
-    double* pre_s = edgk + (kTEdgeFields + kSEdgeFields) * (kAlphaTile + 1) + kMBinFields * kAlphaTile;   // [4][225]
-    double* ppt_s = pre_s + 4 * kAwEntries;            // [3][225] (kPP)
-    double* wbase = ppt_s + (kPP ? 3 * kAwEntries : 0) + wave * (2 * kAwCcm + alpha_wave_mbd());
-    double* mem = wbase;                               // [2][cc] this wave's point's member corners
-    double* memb = wbase + 2 * kAwCcm;                 // [mbd]   its member edges
-    double* tmp = X;
-    double* mix = X + 4 * cc;
-    const int mjobs = ct + cs + kAlphaTile;
-    int wsh = 0;
-#pragma unroll 1
-    for (int k = 0; k < 3; ++k) {
-        __syncthreads();   // the previous k's points are done with P3, X, edgk, pre, their slices
-        if (tid < mjobs) alpha_tile_edge_job_k(P, k, tid, tE, ct, sE, cs, g.lo, g.hi, m0, Tm, edgk);
-        __syncthreads();
-        // ---- the batch's shared leaves and brackets of mass state k (k_alpha_batch's phases); the brackets
-        // of entry e go to pre_s / ppt_s
-        if (cornered) {
-            for (int j = tid; j < cc; j += NT) b_corner(j, edgk, ct, cs, P3, tmp);
-            for (int j = tid; j < kAlphaTile * (cs + ct); j += NT)
-                alpha_batch_mixed_job(j, edgk, ct, cs, tl, th, sl, sh, n0, m0, T, Tm, mix, mix + kAlphaTile * cs);
-            __syncthreads();
-            if (tid < kAwEntries) {
-                const int ln = tid % kAlphaTile, lm = tid / kAlphaTile, n = n0 + ln, m = m0 + lm;
-                if (n < m && m < Tm && n < Tn) {
-                    SplitLeaves lv;
-                    lv.cf[0] = P3; lv.cf[1] = tmp; lv.cf[2] = tmp + cc; lv.cf[3] = tmp + 2 * cc; lv.cf[4] = tmp + 3 * cc;
-                    lv.cf[5] = P3 + cc; lv.cf[6] = P3 + 2 * cc;
-                    lv.corm = P3;   // (no member leaf is read by the brackets)
-                    lv.cc = cc; lv.ct = ct; lv.cs = cs; lv.mb = lm; lv.nb = ln;
-                    lv.sidx[0] = sl[lm]; lv.sidx[1] = sh[lm]; lv.tidx[0] = tl[ln]; lv.tidx[1] = th[ln];
-                    lv.ted = edgk; lv.sed = edgk + kTEdgeFields * ct; lv.mbv = lv.sed + kSEdgeFields * cs;
-                    lv.tedm = memb; lv.sedm = memb + ct; lv.mbm = memb + ct + 2 * cs; lv.marg = memb;   // (not read)
-                    lv.xl = mix; lv.yl = mix + kAlphaTile * cs;
-                    const AlphaPre pre = b_pre(P, k, g.lo[n], g.hi[n], g.lo[m], g.hi[m], lv);
-                    pre_s[tid] = pre.Dt; pre_s[kAwEntries + tid] = pre.Bt;
-                    pre_s[2 * kAwEntries + tid] = pre.Dtu; pre_s[3 * kAwEntries + tid] = pre.Btu;
-                    if (kPP) {
-                        const PPTerm pp = alpha_k_pp(P, spl, k, g.lo[n], g.hi[n], g.lo[m], g.hi[m], lv, wsh);
-                        ppt_s[tid] = pp.f1; ppt_s[kAwEntries + tid] = pp.f2; ppt_s[2 * kAwEntries + tid] = pp.den;
-                    }
-                }
-            }
-            __syncthreads();   // X is rewritten with the member coefficients
-            for (int j = tid; j < cc; j += NT) b_xshared(j, edgk, ct, cs, X);
-        }
-        __syncthreads();
-        // ---- the points, one wave each: member edges, member corners, the combine -- no workgroup barrier
-#pragma unroll 1
-        for (int q = wave; q < nb; q += W) {
-            const Point& Q = pts[p0 + q];
-            // the sums of the mass states < k of this point's entries (issued first: their latency is covered
-            // by the member phases)
-            double tot[4];
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const int e = lane + 64 * i, ln = e % kAlphaTile, lm = e / kAlphaTile, n = n0 + ln, m = m0 + lm;
-                const bool need = e < kAwEntries && n < m && m < Tm && n < Tn && (nonres || m == n + 1);
-                tot[i] = (k > 0 && need) ? A[(size_t)(p0 + q) * g.PT + (size_t)m * (m - 1) / 2 + n] : 0.0;
-            }
-            if (lane < mjobs) {
-                MedVals mv{};
-                alpha_batch_medge_load(nonres, lane, tsrc, ct, ssrc, cs, m0, Tm, T,
-                                       med + ((size_t)(p0 + q) * 3 + k) * kMedFields * T, mv);
-                alpha_batch_medge_store(nonres, lane, ct, cs, m0, Tm, mv, memb);
-            }
-            wave_lds_sync();
-            if (cornered)
-                for (int j = lane; j < cc; j += 64) alpha_batch_mcorner_job(Q, j, edgk, ct, cs, X, memb, mem);
-            wave_lds_sync();
-#pragma unroll 1
-            for (int i = 0; i < 4; ++i) {
-                const int e = lane + 64 * i;
-                if (e >= kAwEntries) break;
-                const int ln = e % kAlphaTile, lm = e / kAlphaTile, n = n0 + ln, m = m0 + lm;
-                if (!(n < m && m < Tm && n < Tn)) continue;
-                double t = (i == 0) ? tot[0] : (i == 1) ? tot[1] : (i == 2) ? tot[2] : tot[3];
-                int w = 0;
-                if (nonres || m == n + 1) {
-                    SplitLeaves lv;
-                    lv.cf[0] = P3; lv.cf[1] = P3; lv.cf[2] = P3; lv.cf[3] = P3; lv.cf[4] = P3;
-                    lv.cf[5] = P3 + cc; lv.cf[6] = P3 + 2 * cc;   // (LL, TU1, TU2, G are not read with pre)
-                    lv.corm = mem;
-                    lv.cc = cc; lv.ct = ct; lv.cs = cs; lv.mb = lm; lv.nb = ln;
-                    lv.sidx[0] = sl[lm]; lv.sidx[1] = sh[lm]; lv.tidx[0] = tl[ln]; lv.tidx[1] = th[ln];
-                    lv.ted = edgk; lv.sed = edgk + kTEdgeFields * ct; lv.mbv = lv.sed + kSEdgeFields * cs;
-                    lv.tedm = memb; lv.sedm = memb + ct; lv.mbm = memb + ct + 2 * cs;
-                    lv.marg = memb + ct + 2 * cs + kAlphaTile + 2 * ct;   // sT | fT | sS | fS
-                    lv.xl = mix; lv.yl = mix;   // (not read with pre)
-                    const AlphaPre pre{pre_s[e], pre_s[kAwEntries + e], pre_s[2 * kAwEntries + e], pre_s[3 * kAwEntries + e]};
-                    PPTerm ppt{0.0, 1.0, 1.0};
-                    if (kPP) ppt = PPTerm{ppt_s[e], ppt_s[kAwEntries + e], ppt_s[2 * kAwEntries + e]};
-                    alpha_k(Q, spl, k, g.lo[n], g.hi[n], g.lo[m], g.hi[m], lv, t, w, cornered ? &pre : nullptr,
-                            kPP && cornered ? &ppt : nullptr);
-                    A[(size_t)(p0 + q) * g.PT + (size_t)m * (m - 1) / 2 + n] = t;
-                } else {
-                    A[(size_t)(p0 + q) * g.PT + (size_t)m * (m - 1) / 2 + n] = 0.0;
-                }
-                if (w) atomicOr(&warn[p0 + q], w);
-            }
-            wave_lds_sync();   // the next point overwrites this wave's slice
-        }
-    }
-    if (wsh)
-        for (int q = 0; q < nb; ++q) atomicOr(&warn[p0 + q], wsh);
-}
-
 hipError_t alpha_tiles_create(int T, const unsigned char* shared, AlphaTilesDev* out)
 {
     const int nt = (T + kAlphaTile - 1) / kAlphaTile;
@@ -766,9 +574,8 @@ hipError_t launch_alpha(const GridDev& g, const Point* pts, int npts, const Spli
                         int kernel, int nb_plain)
 {
     t_alpha_kernel = "k_alpha_tile";
-    if ((kernel == 0 || kernel == 3) && batches) {
-        const bool wave = kernel == 0;
-        t_alpha_kernel = wave ? "k_alpha_wave" : "k_alpha_batch";
+    if (kernel == 0 && batches) {
+        t_alpha_kernel = "k_alpha_batch";
         // class 0 on the big-batch kernel (batches of up to gmax tables), classes 1 / 2 per table
         if (at.ext_lo < g.T) {
             const long long L = g.T - at.ext_lo, ne = L * (L - 1) / 2;
@@ -782,29 +589,17 @@ hipError_t launch_alpha(const GridDev& g, const Point* pts, int npts, const Spli
             if (c == 0) {   // batches [0, nb_plain) without the phi-phi channel, then those with it
                 const size_t lds = sizeof(double) * (size_t)alpha_batch_lds_doubles();
                 if (cs > kAlphaTile + 1 || ct > kAlphaTile + 1) return hipErrorInvalidValue;
-                if (NUSI_MEDGE_GLOBAL || wave) {
+                if (NUSI_MEDGE_GLOBAL) {
                     if (!t.Med) return hipErrorInvalidValue;
                     hipLaunchKernelGGL(k_alpha_medge, dim3((unsigned)((5 * g.T + 255) / 256), npts, 3), dim3(256), 0, s,
                                        g, pts, t.Med);
                 }
-                if (wave) {
-                    constexpr int W0 = AwCfg<false>::W, W1 = AwCfg<true>::W;
-                    const size_t l0 = sizeof(double) * (size_t)alpha_wave_lds_doubles(false, W0);
-                    const size_t l1 = sizeof(double) * (size_t)alpha_wave_lds_doubles(true, W1);
-                    if (nb_plain > 0)
-                        hipLaunchKernelGGL(k_alpha_wave<false>, dim3(at.ncls[0], nb_plain), dim3(64 * W0), l0, s, g, pts,
-                                           spl, at.tiles, batches, t.A, t.Med, warn);
-                    if (nbatches > nb_plain)
-                        hipLaunchKernelGGL(k_alpha_wave<true>, dim3(at.ncls[0], nbatches - nb_plain), dim3(64 * W1), l1, s,
-                                           g, pts, spl, at.tiles, batches + nb_plain, t.A, t.Med, warn);
-                } else {
-                    if (nb_plain > 0)
-                        hipLaunchKernelGGL(k_alpha_batch<false>, dim3(at.ncls[0], nb_plain), dim3(kTileThreads), lds, s, g,
-                                           pts, spl, at.tiles, batches, t.A, t.Med, warn);
-                    if (nbatches > nb_plain)
-                        hipLaunchKernelGGL(k_alpha_batch<true>, dim3(at.ncls[0], nbatches - nb_plain), dim3(kTileThreads),
-                                           lds, s, g, pts, spl, at.tiles, batches + nb_plain, t.A, t.Med, warn);
-                }
+                if (nb_plain > 0)
+                    hipLaunchKernelGGL(k_alpha_batch<false>, dim3(at.ncls[0], nb_plain), dim3(kTileThreads), lds, s, g,
+                                       pts, spl, at.tiles, batches, t.A, t.Med, warn);
+                if (nbatches > nb_plain)
+                    hipLaunchKernelGGL(k_alpha_batch<true>, dim3(at.ncls[0], nbatches - nb_plain), dim3(kTileThreads),
+                                       lds, s, g, pts, spl, at.tiles, batches + nb_plain, t.A, t.Med, warn);
             } else {
                 const size_t lds = sizeof(double) * (size_t)alpha_tile_lds_doubles(cs, ct, 1);
                 hipLaunchKernelGGL(k_alpha_tile<1>, dim3(at.ncls[c], npts), dim3(kTileThreads), lds, s, g, pts, spl,

@@ -267,18 +267,17 @@ def test_plan_serialises_calls_across_streams(nusi):
 
 
 def test_alpha_batch_kernel_equals_tile_kernel(nusi):
-    """The batch alpha kernels -- k_alpha_wave (default: shared leaves once per batch, the batch's points dealt to
-    waves) and k_alpha_batch (points one after the other through the whole workgroup) -- and the k_alpha_tile<G>
-    batches of 3 give the same tables and fluxes bit for bit: a C4-style slice (2 m_phi x 8 couplings,
-    Majorana) plus Dirac and resonant-only points, several batch caps."""
+    """The big-batch alpha kernel (shared leaves once per batch of up to 64 tables, points one after the
+    other) and the k_alpha_tile<G> batches of 3 give the same tables and fluxes bit for bit: a C4-style
+    slice (2 m_phi x 8 couplings, Majorana) plus Dirac and resonant-only points, several batch caps."""
     base = [dict(cases.C2B_100, mphi=m, g=g) for m in (6e5, 2e6) for g in np.logspace(-3, 0, 8)]
     pts = base + [dict(cases.C2B_100, mphi=1e6, g=0.1, majorana=False), dict(cases.C2B_100, mphi=1e6, g=0.2,
                                                                              non_resonant=False)]
     ref = _gpu(nusi, pts, alpha_kernel=1)
     assert ref[0].kernels()[0] == "k_alpha_tile"
-    for kern, cap in ((0, 0), (0, 1), (0, 5), (0, 64), (3, 0), (3, 5)):
+    for kern, cap in ((0, 0), (0, 1), (0, 5), (0, 64)):
         got = _gpu(nusi, pts, alpha_batch=cap, alpha_kernel=kern)
-        assert got[0].kernels()[0] == ("k_alpha_wave" if kern == 0 else "k_alpha_batch")
+        assert got[0].kernels()[0] == "k_alpha_batch"
         assert np.array_equal(got[1], ref[1]) and np.array_equal(got[2], ref[2]), (kern, cap)
         for a, b in zip(got[3], ref[3]):
             for x, y in zip(a, b):
@@ -379,7 +378,7 @@ def test_plan_kernels_names(nusi):
         return k
     two = [dict(mphi=6e5, g=0.01), dict(mphi=2e6, g=0.1)]
     for kind in (_lib.CASCADE_AUTO, _lib.CASCADE_MFMA):
-        assert run(100, 12.0, two, kind) == ("k_alpha_wave", "k_cascade_ws")
+        assert run(100, 12.0, two, kind) == ("k_alpha_batch", "k_cascade_ws")
         assert run(100, 12.0, [dict(mphi=6e5, g=0.01, si=s) for s in (2.0, 2.5)], kind)[1] == "k_cascade_ws_mrhs"
         assert run(700, 12.0, two, kind)[1] == "k_cascade_ws_passes"
         assert run(100, 12.0, [dict(mphi=6e5, g=0.01, source_model=0, non_resonant=False)], kind)[1] == "k_cascade_ws"

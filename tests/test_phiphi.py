@@ -96,8 +96,7 @@ def test_phiphi_multi_table_batches(tmp_path, oracle_mod):
         refs.append((o, G, aT, al))
     T = refs[0][0].T
     iu = np.triu_indices(T, 1)
-    for opt, val in ((None, 0), (_lib.OPT_ALPHA_BATCH, 1), (_lib.OPT_ALPHA_BATCH, 64), (_lib.OPT_ALPHA_KERNEL, 1),
-                     (_lib.OPT_ALPHA_KERNEL, 3)):
+    for opt, val in ((None, 0), (_lib.OPT_ALPHA_BATCH, 1), (_lib.OPT_ALPHA_BATCH, 64), (_lib.OPT_ALPHA_KERNEL, 1)):
         p = nusi.Plan(PP_SMALL["N_bins_E"], PP_SMALL["lEmin"], PP_SMALL["lEmax"], PP_SMALL["zmax"], max_points=len(pts))
         p.load_phiphi(tabs[0], tabs[2], tabs[1], tabs[3])
         if opt is not None:
