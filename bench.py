@@ -424,8 +424,20 @@ def main():
                                            "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                                            "frac": mf / casc_s / 1e12 / FP64_PEAK_TFLOPS,
                                            "note": "v_mfma_f64_16x16x4f64 rank-4 pushes (scan.cascade_mfma_flops_per_point)"}
+        # matrix-core counters of the cascade kernels (the profile's MFMA pass), summed over a step's launches
+        mc = {}
+        for kname, rec in pmc.get("kernels", {}).items():
+            if "k_cascade" in kname:
+                for c, v in rec.get("mfma_counters_per_launch", {}).items():
+                    mc[c] = mc.get(c, 0.0) + v
+        if mc:
+            out["roofline_cascade"]["mfma"]["pmc_per_step"] = mc
+            busy = mc.get("SQ_VALU_MFMA_BUSY_CYCLES")
+            if busy:   # matrix-core busy cycles per v_mfma_f64_16x16x4f64 the push issues (2048 flops each)
+                out["roofline_cascade"]["mfma"]["busy_cycles_per_mfma_pmc"] = busy / (
+                    out["roofline_cascade"]["mfma"]["flops_per_launch"] / 2048.0)
     fl = pmc.get("k_alpha_fp64_flops_per_step")
-    if fl:   # the dominant kernel: executed fp64 VALU flops (PMC counts) per second vs the fp64 vector peak
+    if fl and alpha_s >= casc_s:   # the dominant kernel: executed fp64 VALU flops (PMC counts) per second vs the fp64 vector peak
         ach = fl / alpha_s / 1e12
         out["roofline"] = {"bound": "valu", "kernel": alpha_kernel, "achieved": ach, "peak": FP64_PEAK_TFLOPS,
                            "unit": "TFLOP/s", "frac": ach / FP64_PEAK_TFLOPS,
@@ -434,7 +446,7 @@ def main():
                                     "from the PMC pass; time = the kernel's HIP events in this run",
                            "note": "dominant kernel (alpha_table.share_of_step); fp64 vector-ALU bound "
                                    "(transcendental leaves), neither HBM nor MFMA"}
-    else:
+    else:   # the cascade dominates (C5's gamma batches), or no alpha counters for this binary
         out["roofline"] = dict(out["roofline_cascade"])
     if args.workload in ("c1", "c2") and rank == 0:
         out["single_propagation"] = single_point_latency(pts[0], max(20, args.steps))

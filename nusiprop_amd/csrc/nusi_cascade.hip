@@ -825,6 +825,10 @@ NUSI_FN double resonant_add(double& racc, double u0, double u1, double u2, doubl
 // push waves not publishing spread their block MFMAs over the block's stages: k_cascade_wsp yes (C3 cascade
 // 37.3 -> 36.0 ms), k_cascade_ws no (C4 0.698 -> 0.728, C5 4.58 -> 4.93 ms; profiles/r2q)
 constexpr bool kWsStagger = false, kWspStagger = true;
+#ifndef NUSI_WS_P2TOP
+#define NUSI_WS_P2TOP 0
+#endif
+constexpr bool kWsP2Top = NUSI_WS_P2TOP;   // R = 1: phase 2 on the top push wave once its rows are consumed (A/B)
 constexpr int kWsP2Wave = 1;   // R = 2: the LU phase of the records on a wave of its own (nw-3), not the chain (A/B: C5 cascade 5.75 -> 4.49 ms)
 template <int R> struct WsCfg;
 template <> struct WsCfg<1> { static constexpr int RT = 4, kMaxThreads = 512; };   // 6 push waves + 2
@@ -984,7 +988,7 @@ void k_cascade_ws(GridDev g, const Point* __restrict__ pts, const int2* __restri
     // R = 1: phase 2 of stage sg+1 runs on the chain wave until the top push wave (nw-3) has no rows left to push
     // or publish (its rows all >= the block's column r = T-1-4q), then on that wave
     const int top_rw0 = (nw - 3) * 16 * RT;
-    auto p2_on_top = [&](int sg) { return !kP2 && top_rw0 >= T - 1 - 4 * (sg >> 2); };
+    auto p2_on_top = [&](int sg) { return kWsP2Top && !kP2 && top_rw0 >= T - 1 - 4 * (sg >> 2); };
     if (wave == nw - 1) {
         // ---- chain: lane j solves (step j, bin N-1-sg+j) of every point at stage sg
         const int j = lane;

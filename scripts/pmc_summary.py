@@ -38,16 +38,20 @@ def per_step(d, counter, name_part):
     for f in glob.glob(d + "/**/*counter_collection.csv", recursive=True):
         for row in csv.DictReader(open(f)):
             if row["Counter_Name"] == counter and name_part in row["Kernel_Name"]:
-                groups[row["Grid_Size"]].append(float(row["Counter_Value"]))
+                groups[(row["Kernel_Name"], row["Grid_Size"])].append(float(row["Counter_Value"]))
     return sum(sum(v) / len(v) for v in groups.values()), len(groups)
 
 
 def main():
     argv = list(sys.argv[1:])
-    lib = None
+    lib = mfma_dir = None
     if "--lib" in argv:
         k = argv.index("--lib")
         lib = argv[k + 1]
+        del argv[k:k + 2]
+    if "--mfma" in argv:   # optional pass of matrix-core counters (whichever the box offered)
+        k = argv.index("--mfma")
+        mfma_dir = argv[k + 1]
         del argv[k:k + 2]
     sys.argv[1:] = argv
     fetch_dir, write_dir, calib_dir = sys.argv[1:4]
@@ -74,9 +78,26 @@ def main():
             rec["fp64_flops_per_launch"] = 64.0 * (mean["SQ_INSTS_VALU_ADD_F64"] + mean["SQ_INSTS_VALU_MUL_F64"]
                                                     + 2.0 * mean["SQ_INSTS_VALU_FMA_F64"]
                                                     + mean["SQ_INSTS_VALU_TRANS_F64"])
-    casc = [v for k, v in out["kernels"].items() if "k_cascade" in k]
-    if casc:
-        out["k_cascade_bytes_per_launch"] = casc[0]["hbm_bytes_per_launch"]
+    if mfma_dir:
+        import os
+        names = set()
+        for f in glob.glob(mfma_dir + "/**/*counter_collection.csv", recursive=True):
+            for row in csv.DictReader(open(f)):
+                names.add(row["Counter_Name"])
+        for c in sorted(names):
+            vals = per_kernel(mfma_dir, c)
+            for k, rec in out["kernels"].items():
+                if vals.get(k):
+                    rec.setdefault("mfma_counters_per_launch", {})[c] = sum(vals[k]) / len(vals[k])
+        if not names and not os.path.isdir(mfma_dir):
+            out["mfma_note"] = "no matrix-core pass"
+    # the cascade stage of one step: the sum over its launches (C5 runs the multi-RHS kernel and, for a table's
+    # odd point, the one-point kernel; grouped by kernel name and grid size like the alpha launches)
+    fk, ng = per_step(fetch_dir, "FETCH_SIZE", "nusi::k_cascade")
+    wk, _ = per_step(write_dir, "WRITE_SIZE", "nusi::k_cascade")
+    if ng:
+        out["k_cascade_launches_per_step"] = ng
+        out["k_cascade_bytes_per_launch"] = fk * 1024.0 * fac64 + wk * 1024.0
     fk, ng = per_step(fetch_dir, "FETCH_SIZE", "nusi::k_alpha")   # tiles + the per-entry region
     wk, _ = per_step(write_dir, "WRITE_SIZE", "nusi::k_alpha")
     if ng:
