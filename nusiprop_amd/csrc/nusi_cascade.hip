@@ -1287,13 +1287,6 @@ void k_cascade_wsp(GridDev g, const Point* __restrict__ pts, TablesDev t, double
     constexpr int S3 = 3 * NJ;
     int jb = 0;   // first step slot of the current pass (step i = Nz-1-jb-j for slot j)
     const bool nonres = P.non_resonant;
-    SrcFactors sf[R];   // each point's source factors and kind (the record wave's)
-    bool pl[R];
-#pragma unroll
-    for (int p = 0; p < R; ++p) {
-        sf[p] = src_factors(pts[pid[p]]);
-        pl[p] = pts[pid[p]].source == NUSI_SOURCE_POWER_LAW;
-    }
     auto phase1 = [&](int s2, int jj) {
         const int b = N - 1 - s2 + jj, i = Nz - 1 - jb - jj;
         if (jj < NJ && jb + jj < nst && b >= 0 && b < N) {
@@ -1310,10 +1303,12 @@ void k_cascade_wsp(GridDev g, const Point* __restrict__ pts, TablesDev t, double
             Rw[(FM + 5) * S3] = m.m21;
             Rw[PR_SDE * S3] = nonres ? gl.step_s[i] * rdE[b] : (gl.Emax[b] - gl.Emin[b]);
 #pragma unroll
-            for (int p = 0; p < R; ++p)
+            for (int p = 0; p < R; ++p) {   // (the point's factors per record: hoisted they cost the kernel registers)
+                const Point& Q = pts[pid[p]];
                 Rw[(p == 0 ? PR_SRC : FSRC + p - 1) * S3] =
-                    pl[p] ? powerlaw_src_h(gl, sf[p], pw + p * (T + 2), i, b)
-                          : t.Src[(size_t)pid[p] * T * nst + src_index(Nz, jb + jj, b)];
+                    Q.source == NUSI_SOURCE_POWER_LAW ? powerlaw_src(gl, Q, pw + p * (T + 2), i, b)
+                                                      : t.Src[(size_t)pid[p] * T * nst + src_index(Nz, jb + jj, b)];
+            }
         }
     };
     auto phase2 = [&](int s2, int jj) {
@@ -1355,15 +1350,13 @@ void k_cascade_wsp(GridDev g, const Point* __restrict__ pts, TablesDev t, double
         const bool act = j < NJ && jb + j < nst;
         const double u0 = P.u[0], u1 = P.u[1], u2 = P.u[2];
         const double cj = act ? gl.step_c[Nz - 1 - jb - j] : 0.0, sj = act ? gl.step_s[Nz - 1 - jb - j] : 0.0;
-        // chain state in registers (k_cascade_ws's; it restarts every pass with the pass's steps)
-        double racc[R], px0[R], px1[R], px2[R], Th[R][4];
+        // chain state: F[:, b] is updated in place in LDS (slot j reads slot j-1's solve of the previous stage),
+        // the T_j of the last four stages come from the Tp ring.  (k_cascade_ws keeps both in registers -- a DPP
+        // shift and a per-lane history; here that spilled loop invariants of the chain to scratch and the C3
+        // cascade took 49.7 instead of 38.7 ms, profiles/r3/r3g.)
+        double racc[R], px0[R], px1[R], px2[R];   // resonant-only chain state (per step: restarts every pass)
 #pragma unroll
-        for (int p = 0; p < R; ++p) {
-            racc[p] = px0[p] = px1[p] = px2[p] = 0.0;
-#pragma unroll
-            for (int k = 0; k < 4; ++k) Th[p][k] = 0.0;
-        }
-        const int jl = (nst - jb < NJ ? nst - jb : NJ) - 1;   // the pass's last step slot
+        for (int p = 0; p < R; ++p) racc[p] = px0[p] = px1[p] = px2[p] = 0.0;
         for (int sg0 = 0; sg0 < Ts; sg0 += 4)
 #pragma unroll
         for (int d = 0; d < 4; ++d) {
@@ -1371,17 +1364,6 @@ void k_cascade_wsp(GridDev g, const Point* __restrict__ pts, TablesDev t, double
             if (sg >= Ts) break;
             const int r = c0 - sg;
             const int b = N - 1 - sg + j;
-            // F[:, b] of this step: slot j-1's solve of bin b at stage sg-1; slot 0 reads the previous pass's
-            // last step from LDS (0 in the first pass)
-            double f0[R], f1[R], f2[R];
-#pragma unroll
-            for (int p = 0; p < R; ++p) {
-                const double* Fp = F + 3 * N * p;
-                const bool from_lds = j == 0 && b >= 0 && b < N;
-                f0[p] = wave_shr1(px0[p], from_lds ? Fp[b] : 0.0);
-                f1[p] = wave_shr1(px1[p], from_lds ? Fp[N + b] : 0.0);
-                f2[p] = wave_shr1(px2[p], from_lds ? Fp[2 * N + b] : 0.0);
-            }
             double Tn[R];
 #pragma unroll
             for (int p = 0; p < R; ++p) Tn[p] = 0.0;
@@ -1408,7 +1390,7 @@ void k_cascade_wsp(GridDev g, const Point* __restrict__ pts, TablesDev t, double
                         if (k <= nu) {
                             const double a = sdg[(k - 1) * T + r];
 #pragma unroll
-                            for (int p = 0; p < R; ++p) s[p] = fma(a, Th[p][k - 1], s[p]);
+                            for (int p = 0; p < R; ++p) s[p] = fma(a, Tp[(p * 8 + ((sg - k) & 7)) * NJ + j], s[p]);
                         }
 #pragma unroll
                     for (int p = 0; p < R; ++p) add[p] = cj * s[p];
@@ -1424,20 +1406,14 @@ void k_cascade_wsp(GridDev g, const Point* __restrict__ pts, TablesDev t, double
                     double* Fp = F + 3 * N * p;
                     const double src = Rc[(p == 0 ? PR_SRC : FSRC + p - 1) * S];
                     double x0, x1, x2;
-                    cascade_solve(f0[p], f1[p], f2[p], add[p], src, u0, u1, u2, rz0, rz1, rz2, pmb, l10, l20, l21, u01,
-                                  u02, u12, ru00, ru11, ru22, x0, x1, x2);
-                    if (j == jl) {   // the pass's last step: the next pass's (or the finalisation's) flux
-                        Fp[b] = x0;
-                        Fp[N + b] = x1;
-                        Fp[2 * N + b] = x2;
-                    }
+                    cascade_solve(Fp[b], Fp[N + b], Fp[2 * N + b], add[p], src, u0, u1, u2, rz0, rz1, rz2, pmb, l10,
+                                  l20, l21, u01, u02, u12, ru00, ru11, ru22, x0, x1, x2);
+                    Fp[b] = x0;
+                    Fp[N + b] = x1;
+                    Fp[2 * N + b] = x2;
                     px0[p] = x0; px1[p] = x1; px2[p] = x2;
                     if (nonres && b > 0) Tn[p] = (u0 * x0 + u1 * x1 + u2 * x2) * sde;
                 }
-            }
-#pragma unroll
-            for (int p = 0; p < R; ++p) {
-                Th[p][3] = Th[p][2]; Th[p][2] = Th[p][1]; Th[p][1] = Th[p][0]; Th[p][0] = Tn[p];
             }
             if (act)
 #pragma unroll

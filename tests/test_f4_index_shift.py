@@ -49,3 +49,41 @@ def test_index_shift_reuse_discrepancy(oracle_mod, g, k):
     assert rel_flux < 1e-9                        # inside the north-star bound
     if g >= 0.5:
         assert rel_flux > 1e-12                   # measurably outside the cascade's own rounding
+
+
+def shift_base_zmax(N, lEmin, lEmax, Nz, K):
+    """zmax of the base grid whose redshift axis has Nz + K steps: its table axis is the point's axis extended by K
+    bins on top, bit for bit below (nuSIprop.hpp:113-128, 224-233; the library's NUSI_OPT_SHIFT_REUSE uses the same)."""
+    r = 10 ** ((lEmax - lEmin) / N)
+    return r ** (Nz + K - 1.5) - 1
+
+
+@pytest.mark.parametrize("g,offs", [(0.1, (0, 3, 8)), (0.5, (0, 1, 5))])
+def test_shift_reuse_scheme(oracle_mod, g, offs):
+    """The opt-in scan mode's scheme (NUSI_OPT_SHIFT_REUSE): the tables of the group's largest m_phi on the axis
+    extended by K bins serve every m_phi = m_max r^(-o/2), o <= K, read at offset o.  Fluxes against each point's own
+    evolution <= 1e-9 (the mode's stated bound; the default path stays at FLUX_RTOL)."""
+    base = dict(cases.C2B_100, N_bins_E=100, g=g)
+    K = max(offs)
+    r = 10 ** ((base["lEmax"] - base["lEmin"]) / base["N_bins_E"])
+    mmax = 6e5
+    ob0 = oracle_mod.Oracle(**cases.oracle_kwargs(dict(base, mphi=mmax)))
+    Nz, T = ob0.Nz, ob0.T
+    zb = shift_base_zmax(base["N_bins_E"], base["lEmin"], base["lEmax"], Nz, K)
+    ob = oracle_mod.Oracle(**cases.oracle_kwargs(dict(base, mphi=mmax, zmax=zb)))
+    assert ob.Nz == Nz + K and ob.T == T + K
+    Gb, Ab, alb = ob.tables()
+    worst = 0.0
+    for o in offs:
+        ot = oracle_mod.Oracle(**cases.oracle_kwargs(dict(base, mphi=mmax * r ** (-o / 2))))
+        G, A, al = ot.tables()
+        GS, AS = Gb[o:o + T].copy(), Ab[o:o + T].copy()
+        alS = alb[o:o + T, o:o + T].copy()
+        _, own = ot.cascade(G, A, al)
+        _, sh = ot.cascade(GS, AS, alS)
+        err = cases.rel_err(sh, own)
+        assert err < 1e-9, (o, err)
+        if o == 0:
+            assert err == 0.0   # the base's own tables below T are its tables
+        worst = max(worst, err)
+    assert worst > 0.0

@@ -19,7 +19,7 @@ BUDGET = {
     r"k_cascade_wsILi(16|32)ELi[12]E": (0, 0),
     r"k_cascade_wsILi48ELi1E": (16, 64),     # a few loop-invariant scalars, outside the MFMA loop
     r"k_cascade_wsILi48ELi2E": (0, 0),
-    r"k_cascade_wspILi16E": (24, 192),       # the pivoting-LU fallback's indexed rows, a cold path
+    r"k_cascade_wspILi16E": (20, 96),        # the pivoting-LU fallback's indexed rows, a cold path
     r"k_cascade_wfILi\d+ELb1E": (0, 0),
     r"k_alpha_batchILb[01]E": (64, 1024),      # call frames of the out-of-line per-batch phases
 }
