@@ -39,7 +39,10 @@ def parse():
     ap.add_argument("--gpus", type=int, default=None, help="GPUs = ranks (default: WORLD_SIZE, else 1)")
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--workload", default="c4", choices=["c4", "c5", "c3", "c2", "c1"])
+    ap.add_argument("--workload", default="c4", choices=["c4", "c5", "c3", "c2", "c1", "c4s"],
+                    help="c4s: the opt-in shift-reuse scan mode (NUSI_OPT_SHIFT_REUSE = 128) on a C4-sized scan whose "
+                         "m_phi lie on the table axis' r^(-o/2) lattice; not the headline (its fluxes are held to 1e-9, "
+                         "not bit-exact tables)")
     ap.add_argument("--points", type=int, default=0, help="points per GPU (default: 1024 for c4 and c3, 8192 for c5, 1 for c2)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="budget of the oracle CPU baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -75,6 +78,11 @@ def rank_points(args, rank, world):
         P = args.points or 1024
         pts = scan.c4_points(si=2.5 + 0.05 * rank)
         desc = "C4: (m_phi 32 x g 32) scan per GPU, N_E=300, lE 12->17, power-law source, gamma=2.5+0.05*rank"
+    elif args.workload == "c4s":
+        P = args.points or 1024
+        pts = scan.c4s_points(si=2.5 + 0.05 * rank)
+        desc = ("C4s (opt-in NUSI_OPT_SHIFT_REUSE=128): (m_phi 32 on the r^(-o/2) lattice, o = 0, 4, .., 124 below "
+                "10^6.533 x g 32) scan per GPU, N_E=300, lE 12->17, power-law source; one base table set per g")
     else:
         P = args.points or 8192
         allp = scan.c5_points()
@@ -318,6 +326,8 @@ def main():
         shutil.rmtree(tdir, ignore_errors=True)
     arr = plan.params_array(pts)
     plan.set_cascade({"mfma": _lib.CASCADE_MFMA, "wf": _lib.CASCADE_WAVEFRONT, "auto": _lib.CASCADE_AUTO}[args.cascade])
+    if args.workload == "c4s":
+        plan.set_option(_lib.OPT_SHIFT_REUSE, 128)
     dev = torch.device("cuda", local)
     flux = torch.empty((P, 3, plan.N), dtype=torch.float64, device=dev)
     fla = torch.empty((P, 3, plan.N), dtype=torch.float64, device=dev)

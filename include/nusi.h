@@ -174,11 +174,27 @@ int nusi_plan_set_cascade(nusi_plan *plan, int kind);
  *   NUSI_OPT_CASCADE_RHS   max points sharing a table per MFMA-cascade
  *                          workgroup: 0 = automatic, 1 = one point each
  *   NUSI_OPT_STEP_PASSES   0 = automatic (step passes beyond 48 redshift
- *                          steps), 1 = always the step-pass kernel */
+ *                          steps), 1 = always the step-pass kernel
+ *   NUSI_OPT_SHIFT_REUSE   opt-in scan mode, K in
+ *                          [0, 128]; 0 = off (default).  alpha / Gamma /
+ *                          alphaTilde see the energies only through
+ *                          2 m_k E / m_phi^2 (nuSIprop.hpp:1253-1256), so the
+ *                          tables of m_phi' = m_phi r^(-o/2) (r = Emax[0] /
+ *                          Emin[0], integer o) equal those of m_phi read o
+ *                          bins higher.  Tables of one (g, masses, flags)
+ *                          whose m_phi lie on that lattice within K bins of
+ *                          the largest are served by ONE table set of the
+ *                          largest m_phi on the axis extended by K bins.  Not
+ *                          bit-exact: the bin edges round differently, and
+ *                          the fluxes move by <= 1e-9 relative on the tested
+ *                          cases (tests/test_f4_index_shift.py, GPU:
+ *                          test_shift_reuse_scan); the default path is
+ *                          unchanged. */
 #define NUSI_OPT_ALPHA_BATCH 1
 #define NUSI_OPT_ALPHA_KERNEL 2
 #define NUSI_OPT_CASCADE_RHS 3
 #define NUSI_OPT_STEP_PASSES 4
+#define NUSI_OPT_SHIFT_REUSE 5
 int nusi_plan_set_option(nusi_plan *plan, int option, int value);
 /* per-point NUSI_WARN_* bits of the last call */
 int nusi_plan_warnings(nusi_plan *plan, int *out, int n);

@@ -56,7 +56,7 @@ EXPORTS = [
 
 # nusi_plan_set_cascade kinds and nusi_plan_set_option options (include/nusi.h)
 CASCADE_AUTO, CASCADE_WAVEFRONT, CASCADE_REG, CASCADE_LDS, CASCADE_MFMA = 0, 1, 2, 3, 4
-OPT_ALPHA_BATCH, OPT_ALPHA_KERNEL, OPT_CASCADE_RHS, OPT_STEP_PASSES = 1, 2, 3, 4
+OPT_ALPHA_BATCH, OPT_ALPHA_KERNEL, OPT_CASCADE_RHS, OPT_STEP_PASSES, OPT_SHIFT_REUSE = 1, 2, 3, 4, 5
 
 _lib = None
 

@@ -394,6 +394,11 @@ int load_spline(const char* path, int ndim, const int* dims, SplineStore& st, nu
 // ---------------------------------------------------------------------------
 // plan
 // ---------------------------------------------------------------------------
+// the alpha-table batches of one call (nusi::launch_alpha): count, how many lack the phi-phi channel, the cap
+struct AlphaBatches {
+    int nbatch = 0, nb_plain = 0, cap = 1;
+};
+
 struct nusi_plan {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -413,6 +418,11 @@ struct nusi_plan {
     int alpha_kind = 0;             // NUSI_OPT_ALPHA_KERNEL: 0 k_alpha_batch, 1 k_alpha_tile<G> (<= 4), 2 per entry
     int cascade_rhs = 0;            // NUSI_OPT_CASCADE_RHS: 0 = auto, 1 = one point per MFMA-cascade workgroup
     int step_passes = 0;            // NUSI_OPT_STEP_PASSES: 1 = the step-pass cascade also where one pass fits
+    int shift_max = 0;              // NUSI_OPT_SHIFT_REUSE: K, the largest bin offset served by a base table set
+    nusi_plan* shift = nullptr;     // ... its plan: the same grid with K more redshift steps (axis T + K)
+    int2* d_smap = nullptr;         // per shifted table: base index in `shift`, bin offset
+    int2* h_smap = nullptr;         // pinned
+    AlphaBatches shift_batches;     // the base plan's alpha batches of the last call
     double* d_src = nullptr;        // DSNB source terms of the MFMA cascade [src_cap][cascade_src_doubles]
     int src_cap = 0;
     std::vector<int> slot_of;       // table slot of each point of the last call
@@ -506,6 +516,167 @@ int build_point(nusi_plan* pl, const nusi_params& p, nusi::Point& P)
     return NUSI_OK;
 }
 
+
+// Order the tables h_tpts[0, ntab) so that those sharing m_phi, the masses and the flags -- whose alpha tables
+// share every leaf of (S', t) alone -- are neighbours (slots renumbered; perm[old] = new), and cut them into the
+// batches h_batches.
+AlphaBatches alpha_batches(nusi_plan* pl, int ntab, std::vector<int>& perm)
+{
+    AlphaBatches ab;
+    std::vector<int> order(ntab);
+    perm.assign(ntab, 0);
+    for (int j = 0; j < ntab; ++j) order[j] = j;
+    auto bkey = [&](int j) {
+        const nusi::Point& P = pl->h_tpts[j];
+        // phi-phi first: the tables with the channel come last (their batches run on their own launch)
+        return std::make_tuple(P.phiphi && P.non_resonant, P.mphi, P.mn[0], P.mn[1], P.mn[2], P.majorana, P.non_resonant,
+                               P.phiphi);
+    };
+    std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return bkey(a) < bkey(b); });
+    {
+        std::vector<nusi::Point> tmp(pl->h_tpts, pl->h_tpts + ntab);
+        for (int j = 0; j < ntab; ++j) {
+            pl->h_tpts[j] = tmp[order[j]];
+            perm[order[j]] = j;
+        }
+    }
+    for (int j = 0; j < ntab; ++j) pl->h_tpts[j].tslot = j;
+    // batch cap: the tile kernel's LDS holds <= 4 (3 measured best); the big-batch kernel shares the leaves of
+    // any number, but one workgroup runs a batch's points one after the other, so the cap keeps ~2 rounds of
+    // workgroups per CU slot (256 CUs x 3) in the grid: ntab x class-0 tiles / cap >= 1536
+    int cap = pl->alpha_kind == 1 ? std::min(pl->alpha_batch, 4) : pl->alpha_batch;
+    if (cap <= 0) {
+        if (pl->alpha_kind == 1) cap = 3;
+        else {
+            const long long work = (long long)ntab * std::max(1, pl->atiles.ncls[0]);
+            cap = (int)std::max(1LL, std::min(64LL, (work + 1535) / 1536));
+        }
+    }
+    ab.cap = cap;
+    for (int j = 0; j < ntab;) {
+        int run = 1;   // the group of tables sharing bkey, split into near-equal batches of <= cap
+        while (j + run < ntab && bkey(j + run) == bkey(j)) ++run;
+        const int nb = (run + cap - 1) / cap;
+        for (int b = 0; b < nb; ++b) {
+            const int lo = j + (int)((long long)run * b / nb), hi = j + (int)((long long)run * (b + 1) / nb);
+            pl->h_batches[ab.nbatch++] = lo | ((hi - lo) << 24);
+        }
+        j += run;
+    }
+    while (ab.nb_plain < ab.nbatch) {   // batches without the phi-phi channel (sorted first by bkey)
+        const nusi::Point& F = pl->h_tpts[pl->h_batches[ab.nb_plain] & 0xffffff];
+        if (F.phiphi && F.non_resonant) break;
+        ++ab.nb_plain;
+    }
+    return ab;
+}
+
+// NUSI_OPT_SHIFT_REUSE.  alpha / Gamma / alphaTilde see the energies only through
+// 2 m_k E / m_phi^2 (nuSIprop.hpp:1253-1256) and g through g^4 and Gamma_phi / m_phi = g^2 / 16 pi, so the tables of
+// m_phi' = m_phi r^(-o/2) (r = Emax[0] / Emin[0] = the table axis' bin ratio) are those of m_phi read o bins higher.
+// Tables of one (g, masses, |U|^2, flags) are taken in decreasing m_phi: each group starts at its largest m_phi
+// (the base) and takes the following ones whose offset o = 2 ln(m_base / m_phi) / ln r is an integer (to 1e-6) in
+// [1, K].  Groups of two or more go to slots [nd, ntab) in group order (remap[old slot] = new slot; smap[slot - nd]
+// = (base index, o); bases[] = the base Points); the rest stay in [0, nd).  Returns nd.
+int shift_groups(nusi_plan* pl, int ntab, std::vector<int>& remap, std::vector<int2>& smap, std::vector<nusi::Point>& bases)
+{
+    const double lr = log(pl->grid.Emax[0] / pl->grid.Emin[0]);
+    const int K = pl->shift_max;
+    const nusi::Point* tp = pl->h_tpts;
+    auto gkey = [&](int j) {
+        const nusi::Point& P = tp[j];
+        return std::make_tuple(P.g, P.mn[0], P.mn[1], P.mn[2], P.u[0], P.u[1], P.u[2], P.majorana, P.non_resonant,
+                               P.phiphi);
+    };
+    std::vector<int> idx(ntab);
+    for (int j = 0; j < ntab; ++j) idx[j] = j;
+    std::stable_sort(idx.begin(), idx.end(), [&](int a, int b) {
+        const auto ka = gkey(a), kb = gkey(b);
+        return ka != kb ? ka < kb : tp[a].mphi > tp[b].mphi;
+    });
+    std::vector<int> grp(ntab, -1), off(ntab, 0);
+    std::vector<std::vector<int>> members;
+    for (int a = 0; a < ntab;) {
+        int b = a + 1;
+        while (b < ntab && gkey(idx[b]) == gkey(idx[a])) ++b;
+        std::vector<int> cur{idx[a]};
+        int last = 0;
+        for (int c = a + 1; c <= b; ++c) {
+            bool join = false;
+            int o = 0;
+            if (c < b) {
+                const double kf = 2.0 * log(tp[cur[0]].mphi / tp[idx[c]].mphi) / lr;
+                o = (int)lround(kf);
+                join = o > last && o <= K && fabs(kf - o) < 1e-6;
+            }
+            if (join) {
+                cur.push_back(idx[c]);
+                off[idx[c]] = last = o;
+                continue;
+            }
+            if (cur.size() >= 2) {
+                for (int m : cur) grp[m] = (int)members.size();
+                members.push_back(cur);
+            }
+            if (c < b) {
+                cur.assign(1, idx[c]);
+                off[idx[c]] = last = 0;
+            }
+        }
+        a = b;
+    }
+    remap.assign(ntab, 0);
+    int nd = 0;
+    for (int j = 0; j < ntab; ++j)
+        if (grp[j] < 0) remap[j] = nd++;
+    int s = nd;
+    smap.clear();
+    bases.clear();
+    for (size_t g = 0; g < members.size(); ++g) {
+        bases.push_back(tp[members[g][0]]);
+        for (int m : members[g]) {
+            remap[m] = s++;
+            smap.push_back(make_int2((int)g, off[m]));
+        }
+    }
+    return nd;
+}
+
+// the base plan of NUSI_OPT_SHIFT_REUSE: the plan's grid with K more redshift steps, so that its table axis is
+// the plan's, bit for bit, extended by K bins on top (nuSIprop.hpp:224-233: bins >= N are Emin/Emax[N-1] (1 + z));
+// it holds up to max_points / 2 base tables (a base serves >= 2 tables)
+int ensure_shift_plan(nusi_plan* pl)
+{
+    const int K = pl->shift_max;
+    if (pl->shift && pl->shift->grid.T == pl->grid.T + K) return NUSI_OK;
+    if (pl->shift) {
+        nusi_plan_destroy(pl->shift);
+        pl->shift = nullptr;
+    }
+    const HostGrid& G = pl->grid;
+    const double r = G.Emax[0] / G.Emin[0];
+    const double zb = pow(r, G.Nz + K - 1.5) - 1;   // N_steps_z = (int)(ln(1 + zb) / ln r + 2) = Nz + K
+    nusi_plan* sp = nullptr;
+    int rc = nusi_plan_create(pl->device, G.N, G.lEmin, G.lEmax, zb, std::max(1, pl->max_points / 2), &sp);
+    if (rc) return rc;
+    const HostGrid& B = sp->grid;
+    bool same = B.T == G.T + K;
+    for (int n = 0; same && n < G.T; ++n) same = B.lo[n] == G.lo[n] && B.hi[n] == G.hi[n];
+    if (!same) {
+        nusi_plan_destroy(sp);
+        return fail(NUSI_EPARAM, "shift reuse: the extended axis does not match the plan's below T");
+    }
+    sp->alpha_batch = pl->alpha_batch;
+    sp->alpha_kind = pl->alpha_kind;
+    sp->spl = pl->spl;
+    HIPCHECK(hipSetDevice(pl->device));
+    if (!pl->d_smap) {
+        HIPCHECK(hipMalloc(&pl->d_smap, sizeof(int2) * pl->max_points));
+        HIPCHECK(hipHostMalloc((void**)&pl->h_smap, sizeof(int2) * pl->max_points, hipHostMallocDefault));
+    }
+    pl->shift = sp;
+    return NUSI_OK;
+}
 }  // namespace
 
 extern "C" {
@@ -564,13 +735,17 @@ void nusi_plan_destroy(nusi_plan* pl)
     hipFree(pl->tabs.A);
     hipFree(pl->tabs.Med);
     hipFree(pl->d_src);
+    hipFree(pl->d_smap);
+    if (pl->h_smap) hipHostFree(pl->h_smap);
     nusi::alpha_tiles_destroy(&pl->atiles);
     hipFree(pl->d_scratch);
     if (pl->h_pts) hipHostFree(pl->h_pts);
     if (pl->stream) hipStreamDestroy(pl->stream);
     pl->spl.reset();
+    nusi_plan* sh = pl->shift;
     hipSetDevice(prev);
     delete pl;
+    nusi_plan_destroy(sh);
 }
 
 int nusi_plan_create(int device, int N_bins_E, double lEmin, double lEmax, double zmax, int max_points, nusi_plan** out)
@@ -724,54 +899,45 @@ int nusi_plan_evolve(nusi_plan* pl, const nusi_params* pts, int n, double* d_flu
         P.tslot = it->second;
         pl->slot_of[i] = it->second;
     }
-    // order the tables so that those sharing m_phi, the masses and the flags -- whose alpha tables
-    // share every leaf of (S', t) alone -- are neighbours, and cut them into batches
-    std::vector<int> order(ntab), perm(ntab);
-    for (int j = 0; j < ntab; ++j) order[j] = j;
-    auto bkey = [&](int j) {
-        const nusi::Point& P = pl->h_tpts[j];
-        // phi-phi first: the tables with the channel come last (their batches run on their own launch)
-        return std::make_tuple(P.phiphi && P.non_resonant, P.mphi, P.mn[0], P.mn[1], P.mn[2], P.majorana, P.non_resonant,
-                               P.phiphi);
-    };
-    std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return bkey(a) < bkey(b); });
-    {
-        std::vector<nusi::Point> tmp(pl->h_tpts, pl->h_tpts + ntab);
-        for (int j = 0; j < ntab; ++j) {
-            pl->h_tpts[j] = tmp[order[j]];
-            perm[order[j]] = j;
+    // NUSI_OPT_SHIFT_REUSE (opt-in): the tables a shifted base set serves go to the slots
+    // [nd, ntab) (filled by k_table_shift), the others are built directly in [0, nd)
+    int nd = ntab, nbase = 0;
+    if (pl->shift_max > 0) {
+        std::vector<int> remap;
+        std::vector<nusi::Point> bases;
+        std::vector<int2> smap;
+        nd = shift_groups(pl, ntab, remap, smap, bases);
+        nbase = (int)bases.size();
+        if (nbase) {
+            const int r = ensure_shift_plan(pl);
+            if (r) return r;
+            if (nbase > pl->shift->max_points) return fail(NUSI_EPARAM, "shift reuse: more base tables than the base plan holds");
+            std::vector<nusi::Point> tmp(pl->h_tpts, pl->h_tpts + ntab);
+            for (int j = 0; j < ntab; ++j) pl->h_tpts[remap[j]] = tmp[j];
+            for (int j = 0; j < ntab; ++j) pl->h_tpts[j].tslot = j;
+            for (int i = 0; i < n; ++i) pl->h_pts[i].tslot = pl->slot_of[i] = remap[pl->slot_of[i]];
+            // the base plan's tables, ordered and batched like any others (their slots move: remap the map)
+            nusi_plan* sp = pl->shift;
+            sp->spl = pl->spl;   // (the phi-phi set may have been loaded after the base plan was made)
+            if (sp->ran) HIPCHECK(hipEventSynchronize(sp->ev_copy));
+            for (int b = 0; b < nbase; ++b) {
+                sp->h_tpts[b] = bases[b];
+                sp->h_tpts[b].tslot = b;
+            }
+            std::vector<int> bperm;
+            const AlphaBatches bb = alpha_batches(sp, nbase, bperm);
+            for (int q = 0; q < ntab - nd; ++q) pl->h_smap[q] = make_int2(bperm[smap[q].x], smap[q].y);
+            pl->shift_batches = bb;
         }
+        if (!nbase) nd = ntab;
     }
-    for (int i = 0; i < n; ++i) pl->h_pts[i].tslot = pl->slot_of[i] = perm[pl->slot_of[i]];
-    for (int j = 0; j < ntab; ++j) pl->h_tpts[j].tslot = j;
-    // batch cap: the tile kernel's LDS holds <= 4 (3 measured best); the big-batch kernel shares the leaves of
-    // any number, but one workgroup runs a batch's points one after the other, so the cap keeps ~2 rounds of
-    // workgroups per CU slot (256 CUs x 3) in the grid: ntab x class-0 tiles / cap >= 1536
-    int cap = pl->alpha_kind == 1 ? std::min(pl->alpha_batch, 4) : pl->alpha_batch;
-    if (cap <= 0) {
-        if (pl->alpha_kind == 1) cap = 3;
-        else {
-            const long long work = (long long)ntab * std::max(1, pl->atiles.ncls[0]);
-            cap = (int)std::max(1LL, std::min(64LL, (work + 1535) / 1536));
-        }
-    }
-    int nbatch = 0;
-    for (int j = 0; j < ntab;) {
-        int run = 1;   // the group of tables sharing bkey, split into near-equal batches of <= cap
-        while (j + run < ntab && bkey(j + run) == bkey(j)) ++run;
-        const int nb = (run + cap - 1) / cap;
-        for (int b = 0; b < nb; ++b) {
-            const int lo = j + (int)((long long)run * b / nb), hi = j + (int)((long long)run * (b + 1) / nb);
-            pl->h_batches[nbatch++] = lo | ((hi - lo) << 24);
-        }
-        j += run;
-    }
-    int nb_plain = 0;   // batches without the phi-phi channel (sorted first by bkey)
-    while (nb_plain < nbatch) {
-        const nusi::Point& F = pl->h_tpts[pl->h_batches[nb_plain] & 0xffffff];
-        if (F.phiphi && F.non_resonant) break;
-        ++nb_plain;
-    }
+    // the directly built tables, ordered so that those sharing m_phi, the masses and the flags -- whose alpha
+    // tables share every leaf of (S', t) alone -- are neighbours, and cut into batches
+    std::vector<int> perm;
+    const AlphaBatches ab = alpha_batches(pl, nd, perm);
+    for (int i = 0; i < n; ++i)
+        if (pl->slot_of[i] < nd) pl->h_pts[i].tslot = pl->slot_of[i] = perm[pl->slot_of[i]];
+    const int cap = ab.cap, nbatch = ab.nbatch, nb_plain = ab.nb_plain;
     const size_t N3 = (size_t)3 * pl->grid.N;
     if (!d_flux || !d_fla) {
         if (!pl->d_scratch) HIPCHECK(hipMalloc(&pl->d_scratch, sizeof(double) * 2 * N3 * pl->max_points));
@@ -812,17 +978,36 @@ int nusi_plan_evolve(nusi_plan* pl, const nusi_params* pts, int n, double* d_flu
     if (ngroups) HIPCHECK(hipMemcpyAsync(pl->d_groups, pl->h_groups, sizeof(int2) * ngroups, hipMemcpyHostToDevice, s));
     HIPCHECK(hipMemcpyAsync(pl->d_pts, pl->h_pts, sizeof(nusi::Point) * n, hipMemcpyHostToDevice, s));
     HIPCHECK(hipMemcpyAsync(pl->d_tpts, pl->h_tpts, sizeof(nusi::Point) * ntab, hipMemcpyHostToDevice, s));
-    HIPCHECK(hipMemcpyAsync(pl->d_batches, pl->h_batches, sizeof(int) * nbatch, hipMemcpyHostToDevice, s));
+    if (nbatch) HIPCHECK(hipMemcpyAsync(pl->d_batches, pl->h_batches, sizeof(int) * nbatch, hipMemcpyHostToDevice, s));
+    nusi_plan* sp = nbase ? pl->shift : nullptr;
+    if (sp) {
+        HIPCHECK(hipMemcpyAsync(pl->d_smap, pl->h_smap, sizeof(int2) * (ntab - nd), hipMemcpyHostToDevice, s));
+        HIPCHECK(hipMemcpyAsync(sp->d_tpts, sp->h_tpts, sizeof(nusi::Point) * nbase, hipMemcpyHostToDevice, s));
+        HIPCHECK(hipMemcpyAsync(sp->d_batches, sp->h_batches, sizeof(int) * pl->shift_batches.nbatch,
+                                hipMemcpyHostToDevice, s));
+        HIPCHECK(hipEventRecord(sp->ev_copy, s));
+        HIPCHECK(hipMemsetAsync(sp->d_warn, 0, sizeof(int) * nbase, s));
+        sp->ran = true;
+    }
     HIPCHECK(hipEventRecord(pl->ev_copy, s));
     HIPCHECK(hipMemsetAsync(pl->d_warn, 0, sizeof(int) * ntab, s));
     const nusi::SplineSet spl = pl->spl ? pl->spl->set : nusi::SplineSet{};
     hipEvent_t* ev = pl->ev;
     if (pl->prof_n < pl->prof_max) ev = &pl->prof_ev[4 * (size_t)pl->prof_n++];
     HIPCHECK(hipEventRecord(ev[0], s));
-    HIPCHECK(nusi::launch_gamma_alphat(pl->gd, pl->d_tpts, ntab, spl, pl->tabs, pl->d_warn, s));
+    if (nd) HIPCHECK(nusi::launch_gamma_alphat(pl->gd, pl->d_tpts, nd, spl, pl->tabs, pl->d_warn, s));
+    if (sp) HIPCHECK(nusi::launch_gamma_alphat(sp->gd, sp->d_tpts, nbase, spl, sp->tabs, sp->d_warn, s));
     HIPCHECK(hipEventRecord(ev[1], s));
-    HIPCHECK(nusi::launch_alpha(pl->gd, pl->d_tpts, ntab, spl, pl->atiles, pl->tabs, pl->d_warn, s, pl->d_batches,
-                                nbatch, cap, pl->alpha_kind, nb_plain));
+    if (nd)
+        HIPCHECK(nusi::launch_alpha(pl->gd, pl->d_tpts, nd, spl, pl->atiles, pl->tabs, pl->d_warn, s, pl->d_batches,
+                                    nbatch, cap, pl->alpha_kind, nb_plain));
+    if (sp) {
+        const AlphaBatches& bb = pl->shift_batches;
+        HIPCHECK(nusi::launch_alpha(sp->gd, sp->d_tpts, nbase, spl, sp->atiles, sp->tabs, sp->d_warn, s, sp->d_batches,
+                                    bb.nbatch, bb.cap, sp->alpha_kind, bb.nb_plain));
+        HIPCHECK(nusi::launch_table_shift(pl->gd, sp->gd, pl->d_smap, nd, ntab - nd, sp->tabs, sp->d_warn, pl->tabs,
+                                          pl->d_warn, s));
+    }
     HIPCHECK(hipEventRecord(ev[2], s));
     if (fast && any_dsnb) HIPCHECK(nusi::launch_source_dsnb(pl->gd, pl->d_pts, n, pl->d_src, s));
     if (fast && ngroups)
@@ -837,6 +1022,7 @@ int nusi_plan_evolve(nusi_plan* pl, const nusi_params* pts, int n, double* d_flu
     HIPCHECK(hipEventRecord(ev[3], s));
     HIPCHECK(hipEventRecord(pl->ev_done, s));
     pl->alpha_kernel = nusi::last_alpha_kernel();
+    if (sp) pl->alpha_kernel = nd ? "k_alpha_batch + k_table_shift" : "k_alpha_batch (shift base) + k_table_shift";
     pl->cascade_kernel = nusi::last_cascade_kernel();
     for (int k = 0; k < 4; ++k) pl->last_ev[k] = ev[k];   // stage_ms / warnings / tables refer to the latest call
     pl->ran = true;
@@ -914,6 +1100,18 @@ int nusi_plan_set_option(nusi_plan* pl, int option, int value)
     case NUSI_OPT_STEP_PASSES:
         if (value < 0 || value > 1) return fail(NUSI_EPARAM, "NUSI_OPT_STEP_PASSES outside [0, 1]");
         pl->step_passes = value;
+        return NUSI_OK;
+    case NUSI_OPT_SHIFT_REUSE:
+        if (value < 0 || value > 128) return fail(NUSI_EPARAM, "NUSI_OPT_SHIFT_REUSE outside [0, 128]");
+        if (value != pl->shift_max && pl->shift) {   // the base plan's axis follows K
+            if (pl->ran) {
+                HIPCHECK(hipSetDevice(pl->device));
+                HIPCHECK(hipEventSynchronize(pl->ev_done));
+            }
+            nusi_plan_destroy(pl->shift);
+            pl->shift = nullptr;
+        }
+        pl->shift_max = value;
         return NUSI_OK;
     default:
         return fail(NUSI_EPARAM, "unknown plan option");

@@ -839,7 +839,7 @@ template <> struct WsCfg<2> { static constexpr int RT = 2, kMaxThreads = 832 + 6
 // cycles).  nusi_debug_ws_trace() copies them out.  Compiled out of the product.
 #ifdef NUSI_WS_TRACE
 constexpr int kTrWaves = 16, kTrStages = 512, kTrBlocks = 8192;
-__device__ unsigned long long g_ws_trace[kTrWaves * kTrStages * 2];
+__device__ unsigned long long g_ws_trace[kTrWaves * kTrStages * 4];   // [wave][stage][start, barrier, chain: loaded, solved]
 __device__ unsigned int g_ws_hwid[kTrBlocks * kTrWaves];   // HW_ID (SE, CU, SIMD, wave slot) of every wave
 #define NUSI_WS_HWID()                                                                                             \
     do {                                                                                                           \
@@ -848,8 +848,9 @@ __device__ unsigned int g_ws_hwid[kTrBlocks * kTrWaves];   // HW_ID (SE, CU, SIM
     } while (0)
 #define NUSI_WS_STAMP(sg, which)                                                                                   \
     do {                                                                                                           \
+        if (which >= 2) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");                               \
         if (blockIdx.x == 0 && (threadIdx.x & 63) == 0 && (sg) < kTrStages)                                        \
-            g_ws_trace[((threadIdx.x >> 6) * kTrStages + (sg)) * 2 + (which)] = __builtin_amdgcn_s_memtime();        \
+            g_ws_trace[((threadIdx.x >> 6) * kTrStages + (sg)) * 4 + (which)] = __builtin_amdgcn_s_memtime();        \
     } while (0)
 #else
 #define NUSI_WS_STAMP(sg, which) do { } while (0)
@@ -1061,6 +1062,7 @@ void k_cascade_ws(GridDev g, const Point* __restrict__ pts, const int2* __restri
                         add[p] = resonant_add(racc[p], u0, u1, u2, px0[p], px1[p], px2[p], sj, sdg[r], dEb1, sde, cj,
                                               b == N - 1);
                 }
+                NUSI_WS_STAMP(sg, 2);
 #pragma unroll
                 for (int p = 0; p < R; ++p) {
                     double* Fp = F + 3 * N * p;
@@ -1076,6 +1078,7 @@ void k_cascade_ws(GridDev g, const Point* __restrict__ pts, const int2* __restri
                     if (nonres && b > 0) Tn[p] = (u0 * x0 + u1 * x1 + u2 * x2) * sde;
                 }
             }
+            NUSI_WS_STAMP(sg, 3);
 #pragma unroll
             for (int p = 0; p < R; ++p) {
                 Th[p][3] = Th[p][2]; Th[p][2] = Th[p][1]; Th[p][1] = Th[p][0]; Th[p][0] = Tn[p];
@@ -1522,6 +1525,339 @@ void k_cascade_wsp(GridDev g, const Point* __restrict__ pts, TablesDev t, double
     }
 }
 
+// ---------------------------------------------------------------------------
+// k_cascade_gb: the gamma batch -- the north star's transfer-matrix x flux-batch GEMM at full batch width
+// (SURVEY.md sec. 7 K_B').  For fixed tables the cascade is linear in the source, and the source is the only
+// input that depends on gamma (Lum enters through src alone, nuSIprop.hpp:283; the power law :656): the up to 16
+// points of a table slot (C5: the 16 gamma of one (m_phi, g)) share one triangular operator.  One workgroup takes
+// all of them, gamma on the N dimension of v_mfma_f64_16x16x4f64:
+//     ACC_j[16 rows, 16 gamma] += alpha[16 rows, 4 columns] . T_j[4 columns, 16 gamma]     (per row tile, step j)
+// so each alpha block is loaded once for every point, and the records (1/Z, M and its LU, nuSIprop.hpp:289-310)
+// are formed once per (step, bin) for all of them.  The accumulator state is rows x steps x gamma, so the steps
+// are taken kGbNJ = 6 at a time, k_cascade_wsp's passes: 6 x 16 = 96 columns per CU, as the R = 2 kernel's 2 x 48.
+//   * push waves: 16 kGbRT rows each, acc[RT][NJ] tiles, the block pushes of k_cascade_ws at stages 4q;
+//   * two chain waves, lane = 3 p + jj (point p < 16, step jj of the wave's three): step j hands its solve to
+//     j + 1 by a wave shift (DPP), across the two waves through LDS (hb), and across passes through a global FIFO
+//     of the last step's F[:, b] (fh, loaded with non-temporal loads four stages ahead);
+//   * the record wave: phase 1 / phase 2 of the records two / one stage ahead (6 lanes), and per point the power
+//     law's pw at the stage's lower table edge (one exp per point and stage: along a stage b + i is constant, so
+//     every step of the stage reads the same two edges; exp(-si log x) = nm::pow, the same bits as pw[]).
+// Power-law points only (the DSNB source does not depend on gamma).  The solves and pushes are k_cascade_ws's
+// operations on the same operands, so the fluxes agree with it to rounding (the MFMA sums a block in its own
+// order; tests: test_cascade_gamma_batch, FLUX_RTOL against the oracle and the R = 1 kernel).
+// ---------------------------------------------------------------------------
+constexpr int kGbNJ = 6, kGbRT = 2, kGbSPW = 3, kGbChainWaves = kGbNJ / kGbSPW;
+constexpr int kGbNF = kWfFields + 6;   // record fields + the phase-1 M entries
+static_assert(kGbNJ % kGbSPW == 0 && 16 * kGbSPW <= 64, "chain lanes");
+
+template <int NJ>
+__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4, 4)))
+void k_cascade_gb(GridDev g, const Point* __restrict__ pts, const int* __restrict__ gidx, const int2* __restrict__ grp,
+                  TablesDev t, double* __restrict__ fh, double* __restrict__ flux, double* __restrict__ flux_fla)
+{
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    constexpr int RT = kGbRT, NF = kGbNF, FM = kWfFields, S3 = 3 * NJ;
+    const int N = g.N, Nz = g.Nz, T = g.T, nst = Nz - 1;
+    const int tid = threadIdx.x, nthr = blockDim.x, lane = tid & 63, wave = tid >> 6, nw = nthr >> 6;
+    const int nwp = nw - kGbChainWaves - 1, recw = nw - 1;   // push waves, then the chain waves, then the record wave
+    const int2 gr = grp[blockIdx.x];
+    const int R = gr.y;                                      // points of this workgroup (<= 16), one table
+    const Point& P = pts[gidx[gr.x]];
+    double* rec = lds;                       // [3][NF][NJ]     records of stage s in slot s % 3
+    double* pwr = rec + 3 * NF * NJ;         // [4][16]         each point's pw at the lower edge of stage s (slot s & 3)
+    double* Tp = pwr + 64;                   // [8][NJ][16]     T_j of each point by stage
+    double* AX = Tp + 8 * NJ * 16;           // [2][4][NJ][16]  rows published by block q (parity q & 1)
+    double* hb = AX + 8 * NJ * 16;           // [2][3][16]      chain wave 0's top step -> wave 1 (stage parity)
+    double* rdE = hb + 96;                   // [N]
+    double* lx = rdE + N;                    // [T + 2]         log of the power law's argument on table edge e
+    double* sGt = lx + T + 2;
+    double* sAt = sGt + T;
+    double* sdg = sAt + T;                   // [4][T]: alpha(n, n+k), k = 1..4 (0 past the table)
+    double* sEmin = sdg + 4 * T;
+    double* sEmax = sEmin + N;
+    double* sgz = sEmax + N;                 // z, step_c, step_s, sfr [Nz each]
+    GridDev gl = g;
+    gl.Emin = sEmin;
+    gl.Emax = sEmax;
+    gl.z = sgz;
+    gl.step_c = sgz + Nz;
+    gl.step_s = sgz + 2 * Nz;
+    gl.sfr = sgz + 3 * Nz;
+    const double* __restrict__ Al = t.A + (size_t)P.tslot * g.PT;
+    {
+        const double* __restrict__ Gt = t.G + (size_t)P.tslot * T;
+        const double* __restrict__ At = t.At + (size_t)P.tslot * T;
+        for (int n = tid; n < T; n += nthr) {
+            sGt[n] = Gt[n];
+            sAt[n] = At[n];
+#pragma unroll
+            for (int k = 1; k <= 4; ++k) sdg[(k - 1) * T + n] = (n + k < T) ? Al[(size_t)(n + k) * (n + k - 1) / 2 + n] : 0.0;
+        }
+        for (int b = tid; b < N; b += nthr) {
+            sEmin[b] = g.Emin[b];
+            sEmax[b] = g.Emax[b];
+            rdE[b] = 1.0 / (g.Emax[b] - g.Emin[b]);   // cascade_aux_init's expression
+        }
+        for (int i = tid; i < Nz; i += nthr) {
+            sgz[i] = g.z[i];
+            sgz[Nz + i] = g.step_c[i];
+            sgz[2 * Nz + i] = g.step_s[i];
+            sgz[3 * Nz + i] = g.sfr[i];
+        }
+        for (int e = tid + 1; e <= T + 1; e += nthr) {   // cascade_aux_init's argument of pw[e]: pow = exp(y log x)
+            const int i = min(Nz - 1, max(1, e - N + 1)), b = e - i;
+            const double E = (b < N) ? g.Emin[b] : g.Emax[N - 1];
+            lx[e] = nm::log(E / 1e14 * (1 + g.z[i]));
+        }
+    }
+    const bool nonres = P.non_resonant;
+    int jb = 0;   // first step slot of the current pass (step i = Nz-1-jb-j for slot j)
+    auto phase1 = [&](int s2, int jj) {
+        const int b = N - 1 - s2 + jj, i = Nz - 1 - jb - jj;
+        if (jj < NJ && jb + jj < nst && b >= 0 && b < N) {
+            double* Rw = rec + (s2 % 3) * NJ + jj;
+            const RecM m = record_phase1(gl, P, sGt, sAt, rdE, i, b);
+            Rw[PR_RZ0 * S3] = m.rz0;
+            Rw[PR_RZ1 * S3] = m.rz1;
+            Rw[PR_RZ2 * S3] = m.rz2;
+            Rw[(FM + 0) * S3] = m.m01;
+            Rw[(FM + 1) * S3] = m.m02;
+            Rw[(FM + 2) * S3] = m.m10;
+            Rw[(FM + 3) * S3] = m.m12;
+            Rw[(FM + 4) * S3] = m.m20;
+            Rw[(FM + 5) * S3] = m.m21;
+            Rw[PR_SDE * S3] = nonres ? gl.step_s[i] * rdE[b] : (gl.Emax[b] - gl.Emin[b]);
+        }
+    };
+    auto phase2 = [&](int s2, int jj) {
+        const int b = N - 1 - s2 + jj;
+        if (jj < NJ && jb + jj < nst && b >= 0 && b < N) {
+            double* Rw = rec + (s2 % 3) * NJ + jj;
+            RecM m;
+            m.m01 = Rw[(FM + 0) * S3];
+            m.m02 = Rw[(FM + 1) * S3];
+            m.m10 = Rw[(FM + 2) * S3];
+            m.m12 = Rw[(FM + 3) * S3];
+            m.m20 = Rw[(FM + 4) * S3];
+            m.m21 = Rw[(FM + 5) * S3];
+            record_phase2<true>(m, Rw, S3);
+        }
+    };
+    // (the role-specific values below are formed inside each role's branch: live across the pass loop they would
+    // share the push waves' register budget)
+    const int npass = (nst + NJ - 1) / NJ;
+#pragma unroll 1
+    for (int pass = 0; pass < npass; ++pass) {
+        jb = pass * NJ;
+        const int njp = nst - jb < NJ ? nst - jb : NJ;   // steps of this pass
+        const int Ts = N - 1 + njp, c0 = T - 1 - jb;     // its stages; the table column of its stage 0
+        const bool last_pass = pass == npass - 1;
+        __syncthreads();   // (the previous pass is done with Tp, AX, hb and the records)
+        for (int j = tid; j < 16 * NJ * 16; j += nthr) Tp[j] = 0.0;   // Tp and AX
+        if (wave == recw) {
+            phase1(0, lane);
+            if (1 < Ts) phase1(1, lane);
+            if (lane < R) {   // slot 3 = stage -1: the upper edge of stage 0
+                const double si_l = pts[gidx[gr.x + lane]].si;
+                pwr[3 * 16 + lane] = nm::exp(-si_l * lx[c0 + 2]);
+                pwr[0 * 16 + lane] = nm::exp(-si_l * lx[c0 + 1]);
+                if (1 < Ts) pwr[1 * 16 + lane] = nm::exp(-si_l * lx[c0]);
+            }
+        }
+        __syncthreads();
+        if (wave == recw) phase2(0, lane);
+        __syncthreads();
+        if (wave >= nwp && wave < nwp + kGbChainWaves) {
+            // ---- chain: lane (cp, cjj) of wave cw solves (step jb + j, bin N-1-sg+j) of point cp, j = 3 cw + cjj
+            const int cw = wave - nwp, cp = lane / kGbSPW, cjj = lane - kGbSPW * (lane / kGbSPW);
+            const bool clane = lane < 16 * kGbSPW && cp < R;
+            const int cpid = clane ? gidx[gr.x + cp] : 0;
+            const SrcFactors csf = clane ? src_factors(pts[cpid]) : SrcFactors{0.0, 0.0};
+            double* const fhw = fh + (size_t)blockIdx.x * 3 * N * 16;   // this workgroup's F FIFO [3][N][16]
+            const int j = kGbSPW * cw + cjj;
+            const bool act = clane && j < njp;
+            const int i = Nz - 1 - jb - j;
+            const double u0 = P.u[0], u1 = P.u[1], u2 = P.u[2];
+            const double cj = act ? gl.step_c[i] : 0.0, sj = act ? gl.step_s[i] : 0.0, sfr = act ? gl.sfr[i] : 0.0;
+            const bool top = j == njp - 1;   // the pass's last step: its solves feed the next pass or the output
+            double racc = 0.0, px0 = 0.0, px1 = 0.0, px2 = 0.0, Th[4] = {0.0, 0.0, 0.0, 0.0};
+            // slot 0 of wave 0 after the first pass: F[:, b] of the previous pass' last step from the FIFO, four
+            // stages ahead (non-temporal: the FIFO's lines were rewritten since an earlier pass read them)
+            const bool ffifo = pass > 0 && cw == 0 && cjj == 0 && clane;
+            double fq0[4], fq1[4], fq2[4];
+#pragma unroll
+            for (int d = 0; d < 4; ++d) {
+                fq0[d] = fq1[d] = fq2[d] = 0.0;
+                const int bq = N - 1 - d;
+                if (ffifo && d < Ts && bq >= 0) {
+                    fq0[d] = __builtin_nontemporal_load(fhw + (0 * N + bq) * 16 + cp);
+                    fq1[d] = __builtin_nontemporal_load(fhw + (1 * N + bq) * 16 + cp);
+                    fq2[d] = __builtin_nontemporal_load(fhw + (2 * N + bq) * 16 + cp);
+                }
+            }
+            for (int sg0 = 0; sg0 < Ts; sg0 += 4)
+#pragma unroll
+            for (int d = 0; d < 4; ++d) {
+                const int sg = sg0 + d;
+                if (sg >= Ts) break;
+                NUSI_WS_STAMP(sg, 0);
+                const int r = c0 - sg;
+                const int b = N - 1 - sg + j;
+                // F[:, b] of this step: step j-1's solve of bin b at stage sg-1 (the lane below; for the wave's first
+                // step the other wave's top step through hb, or the previous pass through the FIFO)
+                double f0 = wave_shr1(px0, 0.0), f1 = wave_shr1(px1, 0.0), f2 = wave_shr1(px2, 0.0);
+                if (cjj == 0) {
+                    if (cw == 0) {
+                        f0 = fq0[d];
+                        f1 = fq1[d];
+                        f2 = fq2[d];
+                    } else if (sg >= 1 && clane) {
+                        const double* h = hb + ((sg - 1) & 1) * 48 + cp;
+                        f0 = h[0];
+                        f1 = h[16];
+                        f2 = h[32];
+                    }
+                }
+                if (ffifo) {   // the FIFO entry of stage sg + 4 into the slot just consumed
+                    const int bq = N - 5 - sg;
+                    if (sg + 4 < Ts && bq >= 0) {
+                        fq0[d] = __builtin_nontemporal_load(fhw + (0 * N + bq) * 16 + cp);
+                        fq1[d] = __builtin_nontemporal_load(fhw + (1 * N + bq) * 16 + cp);
+                        fq2[d] = __builtin_nontemporal_load(fhw + (2 * N + bq) * 16 + cp);
+                    }
+                }
+                double Tn = 0.0;
+                if (act && b >= 0 && b < N) {
+                    const double* Rc = rec + (sg % 3) * NJ + j;
+                    constexpr int S = S3;
+                    const double rz0 = Rc[PR_RZ0 * S], rz1 = Rc[PR_RZ1 * S], rz2 = Rc[PR_RZ2 * S];
+                    const int pmb = (int)Rc[kPreFields * S];
+                    const double l10 = Rc[PR_L10 * S], l20 = Rc[PR_L20 * S], l21 = Rc[PR_L21 * S];
+                    const double u01 = Rc[PR_U01 * S], u02 = Rc[PR_U02 * S], u12 = Rc[PR_U12 * S];
+                    const double ru00 = Rc[PR_RU00 * S], ru11 = Rc[PR_RU11 * S], ru22 = Rc[PR_RU22 * S];
+                    const double sde = Rc[PR_SDE * S];
+                    // the power-law source c_i Lum (powerlaw_src_h's expression): pw at b+i+1 and b+i
+                    const double pwlo = pwr[(sg & 3) * 16 + cp], pwhi = pwr[((sg - 1) & 3) * 16 + cp];
+                    const double src = cj * (csf.a3 * sfr * (sEmax[b] * pwhi - sEmin[b] * pwlo) * csf.rs);
+                    double add;
+                    if (nonres) {
+                        const int qq = (sg - 1) >> 2;              // block whose publication serves stage sg
+                        const int nu = (d == 0) ? 4 : d;           // columns r+1 .. r+nu not yet pushed
+                        double s = AX[(((qq & 1) * 4 + (sg - 1 - 4 * qq)) * NJ + j) * 16 + cp];
+#pragma unroll
+                        for (int k = 4; k >= 1; --k)
+                            if (k <= nu) s = fma(sdg[(k - 1) * T + r], Th[k - 1], s);
+                        add = cj * s;
+                    } else {
+                        const double dEb1 = (b + 1 < N) ? sEmax[b + 1] - sEmin[b + 1] : 1.0;
+                        add = resonant_add(racc, u0, u1, u2, px0, px1, px2, sj, sdg[r], dEb1, sde, cj, b == N - 1);
+                    }
+                    double x0, x1, x2;
+                    cascade_solve(f0, f1, f2, add, src, u0, u1, u2, rz0, rz1, rz2, pmb, l10, l20, l21, u01, u02, u12,
+                                  ru00, ru11, ru22, x0, x1, x2);
+                    if (top) {
+                        if (last_pass) {   // finalise (nuSIprop.hpp:328-336)
+                            const Point& Q = pts[cpid];
+                            const double dE = gl.Emax[b] - gl.Emin[b];
+                            const double g0 = x0 / dE, g1 = x1 / dE, g2 = x2 / dE;
+                            double* fo = flux + (size_t)cpid * 3 * N;
+                            double* fl = flux_fla + (size_t)cpid * 3 * N;
+                            fo[b] = g0;
+                            fo[N + b] = g1;
+                            fo[2 * N + b] = g2;
+                            for (int f = 0; f < 3; ++f)
+                                fl[f * N + b] = Q.U2[3 * f + 0] * g0 + Q.U2[3 * f + 1] * g1 + Q.U2[3 * f + 2] * g2;
+                        } else {
+                            fhw[(0 * N + b) * 16 + cp] = x0;
+                            fhw[(1 * N + b) * 16 + cp] = x1;
+                            fhw[(2 * N + b) * 16 + cp] = x2;
+                        }
+                    }
+                    if (kGbChainWaves > 1 && cw == 0 && cjj == kGbSPW - 1) {
+                        double* h = hb + (sg & 1) * 48 + cp;
+                        h[0] = x0;
+                        h[16] = x1;
+                        h[32] = x2;
+                    }
+                    px0 = x0; px1 = x1; px2 = x2;
+                    if (nonres && b > 0) Tn = (u0 * x0 + u1 * x1 + u2 * x2) * sde;
+                }
+                Th[3] = Th[2]; Th[2] = Th[1]; Th[1] = Th[0]; Th[0] = Tn;
+                if (clane && j < njp) Tp[((sg & 7) * NJ + j) * 16 + cp] = Tn;
+                NUSI_WS_STAMP(sg, 1);
+                __syncthreads();
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the FIFO stores land before the next pass reads
+        } else if (wave == recw) {
+            // ---- records two / one stage ahead, pw of each point (lane < R) at the lower edge of the stage two ahead
+            const double si_l = lane < R ? pts[gidx[gr.x + lane]].si : 0.0;
+            for (int sg = 0; sg < Ts; ++sg) {
+                NUSI_WS_STAMP(sg, 0);
+                if (sg + 2 < Ts) {
+                    phase1(sg + 2, lane);
+                    if (lane < R) pwr[((sg + 2) & 3) * 16 + lane] = nm::exp(-si_l * lx[c0 - 1 - sg]);
+                }
+                if (sg + 1 < Ts) phase2(sg + 1, lane);
+                NUSI_WS_STAMP(sg, 1);
+                __syncthreads();
+            }
+        } else {
+            // ---- push: block q (stage 4q) adds columns c0+1-4q .. c0+4-4q into the rows below r = c0-4q for every
+            // step and point, then publishes rows r-1 .. r-4
+            const int rw0 = wave * 16 * RT;
+            nusi_f64x4 acc[RT][NJ];
+#pragma unroll
+            for (int a = 0; a < RT; ++a)
+#pragma unroll
+                for (int s = 0; s < NJ; ++s) acc[a][s] = nusi_f64x4{0.0, 0.0, 0.0, 0.0};
+            auto load_blk = [&](int q, double (&dst)[RT]) {
+                int c = c0 + 1 - 4 * q + (lane >> 4);
+                c = c < 1 ? 1 : (c > T - 1 ? T - 1 : c);
+                const size_t cb = (size_t)c * (c - 1) / 2;
+#pragma unroll
+                for (int a = 0; a < RT; ++a) {
+                    const int row = rw0 + 16 * a + (lane & 15);
+                    dst[a] = Al[cb + (row < c - 1 ? row : c - 1)];
+                }
+            };
+            double ablk[RT];
+            load_blk(1, ablk);
+            for (int sg = 0; sg < Ts; ++sg) {
+                NUSI_WS_STAMP(sg, 0);
+                const int q = sg >> 2, r = c0 - 4 * q, hi = r - 1;
+                if ((sg & 3) == 0 && nonres) {
+                    if (q >= 1) {
+#pragma unroll
+                        for (int s = 0; s < NJ; ++s) {
+                            const double bop = Tp[(((4 * q - 1 - (lane >> 4)) & 7) * NJ + s) * 16 + (lane & 15)];
+#pragma unroll
+                            for (int a = 0; a < RT; ++a)
+                                if (rw0 + 16 * a < r)   // tiles wholly at or above r hold consumed rows only
+                                    acc[a][s] = __builtin_amdgcn_mfma_f64_16x16x4f64(ablk[a], bop, acc[a][s], 0, 0, 0);
+                        }
+                        load_blk(q + 1, ablk);
+                    }
+#pragma unroll
+                    for (int a = 0; a < RT; ++a)
+                        if (rw0 + 16 * a <= hi && rw0 + 16 * a + 15 >= hi - 3)   // uniform: tiles holding those rows
+#pragma unroll
+                            for (int e = 0; e < 4; ++e) {
+                                const int row = rw0 + 16 * a + (lane >> 4) + 4 * e;
+                                const int slot = hi - row;
+                                if (slot >= 0 && slot < 4)
+#pragma unroll
+                                    for (int s = 0; s < NJ; ++s)
+                                        AX[((((q & 1) * 4 + slot) * NJ) + s) * 16 + (lane & 15)] = acc[a][s][e];
+                            }
+                }
+                NUSI_WS_STAMP(sg, 1);
+                __syncthreads();
+            }
+        }
+    }   // passes
+}
+size_t cascade_gb_scratch_doubles(const GridDev& g) { return (size_t)3 * g.N * 16; }
+
 // launch geometry of the wavefront kernel: one thread per pushed row (T-1), whole waves; K stages
 // of records per batch, as many as the threads cover and kWfMaxLds allows
 constexpr size_t kWfMaxLds = 64 * 1024;
@@ -1609,6 +1945,29 @@ hipError_t launch_cascade_ws(const GridDev& g, const Point* pts, int R, const in
     return hipGetLastError();
 }
 
+// the gamma-batch kernel: push waves of 16 kGbRT rows, two chain waves, one record wave; ~45 KB of LDS at N = 300
+static int gb_push_waves(const GridDev& g) { return (g.T - 1 + 16 * kGbRT - 1) / (16 * kGbRT); }
+static size_t gb_lds(const GridDev& g)
+{
+    return sizeof(double) * (3 * (size_t)kGbNF * kGbNJ + 64 + 16 * (size_t)kGbNJ * 16 + 96 + (size_t)g.N + (g.T + 2) +
+                             6 * (size_t)g.T + 2 * (size_t)g.N + 4 * (size_t)g.Nz);
+}
+bool cascade_gb_fits(const GridDev& g)
+{
+    return g.T >= 2 && g.Nz >= 2 && gb_push_waves(g) + kGbChainWaves + 1 <= 16 && gb_lds(g) <= 160 * 1024;
+}
+hipError_t launch_cascade_gb(const GridDev& g, const Point* pts, const int* gidx, const int2* grp, int nwg, TablesDev t,
+                             double* fh, double* flux, double* flux_fla, hipStream_t s)
+{
+    if (!cascade_gb_fits(g)) return hipErrorInvalidValue;
+    if (nwg <= 0) return hipSuccess;
+    t_cascade_kernel = "k_cascade_gb";
+    const int nthr = 64 * (gb_push_waves(g) + kGbChainWaves + 1);
+    hipLaunchKernelGGL((k_cascade_gb<kGbNJ>), dim3(nwg), dim3(nthr), gb_lds(g), s, g, pts, gidx, grp, t, fh, flux,
+                       flux_fla);
+    return hipGetLastError();
+}
+
 hipError_t launch_cascade_wsp(const GridDev& g, const Point* pts, int npts, TablesDev t, double* flux, double* flux_fla,
                               hipStream_t s)
 {
@@ -1680,7 +2039,7 @@ hipError_t launch_cascade_exact(const GridDev& g, const Point* pts, int npts, Ta
 // diagnostic build: workgroup 0's stage stamps of the latest k_cascade_ws launch, [wave][stage][start, barrier]
 extern "C" int nusi_debug_ws_trace(unsigned long long* out, int n)
 {
-    const int m = n < nusi::kTrWaves * nusi::kTrStages * 2 ? n : nusi::kTrWaves * nusi::kTrStages * 2;
+    const int m = n < nusi::kTrWaves * nusi::kTrStages * 4 ? n : nusi::kTrWaves * nusi::kTrStages * 4;
     return hipMemcpyFromSymbol(out, HIP_SYMBOL(nusi::g_ws_trace), sizeof(unsigned long long) * m) == hipSuccess ? 0 : -5;
 }
 // HW_ID of every wave of the first kTrBlocks workgroups, [block][wave]

@@ -58,6 +58,10 @@ hipError_t launch_gamma_alphat(const GridDev& g, const Point* pts, int npts, con
 hipError_t launch_alpha(const GridDev& g, const Point* pts, int npts, const SplineSet& spl, const AlphaTilesDev& tiles,
                         TablesDev t, int* warn, hipStream_t s, const int* batches, int nbatches, int gmax,
                         int kernel, int nb_plain);
+// NUSI_OPT_SHIFT_REUSE: tables s0 .. s0 + nshift - 1 of t (grid g) <- base tables map[q].x of tb (grid gb, the
+// axis extended on top), read map[q].y bins higher; warn[s] |= warnb[base]
+hipError_t launch_table_shift(const GridDev& g, const GridDev& gb, const int2* map, int s0, int nshift, TablesDev tb,
+                              const int* warnb, TablesDev t, int* warn, hipStream_t s);
 // The MFMA cascade (NUSI_CASCADE_AUTO / MFMA): k_cascade_ws -- R = 1, one point per workgroup (groups
 // unused, nwg = points), or R = 2, groups[k] = two points sharing one table slot (y < 0: one point) -- for
 // Nz - 1 <= 48, k_cascade_wsp (step passes) for any number of steps.  Every point kind: the DSNB points'
@@ -68,6 +72,13 @@ hipError_t launch_cascade_ws(const GridDev& g, const Point* pts, int R, const in
                              double* flux, double* flux_fla, hipStream_t s);
 hipError_t launch_cascade_wsp(const GridDev& g, const Point* pts, int npts, TablesDev t, double* flux, double* flux_fla,
                               hipStream_t s);
+// The gamma batch (k_cascade_gb): workgroup k takes the grp[k].y <= 16 power-law points gidx[grp[k].x ..] that share one
+// table slot, gamma on the MFMA N dimension, the redshift steps in passes of 6; fh: a scratch FIFO of
+// cascade_gb_scratch_doubles per workgroup
+bool cascade_gb_fits(const GridDev& g);
+size_t cascade_gb_scratch_doubles(const GridDev& g);
+hipError_t launch_cascade_gb(const GridDev& g, const Point* pts, const int* gidx, const int2* grp, int nwg, TablesDev t,
+                             double* fh, double* flux, double* flux_fla, hipStream_t s);
 size_t cascade_src_doubles(const GridDev& g);   // t.Src doubles per point
 hipError_t launch_source_dsnb(const GridDev& g, const Point* pts, int npts, double* src, hipStream_t s);
 // The bit-exact scalar cascades (NUSI_CASCADE_WAVEFRONT / REG / LDS; a kind that does not fit the grid falls

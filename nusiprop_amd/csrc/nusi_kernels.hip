@@ -499,6 +499,38 @@ void k_alpha_batch(GridDev g, const Point* __restrict__ pts, SplineSet spl, cons
         for (int q = 0; q < nb; ++q) atomicOr(&warn[p0 + q], wsh);
 }
 
+// NUSI_OPT_SHIFT_REUSE: table slot s0 + q <- base table map[q].x of the extended axis (Tb bins),
+// read map[q].y bins higher; the base's warning bits go with it.  A copy, HBM-bound: 2 x 8 B per entry.
+__global__ __launch_bounds__(256) void k_table_shift(int T, long long PT, int Tb, long long PTb, const int2* __restrict__ map,
+                                                     int s0, TablesDev tb, const int* __restrict__ warnb, TablesDev t,
+                                                     int* __restrict__ warn)
+{
+    const int q = blockIdx.y, s = s0 + q;
+    const int bi = map[q].x, o = map[q].y;
+    const long long e = (long long)blockIdx.x * 256 + threadIdx.x;
+    if (e < T) {
+        t.G[(size_t)s * T + e] = tb.G[(size_t)bi * Tb + e + o];
+        t.At[(size_t)s * T + e] = tb.At[(size_t)bi * Tb + e + o];
+        if (e == 0 && warnb[bi]) atomicOr(&warn[s], warnb[bi]);
+    }
+    if (e >= PT) return;
+    int m = (int)((1.0 + sqrt(1.0 + 8.0 * (double)e)) * 0.5);   // packed index e = m (m - 1) / 2 + n, n < m
+    while ((long long)m * (m - 1) / 2 > e) --m;
+    while ((long long)(m + 1) * m / 2 <= e) ++m;
+    const long long n = e - (long long)m * (m - 1) / 2, mb = m + o;
+    t.A[(size_t)s * PT + e] = tb.A[(size_t)bi * PTb + mb * (mb - 1) / 2 + n + o];
+}
+
+hipError_t launch_table_shift(const GridDev& g, const GridDev& gb, const int2* map, int s0, int nshift, TablesDev tb,
+                              const int* warnb, TablesDev t, int* warn, hipStream_t s)
+{
+    if (nshift <= 0) return hipSuccess;
+    const long long ne = std::max<long long>(g.PT, g.T);
+    hipLaunchKernelGGL(k_table_shift, dim3((unsigned)((ne + 255) / 256), nshift), dim3(256), 0, s, g.T, g.PT, gb.T, gb.PT,
+                       map, s0, tb, warnb, t, warn);
+    return hipGetLastError();
+}
+
 hipError_t alpha_tiles_create(int T, const unsigned char* shared, AlphaTilesDev* out)
 {
     const int nt = (T + kAlphaTile - 1) / kAlphaTile;

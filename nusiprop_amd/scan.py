@@ -24,6 +24,17 @@ def c4_points(si=2.5, n_mphi=32, n_g=32, **over):
             for m in np.logspace(5.5, 8.0, n_mphi) for g in np.logspace(-3.0, 0.0, n_g)]
 
 
+def c4s_points(si=2.5, n_mphi=32, n_g=32, step=4, **over):
+    """The opt-in shift-reuse scan (NUSI_OPT_SHIFT_REUSE): C4's g grid and 32 m_phi on the
+    lattice m_max r^(-o/2), o = 0, step, 2 step, ... (r = 10^((lEmax - lEmin) / N_E), the table axis' bin ratio),
+    m_max = 10^6.533 (o = 124 reaches 10^5.5, C4's lower end).  Needs K >= step (n_mphi - 1)."""
+    base = dict(BASE, **over)
+    r = 10 ** ((base["lEmax"] - base["lEmin"]) / base["N_bins_E"])
+    m_max = 10 ** 6.533
+    return [dict(base, mphi=float(m_max * r ** (-step * k / 2)), g=float(g), si=float(si))
+            for k in range(n_mphi) for g in np.logspace(-3.0, 0.0, n_g)]
+
+
 def c5_points(**over):
     """BASELINE config 5: mphi (64) x g (64) x gamma in linspace(2, 3, 16) = 65 536 points, gamma fastest."""
     base = dict(BASE, **over)

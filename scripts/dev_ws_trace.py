@@ -26,9 +26,9 @@ def main():
     for _ in range(3):
         plan.evolve(arr)
     L = ctypes.CDLL(_lib.LIB_PATH)
-    buf = (ctypes.c_ulonglong * (TW * TS * 2))()
-    assert L.nusi_debug_ws_trace(buf, TW * TS * 2) == 0
-    a = np.frombuffer(buf, dtype=np.uint64).reshape(TW, TS, 2).astype(np.int64)
+    buf = (ctypes.c_ulonglong * (TW * TS * 4))()
+    assert L.nusi_debug_ws_trace(buf, TW * TS * 4) == 0
+    a = np.frombuffer(buf, dtype=np.uint64).reshape(TW, TS, 4).astype(np.int64)
     T = plan.T
     waves = [w for w in range(TW) if a[w, 10, 0] != 0]
     nw = len(waves)
@@ -45,6 +45,12 @@ def main():
                                            ("phase2" if w == chain - 2 and "mrhs" in plan.kernels()[1] else "push"))
         print("  wave %2d %-6s busy median %5d  mean %6.0f  p90 %6d  (stage 4q: %6.0f)" % (
             w, kind, np.median(busy), busy.mean(), np.quantile(busy, 0.9), busy[::4].mean()))
+    # the chain's segments (the stamps at 2 and 3 wait for the wave's outstanding loads first)
+    c2, c3 = a[chain, 4:T - 4, 2], a[chain, 4:T - 4, 3]
+    ok = (c2 > 0) & (c3 > 0)
+    s0 = st[chain, 4:T - 4]
+    print("chain segments (median cycles): start -> records/AX loaded and coupling added %d, -> solved %d, -> barrier %d"
+          % (np.median((c2 - s0)[ok]), np.median((c3 - c2)[ok]), np.median((en[chain, 4:T - 4] - c3)[ok])))
     last = np.argmax(en[waves, 4:T - 4], axis=0)
     cnt = np.bincount(last, minlength=nw)
     print("last to reach the barrier:", {waves[i]: int(c) for i, c in enumerate(cnt) if c})
