@@ -49,6 +49,9 @@ def parse():
     ap.add_argument("--cascade", default="auto", choices=["auto", "mfma", "wf"],
                     help="cascade kernel: auto = the library default (= mfma: the warp-specialised wavefront with "
                          "the push on the fp64 matrix cores), wf = the bit-exact scalar wavefront")
+    ap.add_argument("--rhs", type=int, default=0,
+                    help="NUSI_OPT_CASCADE_RHS: 0 = the library default, 1 = one point per cascade workgroup, 2 = pairs "
+                         "of points sharing a table, 3..16 = the gamma batch k_cascade_gb")
     ap.add_argument("--dry-run", action="store_true",
                     help="launch / rank / reduction plumbing only, no GPU work (gloo; CPU tests): prints the JSON "
                          "line with value null")
@@ -328,6 +331,8 @@ def main():
     plan.set_cascade({"mfma": _lib.CASCADE_MFMA, "wf": _lib.CASCADE_WAVEFRONT, "auto": _lib.CASCADE_AUTO}[args.cascade])
     if args.workload == "c4s":
         plan.set_option(_lib.OPT_SHIFT_REUSE, 128)
+    if args.rhs:
+        plan.set_option(_lib.OPT_CASCADE_RHS, args.rhs)
     dev = torch.device("cuda", local)
     flux = torch.empty((P, 3, plan.N), dtype=torch.float64, device=dev)
     fla = torch.empty((P, 3, plan.N), dtype=torch.float64, device=dev)
@@ -390,6 +395,10 @@ def main():
         from collections import Counter
         readers = sum((c + 1) // 2 for c in Counter(scan.table_key(p) for p in pts).values())
     casc_min = scan.cascade_min_bytes_per_point(N, Nz, passes=casc_kernel == "k_cascade_ws_passes") * readers
+    gbs = scan.gamma_batches(pts, args.rhs or 16) if "k_cascade_gb" in casc_kernel else []
+    if gbs:   # the gamma batch: each workgroup reads its table once per pass; the points write their fluxes
+        readers = len(gbs)
+        casc_min = scan.cascade_gb_bytes_per_batch(N, Nz) * len(gbs) + 8 * 6 * N * P
     step_ms = sum(sum_ms) / max(ncalls, 1)
     out = {
         "metric": METRIC,
@@ -406,7 +415,8 @@ def main():
         "data": "synthetic (deterministic scan grid; power-law source)",
         "config": {"workload": desc, "N_E": N, "N_z": Nz, "points_per_gpu": P, "lEmin": p0["lEmin"],
                    "lEmax": p0["lEmax"], "parallelism": "independent points, %d GPU(s), no collective" % world,
-                   "alpha_kernel": alpha_kernel, "cascade_kernel": casc_kernel, "cascade_kind": args.cascade},
+                   "alpha_kernel": alpha_kernel, "cascade_kernel": casc_kernel, "cascade_kind": args.cascade,
+                   "cascade_rhs": args.rhs or "auto"},
         "libnusi": {"path": os.path.relpath(_lib.LIB_PATH, ROOT), "sha256": lib_sha, "pmc_source": tsrc,
                     "pmc_note": pmc_note},
         "stage_ms_per_step": {"gamma_alphatilde": sum_ms[0] / max(ncalls, 1), "alpha": sum_ms[1] / max(ncalls, 1),
@@ -428,12 +438,13 @@ def main():
         "invalid_outputs": bad,
         "phiphi_lookups_out_of_range": oob,
     }
-    if "ws" in casc_kernel:   # the push on the matrix cores
-        mf = scan.cascade_mfma_flops_per_point(N, Nz) * P
+    if "ws" in casc_kernel or gbs:   # the push on the matrix cores
+        mf = scan.cascade_gb_flops_per_batch(N, Nz) * len(gbs) if gbs else scan.cascade_mfma_flops_per_point(N, Nz) * P
         out["roofline_cascade"]["mfma"] = {"flops_per_launch": mf, "achieved": mf / casc_s / 1e12,
                                            "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                                            "frac": mf / casc_s / 1e12 / FP64_PEAK_TFLOPS,
-                                           "note": "v_mfma_f64_16x16x4f64 rank-4 pushes (scan.cascade_mfma_flops_per_point)"}
+                                           "note": "v_mfma_f64_16x16x4f64 rank-4 pushes (scan.cascade_mfma_flops_per_point; "
+                                                   "the gamma batch: scan.cascade_gb_flops_per_batch)"}
         # matrix-core counters of the cascade kernels (the profile's MFMA pass), summed over a step's launches
         mc = {}
         for kname, rec in pmc.get("kernels", {}).items():

@@ -172,7 +172,12 @@ int nusi_plan_set_cascade(nusi_plan *plan, int kind);
  *                          batches of <= 4, 2 = one entry per work-item
  *                          (all three give the same tables bit for bit)
  *   NUSI_OPT_CASCADE_RHS   max points sharing a table per MFMA-cascade
- *                          workgroup: 0 = automatic, 1 = one point each
+ *                          workgroup: 0 = automatic (the gamma batch for
+ *                          tables with >= 3 power-law points, pairs for the
+ *                          rest), 1 = one point each, 2 = pairs
+ *                          (k_cascade_ws<R = 2>), 3..16 = the gamma batch
+ *                          k_cascade_gb (power-law points of a table, gamma
+ *                          on the MFMA N dimension) of up to that many
  *   NUSI_OPT_STEP_PASSES   0 = automatic (step passes beyond 48 redshift
  *                          steps), 1 = always the step-pass kernel
  *   NUSI_OPT_SHIFT_REUSE   opt-in scan mode, K in

@@ -416,7 +416,14 @@ struct nusi_plan {
     int* h_batches = nullptr;       // pinned
     int alpha_batch = 0;            // NUSI_OPT_ALPHA_BATCH: max tables per batch; 0 = auto
     int alpha_kind = 0;             // NUSI_OPT_ALPHA_KERNEL: 0 k_alpha_batch, 1 k_alpha_tile<G> (<= 4), 2 per entry
-    int cascade_rhs = 0;            // NUSI_OPT_CASCADE_RHS: 0 = auto, 1 = one point per MFMA-cascade workgroup
+    int cascade_rhs = 0;            // NUSI_OPT_CASCADE_RHS: 0 = auto, 1 = one point per MFMA-cascade workgroup,
+                                    // 2 = pairs, 3..16 = gamma batches of up to that many (k_cascade_gb)
+    int* d_gidx = nullptr;          // gamma batches: the points of each batch, batch after batch
+    int* h_gidx = nullptr;          // pinned
+    int2* d_gbgrp = nullptr;        // ... per batch: first index into gidx, count
+    int2* h_gbgrp = nullptr;        // pinned
+    double* d_fh = nullptr;         // ... k_cascade_gb's F FIFO, cascade_gb_scratch_doubles per batch
+    int fh_cap = 0;
     int step_passes = 0;            // NUSI_OPT_STEP_PASSES: 1 = the step-pass cascade also where one pass fits
     int shift_max = 0;              // NUSI_OPT_SHIFT_REUSE: K, the largest bin offset served by a base table set
     nusi_plan* shift = nullptr;     // ... its plan: the same grid with K more redshift steps (axis T + K)
@@ -737,6 +744,11 @@ void nusi_plan_destroy(nusi_plan* pl)
     hipFree(pl->d_src);
     hipFree(pl->d_smap);
     if (pl->h_smap) hipHostFree(pl->h_smap);
+    hipFree(pl->d_gidx);
+    hipFree(pl->d_gbgrp);
+    hipFree(pl->d_fh);
+    if (pl->h_gidx) hipHostFree(pl->h_gidx);
+    if (pl->h_gbgrp) hipHostFree(pl->h_gbgrp);
     nusi::alpha_tiles_destroy(&pl->atiles);
     hipFree(pl->d_scratch);
     if (pl->h_pts) hipHostFree(pl->h_pts);
@@ -955,17 +967,58 @@ int nusi_plan_evolve(nusi_plan* pl, const nusi_params* pts, int n, double* d_flu
     }
     const bool one_pass = nusi::cascade_ws_fits(pl->gd, 1) && pl->step_passes != 1;
     const bool fast = kind == NUSI_CASCADE_MFMA && (one_pass || nusi::cascade_wsp_fits(pl->gd));
+    const bool pairs_fit = fast && one_pass && nusi::cascade_ws_fits(pl->gd, 2);
+    // the gamma batch (k_cascade_gb; NUSI_OPT_CASCADE_RHS 0 = auto = 16, or 3..16): the power-law points of a table
+    // slot -- C5's 16 gamma of one (m_phi, g) -- when there are at least 3, up to 16 per workgroup, gamma on the
+    // MFMA N dimension; the other points take the pair / one-point kernels below
+    int ngb = 0, ngidx = 0;
+    std::vector<char> in_gb;
+    const int gbmax = pl->cascade_rhs == 0 ? 16 : pl->cascade_rhs;   // auto: the gamma batch (C5 cascade 4.54 -> 4.13 ms)
+    if (pairs_fit && gbmax >= 3 && nusi::cascade_gb_fits(pl->gd)) {
+        if (!pl->d_gidx) {
+            HIPCHECK(hipMalloc(&pl->d_gidx, sizeof(int) * pl->max_points));
+            HIPCHECK(hipMalloc(&pl->d_gbgrp, sizeof(int2) * pl->max_points));
+            HIPCHECK(hipHostMalloc((void**)&pl->h_gidx, sizeof(int) * pl->max_points, hipHostMallocDefault));
+            HIPCHECK(hipHostMalloc((void**)&pl->h_gbgrp, sizeof(int2) * pl->max_points, hipHostMallocDefault));
+        }
+        std::vector<std::vector<int>> by(ntab);
+        for (int i = 0; i < n; ++i)
+            if (pl->h_pts[i].source == NUSI_SOURCE_POWER_LAW) by[pl->h_pts[i].tslot].push_back(i);
+        in_gb.assign(n, 0);
+        for (int j = 0; j < ntab; ++j) {
+            const int c = (int)by[j].size();
+            if (c < 3) continue;
+            const int nb = (c + gbmax - 1) / gbmax;   // near-equal batches
+            for (int k = 0; k < nb; ++k) {
+                const int lo = (int)((long long)c * k / nb), hi = (int)((long long)c * (k + 1) / nb);
+                pl->h_gbgrp[ngb++] = make_int2(ngidx, hi - lo);
+                for (int q = lo; q < hi; ++q) {
+                    pl->h_gidx[ngidx++] = by[j][q];
+                    in_gb[by[j][q]] = 1;
+                }
+            }
+        }
+        if (ngb > pl->fh_cap) {
+            hipFree(pl->d_fh);
+            pl->d_fh = nullptr;
+            pl->fh_cap = 0;
+            HIPCHECK(hipMalloc(&pl->d_fh, sizeof(double) * nusi::cascade_gb_scratch_doubles(pl->gd) * ngb));
+            pl->fh_cap = ngb;
+        }
+    }
     int ngroups = 0;
-    if (fast && one_pass && pl->cascade_rhs != 1 && nusi::cascade_ws_fits(pl->gd, 2)) {
+    if (pairs_fit && (pl->cascade_rhs != 1 || ngb)) {
         std::vector<int> open(ntab, -1);   // per table slot: a point waiting for its partner
         for (int i = 0; i < n; ++i) {
+            if (ngb && in_gb[i]) continue;
             int& o = open[pl->h_pts[i].tslot];
-            if (o < 0) o = i;
+            if (pl->cascade_rhs == 1) pl->h_groups[ngroups++] = make_int2(i, -1);
+            else if (o < 0) o = i;
             else { pl->h_groups[ngroups++] = make_int2(o, i); o = -1; }
         }
         for (int j = 0; j < ntab; ++j)
             if (open[j] >= 0) pl->h_groups[ngroups++] = make_int2(open[j], -1);
-        if (4 * ngroups > 3 * n) ngroups = 0;   // too few pairs: one point per workgroup
+        if (!ngb && 4 * ngroups > 3 * n) ngroups = 0;   // too few pairs: one point per workgroup
     }
     if (fast && any_dsnb && pl->src_cap < pl->max_points) {
         hipFree(pl->d_src);
@@ -976,6 +1029,10 @@ int nusi_plan_evolve(nusi_plan* pl, const nusi_params* pts, int n, double* d_flu
         pl->tabs.Src = pl->d_src;
     }
     if (ngroups) HIPCHECK(hipMemcpyAsync(pl->d_groups, pl->h_groups, sizeof(int2) * ngroups, hipMemcpyHostToDevice, s));
+    if (ngb) {
+        HIPCHECK(hipMemcpyAsync(pl->d_gidx, pl->h_gidx, sizeof(int) * ngidx, hipMemcpyHostToDevice, s));
+        HIPCHECK(hipMemcpyAsync(pl->d_gbgrp, pl->h_gbgrp, sizeof(int2) * ngb, hipMemcpyHostToDevice, s));
+    }
     HIPCHECK(hipMemcpyAsync(pl->d_pts, pl->h_pts, sizeof(nusi::Point) * n, hipMemcpyHostToDevice, s));
     HIPCHECK(hipMemcpyAsync(pl->d_tpts, pl->h_tpts, sizeof(nusi::Point) * ntab, hipMemcpyHostToDevice, s));
     if (nbatch) HIPCHECK(hipMemcpyAsync(pl->d_batches, pl->h_batches, sizeof(int) * nbatch, hipMemcpyHostToDevice, s));
@@ -1010,9 +1067,16 @@ int nusi_plan_evolve(nusi_plan* pl, const nusi_params* pts, int n, double* d_flu
     }
     HIPCHECK(hipEventRecord(ev[2], s));
     if (fast && any_dsnb) HIPCHECK(nusi::launch_source_dsnb(pl->gd, pl->d_pts, n, pl->d_src, s));
+    const char* gb_name = nullptr;
+    if (ngb) {
+        HIPCHECK(nusi::launch_cascade_gb(pl->gd, pl->d_pts, pl->d_gidx, pl->d_gbgrp, ngb, pl->tabs, pl->d_fh, d_flux,
+                                         d_fla, s));
+        gb_name = ngroups ? "k_cascade_gb + k_cascade_ws_mrhs" : "k_cascade_gb";
+    }
     if (fast && ngroups)
         HIPCHECK(nusi::launch_cascade_ws(pl->gd, pl->d_pts, 2, pl->d_groups, ngroups, pl->tabs, d_flux, d_fla, s));
-    else if (fast && one_pass)
+    else if (ngb) {
+    } else if (fast && one_pass)
         HIPCHECK(nusi::launch_cascade_ws(pl->gd, pl->d_pts, 1, nullptr, n, pl->tabs, d_flux, d_fla, s));
     else if (fast)
         HIPCHECK(nusi::launch_cascade_wsp(pl->gd, pl->d_pts, n, pl->tabs, d_flux, d_fla, s));
@@ -1023,7 +1087,7 @@ int nusi_plan_evolve(nusi_plan* pl, const nusi_params* pts, int n, double* d_flu
     HIPCHECK(hipEventRecord(pl->ev_done, s));
     pl->alpha_kernel = nusi::last_alpha_kernel();
     if (sp) pl->alpha_kernel = nd ? "k_alpha_batch + k_table_shift" : "k_alpha_batch (shift base) + k_table_shift";
-    pl->cascade_kernel = nusi::last_cascade_kernel();
+    pl->cascade_kernel = gb_name ? gb_name : nusi::last_cascade_kernel();
     for (int k = 0; k < 4; ++k) pl->last_ev[k] = ev[k];   // stage_ms / warnings / tables refer to the latest call
     pl->ran = true;
     pl->last_n = n;
@@ -1094,7 +1158,7 @@ int nusi_plan_set_option(nusi_plan* pl, int option, int value)
         pl->alpha_kind = value;
         return NUSI_OK;
     case NUSI_OPT_CASCADE_RHS:
-        if (value < 0 || value > 2) return fail(NUSI_EPARAM, "NUSI_OPT_CASCADE_RHS outside [0, 2]");
+        if (value < 0 || value > 16) return fail(NUSI_EPARAM, "NUSI_OPT_CASCADE_RHS outside [0, 16]");
         pl->cascade_rhs = value;
         return NUSI_OK;
     case NUSI_OPT_STEP_PASSES:

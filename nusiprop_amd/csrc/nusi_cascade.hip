@@ -1559,18 +1559,17 @@ void k_cascade_gb(GridDev g, const Point* __restrict__ pts, const int* __restric
     constexpr int RT = kGbRT, NF = kGbNF, FM = kWfFields, S3 = 3 * NJ;
     const int N = g.N, Nz = g.Nz, T = g.T, nst = Nz - 1;
     const int tid = threadIdx.x, nthr = blockDim.x, lane = tid & 63, wave = tid >> 6, nw = nthr >> 6;
-    const int nwp = nw - kGbChainWaves - 1, recw = nw - 1;   // push waves, then the chain waves, then the record wave
+    const int nwp = nw - kGbChainWaves - 2, recw = nw - 2;   // push waves, the chain waves, the two record waves
     const int2 gr = grp[blockIdx.x];
     const int R = gr.y;                                      // points of this workgroup (<= 16), one table
     const Point& P = pts[gidx[gr.x]];
     double* rec = lds;                       // [3][NF][NJ]     records of stage s in slot s % 3
-    double* pwr = rec + 3 * NF * NJ;         // [4][16]         each point's pw at the lower edge of stage s (slot s & 3)
-    double* Tp = pwr + 64;                   // [8][NJ][16]     T_j of each point by stage
+    double* Tp = rec + 3 * NF * NJ;          // [8][NJ][16]     T_j of each point by stage
     double* AX = Tp + 8 * NJ * 16;           // [2][4][NJ][16]  rows published by block q (parity q & 1)
     double* hb = AX + 8 * NJ * 16;           // [2][3][16]      chain wave 0's top step -> wave 1 (stage parity)
     double* rdE = hb + 96;                   // [N]
-    double* lx = rdE + N;                    // [T + 2]         log of the power law's argument on table edge e
-    double* sGt = lx + T + 2;
+    double* pw = rdE + N;                    // [T + 2][16]     each point's pw on table edge e (cascade_aux_init's)
+    double* sGt = pw + 16 * (T + 2);
     double* sAt = sGt + T;
     double* sdg = sAt + T;                   // [4][T]: alpha(n, n+k), k = 1..4 (0 past the table)
     double* sEmin = sdg + 4 * T;
@@ -1604,10 +1603,12 @@ void k_cascade_gb(GridDev g, const Point* __restrict__ pts, const int* __restric
             sgz[2 * Nz + i] = g.step_s[i];
             sgz[3 * Nz + i] = g.sfr[i];
         }
-        for (int e = tid + 1; e <= T + 1; e += nthr) {   // cascade_aux_init's argument of pw[e]: pow = exp(y log x)
+        for (int q = tid; q < 16 * (T + 1); q += nthr) {   // cascade_aux_init's pw[e] of every point
+            const int e = 1 + q / 16, p = q - 16 * (q / 16);
+            if (p >= R) continue;
             const int i = min(Nz - 1, max(1, e - N + 1)), b = e - i;
             const double E = (b < N) ? g.Emin[b] : g.Emax[N - 1];
-            lx[e] = nm::log(E / 1e14 * (1 + g.z[i]));
+            pw[e * 16 + p] = nm::pow(E / 1e14 * (1 + g.z[i]), -pts[gidx[gr.x + p]].si);
         }
     }
     const bool nonres = P.non_resonant;
@@ -1643,50 +1644,48 @@ void k_cascade_gb(GridDev g, const Point* __restrict__ pts, const int* __restric
             record_phase2<true>(m, Rw, S3);
         }
     };
-    // (the role-specific values below are formed inside each role's branch: live across the pass loop they would
-    // share the push waves' register budget)
+    // Every role runs the passes in its own loop (one loop around the role branches made the compiler spill the
+    // push waves' accumulators), with the same barriers: pass start, records 0/1 written, record 0 complete, then
+    // one per stage.
     const int npass = (nst + NJ - 1) / NJ;
-#pragma unroll 1
-    for (int pass = 0; pass < npass; ++pass) {
+    auto pass_geom = [&](int pass, int& njp, int& Ts, int& c0) {
         jb = pass * NJ;
-        const int njp = nst - jb < NJ ? nst - jb : NJ;   // steps of this pass
-        const int Ts = N - 1 + njp, c0 = T - 1 - jb;     // its stages; the table column of its stage 0
-        const bool last_pass = pass == npass - 1;
-        __syncthreads();   // (the previous pass is done with Tp, AX, hb and the records)
-        for (int j = tid; j < 16 * NJ * 16; j += nthr) Tp[j] = 0.0;   // Tp and AX
-        if (wave == recw) {
-            phase1(0, lane);
-            if (1 < Ts) phase1(1, lane);
-            if (lane < R) {   // slot 3 = stage -1: the upper edge of stage 0
-                const double si_l = pts[gidx[gr.x + lane]].si;
-                pwr[3 * 16 + lane] = nm::exp(-si_l * lx[c0 + 2]);
-                pwr[0 * 16 + lane] = nm::exp(-si_l * lx[c0 + 1]);
-                if (1 < Ts) pwr[1 * 16 + lane] = nm::exp(-si_l * lx[c0]);
-            }
-        }
-        __syncthreads();
-        if (wave == recw) phase2(0, lane);
-        __syncthreads();
-        if (wave >= nwp && wave < nwp + kGbChainWaves) {
-            // ---- chain: lane (cp, cjj) of wave cw solves (step jb + j, bin N-1-sg+j) of point cp, j = 3 cw + cjj
-            const int cw = wave - nwp, cp = lane / kGbSPW, cjj = lane - kGbSPW * (lane / kGbSPW);
-            const bool clane = lane < 16 * kGbSPW && cp < R;
-            const int cpid = clane ? gidx[gr.x + cp] : 0;
-            const SrcFactors csf = clane ? src_factors(pts[cpid]) : SrcFactors{0.0, 0.0};
-            double* const fhw = fh + (size_t)blockIdx.x * 3 * N * 16;   // this workgroup's F FIFO [3][N][16]
-            const int j = kGbSPW * cw + cjj;
+        njp = nst - jb < NJ ? nst - jb : NJ;   // steps of this pass
+        Ts = N - 1 + njp;                      // its stages
+        c0 = T - 1 - jb;                       // the table column of its stage 0
+    };
+    auto pass_head = [&]() {   // the barriers and shared set-up every role runs at a pass start
+        __syncthreads();       // (the previous pass is done with Tp, AX, hb and the records)
+        for (int q = tid; q < 16 * NJ * 16; q += nthr) Tp[q] = 0.0;   // Tp and AX
+    };
+    if (wave >= nwp && wave < nwp + kGbChainWaves) {
+        // ---- chain: lane (cp, cjj) of wave cw solves (step jb + j, bin N-1-sg+j) of point cp, j = 3 cw + cjj
+        const int cw = wave - nwp, cp = lane / kGbSPW, cjj = lane - kGbSPW * (lane / kGbSPW);
+        const bool clane = lane < 16 * kGbSPW && cp < R;
+        const int cpid = clane ? gidx[gr.x + cp] : 0;
+        const SrcFactors csf = clane ? src_factors(pts[cpid]) : SrcFactors{0.0, 0.0};
+        double* const fhw = fh + (size_t)blockIdx.x * 3 * N * 16;   // this workgroup's F FIFO [3][N][16]
+        const int j = kGbSPW * cw + cjj;
+        const double u0 = P.u[0], u1 = P.u[1], u2 = P.u[2];
+#pragma unroll 1
+        for (int pass = 0; pass < npass; ++pass) {
+            int njp, Ts, c0;
+            pass_geom(pass, njp, Ts, c0);
+            const bool last_pass = pass == npass - 1;
+            pass_head();
+            __syncthreads();
+            __syncthreads();
             const bool act = clane && j < njp;
             const int i = Nz - 1 - jb - j;
-            const double u0 = P.u[0], u1 = P.u[1], u2 = P.u[2];
             const double cj = act ? gl.step_c[i] : 0.0, sj = act ? gl.step_s[i] : 0.0, sfr = act ? gl.sfr[i] : 0.0;
             const bool top = j == njp - 1;   // the pass's last step: its solves feed the next pass or the output
             double racc = 0.0, px0 = 0.0, px1 = 0.0, px2 = 0.0, Th[4] = {0.0, 0.0, 0.0, 0.0};
-            // slot 0 of wave 0 after the first pass: F[:, b] of the previous pass' last step from the FIFO, four
+            // slot 0 of wave 0 after the first pass: F[:, b] of the previous pass' last step from the FIFO, two
             // stages ahead (non-temporal: the FIFO's lines were rewritten since an earlier pass read them)
             const bool ffifo = pass > 0 && cw == 0 && cjj == 0 && clane;
-            double fq0[4], fq1[4], fq2[4];
+            double fq0[2], fq1[2], fq2[2];
 #pragma unroll
-            for (int d = 0; d < 4; ++d) {
+            for (int d = 0; d < 2; ++d) {
                 fq0[d] = fq1[d] = fq2[d] = 0.0;
                 const int bq = N - 1 - d;
                 if (ffifo && d < Ts && bq >= 0) {
@@ -1703,14 +1702,14 @@ void k_cascade_gb(GridDev g, const Point* __restrict__ pts, const int* __restric
                 NUSI_WS_STAMP(sg, 0);
                 const int r = c0 - sg;
                 const int b = N - 1 - sg + j;
-                // F[:, b] of this step: step j-1's solve of bin b at stage sg-1 (the lane below; for the wave's first
-                // step the other wave's top step through hb, or the previous pass through the FIFO)
+                // F[:, b] of this step: step j-1's solve of bin b at stage sg-1 (the lane below; for the wave's
+                // first step the other wave's top step through hb, or the previous pass through the FIFO)
                 double f0 = wave_shr1(px0, 0.0), f1 = wave_shr1(px1, 0.0), f2 = wave_shr1(px2, 0.0);
                 if (cjj == 0) {
                     if (cw == 0) {
-                        f0 = fq0[d];
-                        f1 = fq1[d];
-                        f2 = fq2[d];
+                        f0 = fq0[d & 1];
+                        f1 = fq1[d & 1];
+                        f2 = fq2[d & 1];
                     } else if (sg >= 1 && clane) {
                         const double* h = hb + ((sg - 1) & 1) * 48 + cp;
                         f0 = h[0];
@@ -1718,12 +1717,12 @@ void k_cascade_gb(GridDev g, const Point* __restrict__ pts, const int* __restric
                         f2 = h[32];
                     }
                 }
-                if (ffifo) {   // the FIFO entry of stage sg + 4 into the slot just consumed
-                    const int bq = N - 5 - sg;
-                    if (sg + 4 < Ts && bq >= 0) {
-                        fq0[d] = __builtin_nontemporal_load(fhw + (0 * N + bq) * 16 + cp);
-                        fq1[d] = __builtin_nontemporal_load(fhw + (1 * N + bq) * 16 + cp);
-                        fq2[d] = __builtin_nontemporal_load(fhw + (2 * N + bq) * 16 + cp);
+                if (ffifo) {   // the FIFO entry of stage sg + 2 into the slot just consumed
+                    const int bq = N - 3 - sg;
+                    if (sg + 2 < Ts && bq >= 0) {
+                        fq0[d & 1] = __builtin_nontemporal_load(fhw + (0 * N + bq) * 16 + cp);
+                        fq1[d & 1] = __builtin_nontemporal_load(fhw + (1 * N + bq) * 16 + cp);
+                        fq2[d & 1] = __builtin_nontemporal_load(fhw + (2 * N + bq) * 16 + cp);
                     }
                 }
                 double Tn = 0.0;
@@ -1736,18 +1735,18 @@ void k_cascade_gb(GridDev g, const Point* __restrict__ pts, const int* __restric
                     const double u01 = Rc[PR_U01 * S], u02 = Rc[PR_U02 * S], u12 = Rc[PR_U12 * S];
                     const double ru00 = Rc[PR_RU00 * S], ru11 = Rc[PR_RU11 * S], ru22 = Rc[PR_RU22 * S];
                     const double sde = Rc[PR_SDE * S];
-                    // the power-law source c_i Lum (powerlaw_src_h's expression): pw at b+i+1 and b+i
-                    const double pwlo = pwr[(sg & 3) * 16 + cp], pwhi = pwr[((sg - 1) & 3) * 16 + cp];
+                    // the power-law source c_i Lum (powerlaw_src_h's expression): pw at b+i+1 and b+i = c0+1-sg
+                    const double pwlo = pw[(c0 + 1 - sg) * 16 + cp], pwhi = pw[(c0 + 2 - sg) * 16 + cp];
                     const double src = cj * (csf.a3 * sfr * (sEmax[b] * pwhi - sEmin[b] * pwlo) * csf.rs);
                     double add;
                     if (nonres) {
                         const int qq = (sg - 1) >> 2;              // block whose publication serves stage sg
                         const int nu = (d == 0) ? 4 : d;           // columns r+1 .. r+nu not yet pushed
-                        double s = AX[(((qq & 1) * 4 + (sg - 1 - 4 * qq)) * NJ + j) * 16 + cp];
+                        double sa = AX[(((qq & 1) * 4 + (sg - 1 - 4 * qq)) * NJ + j) * 16 + cp];
 #pragma unroll
                         for (int k = 4; k >= 1; --k)
-                            if (k <= nu) s = fma(sdg[(k - 1) * T + r], Th[k - 1], s);
-                        add = cj * s;
+                            if (k <= nu) sa = fma(sdg[(k - 1) * T + r], Th[k - 1], sa);
+                        add = cj * sa;
                     } else {
                         const double dEb1 = (b + 1 < N) ? sEmax[b + 1] - sEmin[b + 1] : 1.0;
                         add = resonant_add(racc, u0, u1, u2, px0, px1, px2, sj, sdg[r], dEb1, sde, cj, b == N - 1);
@@ -1788,23 +1787,53 @@ void k_cascade_gb(GridDev g, const Point* __restrict__ pts, const int* __restric
                 __syncthreads();
             }
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the FIFO stores land before the next pass reads
-        } else if (wave == recw) {
-            // ---- records two / one stage ahead, pw of each point (lane < R) at the lower edge of the stage two ahead
-            const double si_l = lane < R ? pts[gidx[gr.x + lane]].si : 0.0;
+        }
+    } else if (wave == recw) {
+        // ---- phase 1 of the records two stages ahead
+#pragma unroll 1
+        for (int pass = 0; pass < npass; ++pass) {
+            int njp, Ts, c0;
+            pass_geom(pass, njp, Ts, c0);
+            pass_head();
+            phase1(0, lane);
+            if (1 < Ts) phase1(1, lane);
+            __syncthreads();
+            __syncthreads();
             for (int sg = 0; sg < Ts; ++sg) {
                 NUSI_WS_STAMP(sg, 0);
-                if (sg + 2 < Ts) {
-                    phase1(sg + 2, lane);
-                    if (lane < R) pwr[((sg + 2) & 3) * 16 + lane] = nm::exp(-si_l * lx[c0 - 1 - sg]);
-                }
+                if (sg + 2 < Ts) phase1(sg + 2, lane);
+                NUSI_WS_STAMP(sg, 1);
+                __syncthreads();
+            }
+        }
+    } else if (wave == recw + 1) {
+        // ---- phase 2 (the LU of M) one stage ahead, on a wave of its own as in k_cascade_ws<NJ, 2>
+#pragma unroll 1
+        for (int pass = 0; pass < npass; ++pass) {
+            int njp, Ts, c0;
+            pass_geom(pass, njp, Ts, c0);
+            pass_head();
+            __syncthreads();
+            phase2(0, lane);
+            __syncthreads();
+            for (int sg = 0; sg < Ts; ++sg) {
+                NUSI_WS_STAMP(sg, 0);
                 if (sg + 1 < Ts) phase2(sg + 1, lane);
                 NUSI_WS_STAMP(sg, 1);
                 __syncthreads();
             }
-        } else {
-            // ---- push: block q (stage 4q) adds columns c0+1-4q .. c0+4-4q into the rows below r = c0-4q for every
-            // step and point, then publishes rows r-1 .. r-4
-            const int rw0 = wave * 16 * RT;
+        }
+    } else {
+        // ---- push: block q (stage 4q) adds columns c0+1-4q .. c0+4-4q into the rows below r = c0-4q for every
+        // step and point, then publishes rows r-1 .. r-4
+        const int rw0 = wave * 16 * RT;
+#pragma unroll 1
+        for (int pass = 0; pass < npass; ++pass) {
+            int njp, Ts, c0;
+            pass_geom(pass, njp, Ts, c0);
+            pass_head();
+            __syncthreads();
+            __syncthreads();
             nusi_f64x4 acc[RT][NJ];
 #pragma unroll
             for (int a = 0; a < RT; ++a)
@@ -1854,7 +1883,7 @@ void k_cascade_gb(GridDev g, const Point* __restrict__ pts, const int* __restric
                 __syncthreads();
             }
         }
-    }   // passes
+    }
 }
 size_t cascade_gb_scratch_doubles(const GridDev& g) { return (size_t)3 * g.N * 16; }
 
@@ -1945,16 +1974,16 @@ hipError_t launch_cascade_ws(const GridDev& g, const Point* pts, int R, const in
     return hipGetLastError();
 }
 
-// the gamma-batch kernel: push waves of 16 kGbRT rows, two chain waves, one record wave; ~45 KB of LDS at N = 300
+// the gamma-batch kernel: push waves of 16 kGbRT rows, two chain waves, two record waves; ~90 KB of LDS at N = 300
 static int gb_push_waves(const GridDev& g) { return (g.T - 1 + 16 * kGbRT - 1) / (16 * kGbRT); }
 static size_t gb_lds(const GridDev& g)
 {
-    return sizeof(double) * (3 * (size_t)kGbNF * kGbNJ + 64 + 16 * (size_t)kGbNJ * 16 + 96 + (size_t)g.N + (g.T + 2) +
+    return sizeof(double) * (3 * (size_t)kGbNF * kGbNJ + 16 * (size_t)kGbNJ * 16 + 96 + (size_t)g.N + 16 * (size_t)(g.T + 2) +
                              6 * (size_t)g.T + 2 * (size_t)g.N + 4 * (size_t)g.Nz);
 }
 bool cascade_gb_fits(const GridDev& g)
 {
-    return g.T >= 2 && g.Nz >= 2 && gb_push_waves(g) + kGbChainWaves + 1 <= 16 && gb_lds(g) <= 160 * 1024;
+    return g.T >= 2 && g.Nz >= 2 && gb_push_waves(g) + kGbChainWaves + 2 <= 16 && gb_lds(g) <= 160 * 1024;
 }
 hipError_t launch_cascade_gb(const GridDev& g, const Point* pts, const int* gidx, const int2* grp, int nwg, TablesDev t,
                              double* fh, double* flux, double* flux_fla, hipStream_t s)
@@ -1962,7 +1991,7 @@ hipError_t launch_cascade_gb(const GridDev& g, const Point* pts, const int* gidx
     if (!cascade_gb_fits(g)) return hipErrorInvalidValue;
     if (nwg <= 0) return hipSuccess;
     t_cascade_kernel = "k_cascade_gb";
-    const int nthr = 64 * (gb_push_waves(g) + kGbChainWaves + 1);
+    const int nthr = 64 * (gb_push_waves(g) + kGbChainWaves + 2);
     hipLaunchKernelGGL((k_cascade_gb<kGbNJ>), dim3(nwg), dim3(nthr), gb_lds(g), s, g, pts, gidx, grp, t, fh, flux,
                        flux_fla);
     return hipGetLastError();

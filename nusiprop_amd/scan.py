@@ -104,10 +104,50 @@ def cascade_bytes_per_point(N, Nz):
 WSP_NJ, WSP_RT = 16, 8   # the step-pass cascade (k_cascade_wsp): step slots per pass, 16-row tiles per push wave
 
 
-def cascade_passes(N, Nz):
-    """The step-pass cascade's passes: (first step slot jb, stages Ts, column of local stage 0 c0)."""
+def cascade_passes(N, Nz, nj=None):
+    """The step-pass cascade's passes: (first step slot jb, stages Ts, column of local stage 0 c0); nj steps per pass
+    (default the step-pass kernel's, GB_NJ for the gamma batch)."""
+    nj = nj or WSP_NJ
     T, nst = N + Nz - 2, Nz - 1
-    return [(jb, N - 1 + min(WSP_NJ, nst - jb), T - 1 - jb) for jb in range(0, nst, WSP_NJ)]
+    return [(jb, N - 1 + min(nj, nst - jb), T - 1 - jb) for jb in range(0, nst, nj)]
+
+
+GB_NJ, GB_RT = 6, 2   # the gamma batch (k_cascade_gb): steps per pass, 16-row tiles per push wave
+
+
+def gamma_batches(points, rhs=16):
+    """The gamma-batch workgroups nusi_plan_evolve forms (NUSI_OPT_CASCADE_RHS = rhs >= 3): per table, its
+    power-law points in near-equal batches of <= rhs when there are at least 3.  Returns the batch sizes."""
+    from collections import Counter
+    cnt = Counter(table_key(p) for p in points if p.get("source_model", 0) == 1)
+    out = []
+    for c in cnt.values():
+        if c >= 3:
+            nb = -(-c // rhs)
+            out += [c * (k + 1) // nb - c * k // nb for k in range(nb)]
+    return out
+
+
+def cascade_gb_bytes_per_batch(N, Nz):
+    """HBM bytes one gamma-batch workgroup must read: the columns each pass visits (as the step-pass kernel), Gamma
+    and alphaTilde; the FIFO of the passes' last step stays in L2/MALL (3 N x 16 doubles per pass, written once,
+    read once) and the fluxes are counted per point (6 N x 8 B)."""
+    T = N + Nz - 2
+    cols = 0
+    for jb, Ts, c0 in cascade_passes(N, Nz, GB_NJ):
+        lo = max(1, c0 + 1 - 4 * ((Ts - 1) // 4))
+        cols += sum(range(lo, min(c0 + 1, T - 1) + 1))
+    return 8 * (cols + 2 * T)
+
+
+def cascade_gb_flops_per_batch(N, Nz):
+    """fp64 matrix-core flops one gamma-batch workgroup issues: per pass and block q >= 1, one v_mfma_f64_16x16x4f64
+    (16 rows x 16 points x 4 columns, 2048 flops) per row tile below r = c0 - 4q and per step tile (GB_NJ)."""
+    T = N + Nz - 2
+    ntile = -(-(T - 1) // (16 * GB_RT)) * GB_RT
+    tiles = sum(min(ntile, -(-(c0 - 4 * q) // 16)) for jb, Ts, c0 in cascade_passes(N, Nz, GB_NJ)
+                for q in range(1, (Ts - 1) // 4 + 1) if c0 - 4 * q > 0)
+    return tiles * GB_NJ * 2 * 16 * 16 * 4
 
 
 def cascade_min_bytes_per_point(N, Nz, passes=False):

@@ -380,6 +380,7 @@ def test_plan_kernels_names(nusi):
     for kind in (_lib.CASCADE_AUTO, _lib.CASCADE_MFMA):
         assert run(100, 12.0, two, kind) == ("k_alpha_batch", "k_cascade_ws")
         assert run(100, 12.0, [dict(mphi=6e5, g=0.01, si=s) for s in (2.0, 2.5)], kind)[1] == "k_cascade_ws_mrhs"
+        assert run(100, 12.0, [dict(mphi=6e5, g=0.01, si=s) for s in (2.0, 2.5, 2.7)], kind)[1] == "k_cascade_gb"
         assert run(700, 12.0, two, kind)[1] == "k_cascade_ws_passes"
         assert run(100, 12.0, [dict(mphi=6e5, g=0.01, source_model=0, non_resonant=False)], kind)[1] == "k_cascade_ws"
     assert run(100, 12.0, two, _lib.CASCADE_WAVEFRONT)[1] == "k_cascade_wf"
@@ -389,17 +390,20 @@ def test_plan_kernels_names(nusi):
 
 def test_c5_gamma_block_vs_oracle(nusi, oracle_mod):
     """BASELINE config 5: one full 16-gamma block of scan.c5_points() (N_E = 300, power law; one
-    Stage-A table, 8 pairs on the multi-RHS cascade) against the oracle -- its tables once, its
-    cascade per gamma -- to FLUX_RTOL with the same exact zeros; and the block through the
-    one-point-per-workgroup kernel bit for bit (A/B)."""
+    Stage-A table, the gamma batch k_cascade_gb by default) against the oracle -- its tables once, its
+    cascade per gamma -- to FLUX_RTOL with the same exact zeros; the pairs on the multi-RHS kernel give
+    the one-point-per-workgroup fluxes bit for bit (A/B), the gamma batch to rounding."""
     from nusiprop_amd import scan
     allp = scan.c5_points()
     blk = allp[16 * 1234:16 * 1235]
     assert len({scan.table_key(p) for p in blk}) == 1 and len({p["si"] for p in blk}) == 16
     flux, fla, names = _evolve_opts(nusi, blk)
-    assert names[1] == "k_cascade_ws_mrhs"
+    assert names[1] == "k_cascade_gb"
     ref1 = _evolve_opts(nusi, blk, cascade_rhs=1)
-    assert np.array_equal(flux, ref1[0]) and np.array_equal(fla, ref1[1])
+    two = _evolve_opts(nusi, blk, cascade_rhs=2)
+    assert two[2][1] == "k_cascade_ws_mrhs"
+    assert np.array_equal(two[0], ref1[0]) and np.array_equal(two[1], ref1[1])
+    assert cases.rel_err(flux, ref1[0]) <= FLUX_RTOL and np.array_equal(flux == 0, ref1[0] == 0)
     o = oracle_mod.Oracle(**cases.oracle_kwargs(blk[0]))
     G, aT, al = o.tables()
     for k, p in enumerate(blk):

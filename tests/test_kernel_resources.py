@@ -21,6 +21,7 @@ BUDGET = {
     r"k_cascade_wsILi48ELi2E": (0, 0),
     r"k_cascade_wspILi16E": (20, 96),        # the pivoting-LU fallback's indexed rows, a cold path
     r"k_cascade_wfILi\d+ELb1E": (0, 0),
+    r"k_cascade_gbILi6E": (8, 48),             # a few chain values around the solve
     r"k_alpha_batchILb[01]E": (64, 1024),      # call frames of the out-of-line per-batch phases
 }
 
