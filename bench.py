@@ -46,6 +46,9 @@ def parse():
     ap.add_argument("--points", type=int, default=0, help="points per GPU (default: 1024 for c4 and c3, 8192 for c5, 1 for c2)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="budget of the oracle CPU baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-secondary", action="store_true",
+                    help="skip the C5 and C3 lines the default C4 run adds (secondary_lines: each its own child "
+                         "process, a few steps, after the timed region)")
     ap.add_argument("--cascade", default="auto", choices=["auto", "mfma", "wf"],
                     help="cascade kernel: auto = the library default (= mfma: the warp-specialised wavefront with "
                          "the push on the fp64 matrix cores), wf = the bit-exact scalar wavefront")
@@ -253,6 +256,27 @@ def launch_ranks(args):
            "--master-addr", "127.0.0.1", "--master-port", str(free_port()), os.path.abspath(__file__)] + sys.argv[1:]
     print("bench.py: launching %d ranks: %s" % (args.gpus, " ".join(cmd)), file=sys.stderr, flush=True)
     return subprocess.call(cmd)
+
+
+def secondary_lines(local):
+    """BASELINE configs 5 and 3 measured beside the headline C4 line, each by a child bench.py process on the same
+    GPU after the C4 timed region (so the driver's run records them too): props/s, stage times, kernels."""
+    import subprocess
+    out = {}
+    env = dict(os.environ, HIP_VISIBLE_DEVICES=os.environ.get("HIP_VISIBLE_DEVICES", str(local)))
+    for wl, steps in (("c5", 10), ("c3", 3)):
+        cmd = [sys.executable, os.path.abspath(__file__), "--workload", wl, "--steps", str(steps), "--warmup", "1",
+               "--no-cpu-baseline", "--no-secondary"]
+        try:
+            r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env)
+            d = json.loads(r.stdout.strip().splitlines()[-1])
+            out[wl] = {k: d.get(k) for k in ("value", "unit", "ms_per_step", "steps", "stage_ms_per_step")}
+            out[wl]["workload"] = d["config"]["workload"]
+            out[wl]["kernels"] = [d["config"]["alpha_kernel"], d["config"]["cascade_kernel"]]
+            out[wl]["roofline"] = {k: d["roofline"].get(k) for k in ("kernel", "achieved", "unit", "frac", "traffic")}
+        except Exception as e:   # a secondary line never fails the headline run
+            out[wl] = {"error": "%s: %s" % (type(e).__name__, e)}
+    return out
 
 
 def file_sha256(path):
@@ -472,6 +496,8 @@ def main():
     if args.workload in ("c1", "c2") and rank == 0:
         out["single_propagation"] = single_point_latency(pts[0], max(20, args.steps))
         out["single_propagation"]["plan_ms_per_step"] = dt / args.steps * 1e3
+    if rank == 0 and world == 1 and args.workload == "c4" and not args.no_secondary and not args.points:
+        out["secondary_lines"] = secondary_lines(local)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(pts, args.cpu_seconds)
         if args.workload == "c1":
