@@ -825,10 +825,6 @@ NUSI_FN double resonant_add(double& racc, double u0, double u1, double u2, doubl
 // push waves not publishing spread their block MFMAs over the block's stages: k_cascade_wsp yes (C3 cascade
 // 37.3 -> 36.0 ms), k_cascade_ws no (C4 0.698 -> 0.728, C5 4.58 -> 4.93 ms; profiles/r2q)
 constexpr bool kWsStagger = false, kWspStagger = true;
-#ifndef NUSI_WS_P2TOP
-#define NUSI_WS_P2TOP 0
-#endif
-constexpr bool kWsP2Top = NUSI_WS_P2TOP;   // R = 1: phase 2 on the top push wave once its rows are consumed (A/B)
 constexpr int kWsP2Wave = 1;   // R = 2: the LU phase of the records on a wave of its own (nw-3), not the chain (A/B: C5 cascade 5.75 -> 4.49 ms)
 template <int R> struct WsCfg;
 template <> struct WsCfg<1> { static constexpr int RT = 4, kMaxThreads = 512; };   // 6 push waves + 2
@@ -986,10 +982,8 @@ void k_cascade_ws(GridDev g, const Point* __restrict__ pts, const int2* __restri
     if (wave == (kP2 ? nw - 3 : nw - 1)) phase2(0, lane);
     __syncthreads();
 
-    // R = 1: phase 2 of stage sg+1 runs on the chain wave until the top push wave (nw-3) has no rows left to push
-    // or publish (its rows all >= the block's column r = T-1-4q), then on that wave
-    const int top_rw0 = (nw - 3) * 16 * RT;
-    auto p2_on_top = [&](int sg) { return kWsP2Top && !kP2 && top_rw0 >= T - 1 - 4 * (sg >> 2); };
+    // R = 1: phase 2 of stage sg+1 runs on the chain wave (on the top push wave once its rows were consumed, the
+    // LU code entered the push branch and spilled its accumulators: C4 cascade 0.706 -> 2.93 ms, profiles/r3/r3f)
     if (wave == nw - 1) {
         // ---- chain: lane j solves (step j, bin N-1-sg+j) of every point at stage sg
         const int j = lane;
@@ -1025,7 +1019,7 @@ void k_cascade_ws(GridDev g, const Point* __restrict__ pts, const int2* __restri
             double Tn[R];
 #pragma unroll
             for (int p = 0; p < R; ++p) Tn[p] = 0.0;
-            if (!kP2 && sg + 1 < T && !p2_on_top(sg)) phase2(sg + 1, j);   // independent of this stage's solve
+            if (!kP2 && sg + 1 < T) phase2(sg + 1, j);   // independent of this stage's solve
             if (act && b >= 0 && b < N) {
                 const double* Rc = rec + (sg % 3) * NJ + j;
                 constexpr int S = S3;
@@ -1135,12 +1129,6 @@ void k_cascade_ws(GridDev g, const Point* __restrict__ pts, const int2* __restri
             // stages later by the others (their rows are needed >= 5 stages on; the T_j ring keeps 8):
             // the matrix-core work of a block is spread over its four stages (kWsStagger)
             const int q = sg >> 2, r = T - 1 - 4 * q, hi = r - 1;
-            if (wave == nw - 3 && p2_on_top(sg)) {   // (uniform: this wave's rows are all consumed)
-                if (sg + 1 < T) phase2(sg + 1, lane);
-                NUSI_WS_STAMP(sg, 1);
-                __syncthreads();
-                continue;
-            }
             const bool crit = rw0 <= hi && rw0 + 16 * RT - 1 >= hi - 3;
             const int dw = (!kWsStagger || crit) ? 0 : 1 + wave % 3;
             if ((sg & 3) == dw && nonres) {

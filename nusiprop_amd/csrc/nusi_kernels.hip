@@ -207,7 +207,6 @@ __global__ __launch_bounds__(kTileThreads) NUSI_TILE_ATTR void k_alpha_tile(Grid
     }
     for (int k = 0; k < 3; ++k) {
         __syncthreads();   // edge leaves written / previous k's corners consumed
-#ifndef NUSI_AB_NO_CORNERS   // timing experiments only (scripts/build_variant.sh)
         if (nonres && maj) {
             const double* edgk = edg + k * alpha_tile_edge_stride(cs, ct);
             for (int j = tid; j < cc; j += kTileThreads) {   // corner j: shared leaves, then each point's
@@ -218,7 +217,6 @@ __global__ __launch_bounds__(kTileThreads) NUSI_TILE_ATTR void k_alpha_tile(Grid
             for (int j = tid; j < kAlphaTile * (cs + ct); j += kTileThreads)
                 alpha_tile_mixed_job(j, edgk, ct, cs, G, tl, th, sl, sh, n0, m0, Tn, Tm, cor);
         }
-#endif
         __syncthreads();
         if (needed) {
             // the t and tu channels' brackets depend on the shared leaves only: once per entry
@@ -232,12 +230,8 @@ __global__ __launch_bounds__(kTileThreads) NUSI_TILE_ATTR void k_alpha_tile(Grid
             for (int q = 0; q < nb; ++q) {
                 double tot = (G > 1) ? tsum[q * kTileThreads + tid] : tot1;
                 int w = 0;
-#ifdef NUSI_AB_NO_COMBINE
-                tot += cor[(tid * 7) % cc] + edg[tid % 64];
-#else
                 const TileLeaves lv = alpha_tile_leaves(cor, edg, k, q, G, cs, ct, lm, sl, sh, tl, th, ln);
                 alpha_k(pts[p0 + q], spl, k, g.lo[n], g.hi[n], g.lo[m], g.hi[m], lv, tot, w, share ? &pre : nullptr);
-#endif
                 if (G > 1) tsum[q * kTileThreads + tid] = tot;
                 else tot1 = tot;
                 if (w) atomicOr(&warn[p0 + q], w);
@@ -281,33 +275,17 @@ static_assert(kXFields * (kAlphaTile + 1) * (kAlphaTile + 1) >= 4 * (kAlphaTile 
               "the bracket phase's blocks fit X");
 static_assert(kBatchQC * (2 * (kAlphaTile + 1) + kAlphaTile) <= kTileThreads, "one member-edge round per chunk");
 
-#ifndef NUSI_AB_BATCH   // timing experiments only: 1 skip the member corner leaves, 2 skip the combine, 4 skip brackets,
-                        // 16 skip the member edges, 32 skip the shared corner / mixed / member-coefficient phases
-#define NUSI_AB_BATCH 0
-#endif
 #ifndef NUSI_BATCH_WAVES
 #define NUSI_BATCH_WAVES 4
 #endif
-// the batch-shared phases out of line: they run once per batch, and inlined their working sets would
-// raise the register pressure of the per-point loop (NUSI_BATCH_OUTLINE=0: inline, A/B)
-#ifndef NUSI_BATCH_OUTLINE
-#define NUSI_BATCH_OUTLINE 1
-#endif
-#if NUSI_BATCH_OUTLINE
+// the batch-shared phases out of line: they run once per batch, and inlined their working sets raise the register
+// pressure of the per-point loop (measured slower: round 1 profiles/r1e, round 2 profiles/r2s, r2aa)
 #define NUSI_BCOLD __device__ __attribute__((noinline))
-#else
-#define NUSI_BCOLD __device__ inline
-#endif
 NUSI_BCOLD void b_corner(int j, const double* edgk, int ct, int cs, double* per, double* tmp)
 {
     alpha_batch_corner_job(j, edgk, ct, cs, per, tmp);
 }
 NUSI_BCOLD void b_xshared(int j, const double* edgk, int ct, int cs, double* X) { alpha_batch_xshared_job(j, edgk, ct, cs, X); }
-NUSI_BCOLD void b_medge(const Point& P, int k, int job, const double* tE, int ct, const double* sE, int cs,
-                        const double* lo, const double* hi, int m0, int Tm, double* memb)
-{
-    alpha_batch_medge_job(P, k, job, tE, ct, sE, cs, lo, hi, m0, Tm, memb);
-}
 // (returned by value: an out parameter's address would keep the caller's copy in scratch, reloaded by every
 // point's combine)
 NUSI_BCOLD AlphaPre b_pre(const Point& P, int k, double Em, double Ep, double Emp, double Epp, SplitLeaves lv)
@@ -325,12 +303,6 @@ __global__ __launch_bounds__(256) void k_alpha_medge(GridDev g, const Point* __r
     alpha_medge_job(pts[p], k, j, T, g.lo, g.hi, med + ((size_t)p * 3 + k) * kMedFields * T);
 }
 
-#ifndef NUSI_ALPHA_XCD   // 1: k_alpha_batch's blocks remapped so that each XCD runs contiguous (batch, tile) ranges
-#define NUSI_ALPHA_XCD 0    // (A/B, profiles/r2s: C4 alpha 5.97 -> 6.09 ms, C3 90.7 -> 94.4 ms; the dealt order wins)
-#endif
-#ifndef NUSI_MEDGE_GLOBAL   // 1: member edges copied from k_alpha_medge's table; 0: evaluated per tile (A/B)
-#define NUSI_MEDGE_GLOBAL 1
-#endif
 
 template <bool kPP>   // the batches' tables have the phi-phi channel (its shared term per k)
 __global__ __launch_bounds__(kTileThreads) __attribute__((amdgpu_waves_per_eu(NUSI_BATCH_WAVES, NUSI_BATCH_WAVES)))
@@ -344,17 +316,9 @@ void k_alpha_batch(GridDev g, const Point* __restrict__ pts, SplineSet spl, cons
     __shared__ int cnt[2];
     __shared__ double elo[2][kAlphaTile], ehi[2][kAlphaTile];
     const int tid = threadIdx.x, T = g.T;
-    // XCD-aware order: blocks are dealt round-robin over the 8 XCDs (b and b + 8 share one), so the
-    // linear block id is remapped to make each XCD run a contiguous range of (batch, tile) -- the tiles
-    // of one batch read the same member-edge blocks (k_alpha_medge) and share them in that XCD's L2
-    int bx = blockIdx.x, by = blockIdx.y;
-    if (NUSI_ALPHA_XCD) {
-        const int nbk = gridDim.x * gridDim.y, L = by * gridDim.x + bx;
-        const int xcd = L & 7, slot = L >> 3, q8 = nbk >> 3, rem = nbk & 7;
-        const int M = xcd < rem ? xcd * (q8 + 1) + slot : rem * (q8 + 1) + (xcd - rem) * q8 + slot;
-        by = M / gridDim.x;
-        bx = M - by * gridDim.x;
-    }
+    // (an XCD-contiguous remap of the blocks measured slower than the dealt order: C4 alpha 5.97 -> 6.09 ms,
+    // profiles/r2s)
+    const int bx = blockIdx.x, by = blockIdx.y;
     const int bw = batches[by];
     const int p0 = bw & 0xffffff, nb = (int)((unsigned)bw >> 24);   // tables p0 .. p0 + nb - 1
     const unsigned tu = (unsigned)tiles[bx];                         // tile word, as in k_alpha_tile
@@ -376,7 +340,7 @@ void k_alpha_batch(GridDev g, const Point* __restrict__ pts, SplineSet spl, cons
     __syncthreads();
     const int ct = cnt[0], cs = cnt[1], cc = cs * ct;
     __shared__ int tsrc[2 * kAlphaTile], ssrc[2 * kAlphaTile];   // bin edge (2 b + side) behind each list slot
-    if (NUSI_MEDGE_GLOBAL && tid < 2 * kAlphaTile) {
+    if (tid < 2 * kAlphaTile) {
         const int side = tid / kAlphaTile, j = tid - side * kAlphaTile, b0 = side ? m0 : n0;
         const int* il = side ? sl : tl;
         const int* ih = side ? sh : th;
@@ -417,11 +381,9 @@ void k_alpha_batch(GridDev g, const Point* __restrict__ pts, SplineSet spl, cons
         AlphaPre pre{};
         PPTerm ppt{0.0, 1.0, 1.0};
         if (cornered) {
-            if (!(NUSI_AB_BATCH & 32)) {
-                for (int j = tid; j < cc; j += kTileThreads) b_corner(j, edgk, ct, cs, P3, tmp);
-                for (int j = tid; j < kAlphaTile * (cs + ct); j += kTileThreads)
-                    alpha_batch_mixed_job(j, edgk, ct, cs, tl, th, sl, sh, n0, m0, T, Tm, mix, mix + kAlphaTile * cs);
-            }
+            for (int j = tid; j < cc; j += kTileThreads) b_corner(j, edgk, ct, cs, P3, tmp);
+            for (int j = tid; j < kAlphaTile * (cs + ct); j += kTileThreads)
+                alpha_batch_mixed_job(j, edgk, ct, cs, tl, th, sl, sh, n0, m0, T, Tm, mix, mix + kAlphaTile * cs);
             __syncthreads();
             if (needed) {
                 SplitLeaves lv;
@@ -433,18 +395,16 @@ void k_alpha_batch(GridDev g, const Point* __restrict__ pts, SplineSet spl, cons
                 lv.ted = edgk; lv.sed = edgk + kTEdgeFields * ct; lv.mbv = lv.sed + kSEdgeFields * cs;
                 lv.tedm = membq; lv.sedm = membq + ct; lv.mbm = membq + ct + 2 * cs; lv.marg = membq;   // (not read)
                 lv.xl = mix; lv.yl = mix + kAlphaTile * cs;
-                if (NUSI_AB_BATCH & 4) pre = AlphaPre{lv.cf[1][tid % cc], lv.cf[2][tid % cc], 1.0, 1.0};
-                else pre = b_pre(P, k, g.lo[n], g.hi[n], g.lo[m], g.hi[m], lv);
+                pre = b_pre(P, k, g.lo[n], g.hi[n], g.lo[m], g.hi[m], lv);
                 if (kPP) ppt = alpha_k_pp(P, spl, k, g.lo[n], g.hi[n], g.lo[m], g.hi[m], lv, wsh);
             }
             __syncthreads();   // X is rewritten with the member coefficients
-            if (!(NUSI_AB_BATCH & 32))
-                for (int j = tid; j < cc; j += kTileThreads) b_xshared(j, edgk, ct, cs, X);
+            for (int j = tid; j < cc; j += kTileThreads) b_xshared(j, edgk, ct, cs, X);
         }
         // ---- the points, kBatchQC at a time: their member edge leaves in one round, then point by point.
         // A point's entry accumulates over the mass states in A; the sum of the states < k is loaded one
         // point ahead (timed equal to loading it in place, profiles/r2m: four blocks per CU already hide it).
-        const bool reload = k > 0 && needed && !(NUSI_AB_BATCH & 8);
+        const bool reload = k > 0 && needed;
         double tnext = reload ? A[(size_t)p0 * g.PT + eidx] : 0.0;
         // member edges: thread (mq, mjob) copies job mjob of point mq of each chunk (loading the next chunk's
         // values a chunk ahead measured slower: their registers stay live through the combine)
@@ -453,15 +413,11 @@ void k_alpha_batch(GridDev g, const Point* __restrict__ pts, SplineSet spl, cons
         for (int q0 = 0; q0 < nb; q0 += kBatchQC) {
             const int nq = (nb - q0 < kBatchQC) ? nb - q0 : kBatchQC;
             __syncthreads();   // the previous chunk is done with membq (and mem)
-            if (mq < nq && !(NUSI_AB_BATCH & 16)) {
-                if (NUSI_MEDGE_GLOBAL) {
-                    MedVals mv{};
-                    alpha_batch_medge_load(nonres, mjob, tsrc, ct, ssrc, cs, m0, Tm, T,
-                                           med + ((size_t)(p0 + q0 + mq) * 3 + k) * kMedFields * T, mv);
-                    alpha_batch_medge_store(nonres, mjob, ct, cs, m0, Tm, mv, membq + mq * mbd);
-                } else {
-                    b_medge(pts[p0 + q0 + mq], k, mjob, tE, ct, sE, cs, g.lo, g.hi, m0, Tm, membq + mq * mbd);
-                }
+            if (mq < nq) {
+                MedVals mv{};
+                alpha_batch_medge_load(nonres, mjob, tsrc, ct, ssrc, cs, m0, Tm, T,
+                                       med + ((size_t)(p0 + q0 + mq) * 3 + k) * kMedFields * T, mv);
+                alpha_batch_medge_store(nonres, mjob, ct, cs, m0, Tm, mv, membq + mq * mbd);
             }
 #pragma unroll 1
             for (int qq = 0; qq < nq; ++qq) {
@@ -471,7 +427,7 @@ void k_alpha_batch(GridDev g, const Point* __restrict__ pts, SplineSet spl, cons
                 double tot = tnext;   // after states < k
                 if (reload && q + 1 < nb) tnext = A[(size_t)(p0 + q + 1) * g.PT + eidx];
                 __syncthreads();   // member edges written / the previous point's combine is done with mem
-                if (cornered && !(NUSI_AB_BATCH & 1))
+                if (cornered)
                     for (int j = tid; j < cc; j += kTileThreads) alpha_batch_mcorner_job(Q, j, edgk, ct, cs, X, memb, mem);
                 __syncthreads();   // mem of q written
                 int w = 0;
@@ -486,11 +442,10 @@ void k_alpha_batch(GridDev g, const Point* __restrict__ pts, SplineSet spl, cons
                     lv.tedm = memb; lv.sedm = memb + ct; lv.mbm = memb + ct + 2 * cs;
                     lv.marg = memb + ct + 2 * cs + kAlphaTile + 2 * ct;   // sT | fT | sS | fS
                     lv.xl = mix; lv.yl = mix;   // (not read with pre)
-                    if (NUSI_AB_BATCH & 2) tot += mem[(tid * 7) % cc] + memb[tid % ct] + pre.Bt;
-                    else alpha_k(Q, spl, k, g.lo[n], g.hi[n], g.lo[m], g.hi[m], lv, tot, w, cornered ? &pre : nullptr,
-                                 kPP && cornered ? &ppt : nullptr);
+                    alpha_k(Q, spl, k, g.lo[n], g.hi[n], g.lo[m], g.hi[m], lv, tot, w, cornered ? &pre : nullptr,
+                            kPP && cornered ? &ppt : nullptr);
                 }
-                if (valid && (!(NUSI_AB_BATCH & 8) || k == 2)) A[(size_t)(p0 + q) * g.PT + eidx] = needed ? tot : 0.0;
+                if (valid) A[(size_t)(p0 + q) * g.PT + eidx] = needed ? tot : 0.0;
                 if (w) atomicOr(&warn[p0 + q], w);
             }
         }
@@ -621,7 +576,7 @@ hipError_t launch_alpha(const GridDev& g, const Point* pts, int npts, const Spli
             if (c == 0) {   // batches [0, nb_plain) without the phi-phi channel, then those with it
                 const size_t lds = sizeof(double) * (size_t)alpha_batch_lds_doubles();
                 if (cs > kAlphaTile + 1 || ct > kAlphaTile + 1) return hipErrorInvalidValue;
-                if (NUSI_MEDGE_GLOBAL) {
+                {
                     if (!t.Med) return hipErrorInvalidValue;
                     hipLaunchKernelGGL(k_alpha_medge, dim3((unsigned)((5 * g.T + 255) / 256), npts, 3), dim3(256), 0, s,
                                        g, pts, t.Med);

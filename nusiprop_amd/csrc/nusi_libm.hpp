@@ -84,9 +84,6 @@ NUSI_FN double log_kernel(unsigned long long ix, double c, int kadj)
 
 NUSI_FN double log_i(double x)
 {
-#ifdef NUSI_AB_STUB_LOG   // timing experiments only (scripts/build_variant.sh)
-    return (x - 1.0) * 0.9;
-#endif
     const unsigned long long ix = bits(x);
     if (ix - 0x0010000000000000ULL >= 0x7fe0000000000000ULL) {   // not a normal positive double
         if (x != x || x == 1.0 / 0.0) return x + x;
@@ -100,9 +97,6 @@ NUSI_FN double log_i(double x)
 // log1p(x) = log(u) + c / u, u = 1 + x rounded, c its exact rounding error (Fast2Sum)
 NUSI_FN double log1p_i(double x)
 {
-#ifdef NUSI_AB_STUB_LOG
-    return x * 0.9;
-#endif
     if (!(x > -1.0) || x == 1.0 / 0.0) {
         if (x == -1.0) return -1.0 / 0.0;
         if (x != x || x > 0.0) return x + x;
@@ -161,9 +155,6 @@ NUSI_FN double exp_i(double x)
 // s_atan.c
 NUSI_FN double atan_i(double x)
 {
-#ifdef NUSI_AB_STUB_ATAN
-    return x * 0.9;
-#endif
     constexpr double atanhi[4] = {4.63647609000806093515e-01, 7.85398163397448278999e-01, 9.82793723247329054082e-01,
                                   1.57079632679489655800e+00};
     constexpr double atanlo[4] = {2.26987774529616870924e-17, 3.06161699786838301793e-17, 1.39033110312309984516e-17,
@@ -222,9 +213,6 @@ NUSI_FN double atan_i(double x)
 // e_atan2.c
 NUSI_FN double atan2_i(double y, double x)
 {
-#ifdef NUSI_AB_STUB_ATAN
-    return y * 0.9 + x * 0.1;
-#endif
     constexpr double pi_o_2 = 1.5707963267948965580E+00, pi = 3.1415926535897931160E+00,
                      pi_lo = 1.2246467991473531772E-16, pi_o_4 = 7.8539816339744827900E-01;
     const int hx = hiw(x), hy = hiw(y);

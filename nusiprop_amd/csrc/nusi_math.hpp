@@ -109,9 +109,6 @@ NUSI_FN double li2_useries(double u)
 // Re Li2(x) for real x (gsl_sf_dilog semantics)
 NUSI_FN_OUT double li2(double x)
 {
-#ifdef NUSI_AB_STUB_LI2   // timing experiments only (scripts/build_variant.sh)
-    return 0.5 * x;
-#endif
     double add = 0.0, sgn = 1.0;
     if (fabs(x) > 1.0) {   // x > 1: 2 zeta2 - log^2(x)/2 ; x < -1: -zeta2 - log^2(-x)/2 (one log for both)
         const double L = NUSI_PLOG(fabs(x));
@@ -227,9 +224,6 @@ NUSI_FN cd cli2_body(double x, double y)
         const double ax = fabs(x), a1 = fabs(1.0 - x);
         if (fabs(y) <= kLi2AxisRatio * (ax < a1 ? ax : a1)) return cli2_axis(x, y);
     }
-#ifdef NUSI_AB_STUB_CLI2   // timing experiments only
-    return C(0.5 * x, 0.5 * y);
-#endif
     cd z = C(x, y), add = C(0.0), lz;
     double sgn = 1.0;
     bool have_lz = false;
