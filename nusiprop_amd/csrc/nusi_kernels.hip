@@ -286,10 +286,31 @@ NUSI_BCOLD void b_corner(int j, const double* edgk, int ct, int cs, double* per,
     alpha_batch_corner_job(j, edgk, ct, cs, per, tmp);
 }
 NUSI_BCOLD void b_xshared(int j, const double* edgk, int ct, int cs, double* X) { alpha_batch_xshared_job(j, edgk, ct, cs, X); }
-// (returned by value: an out parameter's address would keep the caller's copy in scratch, reloaded by every
-// point's combine)
-NUSI_BCOLD AlphaPre b_pre(const Point& P, int k, double Em, double Ep, double Emp, double Epp, SplitLeaves lv)
+// The leaves the batch's shared brackets read (alpha_k_pre, alpha_k_pp): the shared corner blocks P3 | tmp, the
+// edge block edgk and the mixed logs; no member leaf
+NUSI_FN SplitLeaves batch_bracket_leaves(const double* P3, const double* tmp, const double* mix, const double* edgk,
+                                         int cs, int ct, int lm, int ln, int s0, int s1, int t0, int t1)
 {
+    const int cc = cs * ct;
+    SplitLeaves lv;
+    lv.cf[0] = P3; lv.cf[1] = tmp; lv.cf[2] = tmp + cc; lv.cf[3] = tmp + 2 * cc; lv.cf[4] = tmp + 3 * cc;
+    lv.cf[5] = P3 + cc; lv.cf[6] = P3 + 2 * cc;
+    lv.corm = P3;   // (not read by the brackets)
+    lv.cc = cc; lv.ct = ct; lv.cs = cs; lv.mb = lm; lv.nb = ln;
+    lv.sidx[0] = s0; lv.sidx[1] = s1; lv.tidx[0] = t0; lv.tidx[1] = t1;
+    lv.ted = edgk; lv.sed = edgk + kTEdgeFields * ct; lv.mbv = lv.sed + kSEdgeFields * cs;
+    lv.tedm = P3; lv.sedm = P3; lv.mbm = P3; lv.marg = P3;   // (not read)
+    lv.xl = mix; lv.yl = mix + kAlphaTile * cs;
+    return lv;
+}
+// (returned by value: an out parameter's address would keep the caller's copy in scratch, reloaded by every
+// point's combine; the leaves are built here from scalars -- a SplitLeaves argument is passed in memory, and its
+// per-lane copy was ~200 B of scratch stores per thread and mass state)
+NUSI_BCOLD AlphaPre b_pre(const Point& P, int k, double Em, double Ep, double Emp, double Epp, const double* P3,
+                          const double* tmp, const double* mix, const double* edgk, int cs, int ct, int lm, int ln,
+                          int s0, int s1, int t0, int t1)
+{
+    const SplitLeaves lv = batch_bracket_leaves(P3, tmp, mix, edgk, cs, ct, lm, ln, s0, s1, t0, t1);
     AlphaPre pre;
     alpha_k_pre(P, k, Em, Ep, Emp, Epp, lv, pre);
     return pre;
@@ -386,22 +407,21 @@ void k_alpha_batch(GridDev g, const Point* __restrict__ pts, SplineSet spl, cons
                 alpha_batch_mixed_job(j, edgk, ct, cs, tl, th, sl, sh, n0, m0, T, Tm, mix, mix + kAlphaTile * cs);
             __syncthreads();
             if (needed) {
-                SplitLeaves lv;
-                lv.cf[0] = P3; lv.cf[1] = tmp; lv.cf[2] = tmp + cc; lv.cf[3] = tmp + 2 * cc; lv.cf[4] = tmp + 3 * cc;
-                lv.cf[5] = P3 + cc; lv.cf[6] = P3 + 2 * cc;
-                lv.corm = P3;   // (no member leaf is read by the brackets)
-                lv.cc = cc; lv.ct = ct; lv.cs = cs; lv.mb = lm; lv.nb = ln;
-                lv.sidx[0] = sl[lm]; lv.sidx[1] = sh[lm]; lv.tidx[0] = tl[ln]; lv.tidx[1] = th[ln];
-                lv.ted = edgk; lv.sed = edgk + kTEdgeFields * ct; lv.mbv = lv.sed + kSEdgeFields * cs;
-                lv.tedm = membq; lv.sedm = membq + ct; lv.mbm = membq + ct + 2 * cs; lv.marg = membq;   // (not read)
-                lv.xl = mix; lv.yl = mix + kAlphaTile * cs;
-                pre = b_pre(P, k, g.lo[n], g.hi[n], g.lo[m], g.hi[m], lv);
-                if (kPP) ppt = alpha_k_pp(P, spl, k, g.lo[n], g.hi[n], g.lo[m], g.hi[m], lv, wsh);
+                pre = b_pre(P, k, g.lo[n], g.hi[n], g.lo[m], g.hi[m], P3, tmp, mix, edgk, cs, ct, lm, ln, sl[lm], sh[lm],
+                            tl[ln], th[ln]);
+                if (kPP) {
+                    const SplitLeaves lv = batch_bracket_leaves(P3, tmp, mix, edgk, cs, ct, lm, ln, sl[lm], sh[lm],
+                                                                tl[ln], th[ln]);
+                    ppt = alpha_k_pp(P, spl, k, g.lo[n], g.hi[n], g.lo[m], g.hi[m], lv, wsh);
+                }
             }
             __syncthreads();   // X is rewritten with the member coefficients
             for (int j = tid; j < cc; j += kTileThreads) b_xshared(j, edgk, ct, cs, X);
         }
         // ---- the points, kBatchQC at a time: their member edge leaves in one round, then point by point.
+        // (Each wave owning 4 m rows of the tile, with its own block of member corners and no workgroup barrier in
+        // the point loop, measured slower: C4 alpha 9.6 ms, the per-wave corner rows and the values live across the
+        // loop spill at 4 waves per SIMD, 6.7 ms at 3; profiles/r3/r3q.)
         // A point's entry accumulates over the mass states in A; the sum of the states < k is loaded one
         // point ahead (timed equal to loading it in place, profiles/r2m: four blocks per CU already hide it).
         const bool reload = k > 0 && needed;

@@ -8,7 +8,7 @@ V=$1; shift
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
 D=/tmp/nusi_var_$V
 rm -rf $D; mkdir -p $D
-SRC=$ROOT
+SRC=${SRCDIR:-$ROOT}
 if [ -n "$REV" ]; then
   SRC=$D/src; mkdir -p $SRC
   git -C $ROOT archive $REV include nusiprop_amd/csrc | tar -x -C $SRC
