@@ -419,6 +419,8 @@ void k_alpha_batch(GridDev g, const Point* __restrict__ pts, SplineSet spl, cons
             for (int j = tid; j < cc; j += kTileThreads) b_xshared(j, edgk, ct, cs, X);
         }
         // ---- the points, kBatchQC at a time: their member edge leaves in one round, then point by point.
+        // (Two points per pair of barriers -- 512-thread workgroups whose halves share the batch's leaves -- measured
+        // slower too: C4 alpha 8.0 ms, profiles/r3/r3u.)
         // (Each wave owning 4 m rows of the tile, with its own block of member corners and no workgroup barrier in
         // the point loop, measured slower: C4 alpha 9.6 ms, the per-wave corner rows and the values live across the
         // loop spill at 4 waves per SIMD, 6.7 ms at 3; profiles/r3/r3q.)
