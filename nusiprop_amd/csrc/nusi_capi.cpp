@@ -960,10 +960,11 @@ int nusi_plan_evolve(nusi_plan* pl, const nusi_params* pts, int n, double* d_flu
     // slot in pairs on the multi-RHS form (k_cascade_ws<R = 2>: one operator, two sources) when most points pair
     // up; the step-pass kernel beyond 48 redshift steps.  WAVEFRONT / REG / LDS: the bit-exact scalar kernels.
     const int kind = pl->cascade_kind == NUSI_CASCADE_AUTO ? NUSI_CASCADE_MFMA : pl->cascade_kind;
-    bool all_pl = true, any_dsnb = false;
+    bool all_pl = true, any_dsnb = false, all_nr = true;
     for (int i = 0; i < n; ++i) {
         all_pl = all_pl && pl->h_pts[i].source == NUSI_SOURCE_POWER_LAW;
         any_dsnb = any_dsnb || pl->h_pts[i].source == NUSI_SOURCE_DSNB;
+        all_nr = all_nr && pl->h_pts[i].non_resonant;
     }
     const bool one_pass = nusi::cascade_ws_fits(pl->gd, 1) && pl->step_passes != 1;
     const bool fast = kind == NUSI_CASCADE_MFMA && (one_pass || nusi::cascade_wsp_fits(pl->gd));
@@ -1079,7 +1080,7 @@ int nusi_plan_evolve(nusi_plan* pl, const nusi_params* pts, int n, double* d_flu
     } else if (fast && one_pass)
         HIPCHECK(nusi::launch_cascade_ws(pl->gd, pl->d_pts, 1, nullptr, n, pl->tabs, d_flux, d_fla, s));
     else if (fast)
-        HIPCHECK(nusi::launch_cascade_wsp(pl->gd, pl->d_pts, n, pl->tabs, d_flux, d_fla, s));
+        HIPCHECK(nusi::launch_cascade_wsp(pl->gd, pl->d_pts, n, pl->tabs, d_flux, d_fla, s, all_nr));
     else
         HIPCHECK(nusi::launch_cascade_exact(pl->gd, pl->d_pts, n, pl->tabs, d_flux, d_fla, s,
                                             kind == NUSI_CASCADE_MFMA ? NUSI_CASCADE_WAVEFRONT : kind, all_pl));

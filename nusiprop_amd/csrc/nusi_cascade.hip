@@ -3,7 +3,7 @@
 //
 //   k_cascade_ws<NJ, R>   warp-specialised wavefront, push on the fp64 matrix cores, R points sharing a
 //                         table per workgroup (NUSI_CASCADE_AUTO / MFMA, Nz-1 <= 48)
-//   k_cascade_wsp<NJ>     the same in passes of 16 redshift steps (Nz-1 > 48)
+//   k_cascade_wsp<NJ, NR> the same in passes of 16 redshift steps (Nz-1 > 48)
 //   k_source_dsnb         the DSNB source terms those two read
 //   k_cascade_wf<NJ>      bit-exact scalar wavefront (NUSI_CASCADE_WAVEFRONT)
 //   k_cascade_reg<NQ, D>  bit-exact per-step chain in registers, N <= 64 NQ (NUSI_CASCADE_REG, fallback)
@@ -1208,7 +1208,9 @@ void k_cascade_ws(GridDev g, const Point* __restrict__ pts, const int2* __restri
 // ---------------------------------------------------------------------------
 constexpr int kWsBigNJ = 16, kWsBigRT = 8;   // step slots per pass, 16-row tiles per push wave
 
-template <int NJ>
+// kNR: every point of the launch is non-resonant (the launcher checks), so the resonant-only chain code is not
+// compiled in (C3 cascade 38.9 -> 37.3 ms, profiles/r3/r3w)
+template <int NJ, bool kNR>
 __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4, 4)))
 void k_cascade_wsp(GridDev g, const Point* __restrict__ pts, TablesDev t, double* __restrict__ flux,
                    double* __restrict__ flux_fla)
@@ -1277,7 +1279,7 @@ void k_cascade_wsp(GridDev g, const Point* __restrict__ pts, TablesDev t, double
     //   phase 2 (chain wave, one stage later): the LU of M -- cascade_record's operations, split
     constexpr int S3 = 3 * NJ;
     int jb = 0;   // first step slot of the current pass (step i = Nz-1-jb-j for slot j)
-    const bool nonres = P.non_resonant;
+    const bool nonres = kNR || P.non_resonant;
     auto phase1 = [&](int s2, int jj) {
         const int b = N - 1 - s2 + jj, i = Nz - 1 - jb - jj;
         if (jj < NJ && jb + jj < nst && b >= 0 && b < N) {
@@ -1986,12 +1988,15 @@ hipError_t launch_cascade_gb(const GridDev& g, const Point* pts, const int* gidx
 }
 
 hipError_t launch_cascade_wsp(const GridDev& g, const Point* pts, int npts, TablesDev t, double* flux, double* flux_fla,
-                              hipStream_t s)
+                              hipStream_t s, bool all_nonres)
 {
     if (!cascade_wsp_fits(g)) return hipErrorInvalidValue;
     t_cascade_kernel = "k_cascade_ws_passes";
     const WfGeom w = ws_geom(g, kWsBigNJ, 3);
-    hipLaunchKernelGGL((k_cascade_wsp<kWsBigNJ>), dim3(npts), dim3(w.nthr), w.lds, s, g, pts, t, flux, flux_fla);
+    if (all_nonres)
+        hipLaunchKernelGGL((k_cascade_wsp<kWsBigNJ, true>), dim3(npts), dim3(w.nthr), w.lds, s, g, pts, t, flux, flux_fla);
+    else
+        hipLaunchKernelGGL((k_cascade_wsp<kWsBigNJ, false>), dim3(npts), dim3(w.nthr), w.lds, s, g, pts, t, flux, flux_fla);
     return hipGetLastError();
 }
 

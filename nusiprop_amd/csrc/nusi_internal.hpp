@@ -71,7 +71,7 @@ bool cascade_wsp_fits(const GridDev& g);   // the step-pass kernel (any number o
 hipError_t launch_cascade_ws(const GridDev& g, const Point* pts, int R, const int2* groups, int nwg, TablesDev t,
                              double* flux, double* flux_fla, hipStream_t s);
 hipError_t launch_cascade_wsp(const GridDev& g, const Point* pts, int npts, TablesDev t, double* flux, double* flux_fla,
-                              hipStream_t s);
+                              hipStream_t s, bool all_nonres);   // all_nonres: every point non-resonant
 // The gamma batch (k_cascade_gb): workgroup k takes the grp[k].y <= 16 power-law points gidx[grp[k].x ..] that share one
 // table slot, gamma on the MFMA N dimension, the redshift steps in passes of 6; fh: a scratch FIFO of
 // cascade_gb_scratch_doubles per workgroup

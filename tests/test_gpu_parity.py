@@ -363,6 +363,30 @@ def test_cascade_step_passes(nusi, oracle_mod, N, lEmin):
     plan.close()
 
 
+@pytest.mark.parametrize("N", [200, 700])
+def test_cascade_step_passes_resonant_only(nusi, oracle_mod, N):
+    """The step-pass cascade with a resonant-only point in the launch (nuSIprop.hpp:273-278, 285-287): the launcher
+    then takes k_cascade_wsp<16, false>, whose chain keeps the resonant-only running sum (an all-non-resonant
+    launch takes the <16, true> instance without it); against the oracle's cascade on the GPU's own tables."""
+    from nusiprop_amd import _lib
+    pts = [dict(cases.C2B_100, N_bins_E=N, lEmin=12.0, mphi=m, g=g, non_resonant=nr)
+           for m, g, nr in ((6e5, 0.01, True), (2e6, 0.3, False), (1e6, 0.1, False))]
+    got = _evolve_opts(nusi, pts, step_passes=1)
+    assert got[2][1] == "k_cascade_ws_passes"
+    plan = nusi.Plan(N, 12.0, pts[0]["lEmax"], pts[0]["zmax"], max_points=len(pts))
+    plan.set_cascade(_lib.CASCADE_REG)
+    reg = plan.evolve(pts)
+    for k, p in enumerate(pts):
+        G, aT, A = plan.tables(k)
+        o = oracle_mod.Oracle(**cases.oracle_kwargs(p))
+        o.prepare()
+        f_ref, fla_ref = o.cascade(G, aT, nusi.unpack_alpha(A, plan.T))
+        assert cases.rel_err(got[0][k], f_ref) <= FLUX_RTOL, k
+        assert cases.rel_err(got[1][k], fla_ref) <= FLUX_RTOL, k
+        assert np.array_equal(got[0][k] == 0, reg[0][k] == 0)
+    plan.close()
+
+
 def test_plan_kernels_names(nusi):
     """nusi_plan_kernels reports what the last call launched: the batch alpha kernel, and per grid and
     cascade kind the one-pass warp-specialised kernel, its multi-RHS form (gamma pairs sharing a table),
