@@ -32,6 +32,17 @@ sys.path.insert(0, ROOT)
 METRIC = "full propagations/sec at N_E=300, 1 & 8 GPU; achieved HBM GB/s on cascade kernel"
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
 FP64_PEAK_TFLOPS = 78.6        # MI355X fp64 vector spec
+FLUX_RTOL = 1e-11              # the parity tests' flux bound vs the oracle in the matching mode (tests/cases.py)
+NORTH_STAR_RTOL = 1e-9         # BASELINE.json north star: max relative flux error vs the CPU reference
+
+# BASELINE config 2 (single propagation, N_E = 300; test.cpp:6-23 physics): C2a = the DSNB source with the resonance
+# inside lE 4 -> 9, C2b = the power-law source on the constructor-default grid (tests/cases.py C2A / C2B)
+C2_CASES = {
+    "C2a": dict(mphi=3e3, g=0.03, mntot=0.1, si=2.5, norm=6.0, majorana=True, non_resonant=True, normal_ordering=True,
+                N_bins_E=300, lEmin=4.0, lEmax=9.0, zmax=5.0, flav=2, phiphi=False, source_model=0),
+    "C2b": dict(mphi=6e5, g=0.01, mntot=0.1, si=2.5, norm=6.0, majorana=True, non_resonant=True, normal_ordering=True,
+                N_bins_E=300, lEmin=12.0, lEmax=17.0, zmax=5.0, flav=2, phiphi=False, source_model=1),
+}
 
 
 def parse():
@@ -55,6 +66,11 @@ def parse():
     ap.add_argument("--rhs", type=int, default=0,
                     help="NUSI_OPT_CASCADE_RHS: 0 = the library default, 1 = one point per cascade workgroup, 2 = pairs "
                          "of points sharing a table, 3..16 = the gamma batch k_cascade_gb")
+    ap.add_argument("--reference-order", action="store_true",
+                    help="NUSI_OPT_REFERENCE_ORDER: the tables in the reference's own operation order for the complex "
+                         "dilogarithms (bit-exact to the oracle's reference-order mode); default: the shared-algorithm "
+                         "order (bit-exact to the oracle's default mode)")
+    ap.add_argument("--no-parity", action="store_true", help="skip the parity object (oracle fluxes of a sample)")
     ap.add_argument("--dry-run", action="store_true",
                     help="launch / rank / reduction plumbing only, no GPU work (gloo; CPU tests): prints the JSON "
                          "line with value null")
@@ -67,8 +83,10 @@ def parse():
 def rank_points(args, rank, world):
     from nusiprop_amd import scan
     if args.workload == "c2":
-        pts = [dict(scan.BASE, mphi=6e5, g=0.01, si=2.5, norm=6.0)]
-        return pts * max(1, args.points or 1), "C2b: single propagation, N_E=300, lE 12->17, power-law source, test.cpp physics"
+        pts = [dict(C2_CASES["C2b"])]
+        return pts * max(1, args.points or 1), ("C2: single propagation, N_E=300 -- the timed plan runs C2b (lE 12->17, "
+                                                "power-law source, test.cpp physics); single_propagation and parity "
+                                                "cover C2a (DSNB, resonance inside lE 4->9) and C2b")
     if args.workload == "c1":   # test.cpp:6-23 verbatim (N_E = 100, lE 9 -> 14, DSNB source)
         pts = [dict(scan.C1)]
         return pts * max(1, args.points or 1), "C1: test.cpp single propagation (N_E=100, lE 9->14, DSNB source, phiphi off)"
@@ -132,16 +150,31 @@ def _oracle(p):
     return oracle.Oracle(**kw)
 
 
-def cpu_baseline(pts, budget_s):
+def cpu_baseline(pts, budget_s, pp_tables=None):
     """The C oracle (test infrastructure, the reference's algorithm restated) on a bounded sample of the same
     workload: Stage A (tables) and Stage B (cascade) timed apart on one core for a quarter of the budget, then
     whole evolve()s on a thread pool over the host cores for the rest (ctypes releases the GIL, the oracle has
-    no global state).  value = the pool's propagations/s."""
+    no global state).  value = the pool's propagations/s.  With phi-phi tables (C3) one propagation on one core
+    only: each pool worker would hold its own 400 MB copy of the tables, and one C3 propagation takes ~10 s."""
     import concurrent.futures as cf
     import threading
     from oracle import oracle
     oracle.build()
     threads, host = host_cores()
+    if pp_tables is not None:
+        o = _oracle(pts[-1])
+        t0 = time.perf_counter()
+        o.load_phiphi(*pp_tables)
+        t1 = time.perf_counter()
+        G, At, A = o.tables()
+        t2 = time.perf_counter()
+        o.cascade(G, At, A)
+        t3 = time.perf_counter()
+        return {"value": 1.0 / (t3 - t1), "unit": "propagations/s", "cores": 1, "kind": "port", "host": host,
+                "s_per_prop": t3 - t1, "stage_a_s": t2 - t1, "stage_b_s": t3 - t2, "table_load_s": t1 - t0,
+                "sample": "1 full propagation (the workload's strongest point, g = %.3g) of the single-threaded C "
+                          "oracle on one core, phi-phi tables loaded beforehand (not timed)" % pts[-1]["g"],
+                "cores_note": "one core; no pool (each worker would need its own 400 MB table copy)"}
     # one core, stages apart
     ta = tb = 0.0
     n1, t0 = 0, time.perf_counter()
@@ -202,10 +235,12 @@ def c1_cpu_lines(budget_s):
     return out
 
 
-def single_point_latency(pt, reps):
+def single_point_latency(pt, reps, refo=False):
     """One evolve() through the object API (nusi_create / nusi_evolve: host parameters in, tables and cascade
-    on the GPU, fluxes copied to the host) -- the reference's own usage, calculate_flux::evolve() per object."""
+    on the GPU, fluxes copied to the host) -- the reference's own usage, calculate_flux::evolve() per object.
+    Returns (timings, flavour fluxes [3, N] of the last evolve)."""
     import ctypes
+    import numpy as np
     from nusiprop_amd import _lib
     L = _lib.load()
     p = dict(pt)
@@ -213,6 +248,8 @@ def single_point_latency(pt, reps):
     h = ctypes.c_void_p()
     _lib.check(L.nusi_create(ctypes.byref(_lib.make_params(source_model=src, **p)), ctypes.byref(h)))
     try:
+        if refo:
+            _lib.check(L.nusi_set_option(h, _lib.OPT_REFERENCE_ORDER, 1))
         out = (ctypes.c_double * (3 * p["N_bins_E"]))()
         for _ in range(3):
             _lib.check(L.nusi_evolve(h))
@@ -225,8 +262,68 @@ def single_point_latency(pt, reps):
     finally:
         L.nusi_destroy(h)
     ts.sort()
-    return {"median_ms": ts[len(ts) // 2] * 1e3, "min_ms": ts[0] * 1e3, "reps": reps,
-            "path": "nusi_create + nusi_evolve + nusi_get_flux_fla (object API, host I/O and sync included)"}
+    fla = np.array(out[:], dtype=np.float64).reshape(3, p["N_bins_E"])
+    return {"median_ms": ts[len(ts) // 2] * 1e3, "min_ms": ts[0] * 1e3, "reps": reps, "props_per_s": 1e3 / (ts[len(ts) // 2] * 1e3),
+            "path": "nusi_create + nusi_evolve + nusi_get_flux_fla (object API, host I/O and sync included)"}, fla
+
+
+def rel_err(a, b, floor=1e-280):
+    """max |a-b|/|b| over the entries with |b| > floor max|b|; inf unless a == 0 where b == 0 (tests/cases.py)."""
+    import numpy as np
+    a, b = np.asarray(a, dtype=np.float64), np.asarray(b, dtype=np.float64)
+    zero = b == 0
+    if np.any(a[zero] != 0):
+        return float("inf")
+    m = np.abs(b) > floor * (np.max(np.abs(b)) if b.size else 0.0)
+    return float(np.max(np.abs(a[m] - b[m]) / np.abs(b[m]))) if np.any(m) else 0.0
+
+
+def parity_indices(args, pts):
+    """A deterministic sample of the workload for the parity object: the strongest-coupling column (g = max, where
+    the closed forms' conditioning is worst) at every other m_phi, plus seeded picks; C3: its strongest point."""
+    import numpy as np
+    if args.workload == "c3":
+        return [int(np.argmax([p["g"] for p in pts]))]
+    n = 32 if args.workload in ("c4", "c4s") else 16
+    gmax = max(p["g"] for p in pts)
+    col = [i for i, p in enumerate(pts) if p["g"] == gmax]
+    pick = col[::2][:n // 2]
+    rng = np.random.default_rng(20250213)
+    for i in rng.permutation(len(pts)):
+        if len(pick) >= n:
+            break
+        if int(i) not in pick:
+            pick.append(int(i))
+    return sorted(pick)
+
+
+def parity(sel_pts, gpu_fla, gpu_order, phiphi_tables=None, label=""):
+    """The GPU fluxes of `sel_pts` (flavour basis, from the timed run) against the C oracle's evolve() in both of
+    its arithmetic modes: the shared-algorithm order the default tables are bit-exact to, and the reference's own
+    operation order (NUSI_OPT_REFERENCE_ORDER's).  The oracle is the checker here, after the timed region."""
+    import numpy as np
+    from oracle import oracle
+    oracle.build()
+    t0 = time.perf_counter()
+    res = {}
+    for level, key in ((0, "vs_oracle_shared_order"), (1, "vs_oracle_reference_order")):
+        _, fla = oracle.evolve_many(sel_pts, level=level, phiphi_tables=phiphi_tables)
+        e = np.array([rel_err(gpu_fla[k], fla[k]) for k in range(len(sel_pts))])
+        res[key] = {"max_rel": float(e.max()), "median_rel": float(np.median(e)),
+                    "points_above_1e-11": int(np.sum(e > FLUX_RTOL)), "points_above_1e-9": int(np.sum(e > NORTH_STAR_RTOL)),
+                    "worst": {"mphi": sel_pts[int(np.argmax(e))]["mphi"], "g": sel_pts[int(np.argmax(e))]["g"]}}
+    match = "vs_oracle_reference_order" if gpu_order == "reference" else "vs_oracle_shared_order"
+    res.update({
+        "points": len(sel_pts), "sample": label, "gpu_table_order": gpu_order,
+        "tolerance": {"flux_rtol_vs_matching_oracle": FLUX_RTOL, "north_star_rtol": NORTH_STAR_RTOL,
+                      "within_flux_rtol": res[match]["max_rel"] <= FLUX_RTOL,
+                      "note": "this run's tables are bit-exact to the oracle's %s mode (tests/test_gpu_parity.py, "
+                              "tests/test_reference_order_gpu.py); the fluxes differ from it by the cascade's summation "
+                              "order only, held to %.0e. The other mode differs where the s-t interference closed forms "
+                              "cancel (DESIGN.md sec. 2)" % ("reference-order" if gpu_order == "reference" else
+                                                              "shared-algorithm", FLUX_RTOL)},
+        "oracle_seconds": time.perf_counter() - t0})
+    return res
 
 
 def free_port():
@@ -242,15 +339,15 @@ def launch_ranks(args):
     """--gpus N > 1 without a launcher: start N rank processes with torch.distributed.run (one per GPU, RCCL
     rendezvous on 127.0.0.1) -- before anything here has touched the GPU -- and return their exit status.  A
     rank count that differs from --gpus is an error, never an N-GPU label on a different run."""
+    if args.gpus is not None and args.gpus < 1:
+        sys.exit("bench.py: --gpus must be >= 1")
     world_env = os.environ.get("WORLD_SIZE")
     if world_env is not None:
         if args.gpus is not None and int(world_env) != args.gpus:
             sys.exit("bench.py: --gpus %d but WORLD_SIZE=%s ranks were launched" % (args.gpus, world_env))
         return None
-    if not args.gpus or args.gpus == 1:
+    if args.gpus is None or args.gpus == 1:
         return None
-    if args.gpus < 1:
-        sys.exit("bench.py: --gpus must be >= 1")
     import subprocess
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(args.gpus),
            "--master-addr", "127.0.0.1", "--master-port", str(free_port()), os.path.abspath(__file__)] + sys.argv[1:]
@@ -258,24 +355,41 @@ def launch_ranks(args):
     return subprocess.call(cmd)
 
 
+SECONDARY = (   # name, bench.py arguments, steps: BASELINE configs 5, 3 and 2, and C4 in reference-order mode
+    ("c5", ["--workload", "c5", "--no-cpu-baseline"], 10),
+    ("c3", ["--workload", "c3", "--cpu-seconds", "10"], 3),
+    ("c4_refo", ["--workload", "c4", "--reference-order", "--no-cpu-baseline"], 10),
+    ("c2", ["--workload", "c2", "--cpu-seconds", "4"], 20),
+)
+
+
 def secondary_lines(local):
-    """BASELINE configs 5 and 3 measured beside the headline C4 line, each by a child bench.py process on the same
-    GPU after the C4 timed region (so the driver's run records them too): props/s, stage times, kernels."""
+    """BASELINE configs 5, 3 and 2 and the C4 scan in reference-order mode, measured beside the headline C4 line,
+    each by a child bench.py process on the same GPU after the C4 timed region (so the driver's run records them
+    too): props/s, stage times, kernels, parity, and (C3, C2) the oracle's CPU numbers."""
     import subprocess
     out = {}
     env = dict(os.environ, HIP_VISIBLE_DEVICES=os.environ.get("HIP_VISIBLE_DEVICES", str(local)))
-    for wl, steps in (("c5", 10), ("c3", 3)):
-        cmd = [sys.executable, os.path.abspath(__file__), "--workload", wl, "--steps", str(steps), "--warmup", "1",
-               "--no-cpu-baseline", "--no-secondary"]
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT", "GROUP_RANK",
+              "ROLE_RANK", "TORCHELASTIC_RUN_ID"):
+        env.pop(k, None)   # each child is a plain single-GPU run, not a rank of this job
+    for name, extra, steps in SECONDARY:
+        cmd = [sys.executable, os.path.abspath(__file__), "--steps", str(steps), "--warmup", "1", "--no-secondary"] + extra
         try:
-            r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env)
+            r = subprocess.run(cmd, capture_output=True, text=True, timeout=400, env=env)
             d = json.loads(r.stdout.strip().splitlines()[-1])
-            out[wl] = {k: d.get(k) for k in ("value", "unit", "ms_per_step", "steps", "stage_ms_per_step")}
-            out[wl]["workload"] = d["config"]["workload"]
-            out[wl]["kernels"] = [d["config"]["alpha_kernel"], d["config"]["cascade_kernel"]]
-            out[wl]["roofline"] = {k: d["roofline"].get(k) for k in ("kernel", "achieved", "unit", "frac", "traffic")}
+            out[name] = {k: d.get(k) for k in ("value", "unit", "ms_per_step", "steps", "stage_ms_per_step", "parity",
+                                               "single_propagation")}
+            out[name]["workload"] = d["config"]["workload"]
+            out[name]["table_order"] = d["config"].get("table_order")
+            out[name]["kernels"] = [d["config"]["alpha_kernel"], d["config"]["cascade_kernel"]]
+            out[name]["roofline"] = {k: d["roofline"].get(k) for k in ("kernel", "achieved", "unit", "frac", "traffic")}
+            if "cpu_baseline" in d:
+                cb = d["cpu_baseline"]
+                out[name]["cpu_baseline"] = {k: cb.get(k) for k in ("value", "unit", "cores", "kind", "sample",
+                                                                    "s_per_prop", "single_core")}
         except Exception as e:   # a secondary line never fails the headline run
-            out[wl] = {"error": "%s: %s" % (type(e).__name__, e)}
+            out[name] = {"error": "%s: %s" % (type(e).__name__, e)}
     return out
 
 
@@ -330,7 +444,7 @@ def main():
     if local >= ndev:
         sys.exit("bench.py: rank %d needs GPU %d but %d device(s) are visible" % (rank, local, ndev))
     dist = None
-    if world > 1:
+    if "WORLD_SIZE" in os.environ:   # under a launcher (torch.distributed.run): RCCL, even for one rank
         import torch.distributed as dist
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -343,20 +457,35 @@ def main():
     P = len(pts)
     p0 = pts[0]
     plan = nu.Plan(p0["N_bins_E"], p0["lEmin"], p0["lEmax"], p0["zmax"], max_points=P, device=local)
+    pp_tables, tdir = None, None
     if any(p.get("phiphi") for p in pts):
-        import shutil
         import tempfile
         from nusiprop_amd.phiphi_tables import write_synthetic_tables
         tdir = tempfile.mkdtemp(prefix="nusi_phiphi_")
-        at, atd, a, ad = write_synthetic_tables(tdir)     # the reference's geometry (1.6 GB of records)
-        plan.load_phiphi(at, a)                           # dims = NULL: {5000,100}, {1000,1000,100}
-        shutil.rmtree(tdir, ignore_errors=True)
+        pp_tables = write_synthetic_tables(tdir)          # the reference's geometry (1.6 GB of records)
+        plan.load_phiphi(pp_tables[0], pp_tables[2])      # dims = NULL: {5000,100}, {1000,1000,100}
+    try:
+        return run(args, world, rank, local, dist, plan, pts, desc, pp_tables)
+    finally:
+        if tdir:
+            import shutil
+            shutil.rmtree(tdir, ignore_errors=True)
+
+
+def run(args, world, rank, local, dist, plan, pts, desc, pp_tables):
+    import torch
+    from nusiprop_amd import _lib, scan
+    P = len(pts)
+    p0 = pts[0]
     arr = plan.params_array(pts)
     plan.set_cascade({"mfma": _lib.CASCADE_MFMA, "wf": _lib.CASCADE_WAVEFRONT, "auto": _lib.CASCADE_AUTO}[args.cascade])
     if args.workload == "c4s":
         plan.set_option(_lib.OPT_SHIFT_REUSE, 128)
     if args.rhs:
         plan.set_option(_lib.OPT_CASCADE_RHS, args.rhs)
+    if args.reference_order:
+        plan.set_option(_lib.OPT_REFERENCE_ORDER, 1)
+    order = "reference" if args.reference_order else "shared-algorithm"
     dev = torch.device("cuda", local)
     flux = torch.empty((P, 3, plan.N), dtype=torch.float64, device=dev)
     fla = torch.empty((P, 3, plan.N), dtype=torch.float64, device=dev)
@@ -440,7 +569,9 @@ def main():
         "config": {"workload": desc, "N_E": N, "N_z": Nz, "points_per_gpu": P, "lEmin": p0["lEmin"],
                    "lEmax": p0["lEmax"], "parallelism": "independent points, %d GPU(s), no collective" % world,
                    "alpha_kernel": alpha_kernel, "cascade_kernel": casc_kernel, "cascade_kind": args.cascade,
-                   "cascade_rhs": args.rhs or "auto"},
+                   "cascade_rhs": args.rhs or "auto",
+                   "table_order": order + (" (NUSI_OPT_REFERENCE_ORDER)" if args.reference_order else " (default)"),
+                   "process_group": dist.get_backend() if dist is not None else None},
         "libnusi": {"path": os.path.relpath(_lib.LIB_PATH, ROOT), "sha256": lib_sha, "pmc_source": tsrc,
                     "pmc_note": pmc_note},
         "stage_ms_per_step": {"gamma_alphatilde": sum_ms[0] / max(ncalls, 1), "alpha": sum_ms[1] / max(ncalls, 1),
@@ -493,13 +624,28 @@ def main():
                                    "(transcendental leaves), neither HBM nor MFMA"}
     else:   # the cascade dominates (C5's gamma batches), or no alpha counters for this binary
         out["roofline"] = dict(out["roofline_cascade"])
-    if args.workload in ("c1", "c2") and rank == 0:
-        out["single_propagation"] = single_point_latency(pts[0], max(20, args.steps))
+    if args.workload == "c1" and rank == 0:
+        out["single_propagation"], _ = single_point_latency(pts[0], max(20, args.steps), args.reference_order)
         out["single_propagation"]["plan_ms_per_step"] = dt / args.steps * 1e3
+    if args.workload == "c2" and rank == 0:   # both BASELINE config-2 cases through the object API
+        out["single_propagation"], c2_fla = {}, {}
+        for name, cp in C2_CASES.items():
+            out["single_propagation"][name], c2_fla[name] = single_point_latency(cp, max(20, args.steps),
+                                                                                args.reference_order)
+        out["single_propagation"]["plan_ms_per_step_C2b"] = dt / args.steps * 1e3
+        if not args.no_parity:
+            out["parity"] = {name: parity([C2_CASES[name]], c2_fla[name][None], order, label=name + " (object API)")
+                             for name in C2_CASES}
+    elif rank == 0 and not args.no_parity:
+        idx = parity_indices(args, pts)
+        host_fla = fla.cpu().numpy()
+        out["parity"] = parity([pts[i] for i in idx], host_fla[idx], order, phiphi_tables=pp_tables,
+                               label="%d of the %d points: the g = max column at every other m_phi + seeded picks "
+                                     "(parity_indices); fluxes of the last timed step" % (len(idx), P))
     if rank == 0 and world == 1 and args.workload == "c4" and not args.no_secondary and not args.points:
         out["secondary_lines"] = secondary_lines(local)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(pts, args.cpu_seconds)
+        out["cpu_baseline"] = cpu_baseline(pts, args.cpu_seconds, pp_tables)
         if args.workload == "c1":
             out["cpu_baseline"]["c1_test_cpp"] = c1_cpu_lines(min(5.0, args.cpu_seconds / 3))
     if rank == 0:

@@ -109,6 +109,8 @@ int nusi_get_warnings(const nusi_handle *h);                   /* NUSI_WARN_* of
 /* names of the alpha-table and cascade kernels the last evolve() launched (static strings; no reference
  * counterpart -- reports and tests) */
 int nusi_get_kernels(const nusi_handle *h, const char **alpha, const char **cascade);
+/* nusi_plan_set_option on the object's plan (NUSI_OPT_*; kept by nusi_copy).  No reference counterpart. */
+int nusi_set_option(nusi_handle *h, int option, int value);
 
 /* ---------------------------------------------------------------------------
  * 2. plan API -- batched parameter scans on one GPU
@@ -200,6 +202,20 @@ int nusi_plan_set_cascade(nusi_plan *plan, int kind);
 #define NUSI_OPT_CASCADE_RHS 3
 #define NUSI_OPT_STEP_PASSES 4
 #define NUSI_OPT_SHIFT_REUSE 5
+/*   NUSI_OPT_REFERENCE_ORDER  1 = build Gamma / alphaTilde / alpha in the
+ *                          reference's own operation order: every complex
+ *                          dilogarithm by gsl_sf_complex_dilog_xy_e's
+ *                          general series (no near-axis Taylor shortcut),
+ *                          and the alpha table's s-t interference member
+ *                          leaves as the dilogarithm of the reference's
+ *                          quotient (1+S+t)/(2 - i gr + t) and carg of its
+ *                          expression (nuSIprop.hpp:1428-1467, 843-878,
+ *                          1135-1192).  0 = the default shared-algorithm
+ *                          order (batch-shared Taylor coefficients, faster).
+ *                          Both are bit-identical to the oracle in the
+ *                          matching mode; they differ from each other where
+ *                          the closed forms cancel. */
+#define NUSI_OPT_REFERENCE_ORDER 6
 int nusi_plan_set_option(nusi_plan *plan, int option, int value);
 /* per-point NUSI_WARN_* bits of the last call */
 int nusi_plan_warnings(nusi_plan *plan, int *out, int n);

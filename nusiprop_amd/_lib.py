@@ -47,7 +47,7 @@ EXPORTS = [
     "nusi_params_default", "nusi_last_error", "nusi_device_count",
     "nusi_create", "nusi_copy", "nusi_destroy", "nusi_set_params", "nusi_get_params", "nusi_evolve",
     "nusi_check_energy_conservation", "nusi_get_flux", "nusi_get_flux_fla", "nusi_get_energies",
-    "nusi_get_N_bins_E", "nusi_get_N_steps_z", "nusi_get_warnings", "nusi_get_kernels",
+    "nusi_get_N_bins_E", "nusi_get_N_steps_z", "nusi_get_warnings", "nusi_get_kernels", "nusi_set_option",
     "nusi_plan_create", "nusi_plan_destroy", "nusi_plan_load_phiphi", "nusi_plan_grid", "nusi_plan_evolve",
     "nusi_plan_evolve_host", "nusi_plan_stage_ms", "nusi_plan_profile_begin", "nusi_plan_profile_end",
     "nusi_plan_warnings", "nusi_plan_tables", "nusi_evolve_batch", "nusi_plan_set_cascade",
@@ -57,6 +57,7 @@ EXPORTS = [
 # nusi_plan_set_cascade kinds and nusi_plan_set_option options (include/nusi.h)
 CASCADE_AUTO, CASCADE_WAVEFRONT, CASCADE_REG, CASCADE_LDS, CASCADE_MFMA = 0, 1, 2, 3, 4
 OPT_ALPHA_BATCH, OPT_ALPHA_KERNEL, OPT_CASCADE_RHS, OPT_STEP_PASSES, OPT_SHIFT_REUSE = 1, 2, 3, 4, 5
+OPT_REFERENCE_ORDER = 6
 
 _lib = None
 
@@ -90,6 +91,7 @@ def load():
         "nusi_get_N_steps_z": (i, [vp]),
         "nusi_get_warnings": (i, [vp]),
         "nusi_get_kernels": (i, [vp, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_char_p)]),
+        "nusi_set_option": (i, [vp, i, i]),
         "nusi_plan_create": (i, [i, i, d, d, d, i, ctypes.POINTER(vp)]),
         "nusi_plan_destroy": (None, [vp]),
         "nusi_plan_load_phiphi": (i, [vp, ctypes.c_char_p, ip, ctypes.c_char_p, ip]),

@@ -426,6 +426,7 @@ struct nusi_plan {
     int fh_cap = 0;
     int step_passes = 0;            // NUSI_OPT_STEP_PASSES: 1 = the step-pass cascade also where one pass fits
     int shift_max = 0;              // NUSI_OPT_SHIFT_REUSE: K, the largest bin offset served by a base table set
+    int ref_order = 0;              // NUSI_OPT_REFERENCE_ORDER: 1 = the tables in the reference's operation order
     nusi_plan* shift = nullptr;     // ... its plan: the same grid with K more redshift steps (axis T + K)
     int2* d_smap = nullptr;         // per shifted table: base index in `shift`, bin offset
     int2* h_smap = nullptr;         // pinned
@@ -447,6 +448,7 @@ struct nusi_plan {
     std::vector<hipEvent_t> prof_ev;   // 4 per recorded call
     hipEvent_t last_ev[4] = {nullptr, nullptr, nullptr, nullptr};   // the latest call's stage events (handles)
     const char* alpha_kernel = "";     // main kernels of the latest call (nusi_plan_kernels)
+    std::string alpha_label;           // ... storage of a composed alpha label (shift reuse)
     const char* cascade_kernel = "";
     int prof_max = 0, prof_n = 0;
     int cascade_kind = NUSI_CASCADE_AUTO;
@@ -931,6 +933,8 @@ int nusi_plan_evolve(nusi_plan* pl, const nusi_params* pts, int n, double* d_flu
             // the base plan's tables, ordered and batched like any others (their slots move: remap the map)
             nusi_plan* sp = pl->shift;
             sp->spl = pl->spl;   // (the phi-phi set may have been loaded after the base plan was made)
+            sp->alpha_batch = pl->alpha_batch;   // (and the alpha options may have changed since)
+            sp->alpha_kind = pl->alpha_kind;
             if (sp->ran) HIPCHECK(hipEventSynchronize(sp->ev_copy));
             for (int b = 0; b < nbase; ++b) {
                 sp->h_tpts[b] = bases[b];
@@ -1053,16 +1057,17 @@ int nusi_plan_evolve(nusi_plan* pl, const nusi_params* pts, int n, double* d_flu
     hipEvent_t* ev = pl->ev;
     if (pl->prof_n < pl->prof_max) ev = &pl->prof_ev[4 * (size_t)pl->prof_n++];
     HIPCHECK(hipEventRecord(ev[0], s));
-    if (nd) HIPCHECK(nusi::launch_gamma_alphat(pl->gd, pl->d_tpts, nd, spl, pl->tabs, pl->d_warn, s));
-    if (sp) HIPCHECK(nusi::launch_gamma_alphat(sp->gd, sp->d_tpts, nbase, spl, sp->tabs, sp->d_warn, s));
+    const bool refo = pl->ref_order != 0;
+    if (nd) HIPCHECK(nusi::launch_gamma_alphat(pl->gd, pl->d_tpts, nd, spl, pl->tabs, pl->d_warn, s, refo));
+    if (sp) HIPCHECK(nusi::launch_gamma_alphat(sp->gd, sp->d_tpts, nbase, spl, sp->tabs, sp->d_warn, s, refo));
     HIPCHECK(hipEventRecord(ev[1], s));
     if (nd)
         HIPCHECK(nusi::launch_alpha(pl->gd, pl->d_tpts, nd, spl, pl->atiles, pl->tabs, pl->d_warn, s, pl->d_batches,
-                                    nbatch, cap, pl->alpha_kind, nb_plain));
+                                    nbatch, cap, pl->alpha_kind, nb_plain, refo));
     if (sp) {
         const AlphaBatches& bb = pl->shift_batches;
         HIPCHECK(nusi::launch_alpha(sp->gd, sp->d_tpts, nbase, spl, sp->atiles, sp->tabs, sp->d_warn, s, sp->d_batches,
-                                    bb.nbatch, bb.cap, sp->alpha_kind, bb.nb_plain));
+                                    bb.nbatch, bb.cap, pl->alpha_kind, bb.nb_plain, refo));
         HIPCHECK(nusi::launch_table_shift(pl->gd, sp->gd, pl->d_smap, nd, ntab - nd, sp->tabs, sp->d_warn, pl->tabs,
                                           pl->d_warn, s));
     }
@@ -1087,7 +1092,10 @@ int nusi_plan_evolve(nusi_plan* pl, const nusi_params* pts, int n, double* d_flu
     HIPCHECK(hipEventRecord(ev[3], s));
     HIPCHECK(hipEventRecord(pl->ev_done, s));
     pl->alpha_kernel = nusi::last_alpha_kernel();
-    if (sp) pl->alpha_kernel = nd ? "k_alpha_batch + k_table_shift" : "k_alpha_batch (shift base) + k_table_shift";
+    if (sp) {   // the label of the kernel that built the base tables (the base launch runs last)
+        pl->alpha_label = std::string(nusi::last_alpha_kernel()) + (nd ? " + k_table_shift" : " (shift base) + k_table_shift");
+        pl->alpha_kernel = pl->alpha_label.c_str();
+    }
     pl->cascade_kernel = gb_name ? gb_name : nusi::last_cascade_kernel();
     for (int k = 0; k < 4; ++k) pl->last_ev[k] = ev[k];   // stage_ms / warnings / tables refer to the latest call
     pl->ran = true;
@@ -1165,6 +1173,10 @@ int nusi_plan_set_option(nusi_plan* pl, int option, int value)
     case NUSI_OPT_STEP_PASSES:
         if (value < 0 || value > 1) return fail(NUSI_EPARAM, "NUSI_OPT_STEP_PASSES outside [0, 1]");
         pl->step_passes = value;
+        return NUSI_OK;
+    case NUSI_OPT_REFERENCE_ORDER:
+        if (value < 0 || value > 1) return fail(NUSI_EPARAM, "NUSI_OPT_REFERENCE_ORDER outside [0, 1]");
+        pl->ref_order = value;
         return NUSI_OK;
     case NUSI_OPT_SHIFT_REUSE:
         if (value < 0 || value > 128) return fail(NUSI_EPARAM, "NUSI_OPT_SHIFT_REUSE outside [0, 128]");
@@ -1255,6 +1267,7 @@ struct nusi_handle {
     double norm_total = 0.0;   // of the last evolve() (stale in check_energy_conservation)
     bool evolved = false;      // an evolve() has run (norm_total is set)
     int warn = 0;
+    std::vector<std::pair<int, int>> opts;   // nusi_set_option calls, replayed by nusi_copy
     ~nusi_handle() { nusi_plan_destroy(plan); }
 };
 
@@ -1297,6 +1310,14 @@ int nusi_copy(const nusi_handle* src, nusi_handle** out)
     (*out)->norm_total = src->norm_total;
     (*out)->evolved = src->evolved;
     (*out)->warn = src->warn;
+    for (const auto& o : src->opts) {
+        r = nusi_set_option(*out, o.first, o.second);
+        if (r) {
+            nusi_destroy(*out);
+            *out = nullptr;
+            return r;
+        }
+    }
     return NUSI_OK;
 }
 
@@ -1373,6 +1394,13 @@ int nusi_get_energies(const nusi_handle* h, double* out)
 int nusi_get_N_bins_E(const nusi_handle* h) { return h->plan->grid.N; }
 int nusi_get_N_steps_z(const nusi_handle* h) { return h->plan->grid.Nz; }
 int nusi_get_warnings(const nusi_handle* h) { return h->warn; }
+int nusi_set_option(nusi_handle* h, int option, int value)
+{
+    const int r = nusi_plan_set_option(h->plan, option, value);
+    if (r == NUSI_OK) h->opts.emplace_back(option, value);
+    return r;
+}
+
 int nusi_get_kernels(const nusi_handle* h, const char** alpha, const char** cascade)
 {
     if (!h->evolved) return fail(NUSI_ESTATE, "no evolve has run on this object");

@@ -20,6 +20,8 @@ namespace nusi {
 #ifndef NUSI_GA_WAVES   // Gamma / alphaTilde kernel waves per SIMD (A/B)
 #define NUSI_GA_WAVES 4   // with Gamma / alphaTilde split over work-items: 4 0.525, 3 0.535 ms (was 0.572 unsplit at 3)
 #endif
+// kRef: NUSI_OPT_REFERENCE_ORDER (the general complex dilogarithm, gamma_entry / alphat_entry)
+template <bool kRef>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NUSI_GA_WAVES, NUSI_GA_WAVES))) void k_gamma_alphat(GridDev g, const Point* __restrict__ pts, SplineSet spl,
                                                      double* __restrict__ G, double* __restrict__ At,
                                                      int* __restrict__ warn)
@@ -31,9 +33,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NUSI_GA_WAVE
     int w = 0;
     const double lo = g.lo[n], hi = g.hi[n];
     if (blockIdx.z == 0)   // Gamma and alphaTilde of an entry on separate work-items: twice the waves
-        G[(size_t)p * g.T + n] = gamma_entry(P, lo, hi, w);
+        G[(size_t)p * g.T + n] = gamma_entry<kRef>(P, lo, hi, w);
     else
-        At[(size_t)p * g.T + n] = alphat_entry(P, spl, lo, hi, w);
+        At[(size_t)p * g.T + n] = alphat_entry<kRef>(P, spl, lo, hi, w);
     if (w) atomicOr(&warn[p], w);
 }
 
@@ -69,6 +71,7 @@ hipError_t spline_windows_build(const float* f, int n0, int n1, int n2, float* f
 #ifndef NUSI_PE_WAVES   // per-entry kernel waves per SIMD (A/B)
 #define NUSI_PE_WAVES 3   // 3: 20.05 vs 20.24 ms alpha stage (profiles/r1i/ab_occ_*)
 #endif
+template <bool kRef>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NUSI_PE_WAVES, NUSI_PE_WAVES)))
 void k_alpha(GridDev g, const Point* __restrict__ pts, SplineSet spl, int nlo,
                                                double* __restrict__ A, int* __restrict__ warn)
@@ -88,16 +91,17 @@ void k_alpha(GridDev g, const Point* __restrict__ pts, SplineSet spl, int nlo,
     int w = 0;
     double v = 0.0;
     // without non-s channels the cascade reads only alpha(n, n+1) (nuSIprop.hpp:273-275)
-    if (P.non_resonant || m == n + 1) v = alpha_entry(P, spl, g.lo[n], g.hi[n], g.lo[m], g.hi[m], w);
+    if (P.non_resonant || m == n + 1) v = alpha_entry<kRef>(P, spl, g.lo[n], g.hi[n], g.lo[m], g.hi[m], w);
     A[(size_t)p * g.PT + (size_t)m * (m - 1) / 2 + n] = v;
     if (w) atomicOr(&warn[p], w);
 }
 
 hipError_t launch_gamma_alphat(const GridDev& g, const Point* pts, int npts, const SplineSet& spl, TablesDev t,
-                               int* warn, hipStream_t s)
+                               int* warn, hipStream_t s, bool ref)
 {
     dim3 grid((g.T + 63) / 64, npts, 2);
-    hipLaunchKernelGGL(k_gamma_alphat, grid, dim3(64), 0, s, g, pts, spl, t.G, t.At, warn);
+    if (ref) hipLaunchKernelGGL(k_gamma_alphat<true>, grid, dim3(64), 0, s, g, pts, spl, t.G, t.At, warn);
+    else hipLaunchKernelGGL(k_gamma_alphat<false>, grid, dim3(64), 0, s, g, pts, spl, t.G, t.At, warn);
     return hipGetLastError();
 }
 
@@ -133,7 +137,8 @@ __host__ __device__ constexpr int alpha_tile_lds_doubles(int cs, int ct, int G)
 // the channel flags (nusi_capi.cpp orders the tables so): the leaves of (S', t) alone -- the real
 // dilogarithms and most logarithms -- are evaluated once for the batch, the leaves that read
 // gr = Gamma_phi / m_phi once per point.  batches[y] = first table | count << 24 (nullptr: table y alone).
-template <int G>   // batch capacity (compile time, so that G = 1 keeps its sum in a register)
+template <int G, bool kRef>   // batch capacity (compile time, so that G = 1 keeps its sum in a register);
+                              // kRef: NUSI_OPT_REFERENCE_ORDER member corners
 __global__ __launch_bounds__(kTileThreads) NUSI_TILE_ATTR void k_alpha_tile(GridDev g, const Point* __restrict__ pts, SplineSet spl,
                                                            const int* __restrict__ tiles, int cs_max, int ct_max,
                                                            const int* __restrict__ batches,
@@ -212,7 +217,7 @@ __global__ __launch_bounds__(kTileThreads) NUSI_TILE_ATTR void k_alpha_tile(Grid
             for (int j = tid; j < cc; j += kTileThreads) {   // corner j: shared leaves, then each point's
                 alpha_tile_corner_job(j, edgk, ct, cs, cor);
 #pragma unroll 1
-                for (int q = 0; q < nb; ++q) alpha_tile_corner_member_job(pts[p0 + q], q, j, edgk, ct, cs, cor);
+                for (int q = 0; q < nb; ++q) alpha_tile_corner_member_job<kRef>(pts[p0 + q], q, j, edgk, ct, cs, cor);
             }
             for (int j = tid; j < kAlphaTile * (cs + ct); j += kTileThreads)
                 alpha_tile_mixed_job(j, edgk, ct, cs, G, tl, th, sl, sh, n0, m0, Tn, Tm, cor);
@@ -325,7 +330,10 @@ __global__ __launch_bounds__(256) void k_alpha_medge(GridDev g, const Point* __r
 }
 
 
-template <bool kPP>   // the batches' tables have the phi-phi channel (its shared term per k)
+// kPP: the batches' tables have the phi-phi channel (its shared term per k).  kRef: NUSI_OPT_REFERENCE_ORDER -- each
+// point's member corners in the reference's operation order (alpha_batch_mcorner_ref_job: Dcr, Dci, A into the X
+// block, which then holds no Taylor coefficients), the rest of the batch structure unchanged
+template <bool kPP, bool kRef>
 __global__ __launch_bounds__(kTileThreads) __attribute__((amdgpu_waves_per_eu(NUSI_BATCH_WAVES, NUSI_BATCH_WAVES)))
 void k_alpha_batch(GridDev g, const Point* __restrict__ pts, SplineSet spl, const int* __restrict__ tiles,
                    const int* __restrict__ batches, double* __restrict__ A, const double* __restrict__ med,
@@ -415,8 +423,9 @@ void k_alpha_batch(GridDev g, const Point* __restrict__ pts, SplineSet spl, cons
                     ppt = alpha_k_pp(P, spl, k, g.lo[n], g.hi[n], g.lo[m], g.hi[m], lv, wsh);
                 }
             }
-            __syncthreads();   // X is rewritten with the member coefficients
-            for (int j = tid; j < cc; j += kTileThreads) b_xshared(j, edgk, ct, cs, X);
+            __syncthreads();   // X is rewritten with the member coefficients (kRef: with the member corners)
+            if (!kRef)
+                for (int j = tid; j < cc; j += kTileThreads) b_xshared(j, edgk, ct, cs, X);
         }
         // ---- the points, kBatchQC at a time: their member edge leaves in one round, then point by point.
         // (Two points per pair of barriers -- 512-thread workgroups whose halves share the batch's leaves -- measured
@@ -449,15 +458,19 @@ void k_alpha_batch(GridDev g, const Point* __restrict__ pts, SplineSet spl, cons
                 double tot = tnext;   // after states < k
                 if (reload && q + 1 < nb) tnext = A[(size_t)(p0 + q + 1) * g.PT + eidx];
                 __syncthreads();   // member edges written / the previous point's combine is done with mem
-                if (cornered)
-                    for (int j = tid; j < cc; j += kTileThreads) alpha_batch_mcorner_job(Q, j, edgk, ct, cs, X, memb, mem);
+                if (cornered) {
+                    if (kRef)
+                        for (int j = tid; j < cc; j += kTileThreads) alpha_batch_mcorner_ref_job(Q, j, edgk, ct, cs, X);
+                    else
+                        for (int j = tid; j < cc; j += kTileThreads) alpha_batch_mcorner_job(Q, j, edgk, ct, cs, X, memb, mem);
+                }
                 __syncthreads();   // mem of q written
                 int w = 0;
                 if (needed) {
-                    SplitLeaves lv;
+                    SplitLeavesT<kRef> lv;
                     lv.cf[0] = P3; lv.cf[1] = P3; lv.cf[2] = P3; lv.cf[3] = P3; lv.cf[4] = P3;
                     lv.cf[5] = P3 + cc; lv.cf[6] = P3 + 2 * cc;   // (LL, TU1, TU2, G are not read with pre)
-                    lv.corm = mem;
+                    lv.corm = kRef ? X : mem;
                     lv.cc = cc; lv.ct = ct; lv.cs = cs; lv.mb = lm; lv.nb = ln;
                     lv.sidx[0] = sl[lm]; lv.sidx[1] = sh[lm]; lv.tidx[0] = tl[ln]; lv.tidx[1] = th[ln];
                     lv.ted = edgk; lv.sed = edgk + kTEdgeFields * ct; lv.mbv = lv.sed + kSEdgeFields * cs;
@@ -578,18 +591,19 @@ void alpha_tiles_destroy(AlphaTilesDev* t)
 static thread_local const char* t_alpha_kernel = "";   // the main kernel of the latest launch on this thread
 const char* last_alpha_kernel() { return t_alpha_kernel; }
 
-hipError_t launch_alpha(const GridDev& g, const Point* pts, int npts, const SplineSet& spl, const AlphaTilesDev& at,
-                        TablesDev t, int* warn, hipStream_t s, const int* batches, int nbatches, int gmax,
-                        int kernel, int nb_plain)
+template <bool kRef>
+static hipError_t launch_alpha_t(const GridDev& g, const Point* pts, int npts, const SplineSet& spl,
+                                 const AlphaTilesDev& at, TablesDev t, int* warn, hipStream_t s, const int* batches,
+                                 int nbatches, int gmax, int kernel, int nb_plain)
 {
-    t_alpha_kernel = "k_alpha_tile";
+    t_alpha_kernel = kRef ? "k_alpha_tile[refo]" : "k_alpha_tile";
     if (kernel == 0 && batches) {
-        t_alpha_kernel = "k_alpha_batch";
+        t_alpha_kernel = kRef ? "k_alpha_batch[refo]" : "k_alpha_batch";
         // class 0 on the big-batch kernel (batches of up to gmax tables), classes 1 / 2 per table
         if (at.ext_lo < g.T) {
             const long long L = g.T - at.ext_lo, ne = L * (L - 1) / 2;
-            hipLaunchKernelGGL(k_alpha, dim3((unsigned)((ne + 255) / 256), npts), dim3(256), 0, s, g, pts, spl, at.ext_lo,
-                               t.A, warn);
+            hipLaunchKernelGGL(k_alpha<kRef>, dim3((unsigned)((ne + 255) / 256), npts), dim3(256), 0, s, g, pts, spl,
+                               at.ext_lo, t.A, warn);
         }
         int off = 0;
         for (int c = 0; c < 3; ++c) {
@@ -604,15 +618,16 @@ hipError_t launch_alpha(const GridDev& g, const Point* pts, int npts, const Spli
                                        g, pts, t.Med);
                 }
                 if (nb_plain > 0)
-                    hipLaunchKernelGGL(k_alpha_batch<false>, dim3(at.ncls[0], nb_plain), dim3(kTileThreads), lds, s, g,
-                                       pts, spl, at.tiles, batches, t.A, t.Med, warn);
+                    hipLaunchKernelGGL((k_alpha_batch<false, kRef>), dim3(at.ncls[0], nb_plain), dim3(kTileThreads), lds,
+                                       s, g, pts, spl, at.tiles, batches, t.A, t.Med, warn);
                 if (nbatches > nb_plain)
-                    hipLaunchKernelGGL(k_alpha_batch<true>, dim3(at.ncls[0], nbatches - nb_plain), dim3(kTileThreads),
-                                       lds, s, g, pts, spl, at.tiles, batches + nb_plain, t.A, t.Med, warn);
+                    hipLaunchKernelGGL((k_alpha_batch<true, kRef>), dim3(at.ncls[0], nbatches - nb_plain),
+                                       dim3(kTileThreads), lds, s, g, pts, spl, at.tiles, batches + nb_plain, t.A, t.Med,
+                                       warn);
             } else {
                 const size_t lds = sizeof(double) * (size_t)alpha_tile_lds_doubles(cs, ct, 1);
-                hipLaunchKernelGGL(k_alpha_tile<1>, dim3(at.ncls[c], npts), dim3(kTileThreads), lds, s, g, pts, spl,
-                                   at.tiles + off, cs, ct, nullptr, t.A, warn);
+                hipLaunchKernelGGL((k_alpha_tile<1, kRef>), dim3(at.ncls[c], npts), dim3(kTileThreads), lds, s, g, pts,
+                                   spl, at.tiles + off, cs, ct, nullptr, t.A, warn);
             }
             off += at.ncls[c];
         }
@@ -623,10 +638,10 @@ hipError_t launch_alpha(const GridDev& g, const Point* pts, int npts, const Spli
         const long long L = g.T - nlo, ne = L * (L - 1) / 2;
         if (ne <= 0) return;
         dim3 grid((unsigned)((ne + 255) / 256), npts);
-        hipLaunchKernelGGL(k_alpha, grid, dim3(256), 0, s, g, pts, spl, nlo, t.A, warn);
+        hipLaunchKernelGGL(k_alpha<kRef>, grid, dim3(256), 0, s, g, pts, spl, nlo, t.A, warn);
     };
     if (per_entry) {
-        t_alpha_kernel = "k_alpha";
+        t_alpha_kernel = kRef ? "k_alpha[refo]" : "k_alpha";
         per_entry_region(0);
         return hipGetLastError();
     }
@@ -636,21 +651,35 @@ hipError_t launch_alpha(const GridDev& g, const Point* pts, int npts, const Spli
         if (at.ncls[c] == 0) continue;
         const int cs = at.cs_max[c], ct = at.ct_max[c];
         // class 0 (core tiles) runs on batches of tables sharing their (S', t) leaves; the others per table
-        // (batching class 1 too measured slower: its LDS then allows 2 workgroups/CU, profiles/r1l)
-        const bool batched = c == 0 && batches && gmax > 1;
+        // (batching class 1 too measured slower: its LDS then allows 2 workgroups/CU, profiles/r1l).  The
+        // reference-order mode takes this kernel one table per workgroup (its A/B role needs no batches).
+        const bool batched = !kRef && c == 0 && batches && gmax > 1;
         const int G = batched ? (gmax < 4 ? gmax : 4) : 1;
         const size_t lds = sizeof(double) * (size_t)alpha_tile_lds_doubles(cs, ct, G);
         const dim3 grid(at.ncls[c], batched ? nbatches : npts), blk(kTileThreads);
         const int* bt = batched ? batches : nullptr;
-        switch (G) {
-        case 1: hipLaunchKernelGGL(k_alpha_tile<1>, grid, blk, lds, s, g, pts, spl, at.tiles + off, cs, ct, bt, t.A, warn); break;
-        case 2: hipLaunchKernelGGL(k_alpha_tile<2>, grid, blk, lds, s, g, pts, spl, at.tiles + off, cs, ct, bt, t.A, warn); break;
-        case 3: hipLaunchKernelGGL(k_alpha_tile<3>, grid, blk, lds, s, g, pts, spl, at.tiles + off, cs, ct, bt, t.A, warn); break;
-        default: hipLaunchKernelGGL(k_alpha_tile<4>, grid, blk, lds, s, g, pts, spl, at.tiles + off, cs, ct, bt, t.A, warn); break;
+        if (kRef) {
+            hipLaunchKernelGGL((k_alpha_tile<1, true>), grid, blk, lds, s, g, pts, spl, at.tiles + off, cs, ct, bt, t.A,
+                               warn);
+        } else {
+            switch (G) {
+            case 1: hipLaunchKernelGGL((k_alpha_tile<1, false>), grid, blk, lds, s, g, pts, spl, at.tiles + off, cs, ct, bt, t.A, warn); break;
+            case 2: hipLaunchKernelGGL((k_alpha_tile<2, false>), grid, blk, lds, s, g, pts, spl, at.tiles + off, cs, ct, bt, t.A, warn); break;
+            case 3: hipLaunchKernelGGL((k_alpha_tile<3, false>), grid, blk, lds, s, g, pts, spl, at.tiles + off, cs, ct, bt, t.A, warn); break;
+            default: hipLaunchKernelGGL((k_alpha_tile<4, false>), grid, blk, lds, s, g, pts, spl, at.tiles + off, cs, ct, bt, t.A, warn); break;
+            }
         }
         off += at.ncls[c];
     }
     return hipGetLastError();
+}
+
+hipError_t launch_alpha(const GridDev& g, const Point* pts, int npts, const SplineSet& spl, const AlphaTilesDev& at,
+                        TablesDev t, int* warn, hipStream_t s, const int* batches, int nbatches, int gmax,
+                        int kernel, int nb_plain, bool ref)
+{
+    if (ref) return launch_alpha_t<true>(g, pts, npts, spl, at, t, warn, s, batches, nbatches, gmax, kernel, nb_plain);
+    return launch_alpha_t<false>(g, pts, npts, spl, at, t, warn, s, batches, nbatches, gmax, kernel, nb_plain);
 }
 
 }  // namespace nusi

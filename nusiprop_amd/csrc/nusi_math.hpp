@@ -216,11 +216,14 @@ NUSI_FN cd cli2_axis(double x, double y)
 }
 
 // principal-branch Li2(x+iy); y == 0 follows gsl_sf_complex_dilog_xy_e.  cli2_body is the inline body
-// (one call site of the big-batch alpha kernel inlines it), cli2 the out-of-line entry point.
+// (one call site of the big-batch alpha kernel inlines it), cli2 the out-of-line entry point.  kGeneral:
+// no near-axis Taylor shortcut -- the general series everywhere, the operation order of
+// gsl_sf_complex_dilog_xy_e (NUSI_OPT_REFERENCE_ORDER; the oracle's ora_set_reference_order(1))
+template <bool kGeneral = false>
 NUSI_FN cd cli2_body(double x, double y)
 {
     if (y == 0.0) return cd{li2(x), (x >= 1.0) ? -kPi * NUSI_PLOG(x) : 0.0};
-    {
+    if (!kGeneral) {
         const double ax = fabs(x), a1 = fabs(1.0 - x);
         if (fabs(y) <= kLi2AxisRatio * (ax < a1 ? ax : a1)) return cli2_axis(x, y);
     }
@@ -261,8 +264,11 @@ NUSI_FN cd cli2_body(double x, double y)
     const cd s = (u - 0.25 * u2) + (u * u2) * p;
     return add + sgn * s;
 }
-NUSI_FN_OUT cd cli2(double x, double y) { return cli2_body(x, y); }
+NUSI_FN_OUT cd cli2(double x, double y) { return cli2_body<false>(x, y); }
 NUSI_FN cd cli2(cd z) { return cli2(z.r, z.i); }
+NUSI_FN_OUT cd cli2_general(double x, double y) { return cli2_body<true>(x, y); }
+template <bool kRef>
+NUSI_FN cd cli2_t(cd z) { return kRef ? cli2_general(z.r, z.i) : cli2(z.r, z.i); }
 
 // Li3(x), x in [-1, 1/2] (the DSNB source only reaches [-1, 0))
 NUSI_FN double li3(double x)
@@ -299,11 +305,12 @@ NUSI_FN cd li2_asym(cd z)
     return -1 / (16. * (z2 * z2)) - 1 / (9. * (z * z * z)) - 1 / (4. * z2) - 1 / z - C(0.0, 0.5) * t;
 }
 
-// aux.hpp:77-96
+// aux.hpp:77-96 (kRef: the general complex dilogarithm, NUSI_OPT_REFERENCE_ORDER)
+template <bool kRef = false>
 NUSI_FN cd dilogdiff_c(cd x, cd y)
 {
     if (cabs(x) > 1e2 && cabs(y) > 1e2) return li2_asym(x) - li2_asym(y);
-    const cd a = cli2(x), b = cli2(y);
+    const cd a = cli2_t<kRef>(x), b = cli2_t<kRef>(y);
     return C(a.r - b.r, a.i - b.i);
 }
 

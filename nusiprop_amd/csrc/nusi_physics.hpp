@@ -180,6 +180,7 @@ NUSI_FN double gpp_analytic(double a, double b)  // nuSIprop.hpp:885 with a = ma
 // ---------------------------------------------------------------------------
 // Gamma(Em, Ep)  -- nuSIprop.hpp:759-922
 // ---------------------------------------------------------------------------
+template <bool kRef = false>   // kRef: NUSI_OPT_REFERENCE_ORDER (the general complex dilogarithm)
 NUSI_FN double gamma_entry(const Point& P, double Em, double Ep, int& warn)
 {
     const double g = P.g, mphi = P.mphi, Ga = P.Ga;
@@ -226,8 +227,8 @@ NUSI_FN double gamma_entry(const Point& P, double Em, double Ep, int& warn)
             d1 = (sm * sm) * (C(-0.0, -0.5) / C(gr, 1.0) - l1 / 2.) + sm * l1 - sp * l1 + ((sp * sp) * (kI / C(gr, 1.0) + l1)) / 2.;
             d2 = (sm * sm) * (C(0.0, 0.5) / C(gr, -1.0) - l2 / 2.) + sm * l2 - sp * l2 + ((sp * sp) * (C(-0.0, -1.0) / C(gr, -1.0) + l2)) / 2.;
         } else {
-            d1 = dilogdiff_c(z1p, z1m);
-            d2 = dilogdiff_c(z2p, z2m);
+            d1 = dilogdiff_c<kRef>(z1p, z1m);
+            d2 = dilogdiff_c<kRef>(z2p, z2m);
         }
         const double Lgp = nm::log1p(((-1 + sp) * (-1 + sp)) / gr2), Lgm = nm::log1p(((-1 + sm) * (-1 + sm)) / gr2);
         double Gst = -g4 / (32 * kPi * m2 * (1 + gr2)) *
@@ -255,6 +256,7 @@ NUSI_FN double gamma_entry(const Point& P, double Em, double Ep, int& warn)
 // ---------------------------------------------------------------------------
 // alphaTilde(Em, Ep)  -- nuSIprop.hpp:924-1235
 // ---------------------------------------------------------------------------
+template <bool kRef = false>   // kRef: NUSI_OPT_REFERENCE_ORDER (the general complex dilogarithm)
 NUSI_FN double alphat_entry(const Point& P, const SplineSet& spl, double Em, double Ep, int& warn)
 {
     const double g = P.g, mphi = P.mphi, Ga = P.Ga;
@@ -358,10 +360,10 @@ NUSI_FN double alphat_entry(const Point& P, const SplineSet& spl, double Em, dou
             const cd z4 = (1 + tm - tp) / dt_m;
             const cd z5 = C(0.0, 1 - tp) / den;
             const double z6 = 1 - tp / (1 + tm);
-            d78 = dilogdiff_c(C(1 - tm), C(1 - tp));
-            d51 = dilogdiff_c(z5, z1);
-            d26 = dilogdiff_c(C(z2), C(z6));
-            d43 = dilogdiff_c(z4, z3);
+            d78 = dilogdiff_c<kRef>(C(1 - tm), C(1 - tp));
+            d51 = dilogdiff_c<kRef>(z5, z1);
+            d26 = dilogdiff_c<kRef>(C(z2), C(z6));
+            d43 = dilogdiff_c<kRef>(z4, z3);
         }
         const double Lgp = nm::log1p(((1 + tp) * (1 + tp)) / gr2), Lgm = nm::log1p(((1 + tm) * (1 + tm)) / gr2);
         const double Am = carg(C(-1 - tm, gr)), Ap = carg(C(-1 - tp, gr));
@@ -531,9 +533,27 @@ NUSI_FN void alpha_member_corner(const MemberShared& M, double S, double t, doub
     Dci = Dc.i;
     A = (sS + e.sT) + (fS + e.fT - 1.0) * kPi;
 }
-template <bool kInlineCli2 = false>
+// NUSI_OPT_REFERENCE_ORDER: the member leaves in the reference's own operation order -- Dc =
+// gsl_sf_complex_dilog_xy_e of its quotient z = (1 + S + t) / (2 - i gr + t) (C99 complex division,
+// nuSIprop.hpp:1432-1438, 1444-1451), by the general series, and A = carg(-((-1 + i gr + S) / (2 - i gr + t)))
+// (:1456); no Taylor expansion about the real point and no sum of edge arguments.  The oracle's
+// member_dc_ref / member_arg_ref (ora_set_reference_order(1)).
+NUSI_FN void alpha_member_ref(double S, double t, double gr, double& Dcr, double& Dci, double& A)
+{
+    const cd dt = C(2 + t, -gr);
+    const cd z = (1 + S + t) / dt;
+    const cd Dc = cli2_general(z.r, z.i);
+    Dcr = Dc.r;
+    Dci = Dc.i;
+    A = carg(-(C(-1 + S, gr) / dt));
+}
+template <bool kRef = false>
 NUSI_FN void alpha_corner_member(double S, double t, double gr, AlphaCorner& c)
 {
+    if (kRef) {
+        alpha_member_ref(S, t, gr, c.Dcr, c.Dci, c.A);
+        return;
+    }
     MemberShared M;
     alpha_member_shared(S, t, M);
     const MemberTEdge e = alpha_member_tedge(t, gr);
@@ -541,10 +561,11 @@ NUSI_FN void alpha_corner_member(double S, double t, double gr, AlphaCorner& c)
     alpha_member_sarg(S, gr, sS, fS);
     alpha_member_corner(M, S, t, gr, e, sS, fS, c.Dcr, c.Dci, c.A);
 }
+template <bool kRef = false>
 NUSI_FN void alpha_corner(double S, double t, double gr, AlphaCorner& c)
 {
     alpha_corner_shared(S, t, c);
-    alpha_corner_member(S, t, gr, c);
+    alpha_corner_member<kRef>(S, t, gr, c);
 }
 // t-edge leaves (L2 is the member leaf)
 struct AlphaTEdge { double Lm1, la, cm, L2, am; };
@@ -600,18 +621,20 @@ NUSI_FN void alpha_mbin(double Sm, double Sp, double mphi, double Ga, AlphaMBin&
 constexpr int kCornerFields = 10, kTEdgeFields = 5, kSEdgeFields = 4, kMBinFields = 2;
 constexpr int kTEdgeVal = 4, kSEdgeVal = 3;   // edge field holding t resp. S' itself (alpha_t / alpha_S)
 
-// leaves evaluated on the spot (per-entry path, host checks)
-struct DirectLeaves {
+// leaves evaluated on the spot (per-entry path, host checks); kRef: NUSI_OPT_REFERENCE_ORDER
+template <bool kRef = false>
+struct DirectLeavesT {
     double gr, gr2, mphi, Ga;
     NUSI_FN double tval(int, double mk, double E, double m2) const { return alpha_t(mk, E, m2); }
     NUSI_FN double Sval(int, double mk, double E, double m2) const { return alpha_S(mk, E, m2); }
-    NUSI_FN AlphaCorner corner(int, int, double S, double t) const { AlphaCorner c; alpha_corner(S, t, gr, c); return c; }
+    NUSI_FN AlphaCorner corner(int, int, double S, double t) const { AlphaCorner c; alpha_corner<kRef>(S, t, gr, c); return c; }
     NUSI_FN AlphaTEdge tedge(int, double t) const { AlphaTEdge e; alpha_tedge(t, gr2, e); return e; }
     NUSI_FN AlphaSEdge sedge(int, double S) const { AlphaSEdge e; alpha_sedge(S, gr, gr2, e); return e; }
     NUSI_FN AlphaMBin mbin(double Sm, double Sp) const { AlphaMBin b; alpha_mbin(Sm, Sp, mphi, Ga, b); return b; }
     NUSI_FN double xlog(int, double S, double tm, double tp) const { return alpha_xlog(S, tm, tp); }
     NUSI_FN double ylog(int, double Sm, double Sp, double t) const { return alpha_ylog(Sm, Sp, t); }
 };
+using DirectLeaves = DirectLeavesT<false>;
 
 // leaves read from a tile's precomputed arrays (structure of arrays):
 //   cor[v * cc + s * ct + t]  (v = shared field of AlphaCorner, cc = cs * ct),
@@ -767,12 +790,13 @@ NUSI_FN void alpha_tile_corner_job(int j, const double* edgk, int ct, int cs, do
     cor[5 * cc + j] = c.Drr; cor[6 * cc + j] = c.Dri;
 }
 // job j in [0, cs ct): the member leaves of corner j for point P (slot m of the batch)
+template <bool kRef = false>
 NUSI_FN void alpha_tile_corner_member_job(const Point& P, int m, int j, const double* edgk, int ct, int cs, double* cor)
 {
     const int cc = cs * ct;
     const int si = j / ct, ti = j - si * ct;
     AlphaCorner c;
-    alpha_corner_member(edgk[kTEdgeFields * ct + kSEdgeVal * cs + si], edgk[kTEdgeVal * ct + ti], P.a_gr, c);
+    alpha_corner_member<kRef>(edgk[kTEdgeFields * ct + kSEdgeVal * cs + si], edgk[kTEdgeVal * ct + ti], P.a_gr, c);
     double* d = cor + (kCornerShared + kCornerMember * m) * cc;
     d[j] = c.Dcr; d[cc + j] = c.Dci; d[2 * cc + j] = c.A;
 }
@@ -885,8 +909,10 @@ NUSI_FN double alpha_phiphi_scale(const Point& P, double uk, const PPTerm& X)
 
 // Leaves of the big-batch tile kernel (k_alpha_batch): the shared corner fields live in separate blocks
 // (L, Drr, Dri persist for every mass state through the batch loop; LL, TU1, TU2, G and the mixed logs
-// only while the batch's shared brackets are formed), so each field has its own base pointer.
-struct SplitLeaves {
+// only while the batch's shared brackets are formed), so each field has its own base pointer.  kRefA
+// (NUSI_OPT_REFERENCE_ORDER): A is a corner field of its own, corm[2 cc + o] (alpha_batch_mcorner_ref_job).
+template <bool kRefA = false>
+struct SplitLeavesT {
     const double* cf[kCornerShared];   // L LL TU1 TU2 G Drr Dri, each [cc]
     const double *corm, *ted, *sed, *mbv, *tedm, *sedm, *mbm, *xl, *yl;
     const double* marg;                // sT [ct] | fT [ct] | sS [cs] | fS [cs]: A from the edge arguments
@@ -897,7 +923,7 @@ struct SplitLeaves {
         const int o = sidx[si] * ct + tidx[ti];
         const int a = sidx[si], b = tidx[ti];
         // A = arg(S - 1 + i gr) + arg(c + i gr) - pi, the expression of alpha_member_corner
-        const double A = (marg[2 * ct + a] + marg[b]) + (marg[2 * ct + cs + a] + marg[ct + b] - 1.0) * kPi;
+        const double A = kRefA ? corm[2 * cc + o] : (marg[2 * ct + a] + marg[b]) + (marg[2 * ct + cs + a] + marg[ct + b] - 1.0) * kPi;
         return AlphaCorner{cf[0][o], cf[1][o], cf[2][o], cf[3][o], cf[4][o], cf[5][o], cf[6][o],
                            corm[o], corm[cc + o], A};
     }
@@ -917,6 +943,7 @@ struct SplitLeaves {
     NUSI_FN double xlog(int si, double, double, double) const { return xl[sidx[si] * kAlphaTile + nb]; }
     NUSI_FN double ylog(int ti, double, double, double) const { return yl[mb * ct + tidx[ti]]; }
 };
+using SplitLeaves = SplitLeavesT<false>;
 // shared corner leaves of corner j: L, Drr, Dri -> per[0..2][cc] (kept), LL, TU1, TU2, G -> tmp[0..3][cc]
 NUSI_FN void alpha_batch_corner_job(int j, const double* edgk, int ct, int cs, double* per, double* tmp)
 {
@@ -1068,6 +1095,16 @@ NUSI_FN void alpha_batch_mcorner_job(const Point& P, int j, const double* edgk, 
     alpha_member_corner(M, edgk[kTEdgeFields * ct + kSEdgeVal * cs + si], edgk[kTEdgeVal * ct + ti], P.a_gr, e,
                         ext[4 * ct + si], ext[4 * ct + cs + si], Dcr, Dci, A);
     mem[j] = Dcr; mem[cc + j] = Dci;   // (A: SplitLeaves forms it from the edge arguments)
+}
+// NUSI_OPT_REFERENCE_ORDER: member corner leaves of corner j for point P in the reference's operation order
+// (alpha_member_ref) -> mem[0..2][cc] (Dcr, Dci, A); no batch-shared coefficients
+NUSI_FN void alpha_batch_mcorner_ref_job(const Point& P, int j, const double* edgk, int ct, int cs, double* mem)
+{
+    const int cc = cs * ct;
+    const int si = j / ct, ti = j - si * ct;
+    double Dcr, Dci, A;
+    alpha_member_ref(edgk[kTEdgeFields * ct + kSEdgeVal * cs + si], edgk[kTEdgeVal * ct + ti], P.a_gr, Dcr, Dci, A);
+    mem[j] = Dcr; mem[cc + j] = Dci; mem[2 * cc + j] = A;
 }
 // xlog / ylog leaves of mass state k into xl [cs][kAlphaTile], yl [kAlphaTile][ct] (alpha_tile_mixed_job's jobs)
 NUSI_FN void alpha_batch_mixed_job(int j, const double* edgk, int ct, int cs, const int* tl, const int* th,
@@ -1304,9 +1341,10 @@ NUSI_FN void alpha_k(const Point& P, const SplineSet& spl, int k, double Em, dou
         warn |= kWarnAlpha;
 }
 
+template <bool kRef = false>
 NUSI_FN double alpha_entry(const Point& P, const SplineSet& spl, double Em, double Ep, double Emp, double Epp, int& warn)
 {
-    const DirectLeaves lv{P.Ga / P.mphi, (P.Ga / P.mphi) * (P.Ga / P.mphi), P.mphi, P.Ga};
+    const DirectLeavesT<kRef> lv{P.Ga / P.mphi, (P.Ga / P.mphi) * (P.Ga / P.mphi), P.mphi, P.Ga};
     double tot = 0;
     NUSI_MASS_LOOP
     for (int k = 0; k < 3; ++k) alpha_k(P, spl, k, Em, Ep, Emp, Epp, lv, tot, warn);

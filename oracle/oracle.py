@@ -236,3 +236,34 @@ class Oracle:
 
     def alpha(self, Em, Ep, Emp, Epp):
         return lib().ora_alpha(self.h, Em, Ep, Emp, Epp)
+
+
+def evolve_many(points, threads=None, level=0, phiphi_tables=None):
+    """The oracle's evolve() of every point (dicts of constructor arguments, ``source_model`` or ``source``) on a
+    thread pool (ctypes releases the GIL; each thread its own Oracle object), at reference-order `level` (0 = the
+    shared-algorithm order, 1 = the reference's own order; process-wide for the call's duration).  phiphi_tables:
+    (at_path, at_dims, a_path, a_dims) loaded by every object (load_phiphi).  Returns (flux, flux_fla) as [n, 3, N]
+    arrays.  Test / bench-checker infrastructure only."""
+    import concurrent.futures as cf
+    pts = []
+    for p in points:
+        kw = dict(p)
+        if "source_model" in kw:
+            kw["source"] = kw.pop("source_model")
+        pts.append(kw)
+    if threads is None:
+        threads = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+        cap = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+        if cap > 0:
+            threads = min(threads, cap)
+    threads = max(1, min(int(threads), len(pts)))
+
+    def one(kw):
+        o = Oracle(**kw)
+        if phiphi_tables is not None:
+            o.load_phiphi(*phiphi_tables)
+        return o.evolve()
+    with reference_order(level):
+        with cf.ThreadPoolExecutor(threads) as ex:
+            res = list(ex.map(one, pts))
+    return np.stack([r[0] for r in res]), np.stack([r[1] for r in res])

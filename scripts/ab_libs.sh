@@ -8,6 +8,6 @@ for v in "$@"; do
   L=$PWD/nusiprop_amd/libnusi_$v.so
   [ "$v" = base ] && L=$PWD/nusiprop_amd/libnusi.so
   for w in $WL; do
-    NUSIPROP_LIB=$L timeout -k 10 300 python bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-secondary --workload $w > $OUT/${w}_$v.json 2> $OUT/${w}_$v.err || exit 1
+    NUSIPROP_LIB=$L timeout -k 10 300 python bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-secondary --no-parity --workload $w > $OUT/${w}_$v.json 2> $OUT/${w}_$v.err || exit 1
   done
 done

@@ -21,7 +21,7 @@ for WL in $WLS; do
   case $WL in c3) ST=2;; c5) ST=3;; *) ST=5;; esac
   O=$OUT/$WL
   mkdir -p $O
-  B="--workload $WL --steps $ST --warmup 1 --no-cpu-baseline --no-secondary"
+  B="--workload $WL --steps $ST --warmup 1 --no-cpu-baseline --no-secondary --no-parity"
   P="timeout -s KILL 420 rocprofv3 --kernel-trace --output-format csv"
   timeout -k 10 420 rocprofv3 --kernel-trace --stats -d $O/kt -o kt --output-format csv -- python3 bench.py $B > $O/kt.log 2>&1 && \
   $P --pmc FETCH_SIZE -d $O/pmc_fetch -o fetch -- python3 bench.py $B > $O/pmc_fetch.log 2>&1 && \

@@ -1,6 +1,46 @@
+#!/bin/bash
+# One GPU session on the box (the only session driver; round-specific scripts are not kept):
+#   gpurun -- bash scripts/gpu_session.sh <tag> <step> [<step> ...]
+# Steps run in order, each under its own time limit, and the session stops at the first failing step
+# (a GPU fault, abort, time limit or failed test ends it; nothing is retried).  Output: gpurun_out/<tag>/.
+#   tests[=<k-expr>]        python -m pytest tests -m gpu [-k <k-expr>]            -> pytest.log
+#   smoke                   __graft_entry__.smoke()                                 -> smoke.log
+#   profile=<wl>[,<wl>..]   rocprofv3 kernel stats + PMC passes (scripts/gpu_profile_all.sh) -> prof/<wl>/;
+#                           the summaries are copied to profiles/pmc_traffic_<wl>.json
+#   bench[=<a>,<b>,..]      python bench.py <a> <b> ..  (commas = spaces)           -> bench_<i>.json / .err
+#   prof=<a>,<b>,..         rocprofv3 --kernel-trace --stats of bench.py <a> <b> .. -> kt_<i>/
 set -o pipefail
-TAG=${1:-r1n}
-mkdir -p gpurun_out/$TAG
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/$TAG/pytest.log 2>&1 && \
-bash scripts/gpu_bench_profile.sh $TAG && \
-timeout -k 10 600 python bench.py --workload c5 --no-cpu-baseline > gpurun_out/$TAG/bench_c5.json 2> gpurun_out/$TAG/bench_c5.err
+TAG=${1:?tag}
+shift
+OUT=gpurun_out/$TAG
+mkdir -p $OUT
+export TMPDIR=/tmp
+i=0
+for STEP in "$@"; do
+  i=$((i + 1))
+  NAME=${STEP%%=*}
+  ARG=""
+  [ "$NAME" != "$STEP" ] && ARG=${STEP#*=}
+  ARGS=${ARG//,/ }
+  echo "[$(date +%T)] step $i: $STEP" >> $OUT/session.log
+  case $NAME in
+    tests)
+      K=()
+      [ -n "$ARG" ] && K=(-k "$ARG")
+      timeout -k 10 1500 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread "${K[@]}" \
+        > $OUT/pytest.log 2>&1 || { echo "tests failed" >> $OUT/session.log; exit 1; } ;;
+    smoke)
+      timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || exit 1 ;;
+    profile)
+      bash scripts/gpu_profile_all.sh $TAG/prof "$ARGS" || exit 1
+      for w in $ARGS; do cp $OUT/prof/$w/pmc_traffic_summary.json profiles/pmc_traffic_$w.json || exit 1; done ;;
+    bench)
+      timeout -k 10 900 python bench.py $ARGS > $OUT/bench_$i.json 2> $OUT/bench_$i.err || exit 1 ;;
+    prof)
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/kt_$i -o kt --output-format csv -- python3 bench.py $ARGS \
+        > $OUT/kt_$i.log 2>&1 || exit 1 ;;
+    *)
+      echo "unknown step $STEP" >> $OUT/session.log; exit 2 ;;
+  esac
+done
+echo "[$(date +%T)] done" >> $OUT/session.log

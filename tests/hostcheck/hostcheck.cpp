@@ -19,23 +19,44 @@ static nusi::Point mk(const double* pt, const int* flags)
     return P;
 }
 
-int hc_tables(const double* pt, const int* flags, int T, const double* lo, const double* hi,
-              double* G, double* At, double* A /* T*T dense, m>n */)
+}  // extern "C"
+
+// ref: the NUSI_OPT_REFERENCE_ORDER instances (kRef)
+template <bool kRef>
+static int tables_t(const double* pt, const int* flags, int T, const double* lo, const double* hi, double* G, double* At,
+                    double* A)
 {
     const nusi::Point P = mk(pt, flags);
     nusi::SplineSet spl{};
     int w = 0;
     for (int n = 0; n < T; ++n) {
-        G[n] = nusi::gamma_entry(P, lo[n], hi[n], w);
-        At[n] = nusi::alphat_entry(P, spl, lo[n], hi[n], w);
-        for (int m = n + 1; m < T; ++m) A[(size_t)n * T + m] = nusi::alpha_entry(P, spl, lo[n], hi[n], lo[m], hi[m], w);
+        G[n] = nusi::gamma_entry<kRef>(P, lo[n], hi[n], w);
+        At[n] = nusi::alphat_entry<kRef>(P, spl, lo[n], hi[n], w);
+        for (int m = n + 1; m < T; ++m)
+            A[(size_t)n * T + m] = nusi::alpha_entry<kRef>(P, spl, lo[n], hi[n], lo[m], hi[m], w);
     }
     return w;
 }
 
+extern "C" {
+
+int hc_tables(const double* pt, const int* flags, int T, const double* lo, const double* hi,
+              double* G, double* At, double* A /* T*T dense, m>n */)
+{
+    return tables_t<false>(pt, flags, T, lo, hi, G, At, A);
+}
+int hc_tables_ref(const double* pt, const int* flags, int T, const double* lo, const double* hi, double* G, double* At,
+                  double* A)
+{
+    return tables_t<true>(pt, flags, T, lo, hi, G, At, A);
+}
+
+}  // extern "C"
+
 // Host emulation of k_alpha_tile: the same edge lists, job helpers and TileLeaves combine, one
 // tile at a time (work-items run sequentially, phases in kernel order).  alpha dense T*T, m > n.
-int hc_alpha_tiled(const double* pt, const int* flags, int T, const double* lo, const double* hi, double* A)
+template <bool kRef>
+static int alpha_tiled_t(const double* pt, const int* flags, int T, const double* lo, const double* hi, double* A)
 {
     using namespace nusi;
     const Point P = mk(pt, flags);
@@ -65,7 +86,7 @@ int hc_alpha_tiled(const double* pt, const int* flags, int T, const double* lo, 
                     const double* edgk = edg + k * alpha_tile_edge_stride(cs, ct);
                     for (int j = 0; j < cc; ++j) {
                         alpha_tile_corner_job(j, edgk, ct, cs, cor);
-                        alpha_tile_corner_member_job(P, 0, j, edgk, ct, cs, cor);
+                        alpha_tile_corner_member_job<kRef>(P, 0, j, edgk, ct, cs, cor);
                     }
                     for (int j = 0; j < kAlphaTile * (cs + ct); ++j)
                         alpha_tile_mixed_job(j, edgk, ct, cs, G, tl, th, sl, sh, n0, m0, T, T, cor);
@@ -83,6 +104,17 @@ int hc_alpha_tiled(const double* pt, const int* flags, int T, const double* lo, 
             }
         }
     return warn;
+}
+
+extern "C" {
+
+int hc_alpha_tiled(const double* pt, const int* flags, int T, const double* lo, const double* hi, double* A)
+{
+    return alpha_tiled_t<false>(pt, flags, T, lo, hi, A);
+}
+int hc_alpha_tiled_ref(const double* pt, const int* flags, int T, const double* lo, const double* hi, double* A)
+{
+    return alpha_tiled_t<true>(pt, flags, T, lo, hi, A);
 }
 
 double hc_lum(const double* pt, const int* flags, double z, double sfr_z, double Em, double Ep)

@@ -45,3 +45,26 @@ def test_rank_count_mismatch_is_an_error():
     out = _bench(["--gpus", "4", "--dry-run"], env={"WORLD_SIZE": "2", "RANK": "0", "LOCAL_RANK": "0"})
     assert out.returncode != 0 and "WORLD_SIZE=2" in out.stderr
     assert not [l for l in out.stdout.splitlines() if l.startswith("{")]
+
+
+def test_gpus0_is_an_error():
+    """--gpus 0 is rejected, never run as a one-GPU line."""
+    out = _bench(["--gpus", "0", "--dry-run"])
+    assert out.returncode != 0 and "--gpus must be >= 1" in out.stderr
+    assert not [l for l in out.stdout.splitlines() if l.startswith("{")]
+
+
+def test_parity_sample_and_rel_err():
+    """The bench line's parity sample (parity_indices) is deterministic and includes the strongest-coupling column;
+    rel_err follows tests/cases.py (exact zeros required)."""
+    import argparse
+    import numpy as np
+    sys.path.insert(0, ROOT)
+    import bench
+    from nusiprop_amd import scan
+    pts = scan.c4_points()
+    a = bench.parity_indices(argparse.Namespace(workload="c4"), pts)
+    assert a == bench.parity_indices(argparse.Namespace(workload="c4"), pts) and len(a) == 32 == len(set(a))
+    assert sum(1 for i in a if pts[i]["g"] == 1.0) == 16
+    assert bench.rel_err([1.0, 0.0], [1.0, 0.0]) == 0.0 and bench.rel_err([1.0, 1e-300], [1.0, 0.0]) == float("inf")
+    assert abs(bench.rel_err(np.array([1.0 + 1e-12]), np.array([1.0])) - 1e-12) < 1e-15

@@ -89,3 +89,36 @@ def test_tiled_alpha_bit_identical(oracle_mod, name, N):
         d = np.arange(T - 1)
         assert np.array_equal(Ah[d, d + 1], al[d, d + 1])
     assert (w & 4) == (o.warnings() & 4)
+
+
+@pytest.mark.parametrize("name", sorted(cases.SMALL_CASES))
+def test_reference_order_tables_bit_identical(oracle_mod, name):
+    """NUSI_OPT_REFERENCE_ORDER on the device headers (the kRef instances of gamma_entry / alphat_entry /
+    alpha_entry: the general complex dilogarithm, the reference's quotient and carg for the s-t member leaves)
+    against the oracle in reference-order mode (ora_set_reference_order(1)): bit for bit; and they differ from
+    the default order somewhere (the mode is not a no-op) wherever the s-t interference is computed."""
+    from tests.hostcheck import build_hostcheck
+    H = build_hostcheck()
+    kw = dict(cases.SMALL_CASES[name], N_bins_E=40)
+    o = oracle_mod.Oracle(**cases.oracle_kwargs(kw))
+    with oracle_mod.reference_order(1):
+        G, aT, al = o.tables()
+    lo, hi = extended_axis(o)
+    pt, flags = point_array(o, kw)
+    T = o.T
+    Gh, aTh, Ah = np.zeros(T), np.zeros(T), np.zeros((T, T))
+    H.hc_tables_ref.restype = ctypes.c_int
+    w = H.hc_tables_ref(_dp(pt), flags, T, _dp(lo), _dp(hi), _dp(Gh), _dp(aTh), _dp(Ah))
+    assert np.array_equal(Gh, G)
+    assert np.array_equal(aTh, aT)
+    iu = np.triu_indices(T, 1)
+    assert np.array_equal(Ah[iu], al[iu]), "%d alpha entries differ" % np.sum(Ah[iu] != al[iu])
+    assert (w & 7) == o.warnings()
+    Ad = np.zeros((T, T))
+    H.hc_alpha_tiled_ref.restype = ctypes.c_int
+    H.hc_alpha_tiled_ref(_dp(pt), flags, T, _dp(lo), _dp(hi), _dp(Ad))
+    if kw["non_resonant"]:
+        assert np.array_equal(Ad[iu], al[iu]), "tiled: %d alpha entries differ" % np.sum(Ad[iu] != al[iu])
+        if kw["majorana"]:
+            _, _, al0 = o.tables()
+            assert np.any(al0[iu] != al[iu])
