@@ -616,7 +616,10 @@ int shift_groups(nusi_plan* pl, int ntab, std::vector<int>& remap, std::vector<i
             if (c < b) {
                 const double kf = 2.0 * log(tp[cur[0]].mphi / tp[idx[c]].mphi) / lr;
                 o = (int)lround(kf);
-                join = o > last && o <= K && fabs(kf - o) < 1e-6;
+                // the lattice m_phi must reproduce the point's own to a few ulp: m_base r^(-o/2) differs from it by
+                // |kf - o| ln(r) / 2 relative, and the cascade sees only the tables (1e-6 in o let a
+                // point 2e-8 off the lattice take the tables of a slightly different m_phi)
+                join = o > last && o <= K && fabs(kf - o) * lr * 0.5 < 1e-13;
             }
             if (join) {
                 cur.push_back(idx[c]);
@@ -653,12 +656,19 @@ int shift_groups(nusi_plan* pl, int ntab, std::vector<int>& remap, std::vector<i
 
 // the base plan of NUSI_OPT_SHIFT_REUSE: the plan's grid with K more redshift steps, so that its table axis is
 // the plan's, bit for bit, extended by K bins on top (nuSIprop.hpp:224-233: bins >= N are Emin/Emax[N-1] (1 + z));
-// it holds up to max_points / 2 base tables (a base serves >= 2 tables)
-int ensure_shift_plan(nusi_plan* pl)
+// sized for the call's nbase base tables (grown on demand, at most max_points / 2: a base serves >= 2 tables), with
+// the per-row warning records (TablesDev::Wmin) that k_table_shift reads
+int ensure_shift_plan(nusi_plan* pl, int nbase)
 {
     const int K = pl->shift_max;
-    if (pl->shift && pl->shift->grid.T == pl->grid.T + K) return NUSI_OK;
+    if (pl->shift && pl->shift->grid.T == pl->grid.T + K && pl->shift->max_points >= nbase) return NUSI_OK;
+    int cap = nbase;
     if (pl->shift) {
+        cap = std::max(nbase, std::min(2 * pl->shift->max_points, std::max(1, pl->max_points / 2)));
+        if (pl->ran) {   // the previous call's kernels read the old base tables
+            HIPCHECK(hipSetDevice(pl->device));
+            HIPCHECK(hipEventSynchronize(pl->ev_done));
+        }
         nusi_plan_destroy(pl->shift);
         pl->shift = nullptr;
     }
@@ -666,7 +676,7 @@ int ensure_shift_plan(nusi_plan* pl)
     const double r = G.Emax[0] / G.Emin[0];
     const double zb = pow(r, G.Nz + K - 1.5) - 1;   // N_steps_z = (int)(ln(1 + zb) / ln r + 2) = Nz + K
     nusi_plan* sp = nullptr;
-    int rc = nusi_plan_create(pl->device, G.N, G.lEmin, G.lEmax, zb, std::max(1, pl->max_points / 2), &sp);
+    int rc = nusi_plan_create(pl->device, G.N, G.lEmin, G.lEmax, zb, std::max(1, cap), &sp);
     if (rc) return rc;
     const HostGrid& B = sp->grid;
     bool same = B.T == G.T + K;
@@ -679,6 +689,10 @@ int ensure_shift_plan(nusi_plan* pl)
     sp->alpha_kind = pl->alpha_kind;
     sp->spl = pl->spl;
     HIPCHECK(hipSetDevice(pl->device));
+    if (hipMalloc(&sp->tabs.Wmin, sizeof(int) * 4 * (size_t)B.T * sp->max_points) != hipSuccess) {
+        nusi_plan_destroy(sp);
+        return fail(NUSI_EHIP, "shift reuse: no device memory for the base plan's warning records");
+    }
     if (!pl->d_smap) {
         HIPCHECK(hipMalloc(&pl->d_smap, sizeof(int2) * pl->max_points));
         HIPCHECK(hipHostMalloc((void**)&pl->h_smap, sizeof(int2) * pl->max_points, hipHostMallocDefault));
@@ -743,6 +757,7 @@ void nusi_plan_destroy(nusi_plan* pl)
     hipFree(pl->tabs.At);
     hipFree(pl->tabs.A);
     hipFree(pl->tabs.Med);
+    hipFree(pl->tabs.Wmin);
     hipFree(pl->d_src);
     hipFree(pl->d_smap);
     if (pl->h_smap) hipHostFree(pl->h_smap);
@@ -923,7 +938,7 @@ int nusi_plan_evolve(nusi_plan* pl, const nusi_params* pts, int n, double* d_flu
         nd = shift_groups(pl, ntab, remap, smap, bases);
         nbase = (int)bases.size();
         if (nbase) {
-            const int r = ensure_shift_plan(pl);
+            const int r = ensure_shift_plan(pl, nbase);
             if (r) return r;
             if (nbase > pl->shift->max_points) return fail(NUSI_EPARAM, "shift reuse: more base tables than the base plan holds");
             std::vector<nusi::Point> tmp(pl->h_tpts, pl->h_tpts + ntab);
@@ -1049,6 +1064,7 @@ int nusi_plan_evolve(nusi_plan* pl, const nusi_params* pts, int n, double* d_flu
                                 hipMemcpyHostToDevice, s));
         HIPCHECK(hipEventRecord(sp->ev_copy, s));
         HIPCHECK(hipMemsetAsync(sp->d_warn, 0, sizeof(int) * nbase, s));
+        HIPCHECK(hipMemsetAsync(sp->tabs.Wmin, 0x7f, sizeof(int) * 4 * (size_t)sp->grid.T * nbase, s));   // no row warned
         sp->ran = true;
     }
     HIPCHECK(hipEventRecord(pl->ev_copy, s));
@@ -1068,8 +1084,7 @@ int nusi_plan_evolve(nusi_plan* pl, const nusi_params* pts, int n, double* d_flu
         const AlphaBatches& bb = pl->shift_batches;
         HIPCHECK(nusi::launch_alpha(sp->gd, sp->d_tpts, nbase, spl, sp->atiles, sp->tabs, sp->d_warn, s, sp->d_batches,
                                     bb.nbatch, bb.cap, pl->alpha_kind, bb.nb_plain, refo));
-        HIPCHECK(nusi::launch_table_shift(pl->gd, sp->gd, pl->d_smap, nd, ntab - nd, sp->tabs, sp->d_warn, pl->tabs,
-                                          pl->d_warn, s));
+        HIPCHECK(nusi::launch_table_shift(pl->gd, sp->gd, pl->d_smap, nd, ntab - nd, sp->tabs, pl->tabs, pl->d_warn, s));
     }
     HIPCHECK(hipEventRecord(ev[2], s));
     if (fast && any_dsnb) HIPCHECK(nusi::launch_source_dsnb(pl->gd, pl->d_pts, n, pl->d_src, s));

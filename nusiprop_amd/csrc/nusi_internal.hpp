@@ -32,6 +32,9 @@ struct TablesDev {
     double* A;    // [npts][PT]
     double* Med;  // [npts][3][kMedFields T]: member edge leaves of every bin edge (k_alpha_medge)
     double* Src;  // [npts][T (Nz-1)]: DSNB source terms c_i Lum (k_source_dsnb, diagonal layout), or nullptr
+    int* Wmin;    // [npts][4][T] or nullptr (only the base plan of NUSI_OPT_SHIFT_REUSE): per warning bit b and table
+                  // row n, the smallest column m of an entry (n, m) that raised it (Gamma / alphaTilde: m = n), so
+                  // that k_table_shift passes on exactly the warnings of the rows a shifted slot reads
 };
 
 // Tiles of the alpha table for k_alpha_tile: kAlphaTile x kAlphaTile (n, m) bin blocks with
@@ -61,9 +64,10 @@ hipError_t launch_alpha(const GridDev& g, const Point* pts, int npts, const Spli
                         TablesDev t, int* warn, hipStream_t s, const int* batches, int nbatches, int gmax,
                         int kernel, int nb_plain, bool ref);
 // NUSI_OPT_SHIFT_REUSE: tables s0 .. s0 + nshift - 1 of t (grid g) <- base tables map[q].x of tb (grid gb, the
-// axis extended on top), read map[q].y bins higher; warn[s] |= warnb[base]
+// axis extended on top), read map[q].y bins higher; warn[s] |= the warning bits of the base rows the slot reads
+// (tb.Wmin, required)
 hipError_t launch_table_shift(const GridDev& g, const GridDev& gb, const int2* map, int s0, int nshift, TablesDev tb,
-                              const int* warnb, TablesDev t, int* warn, hipStream_t s);
+                              TablesDev t, int* warn, hipStream_t s);
 // The MFMA cascade (NUSI_CASCADE_AUTO / MFMA): k_cascade_ws -- R = 1, one point per workgroup (groups
 // unused, nwg = points), or R = 2, groups[k] = two points sharing one table slot (y < 0: one point) -- for
 // Nz - 1 <= 48, k_cascade_wsp (step passes) for any number of steps.  Every point kind: the DSNB points'

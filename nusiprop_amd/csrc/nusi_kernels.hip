@@ -17,6 +17,17 @@ namespace nusi {
 // ---------------------------------------------------------------------------
 // Stage A
 // ---------------------------------------------------------------------------
+// a warning w of entry (n, m) of table p: the table's word, and (shift-reuse base plans, wmin != nullptr) the
+// row record TablesDev::Wmin
+__device__ inline void warn_entry(int* warn, int* wmin, int T, int p, int w, int n, int m)
+{
+    atomicOr(&warn[p], w);
+    if (wmin)
+#pragma unroll
+        for (int b = 0; b < 4; ++b)
+            if ((w >> b) & 1) atomicMin(&wmin[((size_t)p * 4 + b) * T + n], m);
+}
+
 #ifndef NUSI_GA_WAVES   // Gamma / alphaTilde kernel waves per SIMD (A/B)
 #define NUSI_GA_WAVES 4   // with Gamma / alphaTilde split over work-items: 4 0.525, 3 0.535 ms (was 0.572 unsplit at 3)
 #endif
@@ -24,7 +35,7 @@ namespace nusi {
 template <bool kRef>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NUSI_GA_WAVES, NUSI_GA_WAVES))) void k_gamma_alphat(GridDev g, const Point* __restrict__ pts, SplineSet spl,
                                                      double* __restrict__ G, double* __restrict__ At,
-                                                     int* __restrict__ warn)
+                                                     int* __restrict__ warn, int* __restrict__ wmin)
 {
     const int p = blockIdx.y;
     const int n = blockIdx.x * 64 + threadIdx.x;
@@ -36,7 +47,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NUSI_GA_WAVE
         G[(size_t)p * g.T + n] = gamma_entry<kRef>(P, lo, hi, w);
     else
         At[(size_t)p * g.T + n] = alphat_entry<kRef>(P, spl, lo, hi, w);
-    if (w) atomicOr(&warn[p], w);
+    if (w) warn_entry(warn, wmin, g.T, p, w, n, n);
 }
 
 // 4 x 4 windows of a 3-D spline table (nusi_spline.hpp): fw[16 node + 4 a1 + a2] = f[i0][i1 + a1][i2 + a2]
@@ -74,7 +85,7 @@ hipError_t spline_windows_build(const float* f, int n0, int n1, int n2, float* f
 template <bool kRef>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NUSI_PE_WAVES, NUSI_PE_WAVES)))
 void k_alpha(GridDev g, const Point* __restrict__ pts, SplineSet spl, int nlo,
-                                               double* __restrict__ A, int* __restrict__ warn)
+                                               double* __restrict__ A, int* __restrict__ warn, int* __restrict__ wmin)
 {
     const int p = blockIdx.y;
     const long long L = g.T - nlo;
@@ -93,15 +104,15 @@ void k_alpha(GridDev g, const Point* __restrict__ pts, SplineSet spl, int nlo,
     // without non-s channels the cascade reads only alpha(n, n+1) (nuSIprop.hpp:273-275)
     if (P.non_resonant || m == n + 1) v = alpha_entry<kRef>(P, spl, g.lo[n], g.hi[n], g.lo[m], g.hi[m], w);
     A[(size_t)p * g.PT + (size_t)m * (m - 1) / 2 + n] = v;
-    if (w) atomicOr(&warn[p], w);
+    if (w) warn_entry(warn, wmin, g.T, p, w, n, m);
 }
 
 hipError_t launch_gamma_alphat(const GridDev& g, const Point* pts, int npts, const SplineSet& spl, TablesDev t,
                                int* warn, hipStream_t s, bool ref)
 {
     dim3 grid((g.T + 63) / 64, npts, 2);
-    if (ref) hipLaunchKernelGGL(k_gamma_alphat<true>, grid, dim3(64), 0, s, g, pts, spl, t.G, t.At, warn);
-    else hipLaunchKernelGGL(k_gamma_alphat<false>, grid, dim3(64), 0, s, g, pts, spl, t.G, t.At, warn);
+    if (ref) hipLaunchKernelGGL(k_gamma_alphat<true>, grid, dim3(64), 0, s, g, pts, spl, t.G, t.At, warn, t.Wmin);
+    else hipLaunchKernelGGL(k_gamma_alphat<false>, grid, dim3(64), 0, s, g, pts, spl, t.G, t.At, warn, t.Wmin);
     return hipGetLastError();
 }
 
@@ -142,7 +153,8 @@ template <int G, bool kRef>   // batch capacity (compile time, so that G = 1 kee
 __global__ __launch_bounds__(kTileThreads) NUSI_TILE_ATTR void k_alpha_tile(GridDev g, const Point* __restrict__ pts, SplineSet spl,
                                                            const int* __restrict__ tiles, int cs_max, int ct_max,
                                                            const int* __restrict__ batches,
-                                                           double* __restrict__ A, int* __restrict__ warn)
+                                                           double* __restrict__ A, int* __restrict__ warn,
+                                                           int* __restrict__ wmin)
 {
     extern __shared__ __attribute__((aligned(16))) double sm[];
     __shared__ double tE[2 * kAlphaTile], sE[2 * kAlphaTile];
@@ -239,7 +251,7 @@ __global__ __launch_bounds__(kTileThreads) NUSI_TILE_ATTR void k_alpha_tile(Grid
                 alpha_k(pts[p0 + q], spl, k, g.lo[n], g.hi[n], g.lo[m], g.hi[m], lv, tot, w, share ? &pre : nullptr);
                 if (G > 1) tsum[q * kTileThreads + tid] = tot;
                 else tot1 = tot;
-                if (w) atomicOr(&warn[p0 + q], w);
+                if (w) warn_entry(warn, wmin, T, p0 + q, w, n, m);
             }
         }
     }
@@ -337,7 +349,7 @@ template <bool kPP, bool kRef>
 __global__ __launch_bounds__(kTileThreads) __attribute__((amdgpu_waves_per_eu(NUSI_BATCH_WAVES, NUSI_BATCH_WAVES)))
 void k_alpha_batch(GridDev g, const Point* __restrict__ pts, SplineSet spl, const int* __restrict__ tiles,
                    const int* __restrict__ batches, double* __restrict__ A, const double* __restrict__ med,
-                   int* __restrict__ warn)
+                   int* __restrict__ warn, int* __restrict__ wmin)
 {
     extern __shared__ __attribute__((aligned(16))) double sm[];
     __shared__ double tE[2 * kAlphaTile], sE[2 * kAlphaTile];
@@ -481,19 +493,21 @@ void k_alpha_batch(GridDev g, const Point* __restrict__ pts, SplineSet spl, cons
                             kPP && cornered ? &ppt : nullptr);
                 }
                 if (valid) A[(size_t)(p0 + q) * g.PT + eidx] = needed ? tot : 0.0;
-                if (w) atomicOr(&warn[p0 + q], w);
+                if (w) warn_entry(warn, wmin, T, p0 + q, w, n, m);
             }
         }
     }
-    if (wsh)
-        for (int q = 0; q < nb; ++q) atomicOr(&warn[p0 + q], wsh);
+    if (wsh)   // (the batch-shared phi-phi term of this thread's entry)
+        for (int q = 0; q < nb; ++q) warn_entry(warn, wmin, T, p0 + q, wsh, n, m);
 }
 
 // NUSI_OPT_SHIFT_REUSE: table slot s0 + q <- base table map[q].x of the extended axis (Tb bins),
-// read map[q].y bins higher; the base's warning bits go with it.  A copy, HBM-bound: 2 x 8 B per entry.
+// read map[q].y = o bins higher.  A copy, HBM-bound: 2 x 8 B per entry.  The slot reads the base's entries (n', m')
+// with o <= n' <= m' <= T - 1 + o, so it takes warning bit b iff some row n' in [o, T + o) has an entry of column
+// <= T - 1 + o that raised it (tb.Wmin, the base's row records): the bits of the base's bins outside the slot's
+// range -- below o and above T - 1 + o -- are not passed on.
 __global__ __launch_bounds__(256) void k_table_shift(int T, long long PT, int Tb, long long PTb, const int2* __restrict__ map,
-                                                     int s0, TablesDev tb, const int* __restrict__ warnb, TablesDev t,
-                                                     int* __restrict__ warn)
+                                                     int s0, TablesDev tb, TablesDev t, int* __restrict__ warn)
 {
     const int q = blockIdx.y, s = s0 + q;
     const int bi = map[q].x, o = map[q].y;
@@ -501,7 +515,11 @@ __global__ __launch_bounds__(256) void k_table_shift(int T, long long PT, int Tb
     if (e < T) {
         t.G[(size_t)s * T + e] = tb.G[(size_t)bi * Tb + e + o];
         t.At[(size_t)s * T + e] = tb.At[(size_t)bi * Tb + e + o];
-        if (e == 0 && warnb[bi]) atomicOr(&warn[s], warnb[bi]);
+        int bits = 0;
+#pragma unroll
+        for (int b = 0; b < 4; ++b)
+            if (tb.Wmin[((size_t)bi * 4 + b) * Tb + e + o] <= T - 1 + o) bits |= 1 << b;
+        if (bits) atomicOr(&warn[s], bits);
     }
     if (e >= PT) return;
     int m = (int)((1.0 + sqrt(1.0 + 8.0 * (double)e)) * 0.5);   // packed index e = m (m - 1) / 2 + n, n < m
@@ -512,12 +530,13 @@ __global__ __launch_bounds__(256) void k_table_shift(int T, long long PT, int Tb
 }
 
 hipError_t launch_table_shift(const GridDev& g, const GridDev& gb, const int2* map, int s0, int nshift, TablesDev tb,
-                              const int* warnb, TablesDev t, int* warn, hipStream_t s)
+                              TablesDev t, int* warn, hipStream_t s)
 {
     if (nshift <= 0) return hipSuccess;
+    if (!tb.Wmin) return hipErrorInvalidValue;
     const long long ne = std::max<long long>(g.PT, g.T);
     hipLaunchKernelGGL(k_table_shift, dim3((unsigned)((ne + 255) / 256), nshift), dim3(256), 0, s, g.T, g.PT, gb.T, gb.PT,
-                       map, s0, tb, warnb, t, warn);
+                       map, s0, tb, t, warn);
     return hipGetLastError();
 }
 
@@ -603,7 +622,7 @@ static hipError_t launch_alpha_t(const GridDev& g, const Point* pts, int npts, c
         if (at.ext_lo < g.T) {
             const long long L = g.T - at.ext_lo, ne = L * (L - 1) / 2;
             hipLaunchKernelGGL(k_alpha<kRef>, dim3((unsigned)((ne + 255) / 256), npts), dim3(256), 0, s, g, pts, spl,
-                               at.ext_lo, t.A, warn);
+                               at.ext_lo, t.A, warn, t.Wmin);
         }
         int off = 0;
         for (int c = 0; c < 3; ++c) {
@@ -619,15 +638,15 @@ static hipError_t launch_alpha_t(const GridDev& g, const Point* pts, int npts, c
                 }
                 if (nb_plain > 0)
                     hipLaunchKernelGGL((k_alpha_batch<false, kRef>), dim3(at.ncls[0], nb_plain), dim3(kTileThreads), lds,
-                                       s, g, pts, spl, at.tiles, batches, t.A, t.Med, warn);
+                                       s, g, pts, spl, at.tiles, batches, t.A, t.Med, warn, t.Wmin);
                 if (nbatches > nb_plain)
                     hipLaunchKernelGGL((k_alpha_batch<true, kRef>), dim3(at.ncls[0], nbatches - nb_plain),
                                        dim3(kTileThreads), lds, s, g, pts, spl, at.tiles, batches + nb_plain, t.A, t.Med,
-                                       warn);
+                                       warn, t.Wmin);
             } else {
                 const size_t lds = sizeof(double) * (size_t)alpha_tile_lds_doubles(cs, ct, 1);
                 hipLaunchKernelGGL((k_alpha_tile<1, kRef>), dim3(at.ncls[c], npts), dim3(kTileThreads), lds, s, g, pts,
-                                   spl, at.tiles + off, cs, ct, nullptr, t.A, warn);
+                                   spl, at.tiles + off, cs, ct, nullptr, t.A, warn, t.Wmin);
             }
             off += at.ncls[c];
         }
@@ -638,7 +657,7 @@ static hipError_t launch_alpha_t(const GridDev& g, const Point* pts, int npts, c
         const long long L = g.T - nlo, ne = L * (L - 1) / 2;
         if (ne <= 0) return;
         dim3 grid((unsigned)((ne + 255) / 256), npts);
-        hipLaunchKernelGGL(k_alpha<kRef>, grid, dim3(256), 0, s, g, pts, spl, nlo, t.A, warn);
+        hipLaunchKernelGGL(k_alpha<kRef>, grid, dim3(256), 0, s, g, pts, spl, nlo, t.A, warn, t.Wmin);
     };
     if (per_entry) {
         t_alpha_kernel = kRef ? "k_alpha[refo]" : "k_alpha";
@@ -660,13 +679,13 @@ static hipError_t launch_alpha_t(const GridDev& g, const Point* pts, int npts, c
         const int* bt = batched ? batches : nullptr;
         if (kRef) {
             hipLaunchKernelGGL((k_alpha_tile<1, true>), grid, blk, lds, s, g, pts, spl, at.tiles + off, cs, ct, bt, t.A,
-                               warn);
+                               warn, t.Wmin);
         } else {
             switch (G) {
-            case 1: hipLaunchKernelGGL((k_alpha_tile<1, false>), grid, blk, lds, s, g, pts, spl, at.tiles + off, cs, ct, bt, t.A, warn); break;
-            case 2: hipLaunchKernelGGL((k_alpha_tile<2, false>), grid, blk, lds, s, g, pts, spl, at.tiles + off, cs, ct, bt, t.A, warn); break;
-            case 3: hipLaunchKernelGGL((k_alpha_tile<3, false>), grid, blk, lds, s, g, pts, spl, at.tiles + off, cs, ct, bt, t.A, warn); break;
-            default: hipLaunchKernelGGL((k_alpha_tile<4, false>), grid, blk, lds, s, g, pts, spl, at.tiles + off, cs, ct, bt, t.A, warn); break;
+            case 1: hipLaunchKernelGGL((k_alpha_tile<1, false>), grid, blk, lds, s, g, pts, spl, at.tiles + off, cs, ct, bt, t.A, warn, t.Wmin); break;
+            case 2: hipLaunchKernelGGL((k_alpha_tile<2, false>), grid, blk, lds, s, g, pts, spl, at.tiles + off, cs, ct, bt, t.A, warn, t.Wmin); break;
+            case 3: hipLaunchKernelGGL((k_alpha_tile<3, false>), grid, blk, lds, s, g, pts, spl, at.tiles + off, cs, ct, bt, t.A, warn, t.Wmin); break;
+            default: hipLaunchKernelGGL((k_alpha_tile<4, false>), grid, blk, lds, s, g, pts, spl, at.tiles + off, cs, ct, bt, t.A, warn, t.Wmin); break;
             }
         }
         off += at.ncls[c];

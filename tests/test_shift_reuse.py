@@ -92,3 +92,82 @@ def test_shift_reuse_option_bounds(nusi):
         plan.set_option(_lib.OPT_SHIFT_REUSE, 129)
     with pytest.raises(Exception):
         plan.set_option(_lib.OPT_SHIFT_REUSE, -1)
+
+
+def test_shift_reuse_c4s_lattice_k128(nusi, oracle_mod):
+    """The bench's c4s workload at its own K (NUSI_OPT_SHIFT_REUSE = 128, offsets 0 .. 124 on scan.c4s_points'
+    lattice), at g = 1e-3 and g = 1 (the coupling extremes): 64 points, every flux within the 1e-9 north-star bound
+    of each point's own oracle evolution (VERDICT r3 #7)."""
+    from nusiprop_amd import _lib, scan
+    pts = scan.c4s_points(n_g=2)
+    assert sorted({p["g"] for p in pts}) == [1e-3, 1.0] and len(pts) == 64
+    p0 = pts[0]
+    plan = nusi.Plan(p0["N_bins_E"], p0["lEmin"], p0["lEmax"], p0["zmax"], max_points=len(pts))
+    plan.set_option(_lib.OPT_SHIFT_REUSE, 128)
+    flux, fla = plan.evolve(pts)
+    assert "k_table_shift" in plan.kernels()[0]
+    plan.close()
+    f_ref, fla_ref = oracle_mod.evolve_many(pts)
+    errs = [max(cases.rel_err(flux[i], f_ref[i]), cases.rel_err(fla[i], fla_ref[i])) for i in range(len(pts))]
+    worst = int(np.argmax(errs))
+    assert errs[worst] <= SHIFT_RTOL, (pts[worst]["mphi"], pts[worst]["g"], errs[worst])
+    print("c4s K=128 at g = 1e-3, 1: worst flux rel err %.2e" % errs[worst])
+
+
+def test_shift_reuse_rounded_mphi_goes_direct(nusi, oracle_mod):
+    """A point within 1e-6 of a lattice offset but not ON the lattice (m_phi rounded to 7 significant digits) is
+    not served by the base's shifted tables, whose m_phi would differ from its own by ~1e-8 (ADVICE r3): it is
+    built directly, bit-exact, while its exact lattice partner still shares the base."""
+    from nusiprop_amd import _lib
+    base = dict(cases.C2B_100)
+    exact = _lattice_points(base, (0, 3), (0.1,))
+    r = 10 ** ((base["lEmax"] - base["lEmin"]) / base["N_bins_E"])
+    m6 = 6e5 * r ** (-6 / 2)
+    rounded = dict(base, mphi=float("%.7g" % m6), g=0.1)
+    assert rounded["mphi"] != m6 and abs(rounded["mphi"] / m6 - 1) < 1e-6
+    pts = exact + [rounded]
+    plan = nusi.Plan(base["N_bins_E"], base["lEmin"], base["lEmax"], base["zmax"], max_points=len(pts))
+    plan.set_option(_lib.OPT_SHIFT_REUSE, 8)
+    flux, fla = plan.evolve(pts)
+    assert "k_table_shift" in plan.kernels()[0]
+    o = oracle_mod.Oracle(**cases.oracle_kwargs(rounded))
+    G, aT, al = o.tables()
+    Gg, aTg, Ag = plan.tables(2)
+    plan.close()
+    assert np.array_equal(Gg, G) and np.array_equal(aTg, aT)
+    iu = np.triu_indices(o.T, 1)
+    assert np.array_equal(nusi.unpack_alpha(Ag, o.T)[iu], al[iu])
+
+
+def test_shift_reuse_phiphi_warnings_in_range(nusi, ref_tables):
+    """phi-phi on with shift reuse: the base tables are built on the axis extended by K bins, where alpha's phi-phi
+    lookups reach x1 = (m - n) 1.0001 > 1000, outside the reference's table nodes (interp.hpp:355-361).  No member
+    reads those entries (its own axis has T <= 1000 bins), so no member may inherit the warning (ADVICE r3): the
+    members' warnings equal the direct path's (none), and the call does not fail with NUSI_EINTERP."""
+    from nusiprop_amd import _lib
+    at, atd, a, ad = ref_tables
+    base = dict(cases.C2B_100, N_bins_E=850, phiphi=True)
+    K = 30
+    pts = _lattice_points(base, (0, 10, 20, 30), (0.1,), m_max=3e7)
+    plan = nusi.Plan(850, base["lEmin"], base["lEmax"], base["zmax"], max_points=len(pts))
+    plan.load_phiphi(at, a)
+    assert plan.T <= 1000
+    f_direct, _ = plan.evolve(pts)
+    w_direct = plan.warnings(len(pts))
+    plan.set_option(_lib.OPT_SHIFT_REUSE, K)
+    f_shift, _ = plan.evolve(pts)
+    assert "k_table_shift" in plan.kernels()[0]
+    assert plan.warnings(len(pts)) == w_direct and all(w & 8 == 0 for w in w_direct)
+    assert cases.rel_err(f_shift, f_direct) <= SHIFT_RTOL
+    # the base axis itself (K more redshift steps, as nusi_capi.cpp ensure_shift_plan makes it) does reach
+    # out-of-node lookups: the case the test is about
+    r = 10 ** ((base["lEmax"] - base["lEmin"]) / base["N_bins_E"])
+    zb = r ** (plan.Nz + K - 1.5) - 1
+    sp = nusi.Plan(850, base["lEmin"], base["lEmax"], zb, max_points=1)
+    sp.load_phiphi(at, a)
+    assert sp.T == plan.T + K
+    with pytest.raises(_lib.NusiError) as e:
+        sp.evolve([dict(pts[0], zmax=zb)])
+    assert e.value.code == _lib.NUSI_EINTERP
+    plan.close()
+    sp.close()
