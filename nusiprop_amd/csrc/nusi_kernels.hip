@@ -18,8 +18,9 @@ namespace nusi {
 // Stage A
 // ---------------------------------------------------------------------------
 // a warning w of entry (n, m) of table p: the table's word, and (shift-reuse base plans, wmin != nullptr) the
-// row record TablesDev::Wmin
-__device__ inline void warn_entry(int* warn, int* wmin, int T, int p, int w, int n, int m)
+// row record TablesDev::Wmin.  Out of line: it runs only on a warning, and inlined its atomics cost the hot
+// kernels' register allocation (k_alpha_batch: 39 -> 41 VGPR spills)
+__device__ __attribute__((noinline)) void warn_entry(int* warn, int* wmin, int T, int p, int w, int n, int m)
 {
     atomicOr(&warn[p], w);
     if (wmin)
