@@ -229,6 +229,9 @@ struct SplineStore {
     int device = 0;
     std::vector<void*> bufs;
     nusi::SplineSet set;
+    nusi::SplineSet* d_set = nullptr;   // `set` in device memory: the kernels take it by pointer (a by-value
+                                        // kernel argument whose address reaches a call is copied to scratch
+                                        // by every work-item, 320 B each)
     ~SplineStore()
     {
         if (bufs.empty()) return;
@@ -440,6 +443,7 @@ struct nusi_plan {
     nusi::AlphaTilesDev atiles{};
     double* d_scratch = nullptr;   // flux outputs when the caller passes NULL
     std::shared_ptr<SplineStore> spl;
+    nusi::SplineSet* d_nospl = nullptr;   // an empty spline set in device memory (no phi-phi tables loaded)
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
     hipEvent_t ev_copy = nullptr;
     hipEvent_t ev_done = nullptr;      // end of the latest call's kernels (the next call waits for it)
@@ -758,6 +762,7 @@ void nusi_plan_destroy(nusi_plan* pl)
     hipFree(pl->tabs.A);
     hipFree(pl->tabs.Med);
     hipFree(pl->tabs.Wmin);
+    hipFree(pl->d_nospl);
     hipFree(pl->d_src);
     hipFree(pl->d_smap);
     if (pl->h_smap) hipHostFree(pl->h_smap);
@@ -846,6 +851,11 @@ int nusi_plan_create(int device, int N_bins_E, double lEmin, double lEmax, doubl
     HIPCHECK(hipMalloc(&pl->tabs.At, sizeof(double) * (size_t)G.T * max_points));
     HIPCHECK(hipMalloc(&pl->tabs.A, sizeof(double) * (size_t)gd.PT * max_points));
     HIPCHECK(hipMalloc(&pl->tabs.Med, sizeof(double) * 3 * nusi::kMedFields * (size_t)G.T * max_points));
+    {   // the empty spline set of plans without phi-phi tables (device memory, like SplineStore::d_set)
+        const nusi::SplineSet none{};
+        HIPCHECK(hipMalloc(&pl->d_nospl, sizeof(nusi::SplineSet)));
+        HIPCHECK(hipMemcpy(pl->d_nospl, &none, sizeof(nusi::SplineSet), hipMemcpyHostToDevice));
+    }
     std::vector<unsigned char> shared(G.T, 0);   // bin edges shared bitwise with the next bin
     for (int n = 0; n + 1 < G.T; ++n) shared[n] = (G.hi[n] == G.lo[n + 1]);
     HIPCHECK(nusi::alpha_tiles_create(G.T, shared.data(), &pl->atiles));
@@ -886,6 +896,9 @@ int nusi_plan_load_phiphi(nusi_plan* pl, const char* at_path, const int* at_dims
     if (r) return r;
     r = load_spline(a_path, 3, d3, *st, st->set.a);
     if (r) return r;
+    HIPCHECK(hipMalloc(&st->d_set, sizeof(nusi::SplineSet)));
+    st->bufs.push_back(st->d_set);
+    HIPCHECK(hipMemcpy(st->d_set, &st->set, sizeof(nusi::SplineSet), hipMemcpyHostToDevice));
     slot->set = st;
     pl->spl = st;
     return NUSI_OK;
@@ -1069,7 +1082,7 @@ int nusi_plan_evolve(nusi_plan* pl, const nusi_params* pts, int n, double* d_flu
     }
     HIPCHECK(hipEventRecord(pl->ev_copy, s));
     HIPCHECK(hipMemsetAsync(pl->d_warn, 0, sizeof(int) * ntab, s));
-    const nusi::SplineSet spl = pl->spl ? pl->spl->set : nusi::SplineSet{};
+    const nusi::SplineSet* spl = pl->spl ? pl->spl->d_set : pl->d_nospl;
     hipEvent_t* ev = pl->ev;
     if (pl->prof_n < pl->prof_max) ev = &pl->prof_ev[4 * (size_t)pl->prof_n++];
     HIPCHECK(hipEventRecord(ev[0], s));

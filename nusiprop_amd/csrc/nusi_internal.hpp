@@ -53,14 +53,14 @@ void alpha_tiles_destroy(AlphaTilesDev* t);
 
 // ref: NUSI_OPT_REFERENCE_ORDER (the kernels' kRef instances: the reference's own operation order for the complex
 // dilogarithms and the s-t interference member leaves, bit-identical to the oracle's ora_set_reference_order(1))
-hipError_t launch_gamma_alphat(const GridDev& g, const Point* pts, int npts, const SplineSet& spl, TablesDev t,
+hipError_t launch_gamma_alphat(const GridDev& g, const Point* pts, int npts, const SplineSet* spl, TablesDev t,
                                int* warn, hipStream_t s, bool ref);
 // batches: device [nbatches] of first table | count << 24 (count <= gmax), tables of a batch sharing
 // m_phi, the masses and the channel flags (nullptr: every table alone).  kernel = NUSI_OPT_ALPHA_KERNEL:
 // 0 -- core tiles on the big-batch kernel k_alpha_batch (any count < 256; the first nb_plain batches without
 // the phi-phi channel, the rest with it); 1 -- k_alpha_tile<G> batches (count <= 4); 2 -- one entry per
 // work-item (k_alpha)
-hipError_t launch_alpha(const GridDev& g, const Point* pts, int npts, const SplineSet& spl, const AlphaTilesDev& tiles,
+hipError_t launch_alpha(const GridDev& g, const Point* pts, int npts, const SplineSet* spl, const AlphaTilesDev& tiles,
                         TablesDev t, int* warn, hipStream_t s, const int* batches, int nbatches, int gmax,
                         int kernel, int nb_plain, bool ref);
 // NUSI_OPT_SHIFT_REUSE: tables s0 .. s0 + nshift - 1 of t (grid g) <- base tables map[q].x of tb (grid gb, the

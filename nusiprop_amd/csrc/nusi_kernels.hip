@@ -34,10 +34,11 @@ __device__ __attribute__((noinline)) void warn_entry(int* warn, int* wmin, int T
 #endif
 // kRef: NUSI_OPT_REFERENCE_ORDER (the general complex dilogarithm, gamma_entry / alphat_entry)
 template <bool kRef>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NUSI_GA_WAVES, NUSI_GA_WAVES))) void k_gamma_alphat(GridDev g, const Point* __restrict__ pts, SplineSet spl,
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NUSI_GA_WAVES, NUSI_GA_WAVES))) void k_gamma_alphat(GridDev g, const Point* __restrict__ pts, const SplineSet* __restrict__ splp,
                                                      double* __restrict__ G, double* __restrict__ At,
                                                      int* __restrict__ warn, int* __restrict__ wmin)
 {
+    const SplineSet& spl = *splp;   // (in global memory: a by-value copy would live in scratch)
     const int p = blockIdx.y;
     const int n = blockIdx.x * 64 + threadIdx.x;
     if (n >= g.T) return;
@@ -85,9 +86,10 @@ hipError_t spline_windows_build(const float* f, int n0, int n1, int n2, float* f
 #endif
 template <bool kRef>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NUSI_PE_WAVES, NUSI_PE_WAVES)))
-void k_alpha(GridDev g, const Point* __restrict__ pts, SplineSet spl, int nlo,
+void k_alpha(GridDev g, const Point* __restrict__ pts, const SplineSet* __restrict__ splp, int nlo,
                                                double* __restrict__ A, int* __restrict__ warn, int* __restrict__ wmin)
 {
+    const SplineSet& spl = *splp;
     const int p = blockIdx.y;
     const long long L = g.T - nlo;
     const long long e = (long long)blockIdx.x * 256 + threadIdx.x;
@@ -108,7 +110,7 @@ void k_alpha(GridDev g, const Point* __restrict__ pts, SplineSet spl, int nlo,
     if (w) warn_entry(warn, wmin, g.T, p, w, n, m);
 }
 
-hipError_t launch_gamma_alphat(const GridDev& g, const Point* pts, int npts, const SplineSet& spl, TablesDev t,
+hipError_t launch_gamma_alphat(const GridDev& g, const Point* pts, int npts, const SplineSet* spl, TablesDev t,
                                int* warn, hipStream_t s, bool ref)
 {
     dim3 grid((g.T + 63) / 64, npts, 2);
@@ -151,13 +153,14 @@ __host__ __device__ constexpr int alpha_tile_lds_doubles(int cs, int ct, int G)
 // gr = Gamma_phi / m_phi once per point.  batches[y] = first table | count << 24 (nullptr: table y alone).
 template <int G, bool kRef>   // batch capacity (compile time, so that G = 1 keeps its sum in a register);
                               // kRef: NUSI_OPT_REFERENCE_ORDER member corners
-__global__ __launch_bounds__(kTileThreads) NUSI_TILE_ATTR void k_alpha_tile(GridDev g, const Point* __restrict__ pts, SplineSet spl,
+__global__ __launch_bounds__(kTileThreads) NUSI_TILE_ATTR void k_alpha_tile(GridDev g, const Point* __restrict__ pts, const SplineSet* __restrict__ splp,
                                                            const int* __restrict__ tiles, int cs_max, int ct_max,
                                                            const int* __restrict__ batches,
                                                            double* __restrict__ A, int* __restrict__ warn,
                                                            int* __restrict__ wmin)
 {
     extern __shared__ __attribute__((aligned(16))) double sm[];
+    const SplineSet& spl = *splp;
     __shared__ double tE[2 * kAlphaTile], sE[2 * kAlphaTile];
     __shared__ int tl[kAlphaTile], th[kAlphaTile], sl[kAlphaTile], sh[kAlphaTile];
     __shared__ int cnt[2];
@@ -348,11 +351,12 @@ __global__ __launch_bounds__(256) void k_alpha_medge(GridDev g, const Point* __r
 // block, which then holds no Taylor coefficients), the rest of the batch structure unchanged
 template <bool kPP, bool kRef>
 __global__ __launch_bounds__(kTileThreads) __attribute__((amdgpu_waves_per_eu(NUSI_BATCH_WAVES, NUSI_BATCH_WAVES)))
-void k_alpha_batch(GridDev g, const Point* __restrict__ pts, SplineSet spl, const int* __restrict__ tiles,
+void k_alpha_batch(GridDev g, const Point* __restrict__ pts, const SplineSet* __restrict__ splp, const int* __restrict__ tiles,
                    const int* __restrict__ batches, double* __restrict__ A, const double* __restrict__ med,
                    int* __restrict__ warn, int* __restrict__ wmin)
 {
     extern __shared__ __attribute__((aligned(16))) double sm[];
+    const SplineSet& spl = *splp;
     __shared__ double tE[2 * kAlphaTile], sE[2 * kAlphaTile];
     __shared__ int tl[kAlphaTile], th[kAlphaTile], sl[kAlphaTile], sh[kAlphaTile];
     __shared__ int cnt[2];
@@ -612,7 +616,7 @@ static thread_local const char* t_alpha_kernel = "";   // the main kernel of the
 const char* last_alpha_kernel() { return t_alpha_kernel; }
 
 template <bool kRef>
-static hipError_t launch_alpha_t(const GridDev& g, const Point* pts, int npts, const SplineSet& spl,
+static hipError_t launch_alpha_t(const GridDev& g, const Point* pts, int npts, const SplineSet* spl,
                                  const AlphaTilesDev& at, TablesDev t, int* warn, hipStream_t s, const int* batches,
                                  int nbatches, int gmax, int kernel, int nb_plain)
 {
@@ -694,7 +698,7 @@ static hipError_t launch_alpha_t(const GridDev& g, const Point* pts, int npts, c
     return hipGetLastError();
 }
 
-hipError_t launch_alpha(const GridDev& g, const Point* pts, int npts, const SplineSet& spl, const AlphaTilesDev& at,
+hipError_t launch_alpha(const GridDev& g, const Point* pts, int npts, const SplineSet* spl, const AlphaTilesDev& at,
                         TablesDev t, int* warn, hipStream_t s, const int* batches, int nbatches, int gmax,
                         int kernel, int nb_plain, bool ref)
 {
