@@ -9,6 +9,7 @@
 #                           the summaries are copied to profiles/pmc_traffic_<wl>.json
 #   bench[=<a>,<b>,..]      python bench.py <a> <b> ..  (commas = spaces)           -> bench_<i>.json / .err
 #   prof=<a>,<b>,..         rocprofv3 --kernel-trace --stats of bench.py <a> <b> .. -> kt_<i>/
+#   py=<script>,<a>,..      python <script> <a> ..                                   -> py_<i>.out / .err
 set -o pipefail
 TAG=${1:?tag}
 shift
@@ -39,6 +40,8 @@ for STEP in "$@"; do
     prof)
       timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/kt_$i -o kt --output-format csv -- python3 bench.py $ARGS \
         > $OUT/kt_$i.log 2>&1 || exit 1 ;;
+    py)
+      timeout -k 10 600 python $ARGS > $OUT/py_$i.out 2> $OUT/py_$i.err || exit 1 ;;
     *)
       echo "unknown step $STEP" >> $OUT/session.log; exit 2 ;;
   esac
