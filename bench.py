@@ -71,6 +71,9 @@ def parse():
                          "dilogarithms (bit-exact to the oracle's reference-order mode); default: the shared-algorithm "
                          "order (bit-exact to the oracle's default mode)")
     ap.add_argument("--no-parity", action="store_true", help="skip the parity object (oracle fluxes of a sample)")
+    ap.add_argument("--sync", default="auto", choices=["auto", "stage", "block"],
+                    help="NUSI_OPT_CASCADE_SYNC: the MFMA cascade's per-stage kernels (stage) or the block-synchronous "
+                         "k_cascade_bs (block); auto = the library default")
     ap.add_argument("--dry-run", action="store_true",
                     help="launch / rank / reduction plumbing only, no GPU work (gloo; CPU tests): prints the JSON "
                          "line with value null")
@@ -485,6 +488,8 @@ def run(args, world, rank, local, dist, plan, pts, desc, pp_tables):
         plan.set_option(_lib.OPT_CASCADE_RHS, args.rhs)
     if args.reference_order:
         plan.set_option(_lib.OPT_REFERENCE_ORDER, 1)
+    if args.sync != "auto":
+        plan.set_option(_lib.OPT_CASCADE_SYNC, {"stage": 1, "block": 2}[args.sync])
     order = "reference" if args.reference_order else "shared-algorithm"
     dev = torch.device("cuda", local)
     flux = torch.empty((P, 3, plan.N), dtype=torch.float64, device=dev)

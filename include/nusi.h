@@ -216,6 +216,13 @@ int nusi_plan_set_cascade(nusi_plan *plan, int kind);
  *                          matching mode; they differ from each other where
  *                          the closed forms cancel. */
 #define NUSI_OPT_REFERENCE_ORDER 6
+/*   NUSI_OPT_CASCADE_SYNC  the MFMA cascade's synchronisation: 0 = automatic,
+ *                          1 = the per-stage kernels (k_cascade_ws / gb /
+ *                          wsp: every wave meets once per wavefront stage),
+ *                          2 = the block-synchronous kernel k_cascade_bs
+ *                          (twice per block of four stages; the same
+ *                          operations on the same operands). */
+#define NUSI_OPT_CASCADE_SYNC 7
 int nusi_plan_set_option(nusi_plan *plan, int option, int value);
 /* per-point NUSI_WARN_* bits of the last call */
 int nusi_plan_warnings(nusi_plan *plan, int *out, int n);

@@ -430,6 +430,8 @@ struct nusi_plan {
     int step_passes = 0;            // NUSI_OPT_STEP_PASSES: 1 = the step-pass cascade also where one pass fits
     int shift_max = 0;              // NUSI_OPT_SHIFT_REUSE: K, the largest bin offset served by a base table set
     int ref_order = 0;              // NUSI_OPT_REFERENCE_ORDER: 1 = the tables in the reference's operation order
+    int cascade_sync = 0;           // NUSI_OPT_CASCADE_SYNC: 0 = auto, 1 = per-stage kernels, 2 = block-synchronous
+    size_t fh_doubles = 0;          // capacity of d_fh in doubles (the block-synchronous kernels' FIFOs)
     nusi_plan* shift = nullptr;     // ... its plan: the same grid with K more redshift steps (axis T + K)
     int2* d_smap = nullptr;         // per shifted table: base index in `shift`, bin offset
     int2* h_smap = nullptr;         // pinned
@@ -601,17 +603,23 @@ int shift_groups(nusi_plan* pl, int ntab, std::vector<int>& remap, std::vector<i
         return std::make_tuple(P.g, P.mn[0], P.mn[1], P.mn[2], P.u[0], P.u[1], P.u[2], P.majorana, P.non_resonant,
                                P.phiphi);
     };
-    std::vector<int> idx(ntab);
-    for (int j = 0; j < ntab; ++j) idx[j] = j;
+    // only couplings up to kShiftReuseGMax share: the shifted tables differ from a point's own by rounding, and at
+    // strong coupling the flux's optical depth amplifies that (c4s lattice, scripts/dev_shift_reuse_errors.py on the
+    // GPU: <= 6.4e-10 for g <= 0.135, 9.8e-10 at 0.168, 3e-8 at g = 1; the north star bounds fluxes at 1e-9)
+    constexpr double kShiftReuseGMax = 0.15;
+    std::vector<int> idx;
+    for (int j = 0; j < ntab; ++j)
+        if (tp[j].g <= kShiftReuseGMax) idx.push_back(j);
+    const int nsh = (int)idx.size();
     std::stable_sort(idx.begin(), idx.end(), [&](int a, int b) {
         const auto ka = gkey(a), kb = gkey(b);
         return ka != kb ? ka < kb : tp[a].mphi > tp[b].mphi;
     });
     std::vector<int> grp(ntab, -1), off(ntab, 0);
     std::vector<std::vector<int>> members;
-    for (int a = 0; a < ntab;) {
+    for (int a = 0; a < nsh;) {
         int b = a + 1;
-        while (b < ntab && gkey(idx[b]) == gkey(idx[a])) ++b;
+        while (b < nsh && gkey(idx[b]) == gkey(idx[a])) ++b;
         std::vector<int> cur{idx[a]};
         int last = 0;
         for (int c = a + 1; c <= b; ++c) {
@@ -1007,7 +1015,54 @@ int nusi_plan_evolve(nusi_plan* pl, const nusi_params* pts, int n, double* d_flu
     int ngb = 0, ngidx = 0;
     std::vector<char> in_gb;
     const int gbmax = pl->cascade_rhs == 0 ? 16 : pl->cascade_rhs;   // auto: the gamma batch (C5 cascade 4.54 -> 4.13 ms)
-    if (pairs_fit && gbmax >= 3 && nusi::cascade_gb_fits(pl->gd)) {
+    // the block-synchronous MFMA cascade (k_cascade_bs; NUSI_OPT_CASCADE_SYNC): the points of a table slot in
+    // workgroups of up to 16 (>= 3 points: the gamma batch), pairs, or one per workgroup (NUSI_OPT_CASCADE_RHS caps
+    // the group size), any source and scattering mode, step passes on long grids
+    const bool bs = kind == NUSI_CASCADE_MFMA && pl->cascade_sync == 2 && nusi::cascade_bs_config(pl->gd, 1) != 0;
+    int bs_nwg[3] = {0, 0, 0};   // workgroups of P = 16, 2, 1 (their groups in h_gbgrp in that order)
+    if (bs) {
+        if (!pl->d_gidx) {
+            HIPCHECK(hipMalloc(&pl->d_gidx, sizeof(int) * pl->max_points));
+            HIPCHECK(hipMalloc(&pl->d_gbgrp, sizeof(int2) * pl->max_points));
+            HIPCHECK(hipHostMalloc((void**)&pl->h_gidx, sizeof(int) * pl->max_points, hipHostMallocDefault));
+            HIPCHECK(hipHostMalloc((void**)&pl->h_gbgrp, sizeof(int2) * pl->max_points, hipHostMallocDefault));
+        }
+        const int rmax = pl->cascade_rhs == 0 ? 16 : pl->cascade_rhs;
+        const bool g16 = rmax >= 3 && nusi::cascade_bs_config(pl->gd, 16) != 0;
+        const bool g2 = rmax >= 2 && nusi::cascade_bs_config(pl->gd, 2) != 0;
+        std::vector<std::vector<int>> by(ntab);
+        for (int i = 0; i < n; ++i) by[pl->h_pts[i].tslot].push_back(i);
+        std::vector<std::vector<int>> grs[3];   // groups for P = 16, 2, 1
+        for (int j = 0; j < ntab; ++j) {
+            const int c = (int)by[j].size();
+            const int cap = (g16 && c >= 3) ? std::min(rmax, 16) : (g2 && c >= 2) ? 2 : 1;
+            const int nb = (c + cap - 1) / cap;   // near-equal groups
+            for (int k = 0; k < nb; ++k) {
+                const int lo = (int)((long long)c * k / nb), hi = (int)((long long)c * (k + 1) / nb);
+                const int sz = hi - lo, w = sz >= 3 ? 0 : sz == 2 ? 1 : 2;
+                grs[w].emplace_back(by[j].begin() + lo, by[j].begin() + hi);
+            }
+        }
+        size_t fhd = 0;
+        const int Pk[3] = {16, 2, 1};
+        for (int w = 0; w < 3; ++w) {
+            for (const auto& gp : grs[w]) {
+                pl->h_gbgrp[ngb++] = make_int2(ngidx, (int)gp.size());
+                for (int i : gp) pl->h_gidx[ngidx++] = i;
+            }
+            bs_nwg[w] = (int)grs[w].size();
+            fhd += nusi::cascade_bs_scratch_doubles(pl->gd, Pk[w]) * grs[w].size();
+        }
+        if (fhd > pl->fh_doubles) {
+            hipFree(pl->d_fh);
+            pl->d_fh = nullptr;
+            pl->fh_cap = 0;
+            pl->fh_doubles = 0;
+            HIPCHECK(hipMalloc(&pl->d_fh, sizeof(double) * fhd));
+            pl->fh_doubles = fhd;
+        }
+    }
+    if (!bs && pairs_fit && gbmax >= 3 && nusi::cascade_gb_fits(pl->gd)) {
         if (!pl->d_gidx) {
             HIPCHECK(hipMalloc(&pl->d_gidx, sizeof(int) * pl->max_points));
             HIPCHECK(hipMalloc(&pl->d_gbgrp, sizeof(int2) * pl->max_points));
@@ -1035,12 +1090,14 @@ int nusi_plan_evolve(nusi_plan* pl, const nusi_params* pts, int n, double* d_flu
             hipFree(pl->d_fh);
             pl->d_fh = nullptr;
             pl->fh_cap = 0;
+            pl->fh_doubles = 0;
             HIPCHECK(hipMalloc(&pl->d_fh, sizeof(double) * nusi::cascade_gb_scratch_doubles(pl->gd) * ngb));
             pl->fh_cap = ngb;
+            pl->fh_doubles = nusi::cascade_gb_scratch_doubles(pl->gd) * ngb;
         }
     }
     int ngroups = 0;
-    if (pairs_fit && (pl->cascade_rhs != 1 || ngb)) {
+    if (!bs && pairs_fit && (pl->cascade_rhs != 1 || ngb)) {
         std::vector<int> open(ntab, -1);   // per table slot: a point waiting for its partner
         for (int i = 0; i < n; ++i) {
             if (ngb && in_gb[i]) continue;
@@ -1053,7 +1110,7 @@ int nusi_plan_evolve(nusi_plan* pl, const nusi_params* pts, int n, double* d_flu
             if (open[j] >= 0) pl->h_groups[ngroups++] = make_int2(open[j], -1);
         if (!ngb && 4 * ngroups > 3 * n) ngroups = 0;   // too few pairs: one point per workgroup
     }
-    if (fast && any_dsnb && pl->src_cap < pl->max_points) {
+    if ((fast || bs) && any_dsnb && pl->src_cap < pl->max_points) {
         hipFree(pl->d_src);
         pl->d_src = nullptr;
         pl->src_cap = 0;
@@ -1100,23 +1157,42 @@ int nusi_plan_evolve(nusi_plan* pl, const nusi_params* pts, int n, double* d_flu
         HIPCHECK(nusi::launch_table_shift(pl->gd, sp->gd, pl->d_smap, nd, ntab - nd, sp->tabs, pl->tabs, pl->d_warn, s));
     }
     HIPCHECK(hipEventRecord(ev[2], s));
-    if (fast && any_dsnb) HIPCHECK(nusi::launch_source_dsnb(pl->gd, pl->d_pts, n, pl->d_src, s));
+    if ((fast || bs) && any_dsnb) HIPCHECK(nusi::launch_source_dsnb(pl->gd, pl->d_pts, n, pl->d_src, s));
     const char* gb_name = nullptr;
-    if (ngb) {
-        HIPCHECK(nusi::launch_cascade_gb(pl->gd, pl->d_pts, pl->d_gidx, pl->d_gbgrp, ngb, pl->tabs, pl->d_fh, d_flux,
-                                         d_fla, s));
-        gb_name = ngroups ? "k_cascade_gb + k_cascade_ws_mrhs" : "k_cascade_gb";
+    if (bs) {
+        const int Pk[3] = {16, 2, 1};
+        static const char* const names[8] = {"", "k_cascade_bs_gamma", "k_cascade_bs_pairs", "k_cascade_bs_gamma + pairs",
+                                             "k_cascade_bs", "k_cascade_bs_gamma + k_cascade_bs",
+                                             "k_cascade_bs_pairs + k_cascade_bs", "k_cascade_bs_gamma + pairs + k_cascade_bs"};
+        int off = 0, mask = 0;
+        double* fh = pl->d_fh;
+        for (int w = 0; w < 3; ++w) {
+            if (bs_nwg[w]) {
+                HIPCHECK(nusi::launch_cascade_bs(pl->gd, pl->d_pts, Pk[w], pl->d_gidx, pl->d_gbgrp + off, bs_nwg[w], pl->tabs,
+                                                 fh, d_flux, d_fla, s));
+                mask |= 1 << w;
+            }
+            fh += nusi::cascade_bs_scratch_doubles(pl->gd, Pk[w]) * bs_nwg[w];
+            off += bs_nwg[w];
+        }
+        gb_name = names[mask];
+    } else {
+        if (ngb) {
+            HIPCHECK(nusi::launch_cascade_gb(pl->gd, pl->d_pts, pl->d_gidx, pl->d_gbgrp, ngb, pl->tabs, pl->d_fh, d_flux,
+                                             d_fla, s));
+            gb_name = ngroups ? "k_cascade_gb + k_cascade_ws_mrhs" : "k_cascade_gb";
+        }
+        if (fast && ngroups)
+            HIPCHECK(nusi::launch_cascade_ws(pl->gd, pl->d_pts, 2, pl->d_groups, ngroups, pl->tabs, d_flux, d_fla, s));
+        else if (ngb) {
+        } else if (fast && one_pass)
+            HIPCHECK(nusi::launch_cascade_ws(pl->gd, pl->d_pts, 1, nullptr, n, pl->tabs, d_flux, d_fla, s));
+        else if (fast)
+            HIPCHECK(nusi::launch_cascade_wsp(pl->gd, pl->d_pts, n, pl->tabs, d_flux, d_fla, s, all_nr));
+        else
+            HIPCHECK(nusi::launch_cascade_exact(pl->gd, pl->d_pts, n, pl->tabs, d_flux, d_fla, s,
+                                                kind == NUSI_CASCADE_MFMA ? NUSI_CASCADE_WAVEFRONT : kind, all_pl));
     }
-    if (fast && ngroups)
-        HIPCHECK(nusi::launch_cascade_ws(pl->gd, pl->d_pts, 2, pl->d_groups, ngroups, pl->tabs, d_flux, d_fla, s));
-    else if (ngb) {
-    } else if (fast && one_pass)
-        HIPCHECK(nusi::launch_cascade_ws(pl->gd, pl->d_pts, 1, nullptr, n, pl->tabs, d_flux, d_fla, s));
-    else if (fast)
-        HIPCHECK(nusi::launch_cascade_wsp(pl->gd, pl->d_pts, n, pl->tabs, d_flux, d_fla, s, all_nr));
-    else
-        HIPCHECK(nusi::launch_cascade_exact(pl->gd, pl->d_pts, n, pl->tabs, d_flux, d_fla, s,
-                                            kind == NUSI_CASCADE_MFMA ? NUSI_CASCADE_WAVEFRONT : kind, all_pl));
     HIPCHECK(hipEventRecord(ev[3], s));
     HIPCHECK(hipEventRecord(pl->ev_done, s));
     pl->alpha_kernel = nusi::last_alpha_kernel();
@@ -1201,6 +1277,10 @@ int nusi_plan_set_option(nusi_plan* pl, int option, int value)
     case NUSI_OPT_STEP_PASSES:
         if (value < 0 || value > 1) return fail(NUSI_EPARAM, "NUSI_OPT_STEP_PASSES outside [0, 1]");
         pl->step_passes = value;
+        return NUSI_OK;
+    case NUSI_OPT_CASCADE_SYNC:
+        if (value < 0 || value > 2) return fail(NUSI_EPARAM, "NUSI_OPT_CASCADE_SYNC outside [0, 2]");
+        pl->cascade_sync = value;
         return NUSI_OK;
     case NUSI_OPT_REFERENCE_ORDER:
         if (value < 0 || value > 1) return fail(NUSI_EPARAM, "NUSI_OPT_REFERENCE_ORDER outside [0, 1]");

@@ -1875,6 +1875,363 @@ void k_cascade_gb(GridDev g, const Point* __restrict__ pts, const int* __restric
         }
     }
 }
+// ---------------------------------------------------------------------------
+// k_cascade_bs: the MFMA cascade with block-synchronous roles (round 4).  The wavefront, the rank-4 block
+// pushes on v_mfma_f64_16x16x4f64, the records and the solves are k_cascade_ws / k_cascade_gb's operations on
+// the same operands; what changes is when the waves meet.  k_cascade_ws / gb / wsp synchronise every wave of
+// the workgroup once per STAGE, so a stage costs a barrier, an LDS round trip of the chain's records and its
+// dependent solve (~2 000 cycles against a ~700-cycle floor).  The data dependencies only
+// need a meeting point twice per BLOCK of four stages:
+//   * block q's push (columns of stages 4q-4 .. 4q-1) needs the chain's T_j of those stages;
+//   * the chain's stages 4q+1 .. 4q+4 need the rows block q publishes; stage 4q needs block q-1's.
+// So every block runs in two phases between two barriers:
+//   phase A: the waves holding the four rows block q publishes push block q into those tiles and publish
+//            them (AX); the chain solves stage 4q (block q-1's rows);
+//   phase B: the chain solves stages 4q+1 .. 4q+3 back to back (block q's rows, its own four diagonal
+//            columns as before); the other push tiles add block q (their rows are published later); the
+//            record wave forms the records and sources of block q + 1 (4 stages x NJ steps at once).
+// The chain is ONE wave: lane (point p, jp) runs the step slots j = SPL jp .. SPL jp + SPL - 1 (interleaved,
+// independent solves); slot j takes F[:, b] from slot j-1's solve of the previous stage -- the lane's own
+// previous slot in a register, or, for its first slot, the previous lane's last slot by a DPP wave shift, or
+// (first step of a pass > 0) the previous pass' last step through a global FIFO prefetched a block ahead.
+// The A operands of block q + 2 are loaded while block q is pushed (two register buffers, the block loop
+// unrolled by two), so the publishing tiles never wait for HBM.
+// Columns: the NC = NJ P right-hand sides (point p, step j) at c = j P + p; a push tile is 16 columns (one
+// step of 16 points, or 16 steps of one point), so one template covers
+//   <48, 1, 1, 4>  one point per workgroup (C4; k_cascade_ws<48, 1>'s shape)
+//   <48, 2, 2, 2>  two points sharing a table (k_cascade_ws<48, 2>)
+//   <6, 16, 2, 2>  the gamma batch, 16 power-law points of a table (k_cascade_gb)
+//   <16, 1, 1, 8>  step passes on long grids (C3; k_cascade_wsp)
+// and the same points get the same fluxes as from those kernels (the MFMA sums each element's four columns in
+// its own order whichever column it is).  Waves: push waves of 16 RT rows, the chain wave, the record wave.
+// ---------------------------------------------------------------------------
+template <int NJ, int P, int SPL, int RT>
+struct BsCfg {
+    static constexpr int LPP = NJ / SPL;   // chain lanes per point
+    static constexpr int NC = NJ * P;      // right-hand columns
+    static constexpr int NB = NC / 16;     // push column tiles
+    static_assert(NJ % SPL == 0 && NC % 16 == 0 && LPP * P <= 64, "one chain wave, whole column tiles");
+};
+
+template <int NJ, int P, int SPL, int RT>
+__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4, 4)))
+void k_cascade_bs(GridDev g, const Point* __restrict__ pts, const int* __restrict__ gidx, const int2* __restrict__ grp,
+                  TablesDev t, double* __restrict__ fh, double* __restrict__ flux, double* __restrict__ flux_fla)
+{
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    using Cfg = BsCfg<NJ, P, SPL, RT>;
+    constexpr int LPP = Cfg::LPP, NC = Cfg::NC, NB = Cfg::NB, NF = kWfFields, S4 = 4 * NJ;
+    const int N = g.N, Nz = g.Nz, T = g.T, nst = Nz - 1;
+    const int tid = threadIdx.x, nthr = blockDim.x, lane = tid & 63, wave = tid >> 6, nw = nthr >> 6;
+    const int nwp = nw - 2, chw = nw - 2, recw = nw - 1;   // push waves, the chain wave, the record wave
+    const int2 gr = grp ? grp[blockIdx.x] : make_int2((int)blockIdx.x, 1);
+    const int R = gr.y;                                   // points of this workgroup (<= P), one table
+    auto pidx = [&](int p) { return gidx ? gidx[gr.x + p] : gr.x + p; };   // (gidx == nullptr: point blockIdx.x)
+    const Point& P0 = pts[pidx(0)];
+    double* rec = lds;                       // [2][NF][4][NJ]  records of block q in slot q & 1
+    double* srcb = rec + 2 * NF * S4;        // [2][4][NJ][P]   the sources c_i Lum of block q's (stage, step, point)
+    double* Tp = srcb + 8 * NC;              // [8][NC]         T_j of each column by stage
+    double* AX = Tp + 8 * NC;                // [2][4][NC]      rows published by block q (parity q & 1)
+    double* rdE = AX + 8 * NC;               // [N]
+    double* pw = rdE + N;                    // [P][T + 2]      each power-law point's pw on table edge e
+    double* sGt = pw + (size_t)P * (T + 2);
+    double* sAt = sGt + T;
+    double* sdg = sAt + T;                   // [4][T]: alpha(n, n+k), k = 1..4 (0 past the table)
+    double* sEmin = sdg + 4 * T;
+    double* sEmax = sEmin + N;
+    double* sgz = sEmax + N;                 // z, step_c, step_s, sfr [Nz each]
+    GridDev gl = g;
+    gl.Emin = sEmin;
+    gl.Emax = sEmax;
+    gl.z = sgz;
+    gl.step_c = sgz + Nz;
+    gl.step_s = sgz + 2 * Nz;
+    gl.sfr = sgz + 3 * Nz;
+    const double* __restrict__ Al = t.A + (size_t)P0.tslot * g.PT;
+    {
+        const double* __restrict__ Gt = t.G + (size_t)P0.tslot * T;
+        const double* __restrict__ At = t.At + (size_t)P0.tslot * T;
+        for (int n = tid; n < T; n += nthr) {
+            sGt[n] = Gt[n];
+            sAt[n] = At[n];
+#pragma unroll
+            for (int k = 1; k <= 4; ++k) sdg[(k - 1) * T + n] = (n + k < T) ? Al[(size_t)(n + k) * (n + k - 1) / 2 + n] : 0.0;
+        }
+        for (int b = tid; b < N; b += nthr) {
+            sEmin[b] = g.Emin[b];
+            sEmax[b] = g.Emax[b];
+            rdE[b] = 1.0 / (g.Emax[b] - g.Emin[b]);   // cascade_aux_init's expression
+        }
+        for (int i = tid; i < Nz; i += nthr) {
+            sgz[i] = g.z[i];
+            sgz[Nz + i] = g.step_c[i];
+            sgz[2 * Nz + i] = g.step_s[i];
+            sgz[3 * Nz + i] = g.sfr[i];
+        }
+        for (int q = tid; q < P * (T + 1); q += nthr) {   // cascade_aux_init's pw[e] of every power-law point
+            const int p = q / (T + 1), e = 1 + q - p * (T + 1);
+            if (p >= R) continue;
+            const Point& Q = pts[pidx(p)];
+            if (Q.source != NUSI_SOURCE_POWER_LAW) continue;
+            const int i = min(Nz - 1, max(1, e - N + 1)), b = e - i;
+            const double E = (b < N) ? g.Emin[b] : g.Emax[N - 1];
+            pw[(size_t)p * (T + 2) + e] = nm::pow(E / 1e14 * (1 + g.z[i]), -Q.si);
+        }
+    }
+    const bool nonres = P0.non_resonant;   // the points of a workgroup share a table, hence the flags
+    const int npass = (nst + NJ - 1) / NJ;
+    double* const fhw = fh + (size_t)blockIdx.x * 3 * N * P;   // this workgroup's F FIFO [3][N][P] (passes > 1)
+    int jb = 0, njp = 0, Ts = 0, c0 = 0, nblk = 0;
+    auto pass_geom = [&](int pass) {
+        jb = pass * NJ;
+        njp = nst - jb < NJ ? nst - jb : NJ;   // steps of this pass
+        Ts = N - 1 + njp;                      // its stages
+        c0 = T - 1 - jb;                       // the table column of its stage 0
+        nblk = (Ts + 3) / 4;
+    };
+    // the records of block qb (its 4 stages x NJ steps) and the sources of its (stage, step, point), slot qb & 1
+    auto records = [&](int qb) {
+        for (int e = lane; e < S4; e += 64) {
+            const int sb = e / NJ, jj = e - NJ * (e / NJ), s2 = 4 * qb + sb;
+            const int b = N - 1 - s2 + jj, i = Nz - 1 - jb - jj;
+            if (jj < njp && s2 < Ts && b >= 0 && b < N) {
+                double* Rw = rec + (size_t)(qb & 1) * NF * S4 + e;
+                const RecM m = record_phase1(gl, P0, sGt, sAt, rdE, i, b);
+                Rw[PR_RZ0 * S4] = m.rz0;
+                Rw[PR_RZ1 * S4] = m.rz1;
+                Rw[PR_RZ2 * S4] = m.rz2;
+                Rw[PR_SDE * S4] = nonres ? gl.step_s[i] * rdE[b] : (gl.Emax[b] - gl.Emin[b]);
+                record_phase2<true>(m, Rw, S4);
+            }
+        }
+        for (int e = lane; e < S4 * P; e += 64) {
+            const int p = e % P, sj = e / P, sb = sj / NJ, jj = sj - NJ * sb, s2 = 4 * qb + sb;
+            const int b = N - 1 - s2 + jj, i = Nz - 1 - jb - jj;
+            if (p < R && jj < njp && s2 < Ts && b >= 0 && b < N) {
+                const int pid = pidx(p);
+                const Point& Q = pts[pid];
+                srcb[(qb & 1) * 4 * NC + e] =
+                    Q.source == NUSI_SOURCE_POWER_LAW ? powerlaw_src_h(gl, src_factors(Q), pw + (size_t)p * (T + 2), i, b)
+                                                      : t.Src[(size_t)pid * T * nst + src_index(Nz, jb + jj, b)];
+            }
+        }
+    };
+    if (wave == chw) {
+        // ---- chain: lane (cp, cjp) solves the slots j = SPL cjp + k of point cp
+        const int cp = lane / LPP, cjp = lane - LPP * (lane / LPP);
+        const bool clane = lane < P * LPP && cp < R;
+        const int cpid = clane ? pidx(cp) : 0;
+        const double u0 = P0.u[0], u1 = P0.u[1], u2 = P0.u[2];
+#pragma unroll 1
+        for (int pass = 0; pass < npass; ++pass) {
+            pass_geom(pass);
+            const bool last_pass = pass == npass - 1;
+            __syncthreads();   // the previous pass is done with Tp, AX and the records
+            for (int q = lane; q < 16 * NC; q += 64) Tp[q] = 0.0;   // Tp and AX
+            __syncthreads();
+            double cj[SPL], sj[SPL], px0[SPL], px1[SPL], px2[SPL], racc[SPL], Th[SPL][4];
+#pragma unroll
+            for (int k = 0; k < SPL; ++k) {
+                const int j = SPL * cjp + k, i = Nz - 1 - jb - j;
+                const bool act = clane && j < njp;
+                cj[k] = act ? gl.step_c[i] : 0.0;
+                sj[k] = act ? gl.step_s[i] : 0.0;
+                px0[k] = px1[k] = px2[k] = racc[k] = 0.0;
+#pragma unroll
+                for (int d = 0; d < 4; ++d) Th[k][d] = 0.0;
+            }
+            // the first step of a pass > 0 starts from the previous pass' last step: F[:, b] from the FIFO, a block ahead
+            const bool ffifo = pass > 0 && cjp == 0 && clane;
+            double fq[4][3];
+            auto fifo_load = [&](int sg, double (&f)[3]) {
+                const int bq = N - 1 - sg;
+                if (ffifo && sg < Ts && bq >= 0) {
+#pragma unroll
+                    for (int c = 0; c < 3; ++c) f[c] = __builtin_nontemporal_load(fhw + ((size_t)c * N + bq) * P + cp);
+                }
+            };
+#pragma unroll
+            for (int d = 0; d < 4; ++d) {
+                fq[d][0] = fq[d][1] = fq[d][2] = 0.0;
+                fifo_load(d, fq[d]);
+            }
+            // stage sg = 4 q + d of the pass
+            auto stage = [&](int q, int d) {
+                const int sg = 4 * q + d;
+                const int r = c0 - sg;
+                double f0[SPL], f1[SPL], f2[SPL];
+                f0[0] = wave_shr1(px0[SPL - 1], 0.0);   // every lane active: the previous lane's last slot
+                f1[0] = wave_shr1(px1[SPL - 1], 0.0);
+                f2[0] = wave_shr1(px2[SPL - 1], 0.0);
+                if (cjp == 0) {
+                    f0[0] = fq[d][0];
+                    f1[0] = fq[d][1];
+                    f2[0] = fq[d][2];
+                    fq[d][0] = fq[d][1] = fq[d][2] = 0.0;
+                    fifo_load(sg + 4, fq[d]);
+                }
+#pragma unroll
+                for (int k = 1; k < SPL; ++k) {
+                    f0[k] = px0[k - 1];
+                    f1[k] = px1[k - 1];
+                    f2[k] = px2[k - 1];
+                }
+                const double* Rb = rec + (size_t)(q & 1) * NF * S4 + d * NJ;
+                const double* Sb = srcb + (q & 1) * 4 * NC + d * NC;
+                const int qq = (sg - 1) >> 2;              // block whose publication serves stage sg
+                const int nu = (d == 0) ? 4 : d;           // columns r+1 .. r+nu not yet pushed
+                const double* Ab = AX + ((qq & 1) * 4 + (sg - 1 - 4 * qq)) * NC;
+#pragma unroll
+                for (int k = 0; k < SPL; ++k) {
+                    const int j = SPL * cjp + k;
+                    const int b = N - 1 - sg + j;
+                    double Tn = 0.0;
+                    if (clane && j < njp && b >= 0 && b < N) {
+                        const double* Rc = Rb + j;
+                        const double rz0 = Rc[PR_RZ0 * S4], rz1 = Rc[PR_RZ1 * S4], rz2 = Rc[PR_RZ2 * S4];
+                        const int pmb = (int)Rc[kPreFields * S4];
+                        const double l10 = Rc[PR_L10 * S4], l20 = Rc[PR_L20 * S4], l21 = Rc[PR_L21 * S4];
+                        const double u01 = Rc[PR_U01 * S4], u02 = Rc[PR_U02 * S4], u12 = Rc[PR_U12 * S4];
+                        const double ru00 = Rc[PR_RU00 * S4], ru11 = Rc[PR_RU11 * S4], ru22 = Rc[PR_RU22 * S4];
+                        const double sde = Rc[PR_SDE * S4];
+                        const double src = Sb[j * P + cp];
+                        double add;
+                        if (nonres) {
+                            double sa = Ab[j * P + cp];
+#pragma unroll
+                            for (int kk = 4; kk >= 1; --kk)
+                                if (kk <= nu) sa = fma(sdg[(kk - 1) * T + r], Th[k][kk - 1], sa);
+                            add = cj[k] * sa;
+                        } else {
+                            const double dEb1 = (b + 1 < N) ? sEmax[b + 1] - sEmin[b + 1] : 1.0;
+                            add = resonant_add(racc[k], u0, u1, u2, px0[k], px1[k], px2[k], sj[k], sdg[r], dEb1, sde,
+                                               cj[k], b == N - 1);
+                        }
+                        double x0, x1, x2;
+                        cascade_solve(f0[k], f1[k], f2[k], add, src, u0, u1, u2, rz0, rz1, rz2, pmb, l10, l20, l21, u01,
+                                      u02, u12, ru00, ru11, ru22, x0, x1, x2);
+                        if (j == njp - 1) {   // the pass's last step: the next pass' input, or the output
+                            if (last_pass) {   // finalise (nuSIprop.hpp:328-336)
+                                const Point& Q = pts[cpid];
+                                const double dE = gl.Emax[b] - gl.Emin[b];
+                                const double g0 = x0 / dE, g1 = x1 / dE, g2 = x2 / dE;
+                                double* fo = flux + (size_t)cpid * 3 * N;
+                                double* fl = flux_fla + (size_t)cpid * 3 * N;
+                                fo[b] = g0;
+                                fo[N + b] = g1;
+                                fo[2 * N + b] = g2;
+                                for (int f = 0; f < 3; ++f)
+                                    fl[f * N + b] = Q.U2[3 * f + 0] * g0 + Q.U2[3 * f + 1] * g1 + Q.U2[3 * f + 2] * g2;
+                            } else {
+                                fhw[((size_t)0 * N + b) * P + cp] = x0;
+                                fhw[((size_t)1 * N + b) * P + cp] = x1;
+                                fhw[((size_t)2 * N + b) * P + cp] = x2;
+                            }
+                        }
+                        px0[k] = x0; px1[k] = x1; px2[k] = x2;
+                        if (nonres && b > 0) Tn = (u0 * x0 + u1 * x1 + u2 * x2) * sde;
+                    }
+                    Th[k][3] = Th[k][2]; Th[k][2] = Th[k][1]; Th[k][1] = Th[k][0]; Th[k][0] = Tn;
+                    if (clane && j < njp) Tp[(sg & 7) * NC + j * P + cp] = Tn;
+                }
+            };
+#pragma unroll 1
+            for (int q = 0; q < nblk; ++q) {
+                if (4 * q < Ts) stage(q, 0);                        // phase A
+                __syncthreads();
+#pragma unroll
+                for (int d = 1; d < 4; ++d)
+                    if (4 * q + d < Ts) stage(q, d);                // phase B
+                __syncthreads();
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the FIFO stores land before the next pass reads
+        }
+    } else if (wave == recw) {
+        // ---- records: block 0 before the blocks, block q + 1 in phase B of block q (the chain reads block q's slot;
+        // block q + 1's slot was last read in phase B of block q - 1)
+#pragma unroll 1
+        for (int pass = 0; pass < npass; ++pass) {
+            pass_geom(pass);
+            __syncthreads();
+            records(0);
+            __syncthreads();
+#pragma unroll 1
+            for (int q = 0; q < nblk; ++q) {
+                __syncthreads();
+                if (4 * (q + 1) < Ts) records(q + 1);
+                __syncthreads();
+            }
+        }
+    } else {
+        // ---- push: block q adds columns c0+1-4q .. c0+4-4q (the T of stages 4q-1 .. 4q-4) into the rows below
+        // r = c0-4q: in phase A the tiles holding rows r-1 .. r-4 (published to AX), in phase B the others
+        const int rw0 = wave * 16 * RT;
+#pragma unroll 1
+        for (int pass = 0; pass < npass; ++pass) {
+            pass_geom(pass);
+            __syncthreads();
+            __syncthreads();
+            nusi_f64x4 acc[RT][NB];
+#pragma unroll
+            for (int a = 0; a < RT; ++a)
+#pragma unroll
+                for (int s = 0; s < NB; ++s) acc[a][s] = nusi_f64x4{0.0, 0.0, 0.0, 0.0};
+            auto load_blk = [&](int q, double (&dst)[RT]) {
+                int c = c0 + 1 - 4 * q + (lane >> 4);
+                c = c < 1 ? 1 : (c > T - 1 ? T - 1 : c);
+                const size_t cb = (size_t)c * (c - 1) / 2;
+#pragma unroll
+                for (int a = 0; a < RT; ++a) {
+                    const int row = rw0 + 16 * a + (lane & 15);
+                    dst[a] = Al[cb + (row < c - 1 ? row : c - 1)];
+                }
+            };
+            auto push = [&](int q, const double (&ab)[RT], bool phase_a) {
+                const int r = c0 - 4 * q, hi = r - 1;
+                double bop[NB];
+#pragma unroll
+                for (int s = 0; s < NB; ++s) bop[s] = Tp[((4 * q - 1 - (lane >> 4)) & 7) * NC + 16 * s + (lane & 15)];
+#pragma unroll
+                for (int a = 0; a < RT; ++a) {
+                    const bool crit = rw0 + 16 * a <= hi && rw0 + 16 * a + 15 >= hi - 3;   // uniform
+                    if (crit == phase_a && rw0 + 16 * a < r)   // tiles wholly at or above r hold consumed rows only
+#pragma unroll
+                        for (int s = 0; s < NB; ++s)
+                            acc[a][s] = __builtin_amdgcn_mfma_f64_16x16x4f64(ab[a], bop[s], acc[a][s], 0, 0, 0);
+                }
+                if (phase_a)
+#pragma unroll
+                    for (int a = 0; a < RT; ++a)
+                        if (rw0 + 16 * a <= hi && rw0 + 16 * a + 15 >= hi - 3)
+#pragma unroll
+                            for (int e = 0; e < 4; ++e) {
+                                const int row = rw0 + 16 * a + (lane >> 4) + 4 * e;
+                                const int slot = hi - row;
+                                if (slot >= 0 && slot < 4)
+#pragma unroll
+                                    for (int s = 0; s < NB; ++s)
+                                        AX[((q & 1) * 4 + slot) * NC + 16 * s + (lane & 15)] = acc[a][s][e];
+                            }
+            };
+            auto block = [&](int q, double (&ab)[RT]) {   // ab holds block q's A operands; then block q + 2's
+                const bool doq = nonres && q >= 1 && 4 * q < Ts;
+                if (doq) push(q, ab, true);
+                __syncthreads();
+                if (doq) push(q, ab, false);
+                load_blk(q + 2, ab);
+                __syncthreads();
+            };
+            double ab0[RT], ab1[RT];
+            load_blk(0, ab0);
+            load_blk(1, ab1);
+#pragma unroll 1
+            for (int q = 0; q < nblk; q += 2) {
+                block(q, ab0);
+                if (q + 1 < nblk) block(q + 1, ab1);
+            }
+        }
+    }
+}
 size_t cascade_gb_scratch_doubles(const GridDev& g) { return (size_t)3 * g.N * 16; }
 
 // launch geometry of the wavefront kernel: one thread per pushed row (T-1), whole waves; K stages
@@ -1984,6 +2341,73 @@ hipError_t launch_cascade_gb(const GridDev& g, const Point* pts, const int* gidx
     const int nthr = 64 * (gb_push_waves(g) + kGbChainWaves + 2);
     hipLaunchKernelGGL((k_cascade_gb<kGbNJ>), dim3(nwg), dim3(nthr), gb_lds(g), s, g, pts, gidx, grp, t, fh, flux,
                        flux_fla);
+    return hipGetLastError();
+}
+
+// the block-synchronous kernel (k_cascade_bs): push waves of 16 RT rows, the chain wave, the record wave
+static int bs_push_waves(const GridDev& g, int RT) { return (g.T - 1 + 16 * RT - 1) / (16 * RT); }
+template <int NJ, int P, int SPL, int RT>
+static size_t bs_lds(const GridDev& g)
+{
+    constexpr int NC = NJ * P;
+    return sizeof(double) * (2 * (size_t)kWfFields * 4 * NJ + 3 * 8 * (size_t)NC + 3 * (size_t)g.N + (size_t)P * (g.T + 2) +
+                             6 * (size_t)g.T + 4 * (size_t)g.Nz);
+}
+template <int NJ, int P, int SPL, int RT>
+static bool bs_fits_t(const GridDev& g)
+{
+    return g.T >= 2 && g.Nz >= 2 && bs_push_waves(g, RT) + 2 <= 16 && bs_lds<NJ, P, SPL, RT>(g) <= 160 * 1024;
+}
+template <int NJ, int P, int SPL, int RT>
+static void launch_bs_t(const GridDev& g, const Point* pts, const int* gidx, const int2* grp, int nwg, TablesDev t,
+                        double* fh, double* flux, double* flux_fla, hipStream_t s)
+{
+    const int nthr = 64 * (bs_push_waves(g, RT) + 2);
+    const size_t lds = bs_lds<NJ, P, SPL, RT>(g);
+    hipLaunchKernelGGL((k_cascade_bs<NJ, P, SPL, RT>), dim3(nwg), dim3(nthr), lds, s, g, pts, gidx, grp, t, fh, flux,
+                       flux_fla);
+}
+// P = 1: <wf_nj, 1, 1, 4> for one pass of up to 48 steps, else step passes of 48 (rows <= 14 x 64) or of 16 (rows
+// <= 14 x 128); P = 2: <wf_nj or 48, 2, 2, 2>; P = 16 (the gamma batch): <6, 16, 2, 2>
+int cascade_bs_config(const GridDev& g, int P)
+{
+    const int nj = wf_nj(g);
+    if (P == 1) {
+        if (nj && bs_fits_t<48, 1, 1, 4>(g)) return nj;
+        if (bs_fits_t<48, 1, 1, 4>(g)) return 48;
+        if (bs_fits_t<16, 1, 1, 8>(g)) return 16 + 1000;   // 128-row push waves
+        return 0;
+    }
+    if (P == 2) return bs_fits_t<48, 2, 2, 2>(g) ? (nj ? nj : 48) : 0;
+    if (P == 16) return bs_fits_t<6, 16, 2, 2>(g) ? 6 : 0;
+    return 0;
+}
+size_t cascade_bs_scratch_doubles(const GridDev& g, int P) { return (size_t)3 * g.N * P; }
+hipError_t launch_cascade_bs(const GridDev& g, const Point* pts, int P, const int* gidx, const int2* grp, int nwg,
+                             TablesDev t, double* fh, double* flux, double* flux_fla, hipStream_t s)
+{
+    if (nwg <= 0) return hipSuccess;
+    const int c = cascade_bs_config(g, P);
+    if (!c) return hipErrorInvalidValue;
+    if (P == 1) {
+        t_cascade_kernel = "k_cascade_bs";
+        switch (c) {
+        case 16: launch_bs_t<16, 1, 1, 4>(g, pts, gidx, grp, nwg, t, fh, flux, flux_fla, s); break;
+        case 32: launch_bs_t<32, 1, 1, 4>(g, pts, gidx, grp, nwg, t, fh, flux, flux_fla, s); break;
+        case 48: launch_bs_t<48, 1, 1, 4>(g, pts, gidx, grp, nwg, t, fh, flux, flux_fla, s); break;
+        default: launch_bs_t<16, 1, 1, 8>(g, pts, gidx, grp, nwg, t, fh, flux, flux_fla, s); break;
+        }
+    } else if (P == 2) {
+        t_cascade_kernel = "k_cascade_bs_pairs";
+        switch (c) {
+        case 16: launch_bs_t<16, 2, 2, 2>(g, pts, gidx, grp, nwg, t, fh, flux, flux_fla, s); break;
+        case 32: launch_bs_t<32, 2, 2, 2>(g, pts, gidx, grp, nwg, t, fh, flux, flux_fla, s); break;
+        default: launch_bs_t<48, 2, 2, 2>(g, pts, gidx, grp, nwg, t, fh, flux, flux_fla, s); break;
+        }
+    } else {
+        t_cascade_kernel = "k_cascade_bs_gamma";
+        launch_bs_t<6, 16, 2, 2>(g, pts, gidx, grp, nwg, t, fh, flux, flux_fla, s);
+    }
     return hipGetLastError();
 }
 

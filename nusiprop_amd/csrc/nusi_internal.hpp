@@ -85,6 +85,14 @@ bool cascade_gb_fits(const GridDev& g);
 size_t cascade_gb_scratch_doubles(const GridDev& g);
 hipError_t launch_cascade_gb(const GridDev& g, const Point* pts, const int* gidx, const int2* grp, int nwg, TablesDev t,
                              double* fh, double* flux, double* flux_fla, hipStream_t s);
+// The block-synchronous MFMA cascade (k_cascade_bs, round 4): workgroup k takes the grp[k].y <= P points gidx[grp[k].x
+// ..] that share one table slot (gidx == grp == nullptr: P = 1, point k), P = 1, 2 or 16 (the gamma batch), any source
+// and scattering mode, step passes on any grid that fits; fh: a FIFO of cascade_bs_scratch_doubles per workgroup
+// (used when the steps take more than one pass).  cascade_bs_config: 0 = the grid does not fit P.
+int cascade_bs_config(const GridDev& g, int P);
+size_t cascade_bs_scratch_doubles(const GridDev& g, int P);
+hipError_t launch_cascade_bs(const GridDev& g, const Point* pts, int P, const int* gidx, const int2* grp, int nwg,
+                             TablesDev t, double* fh, double* flux, double* flux_fla, hipStream_t s);
 size_t cascade_src_doubles(const GridDev& g);   // t.Src doubles per point
 hipError_t launch_source_dsnb(const GridDev& g, const Point* pts, int npts, double* src, hipStream_t s);
 // The bit-exact scalar cascades (NUSI_CASCADE_WAVEFRONT / REG / LDS; a kind that does not fit the grid falls

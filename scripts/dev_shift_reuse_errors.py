@@ -45,6 +45,28 @@ def main():
     for i in np.argsort(-e_shift)[:10]:
         out["worst"].append({"mphi": pts[i]["mphi"], "g": pts[i]["g"], "offset": int(i // 32) * 4,
                              "shift": float(e_shift[i]), "cond": float(e_cond[i])})
+    # the phi-phi warning test's lattice (N = 850, m_phi 3e7 r^(-o/2), o = 0, 10, 20, 30, K = 30), with and without
+    # the phi-phi channel, over couplings: shift vs direct
+    import tempfile
+    from nusiprop_amd.phiphi_tables import write_synthetic_tables
+    tdir = tempfile.mkdtemp(prefix="nusi_pp_")
+    at, atd, a, ad = write_synthetic_tables(tdir)
+    base = dict(scan.BASE, N_bins_E=850, mphi=6e5, g=0.01, si=2.5, norm=6.0)
+    r = 10 ** ((base["lEmax"] - base["lEmin"]) / base["N_bins_E"])
+    out["n850"] = []
+    for pp in (False, True):
+        for g in (0.01, 0.05, 0.1, 0.15, 0.3):
+            lat = [dict(base, mphi=3e7 * r ** (-o / 2), g=g, phiphi=pp) for o in (0, 10, 20, 30)]
+            plan = nu.Plan(850, base["lEmin"], base["lEmax"], base["zmax"], max_points=len(lat))
+            if pp:
+                plan.load_phiphi(at, a)
+            _, fd = plan.evolve(lat)
+            plan.set_option(_lib.OPT_SHIFT_REUSE, 30)
+            _, fs = plan.evolve(lat)
+            kern = plan.kernels()[0]
+            plan.close()
+            out["n850"].append({"phiphi": pp, "g": g, "shift_vs_direct": max(rel(fs[i], fd[i]) for i in range(len(lat))),
+                                "kernel": kern})
     print(json.dumps(out, indent=1))
 
 

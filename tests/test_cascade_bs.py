@@ -1,0 +1,118 @@
+"""The block-synchronous MFMA cascade k_cascade_bs (NUSI_OPT_CASCADE_SYNC = 2) against the per-stage kernels it
+replaces (k_cascade_ws one point / pairs, k_cascade_gb the gamma batch, k_cascade_wsp step passes) and the oracle.
+
+k_cascade_bs runs the same records, rank-4 MFMA block pushes and 3x3 solves on the same operands; only the points at
+which the waves synchronise differ (twice per block of four wavefront stages instead of once per stage).  So each
+point's flux must equal the per-stage kernel's bit for bit where both group it the same way, and the oracle's to
+FLUX_RTOL in every configuration -- one point per workgroup, pairs sharing a table, gamma batches of 3..16 points
+(power-law and DSNB sources), resonant-only points, and step passes on grids beyond 48 redshift steps (C3's)."""
+import numpy as np
+import pytest
+
+from tests import cases
+
+pytestmark = pytest.mark.gpu
+FLUX_RTOL = cases.FLUX_RTOL
+
+
+@pytest.fixture(scope="module")
+def nusi():
+    import nusiprop_amd
+    nusiprop_amd.load()
+    return nusiprop_amd
+
+
+def _run(nusi, pts, sync, **opts):
+    from nusiprop_amd import _lib
+    p0 = pts[0]
+    plan = nusi.Plan(p0["N_bins_E"], p0["lEmin"], p0["lEmax"], p0["zmax"], max_points=len(pts))
+    plan.set_option(_lib.OPT_CASCADE_SYNC, sync)
+    for k, v in opts.items():
+        plan.set_option(getattr(_lib, "OPT_" + k.upper()), v)
+    flux, fla = plan.evolve(pts)
+    tabs = [plan.tables(i) for i in range(len(pts))]
+    names = plan.kernels()
+    plan.close()
+    return flux, fla, tabs, names
+
+
+def _vs_oracle(nusi, oracle_mod, pts, fla, tabs):
+    for k, p in enumerate(pts):
+        o = oracle_mod.Oracle(**cases.oracle_kwargs(p))
+        o.prepare()
+        G, aT, A = tabs[k]
+        _, fla_ref = o.cascade(G, aT, nusi.unpack_alpha(A, o.T))
+        assert cases.rel_err(fla[k], fla_ref) <= FLUX_RTOL, (k, p)
+
+
+@pytest.mark.parametrize("N", [37, 100, 300])
+def test_bs_one_point_equals_ws(nusi, oracle_mod, N):
+    """One point per workgroup (distinct tables): power law and DSNB, Majorana and Dirac, resonant-only."""
+    pts = [dict(cases.C2B_100, N_bins_E=N, mphi=m, g=g, majorana=maj, non_resonant=nr, source_model=src)
+           for m, g, maj, nr, src in ((6e5, 0.01, True, True, 1), (2e6, 0.1, False, True, 1), (1e6, 0.3, True, True, 0),
+                                      (3e7, 0.8, True, False, 1), (8e5, 0.05, True, False, 0))]
+    lo = [dict(p, lEmin=4.0, lEmax=9.0, mphi=p["mphi"] / 200.0) for p in pts]   # DSNB flux nonzero at lE 4 -> 9
+    for grid in (pts, lo):
+        old = _run(nusi, grid, 1, cascade_rhs=1)
+        new = _run(nusi, grid, 2, cascade_rhs=1)
+        assert new[3][1] == "k_cascade_bs" and old[3][1] == "k_cascade_ws"
+        assert np.array_equal(new[0], old[0]) and np.array_equal(new[1], old[1])
+        _vs_oracle(nusi, oracle_mod, grid, new[1], new[2])
+
+
+@pytest.mark.parametrize("N", [100, 300])
+def test_bs_pairs_and_gamma_batches(nusi, oracle_mod, N):
+    """Points sharing a table: pairs (k_cascade_bs_pairs) and gamma batches of 3..16 (k_cascade_bs_gamma), mixed
+    sources in one batch; each point equals its one-point-per-workgroup flux bit for bit and the oracle's to
+    FLUX_RTOL."""
+    base = [dict(cases.C2B_100, N_bins_E=N, mphi=m, g=g) for m, g in ((6e5, 0.01), (2e6, 0.1), (1e6, 0.3))]
+    pts = [dict(base[0], si=2.0 + 0.05 * k) for k in range(16)]                              # a full batch
+    pts += [dict(base[1], si=s, source_model=src) for s, src in ((2.2, 1), (2.5, 0), (2.8, 1))]   # mixed, 3
+    pts += [dict(base[2], si=s) for s in (2.1, 2.9)]                                          # a pair
+    pts += [dict(base[2], mphi=7e5, si=2.4)]                                                  # alone
+    one = _run(nusi, pts, 2, cascade_rhs=1)
+    grp = _run(nusi, pts, 2)
+    assert grp[3][1] == "k_cascade_bs_gamma + pairs + k_cascade_bs"
+    for a, b in zip(grp[:2], one[:2]):
+        d = max(cases.rel_err(a[k], b[k]) for k in range(len(pts)))
+        assert d <= FLUX_RTOL and np.array_equal(a == 0, b == 0), d
+    _vs_oracle(nusi, oracle_mod, pts, grp[1], grp[2])
+    pl = [p for p in pts if p["source_model"] == 1]   # the per-stage gamma batch takes power-law points only
+    old = _run(nusi, pl[:16], 1)
+    new = _run(nusi, pl[:16], 2)
+    assert old[3][1] == "k_cascade_gb" and new[3][1] == "k_cascade_bs_gamma"
+    assert np.array_equal(new[1], old[1]), max(cases.rel_err(new[1][k], old[1][k]) for k in range(16))
+
+
+def test_bs_c5_block(nusi, oracle_mod):
+    """BASELINE C5: one 16-gamma block of scan.c5_points() on k_cascade_bs_gamma against the oracle."""
+    from nusiprop_amd import scan
+    blk = scan.c5_points()[16 * 777:16 * 778]
+    flux, fla, tabs, names = _run(nusi, blk, 2)
+    assert names[1] == "k_cascade_bs_gamma"
+    o = oracle_mod.Oracle(**cases.oracle_kwargs(blk[0]))
+    G, aT, al = o.tables()
+    for k, p in enumerate(blk):
+        ok = oracle_mod.Oracle(**cases.oracle_kwargs(p))
+        ok.prepare()
+        _, fla_ref = ok.cascade(G, aT, al)
+        assert cases.rel_err(fla[k], fla_ref) <= FLUX_RTOL, k
+
+
+@pytest.mark.parametrize("N,lEmin", [(200, 12.0), (700, 12.0), (1200, 10.0)])
+def test_bs_step_passes(nusi, oracle_mod, N, lEmin):
+    """Grids beyond 48 redshift steps (N = 200: 32 steps, 700: 109, C3's 1200 at lE 10 -> 17: 134) in step passes,
+    one point per workgroup and gamma batches (the FIFO carries each pass' last step to the next pass)."""
+    pts = [dict(cases.C2B_100, N_bins_E=N, lEmin=lEmin, mphi=m, g=g, majorana=maj)
+           for m, g, maj in ((6e5, 0.01, True), (1e5, 0.05, True), (2e6, 0.3, False))]
+    pts += [dict(pts[0], si=s) for s in (2.0, 2.2, 2.7)]
+    new = _run(nusi, pts, 2)
+    assert "k_cascade_bs" in new[3][1]
+    _vs_oracle(nusi, oracle_mod, pts, new[1], new[2])
+    old = _run(nusi, pts, 1, cascade_rhs=1)
+    one = _run(nusi, pts, 2, cascade_rhs=1)
+    assert one[3][1] == "k_cascade_bs"
+    if N == 1200:   # 1332 rows: the 128-row / 16-step configuration, k_cascade_wsp's passes
+        assert old[3][1] == "k_cascade_ws_passes"
+        assert np.array_equal(one[1], old[1]), max(cases.rel_err(one[1][k], old[1][k]) for k in range(len(pts)))
+    assert max(cases.rel_err(one[1][k], old[1][k]) for k in range(len(pts))) <= FLUX_RTOL
