@@ -192,11 +192,12 @@ int nusi_plan_set_cascade(nusi_plan *plan, int kind);
  *                          whose m_phi lie on that lattice within K bins of
  *                          the largest are served by ONE table set of the
  *                          largest m_phi on the axis extended by K bins.  Not
- *                          bit-exact: the bin edges round differently, and
- *                          the fluxes move by <= 1e-9 relative on the tested
- *                          cases (tests/test_f4_index_shift.py, GPU:
- *                          test_shift_reuse_scan); the default path is
- *                          unchanged. */
+ *                          bit-exact: the bin edges round differently, and the
+ *                          flux's optical depth amplifies that with the
+ *                          coupling, so only tables with g <= 0.05 share
+ *                          (measured <= 8.8e-10 relative there; 3e-8 at g = 1
+ *                          had they shared; tests/test_shift_reuse.py); the
+ *                          default path is unchanged. */
 #define NUSI_OPT_ALPHA_BATCH 1
 #define NUSI_OPT_ALPHA_KERNEL 2
 #define NUSI_OPT_CASCADE_RHS 3

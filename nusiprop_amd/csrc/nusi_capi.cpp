@@ -603,10 +603,11 @@ int shift_groups(nusi_plan* pl, int ntab, std::vector<int>& remap, std::vector<i
         return std::make_tuple(P.g, P.mn[0], P.mn[1], P.mn[2], P.u[0], P.u[1], P.u[2], P.majorana, P.non_resonant,
                                P.phiphi);
     };
-    // only couplings up to kShiftReuseGMax share: the shifted tables differ from a point's own by rounding, and at
-    // strong coupling the flux's optical depth amplifies that (c4s lattice, scripts/dev_shift_reuse_errors.py on the
-    // GPU: <= 6.4e-10 for g <= 0.135, 9.8e-10 at 0.168, 3e-8 at g = 1; the north star bounds fluxes at 1e-9)
-    constexpr double kShiftReuseGMax = 0.15;
+    // only couplings up to kShiftReuseGMax share: the shifted tables differ from a point's own by rounding, and the
+    // flux's optical depth amplifies that with the coupling (scripts/dev_shift_reuse_errors.py on the GPU, vs each
+    // point's own evolution: c4s lattice <= 1.7e-11 for g <= 0.044, 6.4e-10 at 0.135, 3e-8 at g = 1; N_E = 850,
+    // m_phi = 3e7: 8.8e-10 at g = 0.05, 1.4e-8 at 0.1; the north star bounds fluxes at 1e-9)
+    constexpr double kShiftReuseGMax = 0.05;
     std::vector<int> idx;
     for (int j = 0; j < ntab; ++j)
         if (tp[j].g <= kShiftReuseGMax) idx.push_back(j);

@@ -1913,6 +1913,12 @@ struct BsCfg {
     static_assert(NJ % SPL == 0 && NC % 16 == 0 && LPP * P <= 64, "one chain wave, whole column tiles");
 };
 
+// record fields of the block-synchronous kernel: PR_* without PR_SRC (the sources have a block of their own), so
+// fields >= PR_L10 sit one lower -- record_phase2 writes them through a base pointer one field stride lower
+enum { BR_RZ0, BR_RZ1, BR_RZ2, BR_L10, BR_L20, BR_L21, BR_U01, BR_U02, BR_U12, BR_RU00, BR_RU11, BR_RU22, BR_SDE, BR_PERM,
+       kBsFields };
+static_assert(PR_L10 - 1 == BR_L10 && PR_RU22 - 1 == BR_RU22 && kPreFields - 1 == BR_PERM, "record_phase2's fields, shifted");
+
 template <int NJ, int P, int SPL, int RT>
 __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4, 4)))
 void k_cascade_bs(GridDev g, const Point* __restrict__ pts, const int* __restrict__ gidx, const int2* __restrict__ grp,
@@ -1920,10 +1926,10 @@ void k_cascade_bs(GridDev g, const Point* __restrict__ pts, const int* __restric
 {
     extern __shared__ __attribute__((aligned(16))) double lds[];
     using Cfg = BsCfg<NJ, P, SPL, RT>;
-    constexpr int LPP = Cfg::LPP, NC = Cfg::NC, NB = Cfg::NB, NF = kWfFields, S4 = 4 * NJ;
+    constexpr int LPP = Cfg::LPP, NC = Cfg::NC, NB = Cfg::NB, NF = kBsFields, S4 = 4 * NJ, NQ = 12 * P;
     const int N = g.N, Nz = g.Nz, T = g.T, nst = Nz - 1;
     const int tid = threadIdx.x, nthr = blockDim.x, lane = tid & 63, wave = tid >> 6, nw = nthr >> 6;
-    const int nwp = nw - 2, chw = nw - 2, recw = nw - 1;   // push waves, the chain wave, the record wave
+    const int chw = nw - 2, recw = nw - 1;   // push waves 0 .. nw-3, the chain wave, the record wave
     const int2 gr = grp ? grp[blockIdx.x] : make_int2((int)blockIdx.x, 1);
     const int R = gr.y;                                   // points of this workgroup (<= P), one table
     auto pidx = [&](int p) { return gidx ? gidx[gr.x + p] : gr.x + p; };   // (gidx == nullptr: point blockIdx.x)
@@ -1932,7 +1938,9 @@ void k_cascade_bs(GridDev g, const Point* __restrict__ pts, const int* __restric
     double* srcb = rec + 2 * NF * S4;        // [2][4][NJ][P]   the sources c_i Lum of block q's (stage, step, point)
     double* Tp = srcb + 8 * NC;              // [8][NC]         T_j of each column by stage
     double* AX = Tp + 8 * NC;                // [2][4][NC]      rows published by block q (parity q & 1)
-    double* rdE = AX + 8 * NC;               // [N]
+    double* fqb = AX + 8 * NC;               // [2][4][3][P]    the previous pass' last step, F[:, N-1-sg], block q
+    double* pinf = fqb + 2 * NQ;             // [4][P]          per point: a3, rs, power law (1) / DSNB (0), index
+    double* rdE = pinf + 4 * P;              // [N]
     double* pw = rdE + N;                    // [P][T + 2]      each power-law point's pw on table edge e
     double* sGt = pw + (size_t)P * (T + 2);
     double* sAt = sGt + T;
@@ -1968,6 +1976,14 @@ void k_cascade_bs(GridDev g, const Point* __restrict__ pts, const int* __restric
             sgz[2 * Nz + i] = g.step_s[i];
             sgz[3 * Nz + i] = g.sfr[i];
         }
+        for (int p = tid; p < P; p += nthr) {   // the points' source factors (src_factors), kind and index
+            const int pid = p < R ? pidx(p) : 0;
+            const SrcFactors f = src_factors(pts[pid]);
+            pinf[p] = f.a3;
+            pinf[P + p] = f.rs;
+            pinf[2 * P + p] = p < R && pts[pid].source == NUSI_SOURCE_POWER_LAW ? 1.0 : 0.0;
+            pinf[3 * P + p] = (double)pid;
+        }
         for (int q = tid; q < P * (T + 1); q += nthr) {   // cascade_aux_init's pw[e] of every power-law point
             const int p = q / (T + 1), e = 1 + q - p * (T + 1);
             if (p >= R) continue;
@@ -1989,38 +2005,10 @@ void k_cascade_bs(GridDev g, const Point* __restrict__ pts, const int* __restric
         c0 = T - 1 - jb;                       // the table column of its stage 0
         nblk = (Ts + 3) / 4;
     };
-    // the records of block qb (its 4 stages x NJ steps) and the sources of its (stage, step, point), slot qb & 1
-    auto records = [&](int qb) {
-        for (int e = lane; e < S4; e += 64) {
-            const int sb = e / NJ, jj = e - NJ * (e / NJ), s2 = 4 * qb + sb;
-            const int b = N - 1 - s2 + jj, i = Nz - 1 - jb - jj;
-            if (jj < njp && s2 < Ts && b >= 0 && b < N) {
-                double* Rw = rec + (size_t)(qb & 1) * NF * S4 + e;
-                const RecM m = record_phase1(gl, P0, sGt, sAt, rdE, i, b);
-                Rw[PR_RZ0 * S4] = m.rz0;
-                Rw[PR_RZ1 * S4] = m.rz1;
-                Rw[PR_RZ2 * S4] = m.rz2;
-                Rw[PR_SDE * S4] = nonres ? gl.step_s[i] * rdE[b] : (gl.Emax[b] - gl.Emin[b]);
-                record_phase2<true>(m, Rw, S4);
-            }
-        }
-        for (int e = lane; e < S4 * P; e += 64) {
-            const int p = e % P, sj = e / P, sb = sj / NJ, jj = sj - NJ * sb, s2 = 4 * qb + sb;
-            const int b = N - 1 - s2 + jj, i = Nz - 1 - jb - jj;
-            if (p < R && jj < njp && s2 < Ts && b >= 0 && b < N) {
-                const int pid = pidx(p);
-                const Point& Q = pts[pid];
-                srcb[(qb & 1) * 4 * NC + e] =
-                    Q.source == NUSI_SOURCE_POWER_LAW ? powerlaw_src_h(gl, src_factors(Q), pw + (size_t)p * (T + 2), i, b)
-                                                      : t.Src[(size_t)pid * T * nst + src_index(Nz, jb + jj, b)];
-            }
-        }
-    };
     if (wave == chw) {
         // ---- chain: lane (cp, cjp) solves the slots j = SPL cjp + k of point cp
         const int cp = lane / LPP, cjp = lane - LPP * (lane / LPP);
         const bool clane = lane < P * LPP && cp < R;
-        const int cpid = clane ? pidx(cp) : 0;
         const double u0 = P0.u[0], u1 = P0.u[1], u2 = P0.u[2];
 #pragma unroll 1
         for (int pass = 0; pass < npass; ++pass) {
@@ -2029,31 +2017,12 @@ void k_cascade_bs(GridDev g, const Point* __restrict__ pts, const int* __restric
             __syncthreads();   // the previous pass is done with Tp, AX and the records
             for (int q = lane; q < 16 * NC; q += 64) Tp[q] = 0.0;   // Tp and AX
             __syncthreads();
-            double cj[SPL], sj[SPL], px0[SPL], px1[SPL], px2[SPL], racc[SPL], Th[SPL][4];
+            double px0[SPL], px1[SPL], px2[SPL], racc[SPL], Th[SPL][4];
 #pragma unroll
             for (int k = 0; k < SPL; ++k) {
-                const int j = SPL * cjp + k, i = Nz - 1 - jb - j;
-                const bool act = clane && j < njp;
-                cj[k] = act ? gl.step_c[i] : 0.0;
-                sj[k] = act ? gl.step_s[i] : 0.0;
                 px0[k] = px1[k] = px2[k] = racc[k] = 0.0;
 #pragma unroll
                 for (int d = 0; d < 4; ++d) Th[k][d] = 0.0;
-            }
-            // the first step of a pass > 0 starts from the previous pass' last step: F[:, b] from the FIFO, a block ahead
-            const bool ffifo = pass > 0 && cjp == 0 && clane;
-            double fq[4][3];
-            auto fifo_load = [&](int sg, double (&f)[3]) {
-                const int bq = N - 1 - sg;
-                if (ffifo && sg < Ts && bq >= 0) {
-#pragma unroll
-                    for (int c = 0; c < 3; ++c) f[c] = __builtin_nontemporal_load(fhw + ((size_t)c * N + bq) * P + cp);
-                }
-            };
-#pragma unroll
-            for (int d = 0; d < 4; ++d) {
-                fq[d][0] = fq[d][1] = fq[d][2] = 0.0;
-                fifo_load(d, fq[d]);
             }
             // stage sg = 4 q + d of the pass
             auto stage = [&](int q, int d) {
@@ -2063,12 +2032,11 @@ void k_cascade_bs(GridDev g, const Point* __restrict__ pts, const int* __restric
                 f0[0] = wave_shr1(px0[SPL - 1], 0.0);   // every lane active: the previous lane's last slot
                 f1[0] = wave_shr1(px1[SPL - 1], 0.0);
                 f2[0] = wave_shr1(px2[SPL - 1], 0.0);
-                if (cjp == 0) {
-                    f0[0] = fq[d][0];
-                    f1[0] = fq[d][1];
-                    f2[0] = fq[d][2];
-                    fq[d][0] = fq[d][1] = fq[d][2] = 0.0;
-                    fifo_load(sg + 4, fq[d]);
+                if (cjp == 0) {   // the first step: the previous pass' last step (fqb, staged by the record wave), or 0
+                    const double* fq = fqb + (q & 1) * NQ + d * 3 * P + cp;
+                    f0[0] = fq[0];
+                    f1[0] = fq[P];
+                    f2[0] = fq[2 * P];
                 }
 #pragma unroll
                 for (int k = 1; k < SPL; ++k) {
@@ -2088,30 +2056,32 @@ void k_cascade_bs(GridDev g, const Point* __restrict__ pts, const int* __restric
                     double Tn = 0.0;
                     if (clane && j < njp && b >= 0 && b < N) {
                         const double* Rc = Rb + j;
-                        const double rz0 = Rc[PR_RZ0 * S4], rz1 = Rc[PR_RZ1 * S4], rz2 = Rc[PR_RZ2 * S4];
-                        const int pmb = (int)Rc[kPreFields * S4];
-                        const double l10 = Rc[PR_L10 * S4], l20 = Rc[PR_L20 * S4], l21 = Rc[PR_L21 * S4];
-                        const double u01 = Rc[PR_U01 * S4], u02 = Rc[PR_U02 * S4], u12 = Rc[PR_U12 * S4];
-                        const double ru00 = Rc[PR_RU00 * S4], ru11 = Rc[PR_RU11 * S4], ru22 = Rc[PR_RU22 * S4];
-                        const double sde = Rc[PR_SDE * S4];
+                        const double rz0 = Rc[BR_RZ0 * S4], rz1 = Rc[BR_RZ1 * S4], rz2 = Rc[BR_RZ2 * S4];
+                        const int pmb = (int)Rc[BR_PERM * S4];
+                        const double l10 = Rc[BR_L10 * S4], l20 = Rc[BR_L20 * S4], l21 = Rc[BR_L21 * S4];
+                        const double u01 = Rc[BR_U01 * S4], u02 = Rc[BR_U02 * S4], u12 = Rc[BR_U12 * S4];
+                        const double ru00 = Rc[BR_RU00 * S4], ru11 = Rc[BR_RU11 * S4], ru22 = Rc[BR_RU22 * S4];
+                        const double sde = Rc[BR_SDE * S4];
                         const double src = Sb[j * P + cp];
+                        const double cj = gl.step_c[Nz - 1 - jb - j];
                         double add;
                         if (nonres) {
                             double sa = Ab[j * P + cp];
 #pragma unroll
                             for (int kk = 4; kk >= 1; --kk)
                                 if (kk <= nu) sa = fma(sdg[(kk - 1) * T + r], Th[k][kk - 1], sa);
-                            add = cj[k] * sa;
+                            add = cj * sa;
                         } else {
                             const double dEb1 = (b + 1 < N) ? sEmax[b + 1] - sEmin[b + 1] : 1.0;
-                            add = resonant_add(racc[k], u0, u1, u2, px0[k], px1[k], px2[k], sj[k], sdg[r], dEb1, sde,
-                                               cj[k], b == N - 1);
+                            add = resonant_add(racc[k], u0, u1, u2, px0[k], px1[k], px2[k], gl.step_s[Nz - 1 - jb - j],
+                                               sdg[r], dEb1, sde, cj, b == N - 1);
                         }
                         double x0, x1, x2;
                         cascade_solve(f0[k], f1[k], f2[k], add, src, u0, u1, u2, rz0, rz1, rz2, pmb, l10, l20, l21, u01,
                                       u02, u12, ru00, ru11, ru22, x0, x1, x2);
                         if (j == njp - 1) {   // the pass's last step: the next pass' input, or the output
                             if (last_pass) {   // finalise (nuSIprop.hpp:328-336)
+                                const int cpid = (int)pinf[3 * P + cp];
                                 const Point& Q = pts[cpid];
                                 const double dE = gl.Emax[b] - gl.Emin[b];
                                 const double g0 = x0 / dE, g1 = x1 / dE, g2 = x2 / dE;
@@ -2144,21 +2114,70 @@ void k_cascade_bs(GridDev g, const Point* __restrict__ pts, const int* __restric
                     if (4 * q + d < Ts) stage(q, d);                // phase B
                 __syncthreads();
             }
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the FIFO stores land before the next pass reads
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the FIFO stores land before the next pass reads them
         }
     } else if (wave == recw) {
-        // ---- records: block 0 before the blocks, block q + 1 in phase B of block q (the chain reads block q's slot;
-        // block q + 1's slot was last read in phase B of block q - 1)
+        // ---- records and sources: block 0 (and the FIFO of blocks 0, 1) before the blocks; in block q the records of
+        // block q + 1 (phase A: block q + 1's slot was last read in phase B of block q - 1) and its sources (phase B);
+        // the FIFO values of block q + 2 are loaded in phase A of block q and stored in phase A of block q + 1
+        auto records = [&](int qb) {
+            for (int e = lane; e < S4; e += 64) {
+                const int sb = e / NJ, jj = e - NJ * (e / NJ), s2 = 4 * qb + sb;
+                const int b = N - 1 - s2 + jj, i = Nz - 1 - jb - jj;
+                if (jj < njp && s2 < Ts && b >= 0 && b < N) {
+                    double* Rw = rec + (size_t)(qb & 1) * NF * S4 + e;
+                    const RecM m = record_phase1(gl, P0, sGt, sAt, rdE, i, b);
+                    Rw[BR_RZ0 * S4] = m.rz0;
+                    Rw[BR_RZ1 * S4] = m.rz1;
+                    Rw[BR_RZ2 * S4] = m.rz2;
+                    Rw[BR_SDE * S4] = nonres ? gl.step_s[i] * rdE[b] : (gl.Emax[b] - gl.Emin[b]);
+                    record_phase2<true>(m, Rw - S4, S4);   // (PR_L10 .. PR_RU22, the permutation: BR_* = PR_* - 1)
+                }
+            }
+        };
+        auto sources = [&](int qb) {
+            for (int e = lane; e < S4 * P; e += 64) {
+                const int p = e % P, sj = e / P, sb = sj / NJ, jj = sj - NJ * sb, s2 = 4 * qb + sb;
+                const int b = N - 1 - s2 + jj, i = Nz - 1 - jb - jj;
+                if (p < R && jj < njp && s2 < Ts && b >= 0 && b < N)
+                    srcb[(qb & 1) * 4 * NC + e] =
+                        pinf[2 * P + p] != 0.0
+                            ? powerlaw_src_h(gl, SrcFactors{pinf[p], pinf[P + p]}, pw + (size_t)p * (T + 2), i, b)
+                            : t.Src[(size_t)pinf[3 * P + p] * T * nst + src_index(Nz, jb + jj, b)];
+            }
+        };
+        constexpr int FQL = (NQ + 63) / 64;   // FIFO values per lane and block
+        auto fifo_load = [&](int pass, int qb, double (&v)[FQL]) {
+#pragma unroll
+            for (int u = 0; u < FQL; ++u) {
+                const int e = lane + 64 * u, d = e / (3 * P), c = (e / P) % 3, p = e % P, sg = 4 * qb + d, bq = N - 1 - sg;
+                v[u] = (pass > 0 && e < NQ && sg < Ts && bq >= 0)
+                           ? __builtin_nontemporal_load(fhw + ((size_t)c * N + bq) * P + p) : 0.0;
+            }
+        };
+        auto fifo_store = [&](int qb, const double (&v)[FQL]) {
+#pragma unroll
+            for (int u = 0; u < FQL; ++u)
+                if (lane + 64 * u < NQ) fqb[(qb & 1) * NQ + lane + 64 * u] = v[u];
+        };
 #pragma unroll 1
         for (int pass = 0; pass < npass; ++pass) {
             pass_geom(pass);
             __syncthreads();
             records(0);
+            sources(0);
+            double fv[FQL];
+            fifo_load(pass, 0, fv);
+            fifo_store(0, fv);
+            fifo_load(pass, 1, fv);
             __syncthreads();
 #pragma unroll 1
             for (int q = 0; q < nblk; ++q) {
+                fifo_store(q + 1, fv);                  // block q + 1's FIFO values (loaded a block ago)
+                fifo_load(pass, q + 2, fv);
+                if (4 * (q + 1) < Ts) records(q + 1);   // phase A
                 __syncthreads();
-                if (4 * (q + 1) < Ts) records(q + 1);
+                if (4 * (q + 1) < Ts) sources(q + 1);   // phase B
                 __syncthreads();
             }
         }
@@ -2188,16 +2207,14 @@ void k_cascade_bs(GridDev g, const Point* __restrict__ pts, const int* __restric
             };
             auto push = [&](int q, const double (&ab)[RT], bool phase_a) {
                 const int r = c0 - 4 * q, hi = r - 1;
-                double bop[NB];
-#pragma unroll
-                for (int s = 0; s < NB; ++s) bop[s] = Tp[((4 * q - 1 - (lane >> 4)) & 7) * NC + 16 * s + (lane & 15)];
+                const double* Tq = Tp + ((4 * q - 1 - (lane >> 4)) & 7) * NC + (lane & 15);
 #pragma unroll
                 for (int a = 0; a < RT; ++a) {
                     const bool crit = rw0 + 16 * a <= hi && rw0 + 16 * a + 15 >= hi - 3;   // uniform
                     if (crit == phase_a && rw0 + 16 * a < r)   // tiles wholly at or above r hold consumed rows only
 #pragma unroll
                         for (int s = 0; s < NB; ++s)
-                            acc[a][s] = __builtin_amdgcn_mfma_f64_16x16x4f64(ab[a], bop[s], acc[a][s], 0, 0, 0);
+                            acc[a][s] = __builtin_amdgcn_mfma_f64_16x16x4f64(ab[a], Tq[16 * s], acc[a][s], 0, 0, 0);
                 }
                 if (phase_a)
 #pragma unroll
@@ -2350,8 +2367,8 @@ template <int NJ, int P, int SPL, int RT>
 static size_t bs_lds(const GridDev& g)
 {
     constexpr int NC = NJ * P;
-    return sizeof(double) * (2 * (size_t)kWfFields * 4 * NJ + 3 * 8 * (size_t)NC + 3 * (size_t)g.N + (size_t)P * (g.T + 2) +
-                             6 * (size_t)g.T + 4 * (size_t)g.Nz);
+    return sizeof(double) * (2 * (size_t)kBsFields * 4 * NJ + 3 * 8 * (size_t)NC + 24 * (size_t)P + 4 * (size_t)P +
+                             3 * (size_t)g.N + (size_t)P * (g.T + 2) + 6 * (size_t)g.T + 4 * (size_t)g.Nz);
 }
 template <int NJ, int P, int SPL, int RT>
 static bool bs_fits_t(const GridDev& g)
