@@ -67,7 +67,7 @@ def test_shift_reuse_off_is_default_and_exact(nusi):
     differ from the direct ones only by rounding, and option 0 restores the direct tables bit for bit."""
     from nusiprop_amd import _lib
     base = dict(cases.C2B_100)
-    pts = _lattice_points(base, (0, 2, 4), (0.1,))
+    pts = _lattice_points(base, (0, 2, 4), (0.03,))   # (g <= 0.05: couplings that share)
     plan = nusi.Plan(base["N_bins_E"], base["lEmin"], base["lEmax"], base["zmax"], max_points=len(pts))
     f_direct, _ = plan.evolve(pts)
     t_direct = [plan.tables(i) for i in range(len(pts))]
