@@ -848,8 +848,15 @@ __device__ unsigned int g_ws_hwid[kTrBlocks * kTrWaves];   // HW_ID (SE, CU, SIM
         if (blockIdx.x == 0 && (threadIdx.x & 63) == 0 && (sg) < kTrStages)                                        \
             g_ws_trace[((threadIdx.x >> 6) * kTrStages + (sg)) * 4 + (which)] = __builtin_amdgcn_s_memtime();        \
     } while (0)
+// k_cascade_bs: [wave][block][phase A start, its barrier, phase B start, its barrier], no waits
+#define NUSI_BS_STAMP(blk, which)                                                                                  \
+    do {                                                                                                           \
+        if (blockIdx.x == 0 && (threadIdx.x & 63) == 0 && (blk) < kTrStages)                                       \
+            g_ws_trace[((threadIdx.x >> 6) * kTrStages + (blk)) * 4 + (which)] = __builtin_amdgcn_s_memtime();      \
+    } while (0)
 #else
 #define NUSI_WS_STAMP(sg, which) do { } while (0)
+#define NUSI_BS_STAMP(blk, which) do { } while (0)
 #define NUSI_WS_HWID() do { } while (0)
 #endif
 
@@ -2107,11 +2114,15 @@ void k_cascade_bs(GridDev g, const Point* __restrict__ pts, const int* __restric
             };
 #pragma unroll 1
             for (int q = 0; q < nblk; ++q) {
+                NUSI_BS_STAMP(pass * nblk + q, 0);
                 if (4 * q < Ts) stage(q, 0);                        // phase A
+                NUSI_BS_STAMP(pass * nblk + q, 1);
                 __syncthreads();
+                NUSI_BS_STAMP(pass * nblk + q, 2);
 #pragma unroll
                 for (int d = 1; d < 4; ++d)
                     if (4 * q + d < Ts) stage(q, d);                // phase B
+                NUSI_BS_STAMP(pass * nblk + q, 3);
                 __syncthreads();
             }
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the FIFO stores land before the next pass reads them
@@ -2173,11 +2184,15 @@ void k_cascade_bs(GridDev g, const Point* __restrict__ pts, const int* __restric
             __syncthreads();
 #pragma unroll 1
             for (int q = 0; q < nblk; ++q) {
+                NUSI_BS_STAMP(pass * nblk + q, 0);
                 fifo_store(q + 1, fv);                  // block q + 1's FIFO values (loaded a block ago)
                 fifo_load(pass, q + 2, fv);
                 if (4 * (q + 1) < Ts) records(q + 1);   // phase A
+                NUSI_BS_STAMP(pass * nblk + q, 1);
                 __syncthreads();
+                NUSI_BS_STAMP(pass * nblk + q, 2);
                 if (4 * (q + 1) < Ts) sources(q + 1);   // phase B
+                NUSI_BS_STAMP(pass * nblk + q, 3);
                 __syncthreads();
             }
         }
@@ -2232,10 +2247,14 @@ void k_cascade_bs(GridDev g, const Point* __restrict__ pts, const int* __restric
             };
             auto block = [&](int q, double (&ab)[RT]) {   // ab holds block q's A operands; then block q + 2's
                 const bool doq = nonres && q >= 1 && 4 * q < Ts;
+                NUSI_BS_STAMP(pass * nblk + q, 0);
                 if (doq) push(q, ab, true);
+                NUSI_BS_STAMP(pass * nblk + q, 1);
                 __syncthreads();
+                NUSI_BS_STAMP(pass * nblk + q, 2);
                 if (doq) push(q, ab, false);
                 load_blk(q + 2, ab);
+                NUSI_BS_STAMP(pass * nblk + q, 3);
                 __syncthreads();
             };
             double ab0[RT], ab1[RT];

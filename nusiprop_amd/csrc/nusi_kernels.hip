@@ -287,10 +287,17 @@ __global__ __launch_bounds__(kTileThreads) NUSI_TILE_ATTR void k_alpha_tile(Grid
 #define NUSI_BATCH_QC 5
 #endif
 constexpr int kBatchQC = NUSI_BATCH_QC;   // kBatchQC (ct + cs + kAlphaTile) <= 256 jobs
+// NUSI_BATCH_PIPE (A/B): the member corners of point q + 1 are formed while point q combines (two mem buffers),
+// one barrier per point instead of two
+#ifndef NUSI_BATCH_PIPE
+#define NUSI_BATCH_PIPE 0
+#endif
+constexpr bool kBatchPipe = NUSI_BATCH_PIPE != 0;
 __host__ __device__ inline int alpha_batch_lds_doubles()
 {
     const int c1 = kAlphaTile + 1;
-    return (3 + kXFields + 2) * c1 * c1 + alpha_tile_edge_stride(c1, c1) + kBatchQC * alpha_batch_memb_doubles(c1, c1);
+    return (3 + kXFields + (kBatchPipe ? 4 : 2)) * c1 * c1 + alpha_tile_edge_stride(c1, c1) +
+           kBatchQC * alpha_batch_memb_doubles(c1, c1);
 }
 static_assert(kXFields * (kAlphaTile + 1) * (kAlphaTile + 1) >= 4 * (kAlphaTile + 1) * (kAlphaTile + 1) + kAlphaTile * 2 * (kAlphaTile + 1),
               "the bracket phase's blocks fit X");
@@ -410,8 +417,8 @@ void k_alpha_batch(GridDev g, const Point* __restrict__ pts, const SplineSet* __
     constexpr int ccmax = (kAlphaTile + 1) * (kAlphaTile + 1);
     double* P3 = sm;                           // [3][cc]
     double* X = P3 + 3 * ccmax;                // [kXFields][cc] | LL TU1 TU2 G [4][cc] + mixed
-    double* mem = X + kXFields * ccmax;        // [2][cc]
-    double* edgk = mem + 2 * ccmax;            // [estride]
+    double* mem = X + kXFields * ccmax;        // [2][cc] (kBatchPipe: [2][2][cc], by point parity)
+    double* edgk = mem + (kBatchPipe ? 4 : 2) * ccmax;   // [estride]
     double* membq = edgk + alpha_tile_edge_stride(kAlphaTile + 1, kAlphaTile + 1);   // [kBatchQC][mbd]
     const int mbd = alpha_batch_memb_doubles(cs, ct);
     double* tmp = X;
@@ -467,6 +474,13 @@ void k_alpha_batch(GridDev g, const Point* __restrict__ pts, const SplineSet* __
                                        med + ((size_t)(p0 + q0 + mq) * 3 + k) * kMedFields * T, mv);
                 alpha_batch_medge_store(nonres, mjob, ct, cs, m0, Tm, mv, membq + mq * mbd);
             }
+            constexpr bool pipe = kBatchPipe && !kRef;
+            if (pipe) {
+                __syncthreads();   // member edges written
+                if (cornered)
+                    for (int j = tid; j < cc; j += kTileThreads)
+                        alpha_batch_mcorner_job(pts[p0 + q0], j, edgk, ct, cs, X, membq, mem);
+            }
 #pragma unroll 1
             for (int qq = 0; qq < nq; ++qq) {
                 const int q = q0 + qq;
@@ -474,20 +488,30 @@ void k_alpha_batch(GridDev g, const Point* __restrict__ pts, const SplineSet* __
                 const double* memb = membq + qq * mbd;
                 double tot = tnext;   // after states < k
                 if (reload && q + 1 < nb) tnext = A[(size_t)(p0 + q + 1) * g.PT + eidx];
-                __syncthreads();   // member edges written / the previous point's combine is done with mem
-                if (cornered) {
-                    if (kRef)
-                        for (int j = tid; j < cc; j += kTileThreads) alpha_batch_mcorner_ref_job(Q, j, edgk, ct, cs, X);
-                    else
-                        for (int j = tid; j < cc; j += kTileThreads) alpha_batch_mcorner_job(Q, j, edgk, ct, cs, X, memb, mem);
+                double* memq = mem;
+                if (pipe) {
+                    memq = mem + (qq & 1) * 2 * ccmax;
+                    __syncthreads();   // mem of q written / the previous point's combine is done with the other buffer
+                    if (cornered && qq + 1 < nq)
+                        for (int j = tid; j < cc; j += kTileThreads)
+                            alpha_batch_mcorner_job(pts[p0 + q + 1], j, edgk, ct, cs, X, memb + mbd,
+                                                    mem + ((qq + 1) & 1) * 2 * ccmax);
+                } else {
+                    __syncthreads();   // member edges written / the previous point's combine is done with mem
+                    if (cornered) {
+                        if (kRef)
+                            for (int j = tid; j < cc; j += kTileThreads) alpha_batch_mcorner_ref_job(Q, j, edgk, ct, cs, X);
+                        else
+                            for (int j = tid; j < cc; j += kTileThreads) alpha_batch_mcorner_job(Q, j, edgk, ct, cs, X, memb, mem);
+                    }
+                    __syncthreads();   // mem of q written
                 }
-                __syncthreads();   // mem of q written
                 int w = 0;
                 if (needed) {
                     SplitLeavesT<kRef> lv;
                     lv.cf[0] = P3; lv.cf[1] = P3; lv.cf[2] = P3; lv.cf[3] = P3; lv.cf[4] = P3;
                     lv.cf[5] = P3 + cc; lv.cf[6] = P3 + 2 * cc;   // (LL, TU1, TU2, G are not read with pre)
-                    lv.corm = kRef ? X : mem;
+                    lv.corm = kRef ? X : memq;
                     lv.cc = cc; lv.ct = ct; lv.cs = cs; lv.mb = lm; lv.nb = ln;
                     lv.sidx[0] = sl[lm]; lv.sidx[1] = sh[lm]; lv.tidx[0] = tl[ln]; lv.tidx[1] = th[ln];
                     lv.ted = edgk; lv.sed = edgk + kTEdgeFields * ct; lv.mbv = lv.sed + kSEdgeFields * cs;

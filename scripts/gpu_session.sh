@@ -10,6 +10,8 @@
 #   bench[=<a>,<b>,..]      python bench.py <a> <b> ..  (commas = spaces)           -> bench_<i>.json / .err
 #   prof=<a>,<b>,..         rocprofv3 --kernel-trace --stats of bench.py <a> <b> .. -> kt_<i>/
 #   py=<script>,<a>,..      python <script> <a> ..                                   -> py_<i>.out / .err
+#   vbench=<v>,<a>,..       bench.py <a> .. on the A/B library nusiprop_amd/libnusi_<v>.so (scripts/build_variant.sh)
+#   vpy=<v>,<script>,<a>,.. python <script> <a> .. on that library                   -> vpy_<i>.out / .err
 set -o pipefail
 TAG=${1:?tag}
 shift
@@ -42,6 +44,14 @@ for STEP in "$@"; do
         > $OUT/kt_$i.log 2>&1 || exit 1 ;;
     py)
       timeout -k 10 600 python $ARGS > $OUT/py_$i.out 2> $OUT/py_$i.err || exit 1 ;;
+    vbench)
+      V=${ARGS%% *}; A=${ARGS#* }; [ "$A" = "$ARGS" ] && A=""
+      NUSIPROP_LIB=$PWD/nusiprop_amd/libnusi_$V.so timeout -k 10 600 python bench.py $A > $OUT/vbench_${i}_$V.json \
+        2> $OUT/vbench_${i}_$V.err || exit 1 ;;
+    vpy)
+      V=${ARGS%% *}; A=${ARGS#* }
+      NUSIPROP_LIB=$PWD/nusiprop_amd/libnusi_$V.so timeout -k 10 600 python $A > $OUT/vpy_${i}_$V.out \
+        2> $OUT/vpy_${i}_$V.err || exit 1 ;;
     *)
       echo "unknown step $STEP" >> $OUT/session.log; exit 2 ;;
   esac
