@@ -151,6 +151,10 @@ public:
         return i < N_ ? E_[i] : 0.0;
     }
 
+    // extension (no reference counterpart): evolve() builds the tables in the reference's own complex-dilogarithm
+    // arithmetic (NUSI_OPT_REFERENCE_ORDER, include/nusi.h); kept by copies
+    void set_reference_order(bool on) { check(nusi_set_option(h_, NUSI_OPT_REFERENCE_ORDER, on ? 1 : 0)); }
+
 private:
     nusi_handle* h_ = nullptr;
     int N_ = 0;

@@ -182,3 +182,13 @@ def test_reference_order_object_api(nusi, oracle_mod):
             L.nusi_destroy(h2)
     _, fla, _, _, _ = _gpu_refo(nusi, [cases.C2A], tables=False)
     assert np.array_equal(outs[0], fla[0]) and np.array_equal(outs[1], fla[0])
+
+
+def test_reference_order_pyprop(nusi):
+    """The drop-in pyprop's extension keyword reference_order=True gives the plan's reference-order fluxes."""
+    kw = dict(cases.C2A)
+    kw.pop("source_model")
+    ev = nusi.pyprop(**dict(kw, phiphi=False), reference_order=True)
+    ev.evolve()
+    _, fla, _, _, _ = _gpu_refo(nusi, [cases.C2A], tables=False)
+    assert np.array_equal(np.asarray(ev.get_flux_fla()), fla[0])
