@@ -321,8 +321,8 @@ NUSI_FN SplitLeaves batch_bracket_leaves(const double* P3, const double* tmp, co
 {
     const int cc = cs * ct;
     SplitLeaves lv;
-    lv.cf[0] = P3; lv.cf[1] = tmp; lv.cf[2] = tmp + cc; lv.cf[3] = tmp + 2 * cc; lv.cf[4] = tmp + 3 * cc;
-    lv.cf[5] = P3 + cc; lv.cf[6] = P3 + 2 * cc;
+    lv.cf[0] = P3; lv.cf[1] = tmp; lv.cf[2] = tmp + kCC; lv.cf[3] = tmp + 2 * kCC; lv.cf[4] = tmp + 3 * kCC;
+    lv.cf[5] = P3 + kCC; lv.cf[6] = P3 + 2 * kCC;
     lv.corm = P3;   // (not read by the brackets)
     lv.cc = cc; lv.ct = ct; lv.cs = cs; lv.mb = lm; lv.nb = ln;
     lv.sidx[0] = s0; lv.sidx[1] = s1; lv.tidx[0] = t0; lv.tidx[1] = t1;
@@ -414,7 +414,7 @@ void k_alpha_batch(GridDev g, const Point* __restrict__ pts, const SplineSet* __
     }
     const bool nonres = P.non_resonant, maj = P.majorana, cornered = nonres && maj;
     const bool needed = valid && (nonres || m == n + 1);
-    constexpr int ccmax = (kAlphaTile + 1) * (kAlphaTile + 1);
+    constexpr int ccmax = kCC;
     double* P3 = sm;                           // [3][cc]
     double* X = P3 + 3 * ccmax;                // [kXFields][cc] | LL TU1 TU2 G [4][cc] + mixed
     double* mem = X + kXFields * ccmax;        // [2][cc] (kBatchPipe: [2][2][cc], by point parity)
@@ -422,7 +422,7 @@ void k_alpha_batch(GridDev g, const Point* __restrict__ pts, const SplineSet* __
     double* membq = edgk + alpha_tile_edge_stride(kAlphaTile + 1, kAlphaTile + 1);   // [kBatchQC][mbd]
     const int mbd = alpha_batch_memb_doubles(cs, ct);
     double* tmp = X;
-    double* mix = X + 4 * cc;
+    double* mix = X + 4 * kCC;
     const int mjobs = ct + cs + kAlphaTile;
     int wsh = 0;
 #pragma unroll 1
@@ -510,7 +510,7 @@ void k_alpha_batch(GridDev g, const Point* __restrict__ pts, const SplineSet* __
                 if (needed) {
                     SplitLeavesT<kRef> lv;
                     lv.cf[0] = P3; lv.cf[1] = P3; lv.cf[2] = P3; lv.cf[3] = P3; lv.cf[4] = P3;
-                    lv.cf[5] = P3 + cc; lv.cf[6] = P3 + 2 * cc;   // (LL, TU1, TU2, G are not read with pre)
+                    lv.cf[5] = P3 + kCC; lv.cf[6] = P3 + 2 * kCC;   // (LL, TU1, TU2, G are not read with pre)
                     lv.corm = kRef ? X : memq;
                     lv.cc = cc; lv.ct = ct; lv.cs = cs; lv.mb = lm; lv.nb = ln;
                     lv.sidx[0] = sl[lm]; lv.sidx[1] = sh[lm]; lv.tidx[0] = tl[ln]; lv.tidx[1] = th[ln];

@@ -911,6 +911,9 @@ NUSI_FN double alpha_phiphi_scale(const Point& P, double uk, const PPTerm& X)
 // (L, Drr, Dri persist for every mass state through the batch loop; LL, TU1, TU2, G and the mixed logs
 // only while the batch's shared brackets are formed), so each field has its own base pointer.  kRefA
 // (NUSI_OPT_REFERENCE_ORDER): A is a corner field of its own, corm[2 cc + o] (alpha_batch_mcorner_ref_job).
+// The big-batch kernel's corner blocks (P3, X, mem) keep their fields kCC doubles apart, a compile-time stride, so that
+// every field of a corner is one LDS load at an immediate offset from the same address.
+constexpr int kCC = (kAlphaTile + 1) * (kAlphaTile + 1);
 template <bool kRefA = false>
 struct SplitLeavesT {
     const double* cf[kCornerShared];   // L LL TU1 TU2 G Drr Dri, each [cc]
@@ -923,9 +926,9 @@ struct SplitLeavesT {
         const int o = sidx[si] * ct + tidx[ti];
         const int a = sidx[si], b = tidx[ti];
         // A = arg(S - 1 + i gr) + arg(c + i gr) - pi, the expression of alpha_member_corner
-        const double A = kRefA ? corm[2 * cc + o] : (marg[2 * ct + a] + marg[b]) + (marg[2 * ct + cs + a] + marg[ct + b] - 1.0) * kPi;
+        const double A = kRefA ? corm[2 * kCC + o] : (marg[2 * ct + a] + marg[b]) + (marg[2 * ct + cs + a] + marg[ct + b] - 1.0) * kPi;
         return AlphaCorner{cf[0][o], cf[1][o], cf[2][o], cf[3][o], cf[4][o], cf[5][o], cf[6][o],
-                           corm[o], corm[cc + o], A};
+                           corm[o], corm[kCC + o], A};
     }
     NUSI_FN AlphaTEdge tedge(int ti, double) const
     {
@@ -951,8 +954,8 @@ NUSI_FN void alpha_batch_corner_job(int j, const double* edgk, int ct, int cs, d
     const int si = j / ct, ti = j - si * ct;
     AlphaCorner c;
     alpha_corner_shared(edgk[kTEdgeFields * ct + kSEdgeVal * cs + si], edgk[kTEdgeVal * ct + ti], c);
-    per[j] = c.L; per[cc + j] = c.Drr; per[2 * cc + j] = c.Dri;
-    tmp[j] = c.LL; tmp[cc + j] = c.TU1; tmp[2 * cc + j] = c.TU2; tmp[3 * cc + j] = c.G;
+    per[j] = c.L; per[kCC + j] = c.Drr; per[2 * kCC + j] = c.Dri;
+    tmp[j] = c.LL; tmp[kCC + j] = c.TU1; tmp[2 * kCC + j] = c.TU2; tmp[3 * kCC + j] = c.G;
 }
 // The big-batch kernel's member blocks, per (point, mass state):
 //   X    [10][cc]  shared across the batch: the Taylor coefficients of Li2 about x0 = (1+S+t)/(2+t) per corner
@@ -969,10 +972,10 @@ NUSI_FN void alpha_batch_xshared_job(int j, const double* edgk, int ct, int cs, 
     MemberShared M;
     alpha_member_shared(edgk[kTEdgeFields * ct + kSEdgeVal * cs + si], edgk[kTEdgeVal * ct + ti], M);
 #pragma unroll
-    for (int n = 0; n <= kLi2AxisTerms; ++n) X[n * cc + j] = M.T.c[n];
-    X[(kLi2AxisTerms + 1) * cc + j] = M.T.r;
-    X[(kLi2AxisTerms + 2) * cc + j] = M.T.b0;
-    X[(kLi2AxisTerms + 3) * cc + j] = M.m;
+    for (int n = 0; n <= kLi2AxisTerms; ++n) X[n * kCC + j] = M.T.c[n];
+    X[(kLi2AxisTerms + 1) * kCC + j] = M.T.r;
+    X[(kLi2AxisTerms + 2) * kCC + j] = M.T.b0;
+    X[(kLi2AxisTerms + 3) * kCC + j] = M.m;
 }
 // job in [0, ct + cs + kAlphaTile): the member edge / m-bin leaves of point P for mass state k
 NUSI_FN void alpha_batch_medge_job(const Point& P, int k, int job, const double* tE, int ct, const double* sE, int cs,
@@ -1085,16 +1088,16 @@ NUSI_FN void alpha_batch_mcorner_job(const Point& P, int j, const double* edgk, 
     const int si = j / ct, ti = j - si * ct;
     MemberShared M;
 #pragma unroll
-    for (int n = 0; n <= kLi2AxisTerms; ++n) M.T.c[n] = X[n * cc + j];
-    M.T.r = X[(kLi2AxisTerms + 1) * cc + j];
-    M.T.b0 = X[(kLi2AxisTerms + 2) * cc + j];
-    M.m = X[(kLi2AxisTerms + 3) * cc + j];
+    for (int n = 0; n <= kLi2AxisTerms; ++n) M.T.c[n] = X[n * kCC + j];
+    M.T.r = X[(kLi2AxisTerms + 1) * kCC + j];
+    M.T.b0 = X[(kLi2AxisTerms + 2) * kCC + j];
+    M.m = X[(kLi2AxisTerms + 3) * kCC + j];
     const double* ext = memb + ct + 2 * cs + kAlphaTile;
     const MemberTEdge e{ext[ti], ext[ct + ti], ext[2 * ct + ti], ext[3 * ct + ti]};
     double Dcr, Dci, A;
     alpha_member_corner(M, edgk[kTEdgeFields * ct + kSEdgeVal * cs + si], edgk[kTEdgeVal * ct + ti], P.a_gr, e,
                         ext[4 * ct + si], ext[4 * ct + cs + si], Dcr, Dci, A);
-    mem[j] = Dcr; mem[cc + j] = Dci;   // (A: SplitLeaves forms it from the edge arguments)
+    mem[j] = Dcr; mem[kCC + j] = Dci;   // (A: SplitLeaves forms it from the edge arguments)
 }
 // NUSI_OPT_REFERENCE_ORDER: member corner leaves of corner j for point P in the reference's operation order
 // (alpha_member_ref) -> mem[0..2][cc] (Dcr, Dci, A); no batch-shared coefficients
@@ -1104,7 +1107,7 @@ NUSI_FN void alpha_batch_mcorner_ref_job(const Point& P, int j, const double* ed
     const int si = j / ct, ti = j - si * ct;
     double Dcr, Dci, A;
     alpha_member_ref(edgk[kTEdgeFields * ct + kSEdgeVal * cs + si], edgk[kTEdgeVal * ct + ti], P.a_gr, Dcr, Dci, A);
-    mem[j] = Dcr; mem[cc + j] = Dci; mem[2 * cc + j] = A;
+    mem[j] = Dcr; mem[kCC + j] = Dci; mem[2 * kCC + j] = A;
 }
 // xlog / ylog leaves of mass state k into xl [cs][kAlphaTile], yl [kAlphaTile][ct] (alpha_tile_mixed_job's jobs)
 NUSI_FN void alpha_batch_mixed_job(int j, const double* edgk, int ct, int cs, const int* tl, const int* th,
