@@ -120,10 +120,10 @@ def test_shift_reuse_rounded_mphi_goes_direct(nusi, oracle_mod):
     built directly, bit-exact, while its exact lattice partner still shares the base."""
     from nusiprop_amd import _lib
     base = dict(cases.C2B_100)
-    exact = _lattice_points(base, (0, 3), (0.1,))
+    exact = _lattice_points(base, (0, 3), (0.03,))
     r = 10 ** ((base["lEmax"] - base["lEmin"]) / base["N_bins_E"])
     m6 = 6e5 * r ** (-6 / 2)
-    rounded = dict(base, mphi=float("%.7g" % m6), g=0.1)
+    rounded = dict(base, mphi=float("%.7g" % m6), g=0.03)
     assert rounded["mphi"] != m6 and abs(rounded["mphi"] / m6 - 1) < 1e-6
     pts = exact + [rounded]
     plan = nusi.Plan(base["N_bins_E"], base["lEmin"], base["lEmax"], base["zmax"], max_points=len(pts))
