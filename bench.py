@@ -549,11 +549,14 @@ def run(args, world, rank, local, dist, plan, pts, desc, pp_tables):
     # workgroups that read a table: one per point, or one per pair of points sharing a table on the multi-RHS
     # kernel (the pair reads its alpha table once)
     readers = P
-    if casc_kernel == "k_cascade_ws_mrhs":
+    long_grid = Nz - 1 > 48   # step passes (k_cascade_ws_passes, or k_cascade_bs beyond one pass)
+    if casc_kernel in ("k_cascade_ws_mrhs", "k_cascade_bs_pairs"):
         from collections import Counter
         readers = sum((c + 1) // 2 for c in Counter(scan.table_key(p) for p in pts).values())
-    casc_min = scan.cascade_min_bytes_per_point(N, Nz, passes=casc_kernel == "k_cascade_ws_passes") * readers
-    gbs = scan.gamma_batches(pts, args.rhs or 16) if "k_cascade_gb" in casc_kernel else []
+    passes = casc_kernel == "k_cascade_ws_passes" or (casc_kernel == "k_cascade_bs" and long_grid)
+    casc_min = scan.cascade_min_bytes_per_point(N, Nz, passes=passes) * readers
+    gamma = "k_cascade_gb" in casc_kernel or "k_cascade_bs_gamma" in casc_kernel
+    gbs = scan.gamma_batches(pts, args.rhs or 16) if gamma else []
     if gbs:   # the gamma batch: each workgroup reads its table once per pass; the points write their fluxes
         readers = len(gbs)
         casc_min = scan.cascade_gb_bytes_per_batch(N, Nz) * len(gbs) + 8 * 6 * N * P
@@ -598,7 +601,7 @@ def run(args, world, rank, local, dist, plan, pts, desc, pp_tables):
         "invalid_outputs": bad,
         "phiphi_lookups_out_of_range": oob,
     }
-    if "ws" in casc_kernel or gbs:   # the push on the matrix cores
+    if "ws" in casc_kernel or "bs" in casc_kernel or gbs:   # the push on the matrix cores
         mf = scan.cascade_gb_flops_per_batch(N, Nz) * len(gbs) if gbs else scan.cascade_mfma_flops_per_point(N, Nz) * P
         out["roofline_cascade"]["mfma"] = {"flops_per_launch": mf, "achieved": mf / casc_s / 1e12,
                                            "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",

@@ -222,7 +222,9 @@ int nusi_plan_set_cascade(nusi_plan *plan, int kind);
  *                          wsp: every wave meets once per wavefront stage),
  *                          2 = the block-synchronous kernel k_cascade_bs
  *                          (twice per block of four stages; the same
- *                          operations on the same operands). */
+ *                          operations on the same operands).  Automatic
+ *                          takes k_cascade_bs on grids beyond 48 redshift
+ *                          steps (C3), the per-stage kernels otherwise. */
 #define NUSI_OPT_CASCADE_SYNC 7
 int nusi_plan_set_option(nusi_plan *plan, int option, int value);
 /* per-point NUSI_WARN_* bits of the last call */

@@ -1895,29 +1895,31 @@ void k_cascade_gb(GridDev g, const Point* __restrict__ pts, const int* __restric
 //   phase A: the waves holding the four rows block q publishes push block q into those tiles and publish
 //            them (AX); the chain solves stage 4q (block q-1's rows);
 //   phase B: the chain solves stages 4q+1 .. 4q+3 back to back (block q's rows, its own four diagonal
-//            columns as before); the other push tiles add block q (their rows are published later); the
-//            record wave forms the records and sources of block q + 1 (4 stages x NJ steps at once).
-// The chain is ONE wave: lane (point p, jp) runs the step slots j = SPL jp .. SPL jp + SPL - 1 (interleaved,
-// independent solves); slot j takes F[:, b] from slot j-1's solve of the previous stage -- the lane's own
-// previous slot in a register, or, for its first slot, the previous lane's last slot by a DPP wave shift, or
-// (first step of a pass > 0) the previous pass' last step through a global FIFO prefetched a block ahead.
+//            columns as before); the other push tiles add block q (their rows are published later).
+// The record wave forms block q + 1's records over both phases (a third in A, where the chain solves one stage,
+// the rest in B) and stages the DSNB sources; the chain forms the power-law sources itself.
+// The chain is CW waves of PPW = P / CW whole points: lane (point p, jp) runs the step slots j = SPL jp .. SPL jp +
+// SPL - 1 (interleaved, independent solves); slot j takes F[:, b] from slot j-1's solve of the previous stage -- the
+// lane's own previous slot in a register, or, for its first slot, the previous lane's last slot by a DPP wave shift,
+// or (first step of a pass > 0) the previous pass' last step through a global FIFO prefetched a block ahead.
 // The A operands of block q + 2 are loaded while block q is pushed (two register buffers, the block loop
 // unrolled by two), so the publishing tiles never wait for HBM.
 // Columns: the NC = NJ P right-hand sides (point p, step j) at c = j P + p; a push tile is 16 columns (one
-// step of 16 points, or 16 steps of one point), so one template covers
-//   <48, 1, 1, 4>  one point per workgroup (C4; k_cascade_ws<48, 1>'s shape)
-//   <48, 2, 2, 2>  two points sharing a table (k_cascade_ws<48, 2>)
-//   <6, 16, 2, 2>  the gamma batch, 16 power-law points of a table (k_cascade_gb)
-//   <16, 1, 1, 8>  step passes on long grids (C3; k_cascade_wsp)
+// step of 16 points, or 16 steps of one point), so one template <NJ, P, SPL, RT, CW> covers
+//   <48, 1, 1, 4, 1>  one point per workgroup (C4; k_cascade_ws<48, 1>'s shape)
+//   <48, 2, 1, 2, 2>  two points sharing a table (k_cascade_ws<48, 2>), a chain wave per point
+//   <6, 16, 1, 2, 2>  the gamma batch, 16 power-law points of a table (k_cascade_gb), 8 per chain wave
+//   <16, 1, 1, 8, 1>  step passes on long grids (C3; k_cascade_wsp)
 // and the same points get the same fluxes as from those kernels (the MFMA sums each element's four columns in
-// its own order whichever column it is).  Waves: push waves of 16 RT rows, the chain wave, the record wave.
+// its own order whichever column it is).  Waves: push waves of 16 RT rows, the chain waves, the record wave.
 // ---------------------------------------------------------------------------
-template <int NJ, int P, int SPL, int RT>
+template <int NJ, int P, int SPL, int RT, int CW>
 struct BsCfg {
     static constexpr int LPP = NJ / SPL;   // chain lanes per point
+    static constexpr int PPW = P / CW;     // points per chain wave
     static constexpr int NC = NJ * P;      // right-hand columns
     static constexpr int NB = NC / 16;     // push column tiles
-    static_assert(NJ % SPL == 0 && NC % 16 == 0 && LPP * P <= 64, "one chain wave, whole column tiles");
+    static_assert(NJ % SPL == 0 && P % CW == 0 && NC % 16 == 0 && LPP * PPW <= 64, "whole points per chain wave, whole column tiles");
 };
 
 // record fields of the block-synchronous kernel: PR_* without PR_SRC (the sources have a block of their own), so
@@ -1926,28 +1928,28 @@ enum { BR_RZ0, BR_RZ1, BR_RZ2, BR_L10, BR_L20, BR_L21, BR_U01, BR_U02, BR_U12, B
        kBsFields };
 static_assert(PR_L10 - 1 == BR_L10 && PR_RU22 - 1 == BR_RU22 && kPreFields - 1 == BR_PERM, "record_phase2's fields, shifted");
 
-template <int NJ, int P, int SPL, int RT>
+template <int NJ, int P, int SPL, int RT, int CW>
 __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4, 4)))
 void k_cascade_bs(GridDev g, const Point* __restrict__ pts, const int* __restrict__ gidx, const int2* __restrict__ grp,
                   TablesDev t, double* __restrict__ fh, double* __restrict__ flux, double* __restrict__ flux_fla)
 {
     extern __shared__ __attribute__((aligned(16))) double lds[];
-    using Cfg = BsCfg<NJ, P, SPL, RT>;
-    constexpr int LPP = Cfg::LPP, NC = Cfg::NC, NB = Cfg::NB, NF = kBsFields, S4 = 4 * NJ, NQ = 12 * P;
+    using Cfg = BsCfg<NJ, P, SPL, RT, CW>;
+    constexpr int LPP = Cfg::LPP, PPW = Cfg::PPW, NC = Cfg::NC, NB = Cfg::NB, NF = kBsFields, S4 = 4 * NJ, NQ = 12 * P;
     const int N = g.N, Nz = g.Nz, T = g.T, nst = Nz - 1;
     const int tid = threadIdx.x, nthr = blockDim.x, lane = tid & 63, wave = tid >> 6, nw = nthr >> 6;
-    const int chw = nw - 2, recw = nw - 1;   // push waves 0 .. nw-3, the chain wave, the record wave
+    const int chw = nw - 1 - CW, recw = nw - 1;   // push waves 0 .. chw-1, the CW chain waves, the record wave
     const int2 gr = grp ? grp[blockIdx.x] : make_int2((int)blockIdx.x, 1);
     const int R = gr.y;                                   // points of this workgroup (<= P), one table
     auto pidx = [&](int p) { return gidx ? gidx[gr.x + p] : gr.x + p; };   // (gidx == nullptr: point blockIdx.x)
     const Point& P0 = pts[pidx(0)];
     double* rec = lds;                       // [2][NF][4][NJ]  records of block q in slot q & 1
-    double* srcb = rec + 2 * NF * S4;        // [2][4][NJ][P]   the sources c_i Lum of block q's (stage, step, point)
+    double* srcb = rec + 2 * NF * S4;        // [2][4][NJ][P]   block q's DSNB sources c_i Lum (stage, step, point)
     double* Tp = srcb + 8 * NC;              // [8][NC]         T_j of each column by stage
     double* AX = Tp + 8 * NC;                // [2][4][NC]      rows published by block q (parity q & 1)
     double* fqb = AX + 8 * NC;               // [2][4][3][P]    the previous pass' last step, F[:, N-1-sg], block q
-    double* pinf = fqb + 2 * NQ;             // [4][P]          per point: a3, rs, power law (1) / DSNB (0), index
-    double* rdE = pinf + 4 * P;              // [N]
+    double* pinf = fqb + 2 * NQ;             // [13][P]         per point: a3, rs, power law (1) / DSNB (0), index, U2[9]
+    double* rdE = pinf + 13 * P;             // [N]
     double* pw = rdE + N;                    // [P][T + 2]      each power-law point's pw on table edge e
     double* sGt = pw + (size_t)P * (T + 2);
     double* sAt = sGt + T;
@@ -1990,6 +1992,8 @@ void k_cascade_bs(GridDev g, const Point* __restrict__ pts, const int* __restric
             pinf[P + p] = f.rs;
             pinf[2 * P + p] = p < R && pts[pid].source == NUSI_SOURCE_POWER_LAW ? 1.0 : 0.0;
             pinf[3 * P + p] = (double)pid;
+#pragma unroll
+            for (int f = 0; f < 9; ++f) pinf[(4 + f) * P + p] = pts[pid].U2[f];   // the finalise's, off the chain's global path
         }
         for (int q = tid; q < P * (T + 1); q += nthr) {   // cascade_aux_init's pw[e] of every power-law point
             const int p = q / (T + 1), e = 1 + q - p * (T + 1);
@@ -2012,17 +2016,24 @@ void k_cascade_bs(GridDev g, const Point* __restrict__ pts, const int* __restric
         c0 = T - 1 - jb;                       // the table column of its stage 0
         nblk = (Ts + 3) / 4;
     };
-    if (wave == chw) {
-        // ---- chain: lane (cp, cjp) solves the slots j = SPL cjp + k of point cp
-        const int cp = lane / LPP, cjp = lane - LPP * (lane / LPP);
-        const bool clane = lane < P * LPP && cp < R;
+    if (wave >= chw && wave < recw) {
+        // ---- chain wave cw: lane (cp, cjp) solves the slots j = SPL cjp + k of point cp (PPW points per wave, so
+        // a point's steps never cross waves); the power-law sources are formed here (powerlaw_src_h), the DSNB
+        // ones read from srcb
+        const int cw = wave - chw;
+        const int cp = cw * PPW + lane / LPP, cjp = lane - LPP * (lane / LPP);
+        const bool clane = lane < PPW * LPP && cp < R;
         const double u0 = P0.u[0], u1 = P0.u[1], u2 = P0.u[2];
+        const int cpc = cp < P ? cp : P - 1;
+        const double* const cpw = pw + (size_t)cpc * (T + 2);
 #pragma unroll 1
         for (int pass = 0; pass < npass; ++pass) {
             pass_geom(pass);
             const bool last_pass = pass == npass - 1;
-            __syncthreads();   // the previous pass is done with Tp, AX and the records
+            __syncthreads();   // the previous pass is done with Tp, AX and the records (pass 0: the prologue's LDS)
             for (int q = lane; q < 16 * NC; q += 64) Tp[q] = 0.0;   // Tp and AX
+            const bool cpl = pinf[2 * P + cpc] != 0.0;
+            const SrcFactors csf{pinf[cpc], pinf[P + cpc]};
             __syncthreads();
             double px0[SPL], px1[SPL], px2[SPL], racc[SPL], Th[SPL][4];
 #pragma unroll
@@ -2069,7 +2080,7 @@ void k_cascade_bs(GridDev g, const Point* __restrict__ pts, const int* __restric
                         const double u01 = Rc[BR_U01 * S4], u02 = Rc[BR_U02 * S4], u12 = Rc[BR_U12 * S4];
                         const double ru00 = Rc[BR_RU00 * S4], ru11 = Rc[BR_RU11 * S4], ru22 = Rc[BR_RU22 * S4];
                         const double sde = Rc[BR_SDE * S4];
-                        const double src = Sb[j * P + cp];
+                        const double src = cpl ? powerlaw_src_h(gl, csf, cpw, Nz - 1 - jb - j, b) : Sb[j * P + cp];
                         const double cj = gl.step_c[Nz - 1 - jb - j];
                         double add;
                         if (nonres) {
@@ -2089,7 +2100,7 @@ void k_cascade_bs(GridDev g, const Point* __restrict__ pts, const int* __restric
                         if (j == njp - 1) {   // the pass's last step: the next pass' input, or the output
                             if (last_pass) {   // finalise (nuSIprop.hpp:328-336)
                                 const int cpid = (int)pinf[3 * P + cp];
-                                const Point& Q = pts[cpid];
+                                const double* U2 = pinf + 4 * P + cp;
                                 const double dE = gl.Emax[b] - gl.Emin[b];
                                 const double g0 = x0 / dE, g1 = x1 / dE, g2 = x2 / dE;
                                 double* fo = flux + (size_t)cpid * 3 * N;
@@ -2098,7 +2109,7 @@ void k_cascade_bs(GridDev g, const Point* __restrict__ pts, const int* __restric
                                 fo[N + b] = g1;
                                 fo[2 * N + b] = g2;
                                 for (int f = 0; f < 3; ++f)
-                                    fl[f * N + b] = Q.U2[3 * f + 0] * g0 + Q.U2[3 * f + 1] * g1 + Q.U2[3 * f + 2] * g2;
+                                    fl[f * N + b] = U2[(3 * f + 0) * P] * g0 + U2[(3 * f + 1) * P] * g1 + U2[(3 * f + 2) * P] * g2;
                             } else {
                                 fhw[((size_t)0 * N + b) * P + cp] = x0;
                                 fhw[((size_t)1 * N + b) * P + cp] = x1;
@@ -2128,11 +2139,13 @@ void k_cascade_bs(GridDev g, const Point* __restrict__ pts, const int* __restric
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the FIFO stores land before the next pass reads them
         }
     } else if (wave == recw) {
-        // ---- records and sources: block 0 (and the FIFO of blocks 0, 1) before the blocks; in block q the records of
-        // block q + 1 (phase A: block q + 1's slot was last read in phase B of block q - 1) and its sources (phase B);
-        // the FIFO values of block q + 2 are loaded in phase A of block q and stored in phase A of block q + 1
-        auto records = [&](int qb) {
-            for (int e = lane; e < S4; e += 64) {
+        // ---- records and DSNB sources: block 0 (and the FIFO of blocks 0, 1) before the blocks; in block q the
+        // records of block q + 1 (block q + 1's slot was last read in block q - 1), the first kRecA rounds of 64 in
+        // phase A (where the chain solves one stage), the rest and the DSNB sources in phase B (three stages); the
+        // FIFO values of block q + 2 are loaded in phase A of block q and stored in phase A of block q + 1
+        constexpr int kRecRounds = (S4 + 63) / 64, kRecA = (kRecRounds + 2) / 3, kRecSplit = 64 * kRecA < S4 ? 64 * kRecA : S4;
+        auto records = [&](int qb, int e0, int e1) {
+            for (int e = e0 + lane; e < e1; e += 64) {
                 const int sb = e / NJ, jj = e - NJ * (e / NJ), s2 = 4 * qb + sb;
                 const int b = N - 1 - s2 + jj, i = Nz - 1 - jb - jj;
                 if (jj < njp && s2 < Ts && b >= 0 && b < N) {
@@ -2146,15 +2159,14 @@ void k_cascade_bs(GridDev g, const Point* __restrict__ pts, const int* __restric
                 }
             }
         };
-        auto sources = [&](int qb) {
+        bool any_dsnb = false;   // (set after the first barrier: the prologue writes pinf)
+        auto sources = [&](int qb) {   // the DSNB points' (k_source_dsnb's table); the chain forms the power-law ones
+            if (!any_dsnb) return;
             for (int e = lane; e < S4 * P; e += 64) {
                 const int p = e % P, sj = e / P, sb = sj / NJ, jj = sj - NJ * sb, s2 = 4 * qb + sb;
-                const int b = N - 1 - s2 + jj, i = Nz - 1 - jb - jj;
-                if (p < R && jj < njp && s2 < Ts && b >= 0 && b < N)
-                    srcb[(qb & 1) * 4 * NC + e] =
-                        pinf[2 * P + p] != 0.0
-                            ? powerlaw_src_h(gl, SrcFactors{pinf[p], pinf[P + p]}, pw + (size_t)p * (T + 2), i, b)
-                            : t.Src[(size_t)pinf[3 * P + p] * T * nst + src_index(Nz, jb + jj, b)];
+                const int b = N - 1 - s2 + jj;
+                if (p < R && jj < njp && s2 < Ts && b >= 0 && b < N && pinf[2 * P + p] == 0.0)
+                    srcb[(qb & 1) * 4 * NC + e] = t.Src[(size_t)pinf[3 * P + p] * T * nst + src_index(Nz, jb + jj, b)];
             }
         };
         constexpr int FQL = (NQ + 63) / 64;   // FIFO values per lane and block
@@ -2175,7 +2187,9 @@ void k_cascade_bs(GridDev g, const Point* __restrict__ pts, const int* __restric
         for (int pass = 0; pass < npass; ++pass) {
             pass_geom(pass);
             __syncthreads();
-            records(0);
+            any_dsnb = false;
+            for (int p = 0; p < R; ++p) any_dsnb = any_dsnb || pinf[2 * P + p] == 0.0;
+            records(0, 0, S4);
             sources(0);
             double fv[FQL];
             fifo_load(pass, 0, fv);
@@ -2187,11 +2201,14 @@ void k_cascade_bs(GridDev g, const Point* __restrict__ pts, const int* __restric
                 NUSI_BS_STAMP(pass * nblk + q, 0);
                 fifo_store(q + 1, fv);                  // block q + 1's FIFO values (loaded a block ago)
                 fifo_load(pass, q + 2, fv);
-                if (4 * (q + 1) < Ts) records(q + 1);   // phase A
+                if (4 * (q + 1) < Ts) records(q + 1, 0, kRecSplit);   // phase A
                 NUSI_BS_STAMP(pass * nblk + q, 1);
                 __syncthreads();
                 NUSI_BS_STAMP(pass * nblk + q, 2);
-                if (4 * (q + 1) < Ts) sources(q + 1);   // phase B
+                if (4 * (q + 1) < Ts) {                                // phase B
+                    records(q + 1, kRecSplit, S4);
+                    sources(q + 1);
+                }
                 NUSI_BS_STAMP(pass * nblk + q, 3);
                 __syncthreads();
             }
@@ -2382,40 +2399,40 @@ hipError_t launch_cascade_gb(const GridDev& g, const Point* pts, const int* gidx
 
 // the block-synchronous kernel (k_cascade_bs): push waves of 16 RT rows, the chain wave, the record wave
 static int bs_push_waves(const GridDev& g, int RT) { return (g.T - 1 + 16 * RT - 1) / (16 * RT); }
-template <int NJ, int P, int SPL, int RT>
+template <int NJ, int P, int SPL, int RT, int CW>
 static size_t bs_lds(const GridDev& g)
 {
     constexpr int NC = NJ * P;
-    return sizeof(double) * (2 * (size_t)kBsFields * 4 * NJ + 3 * 8 * (size_t)NC + 24 * (size_t)P + 4 * (size_t)P +
+    return sizeof(double) * (2 * (size_t)kBsFields * 4 * NJ + 3 * 8 * (size_t)NC + 24 * (size_t)P + 13 * (size_t)P +
                              3 * (size_t)g.N + (size_t)P * (g.T + 2) + 6 * (size_t)g.T + 4 * (size_t)g.Nz);
 }
-template <int NJ, int P, int SPL, int RT>
+template <int NJ, int P, int SPL, int RT, int CW>
 static bool bs_fits_t(const GridDev& g)
 {
-    return g.T >= 2 && g.Nz >= 2 && bs_push_waves(g, RT) + 2 <= 16 && bs_lds<NJ, P, SPL, RT>(g) <= 160 * 1024;
+    return g.T >= 2 && g.Nz >= 2 && bs_push_waves(g, RT) + CW + 1 <= 16 && bs_lds<NJ, P, SPL, RT, CW>(g) <= 160 * 1024;
 }
-template <int NJ, int P, int SPL, int RT>
+template <int NJ, int P, int SPL, int RT, int CW>
 static void launch_bs_t(const GridDev& g, const Point* pts, const int* gidx, const int2* grp, int nwg, TablesDev t,
                         double* fh, double* flux, double* flux_fla, hipStream_t s)
 {
-    const int nthr = 64 * (bs_push_waves(g, RT) + 2);
-    const size_t lds = bs_lds<NJ, P, SPL, RT>(g);
-    hipLaunchKernelGGL((k_cascade_bs<NJ, P, SPL, RT>), dim3(nwg), dim3(nthr), lds, s, g, pts, gidx, grp, t, fh, flux,
+    const int nthr = 64 * (bs_push_waves(g, RT) + CW + 1);
+    const size_t lds = bs_lds<NJ, P, SPL, RT, CW>(g);
+    hipLaunchKernelGGL((k_cascade_bs<NJ, P, SPL, RT, CW>), dim3(nwg), dim3(nthr), lds, s, g, pts, gidx, grp, t, fh, flux,
                        flux_fla);
 }
-// P = 1: <wf_nj, 1, 1, 4> for one pass of up to 48 steps, else step passes of 48 (rows <= 14 x 64) or of 16 (rows
-// <= 14 x 128); P = 2: <wf_nj or 48, 2, 2, 2>; P = 16 (the gamma batch): <6, 16, 2, 2>
+// P = 1: <wf_nj, 1, 1, 4, 1> for one pass of up to 48 steps, else step passes of 48 (rows <= 14 x 64) or of 16 (rows
+// <= 14 x 128); P = 2: <wf_nj or 48, 2, 1, 2, 2>; P = 16 (the gamma batch): <6, 16, 1, 2, 2>
 int cascade_bs_config(const GridDev& g, int P)
 {
     const int nj = wf_nj(g);
     if (P == 1) {
-        if (nj && bs_fits_t<48, 1, 1, 4>(g)) return nj;
-        if (bs_fits_t<48, 1, 1, 4>(g)) return 48;
-        if (bs_fits_t<16, 1, 1, 8>(g)) return 16 + 1000;   // 128-row push waves
+        if (nj && bs_fits_t<48, 1, 1, 4, 1>(g)) return nj;
+        if (bs_fits_t<48, 1, 1, 4, 1>(g)) return 48;
+        if (bs_fits_t<16, 1, 1, 8, 1>(g)) return 16 + 1000;   // 128-row push waves
         return 0;
     }
-    if (P == 2) return bs_fits_t<48, 2, 2, 2>(g) ? (nj ? nj : 48) : 0;
-    if (P == 16) return bs_fits_t<6, 16, 2, 2>(g) ? 6 : 0;
+    if (P == 2) return bs_fits_t<48, 2, 1, 2, 2>(g) ? (nj ? nj : 48) : 0;
+    if (P == 16) return bs_fits_t<6, 16, 1, 2, 2>(g) ? 6 : 0;
     return 0;
 }
 size_t cascade_bs_scratch_doubles(const GridDev& g, int P) { return (size_t)3 * g.N * P; }
@@ -2428,21 +2445,21 @@ hipError_t launch_cascade_bs(const GridDev& g, const Point* pts, int P, const in
     if (P == 1) {
         t_cascade_kernel = "k_cascade_bs";
         switch (c) {
-        case 16: launch_bs_t<16, 1, 1, 4>(g, pts, gidx, grp, nwg, t, fh, flux, flux_fla, s); break;
-        case 32: launch_bs_t<32, 1, 1, 4>(g, pts, gidx, grp, nwg, t, fh, flux, flux_fla, s); break;
-        case 48: launch_bs_t<48, 1, 1, 4>(g, pts, gidx, grp, nwg, t, fh, flux, flux_fla, s); break;
-        default: launch_bs_t<16, 1, 1, 8>(g, pts, gidx, grp, nwg, t, fh, flux, flux_fla, s); break;
+        case 16: launch_bs_t<16, 1, 1, 4, 1>(g, pts, gidx, grp, nwg, t, fh, flux, flux_fla, s); break;
+        case 32: launch_bs_t<32, 1, 1, 4, 1>(g, pts, gidx, grp, nwg, t, fh, flux, flux_fla, s); break;
+        case 48: launch_bs_t<48, 1, 1, 4, 1>(g, pts, gidx, grp, nwg, t, fh, flux, flux_fla, s); break;
+        default: launch_bs_t<16, 1, 1, 8, 1>(g, pts, gidx, grp, nwg, t, fh, flux, flux_fla, s); break;
         }
     } else if (P == 2) {
         t_cascade_kernel = "k_cascade_bs_pairs";
         switch (c) {
-        case 16: launch_bs_t<16, 2, 2, 2>(g, pts, gidx, grp, nwg, t, fh, flux, flux_fla, s); break;
-        case 32: launch_bs_t<32, 2, 2, 2>(g, pts, gidx, grp, nwg, t, fh, flux, flux_fla, s); break;
-        default: launch_bs_t<48, 2, 2, 2>(g, pts, gidx, grp, nwg, t, fh, flux, flux_fla, s); break;
+        case 16: launch_bs_t<16, 2, 1, 2, 2>(g, pts, gidx, grp, nwg, t, fh, flux, flux_fla, s); break;
+        case 32: launch_bs_t<32, 2, 1, 2, 2>(g, pts, gidx, grp, nwg, t, fh, flux, flux_fla, s); break;
+        default: launch_bs_t<48, 2, 1, 2, 2>(g, pts, gidx, grp, nwg, t, fh, flux, flux_fla, s); break;
         }
     } else {
         t_cascade_kernel = "k_cascade_bs_gamma";
-        launch_bs_t<6, 16, 2, 2>(g, pts, gidx, grp, nwg, t, fh, flux, flux_fla, s);
+        launch_bs_t<6, 16, 1, 2, 2>(g, pts, gidx, grp, nwg, t, fh, flux, flux_fla, s);
     }
     return hipGetLastError();
 }

@@ -22,7 +22,7 @@ def main():
     if wl == "c4":
         pts = scan.c4_points()
     elif wl == "c3":
-        pts = [dict(scan.BASE, mphi=1e5, g=0.05, N_bins_E=1200, lEmin=10.0, lEmax=17.0)] * 256
+        pts = [dict(scan.BASE, mphi=1e5, g=0.05, si=2.5, N_bins_E=1200, lEmin=10.0, lEmax=17.0)] * 256
     else:
         pts = scan.c5_points()[:4096]
     p0 = pts[0]

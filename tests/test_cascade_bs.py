@@ -116,3 +116,34 @@ def test_bs_step_passes(nusi, oracle_mod, N, lEmin):
         assert old[3][1] == "k_cascade_ws_passes"
         assert np.array_equal(one[1], old[1]), max(cases.rel_err(one[1][k], old[1][k]) for k in range(len(pts)))
     assert max(cases.rel_err(one[1][k], old[1][k]) for k in range(len(pts))) <= FLUX_RTOL
+
+
+def test_bs_c3_gamma_block(nusi, oracle_mod, ref_tables):
+    """A 16-gamma block on the C3 grid (N_E = 1200, lE 10 -> 17, N_z - 1 = 134 steps, phi-phi on at the
+    reference's table geometry; nuSIprop.hpp:257-315): one table, the gamma batch in step passes of 6 with the F
+    FIFO between passes (k_cascade_bs_gamma, the automatic choice there), every point against the oracle's
+    cascade on the block's table (bit-exact to the oracle's own, test_phiphi.py::test_c3_n1200_phiphi) to
+    FLUX_RTOL, and against the same points one per workgroup on k_cascade_wsp."""
+    from nusiprop_amd import _lib
+    from tests.test_phiphi import C3
+    at, atd, a, ad = ref_tables
+    blk = [dict(C3, si=2.0 + 0.06 * k, norm=1.0 + 0.1 * k) for k in range(16)]
+    res = {}
+    for sync, rhs in ((0, 0), (1, 1)):
+        p = nusi.Plan(C3["N_bins_E"], C3["lEmin"], C3["lEmax"], C3["zmax"], max_points=16)
+        p.load_phiphi(at, a)
+        p.set_option(_lib.OPT_CASCADE_SYNC, sync)
+        p.set_option(_lib.OPT_CASCADE_RHS, rhs)
+        flux, fla = p.evolve(blk)
+        assert all(w & 8 == 0 for w in p.warnings(16))
+        res[sync] = (flux, fla, p.kernels()[1], p.tables(0))
+        p.close()
+    assert res[0][2] == "k_cascade_bs_gamma" and res[1][2] == "k_cascade_ws_passes"
+    G, aT, A = res[0][3]
+    for k, kw in enumerate(blk):
+        ok = oracle_mod.Oracle(**cases.oracle_kwargs(kw))
+        ok.prepare()
+        f_ref, fla_ref = ok.cascade(G, aT, nusi.unpack_alpha(A, ok.T))
+        assert cases.rel_err(res[0][0][k], f_ref) <= FLUX_RTOL, k
+        assert cases.rel_err(res[0][1][k], fla_ref) <= FLUX_RTOL, k
+        assert cases.rel_err(res[0][1][k], res[1][1][k]) <= FLUX_RTOL, k

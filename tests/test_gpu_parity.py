@@ -390,7 +390,7 @@ def test_cascade_step_passes_resonant_only(nusi, oracle_mod, N):
 def test_plan_kernels_names(nusi):
     """nusi_plan_kernels reports what the last call launched: the batch alpha kernel, and per grid and
     cascade kind the one-pass warp-specialised kernel, its multi-RHS form (gamma pairs sharing a table),
-    the step-pass kernel (N_z - 1 > 48) or the bit-exact wavefront (AUTO)."""
+    the block-synchronous kernel in step passes (N_z - 1 > 48) or the bit-exact wavefront (AUTO)."""
     from nusiprop_amd import _lib
     def run(N, lEmin, pts_kw, kind):
         pts = [dict(cases.C2B_100, N_bins_E=N, lEmin=lEmin, **kw) for kw in pts_kw]
@@ -405,7 +405,7 @@ def test_plan_kernels_names(nusi):
         assert run(100, 12.0, two, kind) == ("k_alpha_batch", "k_cascade_ws")
         assert run(100, 12.0, [dict(mphi=6e5, g=0.01, si=s) for s in (2.0, 2.5)], kind)[1] == "k_cascade_ws_mrhs"
         assert run(100, 12.0, [dict(mphi=6e5, g=0.01, si=s) for s in (2.0, 2.5, 2.7)], kind)[1] == "k_cascade_gb"
-        assert run(700, 12.0, two, kind)[1] == "k_cascade_ws_passes"
+        assert run(700, 12.0, two, kind)[1] == "k_cascade_bs"   # beyond 48 steps: the block-synchronous kernel
         assert run(100, 12.0, [dict(mphi=6e5, g=0.01, source_model=0, non_resonant=False)], kind)[1] == "k_cascade_ws"
     assert run(100, 12.0, two, _lib.CASCADE_WAVEFRONT)[1] == "k_cascade_wf"
     assert run(700, 12.0, two, _lib.CASCADE_WAVEFRONT)[1] == "k_cascade_reg"
