@@ -1898,10 +1898,10 @@ void k_cascade_gb(GridDev g, const Point* __restrict__ pts, const int* __restric
 //            columns as before); the other push tiles add block q (their rows are published later).
 // The record wave forms block q + 1's records over both phases (a third in A, where the chain solves one stage,
 // the rest in B) and stages the DSNB sources; the chain forms the power-law sources itself.
-// The chain is CW waves of PPW = P / CW whole points: lane (point p, jp) runs the step slots j = SPL jp .. SPL jp +
-// SPL - 1 (interleaved, independent solves); slot j takes F[:, b] from slot j-1's solve of the previous stage -- the
-// lane's own previous slot in a register, or, for its first slot, the previous lane's last slot by a DPP wave shift,
-// or (first step of a pass > 0) the previous pass' last step through a global FIFO prefetched a block ahead.
+// The chain is CW waves of PPW = P / CW whole points: lane (point p, j) runs step slot j (SPL = 1); slot j takes
+// F[:, b] from slot j-1's solve of the previous stage by a DPP wave shift, or (first step of a pass > 0) the previous
+// pass' last step through a global FIFO prefetched a block ahead.  Each stage's loads are issued a stage ahead of
+// its solve, and the last pass' finalise (three divisions and six stores per bin) runs on the record wave.
 // The A operands of block q + 2 are loaded while block q is pushed (two register buffers, the block loop
 // unrolled by two), so the publishing tiles never wait for HBM.
 // Columns: the NC = NJ P right-hand sides (point p, step j) at c = j P + p; a push tile is 16 columns (one
@@ -1913,13 +1913,16 @@ void k_cascade_gb(GridDev g, const Point* __restrict__ pts, const int* __restric
 // and the same points get the same fluxes as from those kernels (the MFMA sums each element's four columns in
 // its own order whichever column it is).  Waves: push waves of 16 RT rows, the chain waves, the record wave.
 // ---------------------------------------------------------------------------
+#ifndef NUSI_BS_PIPE   // A/B: k_cascade_bs's chain issues stage d + 1's loads before stage d's solve (two stages'
+#define NUSI_BS_PIPE 0  // operands live: spills at the 128-VGPR budget)
+#endif
 template <int NJ, int P, int SPL, int RT, int CW>
 struct BsCfg {
     static constexpr int LPP = NJ / SPL;   // chain lanes per point
     static constexpr int PPW = P / CW;     // points per chain wave
     static constexpr int NC = NJ * P;      // right-hand columns
     static constexpr int NB = NC / 16;     // push column tiles
-    static_assert(NJ % SPL == 0 && P % CW == 0 && NC % 16 == 0 && LPP * PPW <= 64, "whole points per chain wave, whole column tiles");
+    static_assert(SPL == 1 && P % CW == 0 && NC % 16 == 0 && LPP * PPW <= 64, "a step slot per chain lane, whole points per chain wave, whole column tiles");
 };
 
 // record fields of the block-synchronous kernel: PR_* without PR_SRC (the sources have a block of their own), so
@@ -1948,7 +1951,8 @@ void k_cascade_bs(GridDev g, const Point* __restrict__ pts, const int* __restric
     double* Tp = srcb + 8 * NC;              // [8][NC]         T_j of each column by stage
     double* AX = Tp + 8 * NC;                // [2][4][NC]      rows published by block q (parity q & 1)
     double* fqb = AX + 8 * NC;               // [2][4][3][P]    the previous pass' last step, F[:, N-1-sg], block q
-    double* pinf = fqb + 2 * NQ;             // [13][P]         per point: a3, rs, power law (1) / DSNB (0), index, U2[9]
+    double* fin = fqb + 2 * NQ;              // [2][4][3][P]    the last pass' output F[:, b] of block q's stages (to finalise)
+    double* pinf = fin + 2 * NQ;             // [13][P]         per point: a3, rs, power law (1) / DSNB (0), index, U2[9]
     double* rdE = pinf + 13 * P;             // [N]
     double* pw = rdE + N;                    // [P][T + 2]      each power-law point's pw on table edge e
     double* sGt = pw + (size_t)P * (T + 2);
@@ -2017,15 +2021,23 @@ void k_cascade_bs(GridDev g, const Point* __restrict__ pts, const int* __restric
         nblk = (Ts + 3) / 4;
     };
     if (wave >= chw && wave < recw) {
-        // ---- chain wave cw: lane (cp, cjp) solves the slots j = SPL cjp + k of point cp (PPW points per wave, so
-        // a point's steps never cross waves); the power-law sources are formed here (powerlaw_src_h), the DSNB
-        // ones read from srcb
+        // ---- chain wave cw: lane (cp, cjp) solves step slot j = cjp of point cp (PPW points per wave, so a point's
+        // steps never cross waves).  A stage is split into its loads (records, source operands, published row,
+        // diagonal alphas: none depends on the previous stage's solve) and its solve, and the loads of stage d + 1
+        // are issued before the solve of stage d, so one LDS latency per stage is hidden behind the dependent
+        // solve.  The power-law sources are formed here (powerlaw_src_h), the DSNB ones read from srcb; the
+        // finalise of the last pass goes to the record wave through `fin`
         const int cw = wave - chw;
         const int cp = cw * PPW + lane / LPP, cjp = lane - LPP * (lane / LPP);
         const bool clane = lane < PPW * LPP && cp < R;
         const double u0 = P0.u[0], u1 = P0.u[1], u2 = P0.u[2];
         const int cpc = cp < P ? cp : P - 1;
         const double* const cpw = pw + (size_t)cpc * (T + 2);
+        struct StageIn {
+            double rz0, rz1, rz2, l10, l20, l21, u01, u02, u12, ru00, ru11, ru22, sde, src, cj, ab, sd[4], fq0, fq1, fq2;
+            double ss, dEb1;   // the resonant-only running sum's step_s and dE of the bin above
+            int pmb;
+        };
 #pragma unroll 1
         for (int pass = 0; pass < npass; ++pass) {
             pass_geom(pass);
@@ -2035,104 +2047,106 @@ void k_cascade_bs(GridDev g, const Point* __restrict__ pts, const int* __restric
             const bool cpl = pinf[2 * P + cpc] != 0.0;
             const SrcFactors csf{pinf[cpc], pinf[P + cpc]};
             __syncthreads();
-            double px0[SPL], px1[SPL], px2[SPL], racc[SPL], Th[SPL][4];
+            double px0 = 0.0, px1 = 0.0, px2 = 0.0, racc = 0.0, Th[4] = {0.0, 0.0, 0.0, 0.0};
+            const int j = cjp, i = Nz - 1 - jb - j;
+            const int ic = i < 1 ? 1 : i;   // (lanes past the pass' steps read in range and are masked)
+            // stage sg = 4 q + d of the pass: its loads
+            auto load = [&](int q, int d) {
+                const int sg = 4 * q + d, r = c0 - sg;
+                const int b = N - 1 - sg + j, bc = b < 0 ? 0 : (b > N - 1 ? N - 1 : b);
+                const int rc = r < 0 ? 0 : r;
+                const double* Rc = rec + (size_t)(q & 1) * NF * S4 + d * NJ + j;
+                StageIn in;
+                in.rz0 = Rc[BR_RZ0 * S4]; in.rz1 = Rc[BR_RZ1 * S4]; in.rz2 = Rc[BR_RZ2 * S4];
+                in.pmb = (int)Rc[BR_PERM * S4];
+                in.l10 = Rc[BR_L10 * S4]; in.l20 = Rc[BR_L20 * S4]; in.l21 = Rc[BR_L21 * S4];
+                in.u01 = Rc[BR_U01 * S4]; in.u02 = Rc[BR_U02 * S4]; in.u12 = Rc[BR_U12 * S4];
+                in.ru00 = Rc[BR_RU00 * S4]; in.ru11 = Rc[BR_RU11 * S4]; in.ru22 = Rc[BR_RU22 * S4];
+                in.sde = Rc[BR_SDE * S4];
+                // both sources, selected branch-free (a branch here made the compiler wait for every LDS load)
+                const double spw = powerlaw_src_h(gl, csf, cpw, ic, bc);
+                const double sdn = srcb[(q & 1) * 4 * NC + d * NC + j * P + cpc];
+                in.src = cpl ? spw : sdn;
+                in.cj = gl.step_c[ic];
+                const int qq = (sg - 1) >> 2;   // block whose publication serves stage sg
+                in.ab = AX[((qq & 1) * 4 + (sg - 1 - 4 * qq)) * NC + j * P + cpc];
 #pragma unroll
-            for (int k = 0; k < SPL; ++k) {
-                px0[k] = px1[k] = px2[k] = racc[k] = 0.0;
-#pragma unroll
-                for (int d = 0; d < 4; ++d) Th[k][d] = 0.0;
-            }
-            // stage sg = 4 q + d of the pass
-            auto stage = [&](int q, int d) {
+                for (int kk = 0; kk < 4; ++kk) in.sd[kk] = sdg[kk * T + rc];
+                const double* fq = fqb + (q & 1) * NQ + d * 3 * P + cpc;
+                in.fq0 = fq[0]; in.fq1 = fq[P]; in.fq2 = fq[2 * P];
+                if (!nonres) {
+                    in.ss = gl.step_s[ic];
+                    in.dEb1 = (bc + 1 < N) ? sEmax[bc + 1] - sEmin[bc + 1] : 1.0;
+                } else {
+                    in.ss = in.dEb1 = 0.0;
+                }
+                return in;
+            };
+            // ... and its solve
+            auto solve = [&](int q, int d, const StageIn& in) {
                 const int sg = 4 * q + d;
-                const int r = c0 - sg;
-                double f0[SPL], f1[SPL], f2[SPL];
-                f0[0] = wave_shr1(px0[SPL - 1], 0.0);   // every lane active: the previous lane's last slot
-                f1[0] = wave_shr1(px1[SPL - 1], 0.0);
-                f2[0] = wave_shr1(px2[SPL - 1], 0.0);
+                const int b = N - 1 - sg + j;
+                const int nu = (d == 0) ? 4 : d;   // columns r+1 .. r+nu not yet pushed
+                double f0 = wave_shr1(px0, 0.0), f1 = wave_shr1(px1, 0.0), f2 = wave_shr1(px2, 0.0);   // every lane active
                 if (cjp == 0) {   // the first step: the previous pass' last step (fqb, staged by the record wave), or 0
-                    const double* fq = fqb + (q & 1) * NQ + d * 3 * P + cp;
-                    f0[0] = fq[0];
-                    f1[0] = fq[P];
-                    f2[0] = fq[2 * P];
+                    f0 = in.fq0;
+                    f1 = in.fq1;
+                    f2 = in.fq2;
                 }
+                double Tn = 0.0;
+                if (clane && j < njp && b >= 0 && b < N) {
+                    double add;
+                    if (nonres) {
+                        double sa = in.ab;
 #pragma unroll
-                for (int k = 1; k < SPL; ++k) {
-                    f0[k] = px0[k - 1];
-                    f1[k] = px1[k - 1];
-                    f2[k] = px2[k - 1];
-                }
-                const double* Rb = rec + (size_t)(q & 1) * NF * S4 + d * NJ;
-                const double* Sb = srcb + (q & 1) * 4 * NC + d * NC;
-                const int qq = (sg - 1) >> 2;              // block whose publication serves stage sg
-                const int nu = (d == 0) ? 4 : d;           // columns r+1 .. r+nu not yet pushed
-                const double* Ab = AX + ((qq & 1) * 4 + (sg - 1 - 4 * qq)) * NC;
-#pragma unroll
-                for (int k = 0; k < SPL; ++k) {
-                    const int j = SPL * cjp + k;
-                    const int b = N - 1 - sg + j;
-                    double Tn = 0.0;
-                    if (clane && j < njp && b >= 0 && b < N) {
-                        const double* Rc = Rb + j;
-                        const double rz0 = Rc[BR_RZ0 * S4], rz1 = Rc[BR_RZ1 * S4], rz2 = Rc[BR_RZ2 * S4];
-                        const int pmb = (int)Rc[BR_PERM * S4];
-                        const double l10 = Rc[BR_L10 * S4], l20 = Rc[BR_L20 * S4], l21 = Rc[BR_L21 * S4];
-                        const double u01 = Rc[BR_U01 * S4], u02 = Rc[BR_U02 * S4], u12 = Rc[BR_U12 * S4];
-                        const double ru00 = Rc[BR_RU00 * S4], ru11 = Rc[BR_RU11 * S4], ru22 = Rc[BR_RU22 * S4];
-                        const double sde = Rc[BR_SDE * S4];
-                        const double src = cpl ? powerlaw_src_h(gl, csf, cpw, Nz - 1 - jb - j, b) : Sb[j * P + cp];
-                        const double cj = gl.step_c[Nz - 1 - jb - j];
-                        double add;
-                        if (nonres) {
-                            double sa = Ab[j * P + cp];
-#pragma unroll
-                            for (int kk = 4; kk >= 1; --kk)
-                                if (kk <= nu) sa = fma(sdg[(kk - 1) * T + r], Th[k][kk - 1], sa);
-                            add = cj * sa;
-                        } else {
-                            const double dEb1 = (b + 1 < N) ? sEmax[b + 1] - sEmin[b + 1] : 1.0;
-                            add = resonant_add(racc[k], u0, u1, u2, px0[k], px1[k], px2[k], gl.step_s[Nz - 1 - jb - j],
-                                               sdg[r], dEb1, sde, cj, b == N - 1);
-                        }
-                        double x0, x1, x2;
-                        cascade_solve(f0[k], f1[k], f2[k], add, src, u0, u1, u2, rz0, rz1, rz2, pmb, l10, l20, l21, u01,
-                                      u02, u12, ru00, ru11, ru22, x0, x1, x2);
-                        if (j == njp - 1) {   // the pass's last step: the next pass' input, or the output
-                            if (last_pass) {   // finalise (nuSIprop.hpp:328-336)
-                                const int cpid = (int)pinf[3 * P + cp];
-                                const double* U2 = pinf + 4 * P + cp;
-                                const double dE = gl.Emax[b] - gl.Emin[b];
-                                const double g0 = x0 / dE, g1 = x1 / dE, g2 = x2 / dE;
-                                double* fo = flux + (size_t)cpid * 3 * N;
-                                double* fl = flux_fla + (size_t)cpid * 3 * N;
-                                fo[b] = g0;
-                                fo[N + b] = g1;
-                                fo[2 * N + b] = g2;
-                                for (int f = 0; f < 3; ++f)
-                                    fl[f * N + b] = U2[(3 * f + 0) * P] * g0 + U2[(3 * f + 1) * P] * g1 + U2[(3 * f + 2) * P] * g2;
-                            } else {
-                                fhw[((size_t)0 * N + b) * P + cp] = x0;
-                                fhw[((size_t)1 * N + b) * P + cp] = x1;
-                                fhw[((size_t)2 * N + b) * P + cp] = x2;
-                            }
-                        }
-                        px0[k] = x0; px1[k] = x1; px2[k] = x2;
-                        if (nonres && b > 0) Tn = (u0 * x0 + u1 * x1 + u2 * x2) * sde;
+                        for (int kk = 4; kk >= 1; --kk)
+                            if (kk <= nu) sa = fma(in.sd[kk - 1], Th[kk - 1], sa);
+                        add = in.cj * sa;
+                    } else {
+                        add = resonant_add(racc, u0, u1, u2, px0, px1, px2, in.ss, in.sd[0], in.dEb1, in.sde, in.cj,
+                                           b == N - 1);
                     }
-                    Th[k][3] = Th[k][2]; Th[k][2] = Th[k][1]; Th[k][1] = Th[k][0]; Th[k][0] = Tn;
-                    if (clane && j < njp) Tp[(sg & 7) * NC + j * P + cp] = Tn;
+                    double x0, x1, x2;
+                    cascade_solve(f0, f1, f2, add, in.src, u0, u1, u2, in.rz0, in.rz1, in.rz2, in.pmb, in.l10, in.l20,
+                                  in.l21, in.u01, in.u02, in.u12, in.ru00, in.ru11, in.ru22, x0, x1, x2);
+                    if (j == njp - 1) {   // the pass's last step: the output (the record wave finalises it), or the next pass' input
+                        if (last_pass) {
+                            double* fo = fin + (((q & 1) * 4 + d) * 3) * P + cp;
+                            fo[0] = x0;
+                            fo[P] = x1;
+                            fo[2 * P] = x2;
+                        } else {
+                            fhw[((size_t)0 * N + b) * P + cp] = x0;
+                            fhw[((size_t)1 * N + b) * P + cp] = x1;
+                            fhw[((size_t)2 * N + b) * P + cp] = x2;
+                        }
+                    }
+                    px0 = x0; px1 = x1; px2 = x2;
+                    if (nonres && b > 0) Tn = (u0 * x0 + u1 * x1 + u2 * x2) * in.sde;
                 }
+                Th[3] = Th[2]; Th[2] = Th[1]; Th[1] = Th[0]; Th[0] = Tn;
+                if (clane && j < njp) Tp[(sg & 7) * NC + j * P + cp] = Tn;
             };
 #pragma unroll 1
             for (int q = 0; q < nblk; ++q) {
                 NUSI_BS_STAMP(pass * nblk + q, 0);
-                if (4 * q < Ts) stage(q, 0);                        // phase A
+                if (4 * q < Ts) solve(q, 0, load(q, 0));           // phase A
                 NUSI_BS_STAMP(pass * nblk + q, 1);
                 __syncthreads();
                 NUSI_BS_STAMP(pass * nblk + q, 2);
+#if NUSI_BS_PIPE
+                {                                                    // phase B: stage d + 1 loaded before d solves
+                    StageIn in1 = load(q, 1), in2 = load(q, 2);
+                    if (4 * q + 1 < Ts) solve(q, 1, in1);
+                    in1 = load(q, 3);
+                    if (4 * q + 2 < Ts) solve(q, 2, in2);
+                    if (4 * q + 3 < Ts) solve(q, 3, in1);
+                }
+#else
 #pragma unroll
-                for (int d = 1; d < 4; ++d)
-                    if (4 * q + d < Ts) stage(q, d);                // phase B
+                for (int d = 1; d < 4; ++d)                          // phase B
+                    if (4 * q + d < Ts) solve(q, d, load(q, d));
+#endif
                 NUSI_BS_STAMP(pass * nblk + q, 3);
                 __syncthreads();
             }
@@ -2167,6 +2181,25 @@ void k_cascade_bs(GridDev g, const Point* __restrict__ pts, const int* __restric
                 const int b = N - 1 - s2 + jj;
                 if (p < R && jj < njp && s2 < Ts && b >= 0 && b < N && pinf[2 * P + p] == 0.0)
                     srcb[(qb & 1) * 4 * NC + e] = t.Src[(size_t)pinf[3 * P + p] * T * nst + src_index(Nz, jb + jj, b)];
+            }
+        };
+        auto finalise = [&](int qb) {   // the last pass' stages of block qb (nuSIprop.hpp:328-336)
+            for (int e = lane; e < 4 * P; e += 64) {
+                const int d = e / P, p = e - P * (e / P), sg = 4 * qb + d, b = N - 1 - sg + njp - 1;
+                if (p < R && sg < Ts && b >= 0 && b < N) {
+                    const double* fo = fin + (((qb & 1) * 4 + d) * 3) * P + p;
+                    const int cpid = (int)pinf[3 * P + p];
+                    const double* U2 = pinf + 4 * P + p;
+                    const double dE = gl.Emax[b] - gl.Emin[b];
+                    const double g0 = fo[0] / dE, g1 = fo[P] / dE, g2 = fo[2 * P] / dE;
+                    double* fx = flux + (size_t)cpid * 3 * N;
+                    double* fl = flux_fla + (size_t)cpid * 3 * N;
+                    fx[b] = g0;
+                    fx[N + b] = g1;
+                    fx[2 * N + b] = g2;
+                    for (int f = 0; f < 3; ++f)
+                        fl[f * N + b] = U2[(3 * f + 0) * P] * g0 + U2[(3 * f + 1) * P] * g1 + U2[(3 * f + 2) * P] * g2;
+                }
             }
         };
         constexpr int FQL = (NQ + 63) / 64;   // FIFO values per lane and block
@@ -2209,9 +2242,11 @@ void k_cascade_bs(GridDev g, const Point* __restrict__ pts, const int* __restric
                     records(q + 1, kRecSplit, S4);
                     sources(q + 1);
                 }
+                if (pass == npass - 1 && q > 0) finalise(q - 1);
                 NUSI_BS_STAMP(pass * nblk + q, 3);
                 __syncthreads();
             }
+            if (pass == npass - 1) finalise(nblk - 1);   // (after the loop's last barrier: the chain's last block is in fin)
         }
     } else {
         // ---- push: block q adds columns c0+1-4q .. c0+4-4q (the T of stages 4q-1 .. 4q-4) into the rows below
@@ -2403,7 +2438,7 @@ template <int NJ, int P, int SPL, int RT, int CW>
 static size_t bs_lds(const GridDev& g)
 {
     constexpr int NC = NJ * P;
-    return sizeof(double) * (2 * (size_t)kBsFields * 4 * NJ + 3 * 8 * (size_t)NC + 24 * (size_t)P + 13 * (size_t)P +
+    return sizeof(double) * (2 * (size_t)kBsFields * 4 * NJ + 3 * 8 * (size_t)NC + 48 * (size_t)P + 13 * (size_t)P +
                              3 * (size_t)g.N + (size_t)P * (g.T + 2) + 6 * (size_t)g.T + 4 * (size_t)g.Nz);
 }
 template <int NJ, int P, int SPL, int RT, int CW>

@@ -394,7 +394,7 @@ NUSI_FN double alphat_entry(const Point& P, const SplineSet& spl, double Em, dou
             if (-tp < 1e4) {
                 const double xx[2] = {-tp, nm::log10(tp / tm)};
                 double v = 0;
-                if (!spl.at.eval(xx, v)) warn |= kWarnSplineOOB;
+                if (!spl.at.eval<2>(xx, v)) warn |= kWarnSplineOOB;
                 app = g4 / m4 * v;
             } else {
                 const double lm = nm::log(-tm), lp = nm::log(-tp);
@@ -864,7 +864,7 @@ NUSI_FN_OUT PPTerm alpha_phiphi_core(const SplineSet& spl, double Sm, double Sp,
         const double d = Sp / Sm;
         const double xx[3] = {Sm, nm::log(-Sm / tm) / nm::log(d) * 1.0001, nm::log10(d)};
         double v = 0;
-        const bool in = spl.a.eval(xx, v);
+        const bool in = spl.a.eval<3>(xx, v);
         return PPTerm{fabs(v), 1.0, 1.0, in ? 0 : kWarnSplineOOB};
     }
     if (tm < -1) {

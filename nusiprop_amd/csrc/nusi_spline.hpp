@@ -82,75 +82,94 @@ struct SplineDev {
         return kk;
     }
 
+    // ND = ndim (2: alphaTilde_phiphi, 3: alpha_phiphi) at compile time: every per-axis array is statically
+    // indexed (registers, not the per-lane scratch a runtime dimension loop puts them in) and each descriptor
+    // field is read once; the same operations in the same order as the reference's loops (interp.hpp:425-460)
+    template <int ND>
     NUSI_FN bool eval(const double* x0in, double& out) const
     {
-        double x0[kSplMaxDim];
-        int k[kSplMaxDim], lo[kSplMaxDim], cnt[kSplMaxDim];
-        double t[kSplMaxDim];
-        for (int i = 0; i < ndim; ++i) {
+        double x0[ND], t[ND], fac[ND][4];
+        int k[ND], lo[ND], cnt[ND];
+#pragma unroll
+        for (int i = 0; i < ND; ++i) {
             x0[i] = islog[i] ? nm::log(x0in[i]) : x0in[i];
             const double* xi = x[i];
-            if (x0[i] <= xi[0] || x0[i] >= xi[n[i] - 1]) {
+            const int ni = n[i];
+            if (x0[i] <= xi[0] || x0[i] >= xi[ni - 1]) {
                 out = 0.0;
                 return false;
             }
             const int kk = search(i, x0[i]);
             k[i] = kk;
             if (kk == 0) { lo[i] = 0; cnt[i] = 3; }
-            else if (kk == n[i] - 2) { lo[i] = kk - 1; cnt[i] = 3; }
+            else if (kk == ni - 2) { lo[i] = kk - 1; cnt[i] = 3; }
             else { lo[i] = kk - 1; cnt[i] = 4; }
             t[i] = (x0[i] - xi[kk]) / (xi[kk + 1] - xi[kk]);
         }
         // per-axis stencil factors (t^3 w0 + t^2 w1 + t w2 + w3), interp.hpp:453-454
-        double fac[kSplMaxDim][4];
-        for (int i = 0; i < ndim; ++i)
-            for (int a = 0; a < cnt[i]; ++a) {
-                const double* wk = w[i] + 16 * k[i] + 4 * a;
-                fac[i][a] = t[i] * t[i] * t[i] * wk[0] + (t[i] * t[i]) * wk[1] + t[i] * wk[2] + wk[3];
+#pragma unroll
+        for (int i = 0; i < ND; ++i)
+#pragma unroll
+            for (int a = 0; a < 4; ++a)
+                if (a < cnt[i]) {
+                    const double* wk = w[i] + 16 * k[i] + 4 * a;
+                    fac[i][a] = t[i] * t[i] * t[i] * wk[0] + (t[i] * t[i]) * wk[1] + t[i] * wk[2] + wk[3];
+                } else {
+                    fac[i][a] = 0.0;
+                }
+        double res = 0;   // the reference's order: axis 0 fastest (loops of 4 with guards: static indices)
+        if constexpr (ND == 3) {
+            if (fw) {
+                struct alignas(16) F4 { float v[4]; };
+                F4 win[4][4];   // win[idx0][a1].v[a2] = f[lo0 + idx0][lo1 + a1][lo2 + a2]
+#pragma unroll
+                for (int i0 = 0; i0 < 4; ++i0) {
+                    const int r0 = lo[0] + (i0 < cnt[0] ? i0 : 0);
+                    const F4* src = reinterpret_cast<const F4*>(fw + 16 * (((size_t)r0 * n[1] + lo[1]) * n[2] + lo[2]));
+#pragma unroll
+                    for (int a1 = 0; a1 < 4; ++a1) win[i0][a1] = src[a1];
+                }
+#pragma unroll
+                for (int i2 = 0; i2 < 4; ++i2)
+#pragma unroll
+                    for (int i1 = 0; i1 < 4; ++i1)
+#pragma unroll
+                        for (int i0 = 0; i0 < 4; ++i0)
+                            if (i2 < cnt[2] && i1 < cnt[1] && i0 < cnt[0]) {
+                                double v = (double)win[i0][i1].v[i2];
+                                v *= fac[0][i0];
+                                v *= fac[1][i1];
+                                v *= fac[2][i2];
+                                res += v;
+                            }
+            } else {
+#pragma unroll 1
+                for (int i2 = 0; i2 < cnt[2]; ++i2)
+#pragma unroll 1
+                    for (int i1 = 0; i1 < cnt[1]; ++i1)
+#pragma unroll
+                        for (int i0 = 0; i0 < 4; ++i0)
+                            if (i0 < cnt[0]) {
+                                double v = (double)f[((long long)(lo[0] + i0) * n[1] + (lo[1] + i1)) * n[2] + (lo[2] + i2)];
+                                v *= fac[0][i0];
+                                v *= fac[1][i1];
+                                v *= fac[2][i2];
+                                res += v;
+                            }
             }
-        if (ndim == 3 && fw) {
-            struct alignas(16) F4 { float v[4]; };
-            F4 win[4][4];   // win[idx0][a1].v[a2] = f[lo0 + idx0][lo1 + a1][lo2 + a2]
+        } else {
 #pragma unroll
-            for (int i0 = 0; i0 < 4; ++i0) {
-                const int r0 = lo[0] + (i0 < cnt[0] ? i0 : 0);
-                const F4* src = reinterpret_cast<const F4*>(fw + 16 * (((size_t)r0 * n[1] + lo[1]) * n[2] + lo[2]));
+            for (int i1 = 0; i1 < 4; ++i1)
 #pragma unroll
-                for (int a1 = 0; a1 < 4; ++a1) win[i0][a1] = src[a1];
-            }
-            double res = 0;   // the reference's order: axis 0 fastest (loops of 4 with guards: static indices)
-#pragma unroll
-            for (int i2 = 0; i2 < 4; ++i2)
-#pragma unroll
-                for (int i1 = 0; i1 < 4; ++i1)
-#pragma unroll
-                    for (int i0 = 0; i0 < 4; ++i0)
-                        if (i2 < cnt[2] && i1 < cnt[1] && i0 < cnt[0]) {
-                            double v = (double)win[i0][i1].v[i2];
-                            v *= fac[0][i0];
-                            v *= fac[1][i1];
-                            v *= fac[2][i2];
-                            res += v;
-                        }
-            out = islog[ndim] ? nm::exp(res) : res;
-            return true;
+                for (int i0 = 0; i0 < 4; ++i0)
+                    if (i1 < cnt[1] && i0 < cnt[0]) {
+                        double v = (double)f[(long long)(lo[0] + i0) * n[1] + (lo[1] + i1)];
+                        v *= fac[0][i0];
+                        v *= fac[1][i1];
+                        res += v;
+                    }
         }
-        int idx[kSplMaxDim] = {0, 0, 0};
-        double res = 0;
-        for (;;) {
-            long long off = 0;
-            for (int i = 0; i < ndim; ++i) off = off * n[i] + (lo[i] + idx[i]);
-            double v = (double)f[off];
-            for (int i = 0; i < ndim; ++i) v *= fac[i][idx[i]];
-            res += v;
-            int p = 0;
-            while (p < ndim && ++idx[p] == cnt[p]) {
-                idx[p] = 0;
-                ++p;
-            }
-            if (p == ndim) break;
-        }
-        out = islog[ndim] ? nm::exp(res) : res;
+        out = islog[ND] ? nm::exp(res) : res;
         return true;
     }
 };

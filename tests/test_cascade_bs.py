@@ -102,7 +102,8 @@ def test_bs_c5_block(nusi, oracle_mod):
 @pytest.mark.parametrize("N,lEmin", [(200, 12.0), (700, 12.0), (1200, 10.0)])
 def test_bs_step_passes(nusi, oracle_mod, N, lEmin):
     """Grids beyond 48 redshift steps (N = 200: 32 steps, 700: 109, C3's 1200 at lE 10 -> 17: 134) in step passes,
-    one point per workgroup and gamma batches (the FIFO carries each pass' last step to the next pass)."""
+    one point per workgroup and gamma batches where a batch's accumulators fit the register file (N = 200; the
+    FIFO carries each pass' last step to the next pass)."""
     pts = [dict(cases.C2B_100, N_bins_E=N, lEmin=lEmin, mphi=m, g=g, majorana=maj)
            for m, g, maj in ((6e5, 0.01, True), (1e5, 0.05, True), (2e6, 0.3, False))]
     pts += [dict(pts[0], si=s) for s in (2.0, 2.2, 2.7)]
@@ -120,10 +121,11 @@ def test_bs_step_passes(nusi, oracle_mod, N, lEmin):
 
 def test_bs_c3_gamma_block(nusi, oracle_mod, ref_tables):
     """A 16-gamma block on the C3 grid (N_E = 1200, lE 10 -> 17, N_z - 1 = 134 steps, phi-phi on at the
-    reference's table geometry; nuSIprop.hpp:257-315): one table, the gamma batch in step passes of 6 with the F
-    FIFO between passes (k_cascade_bs_gamma, the automatic choice there), every point against the oracle's
-    cascade on the block's table (bit-exact to the oracle's own, test_phiphi.py::test_c3_n1200_phiphi) to
-    FLUX_RTOL, and against the same points one per workgroup on k_cascade_wsp."""
+    reference's table geometry; nuSIprop.hpp:257-315): one table, every point against the oracle's cascade on the
+    block's table (bit-exact to the oracle's own, test_phiphi.py::test_c3_n1200_phiphi) to FLUX_RTOL, and against
+    the same points one per workgroup on k_cascade_wsp.  The automatic kernel there is k_cascade_bs in step passes,
+    one point per workgroup: a batch's accumulators are 1332 rows x (steps x points) doubles, and at the 96
+    columns of the N_E = 300 gamma batch that is 1 MB against a CU's 512 KB of registers."""
     from nusiprop_amd import _lib
     from tests.test_phiphi import C3
     at, atd, a, ad = ref_tables
@@ -138,7 +140,7 @@ def test_bs_c3_gamma_block(nusi, oracle_mod, ref_tables):
         assert all(w & 8 == 0 for w in p.warnings(16))
         res[sync] = (flux, fla, p.kernels()[1], p.tables(0))
         p.close()
-    assert res[0][2] == "k_cascade_bs_gamma" and res[1][2] == "k_cascade_ws_passes"
+    assert res[0][2] == "k_cascade_bs" and res[1][2] == "k_cascade_ws_passes"
     G, aT, A = res[0][3]
     for k, kw in enumerate(blk):
         ok = oracle_mod.Oracle(**cases.oracle_kwargs(kw))

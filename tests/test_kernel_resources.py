@@ -23,6 +23,12 @@ BUDGET = {
     r"k_cascade_wfILi\d+ELb1E": (0, 0),
     r"k_cascade_gbILi6E": (8, 48),             # a few chain values around the solve
     r"k_alpha_batchILb[01]E": (64, 1024),      # call frames of the out-of-line per-batch phases
+    # the block-synchronous cascade: 96 B of private segment are the prologue's pow() call frames (no spills)
+    r"k_cascade_bsILi(16|32)ELi1ELi1ELi4ELi1E": (0, 96),
+    r"k_cascade_bsILi48ELi1ELi1ELi4ELi1E": (24, 128),     # loop-invariant scalars of the 48-step one-point shape
+    r"k_cascade_bsILi16ELi1ELi1ELi8ELi1E": (40, 192),     # the 128-row push waves of the step-pass shape
+    r"k_cascade_bsILi(16|32|48)ELi2ELi1ELi2ELi2E": (0, 96),
+    r"k_cascade_bsILi6ELi16ELi1ELi2ELi2E": (0, 96),
 }
 
 
