@@ -61,11 +61,11 @@ def parse():
                     help="skip the C5 and C3 lines the default C4 run adds (secondary_lines: each its own child "
                          "process, a few steps, after the timed region)")
     ap.add_argument("--cascade", default="auto", choices=["auto", "mfma", "wf"],
-                    help="cascade kernel: auto = the library default (= mfma: the warp-specialised wavefront with "
-                         "the push on the fp64 matrix cores), wf = the bit-exact scalar wavefront")
+                    help="cascade kernel: auto = the library default (= mfma: the wavefront with the push on the fp64 "
+                         "matrix cores, block-synchronous k_cascade_bs), wf = the bit-exact scalar wavefront")
     ap.add_argument("--rhs", type=int, default=0,
                     help="NUSI_OPT_CASCADE_RHS: 0 = the library default, 1 = one point per cascade workgroup, 2 = pairs "
-                         "of points sharing a table, 3..16 = the gamma batch k_cascade_gb")
+                         "of points sharing a table, 3..16 = the gamma batch (k_cascade_bs_gamma; k_cascade_gb with --sync stage)")
     ap.add_argument("--reference-order", action="store_true",
                     help="NUSI_OPT_REFERENCE_ORDER: the tables in the reference's own operation order for the complex "
                          "dilogarithms (bit-exact to the oracle's reference-order mode); default: the shared-algorithm "
@@ -73,7 +73,7 @@ def parse():
     ap.add_argument("--no-parity", action="store_true", help="skip the parity object (oracle fluxes of a sample)")
     ap.add_argument("--sync", default="auto", choices=["auto", "stage", "block"],
                     help="NUSI_OPT_CASCADE_SYNC: the MFMA cascade's per-stage kernels (stage) or the block-synchronous "
-                         "k_cascade_bs (block); auto = the library default")
+                         "k_cascade_bs (block); auto = the library default (block)")
     ap.add_argument("--dry-run", action="store_true",
                     help="launch / rank / reduction plumbing only, no GPU work (gloo; CPU tests): prints the JSON "
                          "line with value null")

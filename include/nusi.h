@@ -223,8 +223,8 @@ int nusi_plan_set_cascade(nusi_plan *plan, int kind);
  *                          2 = the block-synchronous kernel k_cascade_bs
  *                          (twice per block of four stages; the same
  *                          operations on the same operands).  Automatic
- *                          takes k_cascade_bs on grids beyond 48 redshift
- *                          steps (C3), the per-stage kernels otherwise. */
+ *                          = 2 (unless NUSI_OPT_STEP_PASSES forces the
+ *                          per-stage step-pass kernel). */
 #define NUSI_OPT_CASCADE_SYNC 7
 int nusi_plan_set_option(nusi_plan *plan, int option, int value);
 /* per-point NUSI_WARN_* bits of the last call */

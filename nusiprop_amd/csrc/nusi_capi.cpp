@@ -1018,9 +1018,10 @@ int nusi_plan_evolve(nusi_plan* pl, const nusi_params* pts, int n, double* d_flu
     const int gbmax = pl->cascade_rhs == 0 ? 16 : pl->cascade_rhs;   // auto: the gamma batch (C5 cascade 4.54 -> 4.13 ms)
     // the block-synchronous MFMA cascade (k_cascade_bs; NUSI_OPT_CASCADE_SYNC): the points of a table slot in
     // workgroups of up to 16 (>= 3 points: the gamma batch), pairs, or one per workgroup (NUSI_OPT_CASCADE_RHS caps
-    // the group size), any source and scattering mode, step passes on long grids.  Auto: on the grids beyond one
-    // pass of 48 steps (C3: 37.3 -> 29.8 ms against k_cascade_wsp; profiles/r4), unless step passes are forced
-    const bool bs_auto = pl->cascade_sync == 0 && pl->step_passes != 1 && !nusi::cascade_ws_fits(pl->gd, 1);
+    // the group size), any source and scattering mode, step passes on long grids.  The default (sync 0) unless step
+    // passes are forced: against the per-stage kernels C4 0.70 -> 0.56 ms, C5 4.13 -> 3.66, C3 37.3 -> 30.7
+    // (profiles/r4)
+    const bool bs_auto = pl->cascade_sync == 0 && pl->step_passes != 1;
     const bool bs = kind == NUSI_CASCADE_MFMA && (pl->cascade_sync == 2 || bs_auto) && nusi::cascade_bs_config(pl->gd, 1) != 0;
     int bs_nwg[3] = {0, 0, 0};   // workgroups of P = 16, 2, 1 (their groups in h_gbgrp in that order)
     if (bs) {

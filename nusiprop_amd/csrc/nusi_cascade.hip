@@ -1940,7 +1940,8 @@ void k_cascade_bs(GridDev g, const Point* __restrict__ pts, const int* __restric
     using Cfg = BsCfg<NJ, P, SPL, RT, CW>;
     constexpr int LPP = Cfg::LPP, PPW = Cfg::PPW, NC = Cfg::NC, NB = Cfg::NB, NF = kBsFields, S4 = 4 * NJ, NQ = 12 * P;
     const int N = g.N, Nz = g.Nz, T = g.T, nst = Nz - 1;
-    const int tid = threadIdx.x, nthr = blockDim.x, lane = tid & 63, wave = tid >> 6, nw = nthr >> 6;
+    // the wave index through readfirstlane: wave-uniform in an SGPR, so every role test and per-wave row base is scalar
+    const int tid = threadIdx.x, nthr = blockDim.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6), nw = nthr >> 6;
     const int chw = nw - 1 - CW, recw = nw - 1;   // push waves 0 .. chw-1, the CW chain waves, the record wave
     const int2 gr = grp ? grp[blockIdx.x] : make_int2((int)blockIdx.x, 1);
     const int R = gr.y;                                   // points of this workgroup (<= P), one table

@@ -518,8 +518,8 @@ void k_alpha_batch(GridDev g, const Point* __restrict__ pts, const SplineSet* __
                     lv.tedm = memb; lv.sedm = memb + ct; lv.mbm = memb + ct + 2 * cs;
                     lv.marg = memb + ct + 2 * cs + kAlphaTile + 2 * ct;   // sT | fT | sS | fS
                     lv.xl = mix; lv.yl = mix;   // (not read with pre)
-                    alpha_k(Q, spl, k, g.lo[n], g.hi[n], g.lo[m], g.hi[m], lv, tot, w, cornered ? &pre : nullptr,
-                            kPP && cornered ? &ppt : nullptr);
+                    alpha_k<SplitLeavesT<kRef>, kPP>(Q, spl, k, g.lo[n], g.hi[n], g.lo[m], g.hi[m], lv, tot, w,
+                                                     cornered ? &pre : nullptr, kPP && cornered ? &ppt : nullptr);
                 }
                 if (valid) A[(size_t)(p0 + q) * g.PT + eidx] = needed ? tot : 0.0;
                 if (w) warn_entry(warn, wmin, T, p0 + q, w, n, m);

@@ -1221,8 +1221,11 @@ NUSI_FN PPTerm alpha_k_pp(const Point& P, const SplineSet& spl, int k, double Em
 }
 
 // one mass state k of alpha(Em, Ep, Em', Ep'): tot += wgt * (every channel); pre: the shared brackets
-// of a batch (alpha_k_pre with another point of it), nullptr = evaluate them here
-template <class Lv>
+// of a batch (alpha_k_pre with another point of it), nullptr = evaluate them here.  kPhiPhi = false: the caller's
+// points have no phi-phi channel, and the call of the out-of-line phi-phi term is compiled out (its register
+// footprint otherwise shapes the caller's allocation around the call: C4 alpha 5.58 -> 5.94 ms with the unrolled
+// spline evaluator)
+template <class Lv, bool kPhiPhi = true>
 NUSI_FN void alpha_k(const Point& P, const SplineSet& spl, int k, double Em, double Ep, double Emp, double Epp,
                      const Lv& lv, double& tot, int& warn, const AlphaPre* pre = nullptr, const PPTerm* ppt = nullptr)
 {
@@ -1323,7 +1326,7 @@ NUSI_FN void alpha_k(const Point& P, const SplineSet& spl, int k, double Em, dou
     tot += wgt * asu;
 
     double app = 0.0;
-    if (Sm > 4 && P.phiphi)   // ppt: the term shared by a batch (alpha_k_pp)
+    if (kPhiPhi && Sm > 4 && P.phiphi)   // ppt: the term shared by a batch (alpha_k_pp)
     {
         PPTerm X;
         if (ppt) X = *ppt;

@@ -82,9 +82,10 @@ class Plan:
                                                 ctypes.c_void_p(stream_ptr) if stream_ptr else None))
 
     def set_cascade(self, kind):
-        """Cascade kernel of later calls: _lib.CASCADE_AUTO (default) = CASCADE_MFMA (the warp-specialised
-        wavefront with its push on the fp64 matrix cores), or the bit-exact scalar kernels
-        CASCADE_{WAVEFRONT,REG,LDS} (WAVEFRONT and REG agree bit for bit)."""
+        """Cascade kernel of later calls: _lib.CASCADE_AUTO (default) = CASCADE_MFMA (the wavefront with its push
+        on the fp64 matrix cores: the block-synchronous k_cascade_bs, or with OPT_CASCADE_SYNC = 1 the per-stage
+        k_cascade_ws / gb / wsp), or the bit-exact scalar kernels CASCADE_{WAVEFRONT,REG,LDS} (WAVEFRONT and REG
+        agree bit for bit)."""
         _lib.check(_lib.load().nusi_plan_set_cascade(self._h, int(kind)))
 
     def set_option(self, option, value):

@@ -26,6 +26,7 @@ def _run(nusi, pts, rhs):
     p0 = pts[0]
     plan = nusi.Plan(p0["N_bins_E"], p0["lEmin"], p0["lEmax"], p0["zmax"], max_points=len(pts))
     plan.set_option(_lib.OPT_CASCADE_RHS, rhs)
+    plan.set_option(_lib.OPT_CASCADE_SYNC, 1)   # the per-stage kernels (k_cascade_bs: tests/test_cascade_bs.py)
     flux, fla = plan.evolve(pts)
     return plan, flux, fla
 

@@ -46,7 +46,7 @@ def test_tables_bitexact_and_flux(nusi, oracle_mod, name):
     o = oracle_mod.Oracle(**cases.oracle_kwargs(kw))
     G, aT, al = o.tables()
     plan, flux, fla, tabs, warn = _gpu(nusi, [kw])
-    assert plan.kernels()[1] == "k_cascade_ws"   # the default (AUTO) cascade, for every source and mode
+    assert plan.kernels()[1] == "k_cascade_bs"   # the default (AUTO) cascade, for every source and mode
     Gg, aTg, Ag = tabs[0]
     T = o.T
     assert plan.T == T and plan.N == o.N and plan.Nz == o.Nz
@@ -315,7 +315,7 @@ def test_cascade_ws_multi_rhs(nusi, N):
     # DSNB points at lE 12 -> 17 have a zero source (the Fermi-Dirac tail underflows): move them to lE 4 -> 9
     lo = [dict(p, lEmin=4.0, lEmax=9.0, mphi=p["mphi"] / 200.0) for p in distinct]
     for grid in (distinct, lo):
-        one = _evolve_opts(nusi, grid, cascade_rhs=1)
+        one = _evolve_opts(nusi, grid, cascade_rhs=1, cascade_sync=1)
         wf = _evolve_opts(nusi, grid, kind=_lib.CASCADE_WAVEFRONT)
         assert one[2][1] == "k_cascade_ws"
         for a, b in zip(one[:2], wf[:2]):
@@ -323,8 +323,8 @@ def test_cascade_ws_multi_rhs(nusi, N):
         gam = [dict(p, si=s, norm=nm, source_model=src) for p in grid[:4]
                for s, nm, src in ((2.0, 1.0, 1), (2.3, 3.0, 0), (2.9, 0.5, 1))]
         gam.append(dict(grid[4], si=2.7))
-        ref = _evolve_opts(nusi, gam, cascade_rhs=1)
-        two = _evolve_opts(nusi, gam)
+        ref = _evolve_opts(nusi, gam, cascade_rhs=1, cascade_sync=1)
+        two = _evolve_opts(nusi, gam, cascade_sync=1)
         assert two[2][1] == "k_cascade_ws_mrhs"
         assert np.array_equal(two[0], ref[0]) and np.array_equal(two[1], ref[1])
         wf = _evolve_opts(nusi, gam, kind=_lib.CASCADE_WAVEFRONT)
@@ -345,7 +345,7 @@ def test_cascade_step_passes(nusi, oracle_mod, N, lEmin):
     got = _evolve_opts(nusi, pts, step_passes=1)
     assert got[2][1] == "k_cascade_ws_passes"
     if N == 100:
-        one = _evolve_opts(nusi, pts)
+        one = _evolve_opts(nusi, pts, cascade_sync=1)
         assert one[2][1] == "k_cascade_ws"
         assert np.array_equal(got[0], one[0]) and np.array_equal(got[1], one[1])
     plan = nusi.Plan(N, lEmin, pts[0]["lEmax"], pts[0]["zmax"], max_points=len(pts))
@@ -390,23 +390,35 @@ def test_cascade_step_passes_resonant_only(nusi, oracle_mod, N):
 def test_plan_kernels_names(nusi):
     """nusi_plan_kernels reports what the last call launched: the batch alpha kernel, and per grid and
     cascade kind the one-pass warp-specialised kernel, its multi-RHS form (gamma pairs sharing a table),
-    the block-synchronous kernel in step passes (N_z - 1 > 48) or the bit-exact wavefront (AUTO)."""
+    the block-synchronous kernel in step passes (N_z - 1 > 48) or the bit-exact wavefront (AUTO): by default the
+    block-synchronous k_cascade_bs in every shape, with NUSI_OPT_CASCADE_SYNC = 1 the per-stage kernels."""
     from nusiprop_amd import _lib
-    def run(N, lEmin, pts_kw, kind):
+    def run(N, lEmin, pts_kw, kind, sync=0):
         pts = [dict(cases.C2B_100, N_bins_E=N, lEmin=lEmin, **kw) for kw in pts_kw]
         plan = nusi.Plan(N, lEmin, pts[0]["lEmax"], pts[0]["zmax"], max_points=len(pts))
         plan.set_cascade(kind)
+        plan.set_option(_lib.OPT_CASCADE_SYNC, sync)
         plan.evolve(pts)
         k = plan.kernels()
         plan.close()
         return k
     two = [dict(mphi=6e5, g=0.01), dict(mphi=2e6, g=0.1)]
+    pair = [dict(mphi=6e5, g=0.01, si=s) for s in (2.0, 2.5)]
+    three = [dict(mphi=6e5, g=0.01, si=s) for s in (2.0, 2.5, 2.7)]
+    dsnb_res = [dict(mphi=6e5, g=0.01, source_model=0, non_resonant=False)]
     for kind in (_lib.CASCADE_AUTO, _lib.CASCADE_MFMA):
-        assert run(100, 12.0, two, kind) == ("k_alpha_batch", "k_cascade_ws")
-        assert run(100, 12.0, [dict(mphi=6e5, g=0.01, si=s) for s in (2.0, 2.5)], kind)[1] == "k_cascade_ws_mrhs"
-        assert run(100, 12.0, [dict(mphi=6e5, g=0.01, si=s) for s in (2.0, 2.5, 2.7)], kind)[1] == "k_cascade_gb"
-        assert run(700, 12.0, two, kind)[1] == "k_cascade_bs"   # beyond 48 steps: the block-synchronous kernel
-        assert run(100, 12.0, [dict(mphi=6e5, g=0.01, source_model=0, non_resonant=False)], kind)[1] == "k_cascade_ws"
+        # the default (NUSI_OPT_CASCADE_SYNC = 0): the block-synchronous kernel for every shape
+        assert run(100, 12.0, two, kind) == ("k_alpha_batch", "k_cascade_bs")
+        assert run(100, 12.0, pair, kind)[1] == "k_cascade_bs_pairs"
+        assert run(100, 12.0, three, kind)[1] == "k_cascade_bs_gamma"
+        assert run(700, 12.0, two, kind)[1] == "k_cascade_bs"
+        assert run(100, 12.0, dsnb_res, kind)[1] == "k_cascade_bs"
+        # NUSI_OPT_CASCADE_SYNC = 1: the per-stage kernels
+        assert run(100, 12.0, two, kind, 1)[1] == "k_cascade_ws"
+        assert run(100, 12.0, pair, kind, 1)[1] == "k_cascade_ws_mrhs"
+        assert run(100, 12.0, three, kind, 1)[1] == "k_cascade_gb"
+        assert run(700, 12.0, two, kind, 1)[1] == "k_cascade_ws_passes"
+        assert run(100, 12.0, dsnb_res, kind, 1)[1] == "k_cascade_ws"
     assert run(100, 12.0, two, _lib.CASCADE_WAVEFRONT)[1] == "k_cascade_wf"
     assert run(700, 12.0, two, _lib.CASCADE_WAVEFRONT)[1] == "k_cascade_reg"
     assert run(100, 12.0, two, _lib.CASCADE_LDS)[1] == "k_cascade"
@@ -414,20 +426,23 @@ def test_plan_kernels_names(nusi):
 
 def test_c5_gamma_block_vs_oracle(nusi, oracle_mod):
     """BASELINE config 5: one full 16-gamma block of scan.c5_points() (N_E = 300, power law; one
-    Stage-A table, the gamma batch k_cascade_gb by default) against the oracle -- its tables once, its
-    cascade per gamma -- to FLUX_RTOL with the same exact zeros; the pairs on the multi-RHS kernel give
-    the one-point-per-workgroup fluxes bit for bit (A/B), the gamma batch to rounding."""
+    Stage-A table, the gamma batch k_cascade_bs_gamma by default) against the oracle -- its tables once, its
+    cascade per gamma -- to FLUX_RTOL with the same exact zeros; the pairs give the one-point-per-workgroup fluxes
+    bit for bit (A/B), the gamma batch to rounding; the per-stage gamma batch k_cascade_gb to rounding."""
     from nusiprop_amd import scan
     allp = scan.c5_points()
     blk = allp[16 * 1234:16 * 1235]
     assert len({scan.table_key(p) for p in blk}) == 1 and len({p["si"] for p in blk}) == 16
     flux, fla, names = _evolve_opts(nusi, blk)
-    assert names[1] == "k_cascade_gb"
+    assert names[1] == "k_cascade_bs_gamma"
     ref1 = _evolve_opts(nusi, blk, cascade_rhs=1)
     two = _evolve_opts(nusi, blk, cascade_rhs=2)
-    assert two[2][1] == "k_cascade_ws_mrhs"
+    assert two[2][1] == "k_cascade_bs_pairs"
     assert np.array_equal(two[0], ref1[0]) and np.array_equal(two[1], ref1[1])
     assert cases.rel_err(flux, ref1[0]) <= FLUX_RTOL and np.array_equal(flux == 0, ref1[0] == 0)
+    gb = _evolve_opts(nusi, blk, cascade_sync=1)
+    assert gb[2][1] == "k_cascade_gb"
+    assert cases.rel_err(gb[0], flux) <= FLUX_RTOL and np.array_equal(gb[0] == 0, flux == 0)
     o = oracle_mod.Oracle(**cases.oracle_kwargs(blk[0]))
     G, aT, al = o.tables()
     for k, p in enumerate(blk):

@@ -25,10 +25,12 @@ BUDGET = {
     r"k_alpha_batchILb[01]E": (64, 1024),      # call frames of the out-of-line per-batch phases
     # the block-synchronous cascade: 96 B of private segment are the prologue's pow() call frames (no spills)
     r"k_cascade_bsILi(16|32)ELi1ELi1ELi4ELi1E": (0, 96),
-    r"k_cascade_bsILi48ELi1ELi1ELi4ELi1E": (24, 128),     # loop-invariant scalars of the 48-step one-point shape
-    r"k_cascade_bsILi16ELi1ELi1ELi8ELi1E": (40, 192),     # the 128-row push waves of the step-pass shape
-    r"k_cascade_bsILi(16|32|48)ELi2ELi1ELi2ELi2E": (0, 96),
-    r"k_cascade_bsILi6ELi16ELi1ELi2ELi2E": (0, 96),
+    # (the wave index is readfirstlane'd: per-wave row bases in SGPRs; as VGPRs they spilled 19 / 33 into the push)
+    r"k_cascade_bsILi48ELi1ELi1ELi4ELi1E": (4, 96),
+    r"k_cascade_bsILi16ELi1ELi1ELi8ELi1E": (10, 128),
+    r"k_cascade_bsILi(16|32)ELi2ELi1ELi2ELi2E": (0, 96),
+    r"k_cascade_bsILi48ELi2ELi1ELi2ELi2E": (4, 112),
+    r"k_cascade_bsILi6ELi16ELi1ELi2ELi2E": (4, 112),
 }
 
 

@@ -108,15 +108,16 @@ def test_default_phiphi_needs_tables(nusi, tmp_path, monkeypatch):
 
 
 @pytest.mark.parametrize("kw,kernel", [
-    (dict(cases.TEST_CPP, N_bins_E=300, phiphi=False), "k_cascade_ws"),                      # C1 at N_E = 300 (DSNB)
-    (dict(cases.C2A, phiphi=False), "k_cascade_ws"),                                         # C2a (DSNB, resonance in range)
-    (dict(cases.TEST_PY, phiphi=False), "k_cascade_ws"),                                     # resonant-only, DSNB
+    (dict(cases.TEST_CPP, N_bins_E=300, phiphi=False), "k_cascade_bs"),                      # C1 at N_E = 300 (DSNB)
+    (dict(cases.C2A, phiphi=False), "k_cascade_bs"),                                         # C2a (DSNB, resonance in range)
+    (dict(cases.TEST_PY, phiphi=False), "k_cascade_bs"),                                     # resonant-only, DSNB
     (dict(cases.TEST_CPP, N_bins_E=1200, lEmin=10.0, lEmax=17.0, phiphi=False, source_model=1),
-     "k_cascade_ws_passes"),                                                                 # the C3 grid (134 steps)
+     "k_cascade_bs"),                                                                        # the C3 grid (134 steps)
 ], ids=["C1_N300", "C2a_N300", "test_py", "C3_grid"])
 def test_drop_in_object_gets_the_fast_cascade(nusi, oracle_mod, kw, kernel):
     """The drop-in object (calculate_flux / pyprop: one point, default kernels) runs the MFMA cascade for the
-    reference's own DSNB source and resonant-only mode and, beyond 48 redshift steps, its step-pass form --
+    reference's own DSNB source and resonant-only mode and, beyond 48 redshift steps, the block-synchronous kernel in
+    step passes --
     fluxes against the oracle's evolve() to FLUX_RTOL with the same exact zeros."""
     ev = nusi.pyprop(**_kw(kw))
     ev.evolve()
