@@ -2282,7 +2282,11 @@ void k_cascade_bs(GridDev g, const Point* __restrict__ pts, const int* __restric
                     if (crit == phase_a && rw0 + 16 * a < r)   // tiles wholly at or above r hold consumed rows only
 #pragma unroll
                         for (int s = 0; s < NB; ++s)
+#ifdef NUSI_BS_NOPUSH   // timing diagnostic only (wrong fluxes): the block pushes without the matrix core
+                            acc[a][s][0] += ab[a] * Tq[16 * s];
+#else
                             acc[a][s] = __builtin_amdgcn_mfma_f64_16x16x4f64(ab[a], Tq[16 * s], acc[a][s], 0, 0, 0);
+#endif
                 }
                 if (phase_a)
 #pragma unroll

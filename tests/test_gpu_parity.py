@@ -155,8 +155,9 @@ def test_cascade_sizes(nusi, oracle_mod, N, nonres):
 
 def test_gamma_batches_share_tables(nusi, oracle_mod):
     """Points that differ only in si / norm / source share one Stage-A table (the
-    tables do not read them, nuSIprop.hpp:217-253); each point's flux still equals
-    its own single-point evolve bit for bit, and the oracle's to FLUX_RTOL."""
+    tables do not read them, nuSIprop.hpp:217-253); each point's flux equals its own
+    single-point evolve to rounding (three points of a table run as a gamma batch, its
+    steps in passes of 6) with the same exact zeros, and the oracle's to FLUX_RTOL."""
     base = [dict(cases.C2B_100, mphi=m, g=g) for m, g in ((6e5, 0.01), (2e6, 0.1))]
     pts = [dict(b, si=s, norm=nm, source_model=src) for s, nm, src in ((2.0, 1.0, 1), (2.5, 6.0, 1), (3.0, 2.0, 0))
            for b in base]
@@ -166,7 +167,8 @@ def test_gamma_batches_share_tables(nusi, oracle_mod):
             assert np.array_equal(a, b)
     for i, p in enumerate(pts):
         _, f1, fl1, _, _ = _gpu(nusi, [p])
-        assert np.array_equal(f1[0], flux[i]) and np.array_equal(fl1[0], fla[i])
+        assert cases.rel_err(flux[i], f1[0]) <= FLUX_RTOL and np.array_equal(flux[i] == 0, f1[0] == 0)
+        assert cases.rel_err(fla[i], fl1[0]) <= FLUX_RTOL
         o = oracle_mod.Oracle(**cases.oracle_kwargs(p))
         _, fla_ref = o.evolve()
         assert cases.rel_err(fla[i], fla_ref) <= FLUX_RTOL
