@@ -2155,10 +2155,12 @@ void k_cascade_bs(GridDev g, const Point* __restrict__ pts, const int* __restric
         }
     } else if (wave == recw) {
         // ---- records and DSNB sources: block 0 (and the FIFO of blocks 0, 1) before the blocks; in block q the
-        // records of block q + 1 (block q + 1's slot was last read in block q - 1), the first kRecA rounds of 64 in
-        // phase A (where the chain solves one stage), the rest and the DSNB sources in phase B (three stages); the
-        // FIFO values of block q + 2 are loaded in phase A of block q and stored in phase A of block q + 1
-        constexpr int kRecRounds = (S4 + 63) / 64, kRecA = (kRecRounds + 2) / 3, kRecSplit = 64 * kRecA < S4 ? 64 * kRecA : S4;
+        // records of block q + 1 (block q + 1's slot was last read in block q - 1): one round of 64 lanes goes wholly
+        // into phase B, where the chain solves three stages (C5 / C3: phase A then waits on the chain alone); of
+        // three rounds (48 steps) the first goes into phase A; the DSNB sources into phase B.  The FIFO values of
+        // block q + 2 are loaded in phase A of block q and stored in phase A of block q + 1
+        constexpr int kRecRounds = (S4 + 63) / 64, kRecA = kRecRounds <= 1 ? 0 : (kRecRounds + 2) / 3;
+        constexpr int kRecSplit = 64 * kRecA < S4 ? 64 * kRecA : S4;
         auto records = [&](int qb, int e0, int e1) {
             for (int e = e0 + lane; e < e1; e += 64) {
                 const int sb = e / NJ, jj = e - NJ * (e / NJ), s2 = 4 * qb + sb;
