@@ -854,9 +854,18 @@ __device__ unsigned int g_ws_hwid[kTrBlocks * kTrWaves];   // HW_ID (SE, CU, SIM
         if (blockIdx.x == 0 && (threadIdx.x & 63) == 0 && (blk) < kTrStages)                                       \
             g_ws_trace[((threadIdx.x >> 6) * kTrStages + (blk)) * 4 + (which)] = __builtin_amdgcn_s_memtime();      \
     } while (0)
+// k_cascade_bs chain wave 0, phase B, in wave slot 15: [block][stage 4q+1 loaded, solved, 4q+2 loaded, solved]
+// (the "loaded" stamps wait for the stage's LDS loads first)
+#define NUSI_BS_CSTAMP(blk, which)                                                                                 \
+    do {                                                                                                           \
+        if (((which) & 1) == 0) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                                \
+        if (blockIdx.x == 0 && (threadIdx.x & 63) == 0 && (blk) < kTrStages)                                       \
+            g_ws_trace[(15 * kTrStages + (blk)) * 4 + (which)] = __builtin_amdgcn_s_memtime();                      \
+    } while (0)
 #else
 #define NUSI_WS_STAMP(sg, which) do { } while (0)
 #define NUSI_BS_STAMP(blk, which) do { } while (0)
+#define NUSI_BS_CSTAMP(blk, which) do { } while (0)
 #define NUSI_WS_HWID() do { } while (0)
 #endif
 
@@ -1913,6 +1922,9 @@ void k_cascade_gb(GridDev g, const Point* __restrict__ pts, const int* __restric
 // and the same points get the same fluxes as from those kernels (the MFMA sums each element's four columns in
 // its own order whichever column it is).  Waves: push waves of 16 RT rows, the chain waves, the record wave.
 // ---------------------------------------------------------------------------
+#ifndef NUSI_BS_PRIO   // the chain (3) and record (NUSI_BS_PRIO + 1) waves at raised issue priority (s_setprio): C5
+#define NUSI_BS_PRIO 1    // cascade 3.51 -> 3.25 ms, C3 29.1 -> 24.9, C4 0.555 -> 0.545 (profiles/r4/ab/r4n); 0 = off
+#endif
 #ifndef NUSI_BS_PIPE   // A/B: k_cascade_bs's chain issues stage d + 1's loads before stage d's solve (two stages'
 #define NUSI_BS_PIPE 0  // operands live: spills at the 128-VGPR budget)
 #endif
@@ -2028,6 +2040,9 @@ void k_cascade_bs(GridDev g, const Point* __restrict__ pts, const int* __restric
         // are issued before the solve of stage d, so one LDS latency per stage is hidden behind the dependent
         // solve.  The power-law sources are formed here (powerlaw_src_h), the DSNB ones read from srcb; the
         // finalise of the last pass goes to the record wave through `fin`
+#if NUSI_BS_PRIO
+        __builtin_amdgcn_s_setprio(3);   // the chain's instructions (and LDS requests) before the push waves'
+#endif
         const int cw = wave - chw;
         const int cp = cw * PPW + lane / LPP, cjp = lane - LPP * (lane / LPP);
         const bool clane = lane < PPW * LPP && cp < R;
@@ -2146,7 +2161,12 @@ void k_cascade_bs(GridDev g, const Point* __restrict__ pts, const int* __restric
 #else
 #pragma unroll
                 for (int d = 1; d < 4; ++d)                          // phase B
-                    if (4 * q + d < Ts) solve(q, d, load(q, d));
+                    if (4 * q + d < Ts) {
+                        const StageIn in = load(q, d);
+                        if (d < 3 && cw == 0) NUSI_BS_CSTAMP(pass * nblk + q, 2 * (d - 1));
+                        solve(q, d, in);
+                        if (d < 3 && cw == 0) NUSI_BS_CSTAMP(pass * nblk + q, 2 * (d - 1) + 1);
+                    }
 #endif
                 NUSI_BS_STAMP(pass * nblk + q, 3);
                 __syncthreads();
@@ -2154,6 +2174,9 @@ void k_cascade_bs(GridDev g, const Point* __restrict__ pts, const int* __restric
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the FIFO stores land before the next pass reads them
         }
     } else if (wave == recw) {
+#if NUSI_BS_PRIO
+        __builtin_amdgcn_s_setprio(NUSI_BS_PRIO + 1);
+#endif
         // ---- records and DSNB sources: block 0 (and the FIFO of blocks 0, 1) before the blocks; in block q the
         // records of block q + 1 (block q + 1's slot was last read in block q - 1): one round of 64 lanes goes wholly
         // into phase B, where the chain solves three stages (C5 / C3: phase A then waits on the chain alone); of

@@ -37,9 +37,10 @@ def main():
     buf = (ctypes.c_ulonglong * (TW * TS * 4))()
     assert L.nusi_debug_ws_trace(buf, TW * TS * 4) == 0
     a = np.frombuffer(buf, dtype=np.uint64).reshape(TW, TS, 4).astype(np.int64)
-    waves = [w for w in range(TW) if a[w, 5, 0] != 0]
+    waves = [w for w in range(TW - 1) if a[w, 5, 0] != 0]   # (slot 15: the chain segments)
     nw = len(waves)
-    chain, rec = waves[-2], waves[-1]
+    ncw = 2 if wl == "c5" else 1   # chain waves of the workload's instance (the gamma batch: two)
+    chain, rec, chain0 = waves[-2], waves[-1], waves[-1 - ncw]
     nb = int(np.max(np.nonzero(a[chain, :, 3])[0])) + 1
     sl = slice(4, nb - 4)
     st = a[:, sl, :]
@@ -47,7 +48,7 @@ def main():
     print("%s: %s, %d waves, %d blocks traced; block period median %d cycles (mean %.0f, p90 %d)" % (
         wl, plan.kernels()[1], nw, nb, np.median(period), period.mean(), np.quantile(period, 0.9)))
     for w in waves:
-        kind = "chain" if w == chain else "record" if w == rec else "push"
+        kind = "chain" if chain0 <= w < rec else "record" if w == rec else "push"
         A = st[w, :, 1] - st[w, :, 0]
         B = st[w, :, 3] - st[w, :, 2]
         print("  wave %2d %-6s phase A busy %6d  phase B busy %6d  (medians)" % (w, kind, np.median(A), np.median(B)))
@@ -55,6 +56,12 @@ def main():
     lastB = np.argmax(st[waves, :, 3], axis=0)
     print("last at barrier A->B:", {waves[i]: int(c) for i, c in enumerate(np.bincount(lastA, minlength=nw)) if c})
     print("last at barrier B->A:", {waves[i]: int(c) for i, c in enumerate(np.bincount(lastB, minlength=nw)) if c})
+    cs = a[15, sl, :]
+    if cs[:, 0].any():   # chain wave 0's phase-B segments (NUSI_BS_CSTAMP)
+        B0 = a[chain0, sl, 2]
+        print("chain phase B: stage 4q+1 loads %d, solve %d; stage 4q+2 loads %d, solve %d cycles (medians)" % (
+            np.median(cs[:, 0] - B0), np.median(cs[:, 1] - cs[:, 0]), np.median(cs[:, 2] - cs[:, 1]),
+            np.median(cs[:, 3] - cs[:, 2])))
     relA = st[chain, :, 2] - st[waves, :, 1].max(axis=0)
     relB = st[chain, 1:, 0] - st[waves, :-1, 3].max(axis=0)
     print("barrier release (last arrival -> chain resumes): A->B median %d, B->A median %d cycles" % (
