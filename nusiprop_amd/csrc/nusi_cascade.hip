@@ -1922,9 +1922,9 @@ void k_cascade_gb(GridDev g, const Point* __restrict__ pts, const int* __restric
 // and the same points get the same fluxes as from those kernels (the MFMA sums each element's four columns in
 // its own order whichever column it is).  Waves: push waves of 16 RT rows, the chain waves, the record wave.
 // ---------------------------------------------------------------------------
-#ifndef NUSI_BS_PRIO   // the chain (3) and record (NUSI_BS_PRIO + 1) waves at raised issue priority (s_setprio): C5
-#define NUSI_BS_PRIO 1    // cascade 3.51 -> 3.25 ms, C3 29.1 -> 24.9, C4 0.555 -> 0.545 (profiles/r4/ab/r4n); 0 = off
-#endif
+#ifndef NUSI_BS_PRIO   // the chain and record waves at raised issue priority (s_setprio 3; the push waves 0): C5
+#define NUSI_BS_PRIO 1    // cascade 3.51 -> 3.25 ms, C3 29.1 -> 24.8, C4 0.555 -> 0.528 (profiles/r4/ab/r4n, r4o); 0 = off.
+#endif                    // Sleeping the push waves at phase B's start (to let the chain's loads first) measured no gain
 #ifndef NUSI_BS_PIPE   // A/B: k_cascade_bs's chain issues stage d + 1's loads before stage d's solve (two stages'
 #define NUSI_BS_PIPE 0  // operands live: spills at the 128-VGPR budget)
 #endif
@@ -2175,7 +2175,7 @@ void k_cascade_bs(GridDev g, const Point* __restrict__ pts, const int* __restric
         }
     } else if (wave == recw) {
 #if NUSI_BS_PRIO
-        __builtin_amdgcn_s_setprio(NUSI_BS_PRIO + 1);
+        __builtin_amdgcn_s_setprio(3);
 #endif
         // ---- records and DSNB sources: block 0 (and the FIFO of blocks 0, 1) before the blocks; in block q the
         // records of block q + 1 (block q + 1's slot was last read in block q - 1): one round of 64 lanes goes wholly
