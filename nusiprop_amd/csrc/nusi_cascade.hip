@@ -216,6 +216,24 @@ NUSI_FN void cascade_solve(double f0, double f1, double f2, double add, double s
     x0 = (x0 - u01 * x1 - u02 * x2) * ru00;
 }
 
+// cascade_solve where every lane's LU kept the rows in place (the permutation 0 | 1 << 2 | 2 << 4, and then ru00 =
+// 1 / 1.0 = 1.0: the product by it is exact and dropped) -- the same bits as cascade_solve
+constexpr int kIdPerm = 0 | (1 << 2) | (2 << 4);
+NUSI_FN void cascade_solve_id(double f0, double f1, double f2, double add, double src0, double u0, double u1, double u2,
+                              double rz0, double rz1, double rz2, double l10, double l20, double l21, double u01,
+                              double u02, double u12, double ru11, double ru22, double& x0, double& x1, double& x2)
+{
+    x0 = (f0 + (src0 + u0 * add)) * rz0;
+    x1 = (f1 + (src0 + u1 * add)) * rz1;
+    x2 = (f2 + (src0 + u2 * add)) * rz2;
+    x1 = x1 - l10 * x0;
+    x2 = x2 - l20 * x0;
+    x2 = x2 - l21 * x1;
+    x2 = x2 * ru22;
+    x1 = (x1 - u12 * x2) * ru11;
+    x0 = x0 - u01 * x1 - u02 * x2;
+}
+
 __global__ __launch_bounds__(64) void k_cascade(GridDev g, const Point* __restrict__ pts, TablesDev t,
                                                 double* __restrict__ flux, double* __restrict__ flux_fla)
 {
@@ -1950,6 +1968,10 @@ void k_cascade_bs(GridDev g, const Point* __restrict__ pts, const int* __restric
 {
     extern __shared__ __attribute__((aligned(16))) double lds[];
     using Cfg = BsCfg<NJ, P, SPL, RT, CW>;
+    // the power-law sources: formed on the record wave (into srcb, a block ahead) where that is one round of 64 (one
+    // point, 16 steps: C3, cascade 24.8 -> 23.7 ms), else in the chain (the record wave's loop of 6 rounds for the
+    // gamma batch cost C5 3.25 -> 4.16 ms; at 48 steps its records already fill both phases, C4)
+    constexpr bool kSrcRec = 4 * NJ * P <= 64;
     constexpr int LPP = Cfg::LPP, PPW = Cfg::PPW, NC = Cfg::NC, NB = Cfg::NB, NF = kBsFields, S4 = 4 * NJ, NQ = 12 * P;
     const int N = g.N, Nz = g.Nz, T = g.T, nst = Nz - 1;
     // the wave index through readfirstlane: wave-uniform in an SGPR, so every role test and per-wave row base is scalar
@@ -2079,10 +2101,13 @@ void k_cascade_bs(GridDev g, const Point* __restrict__ pts, const int* __restric
                 in.u01 = Rc[BR_U01 * S4]; in.u02 = Rc[BR_U02 * S4]; in.u12 = Rc[BR_U12 * S4];
                 in.ru00 = Rc[BR_RU00 * S4]; in.ru11 = Rc[BR_RU11 * S4]; in.ru22 = Rc[BR_RU22 * S4];
                 in.sde = Rc[BR_SDE * S4];
-                // both sources, selected branch-free (a branch here made the compiler wait for every LDS load)
-                const double spw = powerlaw_src_h(gl, csf, cpw, ic, bc);
                 const double sdn = srcb[(q & 1) * 4 * NC + d * NC + j * P + cpc];
-                in.src = cpl ? spw : sdn;
+                if (kSrcRec) {   // the record wave formed every source
+                    in.src = sdn;
+                } else {         // both, selected branch-free (a branch here made the compiler wait for every LDS load)
+                    const double spw = powerlaw_src_h(gl, csf, cpw, ic, bc);
+                    in.src = cpl ? spw : sdn;
+                }
                 in.cj = gl.step_c[ic];
                 const int qq = (sg - 1) >> 2;   // block whose publication serves stage sg
                 in.ab = AX[((qq & 1) * 4 + (sg - 1 - 4 * qq)) * NC + j * P + cpc];
@@ -2123,8 +2148,12 @@ void k_cascade_bs(GridDev g, const Point* __restrict__ pts, const int* __restric
                                            b == N - 1);
                     }
                     double x0, x1, x2;
-                    cascade_solve(f0, f1, f2, add, in.src, u0, u1, u2, in.rz0, in.rz1, in.rz2, in.pmb, in.l10, in.l20,
-                                  in.l21, in.u01, in.u02, in.u12, in.ru00, in.ru11, in.ru22, x0, x1, x2);
+                    if (__all(in.pmb == kIdPerm))   // (every active lane: no row exchange -- always, in practice)
+                        cascade_solve_id(f0, f1, f2, add, in.src, u0, u1, u2, in.rz0, in.rz1, in.rz2, in.l10, in.l20,
+                                         in.l21, in.u01, in.u02, in.u12, in.ru11, in.ru22, x0, x1, x2);
+                    else
+                        cascade_solve(f0, f1, f2, add, in.src, u0, u1, u2, in.rz0, in.rz1, in.rz2, in.pmb, in.l10,
+                                      in.l20, in.l21, in.u01, in.u02, in.u12, in.ru00, in.ru11, in.ru22, x0, x1, x2);
                     if (j == njp - 1) {   // the pass's last step: the output (the record wave finalises it), or the next pass' input
                         if (last_pass) {
                             double* fo = fin + (((q & 1) * 4 + d) * 3) * P + cp;
@@ -2200,13 +2229,18 @@ void k_cascade_bs(GridDev g, const Point* __restrict__ pts, const int* __restric
             }
         };
         bool any_dsnb = false;   // (set after the first barrier: the prologue writes pinf)
-        auto sources = [&](int qb) {   // the DSNB points' (k_source_dsnb's table); the chain forms the power-law ones
-            if (!any_dsnb) return;
+        auto sources = [&](int qb) {   // the DSNB points' (k_source_dsnb's table); with kSrcRec the power-law ones too
+            if (!kSrcRec && !any_dsnb) return;
             for (int e = lane; e < S4 * P; e += 64) {
                 const int p = e % P, sj = e / P, sb = sj / NJ, jj = sj - NJ * sb, s2 = 4 * qb + sb;
-                const int b = N - 1 - s2 + jj;
-                if (p < R && jj < njp && s2 < Ts && b >= 0 && b < N && pinf[2 * P + p] == 0.0)
-                    srcb[(qb & 1) * 4 * NC + e] = t.Src[(size_t)pinf[3 * P + p] * T * nst + src_index(Nz, jb + jj, b)];
+                const int b = N - 1 - s2 + jj, i = Nz - 1 - jb - jj;
+                if (p < R && jj < njp && s2 < Ts && b >= 0 && b < N) {
+                    if (pinf[2 * P + p] == 0.0)
+                        srcb[(qb & 1) * 4 * NC + e] = t.Src[(size_t)pinf[3 * P + p] * T * nst + src_index(Nz, jb + jj, b)];
+                    else if (kSrcRec)
+                        srcb[(qb & 1) * 4 * NC + e] =
+                            powerlaw_src_h(gl, SrcFactors{pinf[p], pinf[P + p]}, pw + (size_t)p * (T + 2), i, b);
+                }
             }
         };
         auto finalise = [&](int qb) {   // the last pass' stages of block qb (nuSIprop.hpp:328-336)
