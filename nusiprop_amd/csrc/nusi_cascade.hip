@@ -1940,6 +1940,9 @@ void k_cascade_gb(GridDev g, const Point* __restrict__ pts, const int* __restric
 // and the same points get the same fluxes as from those kernels (the MFMA sums each element's four columns in
 // its own order whichever column it is).  Waves: push waves of 16 RT rows, the chain waves, the record wave.
 // ---------------------------------------------------------------------------
+#ifndef NUSI_BS_SIMDMAP   // the chain and record waves beside the least-busy push waves (wave w runs on SIMD f(w % 4),
+#define NUSI_BS_SIMDMAP 1    // HW_ID in the trace build): C5 cascade 3.19 -> 2.82 ms, C3 23.4 -> 21.4, C4 equal
+#endif                       // (profiles/r4/ab/r4u, r4v); 0 = the push waves' rows in wave order
 #ifndef NUSI_BS_PRIO   // the chain and record waves at raised issue priority (s_setprio 3; the push waves 0): C5
 #define NUSI_BS_PRIO 1    // cascade 3.51 -> 3.25 ms, C3 29.1 -> 24.8, C4 0.555 -> 0.528 (profiles/r4/ab/r4n, r4o); 0 = off.
 #endif                    // Sleeping the push waves at phase B's start (to let the chain's loads first) measured no gain
@@ -1976,7 +1979,16 @@ void k_cascade_bs(GridDev g, const Point* __restrict__ pts, const int* __restric
     const int N = g.N, Nz = g.Nz, T = g.T, nst = Nz - 1;
     // the wave index through readfirstlane: wave-uniform in an SGPR, so every role test and per-wave row base is scalar
     const int tid = threadIdx.x, nthr = blockDim.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6), nw = nthr >> 6;
+#if NUSI_BS_SIMDMAP
+    // the record wave before the chain waves, and the push row blocks dealt so that the push waves sharing a SIMD with
+    // a chain wave (wave w on SIMD w % 4) hold the top rows, which the wavefront consumes first (fewest MFMAs)
+    const int recw = nw - 1 - CW, chw = nw - CW;
+    const bool is_chain = wave >= chw, is_rec = wave == recw;
+#else
     const int chw = nw - 1 - CW, recw = nw - 1;   // push waves 0 .. chw-1, the CW chain waves, the record wave
+    const bool is_chain = wave >= chw && wave < recw, is_rec = wave == recw;
+#endif
+    NUSI_WS_HWID();
     const int2 gr = grp ? grp[blockIdx.x] : make_int2((int)blockIdx.x, 1);
     const int R = gr.y;                                   // points of this workgroup (<= P), one table
     auto pidx = [&](int p) { return gidx ? gidx[gr.x + p] : gr.x + p; };   // (gidx == nullptr: point blockIdx.x)
@@ -2055,7 +2067,7 @@ void k_cascade_bs(GridDev g, const Point* __restrict__ pts, const int* __restric
         c0 = T - 1 - jb;                       // the table column of its stage 0
         nblk = (Ts + 3) / 4;
     };
-    if (wave >= chw && wave < recw) {
+    if (is_chain) {
         // ---- chain wave cw: lane (cp, cjp) solves step slot j = cjp of point cp (PPW points per wave, so a point's
         // steps never cross waves).  A stage is split into its loads (records, source operands, published row,
         // diagonal alphas: none depends on the previous stage's solve) and its solve, and the loads of stage d + 1
@@ -2202,7 +2214,7 @@ void k_cascade_bs(GridDev g, const Point* __restrict__ pts, const int* __restric
             }
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the FIFO stores land before the next pass reads them
         }
-    } else if (wave == recw) {
+    } else if (is_rec) {
 #if NUSI_BS_PRIO
         __builtin_amdgcn_s_setprio(3);
 #endif
@@ -2311,7 +2323,25 @@ void k_cascade_bs(GridDev g, const Point* __restrict__ pts, const int* __restric
     } else {
         // ---- push: block q adds columns c0+1-4q .. c0+4-4q (the T of stages 4q-1 .. 4q-4) into the rows below
         // r = c0-4q: in phase A the tiles holding rows r-1 .. r-4 (published to AX), in phase B the others
+#if NUSI_BS_SIMDMAP
+        int rb = 0;   // this push wave's row block: the waves sharing no SIMD with a chain or the record wave take the
+        {             // bottom rows (busiest), then those beside the record wave, then those beside a chain wave
+            const int npush = nw - 1 - CW;
+            auto cls = [&](int w) {
+                for (int c = chw; c < nw; ++c)
+                    if ((c & 3) == (w & 3)) return 2;
+                return (recw & 3) == (w & 3) ? 1 : 0;
+            };
+            const int mine = cls(wave);
+            for (int w = 0; w < npush; ++w) {
+                const int o = cls(w);
+                if (o < mine || (o == mine && w < wave)) ++rb;
+            }
+        }
+        const int rw0 = rb * 16 * RT;
+#else
         const int rw0 = wave * 16 * RT;
+#endif
 #pragma unroll 1
         for (int pass = 0; pass < npass; ++pass) {
             pass_geom(pass);

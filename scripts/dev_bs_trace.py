@@ -62,6 +62,9 @@ def main():
         print("chain phase B: stage 4q+1 loads %d, solve %d; stage 4q+2 loads %d, solve %d cycles (medians)" % (
             np.median(cs[:, 0] - B0), np.median(cs[:, 1] - cs[:, 0]), np.median(cs[:, 2] - cs[:, 1]),
             np.median(cs[:, 3] - cs[:, 2])))
+    hw = (ctypes.c_uint * TW)()
+    if hasattr(L, "nusi_debug_ws_hwid") and L.nusi_debug_ws_hwid(hw, TW) == 0:   # workgroup 0: HW_ID SIMD_ID bits 5:4
+        print("SIMD of each wave:", {w: (hw[w] >> 4) & 3 for w in waves})
     relA = st[chain, :, 2] - st[waves, :, 1].max(axis=0)
     relB = st[chain, 1:, 0] - st[waves, :-1, 3].max(axis=0)
     print("barrier release (last arrival -> chain resumes): A->B median %d, B->A median %d cycles" % (
