@@ -40,7 +40,8 @@ def main():
     waves = [w for w in range(TW - 1) if a[w, 5, 0] != 0]   # (slot 15: the chain segments)
     nw = len(waves)
     ncw = 2 if wl == "c5" else 1   # chain waves of the workload's instance (the gamma batch: two)
-    chain, rec, chain0 = waves[-2], waves[-1], waves[-1 - ncw]
+    # roles (NUSI_BS_SIMDMAP, the default): push waves, the record wave, then the chain waves
+    rec, chain0, chain = waves[-1 - ncw], waves[-ncw], waves[-1]
     nb = int(np.max(np.nonzero(a[chain, :, 3])[0])) + 1
     sl = slice(4, nb - 4)
     st = a[:, sl, :]
@@ -48,7 +49,7 @@ def main():
     print("%s: %s, %d waves, %d blocks traced; block period median %d cycles (mean %.0f, p90 %d)" % (
         wl, plan.kernels()[1], nw, nb, np.median(period), period.mean(), np.quantile(period, 0.9)))
     for w in waves:
-        kind = "chain" if chain0 <= w < rec else "record" if w == rec else "push"
+        kind = "chain" if w >= chain0 else "record" if w == rec else "push"
         A = st[w, :, 1] - st[w, :, 0]
         B = st[w, :, 3] - st[w, :, 2]
         print("  wave %2d %-6s phase A busy %6d  phase B busy %6d  (medians)" % (w, kind, np.median(A), np.median(B)))
