@@ -642,7 +642,10 @@ using DirectLeaves = DirectLeavesT<false>;
 //   ted[v * ct + t], sed[v * cs + s], mbv[v * kAlphaTile + j] (shared edge / m-bin fields),
 //   tedm[t] = L2, sedm[s] = Ls, sedm[cs + s] = cS, mbm[j] = atd (this point's member fields),
 //   xl[s * kAlphaTile + n bin], yl[m bin * ct + t]
-constexpr int kAlphaTile = 15;
+#ifndef NUSI_ALPHA_TILE   // A/B: bins per alpha tile side (the edges of a core tile side are kAlphaTile + 1 <= 17)
+#define NUSI_ALPHA_TILE 15
+#endif
+constexpr int kAlphaTile = NUSI_ALPHA_TILE;
 constexpr int kCornerShared = 7, kCornerMember = 3;   // L LL TU1 TU2 G Drr Dri | Dcr Dci A
 struct TileLeaves {
     const double *cor, *corm, *ted, *sed, *mbv, *tedm, *sedm, *mbm, *xl, *yl;
