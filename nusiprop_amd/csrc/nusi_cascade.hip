@@ -1943,6 +1943,9 @@ void k_cascade_gb(GridDev g, const Point* __restrict__ pts, const int* __restric
 #ifndef NUSI_BS_SIMDMAP   // the chain and record waves beside the least-busy push waves (wave w runs on SIMD f(w % 4),
 #define NUSI_BS_SIMDMAP 1    // HW_ID in the trace build): C5 cascade 3.19 -> 2.82 ms, C3 23.4 -> 21.4, C4 equal
 #endif                       // (profiles/r4/ab/r4u, r4v); 0 = the push waves' rows in wave order
+#ifndef NUSI_BS_LONG32   // A/B: step passes of 32 on long grids (<32, 1, 1, 6, 1>: 14 push waves of 96 rows)
+#define NUSI_BS_LONG32 0
+#endif
 #ifndef NUSI_BS_PRIO   // the chain and record waves at raised issue priority (s_setprio 3; the push waves 0): C5
 #define NUSI_BS_PRIO 1    // cascade 3.51 -> 3.25 ms, C3 29.1 -> 24.8, C4 0.555 -> 0.528 (profiles/r4/ab/r4n, r4o); 0 = off.
 #endif                    // Sleeping the push waves at phase B's start (to let the chain's loads first) measured no gain
@@ -2557,6 +2560,7 @@ int cascade_bs_config(const GridDev& g, int P)
     if (P == 1) {
         if (nj && bs_fits_t<48, 1, 1, 4, 1>(g)) return nj;
         if (bs_fits_t<48, 1, 1, 4, 1>(g)) return 48;
+        if (NUSI_BS_LONG32 && bs_fits_t<32, 1, 1, 6, 1>(g)) return 32 + 2000;   // 96-row push waves, passes of 32
         if (bs_fits_t<16, 1, 1, 8, 1>(g)) return 16 + 1000;   // 128-row push waves
         return 0;
     }
@@ -2577,6 +2581,9 @@ hipError_t launch_cascade_bs(const GridDev& g, const Point* pts, int P, const in
         case 16: launch_bs_t<16, 1, 1, 4, 1>(g, pts, gidx, grp, nwg, t, fh, flux, flux_fla, s); break;
         case 32: launch_bs_t<32, 1, 1, 4, 1>(g, pts, gidx, grp, nwg, t, fh, flux, flux_fla, s); break;
         case 48: launch_bs_t<48, 1, 1, 4, 1>(g, pts, gidx, grp, nwg, t, fh, flux, flux_fla, s); break;
+#if NUSI_BS_LONG32
+        case 2032: launch_bs_t<32, 1, 1, 6, 1>(g, pts, gidx, grp, nwg, t, fh, flux, flux_fla, s); break;
+#endif
         default: launch_bs_t<16, 1, 1, 8, 1>(g, pts, gidx, grp, nwg, t, fh, flux, flux_fla, s); break;
         }
     } else if (P == 2) {
