@@ -61,6 +61,25 @@ def test_bs_one_point_equals_ws(nusi, oracle_mod, N):
 
 
 @pytest.mark.parametrize("N", [100, 300])
+def test_bs_all_non_resonant_instance(nusi, oracle_mod, N):
+    """A launch whose points are all non-resonant runs k_cascade_bs's kNR instance (the resonant-only terms compiled
+    out); a launch with one resonant point runs the per-point-flag instance.  The non-resonant points get the same
+    bits from both, in every grouping (one point per workgroup, pairs, a gamma batch)."""
+    base = dict(cases.C2B_100, N_bins_E=N, mphi=2e6, g=0.1)
+    nr = [dict(base, si=2.0 + 0.1 * k) for k in range(6)] + [dict(base, mphi=6e5, g=0.01, si=2.3),
+                                                            dict(base, mphi=6e5, g=0.01, si=2.6),
+                                                            dict(base, mphi=9e5, g=0.3, majorana=False, source_model=0)]
+    res = [dict(base, mphi=3e7, g=0.8, non_resonant=False)]
+    for rhs in (1, 0):
+        opts = dict(cascade_rhs=1) if rhs else {}
+        a = _run(nusi, nr, 2, **opts)
+        b = _run(nusi, nr + res, 2, **opts)
+        assert "k_cascade_bs" in a[3][1] and "k_cascade_bs" in b[3][1], (a[3], b[3])
+        assert np.array_equal(a[0], b[0][:len(nr)]) and np.array_equal(a[1], b[1][:len(nr)])
+    _vs_oracle(nusi, oracle_mod, nr + res, b[1], b[2])
+
+
+@pytest.mark.parametrize("N", [100, 300])
 def test_bs_pairs_and_gamma_batches(nusi, oracle_mod, N):
     """Points sharing a table: pairs (k_cascade_bs_pairs) and gamma batches of 3..16 (k_cascade_bs_gamma), mixed
     sources in one batch; each point equals its one-point-per-workgroup flux bit for bit and the oracle's to
