@@ -1173,7 +1173,7 @@ int nusi_plan_evolve(nusi_plan* pl, const nusi_params* pts, int n, double* d_flu
         for (int w = 0; w < 3; ++w) {
             if (bs_nwg[w]) {
                 HIPCHECK(nusi::launch_cascade_bs(pl->gd, pl->d_pts, Pk[w], pl->d_gidx, pl->d_gbgrp + off, bs_nwg[w], pl->tabs,
-                                                 fh, d_flux, d_fla, s));
+                                                 fh, d_flux, d_fla, s, all_nr));
                 mask |= 1 << w;
             }
             fh += nusi::cascade_bs_scratch_doubles(pl->gd, Pk[w]) * bs_nwg[w];

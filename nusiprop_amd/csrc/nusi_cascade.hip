@@ -1967,7 +1967,7 @@ enum { BR_RZ0, BR_RZ1, BR_RZ2, BR_L10, BR_L20, BR_L21, BR_U01, BR_U02, BR_U12, B
        kBsFields };
 static_assert(PR_L10 - 1 == BR_L10 && PR_RU22 - 1 == BR_RU22 && kPreFields - 1 == BR_PERM, "record_phase2's fields, shifted");
 
-template <int NJ, int P, int SPL, int RT, int CW>
+template <int NJ, int P, int SPL, int RT, int CW, bool kNR>   // kNR: every point of the launch non-resonant
 __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4, 4)))
 void k_cascade_bs(GridDev g, const Point* __restrict__ pts, const int* __restrict__ gidx, const int2* __restrict__ grp,
                   TablesDev t, double* __restrict__ fh, double* __restrict__ flux, double* __restrict__ flux_fla)
@@ -2059,7 +2059,7 @@ void k_cascade_bs(GridDev g, const Point* __restrict__ pts, const int* __restric
             pw[(size_t)p * (T + 2) + e] = nm::pow(E / 1e14 * (1 + g.z[i]), -Q.si);
         }
     }
-    const bool nonres = P0.non_resonant;   // the points of a workgroup share a table, hence the flags
+    const bool nonres = kNR || P0.non_resonant;   // the points of a workgroup share a table, hence the flags
     const int npass = (nst + NJ - 1) / NJ;
     double* const fhw = fh + (size_t)blockIdx.x * 3 * N * P;   // this workgroup's F FIFO [3][N][P] (passes > 1)
     int jb = 0, njp = 0, Ts = 0, c0 = 0, nblk = 0;
@@ -2545,12 +2545,16 @@ static bool bs_fits_t(const GridDev& g)
 }
 template <int NJ, int P, int SPL, int RT, int CW>
 static void launch_bs_t(const GridDev& g, const Point* pts, const int* gidx, const int2* grp, int nwg, TablesDev t,
-                        double* fh, double* flux, double* flux_fla, hipStream_t s)
+                        double* fh, double* flux, double* flux_fla, hipStream_t s, bool all_nr)
 {
     const int nthr = 64 * (bs_push_waves(g, RT) + CW + 1);
     const size_t lds = bs_lds<NJ, P, SPL, RT, CW>(g);
-    hipLaunchKernelGGL((k_cascade_bs<NJ, P, SPL, RT, CW>), dim3(nwg), dim3(nthr), lds, s, g, pts, gidx, grp, t, fh, flux,
-                       flux_fla);
+    if (all_nr)   // the instance without the resonant-only running sum (every BASELINE workload)
+        hipLaunchKernelGGL((k_cascade_bs<NJ, P, SPL, RT, CW, true>), dim3(nwg), dim3(nthr), lds, s, g, pts, gidx, grp, t, fh,
+                           flux, flux_fla);
+    else
+        hipLaunchKernelGGL((k_cascade_bs<NJ, P, SPL, RT, CW, false>), dim3(nwg), dim3(nthr), lds, s, g, pts, gidx, grp, t,
+                           fh, flux, flux_fla);
 }
 // P = 1: <wf_nj, 1, 1, 4, 1> for one pass of up to 48 steps, else step passes of 48 (rows <= 14 x 64) or of 16 (rows
 // <= 14 x 128); P = 2: <wf_nj or 48, 2, 1, 2, 2>; P = 16 (the gamma batch): <6, 16, 1, 2, 2>
@@ -2570,7 +2574,7 @@ int cascade_bs_config(const GridDev& g, int P)
 }
 size_t cascade_bs_scratch_doubles(const GridDev& g, int P) { return (size_t)3 * g.N * P; }
 hipError_t launch_cascade_bs(const GridDev& g, const Point* pts, int P, const int* gidx, const int2* grp, int nwg,
-                             TablesDev t, double* fh, double* flux, double* flux_fla, hipStream_t s)
+                             TablesDev t, double* fh, double* flux, double* flux_fla, hipStream_t s, bool all_nr)
 {
     if (nwg <= 0) return hipSuccess;
     const int c = cascade_bs_config(g, P);
@@ -2578,24 +2582,24 @@ hipError_t launch_cascade_bs(const GridDev& g, const Point* pts, int P, const in
     if (P == 1) {
         t_cascade_kernel = "k_cascade_bs";
         switch (c) {
-        case 16: launch_bs_t<16, 1, 1, 4, 1>(g, pts, gidx, grp, nwg, t, fh, flux, flux_fla, s); break;
-        case 32: launch_bs_t<32, 1, 1, 4, 1>(g, pts, gidx, grp, nwg, t, fh, flux, flux_fla, s); break;
-        case 48: launch_bs_t<48, 1, 1, 4, 1>(g, pts, gidx, grp, nwg, t, fh, flux, flux_fla, s); break;
+        case 16: launch_bs_t<16, 1, 1, 4, 1>(g, pts, gidx, grp, nwg, t, fh, flux, flux_fla, s, all_nr); break;
+        case 32: launch_bs_t<32, 1, 1, 4, 1>(g, pts, gidx, grp, nwg, t, fh, flux, flux_fla, s, all_nr); break;
+        case 48: launch_bs_t<48, 1, 1, 4, 1>(g, pts, gidx, grp, nwg, t, fh, flux, flux_fla, s, all_nr); break;
 #if NUSI_BS_LONG32
-        case 2032: launch_bs_t<32, 1, 1, 6, 1>(g, pts, gidx, grp, nwg, t, fh, flux, flux_fla, s); break;
+        case 2032: launch_bs_t<32, 1, 1, 6, 1>(g, pts, gidx, grp, nwg, t, fh, flux, flux_fla, s, all_nr); break;
 #endif
-        default: launch_bs_t<16, 1, 1, 8, 1>(g, pts, gidx, grp, nwg, t, fh, flux, flux_fla, s); break;
+        default: launch_bs_t<16, 1, 1, 8, 1>(g, pts, gidx, grp, nwg, t, fh, flux, flux_fla, s, all_nr); break;
         }
     } else if (P == 2) {
         t_cascade_kernel = "k_cascade_bs_pairs";
         switch (c) {
-        case 16: launch_bs_t<16, 2, 1, 2, 2>(g, pts, gidx, grp, nwg, t, fh, flux, flux_fla, s); break;
-        case 32: launch_bs_t<32, 2, 1, 2, 2>(g, pts, gidx, grp, nwg, t, fh, flux, flux_fla, s); break;
-        default: launch_bs_t<48, 2, 1, 2, 2>(g, pts, gidx, grp, nwg, t, fh, flux, flux_fla, s); break;
+        case 16: launch_bs_t<16, 2, 1, 2, 2>(g, pts, gidx, grp, nwg, t, fh, flux, flux_fla, s, all_nr); break;
+        case 32: launch_bs_t<32, 2, 1, 2, 2>(g, pts, gidx, grp, nwg, t, fh, flux, flux_fla, s, all_nr); break;
+        default: launch_bs_t<48, 2, 1, 2, 2>(g, pts, gidx, grp, nwg, t, fh, flux, flux_fla, s, all_nr); break;
         }
     } else {
         t_cascade_kernel = "k_cascade_bs_gamma";
-        launch_bs_t<6, 16, 1, 2, 2>(g, pts, gidx, grp, nwg, t, fh, flux, flux_fla, s);
+        launch_bs_t<6, 16, 1, 2, 2>(g, pts, gidx, grp, nwg, t, fh, flux, flux_fla, s, all_nr);
     }
     return hipGetLastError();
 }

@@ -92,7 +92,7 @@ hipError_t launch_cascade_gb(const GridDev& g, const Point* pts, const int* gidx
 int cascade_bs_config(const GridDev& g, int P);
 size_t cascade_bs_scratch_doubles(const GridDev& g, int P);
 hipError_t launch_cascade_bs(const GridDev& g, const Point* pts, int P, const int* gidx, const int2* grp, int nwg,
-                             TablesDev t, double* fh, double* flux, double* flux_fla, hipStream_t s);
+                             TablesDev t, double* fh, double* flux, double* flux_fla, hipStream_t s, bool all_nr);
 size_t cascade_src_doubles(const GridDev& g);   // t.Src doubles per point
 hipError_t launch_source_dsnb(const GridDev& g, const Point* pts, int npts, double* src, hipStream_t s);
 // The bit-exact scalar cascades (NUSI_CASCADE_WAVEFRONT / REG / LDS; a kind that does not fit the grid falls

@@ -62,9 +62,9 @@ def test_bs_one_point_equals_ws(nusi, oracle_mod, N):
 
 @pytest.mark.parametrize("N", [100, 300])
 def test_bs_all_non_resonant_instance(nusi, oracle_mod, N):
-    """The non-resonant points of a launch get the same bits whether or not a resonant point shares the launch, in
-    every grouping (one point per workgroup, pairs, a gamma batch): the guard for an all-non-resonant instance of
-    k_cascade_bs with the resonant-only terms compiled out (measured in r4ae)."""
+    """A launch whose points are all non-resonant runs k_cascade_bs's kNR instance (the resonant-only terms compiled
+    out); a launch with one resonant point runs the per-point-flag instance.  The non-resonant points get the same
+    bits from both, in every grouping (one point per workgroup, pairs, a gamma batch)."""
     base = dict(cases.C2B_100, N_bins_E=N, mphi=2e6, g=0.1)
     nr = [dict(base, si=2.0 + 0.1 * k) for k in range(6)] + [dict(base, mphi=6e5, g=0.01, si=2.3),
                                                             dict(base, mphi=6e5, g=0.01, si=2.6),

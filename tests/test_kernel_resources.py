@@ -26,8 +26,10 @@ BUDGET = {
     # the block-synchronous cascade: 96 B of private segment are the prologue's pow() call frames (no spills)
     r"k_cascade_bsILi(16|32)ELi1ELi1ELi4ELi1E": (0, 96),
     # (the wave index is readfirstlane'd: per-wave row bases in SGPRs; as VGPRs they spilled 19 / 33 into the push)
-    r"k_cascade_bsILi48ELi1ELi1ELi4ELi1E": (4, 96),
-    r"k_cascade_bsILi16ELi1ELi1ELi8ELi1E": (10, 128),
+    r"k_cascade_bsILi48ELi1ELi1ELi4ELi1ELb0E": (2, 96),
+    # the all-non-resonant instance (kNR): 4 spills / 112 B, outside the MFMA loop; C4 cascade 0.477 vs 0.562 ms (r4ae)
+    r"k_cascade_bsILi48ELi1ELi1ELi4ELi1ELb1E": (4, 112),
+    r"k_cascade_bsILi16ELi1ELi1ELi8ELi1E": (6, 128),
     r"k_cascade_bsILi(16|32)ELi2ELi1ELi2ELi2E": (0, 96),
     r"k_cascade_bsILi48ELi2ELi1ELi2ELi2E": (4, 112),
     r"k_cascade_bsILi6ELi16ELi1ELi2ELi2E": (4, 112),
