@@ -1,0 +1,332 @@
+// nuSIprop MI355X -- GSL's dilogarithm algorithms, the arithmetic of NUSI_OPT_REFERENCE_ORDER.
+//
+// The reference evaluates its closed forms with GSL (version unpinned, the Homebrew build of setup.py:10-11):
+//   gsl_sf_dilog(x)                      aux.hpp:112,129,147,165   nuSIprop.hpp:1098,1202,1375-1398
+//   gsl_sf_complex_dilog_xy_e(x, y, ..)  aux.hpp:92-93             nuSIprop.hpp:1444-1451
+// Where the closed forms cancel (the s-t / s-u interference of Gamma, alphaTilde and alpha), a one-ulp change in a
+// dilogarithm moves a table entry by up to 1e-6, so "the reference's arithmetic" means GSL's algorithm, not just
+// an accurate Li2.  These functions are GSL 2.x specfunc/dilog.c (with clausen.c, log.c's complex log, trig.c's
+// angle reduction, cheb_eval.c) restated: the same branch points (real: 0.25 / 0.5 / 1 / 1.01 / 2 and the x < 0
+// reduction; complex: |z|^2 ~ 1 Lewin, 1/z for |z| > 1, 1 - z for x > 0.732, series_1 / series_2 / series_3 at
+// |z| 0.25 / 0.98), series, loop bounds and stopping tests, in the same operation order, on this repository's
+// shared libm (nm::log, nm::atan2) -- the oracle runs the same sequence (oracle/ora_gsl.c), bit for bit.
+//
+// Two rewrites are exact, not approximations:
+//   * GSL stops a series when fabs(a / b) < 2^-p (p = 52, 53 or 104).  For a, b >= 0 and b 2^-p a normal number,
+//     RN(a / b) < 2^-p  <=>  a < b 2^-p: the doubles below 2^-p b are those at or below its predecessor, which
+//     lies below the rounding boundary 2^-p b (1 - 2^-54).  So the test is one multiply and one compare
+//     (quot_lt; the division where b < 2^-900);
+//   * series_1 / series_2_c share one loop (cseries): the same recurrence with the term's denominator k^2 or
+//     k^2 (k + 1), so a wave whose lanes take different series runs one loop, not two.
+#pragma once
+
+#include "nusi_libm.hpp"
+
+namespace nusi {
+namespace gsl {
+
+constexpr double kEps = 2.2204460492503131e-16;       // GSL_DBL_EPSILON
+constexpr double kSqrtEps = 1.4901161193847656e-08;   // GSL_SQRT_DBL_EPSILON
+constexpr double kPiD = 3.14159265358979323846;       // M_PI
+
+// fabs(a / b) < c of GSL's stopping tests for a, b >= 0 and c a power of two (header comment)
+NUSI_FN bool quot_lt(double a, double b, double c)
+{
+    if (b >= 0x1p-900) return a < b * c;
+    return a / b < c;
+}
+
+// hypot(x, y) (libm; dilogc_unitdisk): sqrt(a^2 + b^2) and one correction step from the exact residual
+// (oracle/ora_gsl.c ora_hypot)
+NUSI_FN double hypot(double x, double y)
+{
+    double a = fabs(x), b = fabs(y);
+    if (a < b) { const double t = a; a = b; b = t; }
+    if (b == 0.0 || !(a <= 1.79769313486231570815e+308)) return a + b;
+    double s = 1.0;
+    if (a > 0x1p+500) { a *= 0x1p-600; b *= 0x1p-600; s = 0x1p+600; }
+    else if (b < 0x1p-500) { a *= 0x1p+600; b *= 0x1p+600; s = 0x1p-600; }
+    const double a2 = a * a, ea = fma(a, a, -a2), b2 = b * b, eb = fma(b, b, -b2);
+    double h = sqrt(a2 + b2);
+    const double h2 = h * h, eh = fma(h, h, -h2);
+    const double r = ((a2 - h2) + b2) + ((ea + eb) - eh);
+    h = h + r / (2.0 * h);
+    return h * s;
+}
+
+// ------------------------------------------------------------------------------------------------- real --
+// dilog_series_1: sum x^k / k^2, 0 < x <= 1/4
+NUSI_FN double dilog_series_1(double x)
+{
+    double sum = x, term = x;
+    for (int k = 2; k < 1000; k++) {
+        const double rk = (k - 1.0) / k;
+        term *= x;
+        term *= rk * rk;
+        sum += term;
+        if (quot_lt(fabs(term), fabs(sum), 0x1p-52)) break;   // fabs(term / sum) < GSL_DBL_EPSILON
+    }
+    return sum;
+}
+// series_2: sum r^k / (k^2 (k + 1)), the first nine terms unconditionally
+NUSI_FN double series_2(double r)
+{
+    double rk = r, sum = 0.5 * r;
+    int k;
+    for (k = 2; k < 10; k++) {
+        rk *= r;
+        sum += rk / (k * k * (k + 1.0));
+    }
+    for (; k < 100; k++) {
+        rk *= r;
+        const double ds = rk / (k * k * (k + 1.0));
+        sum += ds;
+        if (quot_lt(fabs(ds), fabs(sum), 0x1p-53)) break;   // fabs(ds / sum) < 0.5 GSL_DBL_EPSILON
+    }
+    return sum;
+}
+// dilog_series_2: Li2(x) = 1 + (1 - x) log(1 - x) / x + series_2(x)
+NUSI_FN double dilog_series_2(double x)
+{
+    double val = series_2(x);
+    double t;
+    if (x > 0.01) t = (1.0 - x) * NUSI_PLOG(1.0 - x) / x;
+    else {
+        const double c3 = 1.0 / 3.0, c4 = 1.0 / 4.0, c5 = 1.0 / 5.0, c6 = 1.0 / 6.0, c7 = 1.0 / 7.0, c8 = 1.0 / 8.0;
+        const double t68 = c6 + x * (c7 + x * c8);
+        const double t38 = c3 + x * (c4 + x * (c5 + x * t68));
+        t = (x - 1.0) * (1.0 + x * (0.5 + x * t38));
+    }
+    val += 1.0 + t;
+    return val;
+}
+// dilog_xge0: Re Li2(x), x >= 0
+NUSI_FN double dilog_xge0(double x)
+{
+    if (x > 2.0) {
+        const double ser = dilog_series_2(1.0 / x);
+        const double log_x = NUSI_PLOG(x);
+        const double t1 = kPiD * kPiD / 3.0, t2 = ser, t3 = 0.5 * log_x * log_x;
+        return t1 - t2 - t3;
+    }
+    if (x > 1.01) {
+        const double ser = dilog_series_2(1.0 - 1.0 / x);
+        const double log_x = NUSI_PLOG(x);
+        const double log_term = log_x * (NUSI_PLOG(1.0 - 1.0 / x) + 0.5 * log_x);
+        const double t1 = kPiD * kPiD / 6.0, t2 = ser, t3 = log_term;
+        return t1 + t2 - t3;
+    }
+    if (x > 1.0) {   // series around x = 1
+        const double eps = x - 1.0, lne = NUSI_PLOG(eps);
+        const double c0 = kPiD * kPiD / 6.0, c1 = 1.0 - lne, c2 = -(1.0 - 2.0 * lne) / 4.0, c3 = (1.0 - 3.0 * lne) / 9.0;
+        const double c4 = -(1.0 - 4.0 * lne) / 16.0, c5 = (1.0 - 5.0 * lne) / 25.0, c6 = -(1.0 - 6.0 * lne) / 36.0;
+        const double c7 = (1.0 - 7.0 * lne) / 49.0, c8 = -(1.0 - 8.0 * lne) / 64.0;
+        return c0 + eps * (c1 + eps * (c2 + eps * (c3 + eps * (c4 + eps * (c5 + eps * (c6 + eps * (c7 + eps * c8)))))));
+    }
+    if (x == 1.0) return kPiD * kPiD / 6.0;
+    if (x > 0.5) {
+        const double ser = dilog_series_2(1.0 - x);
+        const double log_x = NUSI_PLOG(x);
+        const double t1 = kPiD * kPiD / 6.0, t2 = ser, t3 = log_x * NUSI_PLOG(1.0 - x);
+        return t1 - t2 - t3;
+    }
+    if (x > 0.25) return dilog_series_2(x);
+    if (x > 0.0) return dilog_series_1(x);
+    return 0.0;
+}
+
+// ---------------------------------------------------------------------------------------------- Clausen --
+// gsl_sf_angle_restrict_pos_e (trig.c): [0, 2 pi) with the synthetic extended-precision 2 pi
+NUSI_FN double angle_restrict_pos(double theta)
+{
+    const double P1 = 4 * 7.85398125648498535156e-01, P2 = 4 * 3.77489470793079817668e-08;
+    const double P3 = 4 * 2.69515142907905952645e-15, TwoPi = 2 * (P1 + P2 + P3);
+    const double y = 2 * floor(theta / TwoPi);
+    double r = ((theta - y * P1) - y * P2) - y * P3;
+    if (r > TwoPi) r = (((r - 2 * P1) - 2 * P2) - 2 * P3);
+    else if (r < 0) r = (((r + 2 * P1) + 2 * P2) + 2 * P3);
+    return r;
+}
+// gsl_sf_clausen_e: Cl2(x); aclaus_cs (clausen.c) summed by cheb_eval_e (order 14 on [-1, 1])
+NUSI_FN double clausen(double x)
+{
+    constexpr double kC[15] = {2.142694363766688447e+00, 0.723324281221257925e-01, 0.101642475021151164e-02,
+                               0.3245250328531645e-04,   0.133315187571472e-05,    0.6213240591653e-07,
+                               0.313004135337e-08,       0.16635723056e-09,        0.919659293e-11,
+                               0.52400462e-12,           0.3058040e-13,            0.18197e-14,
+                               0.1100e-15,               0.68e-17,                 0.4e-18};
+    const double x_cut = kPiD * kSqrtEps;
+    double sgn = 1.0;
+    if (x < 0.0) { x = -x; sgn = -1.0; }
+    x = angle_restrict_pos(x);
+    if (x > kPiD) {
+        const double p0 = 6.28125, p1 = 0.19353071795864769253e-02;
+        x = (p0 - x) + p1;
+        sgn = -sgn;
+    }
+    double val;
+    if (x == 0.0) val = 0.0;
+    else if (x < x_cut) val = x * (1.0 - NUSI_PLOG(x));
+    else {
+        const double t = 2.0 * (x * x / (kPiD * kPiD) - 0.5);
+        const double a = -1.0, b = 1.0;
+        double d = 0.0, dd = 0.0;
+        const double yy = (2.0 * t - a - b) / (b - a), y2 = 2.0 * yy;
+#pragma unroll
+        for (int j = 14; j >= 1; j--) {
+            const double temp = d;
+            d = y2 * d - dd + kC[j];
+            dd = temp;
+        }
+        d = yy * d - dd + 0.5 * kC[0];
+        val = x * (d - NUSI_PLOG(x));
+    }
+    return val * sgn;
+}
+
+// ---------------------------------------------------------------------------------------------- complex --
+// dilogc_series_1 (s2 = false: sum r^k e^(i k theta) / k^2, first term r e^(i theta), kmax 50 + 22 / (-log r))
+// and series_2_c (s2 = true: sum z^k / (k^2 (k + 1)), first term r e^(i theta) / 2, kmax 30 + 18 / (-log r)) as
+// one loop; every operation is GSL's (the denominators (double) k * k and (double) k * k * (k + 1.0) are exact)
+NUSI_FN void cseries(bool s2, double r, double x, double y, double& re, double& im)
+{
+    const double cos_theta = x / r, sin_theta = y / r;
+    const double alpha = 1.0 - cos_theta, beta = sin_theta;
+    double ck = cos_theta, sk = sin_theta, rk = r;
+    double real_sum = s2 ? 0.5 * r * ck : r * ck;
+    double imag_sum = s2 ? 0.5 * r * sk : r * sk;
+    const double nlr = -NUSI_PLOG(r);
+    const int kmax = s2 ? 30 + (int)(18.0 / nlr) : 50 + (int)(22.0 / nlr);
+    for (int k = 2; k < kmax; k++) {
+        const double ck_tmp = ck;
+        ck = ck - (alpha * ck + beta * sk);
+        sk = sk - (alpha * sk - beta * ck_tmp);
+        rk *= r;
+        const double kk = (double)k * k;
+        const double q = rk / (s2 ? kk * (k + 1.0) : kk);
+        const double dr = q * ck, di = q * sk;
+        real_sum += dr;
+        imag_sum += di;
+        if (quot_lt(dr * dr + di * di, real_sum * real_sum + imag_sum * imag_sum, 0x1p-104)) break;
+    }
+    re = real_sum;
+    im = imag_sum;
+}
+// dilogc_series_3: |z| near 1, sum_{n <= 6} (log r)^n / n! H_n(theta)
+NUSI_FN void cseries_3(double r, double x, double y, double& re, double& im)
+{
+    const double theta = NUSI_PATAN2(y, x);
+    const double cos_theta = x / r, sin_theta = y / r;
+    const double a = NUSI_PLOG(r);
+    const double omc = 1.0 - cos_theta, omc2 = omc * omc;
+    double H_re[7], H_im[7];
+    H_re[0] = kPiD * kPiD / 6.0 + 0.25 * (theta * theta - 2.0 * kPiD * fabs(theta));
+    H_im[0] = clausen(theta);
+    H_re[1] = -0.5 * NUSI_PLOG(2.0 * omc);
+    H_im[1] = -NUSI_PATAN2(-sin_theta, omc);
+    H_re[2] = -0.5;
+    H_im[2] = 0.5 * sin_theta / omc;
+    H_re[3] = -0.5 / omc;
+    H_im[3] = 0.0;
+    H_re[4] = 0.0;
+    H_im[4] = -0.5 * sin_theta / omc2;
+    H_re[5] = 0.5 * (2.0 + cos_theta) / omc2;
+    H_im[5] = 0.0;
+    H_re[6] = 0.0;
+    H_im[6] = 0.5 * sin_theta / (omc2 * omc2 * omc) * (8.0 * omc - sin_theta * sin_theta * (3.0 + cos_theta));
+    double sum_re = H_re[0], sum_im = H_im[0], an = 1.0, nfact = 1.0;
+#pragma unroll
+    for (int n = 1; n <= 6; n++) {
+        an *= a;
+        nfact *= n;
+        const double t = an / nfact;
+        sum_re += t * H_re[n];
+        sum_im += t * H_im[n];
+    }
+    re = sum_re;
+    im = sum_im;
+}
+// dilogc_fundamental (r < 1, x <= 0.732): series_3 above r = 0.98, dilogc_series_2 above 0.25, else series_1
+NUSI_FN void fundamental(double r, double x, double y, double& re, double& im)
+{
+    if (r > 0.98) {
+        cseries_3(r, x, y, re, im);
+        return;
+    }
+    const bool s2 = r > 0.25;
+    double sre, sim;
+    cseries(s2, r, x, y, sre, sim);
+    if (!s2) {
+        re = sre;
+        im = sim;
+        return;
+    }
+    // dilogc_series_2: + (1 - z) log(1 - z) / z + 1, log(1 - z) by gsl_sf_complex_log_e
+    const double zr = 1.0 - x, zi = -y;
+    const double ax = fabs(zr), ay = fabs(zi);
+    const double mn = ax < ay ? ax : ay, mx = ax > ay ? ax : ay;
+    const double ln_r = NUSI_PLOG(mx) + 0.5 * NUSI_PLOG(1.0 + (mn / mx) * (mn / mx));
+    const double ln_t = NUSI_PATAN2(zi, zr);
+    const double t_x = (ln_r * x + ln_t * y) / (r * r);
+    const double t_y = (-ln_r * y + ln_t * x) / (r * r);
+    const double r_x = (1.0 - x) * t_x + y * t_y;
+    const double r_y = (1.0 - x) * t_y - y * t_x;
+    re = sre + r_x + 1.0;
+    im = sim + r_y;
+}
+// dilogc_unitdisk: |z| < 1; x > 0.732 reflected, Li2(z) = -Li2(1 - z) + zeta2 - log(z) log(1 - z)
+NUSI_FN void unitdisk(double x, double y, double& re, double& im)
+{
+    const double zeta2 = kPiD * kPiD / 6.0;
+    const double r = gsl::hypot(x, y);
+    if (x > 0.732) {
+        const double x_tmp = 1.0 - x, y_tmp = -y;
+        const double r_tmp = gsl::hypot(x_tmp, y_tmp);
+        double re_tmp, im_tmp;
+        fundamental(r_tmp, x_tmp, y_tmp, re_tmp, im_tmp);
+        const double lnz = NUSI_PLOG(r), lnomz = NUSI_PLOG(r_tmp);
+        const double argz = NUSI_PATAN2(y, x), argomz = NUSI_PATAN2(y_tmp, x_tmp);
+        re = -re_tmp + zeta2 - lnz * lnomz + argz * argomz;
+        im = -im_tmp - argz * lnomz - argomz * lnz;
+        return;
+    }
+    fundamental(r, x, y, re, im);
+}
+
+}  // namespace gsl
+
+// gsl_sf_dilog (x < 0: -dilog_xge0(-x) + dilog_xge0(x^2) / 2)
+NUSI_FN_OUT double gsl_li2(double x)
+{
+    if (x >= 0.0) return gsl::dilog_xge0(x);
+    const double d1 = gsl::dilog_xge0(-x), d2 = gsl::dilog_xge0(x * x);
+    return -d1 + 0.5 * d2;
+}
+
+// gsl_sf_complex_dilog_xy_e
+NUSI_FN_OUT cd gsl_cli2(double x, double y)
+{
+    const double zeta2 = gsl::kPiD * gsl::kPiD / 6.0;
+    const double r2 = x * x + y * y;
+    if (y == 0.0) return cd{gsl_li2(x), (x >= 1.0) ? -gsl::kPiD * NUSI_PLOG(x) : 0.0};
+    if (fabs(r2 - 1.0) < gsl::kEps) {   // Lewin A.2.4.1 / A.2.4.2
+        const double theta = NUSI_PATAN2(y, x);
+        const double term1 = theta * theta / 4.0, term2 = gsl::kPiD * fabs(theta) / 2.0;
+        return cd{zeta2 + term1 - term2, gsl::clausen(theta)};
+    }
+    double re, im;
+    if (r2 < 1.0) {
+        gsl::unitdisk(x, y, re, im);
+        return cd{re, im};
+    }
+    // 1/z into the unit disk, unwound with Li2(z) + Li2(1/z) = -zeta2 - log(-z)^2 / 2
+    const double r = sqrt(r2);
+    gsl::unitdisk(x / r2, -y / r2, re, im);
+    const double theta = NUSI_PATAN2(y, x), theta_abs = fabs(theta), theta_sgn = (theta < 0.0 ? -1.0 : 1.0);
+    const double ln_minusz_re = NUSI_PLOG(r), ln_minusz_im = theta_sgn * (theta_abs - gsl::kPiD);
+    const double lmz2_re = ln_minusz_re * ln_minusz_re - ln_minusz_im * ln_minusz_im;
+    const double lmz2_im = 2.0 * ln_minusz_re * ln_minusz_im;
+    return cd{-re - 0.5 * lmz2_re - zeta2, -im - 0.5 * lmz2_im};
+}
+
+}  // namespace nusi

@@ -231,7 +231,7 @@ __global__ __launch_bounds__(kTileThreads) NUSI_TILE_ATTR void k_alpha_tile(Grid
         if (nonres && maj) {
             const double* edgk = edg + k * alpha_tile_edge_stride(cs, ct);
             for (int j = tid; j < cc; j += kTileThreads) {   // corner j: shared leaves, then each point's
-                alpha_tile_corner_job(j, edgk, ct, cs, cor);
+                alpha_tile_corner_job<kRef>(j, edgk, ct, cs, cor);
 #pragma unroll 1
                 for (int q = 0; q < nb; ++q) alpha_tile_corner_member_job<kRef>(pts[p0 + q], q, j, edgk, ct, cs, cor);
             }
@@ -309,9 +309,10 @@ static_assert(kBatchQC * (2 * (kAlphaTile + 1) + kAlphaTile) <= kTileThreads, "o
 // the batch-shared phases out of line: they run once per batch, and inlined their working sets raise the register
 // pressure of the per-point loop (measured slower: round 1 profiles/r1e, round 2 profiles/r2s, r2aa)
 #define NUSI_BCOLD __device__ __attribute__((noinline))
+template <bool kRef>
 NUSI_BCOLD void b_corner(int j, const double* edgk, int ct, int cs, double* per, double* tmp)
 {
-    alpha_batch_corner_job(j, edgk, ct, cs, per, tmp);
+    alpha_batch_corner_job<kRef>(j, edgk, ct, cs, per, tmp);
 }
 NUSI_BCOLD void b_xshared(int j, const double* edgk, int ct, int cs, double* X) { alpha_batch_xshared_job(j, edgk, ct, cs, X); }
 // The leaves the batch's shared brackets read (alpha_k_pre, alpha_k_pp): the shared corner blocks P3 | tmp, the
@@ -434,7 +435,7 @@ void k_alpha_batch(GridDev g, const Point* __restrict__ pts, const SplineSet* __
         AlphaPre pre{};
         PPTerm ppt{0.0, 1.0, 1.0};
         if (cornered) {
-            for (int j = tid; j < cc; j += kTileThreads) b_corner(j, edgk, ct, cs, P3, tmp);
+            for (int j = tid; j < cc; j += kTileThreads) b_corner<kRef>(j, edgk, ct, cs, P3, tmp);
             for (int j = tid; j < kAlphaTile * (cs + ct); j += kTileThreads)
                 alpha_batch_mixed_job(j, edgk, ct, cs, tl, th, sl, sh, n0, m0, T, Tm, mix, mix + kAlphaTile * cs);
             __syncthreads();

@@ -216,14 +216,12 @@ NUSI_FN cd cli2_axis(double x, double y)
 }
 
 // principal-branch Li2(x+iy); y == 0 follows gsl_sf_complex_dilog_xy_e.  cli2_body is the inline body
-// (one call site of the big-batch alpha kernel inlines it), cli2 the out-of-line entry point.  kGeneral:
-// no near-axis Taylor shortcut -- the general series everywhere, the operation order of
-// gsl_sf_complex_dilog_xy_e (NUSI_OPT_REFERENCE_ORDER; the oracle's ora_set_reference_order(1))
-template <bool kGeneral = false>
+// (one call site of the big-batch alpha kernel inlines it), cli2 the out-of-line entry point.  The shared-algorithm
+// series; NUSI_OPT_REFERENCE_ORDER runs GSL's own algorithm instead (gsl_cli2, nusi_gsl.hpp)
 NUSI_FN cd cli2_body(double x, double y)
 {
     if (y == 0.0) return cd{li2(x), (x >= 1.0) ? -kPi * NUSI_PLOG(x) : 0.0};
-    if (!kGeneral) {
+    {
         const double ax = fabs(x), a1 = fabs(1.0 - x);
         if (fabs(y) <= kLi2AxisRatio * (ax < a1 ? ax : a1)) return cli2_axis(x, y);
     }
@@ -264,11 +262,21 @@ NUSI_FN cd cli2_body(double x, double y)
     const cd s = (u - 0.25 * u2) + (u * u2) * p;
     return add + sgn * s;
 }
-NUSI_FN_OUT cd cli2(double x, double y) { return cli2_body<false>(x, y); }
+NUSI_FN_OUT cd cli2(double x, double y) { return cli2_body(x, y); }
 NUSI_FN cd cli2(cd z) { return cli2(z.r, z.i); }
-NUSI_FN_OUT cd cli2_general(double x, double y) { return cli2_body<true>(x, y); }
+}  // namespace nusi
+
+#include "nusi_gsl.hpp"
+
+namespace nusi {
+// the dilogarithms of a gsl_sf_dilog / gsl_sf_complex_dilog_xy_e call site: the shared-algorithm series, or
+// (kRef, NUSI_OPT_REFERENCE_ORDER) GSL's algorithm
 template <bool kRef>
-NUSI_FN cd cli2_t(cd z) { return kRef ? cli2_general(z.r, z.i) : cli2(z.r, z.i); }
+NUSI_FN cd cli2_t(cd z) { return kRef ? gsl_cli2(z.r, z.i) : cli2(z.r, z.i); }
+template <bool kRef>
+NUSI_FN cd cli2_t(double x, double y) { return kRef ? gsl_cli2(x, y) : cli2(x, y); }
+template <bool kRef>
+NUSI_FN double li2_t(double x) { return kRef ? gsl_li2(x) : li2(x); }
 
 // Li3(x), x in [-1, 1/2] (the DSNB source only reaches [-1, 0))
 NUSI_FN double li3(double x)
@@ -305,7 +313,7 @@ NUSI_FN cd li2_asym(cd z)
     return -1 / (16. * (z2 * z2)) - 1 / (9. * (z * z * z)) - 1 / (4. * z2) - 1 / z - C(0.0, 0.5) * t;
 }
 
-// aux.hpp:77-96 (kRef: the general complex dilogarithm, NUSI_OPT_REFERENCE_ORDER)
+// aux.hpp:77-96 (kRef: GSL's complex dilogarithm, NUSI_OPT_REFERENCE_ORDER)
 template <bool kRef = false>
 NUSI_FN cd dilogdiff_c(cd x, cd y)
 {
@@ -315,6 +323,7 @@ NUSI_FN cd dilogdiff_c(cd x, cd y)
 }
 
 // aux.hpp:98-113 : Li2(-x) - Li2(-y)
+template <bool kRef = false>
 NUSI_FN double dilogdiff(double x, double y)
 {
     if (x > 1e2 && y > 1e2) {
@@ -325,7 +334,7 @@ NUSI_FN double dilogdiff(double x, double y)
     if (x < 1e-2 && y < 1e-2)
         return -x + x * x / 4. - x * x * x / 9. + (x * x) * (x * x) / 16.
                - (-y + y * y / 4. - y * y * y / 9. + (y * y) * (y * y) / 16.);
-    return li2(-x) - li2(-y);
+    return li2_t<kRef>(-x) - li2_t<kRef>(-y);
 }
 
 // aux.hpp:115-130 : Li2(-1-x) - Li2(-1-y)
@@ -341,11 +350,12 @@ NUSI_FN double d1m_small(double v)
     return -v * ln2 + (v * v * (-1 + ln4)) / 4. + (v * v * v * (5 - 8 * ln2)) / 24.
            + (v * v) * (v * v) * (-1. / 6. + ln2 / 4.);
 }
+template <bool kRef = false>
 NUSI_FN double dilog1mdiff(double x, double y)
 {
     if (x > 1e2 && y > 1e2) return d1m_big(x) - d1m_big(y);
     if (x < 1e-2 && y < 1e-2) return d1m_small(x) - d1m_small(y);
-    return li2(-1 - x) - li2(-1 - y);
+    return li2_t<kRef>(-1 - x) - li2_t<kRef>(-1 - y);
 }
 
 // aux.hpp:132-148 : Li2(1+x) - Li2(1+y), x,y < 0
@@ -361,11 +371,12 @@ NUSI_FN double d1p_small(double v)
     return v * (1 - l) + (v * v * (-1 + 2 * l)) / 4. + (v * v * v * (1 - 3 * l)) / 9.
            + ((v * v) * (v * v) * (-1 + 4 * l)) / 16.;
 }
+template <bool kRef = false>
 NUSI_FN double dilog1pdiff(double x, double y)
 {
     if (-x > 1e2 && -y > 1e2) return d1p_big(x) - d1p_big(y);
     if (-x < 1e-2 && -y < 1e-2) return d1p_small(x) - d1p_small(y);
-    return li2(1 + x) - li2(1 + y);
+    return li2_t<kRef>(1 + x) - li2_t<kRef>(1 + y);
 }
 
 // aux.hpp:150-166 : Li2(1/(1-x)) - Li2(1/(1-y)), x,y < 0
@@ -379,11 +390,12 @@ NUSI_FN double d1o_small(double v)
     return ((v * v) * (v * v) * (-19 - 12 * l)) / 48. + (v * v * v * (-7 - 6 * l)) / 18.
            + (v * v * (-1 - 2 * l)) / 4. + v * (1 - l);
 }
+template <bool kRef = false>
 NUSI_FN double dilog1over1mdiff(double x, double y)
 {
     if (-x > 1e2 && -y > 1e2) return d1o_big(x) - d1o_big(y);
     if (-x < 1e-2 && -y < 1e-2) return d1o_small(x) - d1o_small(y);
-    return li2(1 / (1 - x)) - li2(1 / (1 - y));
+    return li2_t<kRef>(1 / (1 - x)) - li2_t<kRef>(1 / (1 - y));
 }
 
 }  // namespace nusi

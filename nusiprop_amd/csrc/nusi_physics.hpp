@@ -161,6 +161,7 @@ NUSI_FN_OUT double gl33_rect(int kind, double tp, double tm, double Sm, double S
     return acc * (1. / 4. * (tm - tp) * (Sp - Sm));
 }
 
+template <bool kRef = false>
 NUSI_FN double gpp_analytic(double a, double b)  // nuSIprop.hpp:885 with a = max(s-,4)
 {
     const double ra4 = sqrt(-4 + a), ra = sqrt(a), rb4 = sqrt(-4 + b), rb = sqrt(b);
@@ -173,14 +174,14 @@ NUSI_FN double gpp_analytic(double a, double b)  // nuSIprop.hpp:885 with a = ma
            - 24 * (sqrt((-4 + a) / a) - sqrt((-4 + b) / b) - nm::log(A4) + nm::log(B4))
            + 2 * nm::log(B1 * B1 / 4.) * nm::log(B2 * B2 / 4.)
            + ((6 + b * nm::log((-2 + b) * b)) * nm::log(B2 * B2 / (B3 * B3))) / b
-           + 8 * dilogdiff(4 / (A4 * A4), 4 / (B4 * B4))
-           + 2 * dilogdiff(4 / (A2 * A2), 4 / (B2 * B2));
+           + 8 * dilogdiff<kRef>(4 / (A4 * A4), 4 / (B4 * B4))
+           + 2 * dilogdiff<kRef>(4 / (A2 * A2), 4 / (B2 * B2));
 }
 
 // ---------------------------------------------------------------------------
 // Gamma(Em, Ep)  -- nuSIprop.hpp:759-922
 // ---------------------------------------------------------------------------
-template <bool kRef = false>   // kRef: NUSI_OPT_REFERENCE_ORDER (the general complex dilogarithm)
+template <bool kRef = false>   // kRef: NUSI_OPT_REFERENCE_ORDER (GSL's dilogarithms, nusi_gsl.hpp)
 NUSI_FN double gamma_entry(const Point& P, double Em, double Ep, int& warn)
 {
     const double g = P.g, mphi = P.mphi, Ga = P.Ga;
@@ -212,7 +213,7 @@ NUSI_FN double gamma_entry(const Point& P, double Em, double Ep, int& warn)
 
         double Gint = g4 / (32 * kPi * m2 * sm * sp) *
                       (sm * L1p * (2 + 2 * sp + sp * nm::log(2 + sp)) - sp * L1m * (2 + 2 * sm + sm * nm::log(2 + sm))
-                       + sm * sp * (dilog1mdiff(sp, sm) + dilogdiff(sp, sm)));
+                       + sm * sp * (dilog1mdiff<kRef>(sp, sm) + dilogdiff<kRef>(sp, sm)));
         if (Gint < 0) Gint = g4 / (16 * kPi * m2) * (sp - sm) / 2. * gl3_Gtu_int(sm, sp);
         Gint *= P.majorana ? uj : 0.5 * uj;
         tot += wgt * Gint;
@@ -233,7 +234,7 @@ NUSI_FN double gamma_entry(const Point& P, double Em, double Ep, int& warn)
         const double Lgp = nm::log1p(((-1 + sp) * (-1 + sp)) / gr2), Lgm = nm::log1p(((-1 + sm) * (-1 + sm)) / gr2);
         double Gst = -g4 / (32 * kPi * m2 * (1 + gr2)) *
                      (d1.r + d2.r + gr * (d2.i - d1.i) + 2 * gr * carg(1.0 - z2p) * L1p - 2 * gr * carg(1.0 - z2m) * L1m
-                      + nm::log1p(4 / gr2) * (L1m - L1p) + Lgp * L1p - Lgm * L1m + (1 + gr2) * (Lgm - Lgp) + 2 * dilogdiff(sp, sm));
+                      + nm::log1p(4 / gr2) * (L1m - L1p) + Lgp * L1p - Lgm * L1m + (1 + gr2) * (Lgm - Lgp) + 2 * dilogdiff<kRef>(sp, sm));
         Gst *= uj;
         tot += wgt * Gst;
         const double Gsu = P.majorana ? Gst : 0;
@@ -242,7 +243,7 @@ NUSI_FN double gamma_entry(const Point& P, double Em, double Ep, int& warn)
         double Gpp = 0;
         if (sp > 4 && P.phiphi) {
             const double a = (sm > 4) ? sm : 4.0;
-            Gpp = g4 / (128. * kPi * m2) * gpp_analytic(a, sp);
+            Gpp = g4 / (128. * kPi * m2) * gpp_analytic<kRef>(a, sp);
             if (Gpp < 0) Gpp = g4 / (64 * kPi * m2) * (sp - a) / 2. * gl3_Gpp(a, sp);
             Gpp *= uj;
             if (P.majorana) Gpp *= 2;
@@ -256,7 +257,7 @@ NUSI_FN double gamma_entry(const Point& P, double Em, double Ep, int& warn)
 // ---------------------------------------------------------------------------
 // alphaTilde(Em, Ep)  -- nuSIprop.hpp:924-1235
 // ---------------------------------------------------------------------------
-template <bool kRef = false>   // kRef: NUSI_OPT_REFERENCE_ORDER (the general complex dilogarithm)
+template <bool kRef = false>   // kRef: NUSI_OPT_REFERENCE_ORDER (GSL's dilogarithms, nusi_gsl.hpp)
 NUSI_FN double alphat_entry(const Point& P, const SplineSet& spl, double Em, double Ep, int& warn)
 {
     const double g = P.g, mphi = P.mphi, Ga = P.Ga;
@@ -328,12 +329,12 @@ NUSI_FN double alphat_entry(const Point& P, const SplineSet& spl, double Em, dou
                         + (-6 + 4 * d + d2 - 2 * d3 - 8 * lq + 8 * d * lq + 2 * d3 * lq - 2 * d4 * lq - 6 * lt + 6 * d * lt) / (3. * (-1 + d) * (tp * tp * tp))
                         + (8 - 12 * d + 3 * d2 + 12 * lq - 24 * d * lq + 12 * d2 * lq + 12 * lt - 24 * d * lt + 12 * d2 * lt) / (3. * ((-1 + d) * (-1 + d)) * ((tp * tp) * (tp * tp)));
             } else
-                combi = li2(1 + 1 / (-2 + tp)) - li2((-1 + tm) / (-2 + tp)) + li2(1 + (1 + tm - tp) / tp) - li2(1 + 1 / tp);
+                combi = li2_t<kRef>(1 + 1 / (-2 + tp)) - li2_t<kRef>((-1 + tm) / (-2 + tp)) + li2_t<kRef>(1 + (1 + tm - tp) / tp) - li2_t<kRef>(1 + 1 / tp);
             atu = g4 / (32 * kPi * m4 * (1 + tm) * tp) *
                   (2 * (2 * (1 + tm) * (tm - tp) - 2 * (1 + tm) * tp * nm::atanh(1 / (1 - tp)) * nm::atanh((tm - tp) / (-2 + tm + tp))
                         + tm * tp * (-Lmt + Lmp) + (1 + tm) * (Lmt - Lmp - Ld) + tp * (-Lmt + Lmp + Ld) - tm * tp * nm::log(tm / tp))
-                   + (1 + tm) * tp * ((-(Lmt * Lmt) + Lmp * Lmp) / 2. + dilog1over1mdiff(tp, tm))
-                   - (1 + tm) * tp * (dilog1pdiff(tm, tp) + combi));
+                   + (1 + tm) * tp * ((-(Lmt * Lmt) + Lmp * Lmp) / 2. + dilog1over1mdiff<kRef>(tp, tm))
+                   - (1 + tm) * tp * (dilog1pdiff<kRef>(tm, tp) + combi));
             if (atu < 0) atu = gl33_tri(2, tp, tm) * (g4 / (16 * kPi * m4));
         }
         atu *= uk;
@@ -400,7 +401,7 @@ NUSI_FN double alphat_entry(const Point& P, const SplineSet& spl, double Em, dou
                 const double lm = nm::log(-tm), lp = nm::log(-tp);
                 app = g4 / m4 *
                       (6 * tm * lm - tp * (lm * lm) + 2 * (-8 * tm + 8 * tp + 4 * tp * lm + nm::log(tm - tp) * (tm - tp - tp * nm::log(tm / tp)))
-                       - 2 * (2 * tm + 5 * tp) * lp + tp * (lp * lp) - 2 * tp * li2(1 - tm / tp)) / (128. * kPi * tp);
+                       - 2 * (2 * tm + 5 * tp) * lp + tp * (lp * lp) - 2 * tp * li2_t<kRef>(1 - tm / tp)) / (128. * kPi * tp);
             }
             app *= uk;
             if (maj) app *= 2;
@@ -458,20 +459,22 @@ struct AlphaCorner {
 #define NUSI_CARG carg_i
 #endif
 // The leaves split into those of (S', t) alone ("shared": every point with the same m_phi and
-// masses has them, bit for bit) and those that also read gr = Gamma_phi / m_phi ("member").
+// masses has them, bit for bit) and those that also read gr = Gamma_phi / m_phi ("member").  kRef:
+// NUSI_OPT_REFERENCE_ORDER (GSL's dilogarithms)
+template <bool kRef = false>
 NUSI_FN void alpha_corner_shared(double S, double t, AlphaCorner& c)
 {
     c.L = NUSI_CLOG1P(S + t);
     c.LL = NUSI_CLOG(1 + S + t);
     if (t < -1) {
-        c.TU1 = li2((1 + S + t) / S);
+        c.TU1 = li2_t<kRef>((1 + S + t) / S);
         c.TU2 = 0.0;
     } else {
-        c.TU1 = li2(S / (1 + S + t));
+        c.TU1 = li2_t<kRef>(S / (1 + S + t));
         c.TU2 = NUSI_CLOG((1 + S + t) / S);
     }
-    c.G = li2((1 + S + t) / (2 + S));
-    const cd Dr = cli2((1 + S + t) / (1 + t), 0.0);
+    c.G = li2_t<kRef>((1 + S + t) / (2 + S));
+    const cd Dr = cli2_t<kRef>((1 + S + t) / (1 + t), 0.0);
     c.Drr = Dr.r;
     c.Dri = Dr.i;
 }
@@ -535,14 +538,14 @@ NUSI_FN void alpha_member_corner(const MemberShared& M, double S, double t, doub
 }
 // NUSI_OPT_REFERENCE_ORDER: the member leaves in the reference's own operation order -- Dc =
 // gsl_sf_complex_dilog_xy_e of its quotient z = (1 + S + t) / (2 - i gr + t) (C99 complex division,
-// nuSIprop.hpp:1432-1438, 1444-1451), by the general series, and A = carg(-((-1 + i gr + S) / (2 - i gr + t)))
+// nuSIprop.hpp:1432-1438, 1444-1451), by GSL's algorithm (gsl_cli2), and A = carg(-((-1 + i gr + S) / (2 - i gr + t)))
 // (:1456); no Taylor expansion about the real point and no sum of edge arguments.  The oracle's
 // member_dc_ref / member_arg_ref (ora_set_reference_order(1)).
 NUSI_FN void alpha_member_ref(double S, double t, double gr, double& Dcr, double& Dci, double& A)
 {
     const cd dt = C(2 + t, -gr);
     const cd z = (1 + S + t) / dt;
-    const cd Dc = cli2_general(z.r, z.i);
+    const cd Dc = gsl_cli2(z.r, z.i);
     Dcr = Dc.r;
     Dci = Dc.i;
     A = carg(-(C(-1 + S, gr) / dt));
@@ -564,7 +567,7 @@ NUSI_FN void alpha_corner_member(double S, double t, double gr, AlphaCorner& c)
 template <bool kRef = false>
 NUSI_FN void alpha_corner(double S, double t, double gr, AlphaCorner& c)
 {
-    alpha_corner_shared(S, t, c);
+    alpha_corner_shared<kRef>(S, t, c);
     alpha_corner_member<kRef>(S, t, gr, c);
 }
 // t-edge leaves (L2 is the member leaf)
@@ -783,12 +786,13 @@ NUSI_FN void alpha_tile_edge_member_job(const Point& P, int m, int G, int job, c
 }
 // job j in [0, cs ct): the shared leaves of corner (S' slot j / ct, t slot j % ct) of mass state k;
 // edgk = the edge block of mass state k (its t and S' values)
+template <bool kRef = false>
 NUSI_FN void alpha_tile_corner_job(int j, const double* edgk, int ct, int cs, double* cor)
 {
     const int cc = cs * ct;
     const int si = j / ct, ti = j - si * ct;
     AlphaCorner c;
-    alpha_corner_shared(edgk[kTEdgeFields * ct + kSEdgeVal * cs + si], edgk[kTEdgeVal * ct + ti], c);
+    alpha_corner_shared<kRef>(edgk[kTEdgeFields * ct + kSEdgeVal * cs + si], edgk[kTEdgeVal * ct + ti], c);
     cor[j] = c.L; cor[cc + j] = c.LL; cor[2 * cc + j] = c.TU1; cor[3 * cc + j] = c.TU2; cor[4 * cc + j] = c.G;
     cor[5 * cc + j] = c.Drr; cor[6 * cc + j] = c.Dri;
 }
@@ -951,12 +955,13 @@ struct SplitLeavesT {
 };
 using SplitLeaves = SplitLeavesT<false>;
 // shared corner leaves of corner j: L, Drr, Dri -> per[0..2][cc] (kept), LL, TU1, TU2, G -> tmp[0..3][cc]
+template <bool kRef = false>
 NUSI_FN void alpha_batch_corner_job(int j, const double* edgk, int ct, int cs, double* per, double* tmp)
 {
     const int cc = cs * ct;
     const int si = j / ct, ti = j - si * ct;
     AlphaCorner c;
-    alpha_corner_shared(edgk[kTEdgeFields * ct + kSEdgeVal * cs + si], edgk[kTEdgeVal * ct + ti], c);
+    alpha_corner_shared<kRef>(edgk[kTEdgeFields * ct + kSEdgeVal * cs + si], edgk[kTEdgeVal * ct + ti], c);
     per[j] = c.L; per[kCC + j] = c.Drr; per[2 * kCC + j] = c.Dri;
     tmp[j] = c.LL; tmp[kCC + j] = c.TU1; tmp[2 * kCC + j] = c.TU2; tmp[3 * kCC + j] = c.G;
 }

@@ -31,7 +31,14 @@ static double li2_useries(double u)
     return fma(u * u2, p, u - 0.25 * u2);
 }
 
-double ora_dilog(double x)
+/* reference-order arithmetic (ora_set_reference_order, test infrastructure): 1 = GSL's algorithms (ora_gsl.c) for
+ * every gsl_sf_dilog / gsl_sf_complex_dilog_xy_e call site, 2 = the long-double evaluation (precision probe);
+ * read-only while tables are built */
+static int g_gsl_level = 0;
+void ora_cdilog_set_general(int level) { g_gsl_level = level; }
+
+/* the shared-algorithm real Li2 (the Bernoulli series after the maps; polylogarithm::Li2 always takes it) */
+static double li2_bern(double x)
 {
     double add = 0.0, sgn = 1.0;
     if (x > 1.0) {
@@ -55,7 +62,16 @@ double ora_dilog(double x)
     return add + sgn * li2_useries(-ora_log1p(-x));
 }
 
-double ora_li2(double x) { return ora_dilog(x); }
+/* gsl_sf_dilog call sites */
+double ora_dilog(double x)
+{
+    if (g_gsl_level == 1) return ora_gsl_dilog(x);
+    if (g_gsl_level == 2) return ora_dilog_ld(x);
+    return li2_bern(x);
+}
+
+/* polylogarithm::Li2 (the DSNB source, nuSIprop.hpp:628-632): not GSL, the shared algorithm in every mode */
+double ora_li2(double x) { return li2_bern(x); }
 
 /* ora_dilog (same operations) with log|1 - x| and, for |x| > 1, log|x| (the logarithms it forms on its
  * way: log1p(-x), or log|x| + log1p(-1/x) after the x -> 1/x map); x != 1 */
@@ -133,25 +149,23 @@ static void cdilog_axis(double x, double y, double *re, double *im)
     ora_li2_taylor_eval(&T, 0.0, y, y > 0.0 ? 1.0 : -1.0, re, im);
 }
 
-/* reference-order arithmetic (ora_set_reference_order): 1 = the complex dilogarithm without the near-axis
- * Taylor shortcut, 2 = its long-double evaluation (precision probe) -- test infrastructure, read-only while
- * tables are built */
-static int g_cdilog_general = 0;
-void ora_cdilog_set_general(int on) { g_cdilog_general = on; }
-
 void ora_complex_dilog_xy(double x, double y, double *re, double *im)
 {
+    if (g_gsl_level == 1) {   /* GSL's algorithm (ora_gsl.c) */
+        ora_gsl_complex_dilog_xy(x, y, re, im);
+        return;
+    }
     if (y == 0.0) {
         /* GSL: on the real axis the imaginary part is -pi*log(x) for x >= 1 */
         *re = ora_dilog(x);
         *im = (x >= 1.0) ? -PI_D * ora_log(x) : 0.0;
         return;
     }
-    if (g_cdilog_general == 2) {   /* (precision probe: the long-double evaluation) */
+    if (g_gsl_level == 2) {   /* (precision probe: the long-double evaluation) */
         ora_complex_dilog_xy_ld(x, y, re, im);
         return;
     }
-    if (!g_cdilog_general) {
+    {
         const double ax = fabs(x), a1 = fabs(1.0 - x);
         if (fabs(y) <= AXIS_RATIO * (ax < a1 ? ax : a1)) {
             cdilog_axis(x, y, re, im);

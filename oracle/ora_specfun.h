@@ -32,8 +32,16 @@ extern "C" {
 
 double ora_dilog(double x);                                  /* gsl_sf_dilog */
 void ora_complex_dilog_xy(double x, double y, double *re, double *im);
-/* 1: ora_complex_dilog_xy skips its near-axis Taylor path (the general series everywhere) */
-void ora_cdilog_set_general(int on);
+/* reference-order level of the gsl_sf_dilog / gsl_sf_complex_dilog_xy_e call sites (ora_dilog,
+ * ora_complex_dilog_xy): 0 = the shared-algorithm series, 1 = GSL's algorithms (ora_gsl.c), 2 = long double */
+void ora_cdilog_set_general(int level);
+/* GSL's published algorithms restated (ora_gsl.c): gsl_sf_dilog, gsl_sf_complex_dilog_xy_e, gsl_sf_clausen,
+ * and the hypot they call; ora_gsl_stats: the series loops' iteration counts of this thread (analysis) */
+double ora_gsl_dilog(double x);
+void ora_gsl_complex_dilog_xy(double x, double y, double *re, double *im);
+double ora_gsl_clausen(double x);
+double ora_hypot(double x, double y);
+void ora_gsl_stats(long *out, int reset);
 /* Li2 about a real point x0 (x0 != 0, 1): coefficients and evaluation at x0 + (dr + i di) on the side
  * `side` (+-1) of the cut x0 > 1; |d| <= ORA_LI2T_RATIO min(|x0|, |1 - x0|) */
 #define ORA_LI2T_TERMS 6

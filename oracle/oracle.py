@@ -85,6 +85,14 @@ def lib():
         L.ora_getmL.argtypes = [d, d, d, dp]
         L.ora_set_channels.argtypes = [p, i]
         L.ora_set_reference_order.argtypes = [i]
+        L.ora_gsl_dilog.restype = d
+        L.ora_gsl_dilog.argtypes = [d]
+        L.ora_gsl_complex_dilog_xy.argtypes = [d, d, dp, dp]
+        L.ora_gsl_clausen.restype = d
+        L.ora_gsl_clausen.argtypes = [d]
+        L.ora_hypot.restype = d
+        L.ora_hypot.argtypes = [d, d]
+        L.ora_gsl_stats.argtypes = [ctypes.POINTER(ctypes.c_long), i]
         L.ora_Gpp_bracket.restype = d
         L.ora_Gpp_bracket.argtypes = [d, d]
         _lib = L
@@ -113,16 +121,44 @@ def complex_dilog(x, y):
 CH_S, CH_T, CH_U, CH_TU, CH_ST, CH_SU, CH_PP, CH_ALL = 1, 2, 4, 8, 16, 32, 64, 127
 
 
+def gsl_dilog(x):
+    """gsl_sf_dilog by GSL's algorithm (ora_gsl.c)."""
+    return lib().ora_gsl_dilog(float(x))
+
+
+def gsl_complex_dilog(x, y):
+    """gsl_sf_complex_dilog_xy_e by GSL's algorithm (ora_gsl.c): (re, im)."""
+    re, im = ctypes.c_double(), ctypes.c_double()
+    lib().ora_gsl_complex_dilog_xy(float(x), float(y), ctypes.byref(re), ctypes.byref(im))
+    return re.value, im.value
+
+
+def gsl_clausen(x):
+    return lib().ora_gsl_clausen(float(x))
+
+
+def hypot(x, y):
+    return lib().ora_hypot(float(x), float(y))
+
+
+def gsl_stats(reset=True):
+    """Iteration counts of ora_gsl.c's series on this thread since the last reset: [dilog_series_1, series_2,
+    dilogc_series_1, series_2_c, dilogc_series_3 calls, ...] (analysis only)."""
+    out = (ctypes.c_long * 8)()
+    lib().ora_gsl_stats(out, int(reset))
+    return list(out)
+
+
 def Gpp_bracket(a, b):
     """The bracket of the analytic phi-phi absorption (nuSIprop.hpp:885), a = max(s-, 4)."""
     return lib().ora_Gpp_bracket(float(a), float(b))
 
 
 class reference_order:
-    """Context: the oracle in reference-order arithmetic (nusi_oracle.h ora_set_reference_order) -- the alpha
-    table's s-t member dilogs as the general complex dilogarithm of the reference's own quotient and carg of
-    its expression (nuSIprop.hpp:1431-1456), no near-axis Taylor shortcut (level 1); level 2 evaluates every
-    complex dilogarithm in long double (a precision probe).  Process-wide: tests only."""
+    """Context: the oracle in reference-order arithmetic (nusi_oracle.h ora_set_reference_order) -- level 1: every
+    gsl_sf_dilog / gsl_sf_complex_dilog_xy_e call site by GSL's own algorithms (ora_gsl.c), and the alpha table's
+    s-t member dilogs of the reference's own quotient with carg of its expression (nuSIprop.hpp:1431-1456);
+    level 2 evaluates those dilogarithms in long double (a precision probe).  Process-wide: tests only."""
 
     def __init__(self, level=1):
         self.level = int(level)

@@ -73,6 +73,32 @@ def main():
             continue
         v = mp.polylog(2, mp.mpc(x, y))
         out["li2_complex_axis"].append([x, y, f(mp.re(v)), f(mp.im(v))])
+    # round 5, GSL's branches (nusi_gsl.hpp / oracle/ora_gsl.c): |z| near and on the unit circle (dilogc_series_3
+    # above |z| = 0.98, Lewin's formula on it), the 0.25 / 0.98 / 0.732 splits, z near -1 with a small imaginary
+    # part (the member quotients of alpha's s-t interference), and Clausen's function; drawn after every set above
+    out["li2_complex_unit"] = []
+    for _ in range(300):
+        r = random.random()
+        t = random.uniform(-mp.pi, mp.pi)
+        if r < 0.2:
+            rad = 1.0
+        elif r < 0.6:
+            rad = 1 + random.choice([-1, 1]) * 10 ** random.uniform(-12, -1.3)
+        elif r < 0.8:
+            rad = random.choice([0.25, 0.98, 1 / 0.98, 4.0]) * (1 + random.uniform(-1e-3, 1e-3))
+        else:
+            rad, t = 1 + random.uniform(-0.05, 0.05), mp.pi - 10 ** random.uniform(-6, -1)
+        x, y = f(rad * mp.cos(t)), f(rad * mp.sin(t))
+        v = mp.polylog(2, mp.mpc(x, y))
+        out["li2_complex_unit"].append([x, y, f(mp.re(v)), f(mp.im(v))])
+    for x0 in (0.732, 0.25):
+        for _ in range(20):
+            x, y = x0 + random.uniform(-1e-6, 1e-6), random.uniform(-0.1, 0.1)
+            v = mp.polylog(2, mp.mpc(x, y))
+            out["li2_complex_unit"].append([x, y, f(mp.re(v)), f(mp.im(v))])
+    out["clausen"] = []
+    for x in [1e-12, 1e-8, 1e-3, 0.5, 1.0, 2.0, 3.0, 3.14159, -1.0, -3.0] + [random.uniform(-7, 7) for _ in range(100)]:
+        out["clausen"].append([x, f(mp.clsin(2, x))])
     with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "specfun_kat.json"), "w") as fh:
         json.dump(out, fh)
 

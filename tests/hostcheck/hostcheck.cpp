@@ -85,7 +85,7 @@ static int alpha_tiled_t(const double* pt, const int* flags, int T, const double
                 if (P.non_resonant && P.majorana) {
                     const double* edgk = edg + k * alpha_tile_edge_stride(cs, ct);
                     for (int j = 0; j < cc; ++j) {
-                        alpha_tile_corner_job(j, edgk, ct, cs, cor);
+                        alpha_tile_corner_job<kRef>(j, edgk, ct, cs, cor);
                         alpha_tile_corner_member_job<kRef>(P, 0, j, edgk, ct, cs, cor);
                     }
                     for (int j = 0; j < kAlphaTile * (cs + ct); ++j)
@@ -124,4 +124,9 @@ double hc_lum(const double* pt, const int* flags, double z, double sfr_z, double
 double hc_li2(double x) { return nusi::li2(x); }
 void hc_cli2(double x, double y, double* re, double* im) { const nusi::cd r = nusi::cli2(x, y); *re = r.r; *im = r.i; }
 double hc_li3(double x) { return nusi::li3(x); }
+// GSL's algorithms as the device runs them (nusi_gsl.hpp), for the bit-identity test against oracle/ora_gsl.c
+double hc_gsl_li2(double x) { return nusi::gsl_li2(x); }
+void hc_gsl_cli2(double x, double y, double* re, double* im) { const nusi::cd r = nusi::gsl_cli2(x, y); *re = r.r; *im = r.i; }
+double hc_gsl_clausen(double x) { return nusi::gsl::clausen(x); }
+double hc_hypot(double x, double y) { return nusi::gsl::hypot(x, y); }
 }

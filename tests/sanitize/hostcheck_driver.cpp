@@ -23,14 +23,21 @@ int main()
     for (const auto& pt : pts)
         for (const auto& fl : flags) {
             std::vector<double> G(T), At(T), A(T * T, 0.0), B(T * T, 0.0);
-            hc_tables(pt, fl, T, lo.data(), hi.data(), G.data(), At.data(), A.data());
-            hc_alpha_tiled(pt, fl, T, lo.data(), hi.data(), B.data());
-            for (int n = 0; n < T; ++n)
-                for (int m = n + 1; m < T; ++m)
-                    if ((fl[1] || m == n + 1) && memcmp(&A[n * T + m], &B[n * T + m], sizeof(double)) != 0) {
-                        if (fails < 5) fprintf(stderr, "tile != entry at (%d, %d)\n", n, m);
-                        ++fails;
-                    }
+            for (int ref = 0; ref < 2; ++ref) {   // the default and the reference-order (GSL) arithmetic
+                if (ref) {
+                    hc_tables_ref(pt, fl, T, lo.data(), hi.data(), G.data(), At.data(), A.data());
+                    hc_alpha_tiled_ref(pt, fl, T, lo.data(), hi.data(), B.data());
+                } else {
+                    hc_tables(pt, fl, T, lo.data(), hi.data(), G.data(), At.data(), A.data());
+                    hc_alpha_tiled(pt, fl, T, lo.data(), hi.data(), B.data());
+                }
+                for (int n = 0; n < T; ++n)
+                    for (int m = n + 1; m < T; ++m)
+                        if ((fl[1] || m == n + 1) && memcmp(&A[n * T + m], &B[n * T + m], sizeof(double)) != 0) {
+                            if (fails < 5) fprintf(stderr, "tile != entry at (%d, %d) ref %d\n", n, m, ref);
+                            ++fails;
+                        }
+            }
         }
     if (fails) return 1;
     printf("hostcheck_asan OK\n");

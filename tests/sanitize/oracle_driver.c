@@ -73,6 +73,13 @@ int main(void)
     p = base(); p.normal_ordering = 0; p.mntot = 0.2; run(p, NULL, NULL, NULL, NULL, 0);
     p = base(); p.source = 0; p.lEmin = 4; p.lEmax = 9; p.mphi = 3e3; p.g = 0.03; run(p, NULL, NULL, NULL, NULL, 0);
     p = base(); p.mphi = 1e7; p.g = 0.5; p.flav = 0; run(p, NULL, NULL, NULL, NULL, 0);
+    /* reference order: GSL's dilogarithm algorithms (ora_gsl.c) at every call site */
+    ora_set_reference_order(1);
+    p = base(); run(p, NULL, NULL, NULL, NULL, 0);
+    p = base(); p.mphi = 1e7; p.g = 1.0; run(p, NULL, NULL, NULL, NULL, 0);
+    p = base(); p.source = 0; p.lEmin = 4; p.lEmax = 9; p.mphi = 3e3; p.g = 0.03; run(p, NULL, NULL, NULL, NULL, 0);
+    p = base(); p.majorana = 0; run(p, NULL, NULL, NULL, NULL, 0);
+    ora_set_reference_order(0);
     /* phi-phi on small tables */
     char dir[] = "/tmp/nusi_asan_XXXXXX";
     CHECK(mkdtemp(dir) != NULL);

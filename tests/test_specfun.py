@@ -8,6 +8,11 @@ the C libm), restated in the oracle and in the product's device headers.
 2. Product device code (nusiprop_amd/csrc/*.hpp compiled for the host by
    tests/hostcheck) vs oracle: BIT-IDENTICAL on every vector.  This is what
    makes the GPU tables bit-exact to the oracle (tests/test_gpu_parity.py).
+3. GSL's own algorithms (the reference-order arithmetic: oracle/ora_gsl.c,
+   nusiprop_amd/csrc/nusi_gsl.hpp) against the same known answers, with
+   vectors on GSL's branch points (|z| 0.25 / 0.98 / 1, x 0.732), and the
+   device restatement bit-identical to the oracle's on them and on seeded
+   random arguments.
 """
 import ctypes
 import json
@@ -41,6 +46,13 @@ def hlib():
     H.hc_li3.restype = D
     H.hc_li3.argtypes = [D]
     H.hc_cli2.argtypes = [D, D, ctypes.POINTER(D), ctypes.POINTER(D)]
+    H.hc_gsl_li2.restype = D
+    H.hc_gsl_li2.argtypes = [D]
+    H.hc_gsl_cli2.argtypes = [D, D, ctypes.POINTER(D), ctypes.POINTER(D)]
+    H.hc_gsl_clausen.restype = D
+    H.hc_gsl_clausen.argtypes = [D]
+    H.hc_hypot.restype = D
+    H.hc_hypot.argtypes = [D, D]
     return H
 
 
@@ -109,3 +121,82 @@ def test_device_specfun_bit_identical_to_oracle(oracle_mod, hlib):
         assert (re.value, im.value) == (z.real, z.imag), (x, y)
     for x, _ in KAT["li3"]:
         assert hlib.hc_li3(x) == oracle_mod.li3(x), x
+
+
+# ---- GSL's algorithms (reference-order arithmetic), round 5
+def test_gsl_dilog_real_vs_mpmath(oracle_mod):
+    """gsl_sf_dilog by GSL's algorithm (dilog_xge0 and the x < 0 reduction): <= 4e-15 of max(1, |Li2|) (relative
+    away from Re Li2's zero at x ~ 12.6, where only the absolute error is meaningful)."""
+    for x, y in KAT["li2_real"]:
+        v = oracle_mod.gsl_dilog(x)
+        assert abs(v - y) <= 4e-15 * max(1.0, abs(y)), (x, v, y)
+        if abs(x - 12.6) > 0.5:
+            assert abs(v - y) <= 4e-15 * abs(y) + 1e-300, (x, v, y)
+
+
+def _gsl_series3_mp(x, y):
+    """GSL's value where dilogc_series_3 runs (|w| in (0.98, 1), Re w <= 0.732 for w = z or 1/z), in exact arithmetic:
+    the six-term expansion in log|w| (dilog.c) unwound as gsl_sf_complex_dilog_xy_e does; None elsewhere."""
+    import mpmath as mp
+    z = mp.mpc(x, y)
+    w = z if abs(z) < 1 else 1 / z
+    r = abs(w)
+    if not (0.98 < r < 1 and w.real <= 0.732):
+        return None
+    th, a = mp.arg(w), mp.log(r)
+    c, s_ = mp.cos(th), mp.sin(th)
+    omc = 1 - c
+    hre = [mp.pi ** 2 / 6 + (th * th - 2 * mp.pi * abs(th)) / 4, -mp.log(2 * omc) / 2, -0.5, -0.5 / omc, 0,
+           (2 + c) / (2 * omc ** 2), 0]
+    him = [mp.clsin(2, th), -mp.atan2(-s_, omc), s_ / (2 * omc), 0, -s_ / (2 * omc ** 2), 0,
+           s_ / (2 * omc ** 5) * (8 * omc - s_ * s_ * (3 + c))]
+    v = sum(a ** n / mp.factorial(n) * mp.mpc(hre[n], him[n]) for n in range(7))
+    if abs(z) > 1:
+        v = -v - mp.log(-z) ** 2 / 2 - mp.pi ** 2 / 6
+    return complex(v)
+
+
+@pytest.mark.parametrize("kat", ["li2_complex", "li2_complex_axis", "li2_complex_unit"])
+def test_gsl_complex_dilog_vs_mpmath(oracle_mod, kat):
+    """gsl_sf_complex_dilog_xy_e by GSL's algorithm, incl. the real-axis convention, the unit circle (Lewin's
+    formula, dilogc_series_3) and the 0.25 / 0.732 / 0.98 splits: modulus-relative error <= 4e-15 against Li2 --
+    except where dilogc_series_3 runs, whose six-term expansion is GSL's own truncation (up to ~1e-13 at |z| = 0.98):
+    there the reference value is that expansion evaluated exactly (_gsl_series3_mp), which pins the algorithm."""
+    for x, y, re, im in KAT[kat]:
+        z = complex(*oracle_mod.gsl_complex_dilog(x, y))
+        ref = complex(re, im)
+        s3 = _gsl_series3_mp(x, y) if abs(complex(x, y)) != 1.0 else None
+        if s3 is not None and abs(z - ref) > 4e-15 * abs(ref):
+            assert abs(z - ref) <= 1e-12 * abs(ref), (x, y, z, ref)
+            ref = s3
+        assert abs(z - ref) <= 4e-15 * max(1e-300, abs(ref)), (x, y, z, ref)
+
+
+def test_gsl_clausen_vs_mpmath(oracle_mod):
+    for x, y in KAT["clausen"]:
+        assert abs(oracle_mod.gsl_clausen(x) - y) <= 2e-15 * abs(y) + 1e-15, (x, y)   # x (c - log x) near pi: absolute
+
+
+def test_device_gsl_bit_identical_to_oracle(oracle_mod, hlib):
+    """nusi_gsl.hpp (the GPU's NUSI_OPT_REFERENCE_ORDER arithmetic) == oracle/ora_gsl.c bit for bit, on every KAT
+    vector and on 20 000 seeded random arguments around GSL's branch points -- including its rewrite of the series'
+    stopping tests as multiply-compare (exact, nusi_gsl.hpp header)."""
+    import numpy as np
+    rng = np.random.default_rng(20250213)
+    re, im = D(), D()
+    xs = [x for x, _ in KAT["li2_real"]] + list(rng.uniform(-40, 40, 3000)) + list(rng.uniform(-1.5, 2.5, 3000))
+    xs += [0.25, 0.5, 1.0, 1.01, 2.0, -0.25, -0.5, -2.0, 0.0] + list(np.nextafter([0.25, 0.5, 1.0, 1.01, 2.0], 3))
+    for x in xs:
+        assert hlib.hc_gsl_li2(float(x)) == oracle_mod.gsl_dilog(float(x)), x
+    zs = [(x, y) for x, y, _, _ in KAT["li2_complex"] + KAT["li2_complex_axis"] + KAT["li2_complex_unit"]]
+    t = rng.uniform(-np.pi, np.pi, 6000)
+    rad = np.concatenate([rng.uniform(0.0, 3.0, 3000), 1 + rng.uniform(-0.05, 0.05, 3000)])
+    zs += list(zip(rad * np.cos(t), rad * np.sin(t)))
+    zs += list(zip(rng.uniform(-3, 3, 4000), rng.uniform(-1e-3, 1e-3, 4000)))
+    for x, y in zs:
+        hlib.hc_gsl_cli2(float(x), float(y), ctypes.byref(re), ctypes.byref(im))
+        assert (re.value, im.value) == oracle_mod.gsl_complex_dilog(float(x), float(y)), (x, y)
+    for x, _ in KAT["clausen"]:
+        assert hlib.hc_gsl_clausen(x) == oracle_mod.gsl_clausen(x), x
+    for a, b in rng.normal(size=(2000, 2)) * 10.0 ** rng.uniform(-200, 200, size=(2000, 1)):
+        assert hlib.hc_hypot(float(a), float(b)) == oracle_mod.hypot(float(a), float(b)), (a, b)
