@@ -1,0 +1,17 @@
+#!/bin/bash
+# On the GPU box: run scripts/gpu_session.sh inside the frozen .snap/ tree and copy its output to the top-level
+# gpurun_out/ (the directory gpurun returns).  The session's own exit status is returned.
+SNAP=$(cd "$(dirname "$0")/.." && pwd)
+TOP=$(cd "$SNAP/.." && pwd)
+TAG=${1:?tag}
+cd "$SNAP"
+bash scripts/gpu_session.sh "$@"
+rc=$?
+mkdir -p "$TOP/gpurun_out/$TAG"
+cp -r "gpurun_out/$TAG/." "$TOP/gpurun_out/$TAG/"
+cp SNAP_HEAD "$TOP/gpurun_out/$TAG/" 2>/dev/null
+for w in c4 c5 c3 c4s; do
+  [ -f "profiles/pmc_traffic_$w.json" ] && [ "profiles/pmc_traffic_$w.json" -nt SNAP_HEAD ] && \
+    cp "profiles/pmc_traffic_$w.json" "$TOP/gpurun_out/$TAG/pmc_traffic_$w.json"
+done
+exit $rc
