@@ -589,9 +589,11 @@ AlphaBatches alpha_batches(nusi_plan* pl, int ntab, std::vector<int>& perm)
 // NUSI_OPT_SHIFT_REUSE.  alpha / Gamma / alphaTilde see the energies only through
 // 2 m_k E / m_phi^2 (nuSIprop.hpp:1253-1256) and g through g^4 and Gamma_phi / m_phi = g^2 / 16 pi, so the tables of
 // m_phi' = m_phi r^(-o/2) (r = Emax[0] / Emin[0] = the table axis' bin ratio) are those of m_phi read o bins higher.
-// Tables of one (g, masses, |U|^2, flags) are taken in decreasing m_phi: each group starts at its largest m_phi
-// (the base) and takes the following ones whose offset o = 2 ln(m_base / m_phi) / ln r is an integer (to 1e-6) in
-// [1, K].  Groups of two or more go to slots [nd, ntab) in group order (remap[old slot] = new slot; smap[slot - nd]
+// Only tables with g <= kShiftReuseGMax = 0.05 take part (the optical depth amplifies the shifted tables' rounding
+// with g); the others are built directly.  Tables of one (g, masses, |U|^2, flags) are taken in
+// decreasing m_phi: each group starts at its largest m_phi (the base) and takes the following ones whose offset
+// o = 2 ln(m_base / m_phi) / ln r is within |o - round(o)| ln(r) / 2 < 1e-13 of an integer (m_phi reproduced to
+// ~1e-13 relative) in [1, K].  Groups of two or more go to slots [nd, ntab) in group order (remap[old slot] = new slot; smap[slot - nd]
 // = (base index, o); bases[] = the base Points); the rest stay in [0, nd).  Returns nd.
 int shift_groups(nusi_plan* pl, int ntab, std::vector<int>& remap, std::vector<int2>& smap, std::vector<nusi::Point>& bases)
 {
@@ -1379,7 +1381,7 @@ struct nusi_handle {
     double norm_total = 0.0;   // of the last evolve() (stale in check_energy_conservation)
     bool evolved = false;      // an evolve() has run (norm_total is set)
     int warn = 0;
-    std::vector<std::pair<int, int>> opts;   // nusi_set_option calls, replayed by nusi_copy
+    std::map<int, int> opts;   // the last value nusi_set_option set per option, replayed by nusi_copy
     ~nusi_handle() { nusi_plan_destroy(plan); }
 };
 
@@ -1509,7 +1511,7 @@ int nusi_get_warnings(const nusi_handle* h) { return h->warn; }
 int nusi_set_option(nusi_handle* h, int option, int value)
 {
     const int r = nusi_plan_set_option(h->plan, option, value);
-    if (r == NUSI_OK) h->opts.emplace_back(option, value);
+    if (r == NUSI_OK) h->opts[option] = value;
     return r;
 }
 

@@ -11,13 +11,23 @@
 // |z| 0.25 / 0.98), series, loop bounds and stopping tests, in the same operation order, on this repository's
 // shared libm (nm::log, nm::atan2) -- the oracle runs the same sequence (oracle/ora_gsl.c), bit for bit.
 //
-// Two rewrites are exact, not approximations:
+// GPU shape (the values are unchanged by any of it):
+//   * each heavy piece exists once in the code: gsl_cli2 forms its unit-disk argument (1/z or z), unitdisk its
+//     fundamental-region argument (1 - z or z), and one call each of the series runs; dilog_xge0 forms its series
+//     argument and runs one series_2 loop for its four branches that need one.  Inlined per branch they made the
+//     function ~30 000 instructions (instruction-cache bound);
+//   * series_1 and series_2_c share one loop (cseries): the same recurrence with the term's denominator k^2 or
+//     k^2 (k + 1), so a wave whose lanes take different series runs one loop, not two;
 //   * GSL stops a series when fabs(a / b) < 2^-p (p = 52, 53 or 104).  For a, b >= 0 and b 2^-p a normal number,
 //     RN(a / b) < 2^-p  <=>  a < b 2^-p: the doubles below 2^-p b are those at or below its predecessor, which
 //     lies below the rounding boundary 2^-p b (1 - 2^-54).  So the test is one multiply and one compare
 //     (quot_lt; the division where b < 2^-900);
-//   * series_1 / series_2_c share one loop (cseries): the same recurrence with the term's denominator k^2 or
-//     k^2 (k + 1), so a wave whose lanes take different series runs one loop, not two.
+//   * the series' term a / d_k with d_k = k^2 or k^2 (k + 1) (exact integers) is RN(a / d_k) from the table value
+//     y_k = RN(1 / d_k) by two residual corrections, q0 = a y_k, q_{i+1} = q_i + (a - d_k q_i) y_k (fma): the first
+//     makes the quotient faithful, the second correctly rounded (Markstein's theorem: y correctly rounded, q
+//     faithful, remainder exact by fma); 6e8 random a over 1800 binades and every d_k agree bit for bit with the
+//     division (tests/test_specfun.py runs the device functions against the oracle's divisions).  Subnormal
+//     ranges (a < 2^-960) take the division.  GSL's (k - 1)/k squared of series_1 is a table of the same values.
 #pragma once
 
 #include "nusi_libm.hpp"
@@ -28,6 +38,36 @@ namespace gsl {
 constexpr double kEps = 2.2204460492503131e-16;       // GSL_DBL_EPSILON
 constexpr double kSqrtEps = 1.4901161193847656e-08;   // GSL_SQRT_DBL_EPSILON
 constexpr double kPiD = 3.14159265358979323846;       // M_PI
+
+// per-k constants of the series: d1 = k^2, d2 = k^2 (k + 1) and their rounded reciprocals; rr = ((k - 1) / k)^2
+// as series_1 forms it (every value is the compiler's IEEE evaluation of GSL's own expression)
+constexpr int kKTab = 1000;
+struct KTab {
+    double d1[kKTab], y1[kKTab], d2[kKTab], y2[kKTab], rr[kKTab];
+};
+constexpr KTab make_ktab()
+{
+    KTab t{};
+    for (int k = 1; k < kKTab; ++k) {
+        t.d1[k] = (double)k * k;
+        t.y1[k] = 1.0 / t.d1[k];
+        t.d2[k] = (double)k * k * (k + 1.0);
+        t.y2[k] = 1.0 / t.d2[k];
+        const double rk = (k - 1.0) / k;
+        t.rr[k] = rk * rk;
+    }
+    return t;
+}
+constexpr KTab kKT = make_ktab();
+
+// RN(a / d) from y = RN(1 / d), a > 0 (header comment)
+NUSI_FN double div_k(double a, double d, double y)
+{
+    if (!(a >= 0x1p-960)) return a / d;
+    const double q0 = a * y;
+    const double q1 = fma(fma(-q0, d, a), y, q0);
+    return fma(fma(-q1, d, a), y, q1);
+}
 
 // fabs(a / b) < c of GSL's stopping tests for a, b >= 0 and c a power of two (header comment)
 NUSI_FN bool quot_lt(double a, double b, double c)
@@ -60,79 +100,71 @@ NUSI_FN double dilog_series_1(double x)
 {
     double sum = x, term = x;
     for (int k = 2; k < 1000; k++) {
-        const double rk = (k - 1.0) / k;
         term *= x;
-        term *= rk * rk;
+        term *= kKT.rr[k];   // rk * rk, rk = (k - 1.0) / k
         sum += term;
         if (quot_lt(fabs(term), fabs(sum), 0x1p-52)) break;   // fabs(term / sum) < GSL_DBL_EPSILON
     }
     return sum;
 }
-// series_2: sum r^k / (k^2 (k + 1)), the first nine terms unconditionally
-NUSI_FN double series_2(double r)
+// dilog_series_2: Li2(x) = 1 + (1 - x) log(1 - x) / x + series_2(x), series_2 = sum r^k / (k^2 (k + 1)) with the
+// first nine terms unconditionally
+NUSI_FN double dilog_series_2(double x)
 {
-    double rk = r, sum = 0.5 * r;
+    double rk = x, sum = 0.5 * x;
     int k;
+#pragma unroll
     for (k = 2; k < 10; k++) {
-        rk *= r;
-        sum += rk / (k * k * (k + 1.0));
+        rk *= x;
+        sum += div_k(rk, kKT.d2[k], kKT.y2[k]);
     }
     for (; k < 100; k++) {
-        rk *= r;
-        const double ds = rk / (k * k * (k + 1.0));
+        rk *= x;
+        const double ds = div_k(rk, kKT.d2[k], kKT.y2[k]);
         sum += ds;
         if (quot_lt(fabs(ds), fabs(sum), 0x1p-53)) break;   // fabs(ds / sum) < 0.5 GSL_DBL_EPSILON
     }
-    return sum;
-}
-// dilog_series_2: Li2(x) = 1 + (1 - x) log(1 - x) / x + series_2(x)
-NUSI_FN double dilog_series_2(double x)
-{
-    double val = series_2(x);
     double t;
-    if (x > 0.01) t = (1.0 - x) * NUSI_PLOG(1.0 - x) / x;
+    if (x > 0.01) t = (1.0 - x) * nm::log(1.0 - x) / x;
     else {
         const double c3 = 1.0 / 3.0, c4 = 1.0 / 4.0, c5 = 1.0 / 5.0, c6 = 1.0 / 6.0, c7 = 1.0 / 7.0, c8 = 1.0 / 8.0;
         const double t68 = c6 + x * (c7 + x * c8);
         const double t38 = c3 + x * (c4 + x * (c5 + x * t68));
         t = (x - 1.0) * (1.0 + x * (0.5 + x * t38));
     }
-    val += 1.0 + t;
-    return val;
+    sum += 1.0 + t;
+    return sum;
 }
-// dilog_xge0: Re Li2(x), x >= 0
-NUSI_FN double dilog_xge0(double x)
+// dilog_xge0: Re Li2(x), x >= 0.  Branches: x > 2 (series_2 of 1/x), 1.01 < x <= 2 (of 1 - 1/x), 1 < x <= 1.01
+// (the series about 1), x == 1, 1/2 < x < 1 (series_2 of 1 - x), 1/4 < x <= 1/2 (of x), 0 < x <= 1/4 (series_1)
+NUSI_FN_OUT double dilog_xge0(double x)
 {
-    if (x > 2.0) {
-        const double ser = dilog_series_2(1.0 / x);
-        const double log_x = NUSI_PLOG(x);
-        const double t1 = kPiD * kPiD / 3.0, t2 = ser, t3 = 0.5 * log_x * log_x;
-        return t1 - t2 - t3;
-    }
-    if (x > 1.01) {
-        const double ser = dilog_series_2(1.0 - 1.0 / x);
-        const double log_x = NUSI_PLOG(x);
-        const double log_term = log_x * (NUSI_PLOG(1.0 - 1.0 / x) + 0.5 * log_x);
-        const double t1 = kPiD * kPiD / 6.0, t2 = ser, t3 = log_term;
-        return t1 + t2 - t3;
-    }
-    if (x > 1.0) {   // series around x = 1
-        const double eps = x - 1.0, lne = NUSI_PLOG(eps);
+    if (x > 1.0 && x <= 1.01) {   // series around x = 1
+        const double eps = x - 1.0, lne = nm::log(eps);
         const double c0 = kPiD * kPiD / 6.0, c1 = 1.0 - lne, c2 = -(1.0 - 2.0 * lne) / 4.0, c3 = (1.0 - 3.0 * lne) / 9.0;
         const double c4 = -(1.0 - 4.0 * lne) / 16.0, c5 = (1.0 - 5.0 * lne) / 25.0, c6 = -(1.0 - 6.0 * lne) / 36.0;
         const double c7 = (1.0 - 7.0 * lne) / 49.0, c8 = -(1.0 - 8.0 * lne) / 64.0;
         return c0 + eps * (c1 + eps * (c2 + eps * (c3 + eps * (c4 + eps * (c5 + eps * (c6 + eps * (c7 + eps * c8)))))));
     }
     if (x == 1.0) return kPiD * kPiD / 6.0;
-    if (x > 0.5) {
-        const double ser = dilog_series_2(1.0 - x);
-        const double log_x = NUSI_PLOG(x);
-        const double t1 = kPiD * kPiD / 6.0, t2 = ser, t3 = log_x * NUSI_PLOG(1.0 - x);
+    if (!(x > 0.25)) return x > 0.0 ? dilog_series_1(x) : 0.0;   // (x == 0 and NaN: GSL's last branch, 0)
+    const int br = x > 2.0 ? 0 : x > 1.01 ? 1 : x > 0.5 ? 2 : 3;
+    const double u = br == 0 ? 1.0 / x : br == 1 ? 1.0 - 1.0 / x : br == 2 ? 1.0 - x : x;   // GSL's series argument
+    const double ser = dilog_series_2(u);
+    if (br == 3) return ser;
+    const double log_x = nm::log(x);
+    const double log_u = br == 0 ? 0.0 : nm::log(u);   // log(1 - 1/x) resp. log(1 - x)
+    if (br == 0) {
+        const double t1 = kPiD * kPiD / 3.0, t2 = ser, t3 = 0.5 * log_x * log_x;
         return t1 - t2 - t3;
     }
-    if (x > 0.25) return dilog_series_2(x);
-    if (x > 0.0) return dilog_series_1(x);
-    return 0.0;
+    if (br == 1) {
+        const double log_term = log_x * (log_u + 0.5 * log_x);
+        const double t1 = kPiD * kPiD / 6.0, t2 = ser, t3 = log_term;
+        return t1 + t2 - t3;
+    }
+    const double t1 = kPiD * kPiD / 6.0, t2 = ser, t3 = log_x * log_u;
+    return t1 - t2 - t3;
 }
 
 // ---------------------------------------------------------------------------------------------- Clausen --
@@ -148,7 +180,7 @@ NUSI_FN double angle_restrict_pos(double theta)
     return r;
 }
 // gsl_sf_clausen_e: Cl2(x); aclaus_cs (clausen.c) summed by cheb_eval_e (order 14 on [-1, 1])
-NUSI_FN double clausen(double x)
+NUSI_FN_OUT double clausen(double x)
 {
     constexpr double kC[15] = {2.142694363766688447e+00, 0.723324281221257925e-01, 0.101642475021151164e-02,
                                0.3245250328531645e-04,   0.133315187571472e-05,    0.6213240591653e-07,
@@ -166,7 +198,7 @@ NUSI_FN double clausen(double x)
     }
     double val;
     if (x == 0.0) val = 0.0;
-    else if (x < x_cut) val = x * (1.0 - NUSI_PLOG(x));
+    else if (x < x_cut) val = x * (1.0 - nm::log(x));
     else {
         const double t = 2.0 * (x * x / (kPiD * kPiD) - 0.5);
         const double a = -1.0, b = 1.0;
@@ -179,7 +211,7 @@ NUSI_FN double clausen(double x)
             dd = temp;
         }
         d = yy * d - dd + 0.5 * kC[0];
-        val = x * (d - NUSI_PLOG(x));
+        val = x * (d - nm::log(x));
     }
     return val * sgn;
 }
@@ -187,7 +219,7 @@ NUSI_FN double clausen(double x)
 // ---------------------------------------------------------------------------------------------- complex --
 // dilogc_series_1 (s2 = false: sum r^k e^(i k theta) / k^2, first term r e^(i theta), kmax 50 + 22 / (-log r))
 // and series_2_c (s2 = true: sum z^k / (k^2 (k + 1)), first term r e^(i theta) / 2, kmax 30 + 18 / (-log r)) as
-// one loop; every operation is GSL's (the denominators (double) k * k and (double) k * k * (k + 1.0) are exact)
+// one loop; every operation is GSL's
 NUSI_FN void cseries(bool s2, double r, double x, double y, double& re, double& im)
 {
     const double cos_theta = x / r, sin_theta = y / r;
@@ -195,15 +227,14 @@ NUSI_FN void cseries(bool s2, double r, double x, double y, double& re, double& 
     double ck = cos_theta, sk = sin_theta, rk = r;
     double real_sum = s2 ? 0.5 * r * ck : r * ck;
     double imag_sum = s2 ? 0.5 * r * sk : r * sk;
-    const double nlr = -NUSI_PLOG(r);
+    const double nlr = -nm::log(r);
     const int kmax = s2 ? 30 + (int)(18.0 / nlr) : 50 + (int)(22.0 / nlr);
     for (int k = 2; k < kmax; k++) {
         const double ck_tmp = ck;
         ck = ck - (alpha * ck + beta * sk);
         sk = sk - (alpha * sk - beta * ck_tmp);
         rk *= r;
-        const double kk = (double)k * k;
-        const double q = rk / (s2 ? kk * (k + 1.0) : kk);
+        const double q = s2 ? div_k(rk, kKT.d2[k], kKT.y2[k]) : div_k(rk, kKT.d1[k], kKT.y1[k]);
         const double dr = q * ck, di = q * sk;
         real_sum += dr;
         imag_sum += di;
@@ -215,15 +246,15 @@ NUSI_FN void cseries(bool s2, double r, double x, double y, double& re, double& 
 // dilogc_series_3: |z| near 1, sum_{n <= 6} (log r)^n / n! H_n(theta)
 NUSI_FN void cseries_3(double r, double x, double y, double& re, double& im)
 {
-    const double theta = NUSI_PATAN2(y, x);
+    const double theta = nm::atan2(y, x);
     const double cos_theta = x / r, sin_theta = y / r;
-    const double a = NUSI_PLOG(r);
+    const double a = nm::log(r);
     const double omc = 1.0 - cos_theta, omc2 = omc * omc;
     double H_re[7], H_im[7];
     H_re[0] = kPiD * kPiD / 6.0 + 0.25 * (theta * theta - 2.0 * kPiD * fabs(theta));
     H_im[0] = clausen(theta);
-    H_re[1] = -0.5 * NUSI_PLOG(2.0 * omc);
-    H_im[1] = -NUSI_PATAN2(-sin_theta, omc);
+    H_re[1] = -0.5 * nm::log(2.0 * omc);
+    H_im[1] = -nm::atan2(-sin_theta, omc);
     H_re[2] = -0.5;
     H_im[2] = 0.5 * sin_theta / omc;
     H_re[3] = -0.5 / omc;
@@ -247,53 +278,60 @@ NUSI_FN void cseries_3(double r, double x, double y, double& re, double& im)
     im = sum_im;
 }
 // dilogc_fundamental (r < 1, x <= 0.732): series_3 above r = 0.98, dilogc_series_2 above 0.25, else series_1
-NUSI_FN void fundamental(double r, double x, double y, double& re, double& im)
+NUSI_FN_OUT cd fundamental(double r, double x, double y)
 {
+    double re, im;
     if (r > 0.98) {
         cseries_3(r, x, y, re, im);
-        return;
+        return cd{re, im};
     }
     const bool s2 = r > 0.25;
-    double sre, sim;
-    cseries(s2, r, x, y, sre, sim);
-    if (!s2) {
-        re = sre;
-        im = sim;
-        return;
-    }
+    cseries(s2, r, x, y, re, im);
+    if (!s2) return cd{re, im};
     // dilogc_series_2: + (1 - z) log(1 - z) / z + 1, log(1 - z) by gsl_sf_complex_log_e
     const double zr = 1.0 - x, zi = -y;
     const double ax = fabs(zr), ay = fabs(zi);
     const double mn = ax < ay ? ax : ay, mx = ax > ay ? ax : ay;
-    const double ln_r = NUSI_PLOG(mx) + 0.5 * NUSI_PLOG(1.0 + (mn / mx) * (mn / mx));
-    const double ln_t = NUSI_PATAN2(zi, zr);
+    const double ln_r = nm::log(mx) + 0.5 * nm::log(1.0 + (mn / mx) * (mn / mx));
+    const double ln_t = nm::atan2(zi, zr);
     const double t_x = (ln_r * x + ln_t * y) / (r * r);
     const double t_y = (-ln_r * y + ln_t * x) / (r * r);
     const double r_x = (1.0 - x) * t_x + y * t_y;
     const double r_y = (1.0 - x) * t_y - y * t_x;
-    re = sre + r_x + 1.0;
-    im = sim + r_y;
+    return cd{re + r_x + 1.0, im + r_y};
 }
 // dilogc_unitdisk: |z| < 1; x > 0.732 reflected, Li2(z) = -Li2(1 - z) + zeta2 - log(z) log(1 - z)
-NUSI_FN void unitdisk(double x, double y, double& re, double& im)
+NUSI_FN cd unitdisk(double x, double y)
 {
     const double zeta2 = kPiD * kPiD / 6.0;
     const double r = gsl::hypot(x, y);
-    if (x > 0.732) {
-        const double x_tmp = 1.0 - x, y_tmp = -y;
-        const double r_tmp = gsl::hypot(x_tmp, y_tmp);
-        double re_tmp, im_tmp;
-        fundamental(r_tmp, x_tmp, y_tmp, re_tmp, im_tmp);
-        const double lnz = NUSI_PLOG(r), lnomz = NUSI_PLOG(r_tmp);
-        const double argz = NUSI_PATAN2(y, x), argomz = NUSI_PATAN2(y_tmp, x_tmp);
-        re = -re_tmp + zeta2 - lnz * lnomz + argz * argomz;
-        im = -im_tmp - argz * lnomz - argomz * lnz;
-        return;
-    }
-    fundamental(r, x, y, re, im);
+    const bool refl = x > 0.732;
+    const double x_tmp = 1.0 - x, y_tmp = -y;
+    const double r_tmp = refl ? gsl::hypot(x_tmp, y_tmp) : r;
+    const cd f = fundamental(refl ? r_tmp : r, refl ? x_tmp : x, refl ? y_tmp : y);   // one call site
+    if (!refl) return f;
+    const double lnz = nm::log(r), lnomz = nm::log(r_tmp);
+    const double argz = nm::atan2(y, x), argomz = nm::atan2(y_tmp, x_tmp);
+    return cd{-f.r + zeta2 - lnz * lnomz + argz * argomz, -f.i - argz * lnomz - argomz * lnz};
 }
 
 }  // namespace gsl
+
+// A cost estimate of gsl_cli2(x, y), used only to order work (no value depends on it): the iterations of the series
+// GSL's dispatch selects -- 0 on the real axis / unit circle, 8 for dilogc_series_3, else ~36 / -log r of the
+// fundamental-region radius r (the terms fall as r^k), plus the series_2 post-processing
+NUSI_FN double gsl_cli2_cost(double x, double y)
+{
+    const double r2 = x * x + y * y;
+    if (y == 0.0 || fabs(r2 - 1.0) < gsl::kEps) return 0.0;
+    double ux = x, uy = y;
+    if (!(r2 < 1.0)) { ux = x / r2; uy = -y / r2; }
+    const double fx = ux > 0.732 ? 1.0 - ux : ux, fy = uy;
+    const double r = sqrt(fx * fx + fy * fy);
+    if (r > 0.98) return 8.0;
+    const double n = 36.0 / -nm::log(r);
+    return r > 0.25 ? 10.0 + n : n;
+}
 
 // gsl_sf_dilog (x < 0: -dilog_xge0(-x) + dilog_xge0(x^2) / 2)
 NUSI_FN_OUT double gsl_li2(double x)
@@ -303,30 +341,27 @@ NUSI_FN_OUT double gsl_li2(double x)
     return -d1 + 0.5 * d2;
 }
 
-// gsl_sf_complex_dilog_xy_e
+// gsl_sf_complex_dilog_xy_e: the real axis; |z| within eps of 1 (Lewin A.2.4.1 / A.2.4.2); the unit disk; 1/z
+// into the unit disk, unwound with Li2(z) + Li2(1/z) = -zeta2 - log(-z)^2 / 2
 NUSI_FN_OUT cd gsl_cli2(double x, double y)
 {
     const double zeta2 = gsl::kPiD * gsl::kPiD / 6.0;
     const double r2 = x * x + y * y;
-    if (y == 0.0) return cd{gsl_li2(x), (x >= 1.0) ? -gsl::kPiD * NUSI_PLOG(x) : 0.0};
-    if (fabs(r2 - 1.0) < gsl::kEps) {   // Lewin A.2.4.1 / A.2.4.2
-        const double theta = NUSI_PATAN2(y, x);
+    if (y == 0.0) return cd{gsl_li2(x), (x >= 1.0) ? -gsl::kPiD * nm::log(x) : 0.0};
+    if (fabs(r2 - 1.0) < gsl::kEps) {
+        const double theta = nm::atan2(y, x);
         const double term1 = theta * theta / 4.0, term2 = gsl::kPiD * fabs(theta) / 2.0;
         return cd{zeta2 + term1 - term2, gsl::clausen(theta)};
     }
-    double re, im;
-    if (r2 < 1.0) {
-        gsl::unitdisk(x, y, re, im);
-        return cd{re, im};
-    }
-    // 1/z into the unit disk, unwound with Li2(z) + Li2(1/z) = -zeta2 - log(-z)^2 / 2
+    const bool inv = !(r2 < 1.0);
+    const cd u = gsl::unitdisk(inv ? x / r2 : x, inv ? -y / r2 : y);   // one instance
+    if (!inv) return u;
     const double r = sqrt(r2);
-    gsl::unitdisk(x / r2, -y / r2, re, im);
-    const double theta = NUSI_PATAN2(y, x), theta_abs = fabs(theta), theta_sgn = (theta < 0.0 ? -1.0 : 1.0);
-    const double ln_minusz_re = NUSI_PLOG(r), ln_minusz_im = theta_sgn * (theta_abs - gsl::kPiD);
+    const double theta = nm::atan2(y, x), theta_abs = fabs(theta), theta_sgn = (theta < 0.0 ? -1.0 : 1.0);
+    const double ln_minusz_re = nm::log(r), ln_minusz_im = theta_sgn * (theta_abs - gsl::kPiD);
     const double lmz2_re = ln_minusz_re * ln_minusz_re - ln_minusz_im * ln_minusz_im;
     const double lmz2_im = 2.0 * ln_minusz_re * ln_minusz_im;
-    return cd{-re - 0.5 * lmz2_re - zeta2, -im - 0.5 * lmz2_im};
+    return cd{-u.r - 0.5 * lmz2_re - zeta2, -u.i - 0.5 * lmz2_im};
 }
 
 }  // namespace nusi

@@ -424,6 +424,9 @@ void k_alpha_batch(GridDev g, const Point* __restrict__ pts, const SplineSet* __
     const int mbd = alpha_batch_memb_doubles(cs, ct);
     double* tmp = X;
     double* mix = X + 4 * kCC;
+    double* const kcost = X + 3 * kCC;                               // (kRef) [cc] corner costs
+    int* const kperm = reinterpret_cast<int*>(X + 4 * kCC);          // (kRef) [cc] corners by decreasing cost
+    static_assert(kXFields * kCC >= 4 * kCC + kCC / 2 + 1, "the kRef corner order fits X");
     const int mjobs = ct + cs + kAlphaTile;
     int wsh = 0;
 #pragma unroll 1
@@ -451,6 +454,22 @@ void k_alpha_batch(GridDev g, const Point* __restrict__ pts, const SplineSet* __
             __syncthreads();   // X is rewritten with the member coefficients (kRef: with the member corners)
             if (!kRef)
                 for (int j = tid; j < cc; j += kTileThreads) b_xshared(j, edgk, ct, cs, X);
+            if (kRef) {
+                // GSL's series run a data-dependent number of iterations (~10 to ~900): the corners go to the
+                // work-items in decreasing order of their cost (gsl_cli2_cost, from the batch's first point), so
+                // that each wave's lanes take similar counts (kcost [cc] and kperm [cc] behind the member corners)
+                if (tid < cc) kcost[tid] = alpha_batch_mcorner_ref_cost(P, tid, edgk, ct, cs);
+                __syncthreads();
+                if (tid < cc) {
+                    const double c = kcost[tid];
+                    int rank = 0;
+                    for (int i = 0; i < cc; ++i) {
+                        const double ci = kcost[i];
+                        rank += (ci > c || (ci == c && i < tid)) ? 1 : 0;
+                    }
+                    kperm[rank] = tid;
+                }
+            }
         }
         // ---- the points, kBatchQC at a time: their member edge leaves in one round, then point by point.
         // (Two points per pair of barriers -- 512-thread workgroups whose halves share the batch's leaves -- measured
@@ -500,8 +519,9 @@ void k_alpha_batch(GridDev g, const Point* __restrict__ pts, const SplineSet* __
                 } else {
                     __syncthreads();   // member edges written / the previous point's combine is done with mem
                     if (cornered) {
-                        if (kRef)
-                            for (int j = tid; j < cc; j += kTileThreads) alpha_batch_mcorner_ref_job(Q, j, edgk, ct, cs, X);
+                        if (kRef) {
+                            if (tid < cc) alpha_batch_mcorner_ref_job(Q, kperm[tid], edgk, ct, cs, X);
+                        }
                         else
                             for (int j = tid; j < cc; j += kTileThreads) alpha_batch_mcorner_job(Q, j, edgk, ct, cs, X, memb, mem);
                     }

@@ -1117,6 +1117,15 @@ NUSI_FN void alpha_batch_mcorner_ref_job(const Point& P, int j, const double* ed
     alpha_member_ref(edgk[kTEdgeFields * ct + kSEdgeVal * cs + si], edgk[kTEdgeVal * ct + ti], P.a_gr, Dcr, Dci, A);
     mem[j] = Dcr; mem[kCC + j] = Dci; mem[2 * kCC + j] = A;
 }
+// NUSI_OPT_REFERENCE_ORDER: the cost of corner j's member dilogarithm for point P (gsl_cli2_cost of its quotient;
+// the points of a batch differ only in gr, which moves the quotient's small imaginary part), to order the corners
+NUSI_FN double alpha_batch_mcorner_ref_cost(const Point& P, int j, const double* edgk, int ct, int cs)
+{
+    const int si = j / ct, ti = j - si * ct;
+    const double S = edgk[kTEdgeFields * ct + kSEdgeVal * cs + si], t = edgk[kTEdgeVal * ct + ti];
+    const cd z = (1 + S + t) / C(2 + t, -P.a_gr);
+    return gsl_cli2_cost(z.r, z.i);
+}
 // xlog / ylog leaves of mass state k into xl [cs][kAlphaTile], yl [kAlphaTile][ct] (alpha_tile_mixed_job's jobs)
 NUSI_FN void alpha_batch_mixed_job(int j, const double* edgk, int ct, int cs, const int* tl, const int* th,
                                    const int* sl, const int* sh, int n0, int m0, int T, int Tm, double* xl, double* yl)

@@ -92,7 +92,8 @@ class Plan:
         """A/B and test options (nusi_plan_set_option): _lib.OPT_ALPHA_BATCH (max tables per alpha batch, 0 =
         auto), OPT_ALPHA_KERNEL (0 batch, 1 tile, 2 per entry), OPT_CASCADE_RHS (1 = one point per cascade
         workgroup), OPT_STEP_PASSES (1 = the step-pass cascade also where one pass fits), OPT_SHIFT_REUSE (K > 0:
-        the opt-in scan mode sharing tables across m_phi on the r^(-o/2) lattice, o <= K), OPT_REFERENCE_ORDER (1 =
+        the opt-in scan mode sharing tables across m_phi on the r^(-o/2) lattice, o <= K; only tables with g <= 0.05
+        share, the others are built directly), OPT_REFERENCE_ORDER (1 =
         the tables in the reference's own operation order for the complex dilogarithms; include/nusi.h)."""
         _lib.check(_lib.load().nusi_plan_set_option(self._h, int(option), int(value)))
 

@@ -128,6 +128,23 @@ def gamma_batches(points, rhs=16):
     return out
 
 
+def bs_groups(points, rhs=0, gamma=True, pairs=True):
+    """The workgroups of the block-synchronous cascade as nusi_plan_evolve forms them (nusi_capi.cpp, the k_cascade_bs
+    grouping): per table, all its points (any source) in near-equal groups of up to min(rhs or 16, 16) when it has 3
+    or more and the gamma instance fits the grid (`gamma`), else pairs when it has 2 (`pairs`), else one per
+    workgroup; a group of 3+ runs on k_cascade_bs_gamma, of 2 on k_cascade_bs_pairs, of 1 on k_cascade_bs.
+    Returns the group sizes."""
+    from collections import Counter
+    rmax = rhs or 16
+    g16, g2 = gamma and rmax >= 3, pairs and rmax >= 2
+    out = []
+    for c in Counter(table_key(p) for p in points).values():
+        cap = min(rmax, 16) if (g16 and c >= 3) else 2 if (g2 and c >= 2) else 1
+        nb = -(-c // cap)
+        out += [c * (k + 1) // nb - c * k // nb for k in range(nb)]
+    return out
+
+
 def cascade_gb_bytes_per_batch(N, Nz):
     """HBM bytes one gamma-batch workgroup must read: the columns each pass visits (as the step-pass kernel), Gamma
     and alphaTilde; the FIFO of the passes' last step stays in L2/MALL (3 N x 16 doubles per pass, written once,
