@@ -101,25 +101,50 @@ def rank_points(args, rank, world):
         return pts, ("C3: %d-point g scan per GPU at m_phi=1e5, N_E=1200, lE 10->17, phi-phi on (synthetic values on "
                      "the reference's exact table axes and dims {5000,100} / {1000,1000,100}, 400 MB float32 in HBM; "
                      "nusiprop_amd.phiphi_tables), power-law source" % P)
+    lo, hi, allp, desc = shard_of_scan(args, rank, world)
+    return allp[lo:hi], desc
+
+
+def global_scan(args, world):
+    """The whole scan the `world` ranks share (C4, C4s, C5), and whether the per-GPU work is fixed as the GPU count
+    grows ("weak") or the scan is ("strong"):
+      c4 / c4s: the BASELINE config-4 grid (32 m_phi x 32 g) once per GPU, at gamma = 2.5 + 0.05 b for block b --
+                one scan of 1024 N points, gamma slowest, so every GPU's shard is one 1024-point block (weak);
+      c5:       BASELINE config 5, the 65 536-point (m_phi 64 x g 64 x gamma 16) scan, gamma fastest, partitioned
+                over the GPUs (strong); --points P takes its first P points."""
+    from nusiprop_amd import scan
+    if args.workload in ("c4", "c4s"):
+        grid = scan.c4_points if args.workload == "c4" else scan.c4s_points
+        P = args.points or 1024
+        allp = []
+        for b in range(world):
+            blk = grid(si=2.5 + 0.05 * b)
+            while len(blk) < P:
+                blk = blk + blk
+            allp += blk[:P]
+        return allp, "weak"
+    allp = scan.c5_points()
+    if args.points:
+        allp = (allp * (1 + args.points // len(allp)))[:args.points]
+    return allp, "strong"
+
+
+def shard_of_scan(args, rank, world):
+    """This rank's block [lo, hi) of global_scan: scan.shard_aligned, the function nusiprop_amd.dist.evolve_sharded
+    partitions with (block ends on table-group boundaries: a gamma batch sharing a Stage-A table stays on one GPU)."""
+    from nusiprop_amd import scan
+    allp, _ = global_scan(args, world)
+    lo, hi = scan.shard_aligned(allp, world, rank)
     if args.workload == "c4":
-        P = args.points or 1024
-        pts = scan.c4_points(si=2.5 + 0.05 * rank)
-        desc = "C4: (m_phi 32 x g 32) scan per GPU, N_E=300, lE 12->17, power-law source, gamma=2.5+0.05*rank"
+        desc = ("C4: (m_phi 32 x g 32) scan per GPU, N_E=300, lE 12->17, power-law source; rank r's block of the %d-point "
+                "scan (gamma = 2.5 + 0.05 b per 1024-point block b, scan.shard_aligned)" % len(allp))
     elif args.workload == "c4s":
-        P = args.points or 1024
-        pts = scan.c4s_points(si=2.5 + 0.05 * rank)
         desc = ("C4s (opt-in NUSI_OPT_SHIFT_REUSE=128): (m_phi 32 on the r^(-o/2) lattice, o = 0, 4, .., 124 below "
                 "10^6.533 x g 32) scan per GPU, N_E=300, lE 12->17, power-law source; one base table set per g")
     else:
-        P = args.points or 8192
-        allp = scan.c5_points()
-        lo = (rank * P) % len(allp)
-        pts = (allp + allp)[lo:lo + P]
-        desc = ("C5: a %d-point block per GPU of the 65536-point (m_phi 64 x g 64 x gamma 16) scan, N_E=300, "
-                "power-law source; %d distinct tables per block (gamma batches share them)" % (P, P // 16))
-    while len(pts) < P:
-        pts = pts + pts
-    return pts[:P], desc
+        desc = ("C5: rank r's block of the %d-point (m_phi 64 x g 64 x gamma 16) scan over %d GPU(s) (scan.shard_aligned: "
+                "%d points here), N_E=300, power-law source; gamma batches of 16 share a table" % (len(allp), world, hi - lo))
+    return lo, hi, allp, desc
 
 
 def host_cores():
@@ -410,7 +435,10 @@ def file_sha256(path):
 
 def dry_run(args, world, rank):
     """The launch / rank / reduction path without GPU work (gloo): each rank 'steps' for 1 ms; the line carries
-    n_gpus = the ranks that ran and value null."""
+    n_gpus = the ranks that ran and value null.  For the scan workloads every rank also forms its shard of the
+    scan (shard_of_scan) and rank 0 checks the blocks: they cover every point exactly once, in order, and no
+    group of points sharing a Stage-A table (a C5 gamma batch) is split across ranks."""
+    import numpy as np
     import torch
     dist = None
     if world > 1:
@@ -421,6 +449,24 @@ def dry_run(args, world, rank):
         time.sleep(0.001)
     dt = time.perf_counter() - t0
     ranks = 1
+    shard = None
+    if args.workload in ("c4", "c4s", "c5"):
+        from nusiprop_amd import scan
+        lo, hi, allp, _ = shard_of_scan(args, rank, world)
+        blocks = torch.tensor([[lo, hi]], dtype=torch.int64)
+        if dist is not None:
+            got = [torch.zeros_like(blocks) for _ in range(world)]
+            dist.all_gather(got, blocks)
+            blocks = torch.cat(got)
+        bl = [tuple(int(v) for v in b) for b in blocks.tolist()]
+        seen = np.zeros(len(allp), dtype=np.int64)
+        for a, b in bl:
+            seen[a:b] += 1
+        keys = [scan.table_key(p) for p in allp]
+        split = sum(1 for a, _ in bl if 0 < a < len(allp) and keys[a] == keys[a - 1])
+        shard = {"points": len(allp), "blocks": bl, "covered_once": bool(np.all(seen == 1)),
+                 "in_order": all(bl[i][1] == bl[i + 1][0] for i in range(len(bl) - 1)), "table_groups_split": split,
+                 "scaling": global_scan(args, world)[1]}
     if dist is not None:
         tt = torch.tensor([dt, 1.0], dtype=torch.float64)
         dist.all_reduce(tt[:1], op=dist.ReduceOp.MAX)
@@ -428,9 +474,12 @@ def dry_run(args, world, rank):
         dist.all_reduce(one, op=dist.ReduceOp.SUM)
         dt, ranks = float(tt[0]), int(one.item())
     if rank == 0:
-        print(json.dumps({"metric": METRIC, "value": None, "unit": "propagations/s", "n_gpus": world,
-                          "ranks_reporting": ranks, "steps": args.steps, "warmup": args.warmup,
-                          "ms_per_step": dt / max(args.steps, 1) * 1e3, "dry_run": True}), flush=True)
+        line = {"metric": METRIC, "value": None, "unit": "propagations/s", "n_gpus": world, "ranks_reporting": ranks,
+                "steps": args.steps, "warmup": args.warmup, "ms_per_step": dt / max(args.steps, 1) * 1e3,
+                "dry_run": True}
+        if shard is not None:
+            line["shard_check"] = shard
+        print(json.dumps(line), flush=True)
     if dist is not None:
         dist.destroy_process_group()
 
@@ -590,7 +639,7 @@ def run(args, world, rank, local, dist, plan, pts, desc, pp_tables):
         "warmup": args.warmup,
         "ms_per_step": dt / args.steps * 1e3,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": global_scan(args, world)[1] if args.workload in ("c4", "c4s", "c5") else "weak",
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic (deterministic scan grid; power-law source)",
@@ -654,6 +703,19 @@ def run(args, world, rank, local, dist, plan, pts, desc, pp_tables):
                                    "(transcendental leaves), neither HBM nor MFMA"}
     else:   # the cascade dominates (C5's gamma batches), or no alpha counters for this binary
         out["roofline"] = dict(out["roofline_cascade"])
+    if dist is not None and args.workload in ("c4", "c4s", "c5"):
+        # the scan's only data exchange, after the timed region: the fluxes of every rank's block gathered to rank 0
+        # (nusiprop_amd.dist._gather_blocks, as evolve_sharded does; float64 tensors staged on the GPU, RCCL)
+        from nusiprop_amd.dist import _gather_blocks
+        torch.cuda.synchronize()
+        barrier()
+        tg = time.perf_counter()
+        parts = _gather_blocks(fla.cpu().numpy(), P, (3, N), None)
+        tg = time.perf_counter() - tg
+        out["gather"] = {"seconds": tg, "bytes": 8 * 3 * N * len(global_scan(args, world)[0]),
+                         "note": "flavour fluxes of all ranks to rank 0 (dist._gather_blocks), not in the timed region"}
+        if rank == 0:
+            out["gather"]["points_gathered"] = int(sum(len(x) for x in parts))
     if args.workload == "c1" and rank == 0:
         out["single_propagation"], _ = single_point_latency(pts[0], max(20, args.steps), args.reference_order)
         out["single_propagation"]["plan_ms_per_step"] = dt / args.steps * 1e3

@@ -68,3 +68,34 @@ def test_parity_sample_and_rel_err():
     assert sum(1 for i in a if pts[i]["g"] == 1.0) == 16
     assert bench.rel_err([1.0, 0.0], [1.0, 0.0]) == 0.0 and bench.rel_err([1.0, 1e-300], [1.0, 0.0]) == float("inf")
     assert abs(bench.rel_err(np.array([1.0 + 1e-12]), np.array([1.0])) - 1e-12) < 1e-15
+
+
+def test_c5_dry_run_world8_is_one_scan_partition():
+    """`--gpus 8 --workload c5` partitions the 65 536-point BASELINE config-5 scan with
+    scan.shard_aligned (the function dist.evolve_sharded uses): the eight blocks cover every point exactly once, in
+    order, 8192 per GPU, and no gamma batch (16 points sharing a Stage-A table) is split; strong scaling."""
+    out = _bench(["--gpus", "8", "--dry-run", "--workload", "c5", "--steps", "1", "--warmup", "0"], timeout=600)
+    assert out.returncode == 0, out.stderr
+    s = _line(out)["shard_check"]
+    assert s["points"] == 65536 and s["covered_once"] and s["in_order"] and s["table_groups_split"] == 0
+    assert [b - a for a, b in s["blocks"]] == [8192] * 8 and s["scaling"] == "strong"
+
+
+def test_c5_dry_run_uneven_world_keeps_gamma_batches():
+    """Three ranks: 65 536 / 3 is not a multiple of the 16-point gamma batches; the block ends move to batch
+    boundaries (no batch split), every point still covered once."""
+    out = _bench(["--gpus", "3", "--dry-run", "--workload", "c5", "--steps", "1", "--warmup", "0"], timeout=600)
+    assert out.returncode == 0, out.stderr
+    s = _line(out)["shard_check"]
+    assert s["covered_once"] and s["in_order"] and s["table_groups_split"] == 0
+    assert all((b - a) % 16 == 0 for a, b in s["blocks"])
+
+
+def test_c4_dry_run_world2_weak_blocks():
+    """C4 on N GPUs is one scan of 1024 N points (the config-4 grid once per GPU at gamma = 2.5 + 0.05 b), each rank
+    one 1024-point block: weak scaling, every point covered once."""
+    out = _bench(["--gpus", "2", "--dry-run", "--workload", "c4", "--steps", "1", "--warmup", "0"])
+    assert out.returncode == 0, out.stderr
+    s = _line(out)["shard_check"]
+    assert s["points"] == 2048 and s["covered_once"] and s["blocks"] == [[0, 1024], [1024, 2048]]
+    assert s["scaling"] == "weak"
