@@ -286,7 +286,10 @@ __global__ __launch_bounds__(kTileThreads) NUSI_TILE_ATTR void k_alpha_tile(Grid
 #ifndef NUSI_BATCH_QC   // points per member-edge round (5: C4 alpha 6.05 -> 5.95 ms vs 4, profiles/r2q)
 #define NUSI_BATCH_QC 5
 #endif
-constexpr int kBatchQC = NUSI_BATCH_QC;   // kBatchQC (ct + cs + kAlphaTile) <= 256 jobs
+constexpr int kBatchQC = NUSI_BATCH_QC;
+#ifndef NUSI_REFO_NOSORT   // timing A/B only: 1 = the reference-order member corners in tile order (no cost sort)
+#define NUSI_REFO_NOSORT 0
+#endif   // kBatchQC (ct + cs + kAlphaTile) <= 256 jobs
 // NUSI_BATCH_PIPE (A/B): the member corners of point q + 1 are formed while point q combines (two mem buffers),
 // one barrier per point instead of two
 #ifndef NUSI_BATCH_PIPE
@@ -467,6 +470,7 @@ void k_alpha_batch(GridDev g, const Point* __restrict__ pts, const SplineSet* __
                         const double ci = kcost[i];
                         rank += (ci > c || (ci == c && i < tid)) ? 1 : 0;
                     }
+                    if (NUSI_REFO_NOSORT) rank = tid;   // (timing A/B: the corners in tile order)
                     kperm[rank] = tid;
                 }
             }

@@ -541,11 +541,15 @@ NUSI_FN void alpha_member_corner(const MemberShared& M, double S, double t, doub
 // nuSIprop.hpp:1432-1438, 1444-1451), by GSL's algorithm (gsl_cli2), and A = carg(-((-1 + i gr + S) / (2 - i gr + t)))
 // (:1456); no Taylor expansion about the real point and no sum of edge arguments.  The oracle's
 // member_dc_ref / member_arg_ref (ora_set_reference_order(1)).
+#ifndef NUSI_REFO_STUB   // timing A/B only: 1 = the member corners without the dilogarithm (Dc = z), 2 = nothing
+#define NUSI_REFO_STUB 0
+#endif
 NUSI_FN void alpha_member_ref(double S, double t, double gr, double& Dcr, double& Dci, double& A)
 {
+    if (NUSI_REFO_STUB == 2) { Dcr = Dci = A = 0.0; return; }
     const cd dt = C(2 + t, -gr);
     const cd z = (1 + S + t) / dt;
-    const cd Dc = gsl_cli2(z.r, z.i);
+    const cd Dc = NUSI_REFO_STUB == 1 ? z : gsl_cli2(z.r, z.i);
     Dcr = Dc.r;
     Dci = Dc.i;
     A = carg(-(C(-1 + S, gr) / dt));
