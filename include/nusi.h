@@ -149,15 +149,16 @@ int nusi_plan_profile_end(nusi_plan *plan, double *sum_ms3, int *ncalls);
  * tolerance against the reference algorithm (<= 1e-11 relative, the same
  * exact zeros); the choice is a performance / cross-check knob:
  * AUTO (default, also for the object API) = MFMA.
- * MFMA = the warp-specialised wavefront with the push on the fp64 matrix
- *   cores (k_cascade_ws, one pass, Nz-1 <= 48; k_cascade_ws_passes beyond),
- *   for both sources and both scattering modes; points sharing a Stage-A
- *   table share one workgroup (multi-RHS).  Grids beyond its limits fall back
- *   to REG / LDS.
- * WAVEFRONT, REG, LDS = the bit-exact scalar kernels (right-looking fma()s in
- *   one fixed order: WAVEFRONT and REG agree bit for bit): wavefront when
- *   the grid fits it (Nz-1 <= 48, T-1 <= 512), else register-resident
- *   (N <= 1280), else LDS.
+ * MFMA = the block-synchronous wavefront with the push on the fp64 matrix
+ *   cores (k_cascade_bs: one pass up to 48 redshift steps, step passes
+ *   beyond), for both sources and both scattering modes; points sharing a
+ *   Stage-A table share one workgroup (multi-RHS: pairs, or the gamma batch
+ *   of up to 16).  Grids beyond its limits (T - 1 > 14 x 128 rows) fall back
+ *   to the scalar kernel.
+ * WAVEFRONT, REG, LDS = the bit-exact scalar cascade k_cascade (one
+ *   wavefront per point, any N; right-looking fma()s in one fixed order).
+ *   The three names are kept for the API; since round 5 they select the same
+ *   kernel.
  * NUSI_EPARAM for an unknown kind. */
 #define NUSI_CASCADE_AUTO 0
 #define NUSI_CASCADE_WAVEFRONT 1
@@ -175,13 +176,18 @@ int nusi_plan_set_cascade(nusi_plan *plan, int kind);
  *                          (all three give the same tables bit for bit)
  *   NUSI_OPT_CASCADE_RHS   max points sharing a table per MFMA-cascade
  *                          workgroup: 0 = automatic (the gamma batch for
- *                          tables with >= 3 power-law points, pairs for the
- *                          rest), 1 = one point each, 2 = pairs
- *                          (k_cascade_ws<R = 2>), 3..16 = the gamma batch
- *                          k_cascade_gb (power-law points of a table, gamma
- *                          on the MFMA N dimension) of up to that many
+ *                          tables with >= 3 points, pairs for two), 1 = one
+ *                          point each, 2 = pairs (k_cascade_bs_pairs),
+ *                          3..16 = the gamma batch k_cascade_bs_gamma (the
+ *                          points of a table, gamma on the MFMA N
+ *                          dimension) of up to that many.  The MFMA sums in
+ *                          blocks of four columns, so a point's fluxes depend
+ *                          on its grouping to rounding (<= 1e-13), not bit for
+ *                          bit; 1 makes them independent of the call's other
+ *                          points
  *   NUSI_OPT_STEP_PASSES   0 = automatic (step passes beyond 48 redshift
- *                          steps), 1 = always the step-pass kernel
+ *                          steps), 1 = always the step-pass instance (one
+ *                          point per workgroup)
  *   NUSI_OPT_SHIFT_REUSE   opt-in scan mode, K in
  *                          [0, 128]; 0 = off (default).  alpha / Gamma /
  *                          alphaTilde see the energies only through
@@ -204,33 +210,31 @@ int nusi_plan_set_cascade(nusi_plan *plan, int kind);
 #define NUSI_OPT_STEP_PASSES 4
 #define NUSI_OPT_SHIFT_REUSE 5
 /*   NUSI_OPT_REFERENCE_ORDER  1 = build Gamma / alphaTilde / alpha in the
- *                          reference's own operation order: every complex
- *                          dilogarithm by gsl_sf_complex_dilog_xy_e's
- *                          general series (no near-axis Taylor shortcut),
- *                          and the alpha table's s-t interference member
- *                          leaves as the dilogarithm of the reference's
- *                          quotient (1+S+t)/(2 - i gr + t) and carg of its
- *                          expression (nuSIprop.hpp:1428-1467, 843-878,
- *                          1135-1192).  0 = the default shared-algorithm
- *                          order (batch-shared Taylor coefficients, faster).
- *                          Both are bit-identical to the oracle in the
- *                          matching mode; they differ from each other where
- *                          the closed forms cancel. */
+ *                          reference's own arithmetic: every gsl_sf_dilog /
+ *                          gsl_sf_complex_dilog_xy_e call site by GSL's own
+ *                          algorithms (dilog.c restated, nusi_gsl.hpp), and
+ *                          the alpha table's s-t interference member leaves
+ *                          as the dilogarithm of the reference's quotient
+ *                          (1+S+t)/(2 - i gr + t) and carg of its expression
+ *                          (nuSIprop.hpp:1428-1467, 843-878, 1135-1192).
+ *                          0 = the shared-algorithm order (Bernoulli series,
+ *                          batch-shared Taylor coefficients; faster).  Both
+ *                          are bit-identical to the oracle in the matching
+ *                          mode; they differ from each other where the
+ *                          closed forms cancel. */
 #define NUSI_OPT_REFERENCE_ORDER 6
-/*   NUSI_OPT_CASCADE_SYNC  the MFMA cascade's synchronisation: 0 = automatic,
- *                          1 = the per-stage kernels (k_cascade_ws / gb /
- *                          wsp: every wave meets once per wavefront stage),
- *                          2 = the block-synchronous kernel k_cascade_bs
- *                          (twice per block of four stages; the same
- *                          operations on the same operands).  Automatic
- *                          = 2 (unless NUSI_OPT_STEP_PASSES forces the
- *                          per-stage step-pass kernel). */
+/*   NUSI_OPT_CASCADE_SYNC  the MFMA cascade's synchronisation: 0 = automatic
+ *                          = 2 = the block-synchronous kernel k_cascade_bs
+ *                          (every wave meets twice per block of four
+ *                          stages).  1 (the per-stage kernels k_cascade_ws /
+ *                          gb / wsp of rounds 2-3) is refused: those kernels
+ *                          were removed in round 5. */
 #define NUSI_OPT_CASCADE_SYNC 7
 int nusi_plan_set_option(nusi_plan *plan, int option, int value);
 /* per-point NUSI_WARN_* bits of the last call */
 int nusi_plan_warnings(nusi_plan *plan, int *out, int n);
 /* Names of the main alpha-table and cascade kernels the last call launched (static strings, e.g.
- * "k_alpha_batch", "k_cascade_ws"); for reports -- bench.py's roofline lines.  No reference
+ * "k_alpha_batch", "k_cascade_bs"); for reports -- bench.py's roofline lines.  No reference
  * counterpart. */
 int nusi_plan_kernels(const nusi_plan *plan, const char **alpha, const char **cascade);
 /* Copy point `i`'s Stage-A tables of the last call to the host (parity

@@ -413,24 +413,21 @@ struct nusi_plan {
     nusi::Point* h_pts = nullptr;  // pinned
     nusi::Point* d_tpts = nullptr;  // one representative per distinct table (table kernels)
     nusi::Point* h_tpts = nullptr;  // pinned
-    int2* d_groups = nullptr;       // multi-RHS cascade: pairs of points sharing a table slot
-    int2* h_groups = nullptr;       // pinned
     int* d_batches = nullptr;       // alpha-table batches (nusi::launch_alpha): first table | count << 24
     int* h_batches = nullptr;       // pinned
     int alpha_batch = 0;            // NUSI_OPT_ALPHA_BATCH: max tables per batch; 0 = auto
     int alpha_kind = 0;             // NUSI_OPT_ALPHA_KERNEL: 0 k_alpha_batch, 1 k_alpha_tile<G> (<= 4), 2 per entry
     int cascade_rhs = 0;            // NUSI_OPT_CASCADE_RHS: 0 = auto, 1 = one point per MFMA-cascade workgroup,
-                                    // 2 = pairs, 3..16 = gamma batches of up to that many (k_cascade_gb)
+                                    // 2 = pairs, 3..16 = gamma batches of up to that many (k_cascade_bs_gamma)
     int* d_gidx = nullptr;          // gamma batches: the points of each batch, batch after batch
     int* h_gidx = nullptr;          // pinned
     int2* d_gbgrp = nullptr;        // ... per batch: first index into gidx, count
     int2* h_gbgrp = nullptr;        // pinned
-    double* d_fh = nullptr;         // ... k_cascade_gb's F FIFO, cascade_gb_scratch_doubles per batch
-    int fh_cap = 0;
-    int step_passes = 0;            // NUSI_OPT_STEP_PASSES: 1 = the step-pass cascade also where one pass fits
+    double* d_fh = nullptr;         // k_cascade_bs's F FIFO between step passes, cascade_bs_scratch_doubles per workgroup
+    int step_passes = 0;            // NUSI_OPT_STEP_PASSES: 1 = the step-pass instance of k_cascade_bs also where one pass fits
     int shift_max = 0;              // NUSI_OPT_SHIFT_REUSE: K, the largest bin offset served by a base table set
     int ref_order = 0;              // NUSI_OPT_REFERENCE_ORDER: 1 = the tables in the reference's operation order
-    int cascade_sync = 0;           // NUSI_OPT_CASCADE_SYNC: 0 = auto, 1 = per-stage kernels, 2 = block-synchronous
+    int cascade_sync = 0;           // NUSI_OPT_CASCADE_SYNC: 0 = auto, 2 = block-synchronous (the same kernel; 1 is refused)
     size_t fh_doubles = 0;          // capacity of d_fh in doubles (the block-synchronous kernels' FIFOs)
     nusi_plan* shift = nullptr;     // ... its plan: the same grid with K more redshift steps (axis T + K)
     int2* d_smap = nullptr;         // per shifted table: base index in `shift`, bin offset
@@ -764,8 +761,6 @@ void nusi_plan_destroy(nusi_plan* pl)
     hipFree(pl->d_tpts);
     if (pl->h_tpts) hipHostFree(pl->h_tpts);
     hipFree(pl->d_batches);
-    hipFree(pl->d_groups);
-    if (pl->h_groups) hipHostFree(pl->h_groups);
     if (pl->h_batches) hipHostFree(pl->h_batches);
     hipFree(pl->d_warn);
     hipFree(pl->tabs.G);
@@ -854,8 +849,6 @@ int nusi_plan_create(int device, int N_bins_E, double lEmin, double lEmax, doubl
     HIPCHECK(hipMalloc(&pl->d_tpts, sizeof(nusi::Point) * max_points));
     HIPCHECK(hipHostMalloc((void**)&pl->h_tpts, sizeof(nusi::Point) * max_points, hipHostMallocDefault));
     HIPCHECK(hipMalloc(&pl->d_batches, sizeof(int) * max_points));
-    HIPCHECK(hipMalloc(&pl->d_groups, sizeof(int2) * max_points));
-    HIPCHECK(hipHostMalloc((void**)&pl->h_groups, sizeof(int2) * max_points, hipHostMallocDefault));
     HIPCHECK(hipHostMalloc((void**)&pl->h_batches, sizeof(int) * max_points, hipHostMallocDefault));
     HIPCHECK(hipMalloc(&pl->d_warn, sizeof(int) * max_points));
     HIPCHECK(hipMalloc(&pl->tabs.G, sizeof(double) * (size_t)G.T * max_points));
@@ -999,32 +992,20 @@ int nusi_plan_evolve(nusi_plan* pl, const nusi_params* pts, int n, double* d_flu
         if (!d_flux) d_flux = pl->d_scratch;
         if (!d_fla) d_fla = pl->d_scratch + N3 * pl->max_points;
     }
-    // the cascade.  AUTO / MFMA: the warp-specialised MFMA kernels for every point kind, points sharing a table
-    // slot in pairs on the multi-RHS form (k_cascade_ws<R = 2>: one operator, two sources) when most points pair
-    // up; the step-pass kernel beyond 48 redshift steps.  WAVEFRONT / REG / LDS: the bit-exact scalar kernels.
+    // the cascade.  AUTO / MFMA: the block-synchronous MFMA cascade k_cascade_bs for every point kind -- the points of
+    // a table slot in workgroups of up to 16 (>= 3 points: the gamma batch), pairs, or one per workgroup
+    // (NUSI_OPT_CASCADE_RHS caps the group size; NUSI_OPT_STEP_PASSES = 1: one point per workgroup on the
+    // step-pass instance), any source and scattering mode, step passes on long grids.  WAVEFRONT / REG / LDS, and a
+    // grid k_cascade_bs does not fit: the bit-exact scalar cascade k_cascade.
     const int kind = pl->cascade_kind == NUSI_CASCADE_AUTO ? NUSI_CASCADE_MFMA : pl->cascade_kind;
-    bool all_pl = true, any_dsnb = false, all_nr = true;
+    bool any_dsnb = false, all_nr = true;
     for (int i = 0; i < n; ++i) {
-        all_pl = all_pl && pl->h_pts[i].source == NUSI_SOURCE_POWER_LAW;
         any_dsnb = any_dsnb || pl->h_pts[i].source == NUSI_SOURCE_DSNB;
         all_nr = all_nr && pl->h_pts[i].non_resonant;
     }
-    const bool one_pass = nusi::cascade_ws_fits(pl->gd, 1) && pl->step_passes != 1;
-    const bool fast = kind == NUSI_CASCADE_MFMA && (one_pass || nusi::cascade_wsp_fits(pl->gd));
-    const bool pairs_fit = fast && one_pass && nusi::cascade_ws_fits(pl->gd, 2);
-    // the gamma batch (k_cascade_gb; NUSI_OPT_CASCADE_RHS 0 = auto = 16, or 3..16): the power-law points of a table
-    // slot -- C5's 16 gamma of one (m_phi, g) -- when there are at least 3, up to 16 per workgroup, gamma on the
-    // MFMA N dimension; the other points take the pair / one-point kernels below
+    const bool force_passes = pl->step_passes == 1;
+    const bool bs = kind == NUSI_CASCADE_MFMA && nusi::cascade_bs_config(pl->gd, 1, force_passes) != 0;
     int ngb = 0, ngidx = 0;
-    std::vector<char> in_gb;
-    const int gbmax = pl->cascade_rhs == 0 ? 16 : pl->cascade_rhs;   // auto: the gamma batch (C5 cascade 4.54 -> 4.13 ms)
-    // the block-synchronous MFMA cascade (k_cascade_bs; NUSI_OPT_CASCADE_SYNC): the points of a table slot in
-    // workgroups of up to 16 (>= 3 points: the gamma batch), pairs, or one per workgroup (NUSI_OPT_CASCADE_RHS caps
-    // the group size), any source and scattering mode, step passes on long grids.  The default (sync 0) unless step
-    // passes are forced: against the per-stage kernels C4 0.70 -> 0.56 ms, C5 4.13 -> 3.66, C3 37.3 -> 30.7
-    // (profiles/r4)
-    const bool bs_auto = pl->cascade_sync == 0 && pl->step_passes != 1;
-    const bool bs = kind == NUSI_CASCADE_MFMA && (pl->cascade_sync == 2 || bs_auto) && nusi::cascade_bs_config(pl->gd, 1) != 0;
     int bs_nwg[3] = {0, 0, 0};   // workgroups of P = 16, 2, 1 (their groups in h_gbgrp in that order)
     if (bs) {
         if (!pl->d_gidx) {
@@ -1033,9 +1014,9 @@ int nusi_plan_evolve(nusi_plan* pl, const nusi_params* pts, int n, double* d_flu
             HIPCHECK(hipHostMalloc((void**)&pl->h_gidx, sizeof(int) * pl->max_points, hipHostMallocDefault));
             HIPCHECK(hipHostMalloc((void**)&pl->h_gbgrp, sizeof(int2) * pl->max_points, hipHostMallocDefault));
         }
-        const int rmax = pl->cascade_rhs == 0 ? 16 : pl->cascade_rhs;
-        const bool g16 = rmax >= 3 && nusi::cascade_bs_config(pl->gd, 16) != 0;
-        const bool g2 = rmax >= 2 && nusi::cascade_bs_config(pl->gd, 2) != 0;
+        const int rmax = force_passes ? 1 : pl->cascade_rhs == 0 ? 16 : pl->cascade_rhs;
+        const bool g16 = rmax >= 3 && nusi::cascade_bs_config(pl->gd, 16, false) != 0;
+        const bool g2 = rmax >= 2 && nusi::cascade_bs_config(pl->gd, 2, false) != 0;
         std::vector<std::vector<int>> by(ntab);
         for (int i = 0; i < n; ++i) by[pl->h_pts[i].tslot].push_back(i);
         std::vector<std::vector<int>> grs[3];   // groups for P = 16, 2, 1
@@ -1062,61 +1043,12 @@ int nusi_plan_evolve(nusi_plan* pl, const nusi_params* pts, int n, double* d_flu
         if (fhd > pl->fh_doubles) {
             hipFree(pl->d_fh);
             pl->d_fh = nullptr;
-            pl->fh_cap = 0;
             pl->fh_doubles = 0;
             HIPCHECK(hipMalloc(&pl->d_fh, sizeof(double) * fhd));
             pl->fh_doubles = fhd;
         }
     }
-    if (!bs && pairs_fit && gbmax >= 3 && nusi::cascade_gb_fits(pl->gd)) {
-        if (!pl->d_gidx) {
-            HIPCHECK(hipMalloc(&pl->d_gidx, sizeof(int) * pl->max_points));
-            HIPCHECK(hipMalloc(&pl->d_gbgrp, sizeof(int2) * pl->max_points));
-            HIPCHECK(hipHostMalloc((void**)&pl->h_gidx, sizeof(int) * pl->max_points, hipHostMallocDefault));
-            HIPCHECK(hipHostMalloc((void**)&pl->h_gbgrp, sizeof(int2) * pl->max_points, hipHostMallocDefault));
-        }
-        std::vector<std::vector<int>> by(ntab);
-        for (int i = 0; i < n; ++i)
-            if (pl->h_pts[i].source == NUSI_SOURCE_POWER_LAW) by[pl->h_pts[i].tslot].push_back(i);
-        in_gb.assign(n, 0);
-        for (int j = 0; j < ntab; ++j) {
-            const int c = (int)by[j].size();
-            if (c < 3) continue;
-            const int nb = (c + gbmax - 1) / gbmax;   // near-equal batches
-            for (int k = 0; k < nb; ++k) {
-                const int lo = (int)((long long)c * k / nb), hi = (int)((long long)c * (k + 1) / nb);
-                pl->h_gbgrp[ngb++] = make_int2(ngidx, hi - lo);
-                for (int q = lo; q < hi; ++q) {
-                    pl->h_gidx[ngidx++] = by[j][q];
-                    in_gb[by[j][q]] = 1;
-                }
-            }
-        }
-        if (ngb > pl->fh_cap) {
-            hipFree(pl->d_fh);
-            pl->d_fh = nullptr;
-            pl->fh_cap = 0;
-            pl->fh_doubles = 0;
-            HIPCHECK(hipMalloc(&pl->d_fh, sizeof(double) * nusi::cascade_gb_scratch_doubles(pl->gd) * ngb));
-            pl->fh_cap = ngb;
-            pl->fh_doubles = nusi::cascade_gb_scratch_doubles(pl->gd) * ngb;
-        }
-    }
-    int ngroups = 0;
-    if (!bs && pairs_fit && (pl->cascade_rhs != 1 || ngb)) {
-        std::vector<int> open(ntab, -1);   // per table slot: a point waiting for its partner
-        for (int i = 0; i < n; ++i) {
-            if (ngb && in_gb[i]) continue;
-            int& o = open[pl->h_pts[i].tslot];
-            if (pl->cascade_rhs == 1) pl->h_groups[ngroups++] = make_int2(i, -1);
-            else if (o < 0) o = i;
-            else { pl->h_groups[ngroups++] = make_int2(o, i); o = -1; }
-        }
-        for (int j = 0; j < ntab; ++j)
-            if (open[j] >= 0) pl->h_groups[ngroups++] = make_int2(open[j], -1);
-        if (!ngb && 4 * ngroups > 3 * n) ngroups = 0;   // too few pairs: one point per workgroup
-    }
-    if ((fast || bs) && any_dsnb && pl->src_cap < pl->max_points) {
+    if (bs && any_dsnb && pl->src_cap < pl->max_points) {
         hipFree(pl->d_src);
         pl->d_src = nullptr;
         pl->src_cap = 0;
@@ -1124,7 +1056,6 @@ int nusi_plan_evolve(nusi_plan* pl, const nusi_params* pts, int n, double* d_flu
         pl->src_cap = pl->max_points;
         pl->tabs.Src = pl->d_src;
     }
-    if (ngroups) HIPCHECK(hipMemcpyAsync(pl->d_groups, pl->h_groups, sizeof(int2) * ngroups, hipMemcpyHostToDevice, s));
     if (ngb) {
         HIPCHECK(hipMemcpyAsync(pl->d_gidx, pl->h_gidx, sizeof(int) * ngidx, hipMemcpyHostToDevice, s));
         HIPCHECK(hipMemcpyAsync(pl->d_gbgrp, pl->h_gbgrp, sizeof(int2) * ngb, hipMemcpyHostToDevice, s));
@@ -1163,7 +1094,7 @@ int nusi_plan_evolve(nusi_plan* pl, const nusi_params* pts, int n, double* d_flu
         HIPCHECK(nusi::launch_table_shift(pl->gd, sp->gd, pl->d_smap, nd, ntab - nd, sp->tabs, pl->tabs, pl->d_warn, s));
     }
     HIPCHECK(hipEventRecord(ev[2], s));
-    if ((fast || bs) && any_dsnb) HIPCHECK(nusi::launch_source_dsnb(pl->gd, pl->d_pts, n, pl->d_src, s));
+    if (bs && any_dsnb) HIPCHECK(nusi::launch_source_dsnb(pl->gd, pl->d_pts, n, pl->d_src, s));
     const char* gb_name = nullptr;
     if (bs) {
         const int Pk[3] = {16, 2, 1};
@@ -1175,7 +1106,7 @@ int nusi_plan_evolve(nusi_plan* pl, const nusi_params* pts, int n, double* d_flu
         for (int w = 0; w < 3; ++w) {
             if (bs_nwg[w]) {
                 HIPCHECK(nusi::launch_cascade_bs(pl->gd, pl->d_pts, Pk[w], pl->d_gidx, pl->d_gbgrp + off, bs_nwg[w], pl->tabs,
-                                                 fh, d_flux, d_fla, s, all_nr));
+                                                 fh, d_flux, d_fla, s, all_nr, force_passes));
                 mask |= 1 << w;
             }
             fh += nusi::cascade_bs_scratch_doubles(pl->gd, Pk[w]) * bs_nwg[w];
@@ -1183,21 +1114,7 @@ int nusi_plan_evolve(nusi_plan* pl, const nusi_params* pts, int n, double* d_flu
         }
         gb_name = names[mask];
     } else {
-        if (ngb) {
-            HIPCHECK(nusi::launch_cascade_gb(pl->gd, pl->d_pts, pl->d_gidx, pl->d_gbgrp, ngb, pl->tabs, pl->d_fh, d_flux,
-                                             d_fla, s));
-            gb_name = ngroups ? "k_cascade_gb + k_cascade_ws_mrhs" : "k_cascade_gb";
-        }
-        if (fast && ngroups)
-            HIPCHECK(nusi::launch_cascade_ws(pl->gd, pl->d_pts, 2, pl->d_groups, ngroups, pl->tabs, d_flux, d_fla, s));
-        else if (ngb) {
-        } else if (fast && one_pass)
-            HIPCHECK(nusi::launch_cascade_ws(pl->gd, pl->d_pts, 1, nullptr, n, pl->tabs, d_flux, d_fla, s));
-        else if (fast)
-            HIPCHECK(nusi::launch_cascade_wsp(pl->gd, pl->d_pts, n, pl->tabs, d_flux, d_fla, s, all_nr));
-        else
-            HIPCHECK(nusi::launch_cascade_exact(pl->gd, pl->d_pts, n, pl->tabs, d_flux, d_fla, s,
-                                                kind == NUSI_CASCADE_MFMA ? NUSI_CASCADE_WAVEFRONT : kind, all_pl));
+        HIPCHECK(nusi::launch_cascade_exact(pl->gd, pl->d_pts, n, pl->tabs, d_flux, d_fla, s));
     }
     HIPCHECK(hipEventRecord(ev[3], s));
     HIPCHECK(hipEventRecord(pl->ev_done, s));
@@ -1286,6 +1203,8 @@ int nusi_plan_set_option(nusi_plan* pl, int option, int value)
         return NUSI_OK;
     case NUSI_OPT_CASCADE_SYNC:
         if (value < 0 || value > 2) return fail(NUSI_EPARAM, "NUSI_OPT_CASCADE_SYNC outside [0, 2]");
+        if (value == 1)   // the per-stage kernels (k_cascade_ws / gb / wsp) were removed in round 5
+            return fail(NUSI_EPARAM, "NUSI_OPT_CASCADE_SYNC = 1: the per-stage cascade kernels are gone; k_cascade_bs is the MFMA cascade");
         pl->cascade_sync = value;
         return NUSI_OK;
     case NUSI_OPT_REFERENCE_ORDER:

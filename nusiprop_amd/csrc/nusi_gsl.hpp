@@ -21,13 +21,16 @@
 //   * GSL stops a series when fabs(a / b) < 2^-p (p = 52, 53 or 104).  For a, b >= 0 and b 2^-p a normal number,
 //     RN(a / b) < 2^-p  <=>  a < b 2^-p: the doubles below 2^-p b are those at or below its predecessor, which
 //     lies below the rounding boundary 2^-p b (1 - 2^-54).  So the test is one multiply and one compare
-//     (quot_lt; the division where b < 2^-900);
+//     (quot_lt);
 //   * the series' term a / d_k with d_k = k^2 or k^2 (k + 1) (exact integers) is RN(a / d_k) from the table value
 //     y_k = RN(1 / d_k) by two residual corrections, q0 = a y_k, q_{i+1} = q_i + (a - d_k q_i) y_k (fma): the first
 //     makes the quotient faithful, the second correctly rounded (Markstein's theorem: y correctly rounded, q
 //     faithful, remainder exact by fma); 6e8 random a over 1800 binades and every d_k agree bit for bit with the
-//     division (tests/test_specfun.py runs the device functions against the oracle's divisions).  Subnormal
-//     ranges (a < 2^-960) take the division.  GSL's (k - 1)/k squared of series_1 is a table of the same values.
+//     division (tests/test_specfun.py runs the device functions against the oracle's divisions).  GSL's (k - 1)/k
+//     squared of series_1 is a table of the same values;
+//   * both rewrites need their operands in the normal range; a series whose argument is below 2^-400 (which the
+//     tables never meet) runs a second instance of its loop with GSL's divisions (kExact), so the loops have no
+//     per-iteration branch.
 #pragma once
 
 #include "nusi_libm.hpp"
@@ -39,20 +42,23 @@ constexpr double kEps = 2.2204460492503131e-16;       // GSL_DBL_EPSILON
 constexpr double kSqrtEps = 1.4901161193847656e-08;   // GSL_SQRT_DBL_EPSILON
 constexpr double kPiD = 3.14159265358979323846;       // M_PI
 
-// per-k constants of the series: d1 = k^2, d2 = k^2 (k + 1) and their rounded reciprocals; rr = ((k - 1) / k)^2
-// as series_1 forms it (every value is the compiler's IEEE evaluation of GSL's own expression)
+// per-k constants of the series: d1 = k^2 and d2 = k^2 (k + 1) (exact) with their rounded reciprocals, side by side
+// (one 32-byte scalar load per iteration, k being uniform), and rr = ((k - 1) / k)^2 as series_1 forms it (every
+// value the compiler's IEEE evaluation of GSL's expression)
 constexpr int kKTab = 1000;
+struct KRow { double d1, d2, y1, y2; };
 struct KTab {
-    double d1[kKTab], y1[kKTab], d2[kKTab], y2[kKTab], rr[kKTab];
+    KRow row[kKTab];
+    double rr[kKTab];
 };
 constexpr KTab make_ktab()
 {
     KTab t{};
     for (int k = 1; k < kKTab; ++k) {
-        t.d1[k] = (double)k * k;
-        t.y1[k] = 1.0 / t.d1[k];
-        t.d2[k] = (double)k * k * (k + 1.0);
-        t.y2[k] = 1.0 / t.d2[k];
+        t.row[k].d1 = (double)k * k;
+        t.row[k].d2 = (double)k * k * (k + 1.0);
+        t.row[k].y1 = 1.0 / t.row[k].d1;
+        t.row[k].y2 = 1.0 / t.row[k].d2;
         const double rk = (k - 1.0) / k;
         t.rr[k] = rk * rk;
     }
@@ -60,20 +66,25 @@ constexpr KTab make_ktab()
 }
 constexpr KTab kKT = make_ktab();
 
-// RN(a / d) from y = RN(1 / d), a > 0 (header comment)
+// RN(a / d) for the series' terms.  kExact: the division; else from y = RN(1 / d) by two residual corrections
+// (header comment), valid for a, d > 0 with a >= 2^-960 -- the callers take kExact for arguments that could reach
+// below (a series argument under 2^-400, never met in the tables)
+template <bool kExact>
 NUSI_FN double div_k(double a, double d, double y)
 {
-    if (!(a >= 0x1p-960)) return a / d;
+    if (kExact) return a / d;
     const double q0 = a * y;
     const double q1 = fma(fma(-q0, d, a), y, q0);
     return fma(fma(-q1, d, a), y, q1);
 }
 
-// fabs(a / b) < c of GSL's stopping tests for a, b >= 0 and c a power of two (header comment)
+// fabs(a / b) < c of GSL's stopping tests for a, b >= 0 and c a power of two: kExact the division, else a < b c
+// (header comment; exact for b c a normal number, b >= 2^-900 -- the callers' kExact covers the rest)
+template <bool kExact>
 NUSI_FN bool quot_lt(double a, double b, double c)
 {
-    if (b >= 0x1p-900) return a < b * c;
-    return a / b < c;
+    if (kExact) return a / b < c;
+    return a < b * c;
 }
 
 // hypot(x, y) (libm; dilogc_unitdisk): sqrt(a^2 + b^2) and one correction step from the exact residual
@@ -96,34 +107,45 @@ NUSI_FN double hypot(double x, double y)
 
 // ------------------------------------------------------------------------------------------------- real --
 // dilog_series_1: sum x^k / k^2, 0 < x <= 1/4
-NUSI_FN double dilog_series_1(double x)
+template <bool kExact>
+NUSI_FN double dilog_series_1_t(double x)
 {
     double sum = x, term = x;
     for (int k = 2; k < 1000; k++) {
         term *= x;
         term *= kKT.rr[k];   // rk * rk, rk = (k - 1.0) / k
         sum += term;
-        if (quot_lt(fabs(term), fabs(sum), 0x1p-52)) break;   // fabs(term / sum) < GSL_DBL_EPSILON
+        if (quot_lt<kExact>(fabs(term), fabs(sum), 0x1p-52)) break;   // fabs(term / sum) < GSL_DBL_EPSILON
     }
     return sum;
 }
-// dilog_series_2: Li2(x) = 1 + (1 - x) log(1 - x) / x + series_2(x), series_2 = sum r^k / (k^2 (k + 1)) with the
-// first nine terms unconditionally
-NUSI_FN double dilog_series_2(double x)
+NUSI_FN double dilog_series_1(double x)
+{
+    return x < 0x1p-400 ? dilog_series_1_t<true>(x) : dilog_series_1_t<false>(x);
+}
+// series_2: sum r^k / (k^2 (k + 1)) with the first nine terms unconditionally (d2 = k * k * (k + 1.0), exact)
+template <bool kExact>
+NUSI_FN double series_2_t(double x)
 {
     double rk = x, sum = 0.5 * x;
     int k;
 #pragma unroll
     for (k = 2; k < 10; k++) {
         rk *= x;
-        sum += div_k(rk, kKT.d2[k], kKT.y2[k]);
+        sum += div_k<kExact>(rk, kKT.row[k].d2, kKT.row[k].y2);
     }
     for (; k < 100; k++) {
         rk *= x;
-        const double ds = div_k(rk, kKT.d2[k], kKT.y2[k]);
+        const double ds = div_k<kExact>(rk, kKT.row[k].d2, kKT.row[k].y2);
         sum += ds;
-        if (quot_lt(fabs(ds), fabs(sum), 0x1p-53)) break;   // fabs(ds / sum) < 0.5 GSL_DBL_EPSILON
+        if (quot_lt<kExact>(fabs(ds), fabs(sum), 0x1p-53)) break;   // fabs(ds / sum) < 0.5 GSL_DBL_EPSILON
     }
+    return sum;
+}
+// dilog_series_2: Li2(x) = 1 + (1 - x) log(1 - x) / x + series_2(x)
+NUSI_FN double dilog_series_2(double x)
+{
+    double sum = x < 0x1p-100 ? series_2_t<true>(x) : series_2_t<false>(x);   // (x^9 stays above 2^-900)
     double t;
     if (x > 0.01) t = (1.0 - x) * nm::log(1.0 - x) / x;
     else {
@@ -220,7 +242,8 @@ NUSI_FN_OUT double clausen(double x)
 // dilogc_series_1 (s2 = false: sum r^k e^(i k theta) / k^2, first term r e^(i theta), kmax 50 + 22 / (-log r))
 // and series_2_c (s2 = true: sum z^k / (k^2 (k + 1)), first term r e^(i theta) / 2, kmax 30 + 18 / (-log r)) as
 // one loop; every operation is GSL's
-NUSI_FN void cseries(bool s2, double r, double x, double y, double& re, double& im)
+template <bool kExact>
+NUSI_FN void cseries_t(bool s2, double r, double x, double y, double& re, double& im)
 {
     const double cos_theta = x / r, sin_theta = y / r;
     const double alpha = 1.0 - cos_theta, beta = sin_theta;
@@ -229,19 +252,31 @@ NUSI_FN void cseries(bool s2, double r, double x, double y, double& re, double& 
     double imag_sum = s2 ? 0.5 * r * sk : r * sk;
     const double nlr = -nm::log(r);
     const int kmax = s2 ? 30 + (int)(18.0 / nlr) : 50 + (int)(22.0 / nlr);
+    KRow next = kKT.row[2];   // (the table row of the next iteration is loaded one iteration ahead; kmax <= 921)
     for (int k = 2; k < kmax; k++) {
+        const KRow kr = next;
+        next = kKT.row[k + 1];
         const double ck_tmp = ck;
         ck = ck - (alpha * ck + beta * sk);
         sk = sk - (alpha * sk - beta * ck_tmp);
         rk *= r;
-        const double q = s2 ? div_k(rk, kKT.d2[k], kKT.y2[k]) : div_k(rk, kKT.d1[k], kKT.y1[k]);
+        const double d = s2 ? kr.d2 : kr.d1;   // (double) k * k * (k + 1.0) or (double) k * k
+        const double yk = s2 ? kr.y2 : kr.y1;
+        const double q = div_k<kExact>(rk, d, yk);
         const double dr = q * ck, di = q * sk;
         real_sum += dr;
         imag_sum += di;
-        if (quot_lt(dr * dr + di * di, real_sum * real_sum + imag_sum * imag_sum, 0x1p-104)) break;
+        if (quot_lt<kExact>(dr * dr + di * di, real_sum * real_sum + imag_sum * imag_sum, 0x1p-104)) break;
     }
     re = real_sum;
     im = imag_sum;
+}
+// (the terms r^k stay above 2^-960 and |sum|^2 above 2^-900 unless r < 2^-400: the series breaks at a term
+// below 2^-52 of the sum, and kmax bounds r^k for larger r)
+NUSI_FN void cseries(bool s2, double r, double x, double y, double& re, double& im)
+{
+    if (r < 0x1p-400) cseries_t<true>(s2, r, x, y, re, im);
+    else cseries_t<false>(s2, r, x, y, re, im);
 }
 // dilogc_series_3: |z| near 1, sum_{n <= 6} (log r)^n / n! H_n(theta)
 NUSI_FN void cseries_3(double r, double x, double y, double& re, double& im)

@@ -68,42 +68,27 @@ hipError_t launch_alpha(const GridDev& g, const Point* pts, int npts, const Spli
 // (tb.Wmin, required)
 hipError_t launch_table_shift(const GridDev& g, const GridDev& gb, const int2* map, int s0, int nshift, TablesDev tb,
                               TablesDev t, int* warn, hipStream_t s);
-// The MFMA cascade (NUSI_CASCADE_AUTO / MFMA): k_cascade_ws -- R = 1, one point per workgroup (groups
-// unused, nwg = points), or R = 2, groups[k] = two points sharing one table slot (y < 0: one point) -- for
-// Nz - 1 <= 48, k_cascade_wsp (step passes) for any number of steps.  Every point kind: the DSNB points'
-// source terms come from t.Src (launch_source_dsnb first), the power law is evaluated in the kernel.
-bool cascade_ws_fits(const GridDev& g, int R);
-bool cascade_wsp_fits(const GridDev& g);   // the step-pass kernel (any number of redshift steps)
-hipError_t launch_cascade_ws(const GridDev& g, const Point* pts, int R, const int2* groups, int nwg, TablesDev t,
-                             double* flux, double* flux_fla, hipStream_t s);
-hipError_t launch_cascade_wsp(const GridDev& g, const Point* pts, int npts, TablesDev t, double* flux, double* flux_fla,
-                              hipStream_t s, bool all_nonres);   // all_nonres: every point non-resonant
-// The gamma batch (k_cascade_gb): workgroup k takes the grp[k].y <= 16 power-law points gidx[grp[k].x ..] that share one
-// table slot, gamma on the MFMA N dimension, the redshift steps in passes of 6; fh: a scratch FIFO of
-// cascade_gb_scratch_doubles per workgroup
-bool cascade_gb_fits(const GridDev& g);
-size_t cascade_gb_scratch_doubles(const GridDev& g);
-hipError_t launch_cascade_gb(const GridDev& g, const Point* pts, const int* gidx, const int2* grp, int nwg, TablesDev t,
-                             double* fh, double* flux, double* flux_fla, hipStream_t s);
 // The block-synchronous MFMA cascade (k_cascade_bs, round 4): workgroup k takes the grp[k].y <= P points gidx[grp[k].x
 // ..] that share one table slot (gidx == grp == nullptr: P = 1, point k), P = 1, 2 or 16 (the gamma batch), any source
 // and scattering mode, step passes on any grid that fits; fh: a FIFO of cascade_bs_scratch_doubles per workgroup
 // (used when the steps take more than one pass).  cascade_bs_config: 0 = the grid does not fit P.
-int cascade_bs_config(const GridDev& g, int P);
+// force_passes (NUSI_OPT_STEP_PASSES = 1, P = 1): the step-pass instance even where one pass fits.
+int cascade_bs_config(const GridDev& g, int P, bool force_passes);
 size_t cascade_bs_scratch_doubles(const GridDev& g, int P);
 hipError_t launch_cascade_bs(const GridDev& g, const Point* pts, int P, const int* gidx, const int2* grp, int nwg,
-                             TablesDev t, double* fh, double* flux, double* flux_fla, hipStream_t s, bool all_nr);
+                             TablesDev t, double* fh, double* flux, double* flux_fla, hipStream_t s, bool all_nr,
+                             bool force_passes);
 size_t cascade_src_doubles(const GridDev& g);   // t.Src doubles per point
 hipError_t launch_source_dsnb(const GridDev& g, const Point* pts, int npts, double* src, hipStream_t s);
-// The bit-exact scalar cascades (NUSI_CASCADE_WAVEFRONT / REG / LDS; a kind that does not fit the grid falls
-// back wavefront -> register-resident -> LDS).  all_power_law selects the call-free wavefront variant.
+// The bit-exact scalar cascade k_cascade (NUSI_CASCADE_WAVEFRONT / REG / LDS all select it): one wavefront per
+// point, any N.
 hipError_t launch_cascade_exact(const GridDev& g, const Point* pts, int npts, TablesDev t, double* flux,
-                                double* flux_fla, hipStream_t s, int kind, bool all_power_law);
+                                double* flux_fla, hipStream_t s);
 
 // 4 x 4 windows of a 3-D spline table f [n0][n1][n2] into fw [n0 n1 n2][16] (synchronous)
 hipError_t spline_windows_build(const float* f, int n0, int n1, int n2, float* fw);
 
-// names of the main alpha-table / cascade kernels the latest launch_alpha / launch_cascade(_ws) on this
+// names of the main alpha-table / cascade kernels the latest launch_alpha / launch_cascade_* on this
 // thread chose (static strings; nusi_plan_kernels)
 const char* last_alpha_kernel();
 const char* last_cascade_kernel();

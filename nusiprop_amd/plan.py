@@ -83,9 +83,8 @@ class Plan:
 
     def set_cascade(self, kind):
         """Cascade kernel of later calls: _lib.CASCADE_AUTO (default) = CASCADE_MFMA (the wavefront with its push
-        on the fp64 matrix cores: the block-synchronous k_cascade_bs, or with OPT_CASCADE_SYNC = 1 the per-stage
-        k_cascade_ws / gb / wsp), or the bit-exact scalar kernels CASCADE_{WAVEFRONT,REG,LDS} (WAVEFRONT and REG
-        agree bit for bit)."""
+        on the fp64 matrix cores, the block-synchronous k_cascade_bs), or CASCADE_{WAVEFRONT,REG,LDS} (since
+        round 5 all three the bit-exact scalar kernel k_cascade)."""
         _lib.check(_lib.load().nusi_plan_set_cascade(self._h, int(kind)))
 
     def set_option(self, option, value):
@@ -118,7 +117,7 @@ class Plan:
         return list(out)
 
     def kernels(self):
-        """(alpha-table kernel, cascade kernel) the last call launched, e.g. ('k_alpha_batch', 'k_cascade_ws')."""
+        """(alpha-table kernel, cascade kernel) the last call launched, e.g. ('k_alpha_batch', 'k_cascade_bs')."""
         a, c = ctypes.c_char_p(), ctypes.c_char_p()
         _lib.check(_lib.load().nusi_plan_kernels(self._h, ctypes.byref(a), ctypes.byref(c)))
         return a.value.decode(), c.value.decode()

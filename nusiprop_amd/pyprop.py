@@ -111,7 +111,7 @@ class pyprop:  # noqa: N801  (name of the reference class)
 
     def kernels(self):
         """Extension (no reference counterpart): names of the alpha-table and cascade kernels the last
-        evolve() launched, e.g. ('k_alpha_batch', 'k_cascade_ws')."""
+        evolve() launched, e.g. ('k_alpha_batch', 'k_cascade_bs')."""
         a, c = ctypes.c_char_p(), ctypes.c_char_p()
         _lib.check(_lib.load().nusi_get_kernels(self._h, ctypes.byref(a), ctypes.byref(c)))
         return a.value.decode(), c.value.decode()

@@ -101,7 +101,7 @@ def cascade_bytes_per_point(N, Nz):
     return 8 * ((Nz - 1) * N * (N - 1) // 2 + 6 * N * (Nz - 1) + Nz * N)
 
 
-WSP_NJ, WSP_RT = 16, 8   # the step-pass cascade (k_cascade_wsp): step slots per pass, 16-row tiles per push wave
+WSP_NJ, WSP_RT = 16, 8   # the step-pass instance k_cascade_bs<16, 1, 1, 8, 1>: step slots per pass, 16-row tiles per push wave
 
 
 def cascade_passes(N, Nz, nj=None):
@@ -112,7 +112,7 @@ def cascade_passes(N, Nz, nj=None):
     return [(jb, N - 1 + min(nj, nst - jb), T - 1 - jb) for jb in range(0, nst, nj)]
 
 
-GB_NJ, GB_RT = 6, 2   # the gamma batch (k_cascade_gb): steps per pass, 16-row tiles per push wave
+GB_NJ, GB_RT = 6, 2   # the gamma batch k_cascade_bs<6, 16, 1, 2, 2>: steps per pass, 16-row tiles per push wave
 
 
 def gamma_batches(points, rhs=16):
@@ -182,10 +182,10 @@ def cascade_min_bytes_per_point(N, Nz, passes=False):
 
 
 def cascade_mfma_flops_per_point(N, Nz):
-    """fp64 matrix-core flops the MFMA-push cascade (k_cascade_wf_mfma) issues per propagation: block q
+    """fp64 matrix-core flops the MFMA-push cascade (k_cascade_bs, one point per workgroup) issues per propagation: block q
     (stage 4q, q >= 1) runs one v_mfma_f64_16x16x4f64 (2*16*16*4 flops) per 16-row tile starting below
     r = T-1-4q, per 16-step tile (NJ/16 of them, NJ = Nz-1 rounded up to 16/32/48).  Grids with more
-    steps run the step-pass kernel (k_cascade_wsp): the same count per pass, one step tile."""
+    steps run the step-pass instance: the same count per pass, one step tile."""
     T, n = N + Nz - 2, Nz - 1
     NJ = 16 if n <= 16 else 32 if n <= 32 else 48 if n <= 48 else 0
     waves = (T - 1 + 63) // 64
