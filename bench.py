@@ -62,18 +62,15 @@ def parse():
                          "process, a few steps, after the timed region)")
     ap.add_argument("--cascade", default="auto", choices=["auto", "mfma", "wf"],
                     help="cascade kernel: auto = the library default (= mfma: the wavefront with the push on the fp64 "
-                         "matrix cores, block-synchronous k_cascade_bs), wf = the bit-exact scalar wavefront")
+                         "matrix cores, block-synchronous k_cascade_bs), wf = the bit-exact scalar cascade k_cascade")
     ap.add_argument("--rhs", type=int, default=0,
                     help="NUSI_OPT_CASCADE_RHS: 0 = the library default, 1 = one point per cascade workgroup, 2 = pairs "
-                         "of points sharing a table, 3..16 = the gamma batch (k_cascade_bs_gamma; k_cascade_gb with --sync stage)")
+                         "of points sharing a table, 3..16 = the gamma batch (k_cascade_bs_gamma)")
     ap.add_argument("--reference-order", action="store_true",
                     help="NUSI_OPT_REFERENCE_ORDER: the tables in the reference's own operation order for the complex "
                          "dilogarithms (bit-exact to the oracle's reference-order mode); default: the shared-algorithm "
                          "order (bit-exact to the oracle's default mode)")
     ap.add_argument("--no-parity", action="store_true", help="skip the parity object (oracle fluxes of a sample)")
-    ap.add_argument("--sync", default="auto", choices=["auto", "stage", "block"],
-                    help="NUSI_OPT_CASCADE_SYNC: the MFMA cascade's per-stage kernels (stage) or the block-synchronous "
-                         "k_cascade_bs (block); auto = the library default (block)")
     ap.add_argument("--dry-run", action="store_true",
                     help="launch / rank / reduction plumbing only, no GPU work (gloo; CPU tests): prints the JSON "
                          "line with value null")
@@ -540,8 +537,6 @@ def run(args, world, rank, local, dist, plan, pts, desc, pp_tables):
         plan.set_option(_lib.OPT_CASCADE_RHS, args.rhs)
     if args.reference_order:
         plan.set_option(_lib.OPT_REFERENCE_ORDER, 1)
-    if args.sync != "auto":
-        plan.set_option(_lib.OPT_CASCADE_SYNC, {"stage": 1, "block": 2}[args.sync])
     order = "reference" if args.reference_order else "shared-algorithm"
     dev = torch.device("cuda", local)
     flux = torch.empty((P, 3, plan.N), dtype=torch.float64, device=dev)
@@ -600,8 +595,8 @@ def run(args, world, rank, local, dist, plan, pts, desc, pp_tables):
     achieved = casc_bytes / casc_s / 1e9
     # workgroups that read a table, and the bytes / matrix-core flops they must move / issue
     readers = P
-    long_grid = Nz - 1 > 48   # step passes (k_cascade_ws_passes, or k_cascade_bs beyond one pass)
-    passes = casc_kernel == "k_cascade_ws_passes" or ("k_cascade_bs" in casc_kernel and long_grid)
+    long_grid = Nz - 1 > 48   # step passes (k_cascade_bs beyond one pass)
+    passes = "k_cascade_bs" in casc_kernel and long_grid
     casc_min = scan.cascade_min_bytes_per_point(N, Nz, passes=passes) * readers
     casc_mf = scan.cascade_mfma_flops_per_point(N, Nz) * P
     gbs = []
@@ -620,15 +615,6 @@ def run(args, world, rank, local, dist, plan, pts, desc, pp_tables):
                        for g in grp)
         casc_mf = sum(scan.cascade_gb_flops_per_batch(N, Nz) if g >= 3 else g * scan.cascade_mfma_flops_per_point(N, Nz)
                       for g in grp)
-    elif casc_kernel in ("k_cascade_ws_mrhs",):
-        from collections import Counter
-        readers = sum((c + 1) // 2 for c in Counter(scan.table_key(p) for p in pts).values())
-        casc_min = scan.cascade_min_bytes_per_point(N, Nz, passes=passes) * readers
-    elif "k_cascade_gb" in casc_kernel:
-        gbs = scan.gamma_batches(pts, args.rhs or 16)
-        readers = len(gbs)
-        casc_min = scan.cascade_gb_bytes_per_batch(N, Nz) * len(gbs) + 8 * 6 * N * P
-        casc_mf = scan.cascade_gb_flops_per_batch(N, Nz) * len(gbs)
     step_ms = sum(sum_ms) / max(ncalls, 1)
     out = {
         "metric": METRIC,

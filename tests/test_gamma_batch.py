@@ -1,10 +1,10 @@
-"""The gamma batch k_cascade_gb (NUSI_OPT_CASCADE_RHS 3..16; SURVEY sec. 7 K_B', the north star's transfer-matrix x
-flux-batch GEMM at full batch width) against the oracle and against the one-point cascade.
+"""The gamma batch k_cascade_bs_gamma (NUSI_OPT_CASCADE_RHS 3..16; SURVEY sec. 7 K_B', the north star's
+transfer-matrix x flux-batch GEMM at full batch width) against the oracle and against the one-point cascade.
 
-The power-law points of one table slot (same m_phi, g, masses, flags: the gamma of a C5 block) share one triangular
-operator; k_cascade_gb runs up to 16 of them per workgroup with gamma on the N dimension of the fp64 MFMA and the
-redshift steps in passes of 6.  Its operations per point are k_cascade_ws's, summed in blocks by the matrix core,
-so the fluxes agree with the oracle to FLUX_RTOL with the same exact zeros.
+The points of one table slot (same m_phi, g, masses, flags: the gamma of a C5 block) share one triangular operator;
+k_cascade_bs_gamma runs up to 16 of them per workgroup with gamma on the N dimension of the fp64 MFMA and the
+redshift steps in passes of 6.  Its operations per point are the one-point kernel's, summed in blocks by the matrix
+core, so the fluxes agree with the oracle to FLUX_RTOL with the same exact zeros.
 """
 import numpy as np
 import pytest
@@ -26,7 +26,6 @@ def _run(nusi, pts, rhs):
     p0 = pts[0]
     plan = nusi.Plan(p0["N_bins_E"], p0["lEmin"], p0["lEmax"], p0["zmax"], max_points=len(pts))
     plan.set_option(_lib.OPT_CASCADE_RHS, rhs)
-    plan.set_option(_lib.OPT_CASCADE_SYNC, 1)   # the per-stage kernels (k_cascade_bs: tests/test_cascade_bs.py)
     flux, fla = plan.evolve(pts)
     return plan, flux, fla
 
@@ -46,8 +45,8 @@ def test_cascade_gamma_batch(nusi, oracle_mod, N):
            + [dict(base, mphi=3e6, g=0.1, si=2.2),                     # a lone point and a DSNB point: pair kernel
               dict(base, mphi=6e5, g=0.01, si=2.5, source_model=0)])
     plan, flux, fla = _run(nusi, pts, 16)
-    assert plan.kernels()[1] == "k_cascade_gb + k_cascade_ws_mrhs"
-    _, f1, fl1 = _run(nusi, pts, 1)   # one point per workgroup (k_cascade_ws)
+    assert plan.kernels()[1] == "k_cascade_bs_gamma + k_cascade_bs"
+    _, f1, fl1 = _run(nusi, pts, 1)   # one point per workgroup
     worst = 0.0
     for i, p in enumerate(pts):
         o = oracle_mod.Oracle(**cases.oracle_kwargs(p))
@@ -60,8 +59,8 @@ def test_cascade_gamma_batch(nusi, oracle_mod, N):
 
 
 def test_gamma_batch_c5_block_equals_pairs(nusi):
-    """A 64-table slice of the C5 scan (16 gamma per table): the gamma batch and the R = 2 pair kernel agree to
-    rounding, point by point."""
+    """A 64-table slice of the C5 scan (16 gamma per table): the gamma batch and the pair kernel agree to rounding,
+    point by point."""
     from nusiprop_amd import scan
     pts = scan.c5_points()[:1024]
     _, f16, fl16 = _run(nusi, pts, 16)

@@ -175,31 +175,32 @@ def test_gamma_batches_share_tables(nusi, oracle_mod):
 
 
 @pytest.mark.parametrize("N,nonres", [(37, True), (64, False), (130, True), (200, True), (300, True), (300, False),
-                                      (700, True)])
+                                      (700, True), (1500, True)])
 def test_cascade_kernels_agree(nusi, N, nonres):
-    """The bit-exact scalar cascades -- the wavefront (all redshift steps in flight, N_z - 1 <= 48) and the
-    register-resident per-step chain -- give the same fluxes bit for bit (same fma()s in the same order); the
-    LDS kernel (separate multiply and add, the reference's record arithmetic) and the default MFMA kernels
-    (AUTO = MFMA: blocks of four columns summed in the matrix core's order) agree to FLUX_RTOL with the same
-    exact zeros.  N = 700 exceeds the one-pass kernels' limits: the wavefront falls back to the register
-    kernel, the MFMA kind runs in step passes."""
+    """The bit-exact scalar cascade k_cascade (WAVEFRONT / REG / LDS, one kernel since round 5) and the default MFMA
+    cascade k_cascade_bs (AUTO = MFMA: blocks of four columns summed in the matrix core's order; step passes at
+    N = 700) agree to FLUX_RTOL with the same exact zeros; the three scalar names give the same bits.  N = 1500
+    (T - 1 = 1546 rows) is past no limit of either."""
     from nusiprop_amd import _lib
     pts = [dict(cases.C2B_100, N_bins_E=N, non_resonant=nonres, majorana=maj, mphi=m, g=gg)
            for maj, m, gg in ((True, 6e5, 0.01), (False, 2e6, 0.1), (True, 1e6, 0.3))]
     plan = nusi.Plan(N, pts[0]["lEmin"], pts[0]["lEmax"], pts[0]["zmax"], max_points=len(pts))
-    out = {}
+    out, names = {}, {}
     for kind in (_lib.CASCADE_WAVEFRONT, _lib.CASCADE_REG, _lib.CASCADE_LDS, _lib.CASCADE_AUTO, _lib.CASCADE_MFMA):
         plan.set_cascade(kind)
         out[kind] = plan.evolve(pts)
-    ref = out[_lib.CASCADE_REG]
+        names[kind] = plan.kernels()[1]
+    plan.close()
+    ref = out[_lib.CASCADE_LDS]
     assert np.all(np.isfinite(ref[1])) and np.any(ref[1] > 0)
     for kind, (f, fl) in out.items():
-        if kind in (_lib.CASCADE_LDS, _lib.CASCADE_MFMA, _lib.CASCADE_AUTO):
+        if kind in (_lib.CASCADE_MFMA, _lib.CASCADE_AUTO):
+            assert names[kind] == "k_cascade_bs"
             assert cases.rel_err(f, ref[0]) <= FLUX_RTOL and cases.rel_err(fl, ref[1]) <= FLUX_RTOL
             assert np.array_equal(f == 0, ref[0] == 0)
             continue
-        assert np.array_equal(f, ref[0]), "kind %d flux differs in %d entries" % (kind, np.sum(f != ref[0]))
-        assert np.array_equal(fl, ref[1])
+        assert names[kind] == "k_cascade"
+        assert np.array_equal(f, ref[0]) and np.array_equal(fl, ref[1])
     assert np.array_equal(out[_lib.CASCADE_AUTO][0], out[_lib.CASCADE_MFMA][0])
 
 
@@ -304,12 +305,11 @@ def _evolve_opts(nusi, pts, kind=None, **opts):
 
 
 @pytest.mark.parametrize("N", [37, 100, 130, 300])
-def test_cascade_ws_multi_rhs(nusi, N):
-    """The warp-specialised MFMA cascade on every point kind -- power-law and DSNB sources, non-resonant and
-    resonant-only, Majorana and Dirac: one point per workgroup (distinct tables) and two per workgroup when
-    they share a table (the multi-RHS kernel: gamma / norm / source batches, one operator, two sources, mixed
-    sources in one pair, a table slot with an odd number of points).  The pairs give the one-point-per-workgroup
-    fluxes bit for bit; both agree with the bit-exact wavefront to FLUX_RTOL with the same exact zeros."""
+def test_cascade_mfma_multi_rhs(nusi, N):
+    """The MFMA cascade on every point kind -- power-law and DSNB sources, non-resonant and resonant-only, Majorana
+    and Dirac: one point per workgroup (distinct tables), and several per workgroup when they share a table (pairs
+    and gamma batches: gamma / norm / source variations, one operator, mixed sources in one group, a table slot with
+    an odd number of points).  Every grouping agrees with the scalar kernel to FLUX_RTOL with the same exact zeros."""
     from nusiprop_amd import _lib
     distinct = [dict(cases.C2B_100, N_bins_E=N, mphi=m, g=g, majorana=maj, non_resonant=nr, source_model=src)
                 for m, g, maj, nr, src in ((6e5, 0.01, True, True, 1), (2e6, 0.1, False, True, 1), (1e6, 0.3, True, True, 0),
@@ -317,42 +317,38 @@ def test_cascade_ws_multi_rhs(nusi, N):
     # DSNB points at lE 12 -> 17 have a zero source (the Fermi-Dirac tail underflows): move them to lE 4 -> 9
     lo = [dict(p, lEmin=4.0, lEmax=9.0, mphi=p["mphi"] / 200.0) for p in distinct]
     for grid in (distinct, lo):
-        one = _evolve_opts(nusi, grid, cascade_rhs=1, cascade_sync=1)
-        wf = _evolve_opts(nusi, grid, kind=_lib.CASCADE_WAVEFRONT)
-        assert one[2][1] == "k_cascade_ws"
-        for a, b in zip(one[:2], wf[:2]):
+        one = _evolve_opts(nusi, grid, cascade_rhs=1)
+        ref = _evolve_opts(nusi, grid, kind=_lib.CASCADE_LDS)
+        assert one[2][1] == "k_cascade_bs" and ref[2][1] == "k_cascade"
+        for a, b in zip(one[:2], ref[:2]):
             assert cases.rel_err(a, b) <= FLUX_RTOL and np.array_equal(a == 0, b == 0)
         gam = [dict(p, si=s, norm=nm, source_model=src) for p in grid[:4]
                for s, nm, src in ((2.0, 1.0, 1), (2.3, 3.0, 0), (2.9, 0.5, 1))]
         gam.append(dict(grid[4], si=2.7))
-        ref = _evolve_opts(nusi, gam, cascade_rhs=1, cascade_sync=1)
-        two = _evolve_opts(nusi, gam, cascade_sync=1)
-        assert two[2][1] == "k_cascade_ws_mrhs"
-        assert np.array_equal(two[0], ref[0]) and np.array_equal(two[1], ref[1])
-        wf = _evolve_opts(nusi, gam, kind=_lib.CASCADE_WAVEFRONT)
-        assert cases.rel_err(two[1], wf[1]) <= FLUX_RTOL and np.array_equal(two[1] == 0, wf[1] == 0)
-        assert np.any(two[1] > 0)
+        gam.append(dict(grid[4], si=2.1, source_model=0))
+        ref = _evolve_opts(nusi, gam, kind=_lib.CASCADE_LDS)
+        for rhs, label in ((2, "k_cascade_bs_pairs + k_cascade_bs"), (0, "k_cascade_bs_gamma + pairs")):
+            got = _evolve_opts(nusi, gam, cascade_rhs=rhs)
+            assert got[2][1] == label, got[2]
+            assert cases.rel_err(got[1], ref[1]) <= FLUX_RTOL and np.array_equal(got[1] == 0, ref[1] == 0)
+        assert np.any(ref[1] > 0)
 
 
 @pytest.mark.parametrize("N,lEmin", [(100, 12.0), (200, 12.0), (700, 12.0), (1200, 10.0)])
 def test_cascade_step_passes(nusi, oracle_mod, N, lEmin):
-    """The step-pass cascade (k_cascade_ws<16, 1, true>: 16 redshift steps in flight per pass, F carried
-    in LDS from pass to pass; nuSIprop.hpp:257-315): N = 100 (16 steps, one pass) equals the one-pass
-    kernel k_cascade_ws<16, 1> bit for bit; N = 200 (32 steps, 2 passes, forced), 700 (109 steps, 7 passes) and
-    BASELINE C3's grid (N = 1200, lE 10 -> 17: 134 steps, 9 passes) against the oracle's cascade on the
-    GPU's own tables to FLUX_RTOL, with the per-step register kernel's exact zeros."""
+    """The step-pass instance of k_cascade_bs (16 redshift steps in flight per pass, the last step's F carried to the
+    next pass; nuSIprop.hpp:257-315), forced by NUSI_OPT_STEP_PASSES = 1: N = 100 (16 steps, one pass) and 200 (32
+    steps, 2 passes) where one pass would fit, 700 (109 steps, 7 passes) and BASELINE C3's grid (N = 1200, lE 10 ->
+    17: 134 steps, 9 passes) against the oracle's cascade on the GPU's own tables to FLUX_RTOL, with the scalar
+    kernel's exact zeros."""
     from nusiprop_amd import _lib
     pts = [dict(cases.C2B_100, N_bins_E=N, lEmin=lEmin, mphi=m, g=g, majorana=maj)
            for m, g, maj in ((6e5, 0.01, True), (1e5, 0.05, True), (2e6, 0.3, False))]
     got = _evolve_opts(nusi, pts, step_passes=1)
-    assert got[2][1] == "k_cascade_ws_passes"
-    if N == 100:
-        one = _evolve_opts(nusi, pts, cascade_sync=1)
-        assert one[2][1] == "k_cascade_ws"
-        assert np.array_equal(got[0], one[0]) and np.array_equal(got[1], one[1])
+    assert got[2][1] == "k_cascade_bs"
     plan = nusi.Plan(N, lEmin, pts[0]["lEmax"], pts[0]["zmax"], max_points=len(pts))
-    plan.set_cascade(_lib.CASCADE_REG)
-    reg = plan.evolve(pts)
+    plan.set_cascade(_lib.CASCADE_LDS)
+    ref = plan.evolve(pts)
     assert plan.Nz - 1 == {100: 16, 200: 32, 700: 109, 1200: 134}[N]
     for k, p in enumerate(pts):
         G, aT, A = plan.tables(k)
@@ -361,23 +357,23 @@ def test_cascade_step_passes(nusi, oracle_mod, N, lEmin):
         f_ref, fla_ref = o.cascade(G, aT, nusi.unpack_alpha(A, plan.T))
         assert cases.rel_err(got[0][k], f_ref) <= FLUX_RTOL, k
         assert cases.rel_err(got[1][k], fla_ref) <= FLUX_RTOL, k
-        assert np.array_equal(got[0][k] == 0, reg[0][k] == 0)
+        assert np.array_equal(got[0][k] == 0, ref[0][k] == 0)
     plan.close()
 
 
 @pytest.mark.parametrize("N", [200, 700])
 def test_cascade_step_passes_resonant_only(nusi, oracle_mod, N):
-    """The step-pass cascade with a resonant-only point in the launch (nuSIprop.hpp:273-278, 285-287): the launcher
-    then takes k_cascade_wsp<16, false>, whose chain keeps the resonant-only running sum (an all-non-resonant
-    launch takes the <16, true> instance without it); against the oracle's cascade on the GPU's own tables."""
+    """Step passes with resonant-only points in the launch (nuSIprop.hpp:273-278, 285-287): the launcher takes the
+    per-point-flag instance of k_cascade_bs, whose chain keeps the resonant-only running sum (an all-non-resonant
+    launch takes the kNR instance without it); against the oracle's cascade on the GPU's own tables."""
     from nusiprop_amd import _lib
     pts = [dict(cases.C2B_100, N_bins_E=N, lEmin=12.0, mphi=m, g=g, non_resonant=nr)
            for m, g, nr in ((6e5, 0.01, True), (2e6, 0.3, False), (1e6, 0.1, False))]
     got = _evolve_opts(nusi, pts, step_passes=1)
-    assert got[2][1] == "k_cascade_ws_passes"
+    assert got[2][1] == "k_cascade_bs"
     plan = nusi.Plan(N, 12.0, pts[0]["lEmax"], pts[0]["zmax"], max_points=len(pts))
-    plan.set_cascade(_lib.CASCADE_REG)
-    reg = plan.evolve(pts)
+    plan.set_cascade(_lib.CASCADE_LDS)
+    ref = plan.evolve(pts)
     for k, p in enumerate(pts):
         G, aT, A = plan.tables(k)
         o = oracle_mod.Oracle(**cases.oracle_kwargs(p))
@@ -385,21 +381,19 @@ def test_cascade_step_passes_resonant_only(nusi, oracle_mod, N):
         f_ref, fla_ref = o.cascade(G, aT, nusi.unpack_alpha(A, plan.T))
         assert cases.rel_err(got[0][k], f_ref) <= FLUX_RTOL, k
         assert cases.rel_err(got[1][k], fla_ref) <= FLUX_RTOL, k
-        assert np.array_equal(got[0][k] == 0, reg[0][k] == 0)
+        assert np.array_equal(got[0][k] == 0, ref[0][k] == 0)
     plan.close()
 
 
 def test_plan_kernels_names(nusi):
-    """nusi_plan_kernels reports what the last call launched: the batch alpha kernel, and per grid and
-    cascade kind the one-pass warp-specialised kernel, its multi-RHS form (gamma pairs sharing a table),
-    the block-synchronous kernel in step passes (N_z - 1 > 48) or the bit-exact wavefront (AUTO): by default the
-    block-synchronous k_cascade_bs in every shape, with NUSI_OPT_CASCADE_SYNC = 1 the per-stage kernels."""
+    """nusi_plan_kernels reports what the last call launched: the batch alpha kernel, and per grid and cascade kind
+    the block-synchronous MFMA cascade in every shape (one point per workgroup, pairs, gamma batches, step passes on
+    N_z - 1 > 48) or the scalar k_cascade (WAVEFRONT / REG / LDS)."""
     from nusiprop_amd import _lib
-    def run(N, lEmin, pts_kw, kind, sync=0):
+    def run(N, lEmin, pts_kw, kind):
         pts = [dict(cases.C2B_100, N_bins_E=N, lEmin=lEmin, **kw) for kw in pts_kw]
         plan = nusi.Plan(N, lEmin, pts[0]["lEmax"], pts[0]["zmax"], max_points=len(pts))
         plan.set_cascade(kind)
-        plan.set_option(_lib.OPT_CASCADE_SYNC, sync)
         plan.evolve(pts)
         k = plan.kernels()
         plan.close()
@@ -409,28 +403,21 @@ def test_plan_kernels_names(nusi):
     three = [dict(mphi=6e5, g=0.01, si=s) for s in (2.0, 2.5, 2.7)]
     dsnb_res = [dict(mphi=6e5, g=0.01, source_model=0, non_resonant=False)]
     for kind in (_lib.CASCADE_AUTO, _lib.CASCADE_MFMA):
-        # the default (NUSI_OPT_CASCADE_SYNC = 0): the block-synchronous kernel for every shape
         assert run(100, 12.0, two, kind) == ("k_alpha_batch", "k_cascade_bs")
         assert run(100, 12.0, pair, kind)[1] == "k_cascade_bs_pairs"
         assert run(100, 12.0, three, kind)[1] == "k_cascade_bs_gamma"
         assert run(700, 12.0, two, kind)[1] == "k_cascade_bs"
         assert run(100, 12.0, dsnb_res, kind)[1] == "k_cascade_bs"
-        # NUSI_OPT_CASCADE_SYNC = 1: the per-stage kernels
-        assert run(100, 12.0, two, kind, 1)[1] == "k_cascade_ws"
-        assert run(100, 12.0, pair, kind, 1)[1] == "k_cascade_ws_mrhs"
-        assert run(100, 12.0, three, kind, 1)[1] == "k_cascade_gb"
-        assert run(700, 12.0, two, kind, 1)[1] == "k_cascade_ws_passes"
-        assert run(100, 12.0, dsnb_res, kind, 1)[1] == "k_cascade_ws"
-    assert run(100, 12.0, two, _lib.CASCADE_WAVEFRONT)[1] == "k_cascade_wf"
-    assert run(700, 12.0, two, _lib.CASCADE_WAVEFRONT)[1] == "k_cascade_reg"
-    assert run(100, 12.0, two, _lib.CASCADE_LDS)[1] == "k_cascade"
+    for kind in (_lib.CASCADE_WAVEFRONT, _lib.CASCADE_REG, _lib.CASCADE_LDS):
+        assert run(100, 12.0, two, kind)[1] == "k_cascade"
+        assert run(700, 12.0, two, kind)[1] == "k_cascade"
 
 
 def test_c5_gamma_block_vs_oracle(nusi, oracle_mod):
     """BASELINE config 5: one full 16-gamma block of scan.c5_points() (N_E = 300, power law; one
     Stage-A table, the gamma batch k_cascade_bs_gamma by default) against the oracle -- its tables once, its
     cascade per gamma -- to FLUX_RTOL with the same exact zeros; the pairs give the one-point-per-workgroup fluxes
-    bit for bit (A/B), the gamma batch to rounding; the per-stage gamma batch k_cascade_gb to rounding."""
+    bit for bit (A/B), the gamma batch to rounding."""
     from nusiprop_amd import scan
     allp = scan.c5_points()
     blk = allp[16 * 1234:16 * 1235]
@@ -442,9 +429,6 @@ def test_c5_gamma_block_vs_oracle(nusi, oracle_mod):
     assert two[2][1] == "k_cascade_bs_pairs"
     assert np.array_equal(two[0], ref1[0]) and np.array_equal(two[1], ref1[1])
     assert cases.rel_err(flux, ref1[0]) <= FLUX_RTOL and np.array_equal(flux == 0, ref1[0] == 0)
-    gb = _evolve_opts(nusi, blk, cascade_sync=1)
-    assert gb[2][1] == "k_cascade_gb"
-    assert cases.rel_err(gb[0], flux) <= FLUX_RTOL and np.array_equal(gb[0] == 0, flux == 0)
     o = oracle_mod.Oracle(**cases.oracle_kwargs(blk[0]))
     G, aT, al = o.tables()
     for k, p in enumerate(blk):
