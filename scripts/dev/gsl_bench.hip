@@ -34,7 +34,7 @@ int main()
     for (int i = 1; i < Nz - 1; ++i) { E.push_back(E[N - 1] * pow(r, i)); E.push_back(E[N] * pow(r, i)); }
     std::sort(E.begin(), E.end());
     const double mn[3] = {0.02183689, 0.02347445, 0.05468866};
-    std::vector<double2> h;
+    std::vector<double2> h, hp;   // point-major (tile-like) and corner-major, the batch's 32 points fastest
     for (int im = 0; im < 32; im += 3) {
         const double mphi = pow(10.0, 5.5 + 2.5 * im / 31.0);
         for (int ig = 0; ig < 32; ig += 4) {
@@ -47,6 +47,15 @@ int main()
                         h.push_back(make_double2(zz.r, zz.i));
                     }
         }
+        for (int k = 0; k < 3; ++k)
+            for (size_t a = 0; a < E.size(); ++a)
+                for (size_t b = a + 1; b < E.size(); b += 4)
+                    for (int ig = 0; ig < 32; ++ig) {
+                        const double g = pow(10.0, -3.0 + 3.0 * ig / 31.0), gr = g * g / (16 * M_PI);
+                        const double t = -2 * mn[k] * E[a] / (mphi * mphi), S = 2 * mn[k] * E[b] / (mphi * mphi);
+                        const cd zz = (1 + S + t) / C(2 + t, -gr);
+                        hp.push_back(make_double2(zz.r, zz.i));
+                    }
     }
     const int n = (int)h.size();
     std::vector<double2> hs = h, hr = h;
@@ -54,18 +63,21 @@ int main()
         return gsl_cli2_cost(x.x, x.y) > gsl_cli2_cost(y.x, y.y);
     });
     std::shuffle(hr.begin(), hr.end(), std::mt19937(1));
-    double2 *dz, *dzs, *dzr, *dout;
+    const int np = (int)hp.size();
+    double2 *dz, *dzs, *dzr, *dzp, *dout;
+    hipMalloc(&dzp, sizeof(double2) * np);
+    hipMemcpy(dzp, hp.data(), sizeof(double2) * np, hipMemcpyHostToDevice);
     hipMalloc(&dz, sizeof(double2) * n);
     hipMalloc(&dzs, sizeof(double2) * n);
     hipMalloc(&dzr, sizeof(double2) * n);
-    hipMalloc(&dout, sizeof(double2) * n);
+    hipMalloc(&dout, sizeof(double2) * (n > np ? n : np));
     hipMemcpy(dz, h.data(), sizeof(double2) * n, hipMemcpyHostToDevice);
     hipMemcpy(dzs, hs.data(), sizeof(double2) * n, hipMemcpyHostToDevice);
     hipMemcpy(dzr, hr.data(), sizeof(double2) * n, hipMemcpyHostToDevice);
     hipEvent_t e0, e1;
     hipEventCreate(&e0);
     hipEventCreate(&e1);
-    auto run = [&](const char* name, auto kern, const double2* src) {
+    auto run = [&](const char* name, auto kern, const double2* src, int n) {
         for (int rep = 0; rep < 2; ++rep) hipLaunchKernelGGL(kern, dim3((n + 255) / 256), dim3(256), 0, 0, src, dout, n);
         hipEventRecord(e0);
         const int reps = 5;
@@ -77,9 +89,10 @@ int main()
         printf("%-30s %8.3f ms per %d calls = %.4f ns/call (device)\n", name, ms / reps, n, ms / reps * 1e6 / n);
         fflush(stdout);
     };
-    run("gsl_cli2 tile order", kbench<0>, dz);
-    run("gsl_cli2 shuffled", kbench<0>, dzr);
-    run("gsl_cli2 cost-sorted", kbench<0>, dzs);
-    run("cli2 (shared algorithm)", kbench<1>, dz);
+    run("gsl_cli2 tile order", kbench<0>, dz, n);
+    run("gsl_cli2 shuffled", kbench<0>, dzr, n);
+    run("gsl_cli2 cost-sorted", kbench<0>, dzs, n);
+    run("gsl_cli2 points fastest", kbench<0>, dzp, np);
+    run("cli2 (shared algorithm)", kbench<1>, dz, n);
     return (int)hipDeviceSynchronize();
 }
