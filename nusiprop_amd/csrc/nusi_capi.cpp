@@ -440,6 +440,7 @@ struct nusi_plan {
     int* d_warn = nullptr;
     nusi::TablesDev tabs{};
     nusi::AlphaTilesDev atiles{};
+    nusi::MCornerDev mc{};         // NUSI_OPT_REFERENCE_ORDER: member corners of the big-batch kernel (mcorner_ensure)
     double* d_scratch = nullptr;   // flux outputs when the caller passes NULL
     std::shared_ptr<SplineStore> spl;
     nusi::SplineSet* d_nospl = nullptr;   // an empty spline set in device memory (no phi-phi tables loaded)
@@ -581,6 +582,41 @@ AlphaBatches alpha_batches(nusi_plan* pl, int ntab, std::vector<int>& perm)
         ++ab.nb_plain;
     }
     return ab;
+}
+
+// NUSI_OPT_REFERENCE_ORDER on the big-batch kernel: the member-corner block of plan p (MCornerDev) for the batches of
+// this call -- 9 NC doubles per table (C4's N_E = 300 axis: NC = 77 421, 5.6 MB), allocated for at most
+// kMCornerBudget bytes of tables (and half the free memory), at least the largest batch; launch_alpha runs the batches in
+// chunks that fit
+constexpr size_t kMCornerBudget = size_t(8) << 30;
+int mcorner_ensure(nusi_plan* p, int ntab, const AlphaBatches& ab)
+{
+    nusi::MCornerDev& mc = p->mc;
+    if (!mc.eu) {
+        std::vector<int> eu;
+        std::vector<double> ue;
+        nusi::mcorner_edges(p->grid.T, p->grid.lo.data(), p->grid.hi.data(), eu, ue);
+        HIPCHECK(hipMalloc(&mc.eu, sizeof(int) * eu.size()));
+        HIPCHECK(hipMemcpy(mc.eu, eu.data(), sizeof(int) * eu.size(), hipMemcpyHostToDevice));
+        HIPCHECK(hipMalloc(&mc.ue, sizeof(double) * ue.size()));
+        HIPCHECK(hipMemcpy(mc.ue, ue.data(), sizeof(double) * ue.size(), hipMemcpyHostToDevice));
+        mc.U = (int)ue.size();
+        mc.NC = (long long)mc.U * (mc.U + 1) / 2;
+    }
+    int nbmax = 1;
+    for (int b = 0; b < ab.nbatch; ++b) nbmax = std::max(nbmax, (int)((unsigned)p->h_batches[b] >> 24));
+    const size_t per = sizeof(double) * 9 * (size_t)mc.NC;
+    size_t fr = 0, tot = 0;
+    if (hipMemGetInfo(&fr, &tot) != hipSuccess) fr = kMCornerBudget;
+    const size_t budget = std::min(kMCornerBudget, (fr + (mc.buf ? per * mc.cap_tables : 0)) / 2);
+    const int want = std::max(nbmax, (int)std::min<size_t>((size_t)ntab, budget / per));
+    if (mc.buf && mc.cap_tables >= want) return NUSI_OK;
+    hipFree(mc.buf);
+    mc.buf = nullptr;
+    mc.cap_tables = 0;
+    HIPCHECK(hipMalloc(&mc.buf, per * want));
+    mc.cap_tables = want;
+    return NUSI_OK;
 }
 
 // NUSI_OPT_SHIFT_REUSE.  alpha / Gamma / alphaTilde see the energies only through
@@ -778,6 +814,9 @@ void nusi_plan_destroy(nusi_plan* pl)
     if (pl->h_gidx) hipHostFree(pl->h_gidx);
     if (pl->h_gbgrp) hipHostFree(pl->h_gbgrp);
     nusi::alpha_tiles_destroy(&pl->atiles);
+    hipFree(pl->mc.buf);
+    hipFree(pl->mc.eu);
+    hipFree(pl->mc.ue);
     hipFree(pl->d_scratch);
     if (pl->h_pts) hipHostFree(pl->h_pts);
     if (pl->stream) hipStreamDestroy(pl->stream);
@@ -1084,13 +1123,22 @@ int nusi_plan_evolve(nusi_plan* pl, const nusi_params* pts, int n, double* d_flu
     if (nd) HIPCHECK(nusi::launch_gamma_alphat(pl->gd, pl->d_tpts, nd, spl, pl->tabs, pl->d_warn, s, refo));
     if (sp) HIPCHECK(nusi::launch_gamma_alphat(sp->gd, sp->d_tpts, nbase, spl, sp->tabs, sp->d_warn, s, refo));
     HIPCHECK(hipEventRecord(ev[1], s));
-    if (nd)
+    const bool mcorn = refo && pl->alpha_kind == 0;   // (the big-batch kernel's member-corner block)
+    if (nd) {
+        if (mcorn && nbatch) {
+            AlphaBatches ab;
+            ab.nbatch = nbatch;
+            if (int r = mcorner_ensure(pl, nd, ab)) return r;
+        }
         HIPCHECK(nusi::launch_alpha(pl->gd, pl->d_tpts, nd, spl, pl->atiles, pl->tabs, pl->d_warn, s, pl->d_batches,
-                                    nbatch, cap, pl->alpha_kind, nb_plain, refo));
+                                    nbatch, cap, pl->alpha_kind, nb_plain, refo, pl->h_batches, &pl->mc));
+    }
     if (sp) {
         const AlphaBatches& bb = pl->shift_batches;
+        if (mcorn && bb.nbatch)
+            if (int r = mcorner_ensure(sp, nbase, bb)) return r;
         HIPCHECK(nusi::launch_alpha(sp->gd, sp->d_tpts, nbase, spl, sp->atiles, sp->tabs, sp->d_warn, s, sp->d_batches,
-                                    bb.nbatch, bb.cap, pl->alpha_kind, bb.nb_plain, refo));
+                                    bb.nbatch, bb.cap, pl->alpha_kind, bb.nb_plain, refo, sp->h_batches, &sp->mc));
         HIPCHECK(nusi::launch_table_shift(pl->gd, sp->gd, pl->d_smap, nd, ntab - nd, sp->tabs, pl->tabs, pl->d_warn, s));
     }
     HIPCHECK(hipEventRecord(ev[2], s));

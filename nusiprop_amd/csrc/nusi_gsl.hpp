@@ -376,6 +376,10 @@ NUSI_FN_OUT double gsl_li2(double x)
     return -d1 + 0.5 * d2;
 }
 
+// gsl_sf_complex_dilog_xy_e on the real axis (gsl_cli2's y == 0 branch, alone: a caller with real arguments keeps
+// the complex series' registers out of its own budget)
+NUSI_FN cd gsl_cli2_real(double x) { return cd{gsl_li2(x), (x >= 1.0) ? -gsl::kPiD * nm::log(x) : 0.0}; }
+
 // gsl_sf_complex_dilog_xy_e: the real axis; |z| within eps of 1 (Lewin A.2.4.1 / A.2.4.2); the unit disk; 1/z
 // into the unit disk, unwound with Li2(z) + Li2(1/z) = -zeta2 - log(-z)^2 / 2
 NUSI_FN_OUT cd gsl_cli2(double x, double y)

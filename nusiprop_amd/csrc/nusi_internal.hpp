@@ -3,6 +3,8 @@
 
 #include <hip/hip_runtime.h>
 
+#include <vector>
+
 #include "nusi.h"
 #include "nusi_physics.hpp"
 
@@ -51,6 +53,19 @@ struct AlphaTilesDev {
 hipError_t alpha_tiles_create(int T, const unsigned char* shared, AlphaTilesDev* out);
 void alpha_tiles_destroy(AlphaTilesDev* t);
 
+// NUSI_OPT_REFERENCE_ORDER on the big-batch kernel: the member corners (Dc, A of alpha_member_ref) of every table, mass
+// state and corner, evaluated by k_alpha_mcorner before k_alpha_batch reads them.  A corner is a pair of distinct bin
+// edges (S' edge us, t edge ut <= us; the edges numbered 0 .. U-1 along the table axis, an edge two neighbouring bins
+// share counted once): c = us (us + 1) / 2 + ut, NC = U (U + 1) / 2.  The block of a batch of nb tables starting at
+// slot p0 is buf + (p0 - pc0) 9 NC, laid out [k][field: Dcr, Dci, A][c][q] (the batch's tables fastest); a launch
+// chunk of batches whose tables fit cap_tables starts at table pc0.
+struct MCornerDev {
+    double* buf = nullptr;   // [cap_tables][3][3][NC]
+    int* eu = nullptr;       // [2 T]: edge number of bin edge 2 b + side (side 0: lo[b], 1: hi[b])
+    double* ue = nullptr;    // [U]: the energy of each edge
+    long long NC = 0;
+    int U = 0, cap_tables = 0;
+};
 // ref: NUSI_OPT_REFERENCE_ORDER (the kernels' kRef instances: the reference's own operation order for the complex
 // dilogarithms and the s-t interference member leaves, bit-identical to the oracle's ora_set_reference_order(1))
 hipError_t launch_gamma_alphat(const GridDev& g, const Point* pts, int npts, const SplineSet* spl, TablesDev t,
@@ -59,10 +74,14 @@ hipError_t launch_gamma_alphat(const GridDev& g, const Point* pts, int npts, con
 // m_phi, the masses and the channel flags (nullptr: every table alone).  kernel = NUSI_OPT_ALPHA_KERNEL:
 // 0 -- core tiles on the big-batch kernel k_alpha_batch (any count < 256; the first nb_plain batches without
 // the phi-phi channel, the rest with it); 1 -- k_alpha_tile<G> batches (count <= 4); 2 -- one entry per
-// work-item (k_alpha)
+// work-item (k_alpha).  h_batches: the same batches in host memory, and mc the member-corner block (both read
+// only by kernel 0 with ref: k_alpha_mcorner + k_alpha_batch in chunks of batches of <= mc->cap_tables tables)
 hipError_t launch_alpha(const GridDev& g, const Point* pts, int npts, const SplineSet* spl, const AlphaTilesDev& tiles,
                         TablesDev t, int* warn, hipStream_t s, const int* batches, int nbatches, int gmax,
-                        int kernel, int nb_plain, bool ref);
+                        int kernel, int nb_plain, bool ref, const int* h_batches = nullptr,
+                        const MCornerDev* mc = nullptr);
+// the edge numbering of MCornerDev for a table axis (hi[n] == lo[n + 1] bitwise: one edge): eu [2 T], ue [U]
+void mcorner_edges(int T, const double* lo, const double* hi, std::vector<int>& eu, std::vector<double>& ue);
 // NUSI_OPT_SHIFT_REUSE: tables s0 .. s0 + nshift - 1 of t (grid g) <- base tables map[q].x of tb (grid gb, the
 // axis extended on top), read map[q].y bins higher; warn[s] |= the warning bits of the base rows the slot reads
 // (tb.Wmin, required)

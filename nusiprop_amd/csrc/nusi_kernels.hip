@@ -286,16 +286,18 @@ __global__ __launch_bounds__(kTileThreads) NUSI_TILE_ATTR void k_alpha_tile(Grid
 #ifndef NUSI_BATCH_QC   // points per member-edge round (5: C4 alpha 6.05 -> 5.95 ms vs 4, profiles/r2q)
 #define NUSI_BATCH_QC 5
 #endif
-constexpr int kBatchQC = NUSI_BATCH_QC;
-#ifndef NUSI_REFO_NOSORT   // timing A/B only: 1 = the reference-order member corners in tile order (no cost sort)
-#define NUSI_REFO_NOSORT 0
-#endif   // kBatchQC (ct + cs + kAlphaTile) <= 256 jobs
+constexpr int kBatchQC = NUSI_BATCH_QC;   // kBatchQC (ct + cs + kAlphaTile) <= 256 jobs
 // NUSI_BATCH_PIPE (A/B): the member corners of point q + 1 are formed while point q combines (two mem buffers),
 // one barrier per point instead of two
 #ifndef NUSI_BATCH_PIPE
 #define NUSI_BATCH_PIPE 0
 #endif
 constexpr bool kBatchPipe = NUSI_BATCH_PIPE != 0;
+// NUSI_REFO_PREFETCH (A/B): the reference-order member corners of point q + 1 are loaded while point q combines
+#ifndef NUSI_REFO_PREFETCH
+#define NUSI_REFO_PREFETCH 1
+#endif
+constexpr bool kRefPrefetch = NUSI_REFO_PREFETCH != 0;
 __host__ __device__ inline int alpha_batch_lds_doubles()
 {
     const int c1 = kAlphaTile + 1;
@@ -356,15 +358,53 @@ __global__ __launch_bounds__(256) void k_alpha_medge(GridDev g, const Point* __r
     alpha_medge_job(pts[p], k, j, T, g.lo, g.hi, med + ((size_t)p * 3 + k) * kMedFields * T);
 }
 
+// NUSI_OPT_REFERENCE_ORDER: the member corners of every table of the batches [0, gridDim.y) -> mc (MCornerDev's
+// layout); grid (NC nbmax / 256, batches, 3 mass states).  Work-item j takes corner c = j / nb of table q = j % nb:
+// a wavefront's lanes hold the batch's tables at a few neighbouring corners, whose quotients -- differing in gr
+// only -- take similar GSL branches and series lengths (the series run ~10 to ~1000 terms: in the tile's corner
+// order the lanes of a wave diverge, 0.21 ns per call against 0.06 here, scripts/dev/gsl_bench.hip)
+__global__ __launch_bounds__(256) void k_alpha_mcorner(const Point* __restrict__ pts, const int* __restrict__ batches,
+                                                       MCornerDev mc, int pc0)
+{
+    const int bw = batches[blockIdx.y], k = blockIdx.z;
+    const int p0 = bw & 0xffffff, nb = (int)((unsigned)bw >> 24);
+    const Point& P = pts[p0];
+    if (!(P.non_resonant && P.majorana)) return;   // (no member corners)
+    const long long j = (long long)blockIdx.x * 256 + threadIdx.x;
+    if (j >= mc.NC * nb) return;
+    const long long c = j / nb;
+    const int q = (int)(j - c * nb);
+    double Dcr, Dci, A;
+    alpha_mcorner_ref_job(P, pts[p0 + q], k, c, mc.ue, Dcr, Dci, A);
+    const size_t mstr = (size_t)mc.NC * nb;
+    double* o = mc.buf + (size_t)(p0 - pc0) * 9 * mc.NC + (size_t)k * 3 * mstr + (size_t)j;
+    o[0] = Dcr;
+    o[mstr] = Dci;
+    o[2 * mstr] = A;
+}
+
+void mcorner_edges(int T, const double* lo, const double* hi, std::vector<int>& eu, std::vector<double>& ue)
+{
+    eu.assign(2 * (size_t)T, 0);
+    ue.clear();
+    for (int b = 0; b < T; ++b) {
+        if (b == 0 || !(lo[b] == hi[b - 1])) ue.push_back(lo[b]);   // else the previous bin's upper edge
+        eu[2 * b] = (int)ue.size() - 1;
+        ue.push_back(hi[b]);
+        eu[2 * b + 1] = (int)ue.size() - 1;
+    }
+}
+
 
 // kPP: the batches' tables have the phi-phi channel (its shared term per k).  kRef: NUSI_OPT_REFERENCE_ORDER -- each
-// point's member corners in the reference's operation order (alpha_batch_mcorner_ref_job: Dcr, Dci, A into the X
-// block, which then holds no Taylor coefficients), the rest of the batch structure unchanged
+// point's member corners in the reference's operation order, read from k_alpha_mcorner's block mc (Dcr, Dci, A into
+// the X block, which then holds no Taylor coefficients; pc0: the first table of the launch chunk), the rest of the
+// batch structure unchanged
 template <bool kPP, bool kRef>
 __global__ __launch_bounds__(kTileThreads) __attribute__((amdgpu_waves_per_eu(NUSI_BATCH_WAVES, NUSI_BATCH_WAVES)))
 void k_alpha_batch(GridDev g, const Point* __restrict__ pts, const SplineSet* __restrict__ splp, const int* __restrict__ tiles,
                    const int* __restrict__ batches, double* __restrict__ A, const double* __restrict__ med,
-                   int* __restrict__ warn, int* __restrict__ wmin)
+                   int* __restrict__ warn, int* __restrict__ wmin, MCornerDev mc, int pc0)
 {
     extern __shared__ __attribute__((aligned(16))) double sm[];
     const SplineSet& spl = *splp;
@@ -427,9 +467,6 @@ void k_alpha_batch(GridDev g, const Point* __restrict__ pts, const SplineSet* __
     const int mbd = alpha_batch_memb_doubles(cs, ct);
     double* tmp = X;
     double* mix = X + 4 * kCC;
-    double* const kcost = X + 3 * kCC;                               // (kRef) [cc] corner costs
-    int* const kperm = reinterpret_cast<int*>(X + 4 * kCC);          // (kRef) [cc] corners by decreasing cost
-    static_assert(kXFields * kCC >= 4 * kCC + kCC / 2 + 1, "the kRef corner order fits X");
     const int mjobs = ct + cs + kAlphaTile;
     int wsh = 0;
 #pragma unroll 1
@@ -457,23 +494,6 @@ void k_alpha_batch(GridDev g, const Point* __restrict__ pts, const SplineSet* __
             __syncthreads();   // X is rewritten with the member coefficients (kRef: with the member corners)
             if (!kRef)
                 for (int j = tid; j < cc; j += kTileThreads) b_xshared(j, edgk, ct, cs, X);
-            if (kRef) {
-                // GSL's series run a data-dependent number of iterations (~10 to ~900): the corners go to the
-                // work-items in decreasing order of their cost (gsl_cli2_cost, from the batch's first point), so
-                // that each wave's lanes take similar counts (kcost [cc] and kperm [cc] behind the member corners)
-                if (tid < cc) kcost[tid] = alpha_batch_mcorner_ref_cost(P, tid, edgk, ct, cs);
-                __syncthreads();
-                if (tid < cc) {
-                    const double c = kcost[tid];
-                    int rank = 0;
-                    for (int i = 0; i < cc; ++i) {
-                        const double ci = kcost[i];
-                        rank += (ci > c || (ci == c && i < tid)) ? 1 : 0;
-                    }
-                    if (NUSI_REFO_NOSORT) rank = tid;   // (timing A/B: the corners in tile order)
-                    kperm[rank] = tid;
-                }
-            }
         }
         // ---- the points, kBatchQC at a time: their member edge leaves in one round, then point by point.
         // (Two points per pair of barriers -- 512-thread workgroups whose halves share the batch's leaves -- measured
@@ -488,6 +508,20 @@ void k_alpha_batch(GridDev g, const Point* __restrict__ pts, const SplineSet* __
         // member edges: thread (mq, mjob) copies job mjob of point mq of each chunk (loading the next chunk's
         // values a chunk ahead measured slower: their registers stay live through the combine)
         const int mq = tid / mjobs, mjob = tid - mq * mjobs;
+        // (kRef) thread tid < cc carries corner tid's member leaves one point ahead, from k_alpha_mcorner's block:
+        // the corner's numbering c (only corners with ut <= us are read by the entries n < m; the others stay unset)
+        const size_t mstr = kRef ? (size_t)mc.NC * nb : 0;   // (uniform: the block's field stride and base)
+        const double* const mcb = kRef ? mc.buf + (size_t)(p0 - pc0) * 9 * mc.NC + (size_t)k * 3 * mstr : nullptr;
+        int moff = -1;   // this thread's corner: c nb, or -1
+        double mc0 = 0.0, mc1 = 0.0, mc2 = 0.0;
+        if (kRef && cornered && tid < cc) {
+            const int si = tid / ct, ti = tid - si * ct;
+            const int us = mc.eu[ssrc[si]], ut = mc.eu[tsrc[ti]];
+            if (ut <= us) {
+                moff = (us * (us + 1) / 2 + ut) * nb;
+                if (kRefPrefetch) { mc0 = mcb[moff]; mc1 = mcb[mstr + moff]; mc2 = mcb[2 * mstr + moff]; }
+            }
+        }
 #pragma unroll 1
         for (int q0 = 0; q0 < nb; q0 += kBatchQC) {
             const int nq = (nb - q0 < kBatchQC) ? nb - q0 : kBatchQC;
@@ -524,7 +558,12 @@ void k_alpha_batch(GridDev g, const Point* __restrict__ pts, const SplineSet* __
                     __syncthreads();   // member edges written / the previous point's combine is done with mem
                     if (cornered) {
                         if (kRef) {
-                            if (tid < cc) alpha_batch_mcorner_ref_job(Q, kperm[tid], edgk, ct, cs, X);
+                            if (moff >= 0) {
+                                const int o = moff + q;
+                                if (!kRefPrefetch) { mc0 = mcb[o]; mc1 = mcb[mstr + o]; mc2 = mcb[2 * mstr + o]; }
+                                X[tid] = mc0; X[kCC + tid] = mc1; X[2 * kCC + tid] = mc2;
+                                if (kRefPrefetch && q + 1 < nb) { mc0 = mcb[o + 1]; mc1 = mcb[mstr + o + 1]; mc2 = mcb[2 * mstr + o + 1]; }
+                            }
                         }
                         else
                             for (int j = tid; j < cc; j += kTileThreads) alpha_batch_mcorner_job(Q, j, edgk, ct, cs, X, memb, mem);
@@ -667,7 +706,8 @@ const char* last_alpha_kernel() { return t_alpha_kernel; }
 template <bool kRef>
 static hipError_t launch_alpha_t(const GridDev& g, const Point* pts, int npts, const SplineSet* spl,
                                  const AlphaTilesDev& at, TablesDev t, int* warn, hipStream_t s, const int* batches,
-                                 int nbatches, int gmax, int kernel, int nb_plain)
+                                 int nbatches, int gmax, int kernel, int nb_plain, const int* h_batches,
+                                 const MCornerDev* mc)
 {
     t_alpha_kernel = kRef ? "k_alpha_tile[refo]" : "k_alpha_tile";
     if (kernel == 0 && batches) {
@@ -690,13 +730,43 @@ static hipError_t launch_alpha_t(const GridDev& g, const Point* pts, int npts, c
                     hipLaunchKernelGGL(k_alpha_medge, dim3((unsigned)((5 * g.T + 255) / 256), npts, 3), dim3(256), 0, s,
                                        g, pts, t.Med);
                 }
-                if (nb_plain > 0)
-                    hipLaunchKernelGGL((k_alpha_batch<false, kRef>), dim3(at.ncls[0], nb_plain), dim3(kTileThreads), lds,
-                                       s, g, pts, spl, at.tiles, batches, t.A, t.Med, warn, t.Wmin);
-                if (nbatches > nb_plain)
-                    hipLaunchKernelGGL((k_alpha_batch<true, kRef>), dim3(at.ncls[0], nbatches - nb_plain),
-                                       dim3(kTileThreads), lds, s, g, pts, spl, at.tiles, batches + nb_plain, t.A, t.Med,
-                                       warn, t.Wmin);
+                if (!kRef) {
+                    if (nb_plain > 0)
+                        hipLaunchKernelGGL((k_alpha_batch<false, false>), dim3(at.ncls[0], nb_plain), dim3(kTileThreads),
+                                           lds, s, g, pts, spl, at.tiles, batches, t.A, t.Med, warn, t.Wmin, MCornerDev{}, 0);
+                    if (nbatches > nb_plain)
+                        hipLaunchKernelGGL((k_alpha_batch<true, false>), dim3(at.ncls[0], nbatches - nb_plain),
+                                           dim3(kTileThreads), lds, s, g, pts, spl, at.tiles, batches + nb_plain, t.A,
+                                           t.Med, warn, t.Wmin, MCornerDev{}, 0);
+                } else {
+                    // the member corners of a chunk of whole batches (<= mc->cap_tables tables, the phi-phi batches
+                    // in chunks of their own), then the chunk's tiles
+                    if (!mc || !mc->buf || !h_batches) return hipErrorInvalidValue;
+                    for (int b = 0; b < nbatches;) {
+                        const int lim = b < nb_plain ? nb_plain : nbatches, pc0 = h_batches[b] & 0xffffff;
+                        int e = b, ntb = 0, nbmax = 0;
+                        while (e < lim) {
+                            const int nbe = (int)((unsigned)h_batches[e] >> 24);
+                            if (e > b && ntb + nbe > mc->cap_tables) break;
+                            ntb += nbe;
+                            nbmax = std::max(nbmax, nbe);
+                            ++e;
+                        }
+                        if (ntb > mc->cap_tables) return hipErrorInvalidValue;
+                        const long long nj = mc->NC * nbmax;
+                        hipLaunchKernelGGL(k_alpha_mcorner, dim3((unsigned)((nj + 255) / 256), e - b, 3), dim3(256), 0, s,
+                                           pts, batches + b, *mc, pc0);
+                        if (b < nb_plain)
+                            hipLaunchKernelGGL((k_alpha_batch<false, true>), dim3(at.ncls[0], e - b), dim3(kTileThreads),
+                                               lds, s, g, pts, spl, at.tiles, batches + b, t.A, t.Med, warn, t.Wmin, *mc,
+                                               pc0);
+                        else
+                            hipLaunchKernelGGL((k_alpha_batch<true, true>), dim3(at.ncls[0], e - b), dim3(kTileThreads),
+                                               lds, s, g, pts, spl, at.tiles, batches + b, t.A, t.Med, warn, t.Wmin, *mc,
+                                               pc0);
+                        b = e;
+                    }
+                }
             } else {
                 const size_t lds = sizeof(double) * (size_t)alpha_tile_lds_doubles(cs, ct, 1);
                 hipLaunchKernelGGL((k_alpha_tile<1, kRef>), dim3(at.ncls[c], npts), dim3(kTileThreads), lds, s, g, pts,
@@ -749,10 +819,13 @@ static hipError_t launch_alpha_t(const GridDev& g, const Point* pts, int npts, c
 
 hipError_t launch_alpha(const GridDev& g, const Point* pts, int npts, const SplineSet* spl, const AlphaTilesDev& at,
                         TablesDev t, int* warn, hipStream_t s, const int* batches, int nbatches, int gmax,
-                        int kernel, int nb_plain, bool ref)
+                        int kernel, int nb_plain, bool ref, const int* h_batches, const MCornerDev* mc)
 {
-    if (ref) return launch_alpha_t<true>(g, pts, npts, spl, at, t, warn, s, batches, nbatches, gmax, kernel, nb_plain);
-    return launch_alpha_t<false>(g, pts, npts, spl, at, t, warn, s, batches, nbatches, gmax, kernel, nb_plain);
+    if (ref)
+        return launch_alpha_t<true>(g, pts, npts, spl, at, t, warn, s, batches, nbatches, gmax, kernel, nb_plain,
+                                    h_batches, mc);
+    return launch_alpha_t<false>(g, pts, npts, spl, at, t, warn, s, batches, nbatches, gmax, kernel, nb_plain, h_batches,
+                                 mc);
 }
 
 }  // namespace nusi

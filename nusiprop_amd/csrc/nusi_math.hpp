@@ -277,6 +277,8 @@ template <bool kRef>
 NUSI_FN cd cli2_t(double x, double y) { return kRef ? gsl_cli2(x, y) : cli2(x, y); }
 template <bool kRef>
 NUSI_FN double li2_t(double x) { return kRef ? gsl_li2(x) : li2(x); }
+template <bool kRef>
+NUSI_FN cd cli2_real_t(double x) { return kRef ? gsl_cli2_real(x) : cli2(x, 0.0); }
 
 // Li3(x), x in [-1, 1/2] (the DSNB source only reaches [-1, 0))
 NUSI_FN double li3(double x)

@@ -474,7 +474,7 @@ NUSI_FN void alpha_corner_shared(double S, double t, AlphaCorner& c)
         c.TU2 = NUSI_CLOG((1 + S + t) / S);
     }
     c.G = li2_t<kRef>((1 + S + t) / (2 + S));
-    const cd Dr = cli2_t<kRef>((1 + S + t) / (1 + t), 0.0);
+    const cd Dr = cli2_real_t<kRef>((1 + S + t) / (1 + t));
     c.Drr = Dr.r;
     c.Dri = Dr.i;
 }
@@ -921,7 +921,7 @@ NUSI_FN double alpha_phiphi_scale(const Point& P, double uk, const PPTerm& X)
 // Leaves of the big-batch tile kernel (k_alpha_batch): the shared corner fields live in separate blocks
 // (L, Drr, Dri persist for every mass state through the batch loop; LL, TU1, TU2, G and the mixed logs
 // only while the batch's shared brackets are formed), so each field has its own base pointer.  kRefA
-// (NUSI_OPT_REFERENCE_ORDER): A is a corner field of its own, corm[2 cc + o] (alpha_batch_mcorner_ref_job).
+// (NUSI_OPT_REFERENCE_ORDER): A is a corner field of its own, corm[2 kCC + o] (alpha_mcorner_ref_job's).
 // The big-batch kernel's corner blocks (P3, X, mem) keep their fields kCC doubles apart, a compile-time stride, so that
 // every field of a corner is one LDS load at an immediate offset from the same address.
 constexpr int kCC = (kAlphaTile + 1) * (kAlphaTile + 1);
@@ -962,7 +962,6 @@ using SplitLeaves = SplitLeavesT<false>;
 template <bool kRef = false>
 NUSI_FN void alpha_batch_corner_job(int j, const double* edgk, int ct, int cs, double* per, double* tmp)
 {
-    const int cc = cs * ct;
     const int si = j / ct, ti = j - si * ct;
     AlphaCorner c;
     alpha_corner_shared<kRef>(edgk[kTEdgeFields * ct + kSEdgeVal * cs + si], edgk[kTEdgeVal * ct + ti], c);
@@ -979,7 +978,6 @@ constexpr int kXFields = kLi2AxisTerms + 4;
 NUSI_FN int alpha_batch_memb_doubles(int cs, int ct) { return 5 * ct + 4 * cs + kAlphaTile; }
 NUSI_FN void alpha_batch_xshared_job(int j, const double* edgk, int ct, int cs, double* X)
 {
-    const int cc = cs * ct;
     const int si = j / ct, ti = j - si * ct;
     MemberShared M;
     alpha_member_shared(edgk[kTEdgeFields * ct + kSEdgeVal * cs + si], edgk[kTEdgeVal * ct + ti], M);
@@ -1096,7 +1094,6 @@ NUSI_FN void alpha_batch_medge_store(bool nonres, int job, int ct, int cs, int m
 NUSI_FN void alpha_batch_mcorner_job(const Point& P, int j, const double* edgk, int ct, int cs, const double* X,
                                      const double* memb, double* mem)
 {
-    const int cc = cs * ct;
     const int si = j / ct, ti = j - si * ct;
     MemberShared M;
 #pragma unroll
@@ -1111,24 +1108,19 @@ NUSI_FN void alpha_batch_mcorner_job(const Point& P, int j, const double* edgk, 
                         ext[4 * ct + si], ext[4 * ct + cs + si], Dcr, Dci, A);
     mem[j] = Dcr; mem[kCC + j] = Dci;   // (A: SplitLeaves forms it from the edge arguments)
 }
-// NUSI_OPT_REFERENCE_ORDER: member corner leaves of corner j for point P in the reference's operation order
-// (alpha_member_ref) -> mem[0..2][cc] (Dcr, Dci, A); no batch-shared coefficients
-NUSI_FN void alpha_batch_mcorner_ref_job(const Point& P, int j, const double* edgk, int ct, int cs, double* mem)
+// NUSI_OPT_REFERENCE_ORDER: member corner c = us (us + 1) / 2 + ut (S' edge us, t edge ut <= us, energies ue[]) of
+// mass state k for point Q of a batch whose first point is P (m_phi and the masses), in the reference's operation
+// order (alpha_member_ref); S and t by the functions the tile's edge block uses (alpha_tile_edge_job_k), so the values
+// are those the batch kernel's own corners would take
+NUSI_FN void alpha_mcorner_ref_job(const Point& P, const Point& Q, int k, long long c, const double* ue, double& Dcr,
+                                   double& Dci, double& A)
 {
-    const int cc = cs * ct;
-    const int si = j / ct, ti = j - si * ct;
-    double Dcr, Dci, A;
-    alpha_member_ref(edgk[kTEdgeFields * ct + kSEdgeVal * cs + si], edgk[kTEdgeVal * ct + ti], P.a_gr, Dcr, Dci, A);
-    mem[j] = Dcr; mem[kCC + j] = Dci; mem[2 * kCC + j] = A;
-}
-// NUSI_OPT_REFERENCE_ORDER: the cost of corner j's member dilogarithm for point P (gsl_cli2_cost of its quotient;
-// the points of a batch differ only in gr, which moves the quotient's small imaginary part), to order the corners
-NUSI_FN double alpha_batch_mcorner_ref_cost(const Point& P, int j, const double* edgk, int ct, int cs)
-{
-    const int si = j / ct, ti = j - si * ct;
-    const double S = edgk[kTEdgeFields * ct + kSEdgeVal * cs + si], t = edgk[kTEdgeVal * ct + ti];
-    const cd z = (1 + S + t) / C(2 + t, -P.a_gr);
-    return gsl_cli2_cost(z.r, z.i);
+    int us = (int)((sqrt(8.0 * (double)c + 1.0) - 1.0) * 0.5);
+    while ((long long)us * (us + 1) / 2 > c) --us;
+    while ((long long)(us + 1) * (us + 2) / 2 <= c) ++us;
+    const int ut = (int)(c - (long long)us * (us + 1) / 2);
+    const double m2 = P.mphi * P.mphi, mk = P.mn[k];
+    alpha_member_ref(alpha_S(mk, ue[us], m2), alpha_t(mk, ue[ut], m2), Q.a_gr, Dcr, Dci, A);
 }
 // xlog / ylog leaves of mass state k into xl [cs][kAlphaTile], yl [kAlphaTile][ct] (alpha_tile_mixed_job's jobs)
 NUSI_FN void alpha_batch_mixed_job(int j, const double* edgk, int ct, int cs, const int* tl, const int* th,
