@@ -317,7 +317,11 @@ static_assert(kBatchQC * (2 * (kAlphaTile + 1) + kAlphaTile) <= kTileThreads, "o
 template <bool kRef>
 NUSI_BCOLD void b_corner(int j, const double* edgk, int ct, int cs, double* per, double* tmp)
 {
+#ifdef NUSI_REFO_SHARED_FAST   // timing A/B only: the reference-order batches' shared corners in the default arithmetic
+    alpha_batch_corner_job<false>(j, edgk, ct, cs, per, tmp);
+#else
     alpha_batch_corner_job<kRef>(j, edgk, ct, cs, per, tmp);
+#endif
 }
 NUSI_BCOLD void b_xshared(int j, const double* edgk, int ct, int cs, double* X) { alpha_batch_xshared_job(j, edgk, ct, cs, X); }
 // The leaves the batch's shared brackets read (alpha_k_pre, alpha_k_pp): the shared corner blocks P3 | tmp, the

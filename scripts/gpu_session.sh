@@ -12,6 +12,7 @@
 #   py=<script>,<a>,..      python <script> <a> ..                                   -> py_<i>.out / .err
 #   vbench=<v>,<a>,..       bench.py <a> .. on the A/B library nusiprop_amd/libnusi_<v>.so (scripts/build_variant.sh)
 #   vpy=<v>,<script>,<a>,.. python <script> <a> .. on that library                   -> vpy_<i>.out / .err
+#   vprof=<v>,<a>,..        prof= of bench.py <a> .. on that library                  -> vkt_<i>_<v>/
 set -o pipefail
 TAG=${1:?tag}
 shift
@@ -48,6 +49,10 @@ for STEP in "$@"; do
       V=${ARGS%% *}; A=${ARGS#* }; [ "$A" = "$ARGS" ] && A=""
       NUSIPROP_LIB=$PWD/nusiprop_amd/libnusi_$V.so timeout -k 10 600 python bench.py $A > $OUT/vbench_${i}_$V.json \
         2> $OUT/vbench_${i}_$V.err || exit 1 ;;
+    vprof)
+      V=${ARGS%% *}; A=${ARGS#* }; [ "$A" = "$ARGS" ] && A=""
+      NUSIPROP_LIB=$PWD/nusiprop_amd/libnusi_$V.so timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/vkt_${i}_$V \
+        -o kt --output-format csv -- python3 bench.py $A > $OUT/vkt_${i}_$V.log 2>&1 || exit 1 ;;
     vpy)
       V=${ARGS%% *}; A=${ARGS#* }
       NUSIPROP_LIB=$PWD/nusiprop_amd/libnusi_$V.so timeout -k 10 600 python $A > $OUT/vpy_${i}_$V.out \
