@@ -106,12 +106,25 @@ NUSI_FN double hypot(double x, double y)
 }
 
 // ------------------------------------------------------------------------------------------------- real --
-// dilog_series_1: sum x^k / k^2, 0 < x <= 1/4
+// dilog_series_1: sum x^k / k^2, 0 < x <= 1/4.  (Not kExact: the partial sums are below x pi^2 / 6, so GSL's test
+// term < 2^-52 sum cannot hold while term >= 2^-50 x -- the first loop runs without it, as cseries_t's.)
 template <bool kExact>
 NUSI_FN double dilog_series_1_t(double x)
 {
     double sum = x, term = x;
-    for (int k = 2; k < 1000; k++) {
+    int k = 2;
+    if (!kExact) {
+        const double big = x * 0x1p-50;
+        for (; k < 1000; k++) {
+            term *= x;
+            term *= kKT.rr[k];
+            sum += term;
+            if (term < big) break;
+        }
+        if (k < 1000 && quot_lt<false>(fabs(term), fabs(sum), 0x1p-52)) return sum;
+        ++k;
+    }
+    for (; k < 1000; k++) {
         term *= x;
         term *= kKT.rr[k];   // rk * rk, rk = (k - 1.0) / k
         sum += term;
@@ -123,7 +136,8 @@ NUSI_FN double dilog_series_1(double x)
 {
     return x < 0x1p-400 ? dilog_series_1_t<true>(x) : dilog_series_1_t<false>(x);
 }
-// series_2: sum r^k / (k^2 (k + 1)) with the first nine terms unconditionally (d2 = k * k * (k + 1.0), exact)
+// series_2: sum r^k / (k^2 (k + 1)) with the first nine terms unconditionally (d2 = k * k * (k + 1.0), exact).
+// (Not kExact: the partial sums are below 0.65 x, so GSL's test ds < 2^-53 sum cannot hold while ds >= 2^-51 x.)
 template <bool kExact>
 NUSI_FN double series_2_t(double x)
 {
@@ -133,6 +147,18 @@ NUSI_FN double series_2_t(double x)
     for (k = 2; k < 10; k++) {
         rk *= x;
         sum += div_k<kExact>(rk, kKT.row[k].d2, kKT.row[k].y2);
+    }
+    if (!kExact) {
+        const double big = x * 0x1p-51;
+        double ds = 0.0;
+        for (; k < 100; k++) {
+            rk *= x;
+            ds = div_k<false>(rk, kKT.row[k].d2, kKT.row[k].y2);
+            sum += ds;
+            if (ds < big) break;
+        }
+        if (k < 100 && quot_lt<false>(fabs(ds), fabs(sum), 0x1p-53)) return sum;
+        ++k;
     }
     for (; k < 100; k++) {
         rk *= x;
@@ -241,32 +267,56 @@ NUSI_FN_OUT double clausen(double x)
 // ---------------------------------------------------------------------------------------------- complex --
 // dilogc_series_1 (s2 = false: sum r^k e^(i k theta) / k^2, first term r e^(i theta), kmax 50 + 22 / (-log r))
 // and series_2_c (s2 = true: sum z^k / (k^2 (k + 1)), first term r e^(i theta) / 2, kmax 30 + 18 / (-log r)) as
-// one loop; every operation is GSL's
-template <bool kExact>
+// one loop; every operation is GSL's.  kS2: 0 / 1 every lane of the wave runs series_1 / series_2_c (the table
+// column a constant), 2 per lane (s2).
+//
+// GSL tests |term|^2 < 2^-104 |sum|^2 after every term.  The partial sums are bounded by the sum of the moduli,
+// |sum| <= r sum_k r^(k-1) / k^2 <= r pi^2 / 6 (series_2_c's terms are smaller still), and |term| = q (ck^2 +
+// sk^2)^(1/2) with q = RN(r^k / d_k) and the rotated (ck, sk) of modulus 1 to ~1e-13 (<= 1000 rotations); so while q
+// >= 2^-50 r (2.4 times the bound's 1.645 2^-52 r) the test is false, and the loop runs without it until the first
+// term below, whose test is GSL's test at that k (the values are unchanged: the same terms, the same break).
+template <bool kExact, int kS2>
 NUSI_FN void cseries_t(bool s2, double r, double x, double y, double& re, double& im)
 {
+    const bool t2 = kS2 == 2 ? s2 : kS2 == 1;
     const double cos_theta = x / r, sin_theta = y / r;
     const double alpha = 1.0 - cos_theta, beta = sin_theta;
     double ck = cos_theta, sk = sin_theta, rk = r;
-    double real_sum = s2 ? 0.5 * r * ck : r * ck;
-    double imag_sum = s2 ? 0.5 * r * sk : r * sk;
+    double real_sum = t2 ? 0.5 * r * ck : r * ck;
+    double imag_sum = t2 ? 0.5 * r * sk : r * sk;
     const double nlr = -nm::log(r);
-    const int kmax = s2 ? 30 + (int)(18.0 / nlr) : 50 + (int)(22.0 / nlr);
+    const int kmax = t2 ? 30 + (int)(18.0 / nlr) : 50 + (int)(22.0 / nlr);
     KRow next = kKT.row[2];   // (the table row of the next iteration is loaded one iteration ahead; kmax <= 921)
-    for (int k = 2; k < kmax; k++) {
+    double q = 0.0, dr = 0.0, di = 0.0;
+    auto term = [&](int k) {
         const KRow kr = next;
         next = kKT.row[k + 1];
         const double ck_tmp = ck;
         ck = ck - (alpha * ck + beta * sk);
         sk = sk - (alpha * sk - beta * ck_tmp);
         rk *= r;
-        const double d = s2 ? kr.d2 : kr.d1;   // (double) k * k * (k + 1.0) or (double) k * k
-        const double yk = s2 ? kr.y2 : kr.y1;
-        const double q = div_k<kExact>(rk, d, yk);
-        const double dr = q * ck, di = q * sk;
+        const double d = t2 ? kr.d2 : kr.d1;   // (double) k * k * (k + 1.0) or (double) k * k
+        const double yk = t2 ? kr.y2 : kr.y1;
+        q = div_k<kExact>(rk, d, yk);
+        dr = q * ck;
+        di = q * sk;
         real_sum += dr;
         imag_sum += di;
-        if (quot_lt<kExact>(dr * dr + di * di, real_sum * real_sum + imag_sum * imag_sum, 0x1p-104)) break;
+    };
+    auto stop = [&]() { return quot_lt<kExact>(dr * dr + di * di, real_sum * real_sum + imag_sum * imag_sum, 0x1p-104); };
+    int k = 2;
+    if (!kExact) {
+        const double big = r * 0x1p-50;
+        for (; k < kmax; k++) {
+            term(k);
+            if (q < big) break;
+        }
+        if (k < kmax && stop()) k = kmax;   // (GSL's test at the k that left the first loop; else the next k)
+        else ++k;
+    }
+    for (; k < kmax; k++) {
+        term(k);
+        if (stop()) break;
     }
     re = real_sum;
     im = imag_sum;
@@ -275,8 +325,18 @@ NUSI_FN void cseries_t(bool s2, double r, double x, double y, double& re, double
 // below 2^-52 of the sum, and kmax bounds r^k for larger r)
 NUSI_FN void cseries(bool s2, double r, double x, double y, double& re, double& im)
 {
-    if (r < 0x1p-400) cseries_t<true>(s2, r, x, y, re, im);
-    else cseries_t<false>(s2, r, x, y, re, im);
+    if (r < 0x1p-400) {
+        cseries_t<true, 2>(s2, r, x, y, re, im);
+        return;
+    }
+#ifdef __HIP_DEVICE_COMPILE__
+    const unsigned long long act = __ballot(1), two = __ballot(s2);
+    if (two == act) cseries_t<false, 1>(s2, r, x, y, re, im);
+    else if (two == 0) cseries_t<false, 0>(s2, r, x, y, re, im);
+    else cseries_t<false, 2>(s2, r, x, y, re, im);
+#else
+    cseries_t<false, 2>(s2, r, x, y, re, im);
+#endif
 }
 // dilogc_series_3: |z| near 1, sum_{n <= 6} (log r)^n / n! H_n(theta)
 NUSI_FN void cseries_3(double r, double x, double y, double& re, double& im)

@@ -57,8 +57,8 @@ void alpha_tiles_destroy(AlphaTilesDev* t);
 // state and corner, evaluated by k_alpha_mcorner before k_alpha_batch reads them.  A corner is a pair of distinct bin
 // edges (S' edge us, t edge ut <= us; the edges numbered 0 .. U-1 along the table axis, an edge two neighbouring bins
 // share counted once): c = us (us + 1) / 2 + ut, NC = U (U + 1) / 2.  The block of a batch of nb tables starting at
-// slot p0 is buf + (p0 - pc0) 9 NC, laid out [k][field: Dcr, Dci, A][c][q] (the batch's tables fastest); a launch
-// chunk of batches whose tables fit cap_tables starts at table pc0.
+// slot p0 is buf + (p0 - pc0) 9 NC, laid out [k][field: Dcr, Dci, A][q][c] (a tile's corner rows contiguous); a
+// launch chunk of batches whose tables fit cap_tables starts at table pc0.
 struct MCornerDev {
     double* buf = nullptr;   // [cap_tables][3][3][NC]
     int* eu = nullptr;       // [2 T]: edge number of bin edge 2 b + side (side 0: lo[b], 1: hi[b])

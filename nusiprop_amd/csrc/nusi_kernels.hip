@@ -363,28 +363,38 @@ __global__ __launch_bounds__(256) void k_alpha_medge(GridDev g, const Point* __r
 }
 
 // NUSI_OPT_REFERENCE_ORDER: the member corners of every table of the batches [0, gridDim.y) -> mc (MCornerDev's
-// layout); grid (NC nbmax / 256, batches, 3 mass states).  Work-item j takes corner c = j / nb of table q = j % nb:
-// a wavefront's lanes hold the batch's tables at a few neighbouring corners, whose quotients -- differing in gr
-// only -- take similar GSL branches and series lengths (the series run ~10 to ~1000 terms: in the tile's corner
-// order the lanes of a wave diverge, 0.21 ns per call against 0.06 here, scripts/dev/gsl_bench.hip)
+// layout); grid (NC / cb, batches, 3 mass states), cb = kMcJobs / (the chunk's largest batch).  A workgroup takes
+// corners [c0, c0 + cb) of its batch's nb tables: job j (4 per work-item) is corner c0 + j / nb of table q = j % nb,
+// so a wavefront's lanes hold the batch's tables at a few neighbouring corners, whose quotients -- differing in gr
+// only -- take similar GSL branches and series lengths (in the tile's corner order the lanes of a wave diverge: 0.21
+// ns per call against 0.06, scripts/dev/gsl_bench.hip).  The values pass through LDS to leave as runs of cb corners
+// per (field, table), the layout the batch kernel reads a tile's corner rows from.
+constexpr int kMcJobs = 1024;
 __global__ __launch_bounds__(256) void k_alpha_mcorner(const Point* __restrict__ pts, const int* __restrict__ batches,
-                                                       MCornerDev mc, int pc0)
+                                                       MCornerDev mc, int pc0, int cb)
 {
-    const int bw = batches[blockIdx.y], k = blockIdx.z;
+    __shared__ double v[3 * kMcJobs];   // [field][q][cl]
+    const int bw = batches[blockIdx.y], k = blockIdx.z, tid = threadIdx.x;
     const int p0 = bw & 0xffffff, nb = (int)((unsigned)bw >> 24);
     const Point& P = pts[p0];
     if (!(P.non_resonant && P.majorana)) return;   // (no member corners)
-    const long long j = (long long)blockIdx.x * 256 + threadIdx.x;
-    if (j >= mc.NC * nb) return;
-    const long long c = j / nb;
-    const int q = (int)(j - c * nb);
-    double Dcr, Dci, A;
-    alpha_mcorner_ref_job(P, pts[p0 + q], k, c, mc.ue, Dcr, Dci, A);
-    const size_t mstr = (size_t)mc.NC * nb;
-    double* o = mc.buf + (size_t)(p0 - pc0) * 9 * mc.NC + (size_t)k * 3 * mstr + (size_t)j;
-    o[0] = Dcr;
-    o[mstr] = Dci;
-    o[2 * mstr] = A;
+    const long long c0 = (long long)blockIdx.x * cb;
+    const int nj = cb * nb;   // <= kMcJobs
+    for (int j = tid; j < nj; j += 256) {
+        const int cl = j / nb, q = j - cl * nb;
+        if (c0 + cl >= mc.NC) break;
+        double Dcr, Dci, A;
+        alpha_mcorner_ref_job(P, pts[p0 + q], k, c0 + cl, mc.ue, Dcr, Dci, A);
+        v[q * cb + cl] = Dcr;
+        v[nj + q * cb + cl] = Dci;
+        v[2 * nj + q * cb + cl] = A;
+    }
+    __syncthreads();
+    double* const o = mc.buf + (size_t)(p0 - pc0) * 9 * mc.NC + (size_t)k * 3 * nb * mc.NC;
+    for (int e = tid; e < 3 * nj; e += 256) {
+        const int fq = e / cb, cl = e - fq * cb;   // fq = field nb + q
+        if (c0 + cl < mc.NC) o[(size_t)fq * mc.NC + c0 + cl] = v[e];
+    }
 }
 
 void mcorner_edges(int T, const double* lo, const double* hi, std::vector<int>& eu, std::vector<double>& ue)
@@ -516,13 +526,13 @@ void k_alpha_batch(GridDev g, const Point* __restrict__ pts, const SplineSet* __
         // the corner's numbering c (only corners with ut <= us are read by the entries n < m; the others stay unset)
         const size_t mstr = kRef ? (size_t)mc.NC * nb : 0;   // (uniform: the block's field stride and base)
         const double* const mcb = kRef ? mc.buf + (size_t)(p0 - pc0) * 9 * mc.NC + (size_t)k * 3 * mstr : nullptr;
-        int moff = -1;   // this thread's corner: c nb, or -1
+        int moff = -1;   // this thread's corner c, or -1 (point q's value at q NC + c)
         double mc0 = 0.0, mc1 = 0.0, mc2 = 0.0;
         if (kRef && cornered && tid < cc) {
             const int si = tid / ct, ti = tid - si * ct;
             const int us = mc.eu[ssrc[si]], ut = mc.eu[tsrc[ti]];
             if (ut <= us) {
-                moff = (us * (us + 1) / 2 + ut) * nb;
+                moff = us * (us + 1) / 2 + ut;
                 if (kRefPrefetch) { mc0 = mcb[moff]; mc1 = mcb[mstr + moff]; mc2 = mcb[2 * mstr + moff]; }
             }
         }
@@ -563,10 +573,13 @@ void k_alpha_batch(GridDev g, const Point* __restrict__ pts, const SplineSet* __
                     if (cornered) {
                         if (kRef) {
                             if (moff >= 0) {
-                                const int o = moff + q;
+                                const size_t o = (size_t)q * mc.NC + moff;
                                 if (!kRefPrefetch) { mc0 = mcb[o]; mc1 = mcb[mstr + o]; mc2 = mcb[2 * mstr + o]; }
                                 X[tid] = mc0; X[kCC + tid] = mc1; X[2 * kCC + tid] = mc2;
-                                if (kRefPrefetch && q + 1 < nb) { mc0 = mcb[o + 1]; mc1 = mcb[mstr + o + 1]; mc2 = mcb[2 * mstr + o + 1]; }
+                                if (kRefPrefetch && q + 1 < nb) {
+                                    const size_t o1 = o + mc.NC;
+                                    mc0 = mcb[o1]; mc1 = mcb[mstr + o1]; mc2 = mcb[2 * mstr + o1];
+                                }
                             }
                         }
                         else
@@ -757,9 +770,9 @@ static hipError_t launch_alpha_t(const GridDev& g, const Point* pts, int npts, c
                             ++e;
                         }
                         if (ntb > mc->cap_tables) return hipErrorInvalidValue;
-                        const long long nj = mc->NC * nbmax;
-                        hipLaunchKernelGGL(k_alpha_mcorner, dim3((unsigned)((nj + 255) / 256), e - b, 3), dim3(256), 0, s,
-                                           pts, batches + b, *mc, pc0);
+                        const int cb = kMcJobs / nbmax;
+                        hipLaunchKernelGGL(k_alpha_mcorner, dim3((unsigned)((mc->NC + cb - 1) / cb), e - b, 3), dim3(256),
+                                           0, s, pts, batches + b, *mc, pc0, cb);
                         if (b < nb_plain)
                             hipLaunchKernelGGL((k_alpha_batch<false, true>), dim3(at.ncls[0], e - b), dim3(kTileThreads),
                                                lds, s, g, pts, spl, at.tiles, batches + b, t.A, t.Med, warn, t.Wmin, *mc,

@@ -179,13 +179,14 @@ def test_gsl_clausen_vs_mpmath(oracle_mod):
 
 def test_device_gsl_bit_identical_to_oracle(oracle_mod, hlib):
     """nusi_gsl.hpp (the GPU's NUSI_OPT_REFERENCE_ORDER arithmetic) == oracle/ora_gsl.c bit for bit, on every KAT
-    vector and on 20 000 seeded random arguments around GSL's branch points -- including its rewrite of the series'
-    stopping tests as multiply-compare (exact, nusi_gsl.hpp header)."""
+    vector and on 26 000 seeded random arguments around GSL's branch points and over 20 decades of |z| -- including
+    its rewrite of the series' stopping tests as multiply-compare and their test-free first loops (exact, nusi_gsl.hpp)."""
     import numpy as np
     rng = np.random.default_rng(20250213)
     re, im = D(), D()
     xs = [x for x, _ in KAT["li2_real"]] + list(rng.uniform(-40, 40, 3000)) + list(rng.uniform(-1.5, 2.5, 3000))
     xs += [0.25, 0.5, 1.0, 1.01, 2.0, -0.25, -0.5, -2.0, 0.0] + list(np.nextafter([0.25, 0.5, 1.0, 1.01, 2.0], 3))
+    xs += list(10.0 ** rng.uniform(-20, 0, 2000)) + list(-(10.0 ** rng.uniform(-20, 3, 1000)))   # (series test-free prefixes)
     for x in xs:
         assert hlib.hc_gsl_li2(float(x)) == oracle_mod.gsl_dilog(float(x)), x
     zs = [(x, y) for x, y, _, _ in KAT["li2_complex"] + KAT["li2_complex_axis"] + KAT["li2_complex_unit"]]
@@ -193,6 +194,8 @@ def test_device_gsl_bit_identical_to_oracle(oracle_mod, hlib):
     rad = np.concatenate([rng.uniform(0.0, 3.0, 3000), 1 + rng.uniform(-0.05, 0.05, 3000)])
     zs += list(zip(rad * np.cos(t), rad * np.sin(t)))
     zs += list(zip(rng.uniform(-3, 3, 4000), rng.uniform(-1e-3, 1e-3, 4000)))
+    rs, ts = 10.0 ** rng.uniform(-20, 0.5, 3000), rng.uniform(-np.pi, np.pi, 3000)
+    zs += list(zip(rs * np.cos(ts), rs * np.sin(ts)))
     for x, y in zs:
         hlib.hc_gsl_cli2(float(x), float(y), ctypes.byref(re), ctypes.byref(im))
         assert (re.value, im.value) == oracle_mod.gsl_complex_dilog(float(x), float(y)), (x, y)
