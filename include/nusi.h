@@ -230,6 +230,14 @@ int nusi_plan_set_cascade(nusi_plan *plan, int kind);
  *                          gb / wsp of rounds 2-3) is refused: those kernels
  *                          were removed in round 5. */
 #define NUSI_OPT_CASCADE_SYNC 7
+/*   NUSI_OPT_REFO_CORNER_MB  the reference-order big-batch kernel's member-
+ *                          corner block (9 doubles per table, pair of bin
+ *                          edges and mass state: 5.6 MB per table at
+ *                          N_E = 300): at most this many MiB, the batches run
+ *                          in chunks that fit (at least one batch); 0 =
+ *                          automatic (8 GiB, at most half the free memory).
+ *                          Any value gives the same tables bit for bit. */
+#define NUSI_OPT_REFO_CORNER_MB 8
 int nusi_plan_set_option(nusi_plan *plan, int option, int value);
 /* per-point NUSI_WARN_* bits of the last call */
 int nusi_plan_warnings(nusi_plan *plan, int *out, int n);

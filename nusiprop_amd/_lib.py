@@ -59,6 +59,7 @@ CASCADE_AUTO, CASCADE_WAVEFRONT, CASCADE_REG, CASCADE_LDS, CASCADE_MFMA = 0, 1, 
 OPT_ALPHA_BATCH, OPT_ALPHA_KERNEL, OPT_CASCADE_RHS, OPT_STEP_PASSES, OPT_SHIFT_REUSE = 1, 2, 3, 4, 5
 OPT_REFERENCE_ORDER = 6
 OPT_CASCADE_SYNC = 7
+OPT_REFO_CORNER_MB = 8
 
 _lib = None
 

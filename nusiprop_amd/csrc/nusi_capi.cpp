@@ -428,6 +428,7 @@ struct nusi_plan {
     int shift_max = 0;              // NUSI_OPT_SHIFT_REUSE: K, the largest bin offset served by a base table set
     int ref_order = 0;              // NUSI_OPT_REFERENCE_ORDER: 1 = the tables in the reference's operation order
     int cascade_sync = 0;           // NUSI_OPT_CASCADE_SYNC: 0 = auto, 2 = block-synchronous (the same kernel; 1 is refused)
+    int corner_mb = 0;              // NUSI_OPT_REFO_CORNER_MB: the member-corner block's budget (0 = automatic)
     size_t fh_doubles = 0;          // capacity of d_fh in doubles (the block-synchronous kernels' FIFOs)
     nusi_plan* shift = nullptr;     // ... its plan: the same grid with K more redshift steps (axis T + K)
     int2* d_smap = nullptr;         // per shifted table: base index in `shift`, bin offset
@@ -586,10 +587,10 @@ AlphaBatches alpha_batches(nusi_plan* pl, int ntab, std::vector<int>& perm)
 
 // NUSI_OPT_REFERENCE_ORDER on the big-batch kernel: the member-corner block of plan p (MCornerDev) for the batches of
 // this call -- 9 NC doubles per table (C4's N_E = 300 axis: NC = 77 421, 5.6 MB), allocated for at most
-// kMCornerBudget bytes of tables (and half the free memory), at least the largest batch; launch_alpha runs the batches in
-// chunks that fit
+// NUSI_OPT_REFO_CORNER_MB (automatic: kMCornerBudget bytes and half the free memory) of tables, at least the largest
+// batch; launch_alpha runs the batches in chunks that fit
 constexpr size_t kMCornerBudget = size_t(8) << 30;
-int mcorner_ensure(nusi_plan* p, int ntab, const AlphaBatches& ab)
+int mcorner_ensure(nusi_plan* p, int ntab, const AlphaBatches& ab, int budget_mb)
 {
     nusi::MCornerDev& mc = p->mc;
     if (!mc.eu) {
@@ -608,9 +609,10 @@ int mcorner_ensure(nusi_plan* p, int ntab, const AlphaBatches& ab)
     const size_t per = sizeof(double) * 9 * (size_t)mc.NC;
     size_t fr = 0, tot = 0;
     if (hipMemGetInfo(&fr, &tot) != hipSuccess) fr = kMCornerBudget;
-    const size_t budget = std::min(kMCornerBudget, (fr + (mc.buf ? per * mc.cap_tables : 0)) / 2);
+    const size_t budget = budget_mb > 0 ? ((size_t)budget_mb << 20)
+                                        : std::min(kMCornerBudget, (fr + (mc.buf ? per * mc.cap_tables : 0)) / 2);
     const int want = std::max(nbmax, (int)std::min<size_t>((size_t)ntab, budget / per));
-    if (mc.buf && mc.cap_tables >= want) return NUSI_OK;
+    if (mc.buf && mc.cap_tables >= want && (budget_mb == 0 || mc.cap_tables == want)) return NUSI_OK;
     hipFree(mc.buf);
     mc.buf = nullptr;
     mc.cap_tables = 0;
@@ -1128,7 +1130,7 @@ int nusi_plan_evolve(nusi_plan* pl, const nusi_params* pts, int n, double* d_flu
         if (mcorn && nbatch) {
             AlphaBatches ab;
             ab.nbatch = nbatch;
-            if (int r = mcorner_ensure(pl, nd, ab)) return r;
+            if (int r = mcorner_ensure(pl, nd, ab, pl->corner_mb)) return r;
         }
         HIPCHECK(nusi::launch_alpha(pl->gd, pl->d_tpts, nd, spl, pl->atiles, pl->tabs, pl->d_warn, s, pl->d_batches,
                                     nbatch, cap, pl->alpha_kind, nb_plain, refo, pl->h_batches, &pl->mc));
@@ -1136,7 +1138,7 @@ int nusi_plan_evolve(nusi_plan* pl, const nusi_params* pts, int n, double* d_flu
     if (sp) {
         const AlphaBatches& bb = pl->shift_batches;
         if (mcorn && bb.nbatch)
-            if (int r = mcorner_ensure(sp, nbase, bb)) return r;
+            if (int r = mcorner_ensure(sp, nbase, bb, pl->corner_mb)) return r;
         HIPCHECK(nusi::launch_alpha(sp->gd, sp->d_tpts, nbase, spl, sp->atiles, sp->tabs, sp->d_warn, s, sp->d_batches,
                                     bb.nbatch, bb.cap, pl->alpha_kind, bb.nb_plain, refo, sp->h_batches, &sp->mc));
         HIPCHECK(nusi::launch_table_shift(pl->gd, sp->gd, pl->d_smap, nd, ntab - nd, sp->tabs, pl->tabs, pl->d_warn, s));
@@ -1254,6 +1256,10 @@ int nusi_plan_set_option(nusi_plan* pl, int option, int value)
         if (value == 1)   // the per-stage kernels (k_cascade_ws / gb / wsp) were removed in round 5
             return fail(NUSI_EPARAM, "NUSI_OPT_CASCADE_SYNC = 1: the per-stage cascade kernels are gone; k_cascade_bs is the MFMA cascade");
         pl->cascade_sync = value;
+        return NUSI_OK;
+    case NUSI_OPT_REFO_CORNER_MB:
+        if (value < 0 || value > (1 << 20)) return fail(NUSI_EPARAM, "NUSI_OPT_REFO_CORNER_MB outside [0, 2^20]");
+        pl->corner_mb = value;
         return NUSI_OK;
     case NUSI_OPT_REFERENCE_ORDER:
         if (value < 0 || value > 1) return fail(NUSI_EPARAM, "NUSI_OPT_REFERENCE_ORDER outside [0, 1]");

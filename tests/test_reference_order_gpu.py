@@ -1,12 +1,16 @@
-"""NUSI_OPT_REFERENCE_ORDER on the GPU: the Stage-A tables in the reference's own operation order, against the
-oracle in reference-order mode (oracle.reference_order(1), nusi_oracle.h ora_set_reference_order).
+"""NUSI_OPT_REFERENCE_ORDER on the GPU: the Stage-A tables in the reference's own arithmetic, against the oracle in
+reference-order mode (oracle.reference_order(1), nusi_oracle.h ora_set_reference_order).
 
 The default tables are bit-exact to the oracle's shared-algorithm order (tests/test_gpu_parity.py), which evaluates
 the alpha table's s-t interference member dilogarithms as Taylor series about a batch-shared real point and their
-arguments as sums of edge arguments, and takes a near-axis Taylor shortcut in every complex dilogarithm.  In
-reference-order mode the kernels instead run gsl_sf_complex_dilog_xy_e's general series on the reference's own
-quotient z = (1+S+t)/(2 - i gr + t) and carg of its expression (nuSIprop.hpp:1428-1467; the complex dilogarithms
-of Gamma :843-878 and alphaTilde :1135-1192 too).  Bar:
+arguments as sums of edge arguments, and every dilogarithm by this repository's own series.  In reference-order mode
+the kernels instead run GSL's algorithms (nusi_gsl.hpp, the restatement of GSL 2.x dilog.c / clausen.c; the oracle's
+ora_gsl.c) for every gsl_sf_dilog and gsl_sf_complex_dilog_xy_e the reference calls, on the reference's own
+arguments -- the member quotient z = (1+S+t)/(2 - i gr + t) and carg of its expression (nuSIprop.hpp:1428-1467), the
+complex dilogarithms of Gamma :843-878 and alphaTilde :1135-1192, the real ones of :1098, :1375-1398 and aux.hpp:77-166.
+On the big-batch kernel the member corners come from k_alpha_mcorner's block (one evaluation per table, mass state
+and pair of bin edges).  Bar:
+Bar:
 
 * tables BIT-EXACT to the reference-order oracle on every small case, C1 / C2a / C2b at N_E = 300, an 8-point subset
   of the C4 scan and C3 (N_E = 1200, phi-phi on at the reference's table geometry);
@@ -30,13 +34,15 @@ def nusi():
     return nusiprop_amd
 
 
-def _gpu_refo(nusi, pts, kernel=None, tables=True):
+def _gpu_refo(nusi, pts, kernel=None, tables=True, corner_mb=None):
     from nusiprop_amd import _lib
     p0 = pts[0]
     plan = nusi.Plan(p0["N_bins_E"], p0["lEmin"], p0["lEmax"], p0["zmax"], max_points=len(pts))
     plan.set_option(_lib.OPT_REFERENCE_ORDER, 1)
     if kernel is not None:
         plan.set_option(_lib.OPT_ALPHA_KERNEL, kernel)
+    if corner_mb is not None:
+        plan.set_option(_lib.OPT_REFO_CORNER_MB, corner_mb)
     flux, fla = plan.evolve(pts)
     tabs = [plan.tables(i) for i in range(len(pts))] if tables else None
     names = plan.kernels()
@@ -122,6 +128,9 @@ def test_reference_order_c4_full_grid(nusi, oracle_mod):
     f_ref, fla_ref = oracle_mod.evolve_many(pts, level=1)
     errs = np.array([max(cases.rel_err(flux[k], f_ref[k]), cases.rel_err(fla[k], fla_ref[k])) for k in range(len(pts))])
     assert np.all(errs <= FLUX_RTOL), (int(np.argmax(errs)), float(errs.max()))
+    # the member-corner block in chunks of one batch (64 MiB: 11 tables' worth, below the 32 of a batch) -- the same bits
+    fc, flac, _, _, _ = _gpu_refo(nusi, pts, tables=False, corner_mb=64)
+    assert np.array_equal(fc, flux) and np.array_equal(flac, fla)
     p0 = pts[0]
     plan = nusi.Plan(p0["N_bins_E"], p0["lEmin"], p0["lEmax"], p0["zmax"], max_points=len(pts))
     f0, fla0 = plan.evolve(pts)
