@@ -105,31 +105,57 @@ NUSI_FN double hypot(double x, double y)
     return h * s;
 }
 
+// Wave-uniform votes for the series' first loops (below): every active lane's predicate / any active lane's.  On the
+// host (tests/hostcheck) a "wave" is the one call.
+NUSI_FN bool wave_all(bool p)
+{
+#ifdef __HIP_DEVICE_COMPILE__
+    return __all(p);
+#else
+    return p;
+#endif
+}
+NUSI_FN bool wave_any(bool p)
+{
+#ifdef __HIP_DEVICE_COMPILE__
+    return __any(p);
+#else
+    return p;
+#endif
+}
+
 // ------------------------------------------------------------------------------------------------- real --
 // dilog_series_1: sum x^k / k^2, 0 < x <= 1/4.  (Not kExact: the partial sums are below x pi^2 / 6, so GSL's test
-// term < 2^-52 sum cannot hold while term >= 2^-50 x -- the first loop runs without it, as cseries_t's.)
+// term < 2^-52 sum cannot hold while term >= 2^-50 x: the first loop runs without it, as cseries_t's.)
 template <bool kExact>
 NUSI_FN double dilog_series_1_t(double x)
 {
     double sum = x, term = x;
     int k = 2;
+    bool done = false;
     if (!kExact) {
         const double big = x * 0x1p-50;
-        for (; k < 1000; k++) {
+        bool small = false;
+        while (k < 1000) {
             term *= x;
             term *= kKT.rr[k];
             sum += term;
-            if (term < big) break;
+            small = wave_any(term < big);
+            if (small) break;
+            ++k;
         }
-        if (k < 1000 && quot_lt<false>(fabs(term), fabs(sum), 0x1p-52)) return sum;
-        ++k;
+        if (small) {
+            done = quot_lt<false>(fabs(term), fabs(sum), 0x1p-52);
+            ++k;
+        }
     }
-    for (; k < 1000; k++) {
-        term *= x;
-        term *= kKT.rr[k];   // rk * rk, rk = (k - 1.0) / k
-        sum += term;
-        if (quot_lt<kExact>(fabs(term), fabs(sum), 0x1p-52)) break;   // fabs(term / sum) < GSL_DBL_EPSILON
-    }
+    if (!done)
+        for (; k < 1000; k++) {
+            term *= x;
+            term *= kKT.rr[k];   // rk * rk, rk = (k - 1.0) / k
+            sum += term;
+            if (quot_lt<kExact>(fabs(term), fabs(sum), 0x1p-52)) break;   // fabs(term / sum) < GSL_DBL_EPSILON
+        }
     return sum;
 }
 NUSI_FN double dilog_series_1(double x)
@@ -148,24 +174,31 @@ NUSI_FN double series_2_t(double x)
         rk *= x;
         sum += div_k<kExact>(rk, kKT.row[k].d2, kKT.row[k].y2);
     }
+    bool done = false;
     if (!kExact) {
         const double big = x * 0x1p-51;
         double ds = 0.0;
-        for (; k < 100; k++) {
+        bool small = false;
+        while (k < 100) {
             rk *= x;
             ds = div_k<false>(rk, kKT.row[k].d2, kKT.row[k].y2);
             sum += ds;
-            if (ds < big) break;
+            small = wave_any(ds < big);
+            if (small) break;
+            ++k;
         }
-        if (k < 100 && quot_lt<false>(fabs(ds), fabs(sum), 0x1p-53)) return sum;
-        ++k;
+        if (small) {
+            done = quot_lt<false>(fabs(ds), fabs(sum), 0x1p-53);
+            ++k;
+        }
     }
-    for (; k < 100; k++) {
-        rk *= x;
-        const double ds = div_k<kExact>(rk, kKT.row[k].d2, kKT.row[k].y2);
-        sum += ds;
-        if (quot_lt<kExact>(fabs(ds), fabs(sum), 0x1p-53)) break;   // fabs(ds / sum) < 0.5 GSL_DBL_EPSILON
-    }
+    if (!done)
+        for (; k < 100; k++) {
+            rk *= x;
+            const double ds = div_k<kExact>(rk, kKT.row[k].d2, kKT.row[k].y2);
+            sum += ds;
+            if (quot_lt<kExact>(fabs(ds), fabs(sum), 0x1p-53)) break;   // fabs(ds / sum) < 0.5 GSL_DBL_EPSILON
+        }
     return sum;
 }
 // dilog_series_2: Li2(x) = 1 + (1 - x) log(1 - x) / x + series_2(x)
@@ -305,19 +338,29 @@ NUSI_FN void cseries_t(bool s2, double r, double x, double y, double& re, double
     };
     auto stop = [&]() { return quot_lt<kExact>(dr * dr + di * di, real_sum * real_sum + imag_sum * imag_sum, 0x1p-104); };
     int k = 2;
+    bool done = false;
     if (!kExact) {
+        // the first loop leaves together (wave votes), so k stays wave-uniform and the table rows scalar loads: at the
+        // first k where a lane reaches its kmax (no term k), or where a lane's term falls below its bound (term k
+        // added, then each lane's test at k -- false for the lanes still above it)
         const double big = r * 0x1p-50;
+        bool small = false;
+        while (wave_all(k < kmax)) {
+            term(k);
+            small = wave_any(q < big);
+            if (small) break;
+            ++k;
+        }
+        if (small) {
+            done = stop();
+            ++k;
+        }
+    }
+    if (!done)
         for (; k < kmax; k++) {
             term(k);
-            if (q < big) break;
+            if (stop()) break;
         }
-        if (k < kmax && stop()) k = kmax;   // (GSL's test at the k that left the first loop; else the next k)
-        else ++k;
-    }
-    for (; k < kmax; k++) {
-        term(k);
-        if (stop()) break;
-    }
     re = real_sum;
     im = imag_sum;
 }
