@@ -66,10 +66,13 @@ def parse():
     ap.add_argument("--rhs", type=int, default=0,
                     help="NUSI_OPT_CASCADE_RHS: 0 = the library default, 1 = one point per cascade workgroup, 2 = pairs "
                          "of points sharing a table, 3..16 = the gamma batch (k_cascade_bs_gamma)")
-    ap.add_argument("--reference-order", action="store_true",
-                    help="NUSI_OPT_REFERENCE_ORDER: the tables in the reference's own operation order for the complex "
-                         "dilogarithms (bit-exact to the oracle's reference-order mode); default: the shared-algorithm "
-                         "order (bit-exact to the oracle's default mode)")
+    ap.add_argument("--shared-order", action="store_true",
+                    help="the library's default table arithmetic (this repository's dilogarithm series and the batch-"
+                         "shared member Taylor coefficients; bit-exact to the oracle's default mode, faster).  Default "
+                         "here: NUSI_OPT_REFERENCE_ORDER, the reference's own arithmetic (GSL's dilogarithm algorithms "
+                         "on the reference's arguments; bit-exact to the oracle's reference-order mode), the mode whose "
+                         "fluxes are within the north star's 1e-9 of the reference on every config (DESIGN.md sec. 2)")
+    ap.add_argument("--reference-order", action="store_true", help="(the default; kept for old command lines)")
     ap.add_argument("--no-parity", action="store_true", help="skip the parity object (oracle fluxes of a sample)")
     ap.add_argument("--dry-run", action="store_true",
                     help="launch / rank / reduction plumbing only, no GPU work (gloo; CPU tests): prints the JSON "
@@ -77,7 +80,11 @@ def parse():
     ap.add_argument("--traffic-json", default="",
                     help="per-launch HBM bytes / fp64 VALU work from rocprofv3 --pmc passes (scripts/pmc_summary.py); "
                          "default: the committed profiles/pmc_traffic_<workload>.json, used only if its libnusi_sha256 matches the loaded library")
-    return ap.parse_args()
+    args = ap.parse_args()
+    if args.shared_order and args.reference_order:
+        ap.error("--shared-order and --reference-order exclude each other")
+    args.reference_order = not args.shared_order
+    return args
 
 
 def rank_points(args, rank, world):
@@ -175,7 +182,18 @@ def _oracle(p):
     return oracle.Oracle(**kw)
 
 
-def cpu_baseline(pts, budget_s, pp_tables=None):
+def cpu_baseline(pts, budget_s, pp_tables=None, level=1):
+    """_cpu_baseline in the oracle's arithmetic mode matching the timed tables (level 1: the reference's own, GSL's
+    dilogarithm algorithms; 0: the shared-algorithm order)."""
+    from oracle import oracle
+    oracle.build()
+    with oracle.reference_order(level):
+        res = _cpu_baseline(pts, budget_s, pp_tables)
+    res["arithmetic"] = "reference order (GSL algorithms, ora_gsl.c)" if level else "shared-algorithm order"
+    return res
+
+
+def _cpu_baseline(pts, budget_s, pp_tables=None):
     """The C oracle (test infrastructure, the reference's algorithm restated) on a bounded sample of the same
     workload: Stage A (tables) and Stage B (cascade) timed apart on one core for a quarter of the budget, then
     whole evolve()s on a thread pool over the host cores for the rest (ctypes releases the GIL, the oracle has
@@ -383,16 +401,16 @@ def launch_ranks(args):
     return subprocess.call(cmd)
 
 
-SECONDARY = (   # name, bench.py arguments, steps: BASELINE configs 5, 3 and 2, and C4 in reference-order mode
+SECONDARY = (   # name, bench.py arguments, steps: BASELINE configs 5, 3 and 2, and C4 in the shared-algorithm order
     ("c5", ["--workload", "c5", "--no-cpu-baseline"], 10),
     ("c3", ["--workload", "c3", "--cpu-seconds", "10"], 3),
-    ("c4_refo", ["--workload", "c4", "--reference-order", "--no-cpu-baseline"], 10),
+    ("c4_shared", ["--workload", "c4", "--shared-order", "--no-cpu-baseline"], 10),
     ("c2", ["--workload", "c2", "--cpu-seconds", "4"], 20),
 )
 
 
 def secondary_lines(local):
-    """BASELINE configs 5, 3 and 2 and the C4 scan in reference-order mode, measured beside the headline C4 line,
+    """BASELINE configs 5, 3 and 2 and the C4 scan in the shared-algorithm order, measured beside the headline C4 line,
     each by a child bench.py process on the same GPU after the C4 timed region (so the driver's run records them
     too): props/s, stage times, kernels, parity, and (C3, C2) the oracle's CPU numbers."""
     import subprocess
@@ -723,7 +741,7 @@ def run(args, world, rank, local, dist, plan, pts, desc, pp_tables):
     if rank == 0 and world == 1 and args.workload == "c4" and not args.no_secondary and not args.points:
         out["secondary_lines"] = secondary_lines(local)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(pts, args.cpu_seconds, pp_tables)
+        out["cpu_baseline"] = cpu_baseline(pts, args.cpu_seconds, pp_tables, 1 if args.reference_order else 0)
         if args.workload == "c1":
             out["cpu_baseline"]["c1_test_cpp"] = c1_cpu_lines(min(5.0, args.cpu_seconds / 3))
     if rank == 0:

@@ -15,7 +15,7 @@ if [ -n "$REV" ]; then
 fi
 C=$SRC/nusiprop_amd/csrc
 F="-O3 -std=c++17 -fPIC -ffp-contract=off --offload-arch=gfx950 -I$SRC/include -Wno-unused-value $*"
-/opt/rocm/bin/hipcc $F -c -o $D/k.o $C/nusi_kernels.hip &
+/opt/rocm/bin/hipcc $F -mllvm -amdgpu-spill-vgpr-to-agpr=0 -c -o $D/k.o $C/nusi_kernels.hip &
 /opt/rocm/bin/hipcc $F -mllvm -pragma-unroll-threshold=1000000 -c -o $D/c.o $C/nusi_cascade.hip &
 /opt/rocm/bin/hipcc $F -c -o $D/a.o $C/nusi_capi.cpp &
 wait
