@@ -340,6 +340,27 @@ def parity_indices(args, pts):
     return sorted(pick)
 
 
+ORDER_SPREAD = ("profiles/r5/reference_order_configs.json", "profiles/r5/reference_order_c4.json")
+
+
+def order_floor(gpu_order):
+    """The per-config floor of this run's fluxes against the reference's own arithmetic (the reference-order oracle):
+    in the reference order the tables are bit-exact to it and the fluxes held to FLUX_RTOL; in the shared-algorithm
+    order the two arithmetics' measured distance (the oracle in both modes on the CPU: tests/test_oracle_reference_order.py
+    -> ORDER_SPREAD[0], the whole C4 grid scripts/reference_order_scan.py -> ORDER_SPREAD[1])."""
+    if gpu_order == "reference":
+        return {c: FLUX_RTOL for c in ("C1", "C2a", "C2b", "C3", "C4")}   # (tests/test_reference_order_gpu.py)
+    try:
+        cf = json.load(open(os.path.join(ROOT, ORDER_SPREAD[0])))
+        c4 = json.load(open(os.path.join(ROOT, ORDER_SPREAD[1])))
+    except (OSError, ValueError):
+        return None
+    out = {"C1": cf["C1_N300"]["flux_max_rel"], "C2a": cf["C2a"]["flux_max_rel"], "C2b": cf["C2b"]["flux_max_rel"],
+           "C3": cf["C3"]["flux_max_rel"], "C4": c4["flux_rel_default_vs_reference_order"]["max"],
+           "C4_points_above_1e-9": c4["flux_rel_default_vs_reference_order"]["points_above_1e-9"]}
+    return {k: max(v, FLUX_RTOL) if isinstance(v, float) else v for k, v in out.items()}
+
+
 def parity(sel_pts, gpu_fla, gpu_order, phiphi_tables=None, label=""):
     """The GPU fluxes of `sel_pts` (flavour basis, from the timed run) against the C oracle's evolve() in both of
     its arithmetic modes: the shared-algorithm order the default tables are bit-exact to, and the reference's own
@@ -363,6 +384,8 @@ def parity(sel_pts, gpu_fla, gpu_order, phiphi_tables=None, label=""):
                       # the north star's bar (<= 1e-9 vs the CPU reference) against the reference-order oracle, whatever
                       # order this run's tables were built in
                       "within_north_star_vs_reference_order": res["vs_oracle_reference_order"]["max_rel"] <= NORTH_STAR_RTOL,
+                      # per BASELINE config: how close this order's fluxes are to the reference's own arithmetic
+                      "floor_vs_reference_order_per_config": order_floor(gpu_order),
                       "note": "this run's tables are bit-exact to the oracle's %s mode (tests/test_gpu_parity.py, "
                               "tests/test_reference_order_gpu.py); the fluxes differ from it by the cascade's summation "
                               "order only, held to %.0e. The other mode differs where the s-t interference closed forms "

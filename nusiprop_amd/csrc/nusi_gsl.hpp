@@ -309,7 +309,7 @@ NUSI_FN_OUT double clausen(double x)
 // >= 2^-50 r (2.4 times the bound's 1.645 2^-52 r) the test is false, and the loop runs without it until the first
 // term below, whose test is GSL's test at that k (the values are unchanged: the same terms, the same break).
 template <bool kExact, int kS2>
-NUSI_FN void cseries_t(bool s2, double r, double x, double y, double& re, double& im)
+NUSI_FN void cseries_t(bool s2, double r, double lr, double x, double y, double& re, double& im)
 {
     const bool t2 = kS2 == 2 ? s2 : kS2 == 1;
     const double cos_theta = x / r, sin_theta = y / r;
@@ -317,7 +317,7 @@ NUSI_FN void cseries_t(bool s2, double r, double x, double y, double& re, double
     double ck = cos_theta, sk = sin_theta, rk = r;
     double real_sum = t2 ? 0.5 * r * ck : r * ck;
     double imag_sum = t2 ? 0.5 * r * sk : r * sk;
-    const double nlr = -nm::log(r);
+    const double nlr = -lr;   // -log(r)
     const int kmax = t2 ? 30 + (int)(18.0 / nlr) : 50 + (int)(22.0 / nlr);
     KRow next = kKT.row[2];   // (the table row of the next iteration is loaded one iteration ahead; kmax <= 921)
     double q = 0.0, dr = 0.0, di = 0.0;
@@ -366,27 +366,27 @@ NUSI_FN void cseries_t(bool s2, double r, double x, double y, double& re, double
 }
 // (the terms r^k stay above 2^-960 and |sum|^2 above 2^-900 unless r < 2^-400: the series breaks at a term
 // below 2^-52 of the sum, and kmax bounds r^k for larger r)
-NUSI_FN void cseries(bool s2, double r, double x, double y, double& re, double& im)
+NUSI_FN void cseries(bool s2, double r, double lr, double x, double y, double& re, double& im)
 {
     if (r < 0x1p-400) {
-        cseries_t<true, 2>(s2, r, x, y, re, im);
+        cseries_t<true, 2>(s2, r, lr, x, y, re, im);
         return;
     }
 #ifdef __HIP_DEVICE_COMPILE__
     const unsigned long long act = __ballot(1), two = __ballot(s2);
-    if (two == act) cseries_t<false, 1>(s2, r, x, y, re, im);
-    else if (two == 0) cseries_t<false, 0>(s2, r, x, y, re, im);
-    else cseries_t<false, 2>(s2, r, x, y, re, im);
+    if (two == act) cseries_t<false, 1>(s2, r, lr, x, y, re, im);
+    else if (two == 0) cseries_t<false, 0>(s2, r, lr, x, y, re, im);
+    else cseries_t<false, 2>(s2, r, lr, x, y, re, im);
 #else
-    cseries_t<false, 2>(s2, r, x, y, re, im);
+    cseries_t<false, 2>(s2, r, lr, x, y, re, im);
 #endif
 }
 // dilogc_series_3: |z| near 1, sum_{n <= 6} (log r)^n / n! H_n(theta)
-NUSI_FN void cseries_3(double r, double x, double y, double& re, double& im)
+NUSI_FN void cseries_3(double r, double lr, double x, double y, double& re, double& im)
 {
     const double theta = nm::atan2(y, x);
     const double cos_theta = x / r, sin_theta = y / r;
-    const double a = nm::log(r);
+    const double a = lr;   // log(r)
     const double omc = 1.0 - cos_theta, omc2 = omc * omc;
     double H_re[7], H_im[7];
     H_re[0] = kPiD * kPiD / 6.0 + 0.25 * (theta * theta - 2.0 * kPiD * fabs(theta));
@@ -415,16 +415,19 @@ NUSI_FN void cseries_3(double r, double x, double y, double& re, double& im)
     re = sum_re;
     im = sum_im;
 }
-// dilogc_fundamental (r < 1, x <= 0.732): series_3 above r = 0.98, dilogc_series_2 above 0.25, else series_1
-NUSI_FN_OUT cd fundamental(double r, double x, double y)
+// dilogc_fundamental (r < 1, x <= 0.732): series_3 above r = 0.98, dilogc_series_2 above 0.25, else series_1.  Every
+// branch takes log(r) (series_3's expansion variable, the series' kmax): formed once, and returned in lr for
+// unitdisk's log(1 - z) of a reflected argument (the same call on the same value)
+NUSI_FN_OUT cd fundamental(double r, double x, double y, double& lr)
 {
     double re, im;
+    lr = nm::log(r);
     if (r > 0.98) {
-        cseries_3(r, x, y, re, im);
+        cseries_3(r, lr, x, y, re, im);
         return cd{re, im};
     }
     const bool s2 = r > 0.25;
-    cseries(s2, r, x, y, re, im);
+    cseries(s2, r, lr, x, y, re, im);
     if (!s2) return cd{re, im};
     // dilogc_series_2: + (1 - z) log(1 - z) / z + 1, log(1 - z) by gsl_sf_complex_log_e
     const double zr = 1.0 - x, zi = -y;
@@ -446,9 +449,10 @@ NUSI_FN cd unitdisk(double x, double y)
     const bool refl = x > 0.732;
     const double x_tmp = 1.0 - x, y_tmp = -y;
     const double r_tmp = refl ? gsl::hypot(x_tmp, y_tmp) : r;
-    const cd f = fundamental(refl ? r_tmp : r, refl ? x_tmp : x, refl ? y_tmp : y);   // one call site
+    double lr;
+    const cd f = fundamental(refl ? r_tmp : r, refl ? x_tmp : x, refl ? y_tmp : y, lr);   // one call site
     if (!refl) return f;
-    const double lnz = nm::log(r), lnomz = nm::log(r_tmp);
+    const double lnz = nm::log(r), lnomz = lr;   // log(r_tmp)
     const double argz = nm::atan2(y, x), argomz = nm::atan2(y_tmp, x_tmp);
     return cd{-f.r + zeta2 - lnz * lnomz + argz * argomz, -f.i - argz * lnomz - argomz * lnz};
 }
