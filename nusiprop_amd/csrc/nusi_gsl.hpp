@@ -35,6 +35,16 @@
 
 #include "nusi_libm.hpp"
 
+// The elementary functions inside the GSL functions: inline by default (each call from an out-of-line function costs
+// the callee's register save / restore and the call; NUSI_GSL_CALL_LIBM: calls, A/B builds).  The same functions.
+#ifdef NUSI_GSL_CALL_LIBM
+#define GSL_LOG nm::log
+#define GSL_ATAN2 nm::atan2
+#else
+#define GSL_LOG nm::log_i
+#define GSL_ATAN2 nm::atan2_i
+#endif
+
 namespace nusi {
 namespace gsl {
 
@@ -206,7 +216,7 @@ NUSI_FN double dilog_series_2(double x)
 {
     double sum = x < 0x1p-100 ? series_2_t<true>(x) : series_2_t<false>(x);   // (x^9 stays above 2^-900)
     double t;
-    if (x > 0.01) t = (1.0 - x) * nm::log(1.0 - x) / x;
+    if (x > 0.01) t = (1.0 - x) * GSL_LOG(1.0 - x) / x;
     else {
         const double c3 = 1.0 / 3.0, c4 = 1.0 / 4.0, c5 = 1.0 / 5.0, c6 = 1.0 / 6.0, c7 = 1.0 / 7.0, c8 = 1.0 / 8.0;
         const double t68 = c6 + x * (c7 + x * c8);
@@ -221,7 +231,7 @@ NUSI_FN double dilog_series_2(double x)
 NUSI_FN_OUT double dilog_xge0(double x)
 {
     if (x > 1.0 && x <= 1.01) {   // series around x = 1
-        const double eps = x - 1.0, lne = nm::log(eps);
+        const double eps = x - 1.0, lne = GSL_LOG(eps);
         const double c0 = kPiD * kPiD / 6.0, c1 = 1.0 - lne, c2 = -(1.0 - 2.0 * lne) / 4.0, c3 = (1.0 - 3.0 * lne) / 9.0;
         const double c4 = -(1.0 - 4.0 * lne) / 16.0, c5 = (1.0 - 5.0 * lne) / 25.0, c6 = -(1.0 - 6.0 * lne) / 36.0;
         const double c7 = (1.0 - 7.0 * lne) / 49.0, c8 = -(1.0 - 8.0 * lne) / 64.0;
@@ -233,8 +243,8 @@ NUSI_FN_OUT double dilog_xge0(double x)
     const double u = br == 0 ? 1.0 / x : br == 1 ? 1.0 - 1.0 / x : br == 2 ? 1.0 - x : x;   // GSL's series argument
     const double ser = dilog_series_2(u);
     if (br == 3) return ser;
-    const double log_x = nm::log(x);
-    const double log_u = br == 0 ? 0.0 : nm::log(u);   // log(1 - 1/x) resp. log(1 - x)
+    const double log_x = GSL_LOG(x);
+    const double log_u = br == 0 ? 0.0 : GSL_LOG(u);   // log(1 - 1/x) resp. log(1 - x)
     if (br == 0) {
         const double t1 = kPiD * kPiD / 3.0, t2 = ser, t3 = 0.5 * log_x * log_x;
         return t1 - t2 - t3;
@@ -279,7 +289,7 @@ NUSI_FN_OUT double clausen(double x)
     }
     double val;
     if (x == 0.0) val = 0.0;
-    else if (x < x_cut) val = x * (1.0 - nm::log(x));
+    else if (x < x_cut) val = x * (1.0 - GSL_LOG(x));
     else {
         const double t = 2.0 * (x * x / (kPiD * kPiD) - 0.5);
         const double a = -1.0, b = 1.0;
@@ -292,7 +302,7 @@ NUSI_FN_OUT double clausen(double x)
             dd = temp;
         }
         d = yy * d - dd + 0.5 * kC[0];
-        val = x * (d - nm::log(x));
+        val = x * (d - GSL_LOG(x));
     }
     return val * sgn;
 }
@@ -384,15 +394,15 @@ NUSI_FN void cseries(bool s2, double r, double lr, double x, double y, double& r
 // dilogc_series_3: |z| near 1, sum_{n <= 6} (log r)^n / n! H_n(theta)
 NUSI_FN void cseries_3(double r, double lr, double x, double y, double& re, double& im)
 {
-    const double theta = nm::atan2(y, x);
+    const double theta = GSL_ATAN2(y, x);
     const double cos_theta = x / r, sin_theta = y / r;
     const double a = lr;   // log(r)
     const double omc = 1.0 - cos_theta, omc2 = omc * omc;
     double H_re[7], H_im[7];
     H_re[0] = kPiD * kPiD / 6.0 + 0.25 * (theta * theta - 2.0 * kPiD * fabs(theta));
     H_im[0] = clausen(theta);
-    H_re[1] = -0.5 * nm::log(2.0 * omc);
-    H_im[1] = -nm::atan2(-sin_theta, omc);
+    H_re[1] = -0.5 * GSL_LOG(2.0 * omc);
+    H_im[1] = -GSL_ATAN2(-sin_theta, omc);
     H_re[2] = -0.5;
     H_im[2] = 0.5 * sin_theta / omc;
     H_re[3] = -0.5 / omc;
@@ -421,7 +431,7 @@ NUSI_FN void cseries_3(double r, double lr, double x, double y, double& re, doub
 NUSI_FN_OUT cd fundamental(double r, double x, double y, double& lr)
 {
     double re, im;
-    lr = nm::log(r);
+    lr = GSL_LOG(r);
     if (r > 0.98) {
         cseries_3(r, lr, x, y, re, im);
         return cd{re, im};
@@ -433,8 +443,8 @@ NUSI_FN_OUT cd fundamental(double r, double x, double y, double& lr)
     const double zr = 1.0 - x, zi = -y;
     const double ax = fabs(zr), ay = fabs(zi);
     const double mn = ax < ay ? ax : ay, mx = ax > ay ? ax : ay;
-    const double ln_r = nm::log(mx) + 0.5 * nm::log(1.0 + (mn / mx) * (mn / mx));
-    const double ln_t = nm::atan2(zi, zr);
+    const double ln_r = GSL_LOG(mx) + 0.5 * GSL_LOG(1.0 + (mn / mx) * (mn / mx));
+    const double ln_t = GSL_ATAN2(zi, zr);
     const double t_x = (ln_r * x + ln_t * y) / (r * r);
     const double t_y = (-ln_r * y + ln_t * x) / (r * r);
     const double r_x = (1.0 - x) * t_x + y * t_y;
@@ -452,8 +462,8 @@ NUSI_FN cd unitdisk(double x, double y)
     double lr;
     const cd f = fundamental(refl ? r_tmp : r, refl ? x_tmp : x, refl ? y_tmp : y, lr);   // one call site
     if (!refl) return f;
-    const double lnz = nm::log(r), lnomz = lr;   // log(r_tmp)
-    const double argz = nm::atan2(y, x), argomz = nm::atan2(y_tmp, x_tmp);
+    const double lnz = GSL_LOG(r), lnomz = lr;   // log(r_tmp)
+    const double argz = GSL_ATAN2(y, x), argomz = GSL_ATAN2(y_tmp, x_tmp);
     return cd{-f.r + zeta2 - lnz * lnomz + argz * argomz, -f.i - argz * lnomz - argomz * lnz};
 }
 
@@ -471,7 +481,7 @@ NUSI_FN double gsl_cli2_cost(double x, double y)
     const double fx = ux > 0.732 ? 1.0 - ux : ux, fy = uy;
     const double r = sqrt(fx * fx + fy * fy);
     if (r > 0.98) return 8.0;
-    const double n = 36.0 / -nm::log(r);
+    const double n = 36.0 / -GSL_LOG(r);
     return r > 0.25 ? 10.0 + n : n;
 }
 
@@ -485,7 +495,7 @@ NUSI_FN_OUT double gsl_li2(double x)
 
 // gsl_sf_complex_dilog_xy_e on the real axis (gsl_cli2's y == 0 branch, alone: a caller with real arguments keeps
 // the complex series' registers out of its own budget)
-NUSI_FN cd gsl_cli2_real(double x) { return cd{gsl_li2(x), (x >= 1.0) ? -gsl::kPiD * nm::log(x) : 0.0}; }
+NUSI_FN cd gsl_cli2_real(double x) { return cd{gsl_li2(x), (x >= 1.0) ? -gsl::kPiD * GSL_LOG(x) : 0.0}; }
 
 // gsl_sf_complex_dilog_xy_e: the real axis; |z| within eps of 1 (Lewin A.2.4.1 / A.2.4.2); the unit disk; 1/z
 // into the unit disk, unwound with Li2(z) + Li2(1/z) = -zeta2 - log(-z)^2 / 2
@@ -493,9 +503,9 @@ NUSI_FN_OUT cd gsl_cli2(double x, double y)
 {
     const double zeta2 = gsl::kPiD * gsl::kPiD / 6.0;
     const double r2 = x * x + y * y;
-    if (y == 0.0) return cd{gsl_li2(x), (x >= 1.0) ? -gsl::kPiD * nm::log(x) : 0.0};
+    if (y == 0.0) return cd{gsl_li2(x), (x >= 1.0) ? -gsl::kPiD * GSL_LOG(x) : 0.0};
     if (fabs(r2 - 1.0) < gsl::kEps) {
-        const double theta = nm::atan2(y, x);
+        const double theta = GSL_ATAN2(y, x);
         const double term1 = theta * theta / 4.0, term2 = gsl::kPiD * fabs(theta) / 2.0;
         return cd{zeta2 + term1 - term2, gsl::clausen(theta)};
     }
@@ -503,8 +513,8 @@ NUSI_FN_OUT cd gsl_cli2(double x, double y)
     const cd u = gsl::unitdisk(inv ? x / r2 : x, inv ? -y / r2 : y);   // one instance
     if (!inv) return u;
     const double r = sqrt(r2);
-    const double theta = nm::atan2(y, x), theta_abs = fabs(theta), theta_sgn = (theta < 0.0 ? -1.0 : 1.0);
-    const double ln_minusz_re = nm::log(r), ln_minusz_im = theta_sgn * (theta_abs - gsl::kPiD);
+    const double theta = GSL_ATAN2(y, x), theta_abs = fabs(theta), theta_sgn = (theta < 0.0 ? -1.0 : 1.0);
+    const double ln_minusz_re = GSL_LOG(r), ln_minusz_im = theta_sgn * (theta_abs - gsl::kPiD);
     const double lmz2_re = ln_minusz_re * ln_minusz_re - ln_minusz_im * ln_minusz_im;
     const double lmz2_im = 2.0 * ln_minusz_re * ln_minusz_im;
     return cd{-u.r - 0.5 * lmz2_re - zeta2, -u.i - 0.5 * lmz2_im};

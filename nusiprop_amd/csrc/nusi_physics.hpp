@@ -552,7 +552,7 @@ NUSI_FN void alpha_member_ref(double S, double t, double gr, double& Dcr, double
     const cd Dc = NUSI_REFO_STUB == 1 ? z : gsl_cli2(z.r, z.i);
     Dcr = Dc.r;
     Dci = Dc.i;
-    A = carg(-(C(-1 + S, gr) / dt));
+    A = carg_i(-(C(-1 + S, gr) / dt));   // (atan2 inline: k_alpha_mcorner's one transcendental outside gsl_cli2)
 }
 template <bool kRef = false>
 NUSI_FN void alpha_corner_member(double S, double t, double gr, AlphaCorner& c)
