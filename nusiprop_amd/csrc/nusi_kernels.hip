@@ -323,6 +323,8 @@ NUSI_BCOLD void b_corner(int j, const double* edgk, int ct, int cs, double* per,
     alpha_batch_corner_job<kRef>(j, edgk, ct, cs, per, tmp);
 #endif
 }
+// (kRef) A of a member corner, out of line: inline, its atan2 raised the point loop's spills 53 -> 85
+NUSI_BCOLD double b_marg(double S, double t, double gr) { return alpha_member_ref_arg(S, t, gr); }
 NUSI_BCOLD void b_xshared(int j, const double* edgk, int ct, int cs, double* X) { alpha_batch_xshared_job(j, edgk, ct, cs, X); }
 // The leaves the batch's shared brackets read (alpha_k_pre, alpha_k_pp): the shared corner blocks P3 | tmp, the
 // edge block edgk and the mixed logs; no member leaf
@@ -373,7 +375,7 @@ constexpr int kMcJobs = 1024;
 __global__ __launch_bounds__(256) void k_alpha_mcorner(const Point* __restrict__ pts, const int* __restrict__ batches,
                                                        MCornerDev mc, int pc0, int cb)
 {
-    __shared__ double v[3 * kMcJobs];   // [field][q][cl]
+    __shared__ double v[kMcFields * kMcJobs];   // [field][q][cl]
     const int bw = batches[blockIdx.y], k = blockIdx.z, tid = threadIdx.x;
     const int p0 = bw & 0xffffff, nb = (int)((unsigned)bw >> 24);
     const Point& P = pts[p0];
@@ -383,15 +385,15 @@ __global__ __launch_bounds__(256) void k_alpha_mcorner(const Point* __restrict__
     for (int j = tid; j < nj; j += 256) {
         const int cl = j / nb, q = j - cl * nb;
         if (c0 + cl >= mc.NC) break;
-        double Dcr, Dci, A;
-        alpha_mcorner_ref_job(P, pts[p0 + q], k, c0 + cl, mc.ue, Dcr, Dci, A);
+        double Dcr, Dci, A = 0.0;
+        alpha_mcorner_ref_job<kMcFields == 3>(P, pts[p0 + q], k, c0 + cl, mc.ue, Dcr, Dci, A);
         v[q * cb + cl] = Dcr;
         v[nj + q * cb + cl] = Dci;
-        v[2 * nj + q * cb + cl] = A;
+        if (kMcFields == 3) v[2 * nj + q * cb + cl] = A;
     }
     __syncthreads();
-    double* const o = mc.buf + (size_t)(p0 - pc0) * 9 * mc.NC + (size_t)k * 3 * nb * mc.NC;
-    for (int e = tid; e < 3 * nj; e += 256) {
+    double* const o = mc.buf + (size_t)(p0 - pc0) * 3 * kMcFields * mc.NC + (size_t)k * kMcFields * nb * mc.NC;
+    for (int e = tid; e < kMcFields * nj; e += 256) {
         const int fq = e / cb, cl = e - fq * cb;   // fq = field nb + q
         if (c0 + cl < mc.NC) o[(size_t)fq * mc.NC + c0 + cl] = v[e];
     }
@@ -525,7 +527,8 @@ void k_alpha_batch(GridDev g, const Point* __restrict__ pts, const SplineSet* __
         // (kRef) thread tid < cc carries corner tid's member leaves one point ahead, from k_alpha_mcorner's block:
         // the corner's numbering c (only corners with ut <= us are read by the entries n < m; the others stay unset)
         const size_t mstr = kRef ? (size_t)mc.NC * nb : 0;   // (uniform: the block's field stride and base)
-        const double* const mcb = kRef ? mc.buf + (size_t)(p0 - pc0) * 9 * mc.NC + (size_t)k * 3 * mstr : nullptr;
+        const double* const mcb =
+            kRef ? mc.buf + (size_t)(p0 - pc0) * 3 * kMcFields * mc.NC + (size_t)k * kMcFields * mstr : nullptr;
         int moff = -1;   // this thread's corner c, or -1 (point q's value at q NC + c)
         double mc0 = 0.0, mc1 = 0.0, mc2 = 0.0;
         if (kRef && cornered && tid < cc) {
@@ -533,7 +536,10 @@ void k_alpha_batch(GridDev g, const Point* __restrict__ pts, const SplineSet* __
             const int us = mc.eu[ssrc[si]], ut = mc.eu[tsrc[ti]];
             if (ut <= us) {
                 moff = us * (us + 1) / 2 + ut;
-                if (kRefPrefetch) { mc0 = mcb[moff]; mc1 = mcb[mstr + moff]; mc2 = mcb[2 * mstr + moff]; }
+                if (kRefPrefetch) {
+                    mc0 = mcb[moff]; mc1 = mcb[mstr + moff];
+                    if (kMcFields == 3) mc2 = mcb[2 * mstr + moff];
+                }
             }
         }
 #pragma unroll 1
@@ -574,11 +580,21 @@ void k_alpha_batch(GridDev g, const Point* __restrict__ pts, const SplineSet* __
                         if (kRef) {
                             if (moff >= 0) {
                                 const size_t o = (size_t)q * mc.NC + moff;
-                                if (!kRefPrefetch) { mc0 = mcb[o]; mc1 = mcb[mstr + o]; mc2 = mcb[2 * mstr + o]; }
-                                X[tid] = mc0; X[kCC + tid] = mc1; X[2 * kCC + tid] = mc2;
+                                if (!kRefPrefetch) {
+                                    mc0 = mcb[o]; mc1 = mcb[mstr + o];
+                                    if (kMcFields == 3) mc2 = mcb[2 * mstr + o];
+                                }
+                                X[tid] = mc0; X[kCC + tid] = mc1;
+                                if (kMcFields == 3) X[2 * kCC + tid] = mc2;
+                                else {   // A of the corner for point q: alpha_member_ref's expression on the tile's S', t
+                                    const int si = tid / ct, ti = tid - si * ct;
+                                    X[2 * kCC + tid] = b_marg(edgk[kTEdgeFields * ct + kSEdgeVal * cs + si],
+                                                              edgk[kTEdgeVal * ct + ti], Q.a_gr);
+                                }
                                 if (kRefPrefetch && q + 1 < nb) {
                                     const size_t o1 = o + mc.NC;
-                                    mc0 = mcb[o1]; mc1 = mcb[mstr + o1]; mc2 = mcb[2 * mstr + o1];
+                                    mc0 = mcb[o1]; mc1 = mcb[mstr + o1];
+                                    if (kMcFields == 3) mc2 = mcb[2 * mstr + o1];
                                 }
                             }
                         }

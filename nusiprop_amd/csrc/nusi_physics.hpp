@@ -544,15 +544,22 @@ NUSI_FN void alpha_member_corner(const MemberShared& M, double S, double t, doub
 #ifndef NUSI_REFO_STUB   // timing A/B only: 1 = the member corners without the dilogarithm (Dc = z), 2 = nothing
 #define NUSI_REFO_STUB 0
 #endif
+NUSI_FN cd alpha_member_ref_dc(double S, double t, double gr)
+{
+    const cd z = (1 + S + t) / C(2 + t, -gr);
+    return NUSI_REFO_STUB == 1 ? z : gsl_cli2(z.r, z.i);
+}
+NUSI_FN double alpha_member_ref_arg(double S, double t, double gr)
+{
+    return carg_i(-(C(-1 + S, gr) / C(2 + t, -gr)));   // (atan2 inline)
+}
 NUSI_FN void alpha_member_ref(double S, double t, double gr, double& Dcr, double& Dci, double& A)
 {
     if (NUSI_REFO_STUB == 2) { Dcr = Dci = A = 0.0; return; }
-    const cd dt = C(2 + t, -gr);
-    const cd z = (1 + S + t) / dt;
-    const cd Dc = NUSI_REFO_STUB == 1 ? z : gsl_cli2(z.r, z.i);
+    const cd Dc = alpha_member_ref_dc(S, t, gr);
     Dcr = Dc.r;
     Dci = Dc.i;
-    A = carg_i(-(C(-1 + S, gr) / dt));   // (atan2 inline: k_alpha_mcorner's one transcendental outside gsl_cli2)
+    A = alpha_member_ref_arg(S, t, gr);
 }
 template <bool kRef = false>
 NUSI_FN void alpha_corner_member(double S, double t, double gr, AlphaCorner& c)
@@ -1112,6 +1119,7 @@ NUSI_FN void alpha_batch_mcorner_job(const Point& P, int j, const double* edgk, 
 // mass state k for point Q of a batch whose first point is P (m_phi and the masses), in the reference's operation
 // order (alpha_member_ref); S and t by the functions the tile's edge block uses (alpha_tile_edge_job_k), so the values
 // are those the batch kernel's own corners would take
+template <bool kWithA>
 NUSI_FN void alpha_mcorner_ref_job(const Point& P, const Point& Q, int k, long long c, const double* ue, double& Dcr,
                                    double& Dci, double& A)
 {
@@ -1120,7 +1128,14 @@ NUSI_FN void alpha_mcorner_ref_job(const Point& P, const Point& Q, int k, long l
     while ((long long)(us + 1) * (us + 2) / 2 <= c) ++us;
     const int ut = (int)(c - (long long)us * (us + 1) / 2);
     const double m2 = P.mphi * P.mphi, mk = P.mn[k];
-    alpha_member_ref(alpha_S(mk, ue[us], m2), alpha_t(mk, ue[ut], m2), Q.a_gr, Dcr, Dci, A);
+    const double S = alpha_S(mk, ue[us], m2), t = alpha_t(mk, ue[ut], m2);
+    if (kWithA) {
+        alpha_member_ref(S, t, Q.a_gr, Dcr, Dci, A);
+    } else {
+        const cd Dc = NUSI_REFO_STUB == 2 ? C(0.0) : alpha_member_ref_dc(S, t, Q.a_gr);
+        Dcr = Dc.r;
+        Dci = Dc.i;
+    }
 }
 // xlog / ylog leaves of mass state k into xl [cs][kAlphaTile], yl [kAlphaTile][ct] (alpha_tile_mixed_job's jobs)
 NUSI_FN void alpha_batch_mixed_job(int j, const double* edgk, int ct, int cs, const int* tl, const int* th,
