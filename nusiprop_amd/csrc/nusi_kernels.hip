@@ -32,23 +32,49 @@ __device__ __attribute__((noinline)) void warn_entry(int* warn, int* wmin, int T
 #ifndef NUSI_GA_WAVES   // Gamma / alphaTilde kernel waves per SIMD (A/B)
 #define NUSI_GA_WAVES 4   // with Gamma / alphaTilde split over work-items: 4 0.525, 3 0.535 ms (was 0.572 unsplit at 3)
 #endif
-// kRef: NUSI_OPT_REFERENCE_ORDER (the general complex dilogarithm, gamma_entry / alphat_entry)
+// Gamma and alphaTilde: grid (T / 64, points, 2 quantities), three waves per workgroup -- wave k runs mass state k
+// of 64 bins (gamma_k / alphat_k), its channel terms go to LDS, and wave 0 sums them in the reference's order
+// (state after state, channel after channel: gamma_entry's additions, the same bits).  Three times the waves of one
+// work-item per entry, each a third as long: the kernel is latency-bound (a one-point plan's 12 waves, the GSL
+// dilogarithms' divergent series in the reference order).  kRef: NUSI_OPT_REFERENCE_ORDER.
+constexpr int kGaTerms = 7;   // channel terms per mass state (alphat_k: s, t, u, t-u, s-t, s-u, phi-phi)
+struct LdsSink {
+    double* v;   // this lane's column of [kGaTerms][64]
+    int n;
+    NUSI_FN void add(double x) { v[n * 64] = x; ++n; }
+};
 template <bool kRef>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NUSI_GA_WAVES, NUSI_GA_WAVES))) void k_gamma_alphat(GridDev g, const Point* __restrict__ pts, const SplineSet* __restrict__ splp,
+__global__ __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(NUSI_GA_WAVES, NUSI_GA_WAVES))) void k_gamma_alphat(GridDev g, const Point* __restrict__ pts, const SplineSet* __restrict__ splp,
                                                      double* __restrict__ G, double* __restrict__ At,
                                                      int* __restrict__ warn, int* __restrict__ wmin)
 {
+    __shared__ double v[3][kGaTerms][64];
+    __shared__ int cnt[3][64], wk[3][64];
     const SplineSet& spl = *splp;   // (in global memory: a by-value copy would live in scratch)
+    const int lane = threadIdx.x & 63;
+    const int k = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int p = blockIdx.y;
-    const int n = blockIdx.x * 64 + threadIdx.x;
-    if (n >= g.T) return;
+    const int n = blockIdx.x * 64 + lane;
+    const bool act = n < g.T;
     const Point& P = pts[p];
+    if (act) {
+        int w = 0;
+        LdsSink sk{&v[k][0][lane], 0};
+        const double lo = g.lo[n], hi = g.hi[n];
+        if (blockIdx.z == 0) gamma_k<kRef>(P, k, lo, hi, sk, w);
+        else alphat_k<kRef>(P, spl, k, lo, hi, sk, w);
+        cnt[k][lane] = sk.n;
+        wk[k][lane] = w;
+    }
+    __syncthreads();
+    if (k != 0 || !act) return;
+    SumSink tot;
     int w = 0;
-    const double lo = g.lo[n], hi = g.hi[n];
-    if (blockIdx.z == 0)   // Gamma and alphaTilde of an entry on separate work-items: twice the waves
-        G[(size_t)p * g.T + n] = gamma_entry<kRef>(P, lo, hi, w);
-    else
-        At[(size_t)p * g.T + n] = alphat_entry<kRef>(P, spl, lo, hi, w);
+    for (int kk = 0; kk < 3; ++kk) {
+        for (int i = 0; i < cnt[kk][lane]; ++i) tot.add(v[kk][i][lane]);
+        w |= wk[kk][lane];
+    }
+    (blockIdx.z == 0 ? G : At)[(size_t)p * g.T + n] = tot.tot;
     if (w) warn_entry(warn, wmin, g.T, p, w, n, n);
 }
 
@@ -114,8 +140,8 @@ hipError_t launch_gamma_alphat(const GridDev& g, const Point* pts, int npts, con
                                int* warn, hipStream_t s, bool ref)
 {
     dim3 grid((g.T + 63) / 64, npts, 2);
-    if (ref) hipLaunchKernelGGL(k_gamma_alphat<true>, grid, dim3(64), 0, s, g, pts, spl, t.G, t.At, warn, t.Wmin);
-    else hipLaunchKernelGGL(k_gamma_alphat<false>, grid, dim3(64), 0, s, g, pts, spl, t.G, t.At, warn, t.Wmin);
+    if (ref) hipLaunchKernelGGL(k_gamma_alphat<true>, grid, dim3(192), 0, s, g, pts, spl, t.G, t.At, warn, t.Wmin);
+    else hipLaunchKernelGGL(k_gamma_alphat<false>, grid, dim3(192), 0, s, g, pts, spl, t.G, t.At, warn, t.Wmin);
     return hipGetLastError();
 }
 

@@ -181,15 +181,22 @@ NUSI_FN double gpp_analytic(double a, double b)  // nuSIprop.hpp:885 with a = ma
 // ---------------------------------------------------------------------------
 // Gamma(Em, Ep)  -- nuSIprop.hpp:759-922
 // ---------------------------------------------------------------------------
-template <bool kRef = false>   // kRef: NUSI_OPT_REFERENCE_ORDER (GSL's dilogarithms, nusi_gsl.hpp)
-NUSI_FN double gamma_entry(const Point& P, double Em, double Ep, int& warn)
+// The entries sum their channels' terms over the mass states into one accumulator, in the reference's order
+// (channel by channel within a state, state after state).  The per-state bodies (gamma_k, alphat_k) hand each term
+// wgt * X to a sink: SumSink accumulates as the reference does (gamma_entry, alphat_entry: the per-entry paths and the
+// host checks); k_gamma_alphat runs the three states on three waves, stores their terms and sums them on one in the
+// same order -- the same additions of the same values, so the same bits.
+struct SumSink {
+    double tot = 0;
+    NUSI_FN void add(double x) { tot += x; }
+};
+template <bool kRef, class Sink>   // kRef: NUSI_OPT_REFERENCE_ORDER (GSL's dilogarithms, nusi_gsl.hpp)
+NUSI_FN void gamma_k(const Point& P, int j, double Em, double Ep, Sink& tot, int& warn)
 {
     const double g = P.g, mphi = P.mphi, Ga = P.Ga;
     const double g4 = (g * g) * (g * g), m2 = mphi * mphi;
     const double gr = Ga / mphi, gr2 = gr * gr;
-    double tot = 0;
-    NUSI_MASS_LOOP
-    for (int j = 0; j < 3; ++j) {
+    {
         const double mj = P.mn[j], uj = P.u[j];
         const double sp = 2 * mj * Ep / m2, sm = 2 * mj * Em / m2;
         const double cs = m2 / (m2 + Ga * Ga);
@@ -202,21 +209,21 @@ NUSI_FN double gamma_entry(const Point& P, double Em, double Ep, int& warn)
             Gs = g4 / (32 * kPi * m2 * Ga) * (2 * mphi * atandiff(mphi * (sp - 1) / Ga, mphi * (sm - 1) / Ga) + lg);
         Gs *= uj;
         const double wgt = m2 / (2 * mj);
-        tot += wgt * Gs;
-        if (!P.non_resonant) continue;
+        tot.add(wgt * Gs);
+        if (!P.non_resonant) return;
 
         const double L1p = nm::log1p(sp), L1m = nm::log1p(sm);
         double Gtu0 = g4 / (16 * kPi * m2) * (2 * L1p / sp - 2 * L1m / sm + L1p - L1m);
         if (Gtu0 < 0) Gtu0 = g4 / (16 * kPi * m2) * (sp - sm) / 2. * gl3_Gtu_nores(sm, sp);
         Gtu0 *= 2 * uj;
-        tot += wgt * Gtu0;
+        tot.add(wgt * Gtu0);
 
         double Gint = g4 / (32 * kPi * m2 * sm * sp) *
                       (sm * L1p * (2 + 2 * sp + sp * nm::log(2 + sp)) - sp * L1m * (2 + 2 * sm + sm * nm::log(2 + sm))
                        + sm * sp * (dilog1mdiff<kRef>(sp, sm) + dilogdiff<kRef>(sp, sm)));
         if (Gint < 0) Gint = g4 / (16 * kPi * m2) * (sp - sm) / 2. * gl3_Gtu_int(sm, sp);
         Gint *= P.majorana ? uj : 0.5 * uj;
-        tot += wgt * Gint;
+        tot.add(wgt * Gint);
 
         // s-t interference
         const cd den = C(gr, 2.0);                    // 2*I + gr
@@ -236,9 +243,9 @@ NUSI_FN double gamma_entry(const Point& P, double Em, double Ep, int& warn)
                      (d1.r + d2.r + gr * (d2.i - d1.i) + 2 * gr * carg(1.0 - z2p) * L1p - 2 * gr * carg(1.0 - z2m) * L1m
                       + nm::log1p(4 / gr2) * (L1m - L1p) + Lgp * L1p - Lgm * L1m + (1 + gr2) * (Lgm - Lgp) + 2 * dilogdiff<kRef>(sp, sm));
         Gst *= uj;
-        tot += wgt * Gst;
+        tot.add(wgt * Gst);
         const double Gsu = P.majorana ? Gst : 0;
-        tot += wgt * Gsu;
+        tot.add(wgt * Gsu);
 
         double Gpp = 0;
         if (sp > 4 && P.phiphi) {
@@ -248,25 +255,30 @@ NUSI_FN double gamma_entry(const Point& P, double Em, double Ep, int& warn)
             Gpp *= uj;
             if (P.majorana) Gpp *= 2;
         }
-        tot += wgt * Gpp;
+        tot.add(wgt * Gpp);
         if (Gs < 0 || Gtu0 < 0 || Gint < 0 || (Gs + Gtu0 + Gst + Gsu) < 0) warn |= kWarnGamma;
     }
-    return tot;
+}
+template <bool kRef = false>
+NUSI_FN double gamma_entry(const Point& P, double Em, double Ep, int& warn)
+{
+    SumSink tot;
+    NUSI_MASS_LOOP
+    for (int j = 0; j < 3; ++j) gamma_k<kRef>(P, j, Em, Ep, tot, warn);
+    return tot.tot;
 }
 
 // ---------------------------------------------------------------------------
 // alphaTilde(Em, Ep)  -- nuSIprop.hpp:924-1235
 // ---------------------------------------------------------------------------
-template <bool kRef = false>   // kRef: NUSI_OPT_REFERENCE_ORDER (GSL's dilogarithms, nusi_gsl.hpp)
-NUSI_FN double alphat_entry(const Point& P, const SplineSet& spl, double Em, double Ep, int& warn)
+template <bool kRef, class Sink>   // kRef: NUSI_OPT_REFERENCE_ORDER (GSL's dilogarithms, nusi_gsl.hpp)
+NUSI_FN void alphat_k(const Point& P, const SplineSet& spl, int k, double Em, double Ep, Sink& tot, int& warn)
 {
     const double g = P.g, mphi = P.mphi, Ga = P.Ga;
     const double g4 = (g * g) * (g * g), m2 = mphi * mphi, m4 = (mphi * mphi) * (mphi * mphi);
     const double gr = Ga / mphi, gr2 = gr * gr;
     const bool maj = P.majorana;
-    double tot = 0;
-    NUSI_MASS_LOOP
-    for (int k = 0; k < 3; ++k) {
+    {
         const double mk = P.mn[k], uk = P.u[k];
         double tp = -2 * mk * Ep / m2, tm = -2 * mk * Em / m2;
         if (fabs(tm + 1) < 1e-7) tm += tm * 1e-6;
@@ -283,8 +295,8 @@ NUSI_FN double alphat_entry(const Point& P, const SplineSet& spl, double Em, dou
             as = g4 / (16 * kPi * Ga * m4) * (2 * mphi * (1 + tm) * atandiff(mphi * (1 + tm) / Ga, mphi * (1 + tp) / Ga) + lg);
         as *= uk;
         if (!maj) as /= 2.;
-        tot += wgt * as;
-        if (!P.non_resonant) continue;
+        tot.add(wgt * as);
+        if (!P.non_resonant) return;
 
         const double Lmt = nm::log1p(-tm), Lmp = nm::log1p(-tp), Ld = nm::log1p(tm - tp);
         const double brk = (-2 + tm) * (tm - tp) - (-1 + tm) * (-2 + tp) * (Lmt - Lmp);
@@ -299,7 +311,7 @@ NUSI_FN double alphat_entry(const Point& P, const SplineSet& spl, double Em, dou
             if (at < 0) at = gl33_tri(1, tp, tm) * (3. / 2. * g4 / (32 * kPi * m4));
         }
         at *= uk;
-        tot += wgt * at;
+        tot.add(wgt * at);
 
         double au;
         if (maj) au = at;
@@ -308,7 +320,7 @@ NUSI_FN double alphat_entry(const Point& P, const SplineSet& spl, double Em, dou
             if (au < 0) au = gl33_tri(1, tp, tm) * (1. / 2. * g4 / (32 * kPi * m4));
             au *= uk;
         }
-        tot += wgt * au;
+        tot.add(wgt * au);
 
         double atu = 0;
         if (maj) {
@@ -338,7 +350,7 @@ NUSI_FN double alphat_entry(const Point& P, const SplineSet& spl, double Em, dou
             if (atu < 0) atu = gl33_tri(2, tp, tm) * (g4 / (16 * kPi * m4));
         }
         atu *= uk;
-        tot += wgt * atu;
+        tot.add(wgt * atu);
 
         // s-t interference
         const cd den = C(gr, 2.0);                  // 2*I + gr
@@ -386,9 +398,9 @@ NUSI_FN double alphat_entry(const Point& P, const SplineSet& spl, double Em, dou
                    + 2 * tm * nm::log(tm / tp) + 2 * Lmp * nm::log(-tp) + (Lmp - Lmt) * (nm::log(4 + gr2) - 2 * nm::log(gr) - Lgp)
                    + (1 + tm + gr2) * (Lgp - Lgm));
         ast *= uk;
-        tot += wgt * ast;
+        tot.add(wgt * ast);
         const double asu = maj ? ast : 0;
-        tot += wgt * asu;
+        tot.add(wgt * asu);
 
         double app = 0;
         if (-tp > 4 && P.phiphi) {
@@ -408,13 +420,20 @@ NUSI_FN double alphat_entry(const Point& P, const SplineSet& spl, double Em, dou
             app *= 2;
             if (maj) app *= 2;
         }
-        tot += wgt * app;
+        tot.add(wgt * app);
 
         const double nrm = P.a_nrm;
         if (as < 0 || at < 0 || au < 0 || atu / nrm < -1e-11 || (ast + at + as) / nrm < -1e-11 || (asu + au + as) / nrm < -1e-11)
             warn |= kWarnAlphaTilde;
     }
-    return tot;
+}
+template <bool kRef = false>
+NUSI_FN double alphat_entry(const Point& P, const SplineSet& spl, double Em, double Ep, int& warn)
+{
+    SumSink tot;
+    NUSI_MASS_LOOP
+    for (int k = 0; k < 3; ++k) alphat_k<kRef>(P, spl, k, Em, Ep, tot, warn);
+    return tot.tot;
 }
 
 // ---------------------------------------------------------------------------
