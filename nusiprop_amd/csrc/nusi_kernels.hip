@@ -770,7 +770,7 @@ static hipError_t launch_alpha_t(const GridDev& g, const Point* pts, int npts, c
 {
     t_alpha_kernel = kRef ? "k_alpha_tile[refo]" : "k_alpha_tile";
     if (kernel == 0 && batches) {
-        t_alpha_kernel = kRef ? "k_alpha_batch[refo]" : "k_alpha_batch";
+        t_alpha_kernel = kRef ? "k_alpha_mcorner + k_alpha_batch[refo]" : "k_alpha_batch";
         // class 0 on the big-batch kernel (batches of up to gmax tables), classes 1 / 2 per table
         if (at.ext_lo < g.T) {
             const long long L = g.T - at.ext_lo, ne = L * (L - 1) / 2;

@@ -74,7 +74,7 @@ def test_reference_order_small_cases(nusi, oracle_mod, name):
     bit-exact to the reference-order oracle, the warnings equal, the fluxes to FLUX_RTOL."""
     kw = cases.SMALL_CASES[name]
     o = oracle_mod.Oracle(**cases.oracle_kwargs(kw))
-    for kernel, label in ((None, "k_alpha_batch[refo]"), (1, "k_alpha_tile[refo]"), (2, "k_alpha[refo]")):
+    for kernel, label in ((None, "k_alpha_mcorner + k_alpha_batch[refo]"), (1, "k_alpha_tile[refo]"), (2, "k_alpha[refo]")):
         flux, fla, tabs, names, warn = _gpu_refo(nusi, [kw], kernel=kernel)
         assert names[0] == label
         with oracle_mod.reference_order(1):
@@ -107,7 +107,7 @@ def test_reference_order_c4_subset_bitexact(nusi, oracle_mod):
     pick = sorted(rng.choice(len(pts), 8, replace=False))
     sel = [pts[i] for i in pick] + [dict(pts[pick[0]], g=pts[pick[0]]["g"] * 1.7)]   # a batch of two
     flux, fla, tabs, names, _ = _gpu_refo(nusi, sel)
-    assert names[0] == "k_alpha_batch[refo]"
+    assert names[0] == "k_alpha_mcorner + k_alpha_batch[refo]"
     for k, kw in enumerate(sel):
         o = oracle_mod.Oracle(**cases.oracle_kwargs(kw))
         with oracle_mod.reference_order(1):
@@ -124,7 +124,7 @@ def test_reference_order_c4_full_grid(nusi, oracle_mod):
     g -> 1 (the conditioning of the s-t interference closed forms)."""
     pts = cases.scan_points()
     flux, fla, _, names, _ = _gpu_refo(nusi, pts, tables=False)
-    assert names[0] == "k_alpha_batch[refo]"
+    assert names[0] == "k_alpha_mcorner + k_alpha_batch[refo]"
     f_ref, fla_ref = oracle_mod.evolve_many(pts, level=1)
     errs = np.array([max(cases.rel_err(flux[k], f_ref[k]), cases.rel_err(fla[k], fla_ref[k])) for k in range(len(pts))])
     assert np.all(errs <= FLUX_RTOL), (int(np.argmax(errs)), float(errs.max()))
@@ -183,7 +183,7 @@ def test_reference_order_object_api(nusi, oracle_mod):
             _lib.check(L.nusi_get_flux_fla(hh, out.ctypes.data_as(ctypes.POINTER(ctypes.c_double))))
             a, c = ctypes.c_char_p(), ctypes.c_char_p()
             _lib.check(L.nusi_get_kernels(hh, ctypes.byref(a), ctypes.byref(c)))
-            assert a.value == b"k_alpha_batch[refo]"
+            assert a.value == b"k_alpha_mcorner + k_alpha_batch[refo]"
             outs.append(out.reshape(3, 300))
     finally:
         L.nusi_destroy(h)
