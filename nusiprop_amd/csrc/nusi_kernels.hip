@@ -402,20 +402,23 @@ __global__ __launch_bounds__(256) void k_alpha_mcorner(const Point* __restrict__
                                                        MCornerDev mc, int pc0, int cb)
 {
     __shared__ double v[kMcFields * kMcJobs];   // [field][q][cl]
+    __shared__ double cst[2][kMcJobs];           // S', t of corner c0 + cl (shared by the batch's tables)
     const int bw = batches[blockIdx.y], k = blockIdx.z, tid = threadIdx.x;
     const int p0 = bw & 0xffffff, nb = (int)((unsigned)bw >> 24);
     const Point& P = pts[p0];
     if (!(P.non_resonant && P.majorana)) return;   // (no member corners)
     const long long c0 = (long long)blockIdx.x * cb;
     const int nj = cb * nb;   // <= kMcJobs
+    for (int cl = tid; cl < cb && c0 + cl < mc.NC; cl += 256) alpha_mcorner_st(P, k, c0 + cl, mc.ue, cst[0][cl], cst[1][cl]);
+    __syncthreads();
     for (int j = tid; j < nj; j += 256) {
         const int cl = j / nb, q = j - cl * nb;
         if (c0 + cl >= mc.NC) break;
-        double Dcr, Dci, A = 0.0;
-        alpha_mcorner_ref_job<kMcFields == 3>(P, pts[p0 + q], k, c0 + cl, mc.ue, Dcr, Dci, A);
-        v[q * cb + cl] = Dcr;
-        v[nj + q * cb + cl] = Dci;
-        if (kMcFields == 3) v[2 * nj + q * cb + cl] = A;
+        const double S = cst[0][cl], t = cst[1][cl], gr = pts[p0 + q].a_gr;
+        const cd Dc = NUSI_REFO_STUB == 2 ? C(0.0) : alpha_member_ref_dc(S, t, gr);
+        v[q * cb + cl] = Dc.r;
+        v[nj + q * cb + cl] = Dc.i;
+        if (kMcFields == 3) v[2 * nj + q * cb + cl] = alpha_member_ref_arg(S, t, gr);
     }
     __syncthreads();
     double* const o = mc.buf + (size_t)(p0 - pc0) * 3 * kMcFields * mc.NC + (size_t)k * kMcFields * nb * mc.NC;

@@ -1134,27 +1134,19 @@ NUSI_FN void alpha_batch_mcorner_job(const Point& P, int j, const double* edgk, 
                         ext[4 * ct + si], ext[4 * ct + cs + si], Dcr, Dci, A);
     mem[j] = Dcr; mem[kCC + j] = Dci;   // (A: SplitLeaves forms it from the edge arguments)
 }
-// NUSI_OPT_REFERENCE_ORDER: member corner c = us (us + 1) / 2 + ut (S' edge us, t edge ut <= us, energies ue[]) of
-// mass state k for point Q of a batch whose first point is P (m_phi and the masses), in the reference's operation
-// order (alpha_member_ref); S and t by the functions the tile's edge block uses (alpha_tile_edge_job_k), so the values
-// are those the batch kernel's own corners would take
-template <bool kWithA>
-NUSI_FN void alpha_mcorner_ref_job(const Point& P, const Point& Q, int k, long long c, const double* ue, double& Dcr,
-                                   double& Dci, double& A)
+// NUSI_OPT_REFERENCE_ORDER: the S' and t of member corner c = us (us + 1) / 2 + ut (S' edge us, t edge ut <= us,
+// energies ue[]) of mass state k for the tables of a batch whose first point is P (m_phi and the masses), by the
+// functions the tile's edge block uses (alpha_tile_edge_job_k), so the values are those the batch kernel's own
+// corners take; the member leaves are then alpha_member_ref_dc / _arg of (S', t, gr)
+NUSI_FN void alpha_mcorner_st(const Point& P, int k, long long c, const double* ue, double& S, double& t)
 {
     int us = (int)((sqrt(8.0 * (double)c + 1.0) - 1.0) * 0.5);
     while ((long long)us * (us + 1) / 2 > c) --us;
     while ((long long)(us + 1) * (us + 2) / 2 <= c) ++us;
     const int ut = (int)(c - (long long)us * (us + 1) / 2);
     const double m2 = P.mphi * P.mphi, mk = P.mn[k];
-    const double S = alpha_S(mk, ue[us], m2), t = alpha_t(mk, ue[ut], m2);
-    if (kWithA) {
-        alpha_member_ref(S, t, Q.a_gr, Dcr, Dci, A);
-    } else {
-        const cd Dc = NUSI_REFO_STUB == 2 ? C(0.0) : alpha_member_ref_dc(S, t, Q.a_gr);
-        Dcr = Dc.r;
-        Dci = Dc.i;
-    }
+    S = alpha_S(mk, ue[us], m2);
+    t = alpha_t(mk, ue[ut], m2);
 }
 // xlog / ylog leaves of mass state k into xl [cs][kAlphaTile], yl [kAlphaTile][ct] (alpha_tile_mixed_job's jobs)
 NUSI_FN void alpha_batch_mixed_job(int j, const double* edgk, int ct, int cs, const int* tl, const int* th,
