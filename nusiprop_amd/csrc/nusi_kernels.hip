@@ -391,15 +391,16 @@ __global__ __launch_bounds__(256) void k_alpha_medge(GridDev g, const Point* __r
 }
 
 // NUSI_OPT_REFERENCE_ORDER: the member corners of every table of the batches [0, gridDim.y) -> mc (MCornerDev's
-// layout); grid (NC / cb, batches, 3 mass states), cb = kMcJobs / (the chunk's largest batch).  A workgroup takes
-// corners [c0, c0 + cb) of its batch's nb tables: job j (4 per work-item) is corner c0 + j / nb of table q = j % nb,
+// layout); grid (NC / cb, batches, 3 mass states), cb = jobs / nb corners of a batch of nb tables per workgroup (the grid
+// sized for the chunk's largest batch).  A workgroup takes corners [c0, c0 + cb): job j (up to 4 per work-item) is
+// corner c0 + j / nb of table q = j % nb,
 // so a wavefront's lanes hold the batch's tables at a few neighbouring corners, whose quotients -- differing in gr
 // only -- take similar GSL branches and series lengths (in the tile's corner order the lanes of a wave diverge: 0.21
 // ns per call against 0.06, scripts/dev/gsl_bench.hip).  The values pass through LDS to leave as runs of cb corners
 // per (field, table), the layout the batch kernel reads a tile's corner rows from.
 constexpr int kMcJobs = 1024;
 __global__ __launch_bounds__(256) void k_alpha_mcorner(const Point* __restrict__ pts, const int* __restrict__ batches,
-                                                       MCornerDev mc, int pc0, int cb)
+                                                       MCornerDev mc, int pc0, int jobs)
 {
     __shared__ double v[kMcFields * kMcJobs];   // [field][q][cl]
     __shared__ double cst[2][kMcJobs];           // S', t of corner c0 + cl (shared by the batch's tables)
@@ -407,8 +408,10 @@ __global__ __launch_bounds__(256) void k_alpha_mcorner(const Point* __restrict__
     const int p0 = bw & 0xffffff, nb = (int)((unsigned)bw >> 24);
     const Point& P = pts[p0];
     if (!(P.non_resonant && P.majorana)) return;   // (no member corners)
+    const int cb = jobs / nb;   // this batch's corners per workgroup (jobs <= kMcJobs)
     const long long c0 = (long long)blockIdx.x * cb;
-    const int nj = cb * nb;   // <= kMcJobs
+    if (c0 >= mc.NC) return;   // (the grid is sized for the chunk's largest batch)
+    const int nj = cb * nb;
     for (int cl = tid; cl < cb && c0 + cl < mc.NC; cl += 256) alpha_mcorner_st(P, k, c0 + cl, mc.ue, cst[0][cl], cst[1][cl]);
     __syncthreads();
     for (int j = tid; j < nj; j += 256) {
@@ -815,9 +818,13 @@ static hipError_t launch_alpha_t(const GridDev& g, const Point* pts, int npts, c
                             ++e;
                         }
                         if (ntb > mc->cap_tables) return hipErrorInvalidValue;
-                        const int cb = kMcJobs / nbmax;
-                        hipLaunchKernelGGL(k_alpha_mcorner, dim3((unsigned)((mc->NC + cb - 1) / cb), e - b, 3), dim3(256),
-                                           0, s, pts, batches + b, *mc, pc0, cb);
+                        // jobs per workgroup: 4 per work-item on scans, 1 when the chunk is too small to fill ~2048
+                        // workgroups (a single propagation: one GSL call per work-item, not four in a row)
+                        const long long tot = mc->NC * 3 * ntb;
+                        const int jobs = 256 * (int)std::max(1LL, std::min<long long>(kMcJobs / 256, tot / (2048 * 256)));
+                        const int cbmin = jobs / nbmax;
+                        hipLaunchKernelGGL(k_alpha_mcorner, dim3((unsigned)((mc->NC + cbmin - 1) / cbmin), e - b, 3),
+                                           dim3(256), 0, s, pts, batches + b, *mc, pc0, jobs);
                         if (b < nb_plain)
                             hipLaunchKernelGGL((k_alpha_batch<false, true>), dim3(at.ncls[0], e - b), dim3(kTileThreads),
                                                lds, s, g, pts, spl, at.tiles, batches + b, t.A, t.Med, warn, t.Wmin, *mc,
