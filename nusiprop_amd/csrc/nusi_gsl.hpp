@@ -455,13 +455,16 @@ NUSI_FN_OUT cd fundamental(double r, double x, double y, double& lr)
 NUSI_FN cd unitdisk(double x, double y)
 {
     const double zeta2 = kPiD * kPiD / 6.0;
-    const double r = gsl::hypot(x, y);
     const bool refl = x > 0.732;
     const double x_tmp = 1.0 - x, y_tmp = -y;
-    const double r_tmp = refl ? gsl::hypot(x_tmp, y_tmp) : r;
+    // the fundamental region's argument and its modulus: one hypot call site (GSL forms |z| and, reflected,
+    // |1 - z|); |z| of a reflected argument after the call
+    const double fx = refl ? x_tmp : x, fy = refl ? y_tmp : y;
+    const double rf = gsl::hypot(fx, fy);
     double lr;
-    const cd f = fundamental(refl ? r_tmp : r, refl ? x_tmp : x, refl ? y_tmp : y, lr);   // one call site
+    const cd f = fundamental(rf, fx, fy, lr);   // one call site
     if (!refl) return f;
+    const double r = gsl::hypot(x, y);
     const double lnz = GSL_LOG(r), lnomz = lr;   // log(r_tmp)
     const double argz = GSL_ATAN2(y, x), argomz = GSL_ATAN2(y_tmp, x_tmp);
     return cd{-f.r + zeta2 - lnz * lnomz + argz * argomz, -f.i - argz * lnomz - argomz * lnz};
