@@ -1367,6 +1367,57 @@ int nusi_evolve_batch(int device, const nusi_params* pts, int n, double* flux, d
 // ---------------------------------------------------------------------------
 // object API
 // ---------------------------------------------------------------------------
+// One-point plans of destroyed objects are kept for the next object on the same device and grid (the reference
+// builds a calculate_flux per parameter point in its own usage, test.py: a fresh plan costs ~a dozen device
+// allocations, a stream and the grid upload).  A plan is handed out with the options at their defaults and no
+// phi-phi tables; its buffers are overwritten by the next evolve.  At most kPlanPoolMax are kept; the pool is never
+// torn down (process exit reclaims the device).
+namespace {
+constexpr size_t kPlanPoolMax = 8;
+struct PlanPool {
+    std::mutex mu;
+    std::vector<nusi_plan*> free;
+};
+PlanPool& plan_pool()
+{
+    static PlanPool* p = new PlanPool;
+    return *p;
+}
+nusi_plan* pool_take(int dev, int N, double lEmin, double lEmax, double zmax)
+{
+    PlanPool& pp = plan_pool();
+    std::lock_guard<std::mutex> lock(pp.mu);
+    for (size_t i = 0; i < pp.free.size(); ++i) {
+        nusi_plan* pl = pp.free[i];
+        const HostGrid& G = pl->grid;
+        if (pl->device == dev && G.N == N && G.lEmin == lEmin && G.lEmax == lEmax && G.zmax_in == zmax) {
+            pp.free.erase(pp.free.begin() + (long)i);
+            return pl;
+        }
+    }
+    return nullptr;
+}
+void pool_give(nusi_plan* pl)
+{
+    if (!pl) return;
+    if (pl->max_points == 1 && !pl->shift) {
+        // the defaults of nusi_plan_create
+        pl->alpha_batch = pl->alpha_kind = pl->cascade_rhs = pl->step_passes = pl->shift_max = 0;
+        pl->ref_order = pl->cascade_sync = pl->corner_mb = 0;
+        pl->cascade_kind = NUSI_CASCADE_AUTO;
+        pl->prof_max = pl->prof_n = 0;
+        pl->spl.reset();
+        PlanPool& pp = plan_pool();
+        std::lock_guard<std::mutex> lock(pp.mu);
+        if (pp.free.size() < kPlanPoolMax) {
+            pp.free.push_back(pl);
+            return;
+        }
+    }
+    nusi_plan_destroy(pl);
+}
+}  // namespace
+
 struct nusi_handle {
     nusi_params p{};
     nusi_plan* plan = nullptr;
@@ -1375,7 +1426,7 @@ struct nusi_handle {
     bool evolved = false;      // an evolve() has run (norm_total is set)
     int warn = 0;
     std::map<int, int> opts;   // the last value nusi_set_option set per option, replayed by nusi_copy
-    ~nusi_handle() { nusi_plan_destroy(plan); }
+    ~nusi_handle() { pool_give(plan); }
 };
 
 extern "C" {
@@ -1388,7 +1439,9 @@ static int open_handle(const nusi_params* p, const std::shared_ptr<SplineStore>*
     if (const char* e = getenv("NUSI_DEVICE")) dev = atoi(e);
     std::unique_ptr<nusi_handle> h(new nusi_handle);
     h->p = *p;
-    int r = nusi_plan_create(dev, p->N_bins_E, p->lEmin, p->lEmax, p->zmax, 1, &h->plan);
+    int r = NUSI_OK;
+    h->plan = pool_take(dev, p->N_bins_E, p->lEmin, p->lEmax, p->zmax);
+    if (!h->plan) r = nusi_plan_create(dev, p->N_bins_E, p->lEmin, p->lEmax, p->zmax, 1, &h->plan);
     if (r) return r;
     if (p->non_resonant && p->phiphi) {   // nuSIprop.hpp:166-170
         if (share && *share) h->plan->spl = *share;

@@ -32,49 +32,62 @@ __device__ __attribute__((noinline)) void warn_entry(int* warn, int* wmin, int T
 #ifndef NUSI_GA_WAVES   // Gamma / alphaTilde kernel waves per SIMD (A/B)
 #define NUSI_GA_WAVES 4   // with Gamma / alphaTilde split over work-items: 4 0.525, 3 0.535 ms (was 0.572 unsplit at 3)
 #endif
-// Gamma and alphaTilde: grid (T / 64, points, 2 quantities), three waves per workgroup -- wave k runs mass state k
-// of 64 bins (gamma_k / alphat_k), its channel terms go to LDS, and wave 0 sums them in the reference's order
-// (state after state, channel after channel: gamma_entry's additions, the same bits).  Three times the waves of one
-// work-item per entry, each a third as long: the kernel is latency-bound (a one-point plan's 12 waves, the GSL
-// dilogarithms' divergent series in the reference order).  kRef: NUSI_OPT_REFERENCE_ORDER.
-constexpr int kGaTerms = 7;   // channel terms per mass state (alphat_k: s, t, u, t-u, s-t, s-u, phi-phi)
+// Gamma and alphaTilde: grid (T / 64, points, 2 quantities), six waves per workgroup -- wave (k, part) runs part
+// `part` of mass state k for 64 bins (gamma_k / alphat_k: part 1 the s-t / s-u interference, part 0 every other
+// channel), its channel terms go to LDS by slot, and wave 0 sums them in the reference's order (state after state,
+// channel after channel: gamma_entry's additions, the same bits) and forms the warnings from the unscaled values.
+// Six times the waves of one work-item per entry, each a sixth to a half as long: the kernel is latency-bound (a
+// one-point plan has a few dozen waves of it; in the reference order GSL's series diverge across lanes).
+// kRef: NUSI_OPT_REFERENCE_ORDER.
+constexpr int kGaTerms = kAlphatSlots;   // >= kGammaSlots
 struct LdsSink {
-    double* v;   // this lane's column of [kGaTerms][64]
-    int n;
-    NUSI_FN void add(double x) { v[n * 64] = x; ++n; }
+    double* v;   // this lane's column of [kGaTerms][64]: the scaled terms
+    double* r;   // ... the unscaled channel values
+    NUSI_FN void put(int slot, double x, double raw) { v[slot * 64] = x; r[slot * 64] = raw; }
 };
 template <bool kRef>
-__global__ __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(NUSI_GA_WAVES, NUSI_GA_WAVES))) void k_gamma_alphat(GridDev g, const Point* __restrict__ pts, const SplineSet* __restrict__ splp,
+__global__ __launch_bounds__(384) __attribute__((amdgpu_waves_per_eu(NUSI_GA_WAVES, NUSI_GA_WAVES))) void k_gamma_alphat(GridDev g, const Point* __restrict__ pts, const SplineSet* __restrict__ splp,
                                                      double* __restrict__ G, double* __restrict__ At,
                                                      int* __restrict__ warn, int* __restrict__ wmin)
 {
-    __shared__ double v[3][kGaTerms][64];
-    __shared__ int cnt[3][64], wk[3][64];
+    __shared__ double v[3][kGaTerms][64], raw[3][kGaTerms][64];
+    __shared__ int wk[6][64];
     const SplineSet& spl = *splp;   // (in global memory: a by-value copy would live in scratch)
     const int lane = threadIdx.x & 63;
-    const int k = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), k = wv >> 1, part = wv & 1;
     const int p = blockIdx.y;
     const int n = blockIdx.x * 64 + lane;
     const bool act = n < g.T;
     const Point& P = pts[p];
+    const bool gam = blockIdx.z == 0;
     if (act) {
         int w = 0;
-        LdsSink sk{&v[k][0][lane], 0};
+        LdsSink sk{&v[k][0][lane], &raw[k][0][lane]};
         const double lo = g.lo[n], hi = g.hi[n];
-        if (blockIdx.z == 0) gamma_k<kRef>(P, k, lo, hi, sk, w);
-        else alphat_k<kRef>(P, spl, k, lo, hi, sk, w);
-        cnt[k][lane] = sk.n;
-        wk[k][lane] = w;
+        if (gam) {
+            if (part == 0) gamma_k<kRef, 0>(P, k, lo, hi, sk, w);
+            else gamma_k<kRef, 1>(P, k, lo, hi, sk, w);
+        } else {
+            if (part == 0) alphat_k<kRef, 0>(P, spl, k, lo, hi, sk, w);
+            else alphat_k<kRef, 1>(P, spl, k, lo, hi, sk, w);
+        }
+        wk[wv][lane] = w;
     }
     __syncthreads();
-    if (k != 0 || !act) return;
+    if (wv != 0 || !act) return;
+    const int ns = !P.non_resonant ? 1 : gam ? kGammaSlots : kAlphatSlots;
     SumSink tot;
     int w = 0;
     for (int kk = 0; kk < 3; ++kk) {
-        for (int i = 0; i < cnt[kk][lane]; ++i) tot.add(v[kk][i][lane]);
-        w |= wk[kk][lane];
+        for (int i = 0; i < ns; ++i) tot.put(i, v[kk][i][lane], 0.0);
+        w |= wk[2 * kk][lane] | wk[2 * kk + 1][lane];
+        if (P.non_resonant) {
+            const double* x = &raw[kk][0][lane];
+            w |= gam ? gamma_warn(x[0], x[64], x[128], x[192], x[256])
+                     : alphat_warn(x[0], x[64], x[128], x[192], x[256], x[320], P.a_nrm);
+        }
     }
-    (blockIdx.z == 0 ? G : At)[(size_t)p * g.T + n] = tot.tot;
+    (gam ? G : At)[(size_t)p * g.T + n] = tot.tot;
     if (w) warn_entry(warn, wmin, g.T, p, w, n, n);
 }
 
@@ -140,8 +153,8 @@ hipError_t launch_gamma_alphat(const GridDev& g, const Point* pts, int npts, con
                                int* warn, hipStream_t s, bool ref)
 {
     dim3 grid((g.T + 63) / 64, npts, 2);
-    if (ref) hipLaunchKernelGGL(k_gamma_alphat<true>, grid, dim3(192), 0, s, g, pts, spl, t.G, t.At, warn, t.Wmin);
-    else hipLaunchKernelGGL(k_gamma_alphat<false>, grid, dim3(192), 0, s, g, pts, spl, t.G, t.At, warn, t.Wmin);
+    if (ref) hipLaunchKernelGGL(k_gamma_alphat<true>, grid, dim3(384), 0, s, g, pts, spl, t.G, t.At, warn, t.Wmin);
+    else hipLaunchKernelGGL(k_gamma_alphat<false>, grid, dim3(384), 0, s, g, pts, spl, t.G, t.At, warn, t.Wmin);
     return hipGetLastError();
 }
 

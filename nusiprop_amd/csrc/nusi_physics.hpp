@@ -183,14 +183,28 @@ NUSI_FN double gpp_analytic(double a, double b)  // nuSIprop.hpp:885 with a = ma
 // ---------------------------------------------------------------------------
 // The entries sum their channels' terms over the mass states into one accumulator, in the reference's order
 // (channel by channel within a state, state after state).  The per-state bodies (gamma_k, alphat_k) hand each term
-// wgt * X to a sink: SumSink accumulates as the reference does (gamma_entry, alphat_entry: the per-entry paths and the
-// host checks); k_gamma_alphat runs the three states on three waves, stores their terms and sums them on one in the
-// same order -- the same additions of the same values, so the same bits.
+// wgt * X to a sink with its channel slot and the unscaled X: SumSink accumulates as the reference does (gamma_entry,
+// alphat_entry: the per-entry paths and the host checks); k_gamma_alphat runs each (mass state, part) on a wave of its
+// own -- kPart 0: every channel but the s-t / s-u interference, 1: those two (the complex dilogarithms), -1: all --
+// stores the terms by slot and sums them on one wave in slot order, state after state: the same additions of the same
+// values, so the same bits.  The warnings, which read several channels, are formed from the unscaled values
+// (gamma_warn, alphat_warn) by whoever holds them all.
 struct SumSink {
     double tot = 0;
-    NUSI_FN void add(double x) { tot += x; }
+    NUSI_FN void put(int, double x, double) { tot += x; }
 };
-template <bool kRef, class Sink>   // kRef: NUSI_OPT_REFERENCE_ORDER (GSL's dilogarithms, nusi_gsl.hpp)
+constexpr int kGammaSlots = 6;    // s, t+u, t-u (int), s-t, s-u, phi-phi
+constexpr int kAlphatSlots = 7;   // s, t, u, t-u, s-t, s-u, phi-phi
+NUSI_FN int gamma_warn(double Gs, double Gtu0, double Gint, double Gst, double Gsu)
+{
+    return (Gs < 0 || Gtu0 < 0 || Gint < 0 || (Gs + Gtu0 + Gst + Gsu) < 0) ? kWarnGamma : 0;
+}
+NUSI_FN int alphat_warn(double as, double at, double au, double atu, double ast, double asu, double nrm)
+{
+    return (as < 0 || at < 0 || au < 0 || atu / nrm < -1e-11 || (ast + at + as) / nrm < -1e-11 || (asu + au + as) / nrm < -1e-11)
+               ? kWarnAlphaTilde : 0;
+}
+template <bool kRef, int kPart, class Sink>   // kRef: NUSI_OPT_REFERENCE_ORDER (GSL's dilogarithms, nusi_gsl.hpp)
 NUSI_FN void gamma_k(const Point& P, int j, double Em, double Ep, Sink& tot, int& warn)
 {
     const double g = P.g, mphi = P.mphi, Ga = P.Ga;
@@ -201,31 +215,35 @@ NUSI_FN void gamma_k(const Point& P, int j, double Em, double Ep, Sink& tot, int
         const double sp = 2 * mj * Ep / m2, sm = 2 * mj * Em / m2;
         const double cs = m2 / (m2 + Ga * Ga);
         const double lg = Ga * (nm::log1p(cs * sp * (sp - 2)) - nm::log1p(cs * sm * (sm - 2)));
-        double Gs;
-        if (sp < 1e-5)
-            Gs = g4 / (32 * kPi * m2 * Ga) *
-                 (2 * mphi * ((gr * (1 + gr2 + 2 * sm)) / ((1 + gr2) * (1 + gr2)) * (sp - sm) + gr / ((1 + gr2) * (1 + gr2)) * ((sp - sm) * (sp - sm))) + lg);
-        else
-            Gs = g4 / (32 * kPi * m2 * Ga) * (2 * mphi * atandiff(mphi * (sp - 1) / Ga, mphi * (sm - 1) / Ga) + lg);
-        Gs *= uj;
         const double wgt = m2 / (2 * mj);
-        tot.add(wgt * Gs);
+        double Gs = 0, Gtu0 = 0, Gint = 0, Gst = 0, Gsu = 0;
+        if (kPart != 1) {
+            if (sp < 1e-5)
+                Gs = g4 / (32 * kPi * m2 * Ga) *
+                     (2 * mphi * ((gr * (1 + gr2 + 2 * sm)) / ((1 + gr2) * (1 + gr2)) * (sp - sm) + gr / ((1 + gr2) * (1 + gr2)) * ((sp - sm) * (sp - sm))) + lg);
+            else
+                Gs = g4 / (32 * kPi * m2 * Ga) * (2 * mphi * atandiff(mphi * (sp - 1) / Ga, mphi * (sm - 1) / Ga) + lg);
+            Gs *= uj;
+            tot.put(0, wgt * Gs, Gs);
+        }
         if (!P.non_resonant) return;
 
         const double L1p = nm::log1p(sp), L1m = nm::log1p(sm);
-        double Gtu0 = g4 / (16 * kPi * m2) * (2 * L1p / sp - 2 * L1m / sm + L1p - L1m);
-        if (Gtu0 < 0) Gtu0 = g4 / (16 * kPi * m2) * (sp - sm) / 2. * gl3_Gtu_nores(sm, sp);
-        Gtu0 *= 2 * uj;
-        tot.add(wgt * Gtu0);
+        if (kPart != 1) {
+            Gtu0 = g4 / (16 * kPi * m2) * (2 * L1p / sp - 2 * L1m / sm + L1p - L1m);
+            if (Gtu0 < 0) Gtu0 = g4 / (16 * kPi * m2) * (sp - sm) / 2. * gl3_Gtu_nores(sm, sp);
+            Gtu0 *= 2 * uj;
+            tot.put(1, wgt * Gtu0, Gtu0);
 
-        double Gint = g4 / (32 * kPi * m2 * sm * sp) *
-                      (sm * L1p * (2 + 2 * sp + sp * nm::log(2 + sp)) - sp * L1m * (2 + 2 * sm + sm * nm::log(2 + sm))
-                       + sm * sp * (dilog1mdiff<kRef>(sp, sm) + dilogdiff<kRef>(sp, sm)));
-        if (Gint < 0) Gint = g4 / (16 * kPi * m2) * (sp - sm) / 2. * gl3_Gtu_int(sm, sp);
-        Gint *= P.majorana ? uj : 0.5 * uj;
-        tot.add(wgt * Gint);
+            Gint = g4 / (32 * kPi * m2 * sm * sp) *
+                   (sm * L1p * (2 + 2 * sp + sp * nm::log(2 + sp)) - sp * L1m * (2 + 2 * sm + sm * nm::log(2 + sm))
+                    + sm * sp * (dilog1mdiff<kRef>(sp, sm) + dilogdiff<kRef>(sp, sm)));
+            if (Gint < 0) Gint = g4 / (16 * kPi * m2) * (sp - sm) / 2. * gl3_Gtu_int(sm, sp);
+            Gint *= P.majorana ? uj : 0.5 * uj;
+            tot.put(2, wgt * Gint, Gint);
+        }
 
-        // s-t interference
+        if (kPart != 0) {   // s-t interference
         const cd den = C(gr, 2.0);                    // 2*I + gr
         const cd z1p = C(0.0, 1 + sp) / den, z1m = C(0.0, 1 + sm) / den;
         const cd z2p = conj(z1p), z2m = conj(z1m);
@@ -239,24 +257,27 @@ NUSI_FN void gamma_k(const Point& P, int j, double Em, double Ep, Sink& tot, int
             d2 = dilogdiff_c<kRef>(z2p, z2m);
         }
         const double Lgp = nm::log1p(((-1 + sp) * (-1 + sp)) / gr2), Lgm = nm::log1p(((-1 + sm) * (-1 + sm)) / gr2);
-        double Gst = -g4 / (32 * kPi * m2 * (1 + gr2)) *
-                     (d1.r + d2.r + gr * (d2.i - d1.i) + 2 * gr * carg(1.0 - z2p) * L1p - 2 * gr * carg(1.0 - z2m) * L1m
-                      + nm::log1p(4 / gr2) * (L1m - L1p) + Lgp * L1p - Lgm * L1m + (1 + gr2) * (Lgm - Lgp) + 2 * dilogdiff<kRef>(sp, sm));
+        Gst = -g4 / (32 * kPi * m2 * (1 + gr2)) *
+              (d1.r + d2.r + gr * (d2.i - d1.i) + 2 * gr * carg(1.0 - z2p) * L1p - 2 * gr * carg(1.0 - z2m) * L1m
+               + nm::log1p(4 / gr2) * (L1m - L1p) + Lgp * L1p - Lgm * L1m + (1 + gr2) * (Lgm - Lgp) + 2 * dilogdiff<kRef>(sp, sm));
         Gst *= uj;
-        tot.add(wgt * Gst);
-        const double Gsu = P.majorana ? Gst : 0;
-        tot.add(wgt * Gsu);
-
-        double Gpp = 0;
-        if (sp > 4 && P.phiphi) {
-            const double a = (sm > 4) ? sm : 4.0;
-            Gpp = g4 / (128. * kPi * m2) * gpp_analytic<kRef>(a, sp);
-            if (Gpp < 0) Gpp = g4 / (64 * kPi * m2) * (sp - a) / 2. * gl3_Gpp(a, sp);
-            Gpp *= uj;
-            if (P.majorana) Gpp *= 2;
+        tot.put(3, wgt * Gst, Gst);
+        Gsu = P.majorana ? Gst : 0;
+        tot.put(4, wgt * Gsu, Gsu);
         }
-        tot.add(wgt * Gpp);
-        if (Gs < 0 || Gtu0 < 0 || Gint < 0 || (Gs + Gtu0 + Gst + Gsu) < 0) warn |= kWarnGamma;
+
+        if (kPart != 1) {
+            double Gpp = 0;
+            if (sp > 4 && P.phiphi) {
+                const double a = (sm > 4) ? sm : 4.0;
+                Gpp = g4 / (128. * kPi * m2) * gpp_analytic<kRef>(a, sp);
+                if (Gpp < 0) Gpp = g4 / (64 * kPi * m2) * (sp - a) / 2. * gl3_Gpp(a, sp);
+                Gpp *= uj;
+                if (P.majorana) Gpp *= 2;
+            }
+            tot.put(5, wgt * Gpp, Gpp);
+        }
+        if (kPart == -1) warn |= gamma_warn(Gs, Gtu0, Gint, Gst, Gsu);
     }
 }
 template <bool kRef = false>
@@ -264,14 +285,14 @@ NUSI_FN double gamma_entry(const Point& P, double Em, double Ep, int& warn)
 {
     SumSink tot;
     NUSI_MASS_LOOP
-    for (int j = 0; j < 3; ++j) gamma_k<kRef>(P, j, Em, Ep, tot, warn);
+    for (int j = 0; j < 3; ++j) gamma_k<kRef, -1>(P, j, Em, Ep, tot, warn);
     return tot.tot;
 }
 
 // ---------------------------------------------------------------------------
 // alphaTilde(Em, Ep)  -- nuSIprop.hpp:924-1235
 // ---------------------------------------------------------------------------
-template <bool kRef, class Sink>   // kRef: NUSI_OPT_REFERENCE_ORDER (GSL's dilogarithms, nusi_gsl.hpp)
+template <bool kRef, int kPart, class Sink>   // kRef: NUSI_OPT_REFERENCE_ORDER (GSL's dilogarithms, nusi_gsl.hpp)
 NUSI_FN void alphat_k(const Point& P, const SplineSet& spl, int k, double Em, double Ep, Sink& tot, int& warn)
 {
     const double g = P.g, mphi = P.mphi, Ga = P.Ga;
@@ -287,20 +308,22 @@ NUSI_FN void alphat_k(const Point& P, const SplineSet& spl, int k, double Em, do
 
         const double cs = m2 / (m2 + Ga * Ga);
         const double lg = Ga * (nm::log1p(cs * tp * (tp + 2)) - nm::log1p(cs * tm * (tm + 2)));
-        double as;
-        if (fabs(tp) < 1e-5)
-            as = g4 / (16 * kPi * Ga * m4) *
-                 (2 * mphi * (1 + tm) * (-((gr * (1 + gr2 - 2 * tm) * (-tm + tp)) / ((1 + gr2) * (1 + gr2))) + (gr * ((-tm + tp) * (-tm + tp))) / ((1 + gr2) * (1 + gr2))) + lg);
-        else
-            as = g4 / (16 * kPi * Ga * m4) * (2 * mphi * (1 + tm) * atandiff(mphi * (1 + tm) / Ga, mphi * (1 + tp) / Ga) + lg);
-        as *= uk;
-        if (!maj) as /= 2.;
-        tot.add(wgt * as);
+        double as = 0, at = 0, au = 0, atu = 0, ast = 0, asu = 0;
+        if (kPart != 1) {
+            if (fabs(tp) < 1e-5)
+                as = g4 / (16 * kPi * Ga * m4) *
+                     (2 * mphi * (1 + tm) * (-((gr * (1 + gr2 - 2 * tm) * (-tm + tp)) / ((1 + gr2) * (1 + gr2))) + (gr * ((-tm + tp) * (-tm + tp))) / ((1 + gr2) * (1 + gr2))) + lg);
+            else
+                as = g4 / (16 * kPi * Ga * m4) * (2 * mphi * (1 + tm) * atandiff(mphi * (1 + tm) / Ga, mphi * (1 + tp) / Ga) + lg);
+            as *= uk;
+            if (!maj) as /= 2.;
+            tot.put(0, wgt * as, as);
+        }
         if (!P.non_resonant) return;
 
         const double Lmt = nm::log1p(-tm), Lmp = nm::log1p(-tp), Ld = nm::log1p(tm - tp);
         const double brk = (-2 + tm) * (tm - tp) - (-1 + tm) * (-2 + tp) * (Lmt - Lmp);
-        double at;
+        if (kPart != 1) {
         if (maj) {
             at = g4 * (1 / (16 * m4 * kPi * (-1 + tm) * tp) * brk
                        + 1 / (16 * m4 * kPi * ((1 + tm) * (1 + tm)) * tp) *
@@ -311,18 +334,16 @@ NUSI_FN void alphat_k(const Point& P, const SplineSet& spl, int k, double Em, do
             if (at < 0) at = gl33_tri(1, tp, tm) * (3. / 2. * g4 / (32 * kPi * m4));
         }
         at *= uk;
-        tot.add(wgt * at);
+        tot.put(1, wgt * at, at);
 
-        double au;
         if (maj) au = at;
         else {
             au = 1. / 2. * g4 / (32 * m4 * kPi * (-1 + tm) * tp) * brk;
             if (au < 0) au = gl33_tri(1, tp, tm) * (1. / 2. * g4 / (32 * kPi * m4));
             au *= uk;
         }
-        tot.add(wgt * au);
+        tot.put(2, wgt * au, au);
 
-        double atu = 0;
         if (maj) {
             double combi;
             if (-tp < 1e-2 && -tm < 1e-2) {
@@ -350,9 +371,10 @@ NUSI_FN void alphat_k(const Point& P, const SplineSet& spl, int k, double Em, do
             if (atu < 0) atu = gl33_tri(2, tp, tm) * (g4 / (16 * kPi * m4));
         }
         atu *= uk;
-        tot.add(wgt * atu);
+        tot.put(3, wgt * atu, atu);
+        }
 
-        // s-t interference
+        if (kPart != 0) {   // s-t interference
         const cd den = C(gr, 2.0);                  // 2*I + gr
         const cd dt_m = C(2 + tm, -gr);             // 2 - I*gr + tm
         cd d78, d51, d26, d43;
@@ -381,7 +403,6 @@ NUSI_FN void alphat_k(const Point& P, const SplineSet& spl, int k, double Em, do
         const double Lgp = nm::log1p(((1 + tp) * (1 + tp)) / gr2), Lgm = nm::log1p(((1 + tm) * (1 + tm)) / gr2);
         const double Am = carg(C(-1 - tm, gr)), Ap = carg(C(-1 - tp, gr));
         const double Bm = carg(C(gr, 1 + tm) / den), Bp = carg(C(gr, 1 + tp) / den);
-        double ast;
         if (maj)
             ast = g4 / (32 * kPi * (1 + gr2) * m4) *
                   (2 * kPi * Am - 2 * kPi * Ap + 2 * gr * (d51.i + d26.i + d43.i) - 2 * (d51.r + d26.r + d43.r + d78.r)
@@ -398,10 +419,12 @@ NUSI_FN void alphat_k(const Point& P, const SplineSet& spl, int k, double Em, do
                    + 2 * tm * nm::log(tm / tp) + 2 * Lmp * nm::log(-tp) + (Lmp - Lmt) * (nm::log(4 + gr2) - 2 * nm::log(gr) - Lgp)
                    + (1 + tm + gr2) * (Lgp - Lgm));
         ast *= uk;
-        tot.add(wgt * ast);
-        const double asu = maj ? ast : 0;
-        tot.add(wgt * asu);
+        tot.put(4, wgt * ast, ast);
+        asu = maj ? ast : 0;
+        tot.put(5, wgt * asu, asu);
+        }
 
+        if (kPart != 1) {
         double app = 0;
         if (-tp > 4 && P.phiphi) {
             if (-tp < 1e4) {
@@ -420,11 +443,10 @@ NUSI_FN void alphat_k(const Point& P, const SplineSet& spl, int k, double Em, do
             app *= 2;
             if (maj) app *= 2;
         }
-        tot.add(wgt * app);
+        tot.put(6, wgt * app, app);
+        }
 
-        const double nrm = P.a_nrm;
-        if (as < 0 || at < 0 || au < 0 || atu / nrm < -1e-11 || (ast + at + as) / nrm < -1e-11 || (asu + au + as) / nrm < -1e-11)
-            warn |= kWarnAlphaTilde;
+        if (kPart == -1) warn |= alphat_warn(as, at, au, atu, ast, asu, P.a_nrm);
     }
 }
 template <bool kRef = false>
@@ -432,7 +454,7 @@ NUSI_FN double alphat_entry(const Point& P, const SplineSet& spl, double Em, dou
 {
     SumSink tot;
     NUSI_MASS_LOOP
-    for (int k = 0; k < 3; ++k) alphat_k<kRef>(P, spl, k, Em, Ep, tot, warn);
+    for (int k = 0; k < 3; ++k) alphat_k<kRef, -1>(P, spl, k, Em, Ep, tot, warn);
     return tot.tot;
 }
 
