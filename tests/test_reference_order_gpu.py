@@ -201,3 +201,39 @@ def test_reference_order_pyprop(nusi):
     ev.evolve()
     _, fla, _, _, _ = _gpu_refo(nusi, [cases.C2A], tables=False)
     assert np.array_equal(np.asarray(ev.get_flux_fla()), fla[0])
+
+
+def test_object_plans_are_reused_with_default_options(nusi):
+    """Destroyed one-point objects hand their plan to the next object on the same grid (nusi_capi.cpp plan pool):
+    an object created after a reference-order one runs the default arithmetic and gives the bits of a fresh plan."""
+    import ctypes
+    from nusiprop_amd import _lib
+    L = _lib.load()
+    kw = dict(cases.C2B)
+    src = kw.pop("source_model")
+
+    def run(ref):
+        h = ctypes.c_void_p()
+        _lib.check(L.nusi_create(ctypes.byref(_lib.make_params(source_model=src, **kw)), ctypes.byref(h)))
+        try:
+            if ref:
+                _lib.check(L.nusi_set_option(h, _lib.OPT_REFERENCE_ORDER, 1))
+            _lib.check(L.nusi_evolve(h))
+            out = np.zeros(3 * 300)
+            _lib.check(L.nusi_get_flux_fla(h, out.ctypes.data_as(ctypes.POINTER(ctypes.c_double))))
+            a, c = ctypes.c_char_p(), ctypes.c_char_p()
+            _lib.check(L.nusi_get_kernels(h, ctypes.byref(a), ctypes.byref(c)))
+            return out.reshape(3, 300), a.value
+        finally:
+            L.nusi_destroy(h)
+
+    ref, ka = run(True)
+    dflt, kb = run(False)   # (the pooled plan of the first object)
+    assert ka == b"k_alpha_mcorner + k_alpha_batch[refo]" and kb == b"k_alpha_batch"
+    p0 = cases.C2B
+    plan = nusi.Plan(p0["N_bins_E"], p0["lEmin"], p0["lEmax"], p0["zmax"], max_points=1)
+    _, fla = plan.evolve([p0])
+    plan.close()
+    assert np.array_equal(dflt, fla[0])
+    _, fla_r, _, _, _ = _gpu_refo(nusi, [p0], tables=False)
+    assert np.array_equal(ref, fla_r[0])
