@@ -412,6 +412,11 @@ __global__ __launch_bounds__(256) void k_alpha_medge(GridDev g, const Point* __r
 // ns per call against 0.06, scripts/dev/gsl_bench.hip).  The values pass through LDS to leave as runs of cb corners
 // per (field, table), the layout the batch kernel reads a tile's corner rows from.
 constexpr int kMcJobs = 1024;
+#ifndef NUSI_MC_SORT   // A/B: 0 = the jobs in (corner, table) order
+#define NUSI_MC_SORT 1
+#endif
+constexpr bool kMcSort = NUSI_MC_SORT != 0;
+constexpr int kMcKeys = 128;   // cost buckets (gsl_cli2_cost, clamped)
 __global__ __launch_bounds__(256) void k_alpha_mcorner(const Point* __restrict__ pts, const int* __restrict__ batches,
                                                        MCornerDev mc, int pc0, int jobs)
 {
@@ -427,9 +432,43 @@ __global__ __launch_bounds__(256) void k_alpha_mcorner(const Point* __restrict__
     const int nj = cb * nb;
     for (int cl = tid; cl < cb && c0 + cl < mc.NC; cl += 256) alpha_mcorner_st(P, k, c0 + cl, mc.ue, cst[0][cl], cst[1][cl]);
     __syncthreads();
-    for (int j = tid; j < nj; j += 256) {
+    // (kMcSort) the workgroup's jobs in increasing order of their estimated series length (gsl_cli2_cost of the
+    // quotient; a counting sort in LDS), so that the lanes of a wave run similar GSL branches and term counts
+    __shared__ int hist[kMcKeys + 1];
+    __shared__ short perm[kMcJobs];
+    if (kMcSort) {
+        for (int i = tid; i <= kMcKeys; i += 256) hist[i] = 0;
+        __syncthreads();
+        int key[kMcJobs / 256], rank[kMcJobs / 256];
+#pragma unroll
+        for (int i = 0; i < kMcJobs / 256; ++i) {
+            const int j = tid + 256 * i;
+            key[i] = -1;
+            if (j >= nj) continue;
+            const int cl = j / nb, q = j - cl * nb;
+            if (c0 + cl >= mc.NC) continue;
+            const double S = cst[0][cl], t = cst[1][cl], gr = pts[p0 + q].a_gr;
+            const cd z = (1 + S + t) / C(2 + t, -gr);
+            key[i] = (int)fmin((double)kMcKeys - 1, gsl_cli2_cost(z.r, z.i));
+            rank[i] = atomicAdd(&hist[key[i]], 1);
+        }
+        __syncthreads();
+        if (tid == 0) {   // exclusive scan over the keys (kMcKeys entries)
+            int acc = 0;
+            for (int b = 0; b < kMcKeys; ++b) { const int c = hist[b]; hist[b] = acc; acc += c; }
+            hist[kMcKeys] = acc;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < kMcJobs / 256; ++i)
+            if (key[i] >= 0) perm[hist[key[i]] + rank[i]] = (short)(tid + 256 * i);
+        __syncthreads();
+    }
+    const int njv = kMcSort ? hist[kMcKeys] : nj;   // (the valid jobs)
+    for (int jj = tid; jj < njv; jj += 256) {
+        const int j = kMcSort ? perm[jj] : jj;
         const int cl = j / nb, q = j - cl * nb;
-        if (c0 + cl >= mc.NC) break;
+        if (!kMcSort && c0 + cl >= mc.NC) break;
         const double S = cst[0][cl], t = cst[1][cl], gr = pts[p0 + q].a_gr;
         const cd Dc = NUSI_REFO_STUB == 2 ? C(0.0) : alpha_member_ref_dc(S, t, gr);
         v[q * cb + cl] = Dc.r;
