@@ -32,29 +32,31 @@ __device__ __attribute__((noinline)) void warn_entry(int* warn, int* wmin, int T
 #ifndef NUSI_GA_WAVES   // Gamma / alphaTilde kernel waves per SIMD (A/B)
 #define NUSI_GA_WAVES 4   // with Gamma / alphaTilde split over work-items: 4 0.525, 3 0.535 ms (was 0.572 unsplit at 3)
 #endif
-// Gamma and alphaTilde: grid (T / 64, points, 2 quantities), six waves per workgroup -- wave (k, part) runs part
-// `part` of mass state k for 64 bins (gamma_k / alphat_k: part 1 the s-t / s-u interference, part 0 every other
-// channel), its channel terms go to LDS by slot, and wave 0 sums them in the reference's order (state after state,
-// channel after channel: gamma_entry's additions, the same bits) and forms the warnings from the unscaled values.
-// Six times the waves of one work-item per entry, each a sixth to a half as long: the kernel is latency-bound (a
-// one-point plan has a few dozen waves of it; in the reference order GSL's series diverge across lanes).
-// kRef: NUSI_OPT_REFERENCE_ORDER.
+// Gamma and alphaTilde: grid (T / 64, points, 2 quantities), 3 kParts waves per workgroup of 64 bins -- wave
+// (k, part) runs mass state k (gamma_k / alphat_k; kParts = 2: part 1 the s-t / s-u interference, part 0 every other
+// channel; kParts = 1: all), its channel terms go to LDS by slot, and wave 0 sums them in the reference's order
+// (state after state, channel after channel: gamma_entry's additions, the same bits).  A wave per mass state: three
+// times the waves of one work-item per entry, each a third as long (C4 reference order 2.1 -> 1.6 ms, spills 202 ->
+// 26).  Calls of few tables (a single propagation: a few dozen waves in all) split the channels too (kParts = 2:
+// 0.34 -> 0.29 ms for one table); on scans that split measured slower (C4 1.6 -> 2.4 ms: the parts repeat the state's
+// common leaves).  With kParts = 2 the warnings, which read several channels, are formed on wave 0 from the
+// unscaled values (gamma_warn, alphat_warn: the per-entry path's own predicates).  kRef: NUSI_OPT_REFERENCE_ORDER.
 constexpr int kGaTerms = kAlphatSlots;   // >= kGammaSlots
 struct LdsSink {
     double* v;   // this lane's column of [kGaTerms][64]: the scaled terms
     double* r;   // ... the unscaled channel values
     NUSI_FN void put(int slot, double x, double raw) { v[slot * 64] = x; r[slot * 64] = raw; }
 };
-template <bool kRef>
-__global__ __launch_bounds__(384) __attribute__((amdgpu_waves_per_eu(NUSI_GA_WAVES, NUSI_GA_WAVES))) void k_gamma_alphat(GridDev g, const Point* __restrict__ pts, const SplineSet* __restrict__ splp,
+template <bool kRef, int kParts>
+__global__ __launch_bounds__(192 * kParts) __attribute__((amdgpu_waves_per_eu(NUSI_GA_WAVES, NUSI_GA_WAVES))) void k_gamma_alphat(GridDev g, const Point* __restrict__ pts, const SplineSet* __restrict__ splp,
                                                      double* __restrict__ G, double* __restrict__ At,
                                                      int* __restrict__ warn, int* __restrict__ wmin)
 {
-    __shared__ double v[3][kGaTerms][64], raw[3][kGaTerms][64];
-    __shared__ int wk[6][64];
+    __shared__ double v[3][kGaTerms][64], raw[kParts == 2 ? 3 : 1][kGaTerms][64];
+    __shared__ int wk[3 * kParts][64];
     const SplineSet& spl = *splp;   // (in global memory: a by-value copy would live in scratch)
     const int lane = threadIdx.x & 63;
-    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), k = wv >> 1, part = wv & 1;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), k = wv / kParts, part = wv - k * kParts;
     const int p = blockIdx.y;
     const int n = blockIdx.x * 64 + lane;
     const bool act = n < g.T;
@@ -62,9 +64,12 @@ __global__ __launch_bounds__(384) __attribute__((amdgpu_waves_per_eu(NUSI_GA_WAV
     const bool gam = blockIdx.z == 0;
     if (act) {
         int w = 0;
-        LdsSink sk{&v[k][0][lane], &raw[k][0][lane]};
+        LdsSink sk{&v[k][0][lane], &raw[kParts == 2 ? k : 0][0][lane]};
         const double lo = g.lo[n], hi = g.hi[n];
-        if (gam) {
+        if (kParts == 1) {
+            if (gam) gamma_k<kRef, -1>(P, k, lo, hi, sk, w);
+            else alphat_k<kRef, -1>(P, spl, k, lo, hi, sk, w);
+        } else if (gam) {
             if (part == 0) gamma_k<kRef, 0>(P, k, lo, hi, sk, w);
             else gamma_k<kRef, 1>(P, k, lo, hi, sk, w);
         } else {
@@ -80,9 +85,9 @@ __global__ __launch_bounds__(384) __attribute__((amdgpu_waves_per_eu(NUSI_GA_WAV
     int w = 0;
     for (int kk = 0; kk < 3; ++kk) {
         for (int i = 0; i < ns; ++i) tot.put(i, v[kk][i][lane], 0.0);
-        w |= wk[2 * kk][lane] | wk[2 * kk + 1][lane];
-        if (P.non_resonant) {
-            const double* x = &raw[kk][0][lane];
+        for (int pp = 0; pp < kParts; ++pp) w |= wk[kk * kParts + pp][lane];
+        if (kParts == 2 && P.non_resonant) {
+            const double* x = &raw[kParts == 2 ? kk : 0][0][lane];
             w |= gam ? gamma_warn(x[0], x[64], x[128], x[192], x[256])
                      : alphat_warn(x[0], x[64], x[128], x[192], x[256], x[320], P.a_nrm);
         }
@@ -153,8 +158,13 @@ hipError_t launch_gamma_alphat(const GridDev& g, const Point* pts, int npts, con
                                int* warn, hipStream_t s, bool ref)
 {
     dim3 grid((g.T + 63) / 64, npts, 2);
-    if (ref) hipLaunchKernelGGL(k_gamma_alphat<true>, grid, dim3(384), 0, s, g, pts, spl, t.G, t.At, warn, t.Wmin);
-    else hipLaunchKernelGGL(k_gamma_alphat<false>, grid, dim3(384), 0, s, g, pts, spl, t.G, t.At, warn, t.Wmin);
+    if (npts <= 16) {   // (a few tables: the channels split too, kParts = 2)
+        if (ref) hipLaunchKernelGGL((k_gamma_alphat<true, 2>), grid, dim3(384), 0, s, g, pts, spl, t.G, t.At, warn, t.Wmin);
+        else hipLaunchKernelGGL((k_gamma_alphat<false, 2>), grid, dim3(384), 0, s, g, pts, spl, t.G, t.At, warn, t.Wmin);
+    } else {
+        if (ref) hipLaunchKernelGGL((k_gamma_alphat<true, 1>), grid, dim3(192), 0, s, g, pts, spl, t.G, t.At, warn, t.Wmin);
+        else hipLaunchKernelGGL((k_gamma_alphat<false, 1>), grid, dim3(192), 0, s, g, pts, spl, t.G, t.At, warn, t.Wmin);
+    }
     return hipGetLastError();
 }
 
@@ -412,11 +422,6 @@ __global__ __launch_bounds__(256) void k_alpha_medge(GridDev g, const Point* __r
 // ns per call against 0.06, scripts/dev/gsl_bench.hip).  The values pass through LDS to leave as runs of cb corners
 // per (field, table), the layout the batch kernel reads a tile's corner rows from.
 constexpr int kMcJobs = 1024;
-#ifndef NUSI_MC_SORT   // A/B: 0 = the jobs in (corner, table) order
-#define NUSI_MC_SORT 1
-#endif
-constexpr bool kMcSort = NUSI_MC_SORT != 0;
-constexpr int kMcKeys = 128;   // cost buckets (gsl_cli2_cost, clamped)
 __global__ __launch_bounds__(256) void k_alpha_mcorner(const Point* __restrict__ pts, const int* __restrict__ batches,
                                                        MCornerDev mc, int pc0, int jobs)
 {
@@ -432,43 +437,9 @@ __global__ __launch_bounds__(256) void k_alpha_mcorner(const Point* __restrict__
     const int nj = cb * nb;
     for (int cl = tid; cl < cb && c0 + cl < mc.NC; cl += 256) alpha_mcorner_st(P, k, c0 + cl, mc.ue, cst[0][cl], cst[1][cl]);
     __syncthreads();
-    // (kMcSort) the workgroup's jobs in increasing order of their estimated series length (gsl_cli2_cost of the
-    // quotient; a counting sort in LDS), so that the lanes of a wave run similar GSL branches and term counts
-    __shared__ int hist[kMcKeys + 1];
-    __shared__ short perm[kMcJobs];
-    if (kMcSort) {
-        for (int i = tid; i <= kMcKeys; i += 256) hist[i] = 0;
-        __syncthreads();
-        int key[kMcJobs / 256], rank[kMcJobs / 256];
-#pragma unroll
-        for (int i = 0; i < kMcJobs / 256; ++i) {
-            const int j = tid + 256 * i;
-            key[i] = -1;
-            if (j >= nj) continue;
-            const int cl = j / nb, q = j - cl * nb;
-            if (c0 + cl >= mc.NC) continue;
-            const double S = cst[0][cl], t = cst[1][cl], gr = pts[p0 + q].a_gr;
-            const cd z = (1 + S + t) / C(2 + t, -gr);
-            key[i] = (int)fmin((double)kMcKeys - 1, gsl_cli2_cost(z.r, z.i));
-            rank[i] = atomicAdd(&hist[key[i]], 1);
-        }
-        __syncthreads();
-        if (tid == 0) {   // exclusive scan over the keys (kMcKeys entries)
-            int acc = 0;
-            for (int b = 0; b < kMcKeys; ++b) { const int c = hist[b]; hist[b] = acc; acc += c; }
-            hist[kMcKeys] = acc;
-        }
-        __syncthreads();
-#pragma unroll
-        for (int i = 0; i < kMcJobs / 256; ++i)
-            if (key[i] >= 0) perm[hist[key[i]] + rank[i]] = (short)(tid + 256 * i);
-        __syncthreads();
-    }
-    const int njv = kMcSort ? hist[kMcKeys] : nj;   // (the valid jobs)
-    for (int jj = tid; jj < njv; jj += 256) {
-        const int j = kMcSort ? perm[jj] : jj;
+    for (int j = tid; j < nj; j += 256) {
         const int cl = j / nb, q = j - cl * nb;
-        if (!kMcSort && c0 + cl >= mc.NC) break;
+        if (c0 + cl >= mc.NC) break;
         const double S = cst[0][cl], t = cst[1][cl], gr = pts[p0 + q].a_gr;
         const cd Dc = NUSI_REFO_STUB == 2 ? C(0.0) : alpha_member_ref_dc(S, t, gr);
         v[q * cb + cl] = Dc.r;
