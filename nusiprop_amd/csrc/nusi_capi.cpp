@@ -588,7 +588,7 @@ AlphaBatches alpha_batches(nusi_plan* pl, int ntab, std::vector<int>& perm)
 }
 
 // NUSI_OPT_REFERENCE_ORDER on the big-batch kernel: the member-corner block of plan p (MCornerDev) for the batches of
-// this call -- 3 kMcFields NC doubles per table (C4's N_E = 300 axis: NC = 77 421, 3.7 MB), allocated for at most
+// this call -- 6 NC doubles per table (C4's N_E = 300 axis: NC = 77 421, 3.7 MB), allocated for at most
 // NUSI_OPT_REFO_CORNER_MB (automatic: kMCornerBudget bytes and half the free memory) of tables, at least the largest
 // batch; launch_alpha runs the batches in chunks that fit
 constexpr size_t kMCornerBudget = size_t(8) << 30;
@@ -616,7 +616,7 @@ int mcorner_ensure(nusi_plan* p, int ntab, const AlphaBatches& ab, int budget_mb
     }
     int nbmax = 1;
     for (int b = 0; b < ab.nbatch; ++b) nbmax = std::max(nbmax, (int)((unsigned)p->h_batches[b] >> 24));
-    const size_t per = sizeof(double) * 3 * nusi::kMcFields * (size_t)mc.NC;
+    const size_t per = sizeof(double) * 6 * (size_t)mc.NC;
     size_t fr = 0, tot = 0;
     if (hipMemGetInfo(&fr, &tot) != hipSuccess) fr = kMCornerBudget;
     const size_t budget = budget_mb > 0 ? ((size_t)budget_mb << 20)

@@ -57,16 +57,10 @@ void alpha_tiles_destroy(AlphaTilesDev* t);
 // state and corner, evaluated by k_alpha_mcorner before k_alpha_batch reads them.  A corner is a pair of distinct bin
 // edges (S' edge us, t edge ut <= us; the edges numbered 0 .. U-1 along the table axis, an edge two neighbouring bins
 // share counted once): c = us (us + 1) / 2 + ut, NC = U (U + 1) / 2.  The block of a batch of nb tables starting at
-// slot p0 is buf + (p0 - pc0) 3 kMcFields NC, laid out [k][field: Dcr, Dci (, A)][q][c] (a tile's corner rows
-// contiguous); a launch chunk of batches whose tables fit cap_tables starts at table pc0.
-// NUSI_REFO_A_INLINE (A/B): the block holds Dcr and Dci only and k_alpha_batch forms A = carg(..) itself (one
-// atan2 per corner and point, against a third of the block's HBM traffic); 0: A in the block too
-#ifndef NUSI_REFO_A_INLINE
-#define NUSI_REFO_A_INLINE 1
-#endif
-constexpr int kMcFields = NUSI_REFO_A_INLINE ? 2 : 3;
+// slot p0 is buf + (p0 - pc0) 6 NC, laid out [k][q][c][Dcr, Dci] (a tile's corner rows contiguous; A = carg(..) is
+// formed by the batch kernel); a launch chunk of batches whose tables fit cap_tables starts at table pc0.
 struct MCornerDev {
-    double* buf = nullptr;   // [cap_tables][3][kMcFields][NC]
+    double* buf = nullptr;   // [cap_tables][3][NC][2]
     int* eu = nullptr;       // [2 T]: edge number of bin edge 2 b + side (side 0: lo[b], 1: hi[b])
     double* ue = nullptr;    // [U]: the energy of each edge
     long long NC = 0;

@@ -431,7 +431,7 @@ constexpr int kMcJobs = 1024;
 __global__ __launch_bounds__(256) void k_alpha_mcorner(const Point* __restrict__ pts, const int* __restrict__ batches,
                                                        MCornerDev mc, int pc0, int jobs)
 {
-    __shared__ double v[kMcFields * kMcJobs];   // [field][q][cl]
+    __shared__ double v[2 * kMcJobs];   // [q][cl][Dcr, Dci]
     __shared__ double cst[2][kMcJobs];           // S', t of corner c0 + cl (shared by the batch's tables)
     const int bw = batches[blockIdx.y], k = blockIdx.z, tid = threadIdx.x;
     const int p0 = bw & 0xffffff, nb = (int)((unsigned)bw >> 24);
@@ -448,15 +448,14 @@ __global__ __launch_bounds__(256) void k_alpha_mcorner(const Point* __restrict__
         if (c0 + cl >= mc.NC) break;
         const double S = cst[0][cl], t = cst[1][cl], gr = pts[p0 + q].a_gr;
         const cd Dc = NUSI_REFO_STUB == 2 ? C(0.0) : alpha_member_ref_dc(S, t, gr);
-        v[q * cb + cl] = Dc.r;
-        v[nj + q * cb + cl] = Dc.i;
-        if (kMcFields == 3) v[2 * nj + q * cb + cl] = alpha_member_ref_arg(S, t, gr);
+        v[2 * (q * cb + cl)] = Dc.r;
+        v[2 * (q * cb + cl) + 1] = Dc.i;
     }
     __syncthreads();
-    double* const o = mc.buf + (size_t)(p0 - pc0) * 3 * kMcFields * mc.NC + (size_t)k * kMcFields * nb * mc.NC;
-    for (int e = tid; e < kMcFields * nj; e += 256) {
-        const int fq = e / cb, cl = e - fq * cb;   // fq = field nb + q
-        if (c0 + cl < mc.NC) o[(size_t)fq * mc.NC + c0 + cl] = v[e];
+    double* const o = mc.buf + (size_t)(p0 - pc0) * 6 * mc.NC + (size_t)k * 2 * nb * mc.NC;
+    for (int e = tid; e < 2 * nj; e += 256) {   // runs of 2 cb doubles per table q
+        const int q = e / (2 * cb), r = e - q * 2 * cb;
+        if (c0 + r / 2 < mc.NC) o[((size_t)q * mc.NC + c0) * 2 + r] = v[e];
     }
 }
 
@@ -587,20 +586,17 @@ void k_alpha_batch(GridDev g, const Point* __restrict__ pts, const SplineSet* __
         const int mq = tid / mjobs, mjob = tid - mq * mjobs;
         // (kRef) thread tid < cc carries corner tid's member leaves one point ahead, from k_alpha_mcorner's block:
         // the corner's numbering c (only corners with ut <= us are read by the entries n < m; the others stay unset)
-        const size_t mstr = kRef ? (size_t)mc.NC * nb : 0;   // (uniform: the block's field stride and base)
-        const double* const mcb =
-            kRef ? mc.buf + (size_t)(p0 - pc0) * 3 * kMcFields * mc.NC + (size_t)k * kMcFields * mstr : nullptr;
-        int moff = -1;   // this thread's corner c, or -1 (point q's value at q NC + c)
-        double mc0 = 0.0, mc1 = 0.0, mc2 = 0.0;
+        const double2* const mcb =   // (uniform: the block of this batch and mass state, [q][c] of (Dcr, Dci))
+            kRef ? reinterpret_cast<const double2*>(mc.buf + (size_t)(p0 - pc0) * 6 * mc.NC + (size_t)k * 2 * nb * mc.NC)
+                 : nullptr;
+        int moff = -1;   // this thread's corner c, or -1 (point q's pair at q NC + c)
+        double2 mcv = make_double2(0.0, 0.0);
         if (kRef && cornered && tid < cc) {
             const int si = tid / ct, ti = tid - si * ct;
             const int us = mc.eu[ssrc[si]], ut = mc.eu[tsrc[ti]];
             if (ut <= us) {
                 moff = us * (us + 1) / 2 + ut;
-                if (kRefPrefetch) {
-                    mc0 = mcb[moff]; mc1 = mcb[mstr + moff];
-                    if (kMcFields == 3) mc2 = mcb[2 * mstr + moff];
-                }
+                if (kRefPrefetch) mcv = mcb[moff];
             }
         }
 #pragma unroll 1
@@ -641,22 +637,14 @@ void k_alpha_batch(GridDev g, const Point* __restrict__ pts, const SplineSet* __
                         if (kRef) {
                             if (moff >= 0) {
                                 const size_t o = (size_t)q * mc.NC + moff;
-                                if (!kRefPrefetch) {
-                                    mc0 = mcb[o]; mc1 = mcb[mstr + o];
-                                    if (kMcFields == 3) mc2 = mcb[2 * mstr + o];
-                                }
-                                X[tid] = mc0; X[kCC + tid] = mc1;
-                                if (kMcFields == 3) X[2 * kCC + tid] = mc2;
-                                else {   // A of the corner for point q: alpha_member_ref's expression on the tile's S', t
+                                if (!kRefPrefetch) mcv = mcb[o];
+                                X[tid] = mcv.x; X[kCC + tid] = mcv.y;
+                                {   // A of the corner for point q: alpha_member_ref's expression on the tile's S', t
                                     const int si = tid / ct, ti = tid - si * ct;
                                     X[2 * kCC + tid] = b_marg(edgk[kTEdgeFields * ct + kSEdgeVal * cs + si],
                                                               edgk[kTEdgeVal * ct + ti], Q.a_gr);
                                 }
-                                if (kRefPrefetch && q + 1 < nb) {
-                                    const size_t o1 = o + mc.NC;
-                                    mc0 = mcb[o1]; mc1 = mcb[mstr + o1];
-                                    if (kMcFields == 3) mc2 = mcb[2 * mstr + o1];
-                                }
+                                if (kRefPrefetch && q + 1 < nb) mcv = mcb[o + mc.NC];
                             }
                         }
                         else
@@ -869,7 +857,7 @@ static hipError_t launch_alpha_t(const GridDev& g, const Point* pts, int npts, c
                         pipe = ch.size() >= 2 && (int)ch.size() * 2 + 1 <= mc->nevs;
                     }
                     if (!pipe) cut(mc->cap_tables, ch);
-                    const size_t half = (size_t)(mc->cap_tables / 2) * 3 * kMcFields * (size_t)mc->NC;
+                    const size_t half = (size_t)(mc->cap_tables / 2) * 6 * (size_t)mc->NC;
                     if (pipe) {
                         HIP_RET(hipEventRecord(mc->evs[0], s));   // the side stream after the call's uploads
                         HIP_RET(hipStreamWaitEvent(mc->side, mc->evs[0], 0));
