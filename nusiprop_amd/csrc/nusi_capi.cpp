@@ -592,17 +592,10 @@ AlphaBatches alpha_batches(nusi_plan* pl, int ntab, std::vector<int>& perm)
 // NUSI_OPT_REFO_CORNER_MB (automatic: kMCornerBudget bytes and half the free memory) of tables, at least the largest
 // batch; launch_alpha runs the batches in chunks that fit
 constexpr size_t kMCornerBudget = size_t(8) << 30;
-constexpr int kMCornerMaxChunks = 32;   // pipelined member-corner chunks per call (more: one after the other)
 constexpr int kOverlapTables = 16;   // calls of at most this many tables overlap Gamma / alphaTilde with alpha
 int mcorner_ensure(nusi_plan* p, int ntab, const AlphaBatches& ab, int budget_mb)
 {
     nusi::MCornerDev& mc = p->mc;
-    if (!mc.side) {   // the pipelined chunks' stream and events (launch_alpha)
-        HIPCHECK(hipStreamCreateWithFlags(&mc.side, hipStreamNonBlocking));
-        mc.nevs = 2 * kMCornerMaxChunks + 1;
-        mc.evs = new hipEvent_t[mc.nevs];
-        for (int i = 0; i < mc.nevs; ++i) HIPCHECK(hipEventCreateWithFlags(&mc.evs[i], hipEventDisableTiming));
-    }
     if (!mc.eu) {
         std::vector<int> eu;
         std::vector<double> ue;
@@ -831,14 +824,6 @@ void nusi_plan_destroy(nusi_plan* pl)
     hipFree(pl->mc.buf);
     hipFree(pl->mc.eu);
     hipFree(pl->mc.ue);
-    if (pl->mc.evs) {
-        for (int i = 0; i < pl->mc.nevs; ++i) hipEventDestroy(pl->mc.evs[i]);
-        delete[] pl->mc.evs;
-    }
-    if (pl->mc.side) {
-        hipStreamSynchronize(pl->mc.side);
-        hipStreamDestroy(pl->mc.side);
-    }
     hipFree(pl->d_scratch);
     if (pl->h_pts) hipHostFree(pl->h_pts);
     if (pl->stream) hipStreamDestroy(pl->stream);

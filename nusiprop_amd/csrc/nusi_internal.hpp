@@ -65,10 +65,6 @@ struct MCornerDev {
     double* ue = nullptr;    // [U]: the energy of each edge
     long long NC = 0;
     int U = 0, cap_tables = 0;
-    // (host) chunks in two halves of buf, k_alpha_mcorner of chunk c + 1 on `side` beside k_alpha_batch of chunk c
-    hipStream_t side = nullptr;
-    hipEvent_t* evs = nullptr;   // [nevs]
-    int nevs = 0;
 };
 // ref: NUSI_OPT_REFERENCE_ORDER (the kernels' kRef instances: the reference's own operation order for the complex
 // dilogarithms and the s-t interference member leaves, bit-identical to the oracle's ora_set_reference_order(1))

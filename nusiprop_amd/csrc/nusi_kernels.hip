@@ -14,11 +14,6 @@
 
 namespace nusi {
 
-#define HIP_RET(x)                                   \
-    do {                                             \
-        const hipError_t e_ = (x);                   \
-        if (e_ != hipSuccess) return e_;             \
-    } while (0)
 
 // ---------------------------------------------------------------------------
 // Stage A
@@ -821,75 +816,38 @@ static hipError_t launch_alpha_t(const GridDev& g, const Point* pts, int npts, c
                                            dim3(kTileThreads), lds, s, g, pts, spl, at.tiles, batches + nb_plain, t.A,
                                            t.Med, warn, t.Wmin, MCornerDev{}, 0);
                 } else {
-                    // the member corners of a chunk of whole batches (the phi-phi batches in chunks of their own),
-                    // then the chunk's tiles.  Pipelined (mc->side, >= 2 chunks): the chunks alternate between the
-                    // two halves of the block, and k_alpha_mcorner of chunk c + 1 runs on the side stream beside
-                    // k_alpha_batch of chunk c -- the one VALU-bound, the other latency-bound, their workgroups share
-                    // the CUs.  Else one chunk after the other in the whole block.
+                    // the member corners of a chunk of whole batches (<= mc->cap_tables tables, the phi-phi batches
+                    // in chunks of their own), then the chunk's tiles.  (k_alpha_mcorner of chunk c + 1 on a second
+                    // stream beside k_alpha_batch of chunk c, in two halves of the block, measured no gain: C4 18.25
+                    // -> 18.26 ms, the two kernels' workgroups sharing the CUs each ran slower by the other's share.)
                     if (!mc || !mc->buf || !h_batches) return hipErrorInvalidValue;
-                    struct Chunk { int b, e, pc0, ntb, nbmax; };
-                    int ntot = 0, nball = 0;
-                    for (int b = 0; b < nbatches; ++b) {
-                        const int nbe = (int)((unsigned)h_batches[b] >> 24);
-                        ntot += nbe;
-                        nball = std::max(nball, nbe);
-                    }
-                    auto cut = [&](int ccap, std::vector<Chunk>& out) {
-                        out.clear();
-                        for (int b = 0; b < nbatches;) {
-                            const int lim = b < nb_plain ? nb_plain : nbatches;
-                            Chunk c{b, b, h_batches[b] & 0xffffff, 0, 0};
-                            while (c.e < lim) {
-                                const int nbe = (int)((unsigned)h_batches[c.e] >> 24);
-                                if (c.e > b && c.ntb + nbe > ccap) break;
-                                c.ntb += nbe;
-                                c.nbmax = std::max(c.nbmax, nbe);
-                                ++c.e;
-                            }
-                            out.push_back(c);
-                            b = c.e;
+                    for (int b = 0; b < nbatches;) {
+                        const int lim = b < nb_plain ? nb_plain : nbatches, pc0 = h_batches[b] & 0xffffff;
+                        int e = b, ntb = 0, nbmax = 0;
+                        while (e < lim) {
+                            const int nbe = (int)((unsigned)h_batches[e] >> 24);
+                            if (e > b && ntb + nbe > mc->cap_tables) break;
+                            ntb += nbe;
+                            nbmax = std::max(nbmax, nbe);
+                            ++e;
                         }
-                    };
-                    std::vector<Chunk> ch;
-                    bool pipe = mc->side && mc->evs && mc->cap_tables / 2 >= nball;
-                    if (pipe) {
-                        cut(std::min(mc->cap_tables / 2, std::max(nball, (ntot + 3) / 4)), ch);
-                        pipe = ch.size() >= 2 && (int)ch.size() * 2 + 1 <= mc->nevs;
-                    }
-                    if (!pipe) cut(mc->cap_tables, ch);
-                    const size_t half = (size_t)(mc->cap_tables / 2) * 6 * (size_t)mc->NC;
-                    if (pipe) {
-                        HIP_RET(hipEventRecord(mc->evs[0], s));   // the side stream after the call's uploads
-                        HIP_RET(hipStreamWaitEvent(mc->side, mc->evs[0], 0));
-                    }
-                    for (size_t ci = 0; ci < ch.size(); ++ci) {
-                        const Chunk& c = ch[ci];
-                        if (c.ntb > mc->cap_tables) return hipErrorInvalidValue;
-                        MCornerDev m = *mc;
-                        if (pipe) m.buf = mc->buf + (ci & 1) * half;
-                        hipStream_t ms = pipe ? mc->side : s;
-                        hipEvent_t evm = pipe ? mc->evs[1 + 2 * ci] : nullptr, evb = pipe ? mc->evs[2 + 2 * ci] : nullptr;
-                        if (pipe && ci >= 2) HIP_RET(hipStreamWaitEvent(ms, mc->evs[2 + 2 * (ci - 2)], 0));   // half free
+                        if (ntb > mc->cap_tables) return hipErrorInvalidValue;
                         // jobs per workgroup: 4 per work-item on scans, 1 when the chunk is too small to fill ~2048
                         // workgroups (a single propagation: one GSL call per work-item, not four in a row)
-                        const long long tot = mc->NC * 3 * c.ntb;
+                        const long long tot = mc->NC * 3 * ntb;
                         const int jobs = 256 * (int)std::max(1LL, std::min<long long>(kMcJobs / 256, tot / (2048 * 256)));
-                        const int cbmin = jobs / c.nbmax;
-                        hipLaunchKernelGGL(k_alpha_mcorner, dim3((unsigned)((mc->NC + cbmin - 1) / cbmin), c.e - c.b, 3),
-                                           dim3(256), 0, ms, pts, batches + c.b, m, c.pc0, jobs);
-                        if (pipe) {
-                            HIP_RET(hipEventRecord(evm, ms));
-                            HIP_RET(hipStreamWaitEvent(s, evm, 0));
-                        }
-                        if (c.b < nb_plain)
-                            hipLaunchKernelGGL((k_alpha_batch<false, true>), dim3(at.ncls[0], c.e - c.b), dim3(kTileThreads),
-                                               lds, s, g, pts, spl, at.tiles, batches + c.b, t.A, t.Med, warn, t.Wmin, m,
-                                               c.pc0);
+                        const int cbmin = jobs / nbmax;
+                        hipLaunchKernelGGL(k_alpha_mcorner, dim3((unsigned)((mc->NC + cbmin - 1) / cbmin), e - b, 3),
+                                           dim3(256), 0, s, pts, batches + b, *mc, pc0, jobs);
+                        if (b < nb_plain)
+                            hipLaunchKernelGGL((k_alpha_batch<false, true>), dim3(at.ncls[0], e - b), dim3(kTileThreads),
+                                               lds, s, g, pts, spl, at.tiles, batches + b, t.A, t.Med, warn, t.Wmin, *mc,
+                                               pc0);
                         else
-                            hipLaunchKernelGGL((k_alpha_batch<true, true>), dim3(at.ncls[0], c.e - c.b), dim3(kTileThreads),
-                                               lds, s, g, pts, spl, at.tiles, batches + c.b, t.A, t.Med, warn, t.Wmin, m,
-                                               c.pc0);
-                        if (pipe) HIP_RET(hipEventRecord(evb, s));
+                            hipLaunchKernelGGL((k_alpha_batch<true, true>), dim3(at.ncls[0], e - b), dim3(kTileThreads),
+                                               lds, s, g, pts, spl, at.tiles, batches + b, t.A, t.Med, warn, t.Wmin, *mc,
+                                               pc0);
+                        b = e;
                     }
                 }
             } else {
