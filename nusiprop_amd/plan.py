@@ -92,8 +92,9 @@ class Plan:
         auto), OPT_ALPHA_KERNEL (0 batch, 1 tile, 2 per entry), OPT_CASCADE_RHS (1 = one point per cascade
         workgroup), OPT_STEP_PASSES (1 = the step-pass cascade also where one pass fits), OPT_SHIFT_REUSE (K > 0:
         the opt-in scan mode sharing tables across m_phi on the r^(-o/2) lattice, o <= K; only tables with g <= 0.05
-        share, the others are built directly), OPT_REFERENCE_ORDER (1 =
-        the tables in the reference's own operation order for the complex dilogarithms; include/nusi.h)."""
+        share, the others are built directly), OPT_REFERENCE_ORDER (1 = the tables in the reference's own arithmetic:
+        GSL's dilogarithm algorithms on the reference's arguments), OPT_REFO_CORNER_MB (the reference order's
+        member-corner block budget in MiB, 0 = automatic); include/nusi.h."""
         _lib.check(_lib.load().nusi_plan_set_option(self._h, int(option), int(value)))
 
     def profile_begin(self, max_calls):
