@@ -32,14 +32,21 @@ def per_kernel(d, counter):
 
 
 def per_step(d, counter, name_part):
-    """Sum over one step's launches of a kernel: dispatches are grouped by grid size (the
-    alpha table is three launches of different grids per step); each group's mean is summed."""
-    groups = defaultdict(list)
+    """Sum over one step's launches of a kernel: every matching dispatch's value, divided by the number of steps the
+    pass ran (the dispatches of k_gamma_alphat, one per step).  (Grouping by grid size, as before round 5, counted
+    the reference order's equal-sized member-corner chunks once.)  Returns (per-step value, launches per step)."""
+    tot, n, steps = 0.0, 0, 0
     for f in glob.glob(d + "/**/*counter_collection.csv", recursive=True):
         for row in csv.DictReader(open(f)):
-            if row["Counter_Name"] == counter and name_part in row["Kernel_Name"]:
-                groups[(row["Kernel_Name"], row["Grid_Size"])].append(float(row["Counter_Value"]))
-    return sum(sum(v) / len(v) for v in groups.values()), len(groups)
+            if row["Counter_Name"] != counter:
+                continue
+            if "k_gamma_alphat" in row["Kernel_Name"]:
+                steps += 1
+            if name_part in row["Kernel_Name"]:
+                tot += float(row["Counter_Value"])
+                n += 1
+    steps = max(steps, 1)
+    return tot / steps, n // steps
 
 
 def main():
