@@ -348,6 +348,9 @@ constexpr bool kBatchPipe = NUSI_BATCH_PIPE != 0;
 #define NUSI_REFO_PREFETCH 1
 #endif
 constexpr bool kRefPrefetch = NUSI_REFO_PREFETCH != 0;
+#ifndef NUSI_REFO_BSTUB   // timing A/B only (wrong tables): bit 0 the batch kernel without A, bit 1 without the block's loads
+#define NUSI_REFO_BSTUB 0
+#endif
 __host__ __device__ inline int alpha_batch_lds_doubles()
 {
     const int c1 = kAlphaTile + 1;
@@ -591,7 +594,7 @@ void k_alpha_batch(GridDev g, const Point* __restrict__ pts, const SplineSet* __
             const int us = mc.eu[ssrc[si]], ut = mc.eu[tsrc[ti]];
             if (ut <= us) {
                 moff = us * (us + 1) / 2 + ut;
-                if (kRefPrefetch) mcv = mcb[moff];
+                if (kRefPrefetch && !(NUSI_REFO_BSTUB & 2)) mcv = mcb[moff];
             }
         }
 #pragma unroll 1
@@ -636,10 +639,14 @@ void k_alpha_batch(GridDev g, const Point* __restrict__ pts, const SplineSet* __
                                 X[tid] = mcv.x; X[kCC + tid] = mcv.y;
                                 {   // A of the corner for point q: alpha_member_ref's expression on the tile's S', t
                                     const int si = tid / ct, ti = tid - si * ct;
+#if NUSI_REFO_BSTUB & 1   // timing A/B only: A not formed
+                                    X[2 * kCC + tid] = edgk[kTEdgeVal * ct + ti] * Q.a_gr;
+#else
                                     X[2 * kCC + tid] = b_marg(edgk[kTEdgeFields * ct + kSEdgeVal * cs + si],
                                                               edgk[kTEdgeVal * ct + ti], Q.a_gr);
+#endif
                                 }
-                                if (kRefPrefetch && q + 1 < nb) mcv = mcb[o + mc.NC];
+                                if (kRefPrefetch && q + 1 < nb && !(NUSI_REFO_BSTUB & 2)) mcv = mcb[o + mc.NC];
                             }
                         }
                         else

@@ -1,7 +1,8 @@
 // Development timing (not part of the product): gsl_cli2 (nusi_gsl.hpp, NUSI_OPT_REFERENCE_ORDER's complex
 // dilogarithm) in isolation on the alpha table's member-corner quotients z = (1 + S + t) / (2 + t - i gr) of a C4-like
 // scan (N_E = 300, lE 12 -> 17, Sum m = 0.1 NO; every corner of the unique bin edges for 11 m_phi x 8 g x 3 mass
-// states), against the shared-algorithm cli2 -- in tile-like order, shuffled, and sorted by gsl_cli2_cost.
+// states), against the shared-algorithm cli2 -- in tile-like order, shuffled, and sorted by gsl_cli2_cost; the
+// member-corner order (a batch's points fastest) as it is and with each workgroup's 1024 jobs sorted by cost.
 //   hipcc -O3 -std=c++17 -ffp-contract=off --offload-arch=gfx950 -I nusiprop_amd/csrc scripts/dev/gsl_bench.hip -o gsl_bench
 #include <hip/hip_runtime.h>
 #include <algorithm>
@@ -64,9 +65,25 @@ int main()
     });
     std::shuffle(hr.begin(), hr.end(), std::mt19937(1));
     const int np = (int)hp.size();
+    // the member-corner kernel's workgroup sets (1024 consecutive jobs of hp) sorted locally by cost, and in 16
+    // cost buckets (a counting sort's order)
+    std::vector<double2> hl = hp, hb = hp;
+    for (int s0 = 0; s0 < np; s0 += 1024) {
+        const int s1 = std::min(np, s0 + 1024);
+        auto cost = [](const double2& x) { return gsl_cli2_cost(x.x, x.y); };
+        std::stable_sort(hl.begin() + s0, hl.begin() + s1, [&](const double2& x, const double2& y) { return cost(x) > cost(y); });
+        std::stable_sort(hb.begin() + s0, hb.begin() + s1, [&](const double2& x, const double2& y) {
+            auto bk = [&](const double2& z) { const double c = cost(z); return c >= 8.0 && c < 8.5 ? 0 : std::min(15, 1 + (int)(c / 8.0)); };
+            return bk(x) > bk(y); });
+    }
     double2 *dz, *dzs, *dzr, *dzp, *dout;
     hipMalloc(&dzp, sizeof(double2) * np);
     hipMemcpy(dzp, hp.data(), sizeof(double2) * np, hipMemcpyHostToDevice);
+    double2 *dzl, *dzb;
+    hipMalloc(&dzl, sizeof(double2) * np);
+    hipMalloc(&dzb, sizeof(double2) * np);
+    hipMemcpy(dzl, hl.data(), sizeof(double2) * np, hipMemcpyHostToDevice);
+    hipMemcpy(dzb, hb.data(), sizeof(double2) * np, hipMemcpyHostToDevice);
     hipMalloc(&dz, sizeof(double2) * n);
     hipMalloc(&dzs, sizeof(double2) * n);
     hipMalloc(&dzr, sizeof(double2) * n);
@@ -93,6 +110,8 @@ int main()
     run("gsl_cli2 shuffled", kbench<0>, dzr, n);
     run("gsl_cli2 cost-sorted", kbench<0>, dzs, n);
     run("gsl_cli2 points fastest", kbench<0>, dzp, np);
+    run("points fastest, 1024-sets sorted", kbench<0>, dzl, np);
+    run("points fastest, 1024-sets bucketed", kbench<0>, dzb, np);
     run("cli2 (shared algorithm)", kbench<1>, dz, n);
     return (int)hipDeviceSynchronize();
 }
