@@ -67,7 +67,17 @@ int main()
     const int np = (int)hp.size();
     // the member-corner kernel's workgroup sets (1024 consecutive jobs of hp) sorted locally by cost, and in 16
     // cost buckets (a counting sort's order)
-    std::vector<double2> hl = hp, hb = hp;
+    std::vector<double2> hl = hp, hb = hp, hc = hp, hk = hp;
+    auto cls = [](const double2& z) {   // GSL's branches: inversion, reflection, series_1 / series_2 / series_3
+        const double x = z.x, y = z.y, r2 = x * x + y * y;
+        if (y == 0.0) return 0;
+        const bool inv = !(r2 < 1.0);
+        const double ux = inv ? x / r2 : x, uy = inv ? -y / r2 : y;
+        const bool refl = ux > 0.732;
+        const double fx = refl ? 1.0 - ux : ux, r = sqrt(fx * fx + uy * uy);
+        const int ser = r > 0.98 ? 2 : r > 0.25 ? 1 : 0;
+        return 1 + ser + 3 * (refl + 2 * inv);
+    };
     for (int s0 = 0; s0 < np; s0 += 1024) {
         const int s1 = std::min(np, s0 + 1024);
         auto cost = [](const double2& x) { return gsl_cli2_cost(x.x, x.y); };
@@ -75,6 +85,10 @@ int main()
         std::stable_sort(hb.begin() + s0, hb.begin() + s1, [&](const double2& x, const double2& y) {
             auto bk = [&](const double2& z) { const double c = cost(z); return c >= 8.0 && c < 8.5 ? 0 : std::min(15, 1 + (int)(c / 8.0)); };
             return bk(x) > bk(y); });
+        std::stable_sort(hc.begin() + s0, hc.begin() + s1, [&](const double2& x, const double2& y) { return cls(x) < cls(y); });
+        std::stable_sort(hk.begin() + s0, hk.begin() + s1, [&](const double2& x, const double2& y) {
+            const int a = cls(x), b = cls(y);
+            return a != b ? a < b : cost(x) > cost(y); });
     }
     double2 *dz, *dzs, *dzr, *dzp, *dout;
     hipMalloc(&dzp, sizeof(double2) * np);
@@ -84,6 +98,11 @@ int main()
     hipMalloc(&dzb, sizeof(double2) * np);
     hipMemcpy(dzl, hl.data(), sizeof(double2) * np, hipMemcpyHostToDevice);
     hipMemcpy(dzb, hb.data(), sizeof(double2) * np, hipMemcpyHostToDevice);
+    double2 *dzc, *dzk;
+    hipMalloc(&dzc, sizeof(double2) * np);
+    hipMalloc(&dzk, sizeof(double2) * np);
+    hipMemcpy(dzc, hc.data(), sizeof(double2) * np, hipMemcpyHostToDevice);
+    hipMemcpy(dzk, hk.data(), sizeof(double2) * np, hipMemcpyHostToDevice);
     hipMalloc(&dz, sizeof(double2) * n);
     hipMalloc(&dzs, sizeof(double2) * n);
     hipMalloc(&dzr, sizeof(double2) * n);
@@ -112,6 +131,13 @@ int main()
     run("gsl_cli2 points fastest", kbench<0>, dzp, np);
     run("points fastest, 1024-sets sorted", kbench<0>, dzl, np);
     run("points fastest, 1024-sets bucketed", kbench<0>, dzb, np);
+    run("points fastest, 1024-sets by branch", kbench<0>, dzc, np);
+    run("1024-sets by branch, then cost", kbench<0>, dzk, np);
+    {   // the branch mix of the set
+        long long nc[13] = {};
+        for (const double2& z : hp) nc[cls(z)]++;
+        for (int c = 0; c < 13; ++c) if (nc[c]) printf("class %2d (inv %d refl %d series %d): %.3f\n", c, c ? (c - 1) / 6 : 0, c ? ((c - 1) / 3) % 2 : 0, c ? (c - 1) % 3 + 1 : 0, (double)nc[c] / hp.size());
+    }
     run("cli2 (shared algorithm)", kbench<1>, dz, n);
     return (int)hipDeviceSynchronize();
 }
