@@ -254,7 +254,11 @@ NUSI_FN void gamma_k(const Point& P, int j, double Em, double Ep, Sink& tot, int
             d2 = (sm * sm) * (C(0.0, 0.5) / C(gr, -1.0) - l2 / 2.) + sm * l2 - sp * l2 + ((sp * sp) * (C(-0.0, -1.0) / C(gr, -1.0) + l2)) / 2.;
         } else {
             d1 = dilogdiff_c<kRef>(z1p, z1m);
-            d2 = dilogdiff_c<kRef>(z2p, z2m);
+            // (kRef) GSL's complex dilogarithm is odd in y operation by operation (every y-dependent quantity is
+            // negated exactly, atan2 and Clausen are odd, the series' rotation and sums negate, the modulus terms do
+            // not change), and so is li2_asym: Li2(conj z) = conj Li2(z) bit for bit, and d2 = conj(d1) is the
+            // reference's own value at half the cost (the tables stay bit-identical to the oracle, which calls both)
+            d2 = kRef ? conj(d1) : dilogdiff_c<kRef>(z2p, z2m);
         }
         const double Lgp = nm::log1p(((-1 + sp) * (-1 + sp)) / gr2), Lgm = nm::log1p(((-1 + sm) * (-1 + sm)) / gr2);
         Gst = -g4 / (32 * kPi * m2 * (1 + gr2)) *

@@ -203,3 +203,27 @@ def test_device_gsl_bit_identical_to_oracle(oracle_mod, hlib):
         assert hlib.hc_gsl_clausen(x) == oracle_mod.gsl_clausen(x), x
     for a, b in rng.normal(size=(2000, 2)) * 10.0 ** rng.uniform(-200, 200, size=(2000, 1)):
         assert hlib.hc_hypot(float(a), float(b)) == oracle_mod.hypot(float(a), float(b)), (a, b)
+
+
+def test_gsl_complex_dilog_conjugate_symmetric(oracle_mod, hlib):
+    """gsl_sf_complex_dilog_xy_e(x, -y) == conj(gsl_sf_complex_dilog_xy_e(x, y)) bit for bit (the oracle's restatement
+    of GSL and the device's): the reference-order Gamma forms Li2 of conj(z1) as conj(Li2(z1)) (gamma_k, nusi_physics.hpp),
+    so this symmetry must hold exactly, on every branch -- the unit circle, inversion, reflection, series 1 / 2 / 3."""
+    import numpy as np
+    rng = np.random.default_rng(20261018)
+    re, im = D(), D()
+    t = rng.uniform(-np.pi, np.pi, 8000)
+    rad = np.concatenate([rng.uniform(0.0, 3.0, 4000), 1 + rng.uniform(-0.05, 0.05, 2000), 10.0 ** rng.uniform(-20, 3, 2000)])
+    zs = list(zip(rad * np.cos(t), rad * np.sin(t))) + [(x, y) for x, y, _, _ in KAT["li2_complex"] + KAT["li2_complex_unit"]]
+    # the Gamma quotients themselves: z1 = i (1 + s) / (gr + 2 i)
+    for s, gr in zip(10.0 ** rng.uniform(-5, 4, 2000), 10.0 ** rng.uniform(-9, 0, 2000)):
+        d = gr * gr + 4.0
+        zs.append(((1 + s) * 2.0 / d, (1 + s) * gr / d))
+    for x, y in zs:
+        if y == 0.0:
+            continue
+        a = oracle_mod.gsl_complex_dilog(float(x), float(y))
+        b = oracle_mod.gsl_complex_dilog(float(x), float(-y))
+        assert b[0] == a[0] and b[1] == -a[1], (x, y, a, b)
+        hlib.hc_gsl_cli2(float(x), float(-y), ctypes.byref(re), ctypes.byref(im))
+        assert re.value == a[0] and im.value == -a[1], (x, y)
