@@ -22,12 +22,13 @@
 //     RN(a / b) < 2^-p  <=>  a < b 2^-p: the doubles below 2^-p b are those at or below its predecessor, which
 //     lies below the rounding boundary 2^-p b (1 - 2^-54).  So the test is one multiply and one compare
 //     (quot_lt);
-//   * the series' term a / d_k with d_k = k^2 or k^2 (k + 1) (exact integers) is RN(a / d_k) from the table value
-//     y_k = RN(1 / d_k) by two residual corrections, q0 = a y_k, q_{i+1} = q_i + (a - d_k q_i) y_k (fma): the first
-//     makes the quotient faithful, the second correctly rounded (Markstein's theorem: y correctly rounded, q
-//     faithful, remainder exact by fma); 6e8 random a over 1800 binades and every d_k agree bit for bit with the
-//     division (tests/test_specfun.py runs the device functions against the oracle's divisions).  GSL's (k - 1)/k
-//     squared of series_1 is a table of the same values;
+//   * the series' term a / d_k with d_k = k^2 or k^2 (k + 1) (exact integers below 2^30) is RN(a / d_k) as
+//     fma(a, y_k, RN(a l_k)), y_k + l_k the reciprocal to 2^-106 (y_k = RN(1 / d_k), l_k = RN(1 / d_k - y_k)): the sum
+//     is a / d_k to a relative 2^-105, and a / d_k is never a rounding midpoint nor within 2^-84 of one (a midpoint
+//     m = M 2^e has an odd 54-bit M, and a = m d_k would need the odd part of M d_k, >= M, in 53 bits; a nearer one
+//     leaves |a - m d_k| >= 2^e >= a 2^-84 for d_k < 2^30), so the one rounding of the fma is the division's.  Two
+//     operations per term instead of a five-operation residual correction (tests/test_specfun.py runs the device
+//     functions against the oracle's divisions).  GSL's (k - 1)/k squared of series_1 is a table of the same values;
 //   * both rewrites need their operands in the normal range; a series whose argument is below 2^-400 (which the
 //     tables never meet) runs a second instance of its loop with GSL's divisions (kExact), so the loops have no
 //     per-iteration branch.
@@ -52,15 +53,24 @@ constexpr double kEps = 2.2204460492503131e-16;       // GSL_DBL_EPSILON
 constexpr double kSqrtEps = 1.4901161193847656e-08;   // GSL_SQRT_DBL_EPSILON
 constexpr double kPiD = 3.14159265358979323846;       // M_PI
 
-// per-k constants of the series: d1 = k^2 and d2 = k^2 (k + 1) (exact) with their rounded reciprocals, side by side
-// (one 32-byte scalar load per iteration, k being uniform), and rr = ((k - 1) / k)^2 as series_1 forms it (every
-// value the compiler's IEEE evaluation of GSL's expression)
+// per-k constants of the series: d1 = k^2 and d2 = k^2 (k + 1) (exact), their rounded reciprocals and the
+// reciprocals' low parts, side by side (one 48-byte scalar load per iteration, k being uniform), and
+// rr = ((k - 1) / k)^2 as series_1 forms it (every value the compiler's IEEE evaluation of GSL's expression)
 constexpr int kKTab = 1000;
-struct KRow { double d1, d2, y1, y2; };
+struct KRow { double d1, d2, y1, y2, l1, l2; };
 struct KTab {
     KRow row[kKTab];
     double rr[kKTab];
 };
+// RN(1 / d - y) for y = RN(1 / d): e = 1 - y d exactly (Dekker's product y d = p + err, 1 - p exact by Sterbenz, and
+// e a multiple of ulp(y) below d ulp(y) / 2, representable), then RN(e / d) -- constexpr, no fma
+constexpr double recip_lo(double d, double y)
+{
+    const double cy = 134217729.0 * y, yh = cy - (cy - y), yl = y - yh;
+    const double cd_ = 134217729.0 * d, dh = cd_ - (cd_ - d), dl = d - dh;
+    const double p = y * d, err = ((yh * dh - p) + yh * dl + yl * dh) + yl * dl;
+    return ((1.0 - p) - err) / d;
+}
 constexpr KTab make_ktab()
 {
     KTab t{};
@@ -69,6 +79,8 @@ constexpr KTab make_ktab()
         t.row[k].d2 = (double)k * k * (k + 1.0);
         t.row[k].y1 = 1.0 / t.row[k].d1;
         t.row[k].y2 = 1.0 / t.row[k].d2;
+        t.row[k].l1 = recip_lo(t.row[k].d1, t.row[k].y1);
+        t.row[k].l2 = recip_lo(t.row[k].d2, t.row[k].y2);
         const double rk = (k - 1.0) / k;
         t.rr[k] = rk * rk;
     }
@@ -76,16 +88,14 @@ constexpr KTab make_ktab()
 }
 constexpr KTab kKT = make_ktab();
 
-// RN(a / d) for the series' terms.  kExact: the division; else from y = RN(1 / d) by two residual corrections
-// (header comment), valid for a, d > 0 with a >= 2^-960 -- the callers take kExact for arguments that could reach
-// below (a series argument under 2^-400, never met in the tables)
+// RN(a / d) for the series' terms.  kExact: the division; else fma(a, y, RN(a l)) from the two-part reciprocal
+// y + l (header comment), valid for a, d > 0 with a l normal (a >= 2^-900) -- the callers take kExact for arguments
+// that could reach below (a series argument under 2^-400, never met in the tables)
 template <bool kExact>
-NUSI_FN double div_k(double a, double d, double y)
+NUSI_FN double div_k(double a, double d, double y, double l)
 {
     if (kExact) return a / d;
-    const double q0 = a * y;
-    const double q1 = fma(fma(-q0, d, a), y, q0);
-    return fma(fma(-q1, d, a), y, q1);
+    return fma(a, y, a * l);
 }
 
 // fabs(a / b) < c of GSL's stopping tests for a, b >= 0 and c a power of two: kExact the division, else a < b c
@@ -182,7 +192,7 @@ NUSI_FN double series_2_t(double x)
 #pragma unroll
     for (k = 2; k < 10; k++) {
         rk *= x;
-        sum += div_k<kExact>(rk, kKT.row[k].d2, kKT.row[k].y2);
+        sum += div_k<kExact>(rk, kKT.row[k].d2, kKT.row[k].y2, kKT.row[k].l2);
     }
     bool done = false;
     if (!kExact) {
@@ -191,7 +201,7 @@ NUSI_FN double series_2_t(double x)
         bool small = false;
         while (k < 100) {
             rk *= x;
-            ds = div_k<false>(rk, kKT.row[k].d2, kKT.row[k].y2);
+            ds = div_k<false>(rk, kKT.row[k].d2, kKT.row[k].y2, kKT.row[k].l2);
             sum += ds;
             small = wave_any(ds < big);
             if (small) break;
@@ -205,7 +215,7 @@ NUSI_FN double series_2_t(double x)
     if (!done)
         for (; k < 100; k++) {
             rk *= x;
-            const double ds = div_k<kExact>(rk, kKT.row[k].d2, kKT.row[k].y2);
+            const double ds = div_k<kExact>(rk, kKT.row[k].d2, kKT.row[k].y2, kKT.row[k].l2);
             sum += ds;
             if (quot_lt<kExact>(fabs(ds), fabs(sum), 0x1p-53)) break;   // fabs(ds / sum) < 0.5 GSL_DBL_EPSILON
         }
@@ -339,8 +349,8 @@ NUSI_FN void cseries_t(bool s2, double r, double lr, double x, double y, double&
         sk = sk - (alpha * sk - beta * ck_tmp);
         rk *= r;
         const double d = t2 ? kr.d2 : kr.d1;   // (double) k * k * (k + 1.0) or (double) k * k
-        const double yk = t2 ? kr.y2 : kr.y1;
-        q = div_k<kExact>(rk, d, yk);
+        const double yk = t2 ? kr.y2 : kr.y1, lk = t2 ? kr.l2 : kr.l1;
+        q = div_k<kExact>(rk, d, yk, lk);
         dr = q * ck;
         di = q * sk;
         real_sum += dr;
