@@ -365,12 +365,24 @@ NUSI_FN void cseries_t(bool s2, double r, double lr, double x, double y, double&
         // added, then each lane's test at k -- false for the lanes still above it)
         const double big = r * 0x1p-50;
         bool small = false;
-        while (wave_all(k < kmax)) {
+        // two terms per kmax vote while both are below every lane's kmax (the same terms and exit as one at a time)
+        while (wave_all(k + 1 < kmax)) {
+            term(k);
+            small = wave_any(q < big);
+            if (small) break;
+            ++k;
             term(k);
             small = wave_any(q < big);
             if (small) break;
             ++k;
         }
+        if (!small)
+            while (wave_all(k < kmax)) {
+                term(k);
+                small = wave_any(q < big);
+                if (small) break;
+                ++k;
+            }
         if (small) {
             done = stop();
             ++k;
