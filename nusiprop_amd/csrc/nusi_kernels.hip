@@ -348,7 +348,7 @@ constexpr bool kBatchPipe = NUSI_BATCH_PIPE != 0;
 #define NUSI_REFO_PREFETCH 1
 #endif
 constexpr bool kRefPrefetch = NUSI_REFO_PREFETCH != 0;
-#ifndef NUSI_REFO_BSTUB   // timing A/B only (wrong tables): bit 0 the batch kernel without A, bit 1 without the block's loads
+#ifndef NUSI_REFO_BSTUB   // timing A/B only (wrong tables): bit 1 the batch kernel without the block's loads
 #define NUSI_REFO_BSTUB 0
 #endif
 __host__ __device__ inline int alpha_batch_lds_doubles()
@@ -360,6 +360,7 @@ __host__ __device__ inline int alpha_batch_lds_doubles()
 static_assert(kXFields * (kAlphaTile + 1) * (kAlphaTile + 1) >= 4 * (kAlphaTile + 1) * (kAlphaTile + 1) + kAlphaTile * 2 * (kAlphaTile + 1),
               "the bracket phase's blocks fit X");
 static_assert(kBatchQC * (2 * (kAlphaTile + 1) + kAlphaTile) <= kTileThreads, "one member-edge round per chunk");
+static_assert(3 + kBatchQC <= kXFields, "(kRef) the chunk's A fields fit X beside Dcr, Dci");
 
 #ifndef NUSI_BATCH_WAVES
 #define NUSI_BATCH_WAVES 4
@@ -607,6 +608,14 @@ void k_alpha_batch(GridDev g, const Point* __restrict__ pts, const SplineSet* __
                                        med + ((size_t)(p0 + q0 + mq) * 3 + k) * kMedFields * T, mv);
                 alpha_batch_medge_store(nonres, mjob, ct, cs, m0, Tm, mv, membq + mq * mbd);
             }
+            // (kRef) A of this thread's corner for the chunk's points, into X's fields 3 .. 3 + nq - 1 (free in the
+            // point loop): the reference's carg of the member quotient (b_marg) out of the per-point phases
+            if (kRef && moff >= 0) {
+                const int si = tid / ct, ti = tid - si * ct;
+                const double S = edgk[kTEdgeFields * ct + kSEdgeVal * cs + si], t = edgk[kTEdgeVal * ct + ti];
+#pragma unroll 1
+                for (int qq = 0; qq < nq; ++qq) X[(3 + qq) * kCC + tid] = b_marg(S, t, pts[p0 + q0 + qq].a_gr);
+            }
             constexpr bool pipe = kBatchPipe && !kRef;
             if (pipe) {
                 __syncthreads();   // member edges written
@@ -637,15 +646,6 @@ void k_alpha_batch(GridDev g, const Point* __restrict__ pts, const SplineSet* __
                                 const size_t o = (size_t)q * mc.NC + moff;
                                 if (!kRefPrefetch) mcv = mcb[o];
                                 X[tid] = mcv.x; X[kCC + tid] = mcv.y;
-                                {   // A of the corner for point q: alpha_member_ref's expression on the tile's S', t
-                                    const int si = tid / ct, ti = tid - si * ct;
-#if NUSI_REFO_BSTUB & 1   // timing A/B only: A not formed
-                                    X[2 * kCC + tid] = edgk[kTEdgeVal * ct + ti] * Q.a_gr;
-#else
-                                    X[2 * kCC + tid] = b_marg(edgk[kTEdgeFields * ct + kSEdgeVal * cs + si],
-                                                              edgk[kTEdgeVal * ct + ti], Q.a_gr);
-#endif
-                                }
                                 if (kRefPrefetch && q + 1 < nb && !(NUSI_REFO_BSTUB & 2)) mcv = mcb[o + mc.NC];
                             }
                         }
@@ -664,7 +664,7 @@ void k_alpha_batch(GridDev g, const Point* __restrict__ pts, const SplineSet* __
                     lv.sidx[0] = sl[lm]; lv.sidx[1] = sh[lm]; lv.tidx[0] = tl[ln]; lv.tidx[1] = th[ln];
                     lv.ted = edgk; lv.sed = edgk + kTEdgeFields * ct; lv.mbv = lv.sed + kSEdgeFields * cs;
                     lv.tedm = memb; lv.sedm = memb + ct; lv.mbm = memb + ct + 2 * cs;
-                    lv.marg = memb + ct + 2 * cs + kAlphaTile + 2 * ct;   // sT | fT | sS | fS
+                    lv.marg = kRef ? X + (3 + qq) * kCC : memb + ct + 2 * cs + kAlphaTile + 2 * ct;   // sT | fT | sS | fS
                     lv.xl = mix; lv.yl = mix;   // (not read with pre)
                     alpha_k<SplitLeavesT<kRef>, kPP>(Q, spl, k, g.lo[n], g.hi[n], g.lo[m], g.hi[m], lv, tot, w,
                                                      cornered ? &pre : nullptr, kPP && cornered ? &ppt : nullptr);

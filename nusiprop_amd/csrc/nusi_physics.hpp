@@ -973,7 +973,7 @@ NUSI_FN double alpha_phiphi_scale(const Point& P, double uk, const PPTerm& X)
 // Leaves of the big-batch tile kernel (k_alpha_batch): the shared corner fields live in separate blocks
 // (L, Drr, Dri persist for every mass state through the batch loop; LL, TU1, TU2, G and the mixed logs
 // only while the batch's shared brackets are formed), so each field has its own base pointer.  kRefA
-// (NUSI_OPT_REFERENCE_ORDER): A is a corner field of its own, corm[2 kCC + o] (alpha_mcorner_ref_job's).
+// (NUSI_OPT_REFERENCE_ORDER): A is a corner field of its own, marg[o] (the batch kernel's per-point A block).
 // The big-batch kernel's corner blocks (P3, X, mem) keep their fields kCC doubles apart, a compile-time stride, so that
 // every field of a corner is one LDS load at an immediate offset from the same address.
 constexpr int kCC = (kAlphaTile + 1) * (kAlphaTile + 1);
@@ -981,7 +981,7 @@ template <bool kRefA = false>
 struct SplitLeavesT {
     const double* cf[kCornerShared];   // L LL TU1 TU2 G Drr Dri, each [cc]
     const double *corm, *ted, *sed, *mbv, *tedm, *sedm, *mbm, *xl, *yl;
-    const double* marg;                // sT [ct] | fT [ct] | sS [cs] | fS [cs]: A from the edge arguments
+    const double* marg;                // sT [ct] | fT [ct] | sS [cs] | fS [cs]: A from the edge arguments (kRefA: A [cc])
     int cc, ct, cs, mb, nb;
     int sidx[2], tidx[2];
     NUSI_FN AlphaCorner corner(int si, int ti, double, double) const
@@ -989,7 +989,7 @@ struct SplitLeavesT {
         const int o = sidx[si] * ct + tidx[ti];
         const int a = sidx[si], b = tidx[ti];
         // A = arg(S - 1 + i gr) + arg(c + i gr) - pi, the expression of alpha_member_corner
-        const double A = kRefA ? corm[2 * kCC + o] : (marg[2 * ct + a] + marg[b]) + (marg[2 * ct + cs + a] + marg[ct + b] - 1.0) * kPi;
+        const double A = kRefA ? marg[o] : (marg[2 * ct + a] + marg[b]) + (marg[2 * ct + cs + a] + marg[ct + b] - 1.0) * kPi;
         return AlphaCorner{cf[0][o], cf[1][o], cf[2][o], cf[3][o], cf[4][o], cf[5][o], cf[6][o],
                            corm[o], corm[kCC + o], A};
     }
