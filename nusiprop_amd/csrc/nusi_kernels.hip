@@ -614,7 +614,12 @@ void k_alpha_batch(GridDev g, const Point* __restrict__ pts, const SplineSet* __
                 const int si = tid / ct, ti = tid - si * ct;
                 const double S = edgk[kTEdgeFields * ct + kSEdgeVal * cs + si], t = edgk[kTEdgeVal * ct + ti];
 #pragma unroll 1
-                for (int qq = 0; qq < nq; ++qq) X[(3 + qq) * kCC + tid] = b_marg(S, t, pts[p0 + q0 + qq].a_gr);
+                for (int qq = 0; qq < nq; ++qq)
+#ifdef NUSI_REFO_AINLINE   // A/B: inline
+                    X[(3 + qq) * kCC + tid] = alpha_member_ref_arg(S, t, pts[p0 + q0 + qq].a_gr);
+#else
+                    X[(3 + qq) * kCC + tid] = b_marg(S, t, pts[p0 + q0 + qq].a_gr);
+#endif
             }
             constexpr bool pipe = kBatchPipe && !kRef;
             if (pipe) {
