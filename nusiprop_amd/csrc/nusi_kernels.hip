@@ -377,8 +377,6 @@ NUSI_BCOLD void b_corner(int j, const double* edgk, int ct, int cs, double* per,
     alpha_batch_corner_job<kRef>(j, edgk, ct, cs, per, tmp);
 #endif
 }
-// (kRef) A of a member corner, out of line: inline, its atan2 raised the point loop's spills 53 -> 85
-NUSI_BCOLD double b_marg(double S, double t, double gr) { return alpha_member_ref_arg(S, t, gr); }
 NUSI_BCOLD void b_xshared(int j, const double* edgk, int ct, int cs, double* X) { alpha_batch_xshared_job(j, edgk, ct, cs, X); }
 // The leaves the batch's shared brackets read (alpha_k_pre, alpha_k_pp): the shared corner blocks P3 | tmp, the
 // edge block edgk and the mixed logs; no member leaf
@@ -609,17 +607,14 @@ void k_alpha_batch(GridDev g, const Point* __restrict__ pts, const SplineSet* __
                 alpha_batch_medge_store(nonres, mjob, ct, cs, m0, Tm, mv, membq + mq * mbd);
             }
             // (kRef) A of this thread's corner for the chunk's points, into X's fields 3 .. 3 + nq - 1 (free in the
-            // point loop): the reference's carg of the member quotient (b_marg) out of the per-point phases
+            // point loop): the reference's carg of the member quotient, out of the per-point phases (formed per point
+            // between their barriers, out of line, it cost 1.23 ms of C4's 7.96; here 7.28 ms in all, profiles/r5/r6p)
             if (kRef && moff >= 0) {
                 const int si = tid / ct, ti = tid - si * ct;
                 const double S = edgk[kTEdgeFields * ct + kSEdgeVal * cs + si], t = edgk[kTEdgeVal * ct + ti];
 #pragma unroll 1
-                for (int qq = 0; qq < nq; ++qq)
-#ifdef NUSI_REFO_AINLINE   // A/B: inline
+                for (int qq = 0; qq < nq; ++qq)   // (inline here: 7.42 -> 7.28 ms against b_marg's call, r6p)
                     X[(3 + qq) * kCC + tid] = alpha_member_ref_arg(S, t, pts[p0 + q0 + qq].a_gr);
-#else
-                    X[(3 + qq) * kCC + tid] = b_marg(S, t, pts[p0 + q0 + qq].a_gr);
-#endif
             }
             constexpr bool pipe = kBatchPipe && !kRef;
             if (pipe) {
