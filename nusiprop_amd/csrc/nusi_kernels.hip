@@ -377,6 +377,8 @@ NUSI_BCOLD void b_corner(int j, const double* edgk, int ct, int cs, double* per,
     alpha_batch_corner_job<kRef>(j, edgk, ct, cs, per, tmp);
 #endif
 }
+// (kRef, kPP) A of a member corner, out of line (the phi-phi instance's point loop spills more with it inline)
+NUSI_BCOLD double b_marg(double S, double t, double gr) { return alpha_member_ref_arg(S, t, gr); }
 NUSI_BCOLD void b_xshared(int j, const double* edgk, int ct, int cs, double* X) { alpha_batch_xshared_job(j, edgk, ct, cs, X); }
 // The leaves the batch's shared brackets read (alpha_k_pre, alpha_k_pp): the shared corner blocks P3 | tmp, the
 // edge block edgk and the mixed logs; no member leaf
@@ -613,8 +615,9 @@ void k_alpha_batch(GridDev g, const Point* __restrict__ pts, const SplineSet* __
                 const int si = tid / ct, ti = tid - si * ct;
                 const double S = edgk[kTEdgeFields * ct + kSEdgeVal * cs + si], t = edgk[kTEdgeVal * ct + ti];
 #pragma unroll 1
-                for (int qq = 0; qq < nq; ++qq)   // (inline here: 7.42 -> 7.28 ms against b_marg's call, r6p)
-                    X[(3 + qq) * kCC + tid] = alpha_member_ref_arg(S, t, pts[p0 + q0 + qq].a_gr);
+                for (int qq = 0; qq < nq; ++qq)   // (inline: C4 7.42 -> 7.28 ms, r6p; kPP, whose point loop holds
+                    X[(3 + qq) * kCC + tid] =     // the phi-phi term too, as a call: C3 12.33 -> 11.24 ms, r6q)
+                        kPP ? b_marg(S, t, pts[p0 + q0 + qq].a_gr) : alpha_member_ref_arg(S, t, pts[p0 + q0 + qq].a_gr);
             }
             constexpr bool pipe = kBatchPipe && !kRef;
             if (pipe) {

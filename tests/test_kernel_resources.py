@@ -19,9 +19,10 @@ LLVM = "/opt/rocm/lib/llvm/bin"
 BUDGET = {
     r"k_alpha_batchILb[01]ELb0E": (64, 1024),  # call frames of the out-of-line per-batch phases
     # the reference-order instances: the member-corner offset and one point's prefetched corner (k_alpha_mcorner's
-    # block) live across the point loop; 128 VGPRs (4 waves per SIMD) held by keeping the complex GSL series out of
-    # the kernel's call graph (gsl_cli2_real for the shared real-axis corners)
-    r"k_alpha_batchILb[01]ELb1E": (80, 1024),
+    # block) live across the point loop, and (non-phi-phi instance) the chunk's A inline -- faster than as a call
+    # despite the spills (profiles/r5/r6p); 128 VGPRs (4 waves per SIMD) held by keeping the complex GSL series out
+    # of the kernel's call graph (gsl_cli2_real for the shared real-axis corners)
+    r"k_alpha_batchILb[01]ELb1E": (96, 1024),
     # the block-synchronous cascade: 96 B of private segment are the prologue's pow() call frames (no spills)
     r"k_cascade_bsILi(16|32)ELi1ELi1ELi4ELi1E": (0, 96),
     # (the wave index is readfirstlane'd: per-wave row bases in SGPRs; as VGPRs they spilled 19 / 33 into the push)
