@@ -365,6 +365,13 @@ static_assert(3 + kBatchQC <= kXFields, "(kRef) the chunk's A fields fit X besid
 #ifndef NUSI_BATCH_WAVES
 #define NUSI_BATCH_WAVES 4
 #endif
+// waves per SIMD of k_alpha_batch: 4 (128 VGPRs; the LDS holds four workgroups per CU), except the reference-order
+// instance without phi-phi at 3 (168 VGPRs: its spills 82 -> 28, C4 7.28 -> 6.78 ms; the default-order instance is
+// equal at 3, the phi-phi reference-order one slower: C3 11.1 -> 12.0 ms per chunk, profiles/r5/r6u)
+#ifndef NUSI_BATCH_WAVES_REFO
+#define NUSI_BATCH_WAVES_REFO 3
+#endif
+constexpr int batch_waves(bool pp, bool ref) { return ref && !pp ? NUSI_BATCH_WAVES_REFO : NUSI_BATCH_WAVES; }
 // the batch-shared phases out of line: they run once per batch, and inlined their working sets raise the register
 // pressure of the per-point loop (measured slower: round 1 profiles/r1e, round 2 profiles/r2s, r2aa)
 #define NUSI_BCOLD __device__ __attribute__((noinline))
@@ -476,7 +483,7 @@ void mcorner_edges(int T, const double* lo, const double* hi, std::vector<int>& 
 // the X block, which then holds no Taylor coefficients; pc0: the first table of the launch chunk), the rest of the
 // batch structure unchanged
 template <bool kPP, bool kRef>
-__global__ __launch_bounds__(kTileThreads) __attribute__((amdgpu_waves_per_eu(NUSI_BATCH_WAVES, NUSI_BATCH_WAVES)))
+__global__ __launch_bounds__(kTileThreads) __attribute__((amdgpu_waves_per_eu(batch_waves(kPP, kRef), batch_waves(kPP, kRef))))
 void k_alpha_batch(GridDev g, const Point* __restrict__ pts, const SplineSet* __restrict__ splp, const int* __restrict__ tiles,
                    const int* __restrict__ batches, double* __restrict__ A, const double* __restrict__ med,
                    int* __restrict__ warn, int* __restrict__ wmin, MCornerDev mc, int pc0)
