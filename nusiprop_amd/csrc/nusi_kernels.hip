@@ -434,7 +434,14 @@ __global__ __launch_bounds__(256) void k_alpha_medge(GridDev g, const Point* __r
 // ns per call against 0.06, scripts/dev/gsl_bench.hip).  The values pass through LDS to leave as runs of cb corners
 // per (field, table), the layout the batch kernel reads a tile's corner rows from.
 constexpr int kMcJobs = 1024;
-__global__ __launch_bounds__(256) void k_alpha_mcorner(const Point* __restrict__ pts, const int* __restrict__ batches,
+#ifndef NUSI_MC_WAVES   // A/B: waves per SIMD the member-corner kernel is built for (0: the compiler's choice)
+#define NUSI_MC_WAVES 0
+#endif
+__global__ __launch_bounds__(256)
+#if NUSI_MC_WAVES
+__attribute__((amdgpu_waves_per_eu(NUSI_MC_WAVES, NUSI_MC_WAVES)))
+#endif
+void k_alpha_mcorner(const Point* __restrict__ pts, const int* __restrict__ batches,
                                                        MCornerDev mc, int pc0, int jobs)
 {
     __shared__ double v[2 * kMcJobs];   // [q][cl][Dcr, Dci]
