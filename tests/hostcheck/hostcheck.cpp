@@ -129,4 +129,11 @@ double hc_gsl_li2(double x) { return nusi::gsl_li2(x); }
 void hc_gsl_cli2(double x, double y, double* re, double* im) { const nusi::cd r = nusi::gsl_cli2(x, y); *re = r.r; *im = r.i; }
 double hc_gsl_clausen(double x) { return nusi::gsl::clausen(x); }
 double hc_hypot(double x, double y) { return nusi::gsl::hypot(x, y); }
+// the series' per-k table row (d1, d2, y1, y2, l1, l2) and its division, for the two-part-reciprocal test
+void hc_gsl_krow(int k, double* o)
+{
+    const nusi::gsl::KRow& r = nusi::gsl::kKT.row[k];
+    o[0] = r.d1; o[1] = r.d2; o[2] = r.y1; o[3] = r.y2; o[4] = r.l1; o[5] = r.l2;
+}
+double hc_gsl_div_k(double a, double d, double y, double l) { return nusi::gsl::div_k<false>(a, d, y, l); }
 }

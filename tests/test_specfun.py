@@ -227,3 +227,26 @@ def test_gsl_complex_dilog_conjugate_symmetric(oracle_mod, hlib):
         assert b[0] == a[0] and b[1] == -a[1], (x, y, a, b)
         hlib.hc_gsl_cli2(float(x), float(-y), ctypes.byref(re), ctypes.byref(im))
         assert re.value == a[0] and im.value == -a[1], (x, y)
+
+
+def test_gsl_series_division_two_part_reciprocal(hlib):
+    """GSL's series terms r^k / d_k on the device are fma(a, y_k, RN(a l_k)) with the table's two-part reciprocal
+    (nusi_gsl.hpp header): every row's y_k = RN(1 / d_k) and l_k = RN(1 / d_k - y_k) exactly (rational arithmetic),
+    and the device's division equals IEEE a / d_k on seeded a over the series' range of binades for every k."""
+    import random
+    from fractions import Fraction as F
+    hlib.hc_gsl_krow.argtypes = [ctypes.c_int, ctypes.POINTER(D)]
+    hlib.hc_gsl_div_k.restype = D
+    hlib.hc_gsl_div_k.argtypes = [D, D, D, D]
+    row = (D * 6)()
+    rng = random.Random(20261018)
+    for k in range(2, 1000):
+        hlib.hc_gsl_krow(k, row)
+        d1, d2, y1, y2, l1, l2 = list(row)
+        assert d1 == float(k * k) and d2 == float(k * k * (k + 1))
+        for d, y, l in ((d1, y1, l1), (d2, y2, l2)):
+            assert y == 1.0 / d
+            assert l == float(F(1) / F(d) - F(y)), (k, d)
+            for _ in range(40):
+                a = rng.uniform(0.5, 1.0) * 2.0 ** rng.randint(-470, 0)
+                assert hlib.hc_gsl_div_k(a, d, y, l) == a / d, (k, d, a)
