@@ -291,8 +291,8 @@ def single_point_latency(pt, reps, refo=False):
     h = ctypes.c_void_p()
     _lib.check(L.nusi_create(ctypes.byref(_lib.make_params(source_model=src, **p)), ctypes.byref(h)))
     try:
-        if refo:
-            _lib.check(L.nusi_set_option(h, _lib.OPT_REFERENCE_ORDER, 1))
+        # (the object API's default is the reference order since round 6; the shared order is the opt-in)
+        _lib.check(L.nusi_set_option(h, _lib.OPT_REFERENCE_ORDER, 1 if refo else 0))
         out = (ctypes.c_double * (3 * p["N_bins_E"]))()
         for _ in range(3):
             _lib.check(L.nusi_evolve(h))
@@ -522,6 +522,33 @@ def dry_run(args, world, rank):
         dist.destroy_process_group()
 
 
+def pmc_summary_path(workload, reference_order):
+    """The committed PMC summary of a workload in one table arithmetic: profiles/pmc_traffic_<workload>.json for the
+    reference order (the library default), ..._<workload>_shared.json for the opt-in shared order
+    (scripts/gpu_profile_all.sh)."""
+    return os.path.join(ROOT, "profiles", "pmc_traffic_%s%s.json" % (workload, "" if reference_order else "_shared"))
+
+
+def load_pmc(path, lib_sha, order):
+    """(summary, source, note): the PMC summary at `path` if it describes the loaded library (its libnusi_sha256) in
+    the table arithmetic this run times (its table_order, "reference" / "shared"); otherwise an empty summary -- no
+    traffic, no flops, no roofline from it -- and a note saying why.  Counters of another binary or of the other
+    arithmetic are not this run's kernels (the shared-order line had been priced with the reference
+    order's flops)."""
+    if not path or not os.path.exists(path):
+        return {}, None, None
+    with open(path) as fh:
+        pmc = json.load(fh)
+    src = os.path.relpath(path, ROOT)
+    if pmc.get("libnusi_sha256") != lib_sha:
+        return {}, src, "%s was collected on libnusi.so %s, not the loaded %s: traffic / flops dropped" % (
+            src, str(pmc.get("libnusi_sha256"))[:12], lib_sha[:12])
+    if pmc.get("table_order") != order:
+        return {}, src, "%s was collected in the %s table order, this run times the %s order: traffic / flops dropped" % (
+            src, pmc.get("table_order"), order)
+    return pmc, src, None
+
+
 def main():
     args = parse()
     rc = launch_ranks(args)
@@ -576,8 +603,7 @@ def run(args, world, rank, local, dist, plan, pts, desc, pp_tables):
         plan.set_option(_lib.OPT_SHIFT_REUSE, 128)
     if args.rhs:
         plan.set_option(_lib.OPT_CASCADE_RHS, args.rhs)
-    if args.reference_order:
-        plan.set_option(_lib.OPT_REFERENCE_ORDER, 1)
+    plan.set_option(_lib.OPT_REFERENCE_ORDER, 1 if args.reference_order else 0)   # (the library default is 1)
     order = "reference" if args.reference_order else "shared-algorithm"
     dev = torch.device("cuda", local)
     flux = torch.empty((P, 3, plan.N), dtype=torch.float64, device=dev)
@@ -618,21 +644,12 @@ def run(args, world, rank, local, dist, plan, pts, desc, pp_tables):
     casc_bytes = scan.cascade_bytes_per_point(N, Nz) * P
     casc_s = sum_ms[2] / max(ncalls, 1) / 1e3
     alpha_s = sum_ms[1] / max(ncalls, 1) / 1e3
-    traffic, tsrc, pmc = None, None, {}
     lib_sha = file_sha256(_lib.LIB_PATH)
     tj = args.traffic_json
     if not tj and not args.points:
-        tj = os.path.join(ROOT, "profiles", "pmc_traffic_%s.json" % args.workload)
-    pmc_note = None
-    if tj and os.path.exists(tj):
-        with open(tj) as fh:
-            pmc = json.load(fh)
-        tsrc = os.path.relpath(tj, ROOT)
-        if pmc.get("libnusi_sha256") != lib_sha:   # counters of another binary: not this kernel's traffic
-            pmc_note = "%s was collected on libnusi.so %s, not the loaded %s: traffic / flops dropped" % (
-                tsrc, str(pmc.get("libnusi_sha256"))[:12], lib_sha[:12])
-            pmc = {}
-        traffic = pmc.get("k_cascade_bytes_per_launch")
+        tj = pmc_summary_path(args.workload, args.reference_order)
+    pmc, tsrc, pmc_note = load_pmc(tj, lib_sha, "reference" if args.reference_order else "shared")
+    traffic = pmc.get("k_cascade_bytes_per_launch")
     achieved = casc_bytes / casc_s / 1e9
     # workgroups that read a table, and the bytes / matrix-core flops they must move / issue
     readers = P
@@ -674,7 +691,8 @@ def run(args, world, rank, local, dist, plan, pts, desc, pp_tables):
                    "lEmax": p0["lEmax"], "parallelism": "independent points, %d GPU(s), no collective" % world,
                    "alpha_kernel": alpha_kernel, "cascade_kernel": casc_kernel, "cascade_kind": args.cascade,
                    "cascade_rhs": args.rhs or "auto",
-                   "table_order": order + (" (NUSI_OPT_REFERENCE_ORDER)" if args.reference_order else " (default)"),
+                   "table_order": order + (" (NUSI_OPT_REFERENCE_ORDER = 1, the library default)" if args.reference_order
+                                           else " (NUSI_OPT_REFERENCE_ORDER = 0, opt-in)"),
                    "process_group": dist.get_backend() if dist is not None else None},
         "libnusi": {"path": os.path.relpath(_lib.LIB_PATH, ROOT), "sha256": lib_sha, "pmc_source": tsrc,
                     "pmc_note": pmc_note},
@@ -728,7 +746,12 @@ def run(args, world, rank, local, dist, plan, pts, desc, pp_tables):
                                     "from the PMC pass; time = the kernel's HIP events in this run",
                            "note": "dominant kernel (alpha_table.share_of_step); fp64 vector-ALU bound "
                                    "(transcendental leaves), neither HBM nor MFMA"}
-    else:   # the cascade dominates (C5's gamma batches), or no alpha counters for this binary
+    elif alpha_s >= casc_s:   # the alpha table dominates, but no counters of this binary in this arithmetic
+        out["roofline"] = {"bound": "valu", "kernel": alpha_kernel, "achieved": None, "peak": FP64_PEAK_TFLOPS,
+                           "unit": "TFLOP/s", "frac": None, "traffic": None, "traffic_source": tsrc,
+                           "note": "no executed-flop count for the dominant kernel: " + (
+                               pmc_note or "no PMC summary of this workload (scripts/gpu_profile_all.sh)")}
+    else:   # the cascade dominates (C5's gamma batches)
         out["roofline"] = dict(out["roofline_cascade"])
     if dist is not None and args.workload in ("c4", "c4s", "c5"):
         # the scan's only data exchange, after the timed region: the fluxes of every rank's block gathered to rank 0

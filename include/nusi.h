@@ -106,7 +106,8 @@ int nusi_get_energies(const nusi_handle *h, double *out_N);    /* get_energy(i) 
 int nusi_get_N_bins_E(const nusi_handle *h);                   /* get_N_bins_E()    :407-410 */
 int nusi_get_N_steps_z(const nusi_handle *h);
 int nusi_get_warnings(const nusi_handle *h);                   /* NUSI_WARN_* of the last evolve */
-/* names of the alpha-table and cascade kernels the last evolve() launched (static strings; no reference
+/* names of the alpha-table and cascade kernels this object's last evolve() launched (strings owned by the object,
+ * valid until its next evolve() or nusi_destroy; a nusi_copy keeps its source's names); no reference
  * counterpart -- reports and tests) */
 int nusi_get_kernels(const nusi_handle *h, const char **alpha, const char **cascade);
 /* nusi_plan_set_option on the object's plan (NUSI_OPT_*; kept by nusi_copy).  No reference counterpart. */
@@ -209,19 +210,24 @@ int nusi_plan_set_cascade(nusi_plan *plan, int kind);
 #define NUSI_OPT_CASCADE_RHS 3
 #define NUSI_OPT_STEP_PASSES 4
 #define NUSI_OPT_SHIFT_REUSE 5
-/*   NUSI_OPT_REFERENCE_ORDER  1 = build Gamma / alphaTilde / alpha in the
- *                          reference's own arithmetic: every gsl_sf_dilog /
+/*   NUSI_OPT_REFERENCE_ORDER  1 (DEFAULT, plans and objects) = build Gamma /
+ *                          alphaTilde / alpha in the reference's own
+ *                          arithmetic: every gsl_sf_dilog /
  *                          gsl_sf_complex_dilog_xy_e call site by GSL's own
  *                          algorithms (dilog.c restated, nusi_gsl.hpp), and
  *                          the alpha table's s-t interference member leaves
  *                          as the dilogarithm of the reference's quotient
  *                          (1+S+t)/(2 - i gr + t) and carg of its expression
  *                          (nuSIprop.hpp:1428-1467, 843-878, 1135-1192).
- *                          0 = the shared-algorithm order (Bernoulli series,
- *                          batch-shared Taylor coefficients; faster).  Both
- *                          are bit-identical to the oracle in the matching
- *                          mode; they differ from each other where the
- *                          closed forms cancel. */
+ *                          Fluxes <= 1e-11 of the GSL-restating oracle on
+ *                          every tested config.
+ *                          0 = opt-in fast mode, the shared-algorithm order
+ *                          (Bernoulli series, batch-shared Taylor
+ *                          coefficients; ~3x faster Stage A).  Bit-identical
+ *                          to the oracle's default mode, but where the closed
+ *                          forms cancel it differs from the reference's
+ *                          arithmetic by up to 2.5e-6 (C2a) / 1.3e-7 (C4 at
+ *                          g = 1) in a flux. */
 #define NUSI_OPT_REFERENCE_ORDER 6
 /*   NUSI_OPT_CASCADE_SYNC  the MFMA cascade's synchronisation: 0 = automatic
  *                          = 2 = the block-synchronous kernel k_cascade_bs
@@ -231,8 +237,9 @@ int nusi_plan_set_cascade(nusi_plan *plan, int kind);
  *                          were removed in round 5. */
 #define NUSI_OPT_CASCADE_SYNC 7
 /*   NUSI_OPT_REFO_CORNER_MB  the reference-order big-batch kernel's member-
- *                          corner block (9 doubles per table, pair of bin
- *                          edges and mass state: 5.6 MB per table at
+ *                          corner block (per table and pair of bin edges,
+ *                          Dc = Li2(quotient) as re/im for each of the 3
+ *                          mass states: 6 doubles, 3.7 MB per table at
  *                          N_E = 300): at most this many MiB, the batches run
  *                          in chunks that fit (at least one batch); 0 =
  *                          automatic (8 GiB, at most half the free memory).

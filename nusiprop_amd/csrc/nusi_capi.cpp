@@ -426,7 +426,8 @@ struct nusi_plan {
     double* d_fh = nullptr;         // k_cascade_bs's F FIFO between step passes, cascade_bs_scratch_doubles per workgroup
     int step_passes = 0;            // NUSI_OPT_STEP_PASSES: 1 = the step-pass instance of k_cascade_bs also where one pass fits
     int shift_max = 0;              // NUSI_OPT_SHIFT_REUSE: K, the largest bin offset served by a base table set
-    int ref_order = 0;              // NUSI_OPT_REFERENCE_ORDER: 1 = the tables in the reference's operation order
+    int ref_order = 1;              // NUSI_OPT_REFERENCE_ORDER: 1 (default) = the tables in the reference's own arithmetic,
+                                    // 0 = the shared-algorithm order (opt-in fast mode)
     int cascade_sync = 0;           // NUSI_OPT_CASCADE_SYNC: 0 = auto, 2 = block-synchronous (the same kernel; 1 is refused)
     int corner_mb = 0;              // NUSI_OPT_REFO_CORNER_MB: the member-corner block's budget (0 = automatic)
     size_t fh_doubles = 0;          // capacity of d_fh in doubles (the block-synchronous kernels' FIFOs)
@@ -607,9 +608,11 @@ int mcorner_ensure(nusi_plan* p, int ntab, const AlphaBatches& ab, int budget_mb
         mc.U = (int)ue.size();
         mc.NC = (long long)mc.U * (mc.U + 1) / 2;
     }
+    const size_t per = sizeof(double) * 6 * (size_t)mc.NC;
+    if (mc.buf && budget_mb == 0 && mc.cap_tables >= ntab && per * mc.cap_tables <= kMCornerBudget)
+        return NUSI_OK;   // every table of the call fits the block already (no hipMemGetInfo per call)
     int nbmax = 1;
     for (int b = 0; b < ab.nbatch; ++b) nbmax = std::max(nbmax, (int)((unsigned)p->h_batches[b] >> 24));
-    const size_t per = sizeof(double) * 6 * (size_t)mc.NC;
     size_t fr = 0, tot = 0;
     if (hipMemGetInfo(&fr, &tot) != hipSuccess) fr = kMCornerBudget;
     const size_t budget = budget_mb > 0 ? ((size_t)budget_mb << 20)
@@ -1104,6 +1107,17 @@ int nusi_plan_evolve(nusi_plan* pl, const nusi_params* pts, int n, double* d_flu
         pl->src_cap = pl->max_points;
         pl->tabs.Src = pl->d_src;
     }
+    // NUSI_OPT_REFERENCE_ORDER on the big-batch kernel: the member-corner blocks sized (allocations, the edge maps'
+    // synchronous upload) before the first event of the call and before any fork to the side stream
+    const bool refo = pl->ref_order != 0;
+    const bool mcorn = refo && pl->alpha_kind == 0;
+    if (mcorn && nd && nbatch) {
+        AlphaBatches ab;
+        ab.nbatch = nbatch;
+        if (int r = mcorner_ensure(pl, nd, ab, pl->corner_mb)) return r;
+    }
+    if (mcorn && nbase && pl->shift_batches.nbatch)
+        if (int r = mcorner_ensure(pl->shift, nbase, pl->shift_batches, pl->corner_mb)) return r;
     if (ngb) {
         HIPCHECK(hipMemcpyAsync(pl->d_gidx, pl->h_gidx, sizeof(int) * ngidx, hipMemcpyHostToDevice, s));
         HIPCHECK(hipMemcpyAsync(pl->d_gbgrp, pl->h_gbgrp, sizeof(int2) * ngb, hipMemcpyHostToDevice, s));
@@ -1128,15 +1142,28 @@ int nusi_plan_evolve(nusi_plan* pl, const nusi_params* pts, int n, double* d_flu
     hipEvent_t* ev = pl->ev;
     if (pl->prof_n < pl->prof_max) ev = &pl->prof_ev[4 * (size_t)pl->prof_n++];
     HIPCHECK(hipEventRecord(ev[0], s));
-    const bool refo = pl->ref_order != 0;
     // A call of few tables leaves most of the GPU idle in each Stage-A kernel: Gamma / alphaTilde (independent of
     // alpha) run on the side stream beside the alpha kernels, and the cascade waits for both.  (Stage times: ev[1]
     // is then Gamma / alphaTilde's end on the side stream, and the alpha stage counts from there.)  Scans keep the
     // stages in order: beside a full alpha launch the overlap measured no gain (C4 155.0 -> 155.4 k, round 4).
     const bool ovl = !sp && nd > 0 && nd <= kOverlapTables;
+    // after a fork, any early error return still joins the side stream into s (the next call's memsets and table
+    // writes on s must not race a still-running Gamma / alphaTilde kernel)
+    struct SideJoin {
+        hipStream_t s = nullptr, side = nullptr;
+        hipEvent_t done = nullptr;
+        bool armed = false;
+        ~SideJoin()
+        {
+            if (!armed) return;
+            if (hipEventRecord(done, side) != hipSuccess) (void)hipStreamSynchronize(side);
+            else (void)hipStreamWaitEvent(s, done, 0);
+        }
+    } join{s, pl->side, pl->ev_fork, false};
     if (ovl) {
         HIPCHECK(hipEventRecord(pl->ev_fork, s));
         HIPCHECK(hipStreamWaitEvent(pl->side, pl->ev_fork, 0));
+        join.armed = true;
         HIPCHECK(nusi::launch_gamma_alphat(pl->gd, pl->d_tpts, nd, spl, pl->tabs, pl->d_warn, pl->side, refo));
         HIPCHECK(hipEventRecord(ev[1], pl->side));
     } else {
@@ -1144,25 +1171,20 @@ int nusi_plan_evolve(nusi_plan* pl, const nusi_params* pts, int n, double* d_flu
         if (sp) HIPCHECK(nusi::launch_gamma_alphat(sp->gd, sp->d_tpts, nbase, spl, sp->tabs, sp->d_warn, s, refo));
         HIPCHECK(hipEventRecord(ev[1], s));
     }
-    const bool mcorn = refo && pl->alpha_kind == 0;   // (the big-batch kernel's member-corner block)
     if (nd) {
-        if (mcorn && nbatch) {
-            AlphaBatches ab;
-            ab.nbatch = nbatch;
-            if (int r = mcorner_ensure(pl, nd, ab, pl->corner_mb)) return r;
-        }
         HIPCHECK(nusi::launch_alpha(pl->gd, pl->d_tpts, nd, spl, pl->atiles, pl->tabs, pl->d_warn, s, pl->d_batches,
                                     nbatch, cap, pl->alpha_kind, nb_plain, refo, pl->h_batches, &pl->mc));
     }
     if (sp) {
         const AlphaBatches& bb = pl->shift_batches;
-        if (mcorn && bb.nbatch)
-            if (int r = mcorner_ensure(sp, nbase, bb, pl->corner_mb)) return r;
         HIPCHECK(nusi::launch_alpha(sp->gd, sp->d_tpts, nbase, spl, sp->atiles, sp->tabs, sp->d_warn, s, sp->d_batches,
                                     bb.nbatch, bb.cap, pl->alpha_kind, bb.nb_plain, refo, sp->h_batches, &sp->mc));
         HIPCHECK(nusi::launch_table_shift(pl->gd, sp->gd, pl->d_smap, nd, ntab - nd, sp->tabs, pl->tabs, pl->d_warn, s));
     }
-    if (ovl) HIPCHECK(hipStreamWaitEvent(s, ev[1], 0));
+    if (ovl) {
+        join.armed = false;
+        HIPCHECK(hipStreamWaitEvent(s, ev[1], 0));
+    }
     HIPCHECK(hipEventRecord(ev[2], s));
     if (bs && any_dsnb) HIPCHECK(nusi::launch_source_dsnb(pl->gd, pl->d_pts, n, pl->d_src, s));
     const char* gb_name = nullptr;
@@ -1403,7 +1425,8 @@ void pool_give(nusi_plan* pl)
     if (pl->max_points == 1 && !pl->shift) {
         // the defaults of nusi_plan_create
         pl->alpha_batch = pl->alpha_kind = pl->cascade_rhs = pl->step_passes = pl->shift_max = 0;
-        pl->ref_order = pl->cascade_sync = pl->corner_mb = 0;
+        pl->cascade_sync = pl->corner_mb = 0;
+        pl->ref_order = 1;
         pl->cascade_kind = NUSI_CASCADE_AUTO;
         pl->prof_max = pl->prof_n = 0;
         pl->spl.reset();
@@ -1426,6 +1449,8 @@ struct nusi_handle {
     bool evolved = false;      // an evolve() has run (norm_total is set)
     int warn = 0;
     std::map<int, int> opts;   // the last value nusi_set_option set per option, replayed by nusi_copy
+    std::string alpha_kernel, cascade_kernel;   // what this object's last evolve() launched (copied by nusi_copy;
+                                                // the pooled plan of a copy may have run another object's call)
     ~nusi_handle() { pool_give(plan); }
 };
 
@@ -1470,6 +1495,8 @@ int nusi_copy(const nusi_handle* src, nusi_handle** out)
     (*out)->norm_total = src->norm_total;
     (*out)->evolved = src->evolved;
     (*out)->warn = src->warn;
+    (*out)->alpha_kernel = src->alpha_kernel;
+    (*out)->cascade_kernel = src->cascade_kernel;
     for (const auto& o : src->opts) {
         r = nusi_set_option(*out, o.first, o.second);
         if (r) {
@@ -1509,6 +1536,8 @@ int nusi_evolve(nusi_handle* h)
     if (r) return r;
     h->norm_total = h->plan->h_pts[0].norm_total;
     h->evolved = true;
+    h->alpha_kernel = h->plan->alpha_kernel;
+    h->cascade_kernel = h->plan->cascade_kernel;
     int w = 0;
     r = nusi_plan_warnings(h->plan, &w, 1);
     h->warn = w & (NUSI_WARN_GAMMA | NUSI_WARN_ALPHATILDE | NUSI_WARN_ALPHA);
@@ -1564,7 +1593,9 @@ int nusi_set_option(nusi_handle* h, int option, int value)
 int nusi_get_kernels(const nusi_handle* h, const char** alpha, const char** cascade)
 {
     if (!h->evolved) return fail(NUSI_ESTATE, "no evolve has run on this object");
-    return nusi_plan_kernels(h->plan, alpha, cascade);
+    if (alpha) *alpha = h->alpha_kernel.c_str();
+    if (cascade) *cascade = h->cascade_kernel.c_str();
+    return NUSI_OK;
 }
 
 }  // extern "C"

@@ -365,13 +365,12 @@ static_assert(3 + kBatchQC <= kXFields, "(kRef) the chunk's A fields fit X besid
 #ifndef NUSI_BATCH_WAVES
 #define NUSI_BATCH_WAVES 4
 #endif
-// waves per SIMD of k_alpha_batch: 4 (128 VGPRs; the LDS holds four workgroups per CU).  NUSI_BATCH_WAVES_REFO=3
-// (the reference-order instance without phi-phi at 168 VGPRs) measured faster -- spills 82 -> 35, C4 7.28 -> 6.76 ms,
-// and the reference-order GPU tests green (profiles/r5/r6u, r6v) -- but is not the shipped default this round: the
-// PMC passes and the full GPU session of the shipped library (r6r, r6s) ran at 4.  The default-order instance is
-// equal at 3 and 4, the phi-phi reference-order one slower at 3 (C3 11.1 -> 12.0 ms per chunk)
+// waves per SIMD of k_alpha_batch: 4 (128 VGPRs; the LDS holds four workgroups per CU), and 3 for the reference-order
+// instance without phi-phi (NUSI_BATCH_WAVES_REFO, 168 VGPRs): spills 82 -> 35, C4 7.28 -> 6.76 ms (profiles/r5/r6u,
+// r6v; shipped in round 6).  The default-order instance is equal at 3 and 4, the phi-phi reference-order one slower at
+// 3 (C3 11.1 -> 12.0 ms per chunk)
 #ifndef NUSI_BATCH_WAVES_REFO
-#define NUSI_BATCH_WAVES_REFO 4
+#define NUSI_BATCH_WAVES_REFO 3
 #endif
 constexpr int batch_waves(bool pp, bool ref) { return ref && !pp ? NUSI_BATCH_WAVES_REFO : NUSI_BATCH_WAVES; }
 // the batch-shared phases out of line: they run once per batch, and inlined their working sets raise the register

@@ -29,11 +29,15 @@ def params_array(points, grid_args=None):
 
 
 class Plan:
-    def __init__(self, N_bins_E=300, lEmin=12.0, lEmax=17.0, zmax=5.0, max_points=1, device=0):
+    def __init__(self, N_bins_E=300, lEmin=12.0, lEmax=17.0, zmax=5.0, max_points=1, device=0, reference_order=None):
+        """reference_order: None = the library default (the reference's own arithmetic, NUSI_OPT_REFERENCE_ORDER = 1);
+        False = the shared-algorithm order (opt-in fast mode, include/nusi.h); True = the reference order explicitly."""
         L = _lib.load()
         self._h = ctypes.c_void_p()
         _lib.check(L.nusi_plan_create(int(device), int(N_bins_E), float(lEmin), float(lEmax), float(zmax),
                                       int(max_points), ctypes.byref(self._h)))
+        if reference_order is not None:
+            self.set_option(_lib.OPT_REFERENCE_ORDER, 1 if reference_order else 0)
         self.device = device
         self.max_points = max_points
         self.grid_args = (int(N_bins_E), float(lEmin), float(lEmax), float(zmax))
@@ -92,8 +96,8 @@ class Plan:
         auto), OPT_ALPHA_KERNEL (0 batch, 1 tile, 2 per entry), OPT_CASCADE_RHS (1 = one point per cascade
         workgroup), OPT_STEP_PASSES (1 = the step-pass cascade also where one pass fits), OPT_SHIFT_REUSE (K > 0:
         the opt-in scan mode sharing tables across m_phi on the r^(-o/2) lattice, o <= K; only tables with g <= 0.05
-        share, the others are built directly), OPT_REFERENCE_ORDER (1 = the tables in the reference's own arithmetic:
-        GSL's dilogarithm algorithms on the reference's arguments), OPT_REFO_CORNER_MB (the reference order's
+        share, the others are built directly), OPT_REFERENCE_ORDER (1, the default = the tables in the reference's own
+        arithmetic: GSL's dilogarithm algorithms on the reference's arguments; 0 = the shared-algorithm order), OPT_REFO_CORNER_MB (the reference order's
         member-corner block budget in MiB, 0 = automatic); include/nusi.h."""
         _lib.check(_lib.load().nusi_plan_set_option(self._h, int(option), int(value)))
 

@@ -22,20 +22,23 @@ class pyprop:  # noqa: N801  (name of the reference class)
     N_bins_E=300, lEmin=12.0, lEmax=17.0, zmax=5.0, flav=2, phiphi=True,
     source_model=SOURCE_DSNB (extension: SOURCE_POWER_LAW selects the
     reference's commented-out power-law source, nuSIprop.hpp:656),
-    reference_order=False (extension: NUSI_OPT_REFERENCE_ORDER, the tables in
-    the reference's own complex-dilogarithm arithmetic, include/nusi.h).
+    reference_order=True (extension: NUSI_OPT_REFERENCE_ORDER, the tables in
+    the reference's own dilogarithm arithmetic -- GSL's algorithms, the
+    library default; False selects the opt-in shared-algorithm order, faster
+    and up to ~1e-6 from the reference's fluxes where its closed forms cancel,
+    include/nusi.h).
     """
 
     def __init__(self, mphi, g, mntot, si, norm=1, majorana=True, non_resonant=True, normal_ordering=True,
                  N_bins_E=300, lEmin=12.0, lEmax=17.0, zmax=5.0, flav=2, phiphi=True,
-                 source_model=_lib.SOURCE_DSNB, reference_order=False):
+                 source_model=_lib.SOURCE_DSNB, reference_order=True):
         L = _lib.load()
         p = _lib.make_params(mphi, g, mntot, si, norm, majorana, non_resonant, normal_ordering, N_bins_E,
                              lEmin, lEmax, zmax, flav, phiphi, source_model)
         self._h = ctypes.c_void_p()
         _lib.check(L.nusi_create(ctypes.byref(p), ctypes.byref(self._h)))
-        if reference_order:
-            _lib.check(L.nusi_set_option(self._h, _lib.OPT_REFERENCE_ORDER, 1))
+        if not reference_order:
+            _lib.check(L.nusi_set_option(self._h, _lib.OPT_REFERENCE_ORDER, 0))
         self.evolved = False
 
     def __del__(self):

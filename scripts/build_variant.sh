@@ -2,7 +2,7 @@
 # Build an A/B variant of libnusi.so (timing experiments only):
 #   scripts/build_variant.sh <name> [flags...]           current tree + extra compile flags
 #   REV=<git rev> scripts/build_variant.sh <name> [...]  sources of a committed revision
-# -> nusiprop_amd/libnusi_<name>.so ; select it with NUSIPROP_LIB=... scripts/dev_scan_timing.py
+# -> build/variants/libnusi_<name>.so ; select it with NUSIPROP_LIB=... scripts/dev_scan_timing.py
 set -e
 V=$1; shift
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
@@ -19,5 +19,6 @@ F="-O3 -std=c++17 -fPIC -ffp-contract=off --offload-arch=gfx950 -I$SRC/include -
 /opt/rocm/bin/hipcc $F -mllvm -pragma-unroll-threshold=1000000 -c -o $D/c.o $C/nusi_cascade.hip &
 /opt/rocm/bin/hipcc $F -c -o $D/a.o $C/nusi_capi.cpp &
 wait
-/opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o $ROOT/nusiprop_amd/libnusi_$V.so $D/k.o $D/c.o $D/a.o
-echo built nusiprop_amd/libnusi_$V.so
+mkdir -p $ROOT/build/variants
+/opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o $ROOT/build/variants/libnusi_$V.so $D/k.o $D/c.o $D/a.o
+echo built build/variants/libnusi_$V.so

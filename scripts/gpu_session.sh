@@ -10,7 +10,7 @@
 #   bench[=<a>,<b>,..]      python bench.py <a> <b> ..  (commas = spaces)           -> bench_<i>.json / .err
 #   prof=<a>,<b>,..         rocprofv3 --kernel-trace --stats of bench.py <a> <b> .. -> kt_<i>/
 #   py=<script>,<a>,..      python <script> <a> ..                                   -> py_<i>.out / .err
-#   vbench=<v>,<a>,..       bench.py <a> .. on the A/B library nusiprop_amd/libnusi_<v>.so (scripts/build_variant.sh)
+#   vbench=<v>,<a>,..       bench.py <a> .. on the A/B library build/variants/libnusi_<v>.so (scripts/build_variant.sh)
 #   vpy=<v>,<script>,<a>,.. python <script> <a> .. on that library                   -> vpy_<i>.out / .err
 #   vprof=<v>,<a>,..        prof= of bench.py <a> .. on that library                  -> vkt_<i>_<v>/
 set -o pipefail
@@ -47,15 +47,15 @@ for STEP in "$@"; do
       timeout -k 10 600 python $ARGS > $OUT/py_$i.out 2> $OUT/py_$i.err || exit 1 ;;
     vbench)
       V=${ARGS%% *}; A=${ARGS#* }; [ "$A" = "$ARGS" ] && A=""
-      NUSIPROP_LIB=$PWD/nusiprop_amd/libnusi_$V.so timeout -k 10 600 python bench.py $A > $OUT/vbench_${i}_$V.json \
+      NUSIPROP_LIB=$PWD/build/variants/libnusi_$V.so timeout -k 10 600 python bench.py $A > $OUT/vbench_${i}_$V.json \
         2> $OUT/vbench_${i}_$V.err || exit 1 ;;
     vprof)
       V=${ARGS%% *}; A=${ARGS#* }; [ "$A" = "$ARGS" ] && A=""
-      NUSIPROP_LIB=$PWD/nusiprop_amd/libnusi_$V.so timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/vkt_${i}_$V \
+      NUSIPROP_LIB=$PWD/build/variants/libnusi_$V.so timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/vkt_${i}_$V \
         -o kt --output-format csv -- python3 bench.py $A > $OUT/vkt_${i}_$V.log 2>&1 || exit 1 ;;
     vpy)
       V=${ARGS%% *}; A=${ARGS#* }
-      NUSIPROP_LIB=$PWD/nusiprop_amd/libnusi_$V.so timeout -k 10 600 python $A > $OUT/vpy_${i}_$V.out \
+      NUSIPROP_LIB=$PWD/build/variants/libnusi_$V.so timeout -k 10 600 python $A > $OUT/vpy_${i}_$V.out \
         2> $OUT/vpy_${i}_$V.err || exit 1 ;;
     *)
       echo "unknown step $STEP" >> $OUT/session.log; exit 2 ;;

@@ -9,10 +9,14 @@ fp64 VALU work per launch (for the table kernel's VALU roofline) comes from an
 optional fourth pass with SQ_INSTS_VALU_{ADD,MUL,FMA,TRANS}_F64: per-wave
 instruction counts, x 64 lanes, FMA counted as 2 flops.
 
-  python scripts/pmc_summary.py <fetch_dir> <write_dir> <calib_dir> [<valu_dir>] [--lib libnusi.so] > traffic.json
+  python scripts/pmc_summary.py <fetch_dir> <write_dir> <calib_dir> [<valu_dir>] [--lib libnusi.so]
+         [--order reference|shared] [--steps K] > traffic.json
 
---lib records the sha256 of the library the passes ran (bench.py drops traffic / flops taken from a
-summary whose hash differs from the library it loads).
+--lib records the sha256 of the library the passes ran and --order the table arithmetic the profiled bench ran
+(NUSI_OPT_REFERENCE_ORDER 1 / 0): bench.py drops traffic / flops taken from a summary whose hash or order differs
+from the library it loads and the mode it times.  --steps is the number of evolve() calls each pass ran (warmup +
+timed); without it the step count is the number of k_gamma_alphat dispatches (one per call, except under
+NUSI_OPT_SHIFT_REUSE, which launches it for the direct and the base tables).
 """
 import csv
 import glob
@@ -31,9 +35,12 @@ def per_kernel(d, counter):
     return vals
 
 
+STEPS = None   # --steps: evolve() calls per pass
+
+
 def per_step(d, counter, name_part):
     """Sum over one step's launches of a kernel: every matching dispatch's value, divided by the number of steps the
-    pass ran (the dispatches of k_gamma_alphat, one per step).  (Grouping by grid size, as before round 5, counted
+    pass ran (--steps, else the dispatches of k_gamma_alphat).  (Grouping by grid size, as before round 5, counted
     the reference order's equal-sized member-corner chunks once.)  Returns (per-step value, launches per step)."""
     tot, n, steps = 0.0, 0, 0
     for f in glob.glob(d + "/**/*counter_collection.csv", recursive=True):
@@ -45,13 +52,23 @@ def per_step(d, counter, name_part):
             if name_part in row["Kernel_Name"]:
                 tot += float(row["Counter_Value"])
                 n += 1
-    steps = max(steps, 1)
+    steps = STEPS if STEPS else max(steps, 1)
     return tot / steps, n // steps
 
 
 def main():
+    global STEPS
     argv = list(sys.argv[1:])
-    lib = mfma_dir = None
+    lib = mfma_dir = order = None
+    if "--order" in argv:
+        k = argv.index("--order")
+        order = argv[k + 1]
+        assert order in ("reference", "shared"), order
+        del argv[k:k + 2]
+    if "--steps" in argv:
+        k = argv.index("--steps")
+        STEPS = int(argv[k + 1])
+        del argv[k:k + 2]
     if "--lib" in argv:
         k = argv.index("--lib")
         lib = argv[k + 1]
@@ -116,6 +133,10 @@ def main():
             fma = per_step(sys.argv[4], "SQ_INSTS_VALU_FMA_F64", "nusi::k_alpha")[0]
             trn = per_step(sys.argv[4], "SQ_INSTS_VALU_TRANS_F64", "nusi::k_alpha")[0]
             out["k_alpha_fp64_flops_per_step"] = 64.0 * (add + mul + 2.0 * fma + trn)
+    if order:
+        out["table_order"] = order
+    if STEPS:
+        out["steps_per_pass"] = STEPS
     if lib:
         import hashlib
         with open(lib, "rb") as fh:

@@ -20,7 +20,7 @@ for f in nusiprop_amd/libnusi.so nusiprop_amd/tools/phiphi_text_to_binary oracle
   [ -e "$f" ] && { mkdir -p ".snap/$(dirname "$f")"; cp -p "$f" ".snap/$f"; }
 done
 git rev-parse --short HEAD > .snap/SNAP_HEAD
-for f in nusiprop_amd/libnusi_*.so; do   # A/B variants (scripts/build_variant.sh), if any
-  [ -e "$f" ] && cp -p "$f" ".snap/$f"
+for f in build/variants/libnusi_*.so; do   # A/B variants (scripts/build_variant.sh), if any
+  [ -e "$f" ] && { mkdir -p .snap/build/variants; cp -p "$f" ".snap/$f"; }
 done
 echo "snap: $(cat .snap/SNAP_HEAD) -> .snap"

@@ -18,7 +18,7 @@ rc=$?
 mkdir -p "$TOP/gpurun_out/$TAG"
 cp -r "gpurun_out/$TAG/." "$TOP/gpurun_out/$TAG/"
 cp SNAP_HEAD "$TOP/gpurun_out/$TAG/" 2>/dev/null
-for w in c4 c5 c3 c4s; do
+for w in c4 c5 c3 c4s c4_shared c5_shared c3_shared; do
   [ -f "profiles/pmc_traffic_$w.json" ] && [ "profiles/pmc_traffic_$w.json" -nt SNAP_HEAD ] && \
     cp "profiles/pmc_traffic_$w.json" "$TOP/gpurun_out/$TAG/pmc_traffic_$w.json"
 done

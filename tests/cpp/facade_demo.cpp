@@ -24,5 +24,12 @@ int main()
     dump("B", other);
     dump("C", evolver);                        // the original is untouched
     printf("R %.17e\n", evolver.get_flux(0, -1) + evolver.get_flux_fla(3, 0) + evolver.get_energy(1000));
+    // BASELINE config 2a (DSNB, the resonance inside lE 4 -> 9, N_E = 300) with no option: the reference's arithmetic
+    nuSIprop::calculate_flux c2a(3e3, 0.03, 0.1, 2.5, 6, true, true, true, 300, 4, 9, 5, 2, false);
+    c2a.evolve();
+    dump("D", c2a);
+    c2a.set_reference_order(false);            // the opt-in shared-algorithm order
+    c2a.evolve();
+    dump("E", c2a);
     return 0;
 }

@@ -99,3 +99,28 @@ def test_c4_dry_run_world2_weak_blocks():
     s = _line(out)["shard_check"]
     assert s["points"] == 2048 and s["covered_once"] and s["blocks"] == [[0, 1024], [1024, 2048]]
     assert s["scaling"] == "weak"
+
+
+def test_pmc_summary_must_match_library_and_table_order(tmp_path):
+    """bench.py prices the dominant kernel's roofline with a committed PMC summary only when that summary was
+    collected on the loaded library (sha256) in the table arithmetic the run times (table_order): a summary of the
+    other arithmetic, of another binary, or without an order is dropped with a note, so no roofline/traffic comes
+    from it (the shared-order line had been priced with the reference order's flop count)."""
+    sys.path.insert(0, ROOT)
+    import bench
+    sha = "ab" * 32
+    good = {"libnusi_sha256": sha, "table_order": "reference", "k_alpha_fp64_flops_per_step": 2.6e11,
+            "k_alpha_hbm_bytes_per_step": 3e10}
+    p = tmp_path / "pmc.json"
+    p.write_text(json.dumps(good))
+    pmc, src, note = bench.load_pmc(str(p), sha, "reference")
+    assert pmc["k_alpha_fp64_flops_per_step"] == 2.6e11 and note is None and src
+    pmc, _, note = bench.load_pmc(str(p), sha, "shared")          # the other arithmetic
+    assert pmc == {} and "table order" in note
+    pmc, _, note = bench.load_pmc(str(p), "cd" * 32, "reference")  # another binary
+    assert pmc == {} and "not the loaded" in note
+    p.write_text(json.dumps(dict(good, table_order=None)))          # a summary that does not say its order
+    assert bench.load_pmc(str(p), sha, "reference")[0] == {}
+    assert bench.load_pmc(str(tmp_path / "missing.json"), sha, "reference") == ({}, None, None)
+    assert bench.pmc_summary_path("c4", True).endswith("profiles/pmc_traffic_c4.json")
+    assert bench.pmc_summary_path("c4", False).endswith("profiles/pmc_traffic_c4_shared.json")

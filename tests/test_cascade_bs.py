@@ -26,7 +26,7 @@ def _run(nusi, pts, exact=False, **opts):
     """Plan.evolve of `pts`: the default MFMA cascade, or (exact) the scalar k_cascade; opts: OPT_* options."""
     from nusiprop_amd import _lib
     p0 = pts[0]
-    plan = nusi.Plan(p0["N_bins_E"], p0["lEmin"], p0["lEmax"], p0["zmax"], max_points=len(pts))
+    plan = nusi.Plan(p0["N_bins_E"], p0["lEmin"], p0["lEmax"], p0["zmax"], max_points=len(pts), reference_order=False)
     if exact:
         plan.set_cascade(_lib.CASCADE_LDS)
     for k, v in opts.items():
@@ -155,7 +155,7 @@ def test_bs_c3_gamma_block(nusi, oracle_mod, ref_tables):
     blk = [dict(C3, si=2.0 + 0.06 * k, norm=1.0 + 0.1 * k) for k in range(16)]
     res = {}
     for exact in (False, True):
-        p = nusi.Plan(C3["N_bins_E"], C3["lEmin"], C3["lEmax"], C3["zmax"], max_points=16)
+        p = nusi.Plan(C3["N_bins_E"], C3["lEmin"], C3["lEmax"], C3["zmax"], max_points=16, reference_order=False)
         p.load_phiphi(at, a)
         if exact:
             p.set_cascade(_lib.CASCADE_LDS)
@@ -178,7 +178,7 @@ def test_per_stage_sync_refused(nusi):
     """NUSI_OPT_CASCADE_SYNC = 1 selected the per-stage kernels of rounds 2-3, which are gone: refused with
     NUSI_EPARAM (0 and 2 both select k_cascade_bs)."""
     from nusiprop_amd import _lib
-    plan = nusi.Plan(100, 12.0, 17.0, 5.0, max_points=1)
+    plan = nusi.Plan(100, 12.0, 17.0, 5.0, max_points=1, reference_order=False)
     try:
         with pytest.raises(_lib.NusiError):
             plan.set_option(_lib.OPT_CASCADE_SYNC, 1)

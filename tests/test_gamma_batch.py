@@ -24,7 +24,7 @@ def nusi():
 def _run(nusi, pts, rhs):
     from nusiprop_amd import _lib
     p0 = pts[0]
-    plan = nusi.Plan(p0["N_bins_E"], p0["lEmin"], p0["lEmax"], p0["zmax"], max_points=len(pts))
+    plan = nusi.Plan(p0["N_bins_E"], p0["lEmin"], p0["lEmax"], p0["zmax"], max_points=len(pts), reference_order=False)
     plan.set_option(_lib.OPT_CASCADE_RHS, rhs)
     flux, fla = plan.evolve(pts)
     return plan, flux, fla

@@ -31,7 +31,7 @@ def nusi():
 def _gpu(nusi, pts, **opts):
     from nusiprop_amd import _lib
     p0 = pts[0]
-    plan = nusi.Plan(p0["N_bins_E"], p0["lEmin"], p0["lEmax"], p0["zmax"], max_points=len(pts))
+    plan = nusi.Plan(p0["N_bins_E"], p0["lEmin"], p0["lEmax"], p0["zmax"], max_points=len(pts), reference_order=False)
     for k, v in opts.items():
         plan.set_option(getattr(_lib, "OPT_" + k.upper()), v)
     flux, fla = plan.evolve(pts)
@@ -93,7 +93,7 @@ def test_mfma_cascade_vs_oracle(nusi, oracle_mod, kw):
     from nusiprop_amd import _lib
     o = oracle_mod.Oracle(**cases.oracle_kwargs(kw))
     f_ref, fla_ref = o.evolve()
-    plan = nusi.Plan(kw["N_bins_E"], kw["lEmin"], kw["lEmax"], kw["zmax"], max_points=3)
+    plan = nusi.Plan(kw["N_bins_E"], kw["lEmin"], kw["lEmax"], kw["zmax"], max_points=3, reference_order=False)
     plan.set_cascade(_lib.CASCADE_MFMA)
     flux, fla = plan.evolve([kw, kw, kw])
     for i in range(3):
@@ -184,7 +184,7 @@ def test_cascade_kernels_agree(nusi, N, nonres):
     from nusiprop_amd import _lib
     pts = [dict(cases.C2B_100, N_bins_E=N, non_resonant=nonres, majorana=maj, mphi=m, g=gg)
            for maj, m, gg in ((True, 6e5, 0.01), (False, 2e6, 0.1), (True, 1e6, 0.3))]
-    plan = nusi.Plan(N, pts[0]["lEmin"], pts[0]["lEmax"], pts[0]["zmax"], max_points=len(pts))
+    plan = nusi.Plan(N, pts[0]["lEmin"], pts[0]["lEmax"], pts[0]["zmax"], max_points=len(pts), reference_order=False)
     out, names = {}, {}
     for kind in (_lib.CASCADE_WAVEFRONT, _lib.CASCADE_REG, _lib.CASCADE_LDS, _lib.CASCADE_AUTO, _lib.CASCADE_MFMA):
         plan.set_cascade(kind)
@@ -246,7 +246,7 @@ def test_plan_serialises_calls_across_streams(nusi):
     H = _hip()
     a = [dict(cases.C2B_100, mphi=m, g=g) for m, g in ((6e5, 0.01), (2e6, 0.1), (1e7, 0.5))]
     b = [dict(cases.C2B_100, mphi=m, g=g, majorana=False) for m, g in ((3e5, 0.3), (8e5, 0.05), (4e6, 0.02))]
-    plan = nusi.Plan(100, 12.0, 17.0, 5.0, max_points=3)
+    plan = nusi.Plan(100, 12.0, 17.0, 5.0, max_points=3, reference_order=False)
     ref_a = plan.evolve(a)
     ref_b = plan.evolve(b)
     nbytes = 3 * 3 * 100 * 8
@@ -293,7 +293,7 @@ def _evolve_opts(nusi, pts, kind=None, **opts):
     cascade_rhs, step_passes, ...)."""
     from nusiprop_amd import _lib
     p0 = pts[0]
-    plan = nusi.Plan(p0["N_bins_E"], p0["lEmin"], p0["lEmax"], p0["zmax"], max_points=len(pts))
+    plan = nusi.Plan(p0["N_bins_E"], p0["lEmin"], p0["lEmax"], p0["zmax"], max_points=len(pts), reference_order=False)
     if kind is not None:
         plan.set_cascade(kind)
     for k, v in opts.items():
@@ -346,7 +346,7 @@ def test_cascade_step_passes(nusi, oracle_mod, N, lEmin):
            for m, g, maj in ((6e5, 0.01, True), (1e5, 0.05, True), (2e6, 0.3, False))]
     got = _evolve_opts(nusi, pts, step_passes=1)
     assert got[2][1] == "k_cascade_bs"
-    plan = nusi.Plan(N, lEmin, pts[0]["lEmax"], pts[0]["zmax"], max_points=len(pts))
+    plan = nusi.Plan(N, lEmin, pts[0]["lEmax"], pts[0]["zmax"], max_points=len(pts), reference_order=False)
     plan.set_cascade(_lib.CASCADE_LDS)
     ref = plan.evolve(pts)
     assert plan.Nz - 1 == {100: 16, 200: 32, 700: 109, 1200: 134}[N]
@@ -371,7 +371,7 @@ def test_cascade_step_passes_resonant_only(nusi, oracle_mod, N):
            for m, g, nr in ((6e5, 0.01, True), (2e6, 0.3, False), (1e6, 0.1, False))]
     got = _evolve_opts(nusi, pts, step_passes=1)
     assert got[2][1] == "k_cascade_bs"
-    plan = nusi.Plan(N, 12.0, pts[0]["lEmax"], pts[0]["zmax"], max_points=len(pts))
+    plan = nusi.Plan(N, 12.0, pts[0]["lEmax"], pts[0]["zmax"], max_points=len(pts), reference_order=False)
     plan.set_cascade(_lib.CASCADE_LDS)
     ref = plan.evolve(pts)
     for k, p in enumerate(pts):
@@ -392,7 +392,7 @@ def test_plan_kernels_names(nusi):
     from nusiprop_amd import _lib
     def run(N, lEmin, pts_kw, kind):
         pts = [dict(cases.C2B_100, N_bins_E=N, lEmin=lEmin, **kw) for kw in pts_kw]
-        plan = nusi.Plan(N, lEmin, pts[0]["lEmax"], pts[0]["zmax"], max_points=len(pts))
+        plan = nusi.Plan(N, lEmin, pts[0]["lEmax"], pts[0]["zmax"], max_points=len(pts), reference_order=False)
         plan.set_cascade(kind)
         plan.evolve(pts)
         k = plan.kernels()

@@ -21,8 +21,10 @@ BUDGET = {
     # the reference-order instances: the member-corner offset and one point's prefetched corner (k_alpha_mcorner's
     # block) live across the point loop, and (non-phi-phi instance) the chunk's A inline -- faster than as a call
     # despite the spills (profiles/r5/r6p); 128 VGPRs (4 waves per SIMD; NUSI_BATCH_WAVES_REFO=3 gives the non-phi-phi
-    # instance 168) held by keeping the complex GSL series out of the kernel's call graph (gsl_cli2_real)
-    r"k_alpha_batchILb[01]ELb1E": (96, 1024),
+    # instance 168, shipped since round 6: spills 82 -> 35) held by keeping the complex GSL series out of the kernel's
+    # call graph (gsl_cli2_real)
+    r"k_alpha_batchILb1ELb1E": (96, 1024),
+    r"k_alpha_batchILb0ELb1E": (40, 256),
     # the block-synchronous cascade: 96 B of private segment are the prologue's pow() call frames (no spills)
     r"k_cascade_bsILi(16|32)ELi1ELi1ELi4ELi1E": (0, 96),
     # (the wave index is readfirstlane'd: per-wave row bases in SGPRs; as VGPRs they spilled 19 / 33 into the push)

@@ -49,7 +49,7 @@ def test_oracle_loads_synthetic_tables(tmp_path, oracle_mod):
 
 
 def _plan(nusi, kw, tabs):
-    p = nusi.Plan(kw["N_bins_E"], kw["lEmin"], kw["lEmax"], kw["zmax"], max_points=1)
+    p = nusi.Plan(kw["N_bins_E"], kw["lEmin"], kw["lEmax"], kw["zmax"], max_points=1, reference_order=False)
     at, atd, a, ad = tabs
     p.load_phiphi(at, a, atd, ad)
     return p
@@ -97,7 +97,7 @@ def test_phiphi_multi_table_batches(tmp_path, oracle_mod):
     T = refs[0][0].T
     iu = np.triu_indices(T, 1)
     for opt, val in ((None, 0), (_lib.OPT_ALPHA_BATCH, 1), (_lib.OPT_ALPHA_BATCH, 64), (_lib.OPT_ALPHA_KERNEL, 1)):
-        p = nusi.Plan(PP_SMALL["N_bins_E"], PP_SMALL["lEmin"], PP_SMALL["lEmax"], PP_SMALL["zmax"], max_points=len(pts))
+        p = nusi.Plan(PP_SMALL["N_bins_E"], PP_SMALL["lEmin"], PP_SMALL["lEmax"], PP_SMALL["zmax"], max_points=len(pts), reference_order=False)
         p.load_phiphi(tabs[0], tabs[2], tabs[1], tabs[3])
         if opt is not None:
             p.set_option(opt, val)
@@ -158,7 +158,7 @@ def test_c3_n1200_phiphi(ref_tables, oracle_mod):
     o = oracle_mod.Oracle(**cases.oracle_kwargs(C3))
     o.load_phiphi(at, atd, a, ad)
     G, aT, al = o.tables()
-    p = nusi.Plan(C3["N_bins_E"], C3["lEmin"], C3["lEmax"], C3["zmax"], max_points=1)
+    p = nusi.Plan(C3["N_bins_E"], C3["lEmin"], C3["lEmax"], C3["zmax"], max_points=1, reference_order=False)
     p.load_phiphi(at, a)                       # dims = NULL: the reference's {5000,100}, {1000,1000,100}
     flux, fla = p.evolve([C3])                 # raises NUSI_EINTERP on an out-of-range lookup
     assert p.warnings(1)[0] & 8 == 0

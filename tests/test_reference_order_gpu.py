@@ -128,16 +128,46 @@ def test_reference_order_c4_full_grid(nusi, oracle_mod):
     f_ref, fla_ref = oracle_mod.evolve_many(pts, level=1)
     errs = np.array([max(cases.rel_err(flux[k], f_ref[k]), cases.rel_err(fla[k], fla_ref[k])) for k in range(len(pts))])
     assert np.all(errs <= FLUX_RTOL), (int(np.argmax(errs)), float(errs.max()))
-    # the member-corner block in chunks of one batch (64 MiB: 11 tables' worth, below the 32 of a batch) -- the same bits
+    # the member-corner block in chunks of one batch (64 MiB: 17 tables' worth at 3.7 MB each, below the 32 of a batch) -- the same bits
     fc, flac, _, _, _ = _gpu_refo(nusi, pts, tables=False, corner_mb=64)
     assert np.array_equal(fc, flux) and np.array_equal(flac, fla)
     p0 = pts[0]
-    plan = nusi.Plan(p0["N_bins_E"], p0["lEmin"], p0["lEmax"], p0["zmax"], max_points=len(pts))
+    plan = nusi.Plan(p0["N_bins_E"], p0["lEmin"], p0["lEmax"], p0["zmax"], max_points=len(pts), reference_order=False)
     f0, fla0 = plan.evolve(pts)
     plan.close()
     d0 = np.array([cases.rel_err(fla0[k], fla_ref[k]) for k in range(len(pts))])
-    print("C4 full grid vs the reference-order oracle: refo mode max %.3g; default mode max %.3g, %d points > 1e-9"
+    print("C4 full grid vs the reference-order oracle: refo mode max %.3g; shared-order mode max %.3g, %d points > 1e-9"
           % (errs.max(), d0.max(), int(np.sum(d0 > 1e-9))))
+
+
+def test_reference_order_c5_gamma_block(nusi, oracle_mod):
+    """BASELINE config 5 in the reference order (the library default): one full 16-gamma block of scan.c5_points()
+    (one Stage-A table, k_alpha_mcorner + k_alpha_batch[refo], the gamma batch k_cascade_bs_gamma) -- the table
+    bit-exact to the reference-order oracle and every gamma's flux within FLUX_RTOL of the oracle's cascade on it."""
+    from nusiprop_amd import scan
+    allp = scan.c5_points()
+    blk = allp[16 * 2345:16 * 2346]
+    assert len({scan.table_key(p) for p in blk}) == 1 and len({p["si"] for p in blk}) == 16
+    p0 = blk[0]
+    plan = nusi.Plan(p0["N_bins_E"], p0["lEmin"], p0["lEmax"], p0["zmax"], max_points=len(blk))
+    flux, fla = plan.evolve(blk)
+    names = plan.kernels()
+    tab = plan.tables(0)
+    for i in range(1, len(blk)):
+        for x, y in zip(plan.tables(i), tab):
+            assert np.array_equal(x, y)
+    plan.close()
+    assert names == ("k_alpha_mcorner + k_alpha_batch[refo]", "k_cascade_bs_gamma")
+    o = oracle_mod.Oracle(**cases.oracle_kwargs(p0))
+    with oracle_mod.reference_order(1):
+        G, aT, al = _check_tables(nusi, o, tab, p0)
+    for k, p in enumerate(blk):
+        ok = oracle_mod.Oracle(**cases.oracle_kwargs(p))
+        ok.prepare()
+        f_ref, fla_ref = ok.cascade(G, aT, al)
+        assert cases.rel_err(flux[k], f_ref) <= FLUX_RTOL, k
+        assert cases.rel_err(fla[k], fla_ref) <= FLUX_RTOL, k
+        assert np.array_equal(flux[k] == 0, f_ref == 0)
 
 
 def test_reference_order_c3(nusi, oracle_mod, ref_tables):
@@ -162,39 +192,93 @@ def test_reference_order_c3(nusi, oracle_mod, ref_tables):
     assert cases.rel_err(fla[0], fla_ref) <= FLUX_RTOL
 
 
-def test_reference_order_object_api(nusi, oracle_mod):
-    """The object API (nusi_set_option on a calculate_flux-style handle, kept by nusi_copy): C2a in reference
-    order through nusi_create / nusi_evolve equals the plan's result bit for bit."""
+def _object_fla(L, _lib, kw, order=None, copy=False):
+    """One evolve() through the object API (nusi_create / nusi_evolve / nusi_get_flux_fla, the calculate_flux
+    path): `order` None = no option at all; else NUSI_OPT_REFERENCE_ORDER set to it.  copy: also evolve a
+    nusi_copy of the handle.  Returns the (3, N) flavour fluxes of each handle and the alpha kernel label."""
     import ctypes
-    from nusiprop_amd import _lib
-    L = _lib.load()
-    kw = dict(cases.C2A)
+    kw = dict(kw)
     src = kw.pop("source_model")
+    N = kw["N_bins_E"]
     h, h2 = ctypes.c_void_p(), ctypes.c_void_p()
     _lib.check(L.nusi_create(ctypes.byref(_lib.make_params(source_model=src, **kw)), ctypes.byref(h)))
+    outs, labels = [], []
     try:
-        _lib.check(L.nusi_set_option(h, _lib.OPT_REFERENCE_ORDER, 1))
-        assert L.nusi_set_option(h, _lib.OPT_REFERENCE_ORDER, 2) == _lib.NUSI_EPARAM
-        _lib.check(L.nusi_copy(h, ctypes.byref(h2)))
-        outs = []
-        for hh in (h, h2):
+        if order is not None:
+            _lib.check(L.nusi_set_option(h, _lib.OPT_REFERENCE_ORDER, order))
+        if copy:
+            _lib.check(L.nusi_copy(h, ctypes.byref(h2)))
+        for hh in ((h, h2) if copy else (h,)):
             _lib.check(L.nusi_evolve(hh))
-            out = np.zeros(3 * 300)
+            out = np.zeros(3 * N)
             _lib.check(L.nusi_get_flux_fla(hh, out.ctypes.data_as(ctypes.POINTER(ctypes.c_double))))
             a, c = ctypes.c_char_p(), ctypes.c_char_p()
             _lib.check(L.nusi_get_kernels(hh, ctypes.byref(a), ctypes.byref(c)))
-            assert a.value == b"k_alpha_mcorner + k_alpha_batch[refo]"
-            outs.append(out.reshape(3, 300))
+            outs.append(out.reshape(3, N))
+            labels.append(a.value)
     finally:
         L.nusi_destroy(h)
         if h2.value:
             L.nusi_destroy(h2)
+    return outs, labels
+
+
+def test_dropin_default_is_reference_arithmetic_c2a(nusi, oracle_mod):
+    """BASELINE config 2a (DSNB, resonance inside lE 4 -> 9, N_E = 300) through the drop-in surfaces WITHOUT ANY
+    OPTION -- the object API (calculate_flux's path), a copy of it, and pyprop -- runs the reference's own arithmetic:
+    fluxes <= FLUX_RTOL of the reference-order oracle's evolve() (the shared order is ~2.5e-6 away on this config),
+    and bit-identical to a default plan's.  The shared order stays available as the opt-in fast mode."""
+    from nusiprop_amd import _lib
+    L = _lib.load()
+    with oracle_mod.reference_order(1):
+        _, fla_ref = oracle_mod.Oracle(**cases.oracle_kwargs(cases.C2A)).evolve()
+    _, fla_shared = oracle_mod.Oracle(**cases.oracle_kwargs(cases.C2A)).evolve()
+    assert cases.rel_err(fla_shared, fla_ref) > 1e-9   # the two arithmetics differ on this config
+    outs, labels = _object_fla(L, _lib, cases.C2A, copy=True)
+    assert labels == [b"k_alpha_mcorner + k_alpha_batch[refo]"] * 2
+    kw = dict(cases.C2A)
+    kw.pop("source_model")
+    ev = nusi.pyprop(**dict(kw, phiphi=False))
+    ev.evolve()
+    assert ev.kernels()[0] == "k_alpha_mcorner + k_alpha_batch[refo]"
+    p0 = cases.C2A
+    plan = nusi.Plan(p0["N_bins_E"], p0["lEmin"], p0["lEmax"], p0["zmax"], max_points=1)
+    _, fla_plan = plan.evolve([p0])
+    assert plan.kernels()[0] == "k_alpha_mcorner + k_alpha_batch[refo]"
+    plan.close()
+    for got in outs + [np.asarray(ev.get_flux_fla())]:
+        assert cases.rel_err(got, fla_ref) <= FLUX_RTOL
+        assert np.array_equal(got, fla_plan[0])
+    # the opt-in fast mode: the oracle's default mode, through both surfaces
+    fast, lab = _object_fla(L, _lib, cases.C2A, order=0)
+    assert lab == [b"k_alpha_batch"] and cases.rel_err(fast[0], fla_shared) <= FLUX_RTOL
+    ev0 = nusi.pyprop(**dict(kw, phiphi=False), reference_order=False)
+    ev0.evolve()
+    assert np.array_equal(np.asarray(ev0.get_flux_fla()), fast[0])
+
+
+def test_reference_order_object_api(nusi, oracle_mod):
+    """The object API's option (nusi_set_option on a calculate_flux-style handle, kept by nusi_copy): an explicit
+    NUSI_OPT_REFERENCE_ORDER = 1 on C2a equals the plan's result bit for bit; values outside [0, 1] are refused."""
+    import ctypes
+    from nusiprop_amd import _lib
+    L = _lib.load()
+    outs, labels = _object_fla(L, _lib, cases.C2A, order=1, copy=True)
+    assert labels == [b"k_alpha_mcorner + k_alpha_batch[refo]"] * 2
+    kw = dict(cases.C2A)
+    src = kw.pop("source_model")
+    h = ctypes.c_void_p()
+    _lib.check(L.nusi_create(ctypes.byref(_lib.make_params(source_model=src, **kw)), ctypes.byref(h)))
+    try:
+        assert L.nusi_set_option(h, _lib.OPT_REFERENCE_ORDER, 2) == _lib.NUSI_EPARAM
+    finally:
+        L.nusi_destroy(h)
     _, fla, _, _, _ = _gpu_refo(nusi, [cases.C2A], tables=False)
     assert np.array_equal(outs[0], fla[0]) and np.array_equal(outs[1], fla[0])
 
 
 def test_reference_order_pyprop(nusi):
-    """The drop-in pyprop's extension keyword reference_order=True gives the plan's reference-order fluxes."""
+    """pyprop's extension keyword reference_order (default True) gives the plan's reference-order fluxes."""
     kw = dict(cases.C2A)
     kw.pop("source_model")
     ev = nusi.pyprop(**dict(kw, phiphi=False), reference_order=True)
@@ -205,35 +289,21 @@ def test_reference_order_pyprop(nusi):
 
 def test_object_plans_are_reused_with_default_options(nusi):
     """Destroyed one-point objects hand their plan to the next object on the same grid (nusi_capi.cpp plan pool):
-    an object created after a reference-order one runs the default arithmetic and gives the bits of a fresh plan."""
-    import ctypes
+    an object created after a shared-order one runs the default (reference) arithmetic and gives the bits of a
+    fresh default plan."""
     from nusiprop_amd import _lib
     L = _lib.load()
-    kw = dict(cases.C2B)
-    src = kw.pop("source_model")
-
-    def run(ref):
-        h = ctypes.c_void_p()
-        _lib.check(L.nusi_create(ctypes.byref(_lib.make_params(source_model=src, **kw)), ctypes.byref(h)))
-        try:
-            if ref:
-                _lib.check(L.nusi_set_option(h, _lib.OPT_REFERENCE_ORDER, 1))
-            _lib.check(L.nusi_evolve(h))
-            out = np.zeros(3 * 300)
-            _lib.check(L.nusi_get_flux_fla(h, out.ctypes.data_as(ctypes.POINTER(ctypes.c_double))))
-            a, c = ctypes.c_char_p(), ctypes.c_char_p()
-            _lib.check(L.nusi_get_kernels(h, ctypes.byref(a), ctypes.byref(c)))
-            return out.reshape(3, 300), a.value
-        finally:
-            L.nusi_destroy(h)
-
-    ref, ka = run(True)
-    dflt, kb = run(False)   # (the pooled plan of the first object)
-    assert ka == b"k_alpha_mcorner + k_alpha_batch[refo]" and kb == b"k_alpha_batch"
+    fast, ka = _object_fla(L, _lib, cases.C2B, order=0)
+    dflt, kb = _object_fla(L, _lib, cases.C2B)   # (the pooled plan of the first object)
+    assert ka == [b"k_alpha_batch"] and kb == [b"k_alpha_mcorner + k_alpha_batch[refo]"]
     p0 = cases.C2B
     plan = nusi.Plan(p0["N_bins_E"], p0["lEmin"], p0["lEmax"], p0["zmax"], max_points=1)
     _, fla = plan.evolve([p0])
     plan.close()
-    assert np.array_equal(dflt, fla[0])
+    assert np.array_equal(dflt[0], fla[0])
     _, fla_r, _, _, _ = _gpu_refo(nusi, [p0], tables=False)
-    assert np.array_equal(ref, fla_r[0])
+    assert np.array_equal(dflt[0], fla_r[0])
+    plan = nusi.Plan(p0["N_bins_E"], p0["lEmin"], p0["lEmax"], p0["zmax"], max_points=1, reference_order=False)
+    _, fla_s = plan.evolve([p0])
+    plan.close()
+    assert np.array_equal(fast[0], fla_s[0])

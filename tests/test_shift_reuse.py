@@ -35,7 +35,7 @@ def test_shift_reuse_scan(nusi, oracle_mod, N, K, offs):
     pts = _lattice_points(base, offs, (0.01, 0.3))
     off_lattice = dict(base, mphi=7.77e5, g=0.3)          # no partner: built directly
     pts.append(off_lattice)
-    plan = nusi.Plan(N, base["lEmin"], base["lEmax"], base["zmax"], max_points=len(pts))
+    plan = nusi.Plan(N, base["lEmin"], base["lEmax"], base["zmax"], max_points=len(pts), reference_order=False)
     plan.set_option(_lib.OPT_SHIFT_REUSE, K)
     flux, fla = plan.evolve(pts)
     assert "k_table_shift" in plan.kernels()[0]
@@ -68,7 +68,7 @@ def test_shift_reuse_off_is_default_and_exact(nusi):
     from nusiprop_amd import _lib
     base = dict(cases.C2B_100)
     pts = _lattice_points(base, (0, 2, 4), (0.03,))   # (g <= 0.05: couplings that share)
-    plan = nusi.Plan(base["N_bins_E"], base["lEmin"], base["lEmax"], base["zmax"], max_points=len(pts))
+    plan = nusi.Plan(base["N_bins_E"], base["lEmin"], base["lEmax"], base["zmax"], max_points=len(pts), reference_order=False)
     f_direct, _ = plan.evolve(pts)
     t_direct = [plan.tables(i) for i in range(len(pts))]
     assert "k_table_shift" not in plan.kernels()[0]
@@ -87,7 +87,7 @@ def test_shift_reuse_off_is_default_and_exact(nusi):
 
 def test_shift_reuse_option_bounds(nusi):
     from nusiprop_amd import _lib
-    plan = nusi.Plan(60, 12.0, 17.0, 5.0, max_points=2)
+    plan = nusi.Plan(60, 12.0, 17.0, 5.0, max_points=2, reference_order=False)
     with pytest.raises(Exception):
         plan.set_option(_lib.OPT_SHIFT_REUSE, 129)
     with pytest.raises(Exception):
@@ -102,7 +102,7 @@ def test_shift_reuse_c4s_lattice_k128(nusi, oracle_mod):
     pts = [p for p in scan.c4s_points(n_g=2)] + [dict(p, g=0.05) for p in scan.c4s_points(n_g=1)]
     assert sorted({p["g"] for p in pts}) == [1e-3, 0.05, 1.0] and len(pts) == 96
     p0 = pts[0]
-    plan = nusi.Plan(p0["N_bins_E"], p0["lEmin"], p0["lEmax"], p0["zmax"], max_points=len(pts))
+    plan = nusi.Plan(p0["N_bins_E"], p0["lEmin"], p0["lEmax"], p0["zmax"], max_points=len(pts), reference_order=False)
     plan.set_option(_lib.OPT_SHIFT_REUSE, 128)
     flux, fla = plan.evolve(pts)
     assert "k_table_shift" in plan.kernels()[0]
@@ -126,7 +126,7 @@ def test_shift_reuse_rounded_mphi_goes_direct(nusi, oracle_mod):
     rounded = dict(base, mphi=float("%.7g" % m6), g=0.03)
     assert rounded["mphi"] != m6 and abs(rounded["mphi"] / m6 - 1) < 1e-6
     pts = exact + [rounded]
-    plan = nusi.Plan(base["N_bins_E"], base["lEmin"], base["lEmax"], base["zmax"], max_points=len(pts))
+    plan = nusi.Plan(base["N_bins_E"], base["lEmin"], base["lEmax"], base["zmax"], max_points=len(pts), reference_order=False)
     plan.set_option(_lib.OPT_SHIFT_REUSE, 8)
     flux, fla = plan.evolve(pts)
     assert "k_table_shift" in plan.kernels()[0]
@@ -149,7 +149,7 @@ def test_shift_reuse_phiphi_warnings_in_range(nusi, ref_tables):
     base = dict(cases.C2B_100, N_bins_E=850, phiphi=True)
     K = 30
     pts = _lattice_points(base, (0, 10, 20, 30), (0.05,), m_max=3e7)   # (couplings above 0.05 do not share)
-    plan = nusi.Plan(850, base["lEmin"], base["lEmax"], base["zmax"], max_points=len(pts))
+    plan = nusi.Plan(850, base["lEmin"], base["lEmax"], base["zmax"], max_points=len(pts), reference_order=False)
     plan.load_phiphi(at, a)
     assert plan.T <= 1000
     f_direct, _ = plan.evolve(pts)
@@ -163,7 +163,7 @@ def test_shift_reuse_phiphi_warnings_in_range(nusi, ref_tables):
     # out-of-node lookups: the case the test is about
     r = 10 ** ((base["lEmax"] - base["lEmin"]) / base["N_bins_E"])
     zb = r ** (plan.Nz + K - 1.5) - 1
-    sp = nusi.Plan(850, base["lEmin"], base["lEmax"], zb, max_points=1)
+    sp = nusi.Plan(850, base["lEmin"], base["lEmax"], zb, max_points=1, reference_order=False)
     sp.load_phiphi(at, a)
     assert sp.T == plan.T + K
     with pytest.raises(_lib.NusiError) as e:
