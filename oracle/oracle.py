@@ -12,7 +12,9 @@ import subprocess
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "_build", "libnusi_oracle.so")
+# NUSI_ORACLE_LIB: a contracted build of the same sources (oracle/Makefile target fc; the platform-arithmetic probe
+# scripts/contraction_floor.py) -- never the parity oracle
+LIB_PATH = os.environ.get("NUSI_ORACLE_LIB") or os.path.join(HERE, "_build", "libnusi_oracle.so")
 
 SOURCE_DSNB = 0
 SOURCE_POWER_LAW = 1

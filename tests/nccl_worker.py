@@ -13,9 +13,9 @@ def main():
     import numpy as np
     import torch
     import torch.distributed as dist
-    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     torch.cuda.set_device(0)                      # torch's runtime first, then libnusi (as bench.py does)
-    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    # world 1: an in-process store (no TCP rendezvous port to race other processes for)
+    dist.init_process_group("nccl", store=dist.HashStore(), rank=0, world_size=1, device_id=torch.device("cuda", 0))
     import nusiprop_amd as nu
     from nusiprop_amd import dist as ndist, scan
     pts = scan.c4_points(n_mphi=4, n_g=3, N_bins_E=100) + [dict(p, si=2.2) for p in scan.c4_points(n_mphi=2, n_g=2,

@@ -46,11 +46,13 @@ def test_evolve_sharded_on_rccl_world1():
 
 
 def test_bench_under_torchrun_one_rank():
-    env, port = _env()
+    env, _ = _env()
     env.pop("MASTER_ADDR")
     env.pop("MASTER_PORT")
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1", "--master-addr",
-           "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"), "--gpus", "1", "--steps", "2",
+    # --standalone: the rendezvous store binds a port the OS picks (a probed-then-closed port was taken by another
+    # process between the probe and torchrun's bind once: EADDRINUSE, gpurun_out/r7a)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--standalone", "--local-addr", "127.0.0.1", "--nnodes=1",
+           "--nproc-per-node", "1", os.path.join(ROOT, "bench.py"), "--gpus", "1", "--steps", "2",
            "--warmup", "1", "--no-cpu-baseline", "--no-secondary", "--no-parity"]
     out = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=110)
     j = _json(out)
