@@ -23,11 +23,10 @@ FLOOR = os.path.join(ROOT, "profiles", "r6", "contraction_floor.json")
 @pytest.fixture(scope="module")
 def cf():
     subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "oracle"), "_build/libnusi_oracle.so", "fc"])
-    import importlib.util
-    spec = importlib.util.spec_from_file_location("contraction_floor", os.path.join(ROOT, "scripts", "contraction_floor.py"))
-    mod = importlib.util.module_from_spec(spec)
-    spec.loader.exec_module(mod)
-    return mod
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "scripts"))   # (importable by name: its spawned workers re-import it)
+    import contraction_floor
+    return contraction_floor
 
 
 def test_contracted_oracle_c2a(cf):
