@@ -67,11 +67,14 @@ def parse():
                     help="NUSI_OPT_CASCADE_RHS: 0 = the library default, 1 = one point per cascade workgroup, 2 = pairs "
                          "of points sharing a table, 3..16 = the gamma batch (k_cascade_bs_gamma)")
     ap.add_argument("--shared-order", action="store_true",
-                    help="the library's default table arithmetic (this repository's dilogarithm series and the batch-"
-                         "shared member Taylor coefficients; bit-exact to the oracle's default mode, faster).  Default "
-                         "here: NUSI_OPT_REFERENCE_ORDER, the reference's own arithmetic (GSL's dilogarithm algorithms "
-                         "on the reference's arguments; bit-exact to the oracle's reference-order mode), the mode whose "
-                         "fluxes are within the north star's 1e-9 of the reference on every config (DESIGN.md sec. 2)")
+                    help="the opt-in fast table arithmetic, NUSI_OPT_REFERENCE_ORDER = 0 (this repository's dilogarithm "
+                         "series and the batch-shared member Taylor coefficients; bit-exact to the oracle's default "
+                         "mode).  Default: NUSI_OPT_REFERENCE_ORDER = 1, the library default -- the reference's own "
+                         "arithmetic (GSL's dilogarithm algorithms on the reference's arguments; bit-exact to the "
+                         "oracle's reference-order mode, DESIGN.md sec. 2)")
+    ap.add_argument("--corner-mb", type=int, default=0,
+                    help="NUSI_OPT_REFO_CORNER_MB (A/B): the reference order's member-corner block budget in MiB, "
+                         "0 = the library's automatic choice")
     ap.add_argument("--reference-order", action="store_true", help="(the default; kept for old command lines)")
     ap.add_argument("--no-parity", action="store_true", help="skip the parity object (oracle fluxes of a sample)")
     ap.add_argument("--dry-run", action="store_true",
@@ -617,6 +620,8 @@ def run(args, world, rank, local, dist, plan, pts, desc, pp_tables):
     if args.rhs:
         plan.set_option(_lib.OPT_CASCADE_RHS, args.rhs)
     plan.set_option(_lib.OPT_REFERENCE_ORDER, 1 if args.reference_order else 0)   # (the library default is 1)
+    if args.corner_mb:
+        plan.set_option(_lib.OPT_REFO_CORNER_MB, args.corner_mb)
     order = "reference" if args.reference_order else "shared-algorithm"
     dev = torch.device("cuda", local)
     flux = torch.empty((P, 3, plan.N), dtype=torch.float64, device=dev)
@@ -706,6 +711,7 @@ def run(args, world, rank, local, dist, plan, pts, desc, pp_tables):
                    "cascade_rhs": args.rhs or "auto",
                    "table_order": order + (" (NUSI_OPT_REFERENCE_ORDER = 1, the library default)" if args.reference_order
                                            else " (NUSI_OPT_REFERENCE_ORDER = 0, opt-in)"),
+                   **({"refo_corner_mb": args.corner_mb} if args.corner_mb else {}),
                    "process_group": dist.get_backend() if dist is not None else None},
         "libnusi": {"path": os.path.relpath(_lib.LIB_PATH, ROOT), "sha256": lib_sha, "pmc_source": tsrc,
                     "pmc_note": pmc_note},
