@@ -440,6 +440,20 @@ struct nusi_plan {
     std::vector<int> slot_of;       // table slot of each point of the last call
     int last_ntab = 0;
     int* d_warn = nullptr;
+    // The per-call inputs in ONE device block and its pinned mirror, uploaded by ONE copy per call (a single
+    // propagation paid a DMA blit of ~4 us per array, five of them, plus a fill for the warnings): sections
+    // [warn | batches | gbgrp | gidx | pts | tpts], each sized for max_points (in_sections); the warnings are zeroed
+    // on the host side of the copy
+    char* d_in = nullptr;
+    char* h_in = nullptr;      // pinned
+    int* h_warn0 = nullptr;    // pinned: the warn section of h_in (zeros)
+    size_t in_tpts = 0;        // byte offset of the tpts section (the copy runs up to its ntab-th Point)
+    // evolve_host's output staging (pinned; the warnings, then flux / flux_fla; only for calls of at most
+    // kStageBytes) and the warnings it fetched, for nusi_plan_warnings without a second round trip
+    char* h_out = nullptr;
+    size_t h_out_bytes = 0;
+    std::vector<int> warn_host;
+    bool warn_host_valid = false;
     nusi::TablesDev tabs{};
     nusi::AlphaTilesDev atiles{};
     nusi::MCornerDev mc{};         // NUSI_OPT_REFERENCE_ORDER: member corners of the big-batch kernel (mcorner_ensure)
@@ -594,6 +608,7 @@ AlphaBatches alpha_batches(nusi_plan* pl, int ntab, std::vector<int>& perm)
 // batch; launch_alpha runs the batches in chunks that fit
 constexpr size_t kMCornerBudget = size_t(8) << 30;
 constexpr int kOverlapTables = 16;   // calls of at most this many tables overlap Gamma / alphaTilde with alpha
+constexpr size_t kStageBytes = size_t(4) << 20;   // nusi_plan_evolve_host's pinned output staging, at most
 int mcorner_ensure(nusi_plan* p, int ntab, const AlphaBatches& ab, int budget_mb)
 {
     nusi::MCornerDev& mc = p->mc;
@@ -803,12 +818,9 @@ void nusi_plan_destroy(nusi_plan* pl)
     if (pl->side) hipStreamDestroy(pl->side);
     for (auto& e : pl->prof_ev) hipEventDestroy(e);
     hipFree(pl->d_grid);
-    hipFree(pl->d_pts);
-    hipFree(pl->d_tpts);
-    if (pl->h_tpts) hipHostFree(pl->h_tpts);
-    hipFree(pl->d_batches);
-    if (pl->h_batches) hipHostFree(pl->h_batches);
-    hipFree(pl->d_warn);
+    hipFree(pl->d_in);   // (d_pts, d_tpts, d_batches, d_warn, d_gidx, d_gbgrp and their pinned mirrors live in it)
+    if (pl->h_in) hipHostFree(pl->h_in);
+    if (pl->h_out) hipHostFree(pl->h_out);
     hipFree(pl->tabs.G);
     hipFree(pl->tabs.At);
     hipFree(pl->tabs.A);
@@ -818,17 +830,12 @@ void nusi_plan_destroy(nusi_plan* pl)
     hipFree(pl->d_src);
     hipFree(pl->d_smap);
     if (pl->h_smap) hipHostFree(pl->h_smap);
-    hipFree(pl->d_gidx);
-    hipFree(pl->d_gbgrp);
     hipFree(pl->d_fh);
-    if (pl->h_gidx) hipHostFree(pl->h_gidx);
-    if (pl->h_gbgrp) hipHostFree(pl->h_gbgrp);
     nusi::alpha_tiles_destroy(&pl->atiles);
     hipFree(pl->mc.buf);
     hipFree(pl->mc.eu);
     hipFree(pl->mc.ue);
     hipFree(pl->d_scratch);
-    if (pl->h_pts) hipHostFree(pl->h_pts);
     if (pl->stream) hipStreamDestroy(pl->stream);
     pl->spl.reset();
     nusi_plan* sh = pl->shift;
@@ -895,13 +902,29 @@ int nusi_plan_create(int device, int N_bins_E, double lEmin, double lEmax, doubl
     gd.step_s = q;
     q += G.Nz;
     gd.sfr = q;
-    HIPCHECK(hipMalloc(&pl->d_pts, sizeof(nusi::Point) * max_points));
-    HIPCHECK(hipHostMalloc((void**)&pl->h_pts, sizeof(nusi::Point) * max_points, hipHostMallocDefault));
-    HIPCHECK(hipMalloc(&pl->d_tpts, sizeof(nusi::Point) * max_points));
-    HIPCHECK(hipHostMalloc((void**)&pl->h_tpts, sizeof(nusi::Point) * max_points, hipHostMallocDefault));
-    HIPCHECK(hipMalloc(&pl->d_batches, sizeof(int) * max_points));
-    HIPCHECK(hipHostMalloc((void**)&pl->h_batches, sizeof(int) * max_points, hipHostMallocDefault));
-    HIPCHECK(hipMalloc(&pl->d_warn, sizeof(int) * max_points));
+    {   // the per-call input block (nusi_plan::d_in)
+        const size_t mp = (size_t)max_points;
+        auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
+        const size_t o_warn = 0, o_bat = al(o_warn + sizeof(int) * mp), o_grp = al(o_bat + sizeof(int) * mp);
+        const size_t o_gidx = al(o_grp + sizeof(int2) * mp), o_pts = al(o_gidx + sizeof(int) * mp);
+        const size_t o_tpts = al(o_pts + sizeof(nusi::Point) * mp), tot = o_tpts + sizeof(nusi::Point) * mp;
+        HIPCHECK(hipMalloc(&pl->d_in, tot));
+        HIPCHECK(hipHostMalloc((void**)&pl->h_in, tot, hipHostMallocDefault));
+        memset(pl->h_in, 0, tot);
+        pl->d_warn = (int*)(pl->d_in + o_warn);
+        pl->h_warn0 = (int*)(pl->h_in + o_warn);
+        pl->d_batches = (int*)(pl->d_in + o_bat);
+        pl->h_batches = (int*)(pl->h_in + o_bat);
+        pl->d_gbgrp = (int2*)(pl->d_in + o_grp);
+        pl->h_gbgrp = (int2*)(pl->h_in + o_grp);
+        pl->d_gidx = (int*)(pl->d_in + o_gidx);
+        pl->h_gidx = (int*)(pl->h_in + o_gidx);
+        pl->d_pts = (nusi::Point*)(pl->d_in + o_pts);
+        pl->h_pts = (nusi::Point*)(pl->h_in + o_pts);
+        pl->d_tpts = (nusi::Point*)(pl->d_in + o_tpts);
+        pl->h_tpts = (nusi::Point*)(pl->h_in + o_tpts);
+        pl->in_tpts = o_tpts;
+    }
     HIPCHECK(hipMalloc(&pl->tabs.G, sizeof(double) * (size_t)G.T * max_points));
     HIPCHECK(hipMalloc(&pl->tabs.At, sizeof(double) * (size_t)G.T * max_points));
     HIPCHECK(hipMalloc(&pl->tabs.A, sizeof(double) * (size_t)gd.PT * max_points));
@@ -971,6 +994,7 @@ int nusi_plan_evolve(nusi_plan* pl, const nusi_params* pts, int n, double* d_flu
 {
     if (n < 1 || n > pl->max_points) return fail(NUSI_EPARAM, "number of points outside [1, max_points]");
     HIPCHECK(hipSetDevice(pl->device));
+    pl->warn_host_valid = false;
     hipStream_t s = stream ? (hipStream_t)stream : pl->stream;
     if (pl->ran) {
         HIPCHECK(hipEventSynchronize(pl->ev_copy));          // the pinned h_pts / h_tpts / h_batches are reused
@@ -1059,12 +1083,6 @@ int nusi_plan_evolve(nusi_plan* pl, const nusi_params* pts, int n, double* d_flu
     int ngb = 0, ngidx = 0;
     int bs_nwg[3] = {0, 0, 0};   // workgroups of P = 16, 2, 1 (their groups in h_gbgrp in that order)
     if (bs) {
-        if (!pl->d_gidx) {
-            HIPCHECK(hipMalloc(&pl->d_gidx, sizeof(int) * pl->max_points));
-            HIPCHECK(hipMalloc(&pl->d_gbgrp, sizeof(int2) * pl->max_points));
-            HIPCHECK(hipHostMalloc((void**)&pl->h_gidx, sizeof(int) * pl->max_points, hipHostMallocDefault));
-            HIPCHECK(hipHostMalloc((void**)&pl->h_gbgrp, sizeof(int2) * pl->max_points, hipHostMallocDefault));
-        }
         const int rmax = force_passes ? 1 : pl->cascade_rhs == 0 ? 16 : pl->cascade_rhs;
         const bool g16 = rmax >= 3 && nusi::cascade_bs_config(pl->gd, 16, false) != 0;
         const bool g2 = rmax >= 2 && nusi::cascade_bs_config(pl->gd, 2, false) != 0;
@@ -1118,13 +1136,8 @@ int nusi_plan_evolve(nusi_plan* pl, const nusi_params* pts, int n, double* d_flu
     }
     if (mcorn && nbase && pl->shift_batches.nbatch)
         if (int r = mcorner_ensure(pl->shift, nbase, pl->shift_batches, pl->corner_mb)) return r;
-    if (ngb) {
-        HIPCHECK(hipMemcpyAsync(pl->d_gidx, pl->h_gidx, sizeof(int) * ngidx, hipMemcpyHostToDevice, s));
-        HIPCHECK(hipMemcpyAsync(pl->d_gbgrp, pl->h_gbgrp, sizeof(int2) * ngb, hipMemcpyHostToDevice, s));
-    }
-    HIPCHECK(hipMemcpyAsync(pl->d_pts, pl->h_pts, sizeof(nusi::Point) * n, hipMemcpyHostToDevice, s));
-    HIPCHECK(hipMemcpyAsync(pl->d_tpts, pl->h_tpts, sizeof(nusi::Point) * ntab, hipMemcpyHostToDevice, s));
-    if (nbatch) HIPCHECK(hipMemcpyAsync(pl->d_batches, pl->h_batches, sizeof(int) * nbatch, hipMemcpyHostToDevice, s));
+    // one upload: the zeroed warnings, batches, gamma groups, points and tables (nusi_plan::d_in)
+    HIPCHECK(hipMemcpyAsync(pl->d_in, pl->h_in, pl->in_tpts + sizeof(nusi::Point) * ntab, hipMemcpyHostToDevice, s));
     nusi_plan* sp = nbase ? pl->shift : nullptr;
     if (sp) {
         HIPCHECK(hipMemcpyAsync(pl->d_smap, pl->h_smap, sizeof(int2) * (ntab - nd), hipMemcpyHostToDevice, s));
@@ -1137,7 +1150,6 @@ int nusi_plan_evolve(nusi_plan* pl, const nusi_params* pts, int n, double* d_flu
         sp->ran = true;
     }
     HIPCHECK(hipEventRecord(pl->ev_copy, s));
-    HIPCHECK(hipMemsetAsync(pl->d_warn, 0, sizeof(int) * ntab, s));
     const nusi::SplineSet* spl = pl->spl ? pl->spl->d_set : pl->d_nospl;
     hipEvent_t* ev = pl->ev;
     if (pl->prof_n < pl->prof_max) ev = &pl->prof_ev[4 * (size_t)pl->prof_n++];
@@ -1328,6 +1340,10 @@ int nusi_plan_warnings(nusi_plan* pl, int* out, int n)
 {
     if (!pl->ran) return fail(NUSI_ESTATE, "no evolve has run on this plan");
     if (n > pl->last_n) n = pl->last_n;
+    if (pl->warn_host_valid) {   // (fetched by nusi_plan_evolve_host with the fluxes)
+        for (int i = 0; i < n; ++i) out[i] = pl->warn_host[pl->slot_of[i]];
+        return NUSI_OK;
+    }
     HIPCHECK(hipSetDevice(pl->device));
     HIPCHECK(hipEventSynchronize(pl->last_ev[3]));
     std::vector<int> w(pl->last_ntab);
@@ -1361,15 +1377,43 @@ int nusi_plan_evolve_host(nusi_plan* pl, const nusi_params* pts, int n, double* 
 {
     int r = nusi_plan_evolve(pl, pts, n, nullptr, nullptr, nullptr);
     if (r) return r;
-    const size_t N3 = (size_t)3 * pl->grid.N;
-    HIPCHECK(hipStreamSynchronize(pl->stream));
+    const size_t N3 = (size_t)3 * pl->grid.N, fb = sizeof(double) * N3 * n;
+    const size_t wb = (sizeof(int) * pl->last_ntab + 255) & ~(size_t)255;
+    hipStream_t s = pl->stream;
+    const double* dflux = pl->d_scratch;
+    const double* dfla = pl->d_scratch + N3 * pl->max_points;
+    pl->warn_host.resize(pl->last_ntab);
+    if (wb + 2 * fb <= kStageBytes) {
+        // small calls (the object API's single propagation): the warnings and both flux arrays into one pinned
+        // staging buffer, one synchronisation, then host copies (pageable hipMemcpy round trips cost ~20 us each)
+        if (pl->h_out_bytes < wb + 2 * fb) {
+            if (pl->h_out) HIPCHECK(hipHostFree(pl->h_out));
+            pl->h_out = nullptr;
+            pl->h_out_bytes = 0;
+            HIPCHECK(hipHostMalloc((void**)&pl->h_out, wb + 2 * fb, hipHostMallocDefault));
+            pl->h_out_bytes = wb + 2 * fb;
+        }
+        HIPCHECK(hipMemcpyAsync(pl->h_out, pl->d_warn, sizeof(int) * pl->last_ntab, hipMemcpyDeviceToHost, s));
+        if (n == pl->max_points)   // flux and flux_fla adjacent in d_scratch
+            HIPCHECK(hipMemcpyAsync(pl->h_out + wb, dflux, 2 * fb, hipMemcpyDeviceToHost, s));
+        else {
+            HIPCHECK(hipMemcpyAsync(pl->h_out + wb, dflux, fb, hipMemcpyDeviceToHost, s));
+            HIPCHECK(hipMemcpyAsync(pl->h_out + wb + fb, dfla, fb, hipMemcpyDeviceToHost, s));
+        }
+        HIPCHECK(hipStreamSynchronize(s));
+        memcpy(pl->warn_host.data(), pl->h_out, sizeof(int) * pl->last_ntab);
+        if (flux) memcpy(flux, pl->h_out + wb, fb);
+        if (fla) memcpy(fla, pl->h_out + wb + fb, fb);
+    } else {
+        HIPCHECK(hipStreamSynchronize(s));
+        HIPCHECK(hipMemcpy(pl->warn_host.data(), pl->d_warn, sizeof(int) * pl->last_ntab, hipMemcpyDeviceToHost));
+        if (flux) HIPCHECK(hipMemcpy(flux, dflux, fb, hipMemcpyDeviceToHost));
+        if (fla) HIPCHECK(hipMemcpy(fla, dfla, fb, hipMemcpyDeviceToHost));
+    }
+    pl->warn_host_valid = true;
     int bad = 0;
-    std::vector<int> w(pl->last_ntab);
-    HIPCHECK(hipMemcpy(w.data(), pl->d_warn, sizeof(int) * w.size(), hipMemcpyDeviceToHost));
-    for (int v : w) bad |= (v & nusi::kWarnSplineOOB);
+    for (int v : pl->warn_host) bad |= (v & nusi::kWarnSplineOOB);
     if (bad) return fail(NUSI_EINTERP, "Error at interp: a phi-phi table lookup fell outside the node range");
-    if (flux) HIPCHECK(hipMemcpy(flux, pl->d_scratch, sizeof(double) * N3 * n, hipMemcpyDeviceToHost));
-    if (fla) HIPCHECK(hipMemcpy(fla, pl->d_scratch + N3 * pl->max_points, sizeof(double) * N3 * n, hipMemcpyDeviceToHost));
     return NUSI_OK;
 }
 
