@@ -132,7 +132,7 @@ NUSI_FN double hypot(double x, double y)
 // the use of the row before it; no value changes.
 NUSI_FN void row_fence()
 {
-#ifdef __HIP_DEVICE_COMPILE__
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(NUSI_NO_ROW_FENCE)   // (NUSI_NO_ROW_FENCE: A/B builds)
     __builtin_amdgcn_sched_barrier(0);
 #endif
 }
