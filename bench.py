@@ -468,7 +468,9 @@ def secondary_lines(local):
             out[name]["workload"] = d["config"]["workload"]
             out[name]["table_order"] = d["config"].get("table_order")
             out[name]["kernels"] = [d["config"]["alpha_kernel"], d["config"]["cascade_kernel"]]
-            out[name]["roofline"] = {k: d["roofline"].get(k) for k in ("kernel", "achieved", "unit", "frac", "traffic")}
+            out[name]["roofline"] = {k: d["roofline"].get(k) for k in ("bound", "kernel", "achieved", "unit", "frac",
+                                                                       "traffic", "critical_path")
+                                     if k in d["roofline"]}
             if "cpu_baseline" in d:
                 cb = d["cpu_baseline"]
                 out[name]["cpu_baseline"] = {k: cb.get(k) for k in ("value", "unit", "cores", "kind", "sample",
@@ -772,6 +774,21 @@ def run(args, world, rank, local, dist, plan, pts, desc, pp_tables):
                                pmc_note or "no PMC summary of this workload (scripts/gpu_profile_all.sh)")}
     else:   # the cascade dominates (C5's gamma batches)
         out["roofline"] = dict(out["roofline_cascade"])
+    if P == 1:   # a single propagation is latency-bound, not HBM- or VALU-bound: its critical path instead
+        st = [m / max(ncalls, 1) for m in sum_ms]
+        out["roofline"] = {
+            "bound": "latency", "kernel": "critical path of one evolve()", "unit": "ms",
+            "achieved": dt / args.steps * 1e3, "peak": None, "frac": None, "traffic": None,
+            "critical_path": {
+                "tables_ms": st[0] + st[1],
+                "tables_note": "Gamma / alphaTilde (%s, side stream) beside the alpha kernels (%s): the later of the two "
+                               "(stage events: gamma_alphatilde = the side stream's end, alpha = what alpha ran past it)"
+                               % ("k_gamma_alphat", alpha_kernel),
+                "cascade_ms": st[2], "cascade_dependent_stages": plan.T,
+                "cascade_ns_per_stage": st[2] * 1e6 / plan.T,
+                "launch_and_gaps_ms": dt / args.steps * 1e3 - sum(st)},
+            "note": "one point fills a few dozen workgroups: the step is the Stage-A kernels' slowest lanes (GSL's "
+                    "series, up to ~900 terms for |w| near 0.98) and the cascade's T dependent stages, not a bandwidth"}
     if dist is not None and args.workload in ("c4", "c4s", "c5"):
         # the scan's only data exchange, after the timed region: the fluxes of every rank's block gathered to rank 0
         # (nusiprop_amd.dist._gather_blocks, as evolve_sharded does; float64 tensors staged on the GPU, RCCL)

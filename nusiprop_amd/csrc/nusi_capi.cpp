@@ -458,6 +458,8 @@ struct nusi_plan {
     nusi::AlphaTilesDev atiles{};
     nusi::MCornerDev mc{};         // NUSI_OPT_REFERENCE_ORDER: member corners of the big-batch kernel (mcorner_ensure)
     double* d_scratch = nullptr;   // flux outputs when the caller passes NULL
+    double* d_kt = nullptr;        // the k-split alpha path's term buffer (TablesDev::Kt), kt_doubles doubles
+    size_t kt_doubles = 0;
     std::shared_ptr<SplineStore> spl;
     nusi::SplineSet* d_nospl = nullptr;   // an empty spline set in device memory (no phi-phi tables loaded)
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
@@ -609,6 +611,7 @@ AlphaBatches alpha_batches(nusi_plan* pl, int ntab, std::vector<int>& perm)
 constexpr size_t kMCornerBudget = size_t(8) << 30;
 constexpr int kOverlapTables = 16;   // calls of at most this many tables overlap Gamma / alphaTilde with alpha
 constexpr size_t kStageBytes = size_t(4) << 20;   // nusi_plan_evolve_host's pinned output staging, at most
+constexpr int kSplitTables = 2;   // calls of at most this many tables (no phi-phi) run the k-split alpha path
 int mcorner_ensure(nusi_plan* p, int ntab, const AlphaBatches& ab, int budget_mb)
 {
     nusi::MCornerDev& mc = p->mc;
@@ -836,6 +839,7 @@ void nusi_plan_destroy(nusi_plan* pl)
     hipFree(pl->mc.eu);
     hipFree(pl->mc.ue);
     hipFree(pl->d_scratch);
+    hipFree(pl->d_kt);
     if (pl->stream) hipStreamDestroy(pl->stream);
     pl->spl.reset();
     nusi_plan* sh = pl->shift;
@@ -1136,6 +1140,20 @@ int nusi_plan_evolve(nusi_plan* pl, const nusi_params* pts, int n, double* d_flu
     }
     if (mcorn && nbase && pl->shift_batches.nbatch)
         if (int r = mcorner_ensure(pl->shift, nbase, pl->shift_batches, pl->corner_mb)) return r;
+    // a call of few tables without the phi-phi channel: the k-split alpha path (TablesDev::Kt, 8 doubles per entry,
+    // mass state and table; 11.5 MB per table at N_E = 300); scans keep the k loop inside the workgroup
+    pl->tabs.Kt = nullptr;
+    if (nbase == 0 && nd > 0 && nd <= kSplitTables && nb_plain == nbatch && pl->alpha_kind == 0) {
+        const size_t need = (size_t)8 * 3 * (size_t)pl->gd.PT * nd;
+        if (pl->kt_doubles < need) {
+            hipFree(pl->d_kt);
+            pl->d_kt = nullptr;
+            pl->kt_doubles = 0;
+            HIPCHECK(hipMalloc(&pl->d_kt, sizeof(double) * need));
+            pl->kt_doubles = need;
+        }
+        pl->tabs.Kt = pl->d_kt;
+    }
     // one upload: the zeroed warnings, batches, gamma groups, points and tables (nusi_plan::d_in)
     HIPCHECK(hipMemcpyAsync(pl->d_in, pl->h_in, pl->in_tpts + sizeof(nusi::Point) * ntab, hipMemcpyHostToDevice, s));
     nusi_plan* sp = nbase ? pl->shift : nullptr;

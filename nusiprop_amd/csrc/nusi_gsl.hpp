@@ -125,18 +125,6 @@ NUSI_FN double hypot(double x, double y)
     return h * s;
 }
 
-// The series loops read the next iteration's table row through the scalar cache.  A scalar load's counter only waits
-// to zero (they return out of order), so a row load the scheduler hoists above the current row's use makes that use
-// wait for the new load too -- a full scalar-cache round trip per iteration, exposed whenever few waves share a SIMD
-// (a single propagation's member corners, whose slowest lanes run ~900 terms).  The fence keeps each prefetch below
-// the use of the row before it; no value changes.
-NUSI_FN void row_fence()
-{
-#if defined(__HIP_DEVICE_COMPILE__) && !defined(NUSI_NO_ROW_FENCE)   // (NUSI_NO_ROW_FENCE: A/B builds)
-    __builtin_amdgcn_sched_barrier(0);
-#endif
-}
-
 // Wave-uniform votes for the series' first loops (below): every active lane's predicate / any active lane's.  On the
 // host (tests/hostcheck) a "wave" is the one call.
 NUSI_FN bool wave_all(bool p)
@@ -168,13 +156,9 @@ NUSI_FN double dilog_series_1_t(double x)
     if (!kExact) {
         const double big = x * 0x1p-50;
         bool small = false;
-        double rrn = kKT.rr[2];   // (the next iteration's row, loaded one ahead: row_fence)
         while (k < 1000) {
-            const double rr = rrn;
             term *= x;
-            term *= rr;
-            row_fence();
-            rrn = kKT.rr[k + 1 < kKTab ? k + 1 : k];
+            term *= kKT.rr[k];
             sum += term;
             small = wave_any(term < big);
             if (small) break;
@@ -215,13 +199,9 @@ NUSI_FN double series_2_t(double x)
         const double big = x * 0x1p-51;
         double ds = 0.0;
         bool small = false;
-        KRow nx = kKT.row[k];   // (the next iteration's row, loaded one ahead: row_fence)
         while (k < 100) {
-            const KRow kr = nx;
             rk *= x;
-            ds = div_k<false>(rk, kr.d2, kr.y2, kr.l2);
-            row_fence();
-            nx = kKT.row[k + 1];
+            ds = div_k<false>(rk, kKT.row[k].d2, kKT.row[k].y2, kKT.row[k].l2);
             sum += ds;
             small = wave_any(ds < big);
             if (small) break;
@@ -359,8 +339,11 @@ NUSI_FN void cseries_t(bool s2, double r, double lr, double x, double y, double&
     double imag_sum = t2 ? 0.5 * r * sk : r * sk;
     const double nlr = -lr;   // -log(r)
     const int kmax = t2 ? 30 + (int)(18.0 / nlr) : 50 + (int)(22.0 / nlr);
+    KRow next = kKT.row[2];   // (the table row of the next iteration is loaded one iteration ahead; kmax <= 921)
     double q = 0.0, dr = 0.0, di = 0.0;
-    auto term = [&](const KRow& kr) {   // term k from table row k (kmax <= 921 < kKTab)
+    auto term = [&](int k) {
+        const KRow kr = next;
+        next = kKT.row[k + 1];
         const double ck_tmp = ck;
         ck = ck - (alpha * ck + beta * sk);
         sk = sk - (alpha * sk - beta * ck_tmp);
@@ -382,50 +365,34 @@ NUSI_FN void cseries_t(bool s2, double r, double lr, double x, double y, double&
         // added, then each lane's test at k -- false for the lanes still above it)
         const double big = r * 0x1p-50;
         bool small = false;
-        // two terms per kmax vote while both are below every lane's kmax (the same terms and exit as one at a time);
-        // the rows of the next pair are loaded while this pair runs (row_fence)
-        KRow ra = kKT.row[2], rb = kKT.row[3];
+        // two terms per kmax vote while both are below every lane's kmax (the same terms and exit as one at a time)
         while (wave_all(k + 1 < kmax)) {
-            const KRow a = ra, b = rb;
-            term(a);
-            row_fence();
-            ra = kKT.row[k + 2];
-            rb = kKT.row[k + 3];
+            term(k);
             small = wave_any(q < big);
             if (small) break;
             ++k;
-            term(b);
+            term(k);
             small = wave_any(q < big);
             if (small) break;
             ++k;
         }
-        if (!small) {
-            KRow nx = kKT.row[k];
+        if (!small)
             while (wave_all(k < kmax)) {
-                const KRow a = nx;
-                term(a);
-                row_fence();
-                nx = kKT.row[k + 1];
+                term(k);
                 small = wave_any(q < big);
                 if (small) break;
                 ++k;
             }
-        }
         if (small) {
             done = stop();
             ++k;
         }
     }
-    if (!done) {
-        KRow nx = kKT.row[k < kKTab ? k : kKTab - 1];   // (k <= kmax <= 921 here)
+    if (!done)
         for (; k < kmax; k++) {
-            const KRow a = nx;
-            term(a);
-            row_fence();
-            nx = kKT.row[k + 1];
+            term(k);
             if (stop()) break;
         }
-    }
     re = real_sum;
     im = imag_sum;
 }

@@ -37,6 +37,8 @@ struct TablesDev {
     int* Wmin;    // [npts][4][T] or nullptr (only the base plan of NUSI_OPT_SHIFT_REUSE): per warning bit b and table
                   // row n, the smallest column m of an entry (n, m) that raised it (Gamma / alphaTilde: m = n), so
                   // that k_table_shift passes on exactly the warnings of the rows a shifted slot reads
+    double* Kt = nullptr;   // [npts][3][PT][8] or nullptr: the k-split alpha path of calls of few tables
+                            // (launch_alpha): each mass state's terms of every entry, summed in order by k_alpha_ksum
 };
 
 // Tiles of the alpha table for k_alpha_tile: kAlphaTile x kAlphaTile (n, m) bin blocks with

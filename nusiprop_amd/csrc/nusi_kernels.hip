@@ -348,6 +348,10 @@ constexpr bool kBatchPipe = NUSI_BATCH_PIPE != 0;
 #define NUSI_REFO_PREFETCH 1
 #endif
 constexpr bool kRefPrefetch = NUSI_REFO_PREFETCH != 0;
+#ifndef NUSI_BATCH_KLAUNCH   // A/B: 1 = the non-phi-phi batch kernels as one launch per mass state (kOneK)
+#define NUSI_BATCH_KLAUNCH 0
+#endif
+constexpr bool kBatchKLaunch = NUSI_BATCH_KLAUNCH != 0;
 #ifndef NUSI_REFO_BSTUB   // timing A/B only (wrong tables): bit 1 the batch kernel without the block's loads
 #define NUSI_REFO_BSTUB 0
 #endif
@@ -489,12 +493,17 @@ void mcorner_edges(int T, const double* lo, const double* hi, std::vector<int>& 
 // kPP: the batches' tables have the phi-phi channel (its shared term per k).  kRef: NUSI_OPT_REFERENCE_ORDER -- each
 // point's member corners in the reference's operation order, read from k_alpha_mcorner's block mc (Dcr, Dci, A into
 // the X block, which then holds no Taylor coefficients; pc0: the first table of the launch chunk), the rest of the
-// batch structure unchanged
-template <bool kPP, bool kRef>
+// batch structure unchanged.  kSplit (calls of few tables, a single propagation): mass state k = blockIdx.z only,
+// its terms of every entry recorded into kt ([table][3][PT][8]: up to 7 terms, then their count, -1 for an entry
+// the resonant-only table does not compute) for k_alpha_ksum -- three times the workgroups, each a third as long
+// kOneK (NUSI_BATCH_KLAUNCH A/B): one mass state per launch, kone, the launches k = 0, 1, 2 in order on the stream
+// (the running sum through A as in the loop): no state lives across the k loop
+template <bool kPP, bool kRef, bool kSplit = false, bool kOneK = false>
 __global__ __launch_bounds__(kTileThreads) __attribute__((amdgpu_waves_per_eu(batch_waves(kPP, kRef), batch_waves(kPP, kRef))))
 void k_alpha_batch(GridDev g, const Point* __restrict__ pts, const SplineSet* __restrict__ splp, const int* __restrict__ tiles,
                    const int* __restrict__ batches, double* __restrict__ A, const double* __restrict__ med,
-                   int* __restrict__ warn, int* __restrict__ wmin, MCornerDev mc, int pc0)
+                   int* __restrict__ warn, int* __restrict__ wmin, MCornerDev mc, int pc0, double* __restrict__ kt,
+                   int kone = 0)
 {
     extern __shared__ __attribute__((aligned(16))) double sm[];
     const SplineSet& spl = *splp;
@@ -559,8 +568,9 @@ void k_alpha_batch(GridDev g, const Point* __restrict__ pts, const SplineSet* __
     double* mix = X + 4 * kCC;
     const int mjobs = ct + cs + kAlphaTile;
     int wsh = 0;
+    const int kb = kSplit ? (int)blockIdx.z : kOneK ? kone : 0, ke = (kSplit || kOneK) ? kb + 1 : 3;
 #pragma unroll 1
-    for (int k = 0; k < 3; ++k) {
+    for (int k = kb; k < ke; ++k) {
         __syncthreads();   // the previous k's points are done with P3, X, mem, edgk, membq
         if (tid < mjobs) alpha_tile_edge_job_k(P, k, tid, tE, ct, sE, cs, g.lo, g.hi, m0, Tm, edgk);
         __syncthreads();
@@ -593,7 +603,7 @@ void k_alpha_batch(GridDev g, const Point* __restrict__ pts, const SplineSet* __
         // loop spill at 4 waves per SIMD, 6.7 ms at 3; profiles/r3/r3q.)
         // A point's entry accumulates over the mass states in A; the sum of the states < k is loaded one
         // point ahead (timed equal to loading it in place, profiles/r2m: four blocks per CU already hide it).
-        const bool reload = k > 0 && needed;
+        const bool reload = !kSplit && k > 0 && needed;
         double tnext = reload ? A[(size_t)p0 * g.PT + eidx] : 0.0;
         // member edges: thread (mq, mjob) copies job mjob of point mq of each chunk (loading the next chunk's
         // values a chunk ahead measured slower: their registers stay live through the combine)
@@ -673,6 +683,7 @@ void k_alpha_batch(GridDev g, const Point* __restrict__ pts, const SplineSet* __
                     __syncthreads();   // mem of q written
                 }
                 int w = 0;
+                TermRec rec;
                 if (needed) {
                     SplitLeavesT<kRef> lv;
                     lv.cf[0] = P3; lv.cf[1] = P3; lv.cf[2] = P3; lv.cf[3] = P3; lv.cf[4] = P3;
@@ -684,16 +695,61 @@ void k_alpha_batch(GridDev g, const Point* __restrict__ pts, const SplineSet* __
                     lv.tedm = memb; lv.sedm = memb + ct; lv.mbm = memb + ct + 2 * cs;
                     lv.marg = kRef ? X + (3 + qq) * kCC : memb + ct + 2 * cs + kAlphaTile + 2 * ct;   // sT | fT | sS | fS
                     lv.xl = mix; lv.yl = mix;   // (not read with pre)
-                    alpha_k<SplitLeavesT<kRef>, kPP>(Q, spl, k, g.lo[n], g.hi[n], g.lo[m], g.hi[m], lv, tot, w,
-                                                     cornered ? &pre : nullptr, kPP && cornered ? &ppt : nullptr);
+                    if (kSplit)
+                        alpha_k<SplitLeavesT<kRef>, kPP>(Q, spl, k, g.lo[n], g.hi[n], g.lo[m], g.hi[m], lv, rec, w,
+                                                         cornered ? &pre : nullptr, kPP && cornered ? &ppt : nullptr);
+                    else
+                        alpha_k<SplitLeavesT<kRef>, kPP>(Q, spl, k, g.lo[n], g.hi[n], g.lo[m], g.hi[m], lv, tot, w,
+                                                         cornered ? &pre : nullptr, kPP && cornered ? &ppt : nullptr);
                 }
-                if (valid) A[(size_t)(p0 + q) * g.PT + eidx] = needed ? tot : 0.0;
+                if (kSplit) {
+                    if (valid) {
+                        double* o = kt + ((((size_t)(p0 + q) * 3 + k) * g.PT + eidx) << 3);
+#pragma unroll
+                        for (int j = 0; j < 7; ++j) o[j] = rec.v[j];
+                        o[7] = needed ? (double)rec.n : -1.0;
+                    }
+                } else if (valid) A[(size_t)(p0 + q) * g.PT + eidx] = needed ? tot : 0.0;
                 if (w) warn_entry(warn, wmin, T, p0 + q, w, n, m);
             }
         }
     }
     if (wsh)   // (the batch-shared phi-phi term of this thread's entry)
         for (int q = 0; q < nb; ++q) warn_entry(warn, wmin, T, p0 + q, wsh, n, m);
+}
+
+// The k-split path's sums (k_alpha_batch<.., kSplit>): every class-0 entry of the batches' tables, its mass states'
+// recorded terms added in order from 0.0 -- k_alpha_batch's own additions (tot starts at 0.0 for k = 0 and at the
+// previous states' sum after), so the same bits; 0.0 for entries a resonant-only table does not compute.  Grid and
+// tile decode as k_alpha_batch's
+__global__ __launch_bounds__(kTileThreads) void k_alpha_ksum(GridDev g, const int* __restrict__ tiles,
+                                                             const int* __restrict__ batches, const double* __restrict__ kt,
+                                                             double* __restrict__ A)
+{
+    const int tid = threadIdx.x, T = g.T;
+    const int bw = batches[blockIdx.y];
+    const int p0 = bw & 0xffffff, nb = (int)((unsigned)bw >> 24);
+    const unsigned tu = (unsigned)tiles[blockIdx.x];
+    const int half = (tu >> 28) & 3, nhalf = (tu >> 30) & 3;
+    const int n0 = (tu & 0x3fff) * kAlphaTile + (nhalf == 2 ? 8 : 0);
+    const int m0 = ((tu >> 14) & 0x3fff) * kAlphaTile + (half == 2 ? 8 : 0);
+    const int mcnt = half == 0 ? kAlphaTile : (half == 1 ? 8 : kAlphaTile - 8);
+    const int ncnt = nhalf == 0 ? kAlphaTile : (nhalf == 1 ? 8 : kAlphaTile - 8);
+    const int Tm = (m0 + mcnt < T) ? m0 + mcnt : T, Tn = (n0 + ncnt < T) ? n0 + ncnt : T;
+    const int n = n0 + tid % kAlphaTile, m = m0 + tid / kAlphaTile;
+    if (!(tid < kAlphaTile * kAlphaTile && n < m && m < Tm && n < Tn)) return;
+    const size_t eidx = (size_t)m * (m - 1) / 2 + n;
+    for (int q = 0; q < nb; ++q) {
+        double tot = 0.0;
+        bool skip = false;
+        for (int k = 0; k < 3; ++k) {
+            const double* o = kt + ((((size_t)(p0 + q) * 3 + k) * g.PT + eidx) << 3);
+            const int cnt = (int)o[7];
+            if (cnt < 0) skip = true;
+            for (int j = 0; j < cnt; ++j) tot += o[j];
+        }
+        A[(size_t)(p0 + q) * g.PT + eidx] = skip ? 0.0 : tot;
+    }
 }
 
 // NUSI_OPT_SHIFT_REUSE: table slot s0 + q <- base table map[q].x of the extended axis (Tb bins),
@@ -832,14 +888,29 @@ static hipError_t launch_alpha_t(const GridDev& g, const Point* pts, int npts, c
                     hipLaunchKernelGGL(k_alpha_medge, dim3((unsigned)((5 * g.T + 255) / 256), npts, 3), dim3(256), 0, s,
                                        g, pts, t.Med);
                 }
+                // (NUSI_BATCH_KLAUNCH: the non-phi-phi batches as three launches, one per mass state)
+                // t.Kt (calls of few tables, no phi-phi channel): the k-split instance, its mass states' workgroups at
+                // once, and k_alpha_ksum's ordered sums
+                const bool split = t.Kt && nb_plain == nbatches;
                 if (!kRef) {
-                    if (nb_plain > 0)
+                    if (split) {
+                        hipLaunchKernelGGL((k_alpha_batch<false, false, true>), dim3(at.ncls[0], nbatches, 3),
+                                           dim3(kTileThreads), lds, s, g, pts, spl, at.tiles, batches, t.A, t.Med, warn,
+                                           t.Wmin, MCornerDev{}, 0, t.Kt);
+                        hipLaunchKernelGGL(k_alpha_ksum, dim3(at.ncls[0], nbatches), dim3(kTileThreads), 0, s, g, at.tiles,
+                                           batches, t.Kt, t.A);
+                    } else if (nb_plain > 0 && kBatchKLaunch) {
+                        for (int kk = 0; kk < 3; ++kk)
+                            hipLaunchKernelGGL((k_alpha_batch<false, false, false, true>), dim3(at.ncls[0], nb_plain),
+                                               dim3(kTileThreads), lds, s, g, pts, spl, at.tiles, batches, t.A, t.Med, warn,
+                                               t.Wmin, MCornerDev{}, 0, nullptr, kk);
+                    } else if (nb_plain > 0)
                         hipLaunchKernelGGL((k_alpha_batch<false, false>), dim3(at.ncls[0], nb_plain), dim3(kTileThreads),
-                                           lds, s, g, pts, spl, at.tiles, batches, t.A, t.Med, warn, t.Wmin, MCornerDev{}, 0);
+                                           lds, s, g, pts, spl, at.tiles, batches, t.A, t.Med, warn, t.Wmin, MCornerDev{}, 0, nullptr);
                     if (nbatches > nb_plain)
                         hipLaunchKernelGGL((k_alpha_batch<true, false>), dim3(at.ncls[0], nbatches - nb_plain),
                                            dim3(kTileThreads), lds, s, g, pts, spl, at.tiles, batches + nb_plain, t.A,
-                                           t.Med, warn, t.Wmin, MCornerDev{}, 0);
+                                           t.Med, warn, t.Wmin, MCornerDev{}, 0, nullptr);
                 } else {
                     // the member corners of a chunk of whole batches (<= mc->cap_tables tables, the phi-phi batches
                     // in chunks of their own), then the chunk's tiles.  (k_alpha_mcorner of chunk c + 1 on a second
@@ -864,14 +935,25 @@ static hipError_t launch_alpha_t(const GridDev& g, const Point* pts, int npts, c
                         const int cbmin = jobs / nbmax;
                         hipLaunchKernelGGL(k_alpha_mcorner, dim3((unsigned)((mc->NC + cbmin - 1) / cbmin), e - b, 3),
                                            dim3(256), 0, s, pts, batches + b, *mc, pc0, jobs);
-                        if (b < nb_plain)
+                        if (split) {
+                            hipLaunchKernelGGL((k_alpha_batch<false, true, true>), dim3(at.ncls[0], e - b, 3),
+                                               dim3(kTileThreads), lds, s, g, pts, spl, at.tiles, batches + b, t.A, t.Med,
+                                               warn, t.Wmin, *mc, pc0, t.Kt);
+                            hipLaunchKernelGGL(k_alpha_ksum, dim3(at.ncls[0], e - b), dim3(kTileThreads), 0, s, g,
+                                               at.tiles, batches + b, t.Kt, t.A);
+                        } else if (b < nb_plain && kBatchKLaunch) {
+                            for (int kk = 0; kk < 3; ++kk)
+                                hipLaunchKernelGGL((k_alpha_batch<false, true, false, true>), dim3(at.ncls[0], e - b),
+                                                   dim3(kTileThreads), lds, s, g, pts, spl, at.tiles, batches + b, t.A,
+                                                   t.Med, warn, t.Wmin, *mc, pc0, nullptr, kk);
+                        } else if (b < nb_plain)
                             hipLaunchKernelGGL((k_alpha_batch<false, true>), dim3(at.ncls[0], e - b), dim3(kTileThreads),
                                                lds, s, g, pts, spl, at.tiles, batches + b, t.A, t.Med, warn, t.Wmin, *mc,
-                                               pc0);
+                                               pc0, nullptr);
                         else
                             hipLaunchKernelGGL((k_alpha_batch<true, true>), dim3(at.ncls[0], e - b), dim3(kTileThreads),
                                                lds, s, g, pts, spl, at.tiles, batches + b, t.A, t.Med, warn, t.Wmin, *mc,
-                                               pc0);
+                                               pc0, nullptr);
                         b = e;
                     }
                 }

@@ -1290,9 +1290,21 @@ NUSI_FN PPTerm alpha_k_pp(const Point& P, const SplineSet& spl, int k, double Em
 // points have no phi-phi channel, and the call of the out-of-line phi-phi term is compiled out (its register
 // footprint otherwise shapes the caller's allocation around the call: C4 alpha 5.58 -> 5.94 ms with the unrolled
 // spline evaluator)
-template <class Lv, bool kPhiPhi = true>
+// The terms alpha_k adds to its running sum, recorded in order instead (the k-split alpha path of calls of few
+// tables: every mass state's workgroups run at once, and k_alpha_ksum adds the terms in the same order -- the same
+// additions from the same 0.0, so the same bits)
+struct TermRec {
+    double v[7];
+    int n = 0;
+    NUSI_FN TermRec& operator+=(double x)
+    {
+        v[n++] = x;
+        return *this;
+    }
+};
+template <class Lv, bool kPhiPhi = true, class Acc = double>
 NUSI_FN void alpha_k(const Point& P, const SplineSet& spl, int k, double Em, double Ep, double Emp, double Epp,
-                     const Lv& lv, double& tot, int& warn, const AlphaPre* pre = nullptr, const PPTerm* ppt = nullptr)
+                     const Lv& lv, Acc& tot, int& warn, const AlphaPre* pre = nullptr, const PPTerm* ppt = nullptr)
 {
     const double g = P.g, mphi = P.mphi;
     const double g4 = (g * g) * (g * g), m2 = mphi * mphi, m4 = (mphi * mphi) * (mphi * mphi);
