@@ -48,6 +48,14 @@ struct LdsSink {
     double* r;   // ... the unscaled channel values
     NUSI_FN void put(int slot, double x, double raw) { v[slot * 64] = x; r[slot * 64] = raw; }
 };
+// Edge sharing (round 6): the dilogarithms Gamma and alphaTilde take of one bin edge (gamma_edge_vals,
+// alphat_edge_vals) are evaluated once per edge -- lane l of a wave holds the lower edge of bin n0 + l and hands it to
+// bin n0 + l - 1 as its upper edge (a lane shift; hi[n] == lo[n + 1] bitwise for the first N bins), so a workgroup
+// takes 63 bins and lane 63 only supplies bin n0 + 62's upper edge; a bin whose upper edge is not shared (the
+// redshift-extended bins) evaluates it itself.  The same functions on the same arguments: the same bits.
+NUSI_FN double shfl_dn(double x) { return __shfl_down(x, 1, 64); }
+NUSI_FN double shfl_upd(double x) { return __shfl_up(x, 1, 64); }
+NUSI_FN cd shfl_dn(cd z) { return cd{__shfl_down(z.r, 1, 64), __shfl_down(z.i, 1, 64)}; }
 template <bool kRef, int kParts>
 __global__ __launch_bounds__(192 * kParts) __attribute__((amdgpu_waves_per_eu(NUSI_GA_WAVES, NUSI_GA_WAVES))) void k_gamma_alphat(GridDev g, const Point* __restrict__ pts, const SplineSet* __restrict__ splp,
                                                      double* __restrict__ G, double* __restrict__ At,
@@ -59,31 +67,59 @@ __global__ __launch_bounds__(192 * kParts) __attribute__((amdgpu_waves_per_eu(NU
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), k = wv / kParts, part = wv - k * kParts;
     const int p = blockIdx.y;
-    const int n = blockIdx.x * 64 + lane;
-    const bool act = n < g.T;
+    const int n = blockIdx.x * 63 + lane, T = g.T;
+    const bool act = lane < 63 && n < T;
     const Point& P = pts[p];
     const bool gam = blockIdx.z == 0;
-    if (act) {
-        int w = 0;
-        LdsSink sk{&v[k][0][lane], &raw[kParts == 2 ? k : 0][0][lane]};
-        const double lo = g.lo[n], hi = g.hi[n];
-        if (kParts == 1) {
-            if (gam) gamma_k<kRef, -1>(P, k, lo, hi, sk, w);
-            else alphat_k<kRef, -1>(P, spl, k, lo, hi, sk, w);
-        } else if (gam) {
-            if (part == 0) gamma_k<kRef, 0>(P, k, lo, hi, sk, w);
-            else gamma_k<kRef, 1>(P, k, lo, hi, sk, w);
-        } else {
-            if (part == 0) alphat_k<kRef, 0>(P, spl, k, lo, hi, sk, w);
-            else alphat_k<kRef, 1>(P, spl, k, lo, hi, sk, w);
+    // this lane's edge: the lower edge of bin n, or (n == T) the last bin's upper edge
+    const double elo = n < T ? g.lo[n] : n == T ? g.hi[T - 1] : 0.0;
+    const double lo = act ? g.lo[n] : 0.0, hi = act ? g.hi[n] : 0.0;
+    const bool up_sh = act && (n + 1 == T || g.hi[n] == g.lo[n + 1]);   // bin n's upper edge is lane + 1's
+    int w = 0;
+    LdsSink sk{&v[k][0][lane], &raw[kParts == 2 ? k : 0][0][lane]};
+    if (gam) {
+        GammaEdgePair ge{};
+        unsigned need = 0;
+        if (act) need = kParts == 1 ? gamma_edge_need<-1>(P, k, lo, hi) : part == 0 ? gamma_edge_need<0>(P, k, lo, hi)
+                                                                                    : gamma_edge_need<1>(P, k, lo, hi);
+        const unsigned from_prev = (unsigned)__shfl_up((int)(up_sh ? need : 0u), 1, 64);
+        const unsigned need_lo = need | (lane > 0 ? from_prev : 0u);
+        gamma_edge_vals<kRef>(P, k, elo, need_lo, ge.lo);
+        ge.hi.ls = shfl_dn(ge.lo.ls);
+        ge.hi.l1s = shfl_dn(ge.lo.l1s);
+        ge.hi.cz = shfl_dn(ge.lo.cz);
+        if (!kRef) ge.hi.czc = shfl_dn(ge.lo.czc);
+        if (act && !up_sh) gamma_edge_vals<kRef>(P, k, hi, need, ge.hi);
+        if (act) {
+            if (kParts == 1) gamma_k<kRef, -1>(P, k, lo, hi, sk, w, &ge);
+            else if (part == 0) gamma_k<kRef, 0>(P, k, lo, hi, sk, w, &ge);
+            else gamma_k<kRef, 1>(P, k, lo, hi, sk, w, &ge);
         }
-        wk[wv][lane] = w;
+    } else {
+        AlphatEdgePair ae{};
+        unsigned need = 0;
+        if (act) need = kParts == 1 ? alphat_edge_need<-1>(P, k, lo, hi) : part == 0 ? alphat_edge_need<0>(P, k, lo, hi)
+                                                                                     : alphat_edge_need<1>(P, k, lo, hi);
+        const unsigned from_prev = (unsigned)__shfl_up((int)(up_sh ? need : 0u), 1, 64);
+        const unsigned need_lo = need | (lane > 0 ? from_prev : 0u);
+        alphat_edge_vals<kRef>(P, k, elo, need_lo, ae.lo);
+        ae.hi.e78 = shfl_dn(ae.lo.e78);
+        ae.hi.e51 = shfl_dn(ae.lo.e51);
+        ae.hi.e1o = shfl_dn(ae.lo.e1o);
+        ae.hi.e1p = shfl_dn(ae.lo.e1p);
+        if (act && !up_sh) alphat_edge_vals<kRef>(P, k, hi, need, ae.hi);
+        if (act) {
+            if (kParts == 1) alphat_k<kRef, -1>(P, spl, k, lo, hi, sk, w, &ae);
+            else if (part == 0) alphat_k<kRef, 0>(P, spl, k, lo, hi, sk, w, &ae);
+            else alphat_k<kRef, 1>(P, spl, k, lo, hi, sk, w, &ae);
+        }
     }
+    if (act) wk[wv][lane] = w;
     __syncthreads();
     if (wv != 0 || !act) return;
     const int ns = !P.non_resonant ? 1 : gam ? kGammaSlots : kAlphatSlots;
     SumSink tot;
-    int w = 0;
+    w = 0;
     for (int kk = 0; kk < 3; ++kk) {
         for (int i = 0; i < ns; ++i) tot.put(i, v[kk][i][lane], 0.0);
         for (int pp = 0; pp < kParts; ++pp) w |= wk[kk * kParts + pp][lane];
@@ -158,7 +194,7 @@ void k_alpha(GridDev g, const Point* __restrict__ pts, const SplineSet* __restri
 hipError_t launch_gamma_alphat(const GridDev& g, const Point* pts, int npts, const SplineSet* spl, TablesDev t,
                                int* warn, hipStream_t s, bool ref)
 {
-    dim3 grid((g.T + 63) / 64, npts, 2);
+    dim3 grid((g.T + 62) / 63, npts, 2);   // (63 bins per workgroup: the edge-shared lanes)
     if (npts <= 16) {   // (a few tables: the channels split too, kParts = 2)
         if (ref) hipLaunchKernelGGL((k_gamma_alphat<true, 2>), grid, dim3(384), 0, s, g, pts, spl, t.G, t.At, warn, t.Wmin);
         else hipLaunchKernelGGL((k_gamma_alphat<false, 2>), grid, dim3(384), 0, s, g, pts, spl, t.G, t.At, warn, t.Wmin);

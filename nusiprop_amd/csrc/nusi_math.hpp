@@ -400,4 +400,35 @@ NUSI_FN double dilog1over1mdiff(double x, double y)
     return li2_t<kRef>(1 / (1 - x)) - li2_t<kRef>(1 / (1 - y));
 }
 
+// Edge-shared forms (k_gamma_alphat, the Gamma / alphaTilde kernel): a difference f(x) - f(y) of the two edges of a
+// bin takes its branch from both arguments, and in the middle branch it evaluates f at each edge -- a function of one
+// bin edge, equal bit for bit for the two bins an edge bounds (hi[n] == lo[n + 1]).  The *_mid predicates are the
+// branch tests, the *_pre forms take the middle branch's two values from the caller (evaluated once per edge); the
+// other branches are the functions above, unchanged.
+NUSI_FN bool dilogdiff_mid(double x, double y) { return !(x > 1e2 && y > 1e2) && !(x < 1e-2 && y < 1e-2); }
+NUSI_FN bool dilog1mdiff_mid(double x, double y) { return dilogdiff_mid(x, y); }
+NUSI_FN bool dilog1pdiff_mid(double x, double y) { return !(-x > 1e2 && -y > 1e2) && !(-x < 1e-2 && -y < 1e-2); }
+NUSI_FN bool dilog1over1mdiff_mid(double x, double y) { return dilog1pdiff_mid(x, y); }
+NUSI_FN bool dilogdiff_c_mid(cd x, cd y) { return !(cabs(x) > 1e2 && cabs(y) > 1e2); }
+NUSI_FN double dilogdiff_pre(double x, double y, double lx, double ly)
+{
+    return dilogdiff_mid(x, y) ? lx - ly : dilogdiff<false>(x, y);   // (the other branches call no dilogarithm)
+}
+NUSI_FN double dilog1mdiff_pre(double x, double y, double lx, double ly)
+{
+    return dilog1mdiff_mid(x, y) ? lx - ly : dilog1mdiff<false>(x, y);
+}
+NUSI_FN double dilog1pdiff_pre(double x, double y, double lx, double ly)
+{
+    return dilog1pdiff_mid(x, y) ? lx - ly : dilog1pdiff<false>(x, y);
+}
+NUSI_FN double dilog1over1mdiff_pre(double x, double y, double lx, double ly)
+{
+    return dilog1over1mdiff_mid(x, y) ? lx - ly : dilog1over1mdiff<false>(x, y);
+}
+NUSI_FN cd dilogdiff_c_pre(cd x, cd y, cd a, cd b)
+{
+    return dilogdiff_c_mid(x, y) ? C(a.r - b.r, a.i - b.i) : dilogdiff_c<false>(x, y);
+}
+
 }  // namespace nusi

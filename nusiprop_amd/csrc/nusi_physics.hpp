@@ -204,8 +204,42 @@ NUSI_FN int alphat_warn(double as, double at, double au, double atu, double ast,
     return (as < 0 || at < 0 || au < 0 || atu / nrm < -1e-11 || (ast + at + as) / nrm < -1e-11 || (asu + au + as) / nrm < -1e-11)
                ? kWarnAlphaTilde : 0;
 }
+// Gamma's dilogarithms of one bin edge (E, s = 2 m_j E / m_phi^2): li2(-s), li2(-1 - s) and Li2 of
+// z = i (1 + s) / (gr + 2 i) (and, in the shared-algorithm order, of conj z) -- the edge-shared path of
+// k_gamma_alphat evaluates them once per edge for the two bins it bounds (the *_pre forms, nusi_math.hpp)
+struct GammaEdgeVals { double ls, l1s; cd cz, czc; };
+struct GammaEdgePair { GammaEdgeVals lo, hi; };
+constexpr unsigned kGeLs = 1, kGeL1s = 2, kGeCz = 4;
+template <bool kRef>
+NUSI_FN void gamma_edge_vals(const Point& P, int j, double E, unsigned need, GammaEdgeVals& v)
+{
+    const double mphi = P.mphi, Ga = P.Ga, m2 = mphi * mphi, gr = Ga / mphi;
+    const double s = 2 * P.mn[j] * E / m2;   // gamma_k's sp / sm
+    if (need & kGeLs) v.ls = li2_t<kRef>(-s);
+    if (need & kGeL1s) v.l1s = li2_t<kRef>(-1 - s);
+    if (need & kGeCz) {
+        const cd z = C(0.0, 1 + s) / C(gr, 2.0);
+        v.cz = cli2_t<kRef>(z);
+        if (!kRef) v.czc = cli2_t<kRef>(conj(z));
+    }
+}
+// the edge values gamma_k<kRef, kPart> reads for bin (Em, Ep): the middle branches of its differences
+template <int kPart>
+NUSI_FN unsigned gamma_edge_need(const Point& P, int j, double Em, double Ep)
+{
+    if (!P.non_resonant) return 0;
+    const double mphi = P.mphi, Ga = P.Ga, m2 = mphi * mphi, gr = Ga / mphi, mj = P.mn[j];
+    const double sp = 2 * mj * Ep / m2, sm = 2 * mj * Em / m2;
+    unsigned m = dilogdiff_mid(sp, sm) ? kGeLs : 0u;   // Gint and Gst
+    if (kPart != 1 && dilog1mdiff_mid(sp, sm)) m |= kGeL1s;
+    if (kPart != 0 && !(sp < 1e-5)) {
+        const cd den = C(gr, 2.0);
+        if (dilogdiff_c_mid(C(0.0, 1 + sp) / den, C(0.0, 1 + sm) / den)) m |= kGeCz;
+    }
+    return m;
+}
 template <bool kRef, int kPart, class Sink>   // kRef: NUSI_OPT_REFERENCE_ORDER (GSL's dilogarithms, nusi_gsl.hpp)
-NUSI_FN void gamma_k(const Point& P, int j, double Em, double Ep, Sink& tot, int& warn)
+NUSI_FN void gamma_k(const Point& P, int j, double Em, double Ep, Sink& tot, int& warn, const GammaEdgePair* ge = nullptr)
 {
     const double g = P.g, mphi = P.mphi, Ga = P.Ga;
     const double g4 = (g * g) * (g * g), m2 = mphi * mphi;
@@ -237,7 +271,8 @@ NUSI_FN void gamma_k(const Point& P, int j, double Em, double Ep, Sink& tot, int
 
             Gint = g4 / (32 * kPi * m2 * sm * sp) *
                    (sm * L1p * (2 + 2 * sp + sp * nm::log(2 + sp)) - sp * L1m * (2 + 2 * sm + sm * nm::log(2 + sm))
-                    + sm * sp * (dilog1mdiff<kRef>(sp, sm) + dilogdiff<kRef>(sp, sm)));
+                    + sm * sp * (ge ? dilog1mdiff_pre(sp, sm, ge->hi.l1s, ge->lo.l1s) + dilogdiff_pre(sp, sm, ge->hi.ls, ge->lo.ls)
+                                    : dilog1mdiff<kRef>(sp, sm) + dilogdiff<kRef>(sp, sm)));
             if (Gint < 0) Gint = g4 / (16 * kPi * m2) * (sp - sm) / 2. * gl3_Gtu_int(sm, sp);
             Gint *= P.majorana ? uj : 0.5 * uj;
             tot.put(2, wgt * Gint, Gint);
@@ -253,17 +288,18 @@ NUSI_FN void gamma_k(const Point& P, int j, double Em, double Ep, Sink& tot, int
             d1 = (sm * sm) * (C(-0.0, -0.5) / C(gr, 1.0) - l1 / 2.) + sm * l1 - sp * l1 + ((sp * sp) * (kI / C(gr, 1.0) + l1)) / 2.;
             d2 = (sm * sm) * (C(0.0, 0.5) / C(gr, -1.0) - l2 / 2.) + sm * l2 - sp * l2 + ((sp * sp) * (C(-0.0, -1.0) / C(gr, -1.0) + l2)) / 2.;
         } else {
-            d1 = dilogdiff_c<kRef>(z1p, z1m);
+            d1 = ge ? dilogdiff_c_pre(z1p, z1m, ge->hi.cz, ge->lo.cz) : dilogdiff_c<kRef>(z1p, z1m);
             // (kRef) GSL's complex dilogarithm is odd in y operation by operation (every y-dependent quantity is
             // negated exactly, atan2 and Clausen are odd, the series' rotation and sums negate, the modulus terms do
             // not change), and so is li2_asym: Li2(conj z) = conj Li2(z) bit for bit, and d2 = conj(d1) is the
             // reference's own value at half the cost (the tables stay bit-identical to the oracle, which calls both)
-            d2 = kRef ? conj(d1) : dilogdiff_c<kRef>(z2p, z2m);
+            d2 = kRef ? conj(d1) : ge ? dilogdiff_c_pre(z2p, z2m, ge->hi.czc, ge->lo.czc) : dilogdiff_c<kRef>(z2p, z2m);
         }
         const double Lgp = nm::log1p(((-1 + sp) * (-1 + sp)) / gr2), Lgm = nm::log1p(((-1 + sm) * (-1 + sm)) / gr2);
         Gst = -g4 / (32 * kPi * m2 * (1 + gr2)) *
               (d1.r + d2.r + gr * (d2.i - d1.i) + 2 * gr * carg(1.0 - z2p) * L1p - 2 * gr * carg(1.0 - z2m) * L1m
-               + nm::log1p(4 / gr2) * (L1m - L1p) + Lgp * L1p - Lgm * L1m + (1 + gr2) * (Lgm - Lgp) + 2 * dilogdiff<kRef>(sp, sm));
+               + nm::log1p(4 / gr2) * (L1m - L1p) + Lgp * L1p - Lgm * L1m + (1 + gr2) * (Lgm - Lgp)
+               + 2 * (ge ? dilogdiff_pre(sp, sm, ge->hi.ls, ge->lo.ls) : dilogdiff<kRef>(sp, sm)));
         Gst *= uj;
         tot.put(3, wgt * Gst, Gst);
         Gsu = P.majorana ? Gst : 0;
@@ -296,8 +332,48 @@ NUSI_FN double gamma_entry(const Point& P, double Em, double Ep, int& warn)
 // ---------------------------------------------------------------------------
 // alphaTilde(Em, Ep)  -- nuSIprop.hpp:924-1235
 // ---------------------------------------------------------------------------
+// alphaTilde's dilogarithms of one bin edge (t = -2 m_k E / m_phi^2 with alphat_k's |t + 1| < 1e-7 nudge): Li2 of
+// 1 - t (real axis) and of i (1 - t) / (gr + 2 i), li2(1 / (1 - t)) and li2(1 + t) (k_gamma_alphat's edge-shared path)
+struct AlphatEdgeVals { cd e78, e51; double e1o, e1p; };
+struct AlphatEdgePair { AlphatEdgeVals lo, hi; };
+constexpr unsigned kAe78 = 1, kAe51 = 2, kAe1o = 4, kAe1p = 8;
+NUSI_FN double alphat_t(double mk, double E, double m2)
+{
+    double t = -2 * mk * E / m2;
+    if (fabs(t + 1) < 1e-7) t += t * 1e-6;
+    return t;
+}
+template <bool kRef>
+NUSI_FN void alphat_edge_vals(const Point& P, int k, double E, unsigned need, AlphatEdgeVals& v)
+{
+    const double mphi = P.mphi, Ga = P.Ga, m2 = mphi * mphi, gr = Ga / mphi;
+    const double t = alphat_t(P.mn[k], E, m2);
+    if (need & kAe78) v.e78 = cli2_t<kRef>(C(1 - t));
+    if (need & kAe51) v.e51 = cli2_t<kRef>(C(0.0, 1 - t) / C(gr, 2.0));
+    if (need & kAe1o) v.e1o = li2_t<kRef>(1 / (1 - t));
+    if (need & kAe1p) v.e1p = li2_t<kRef>(1 + t);
+}
+template <int kPart>
+NUSI_FN unsigned alphat_edge_need(const Point& P, int k, double Em, double Ep)
+{
+    if (!P.non_resonant) return 0;
+    const double mphi = P.mphi, Ga = P.Ga, m2 = mphi * mphi, gr = Ga / mphi;
+    const double tp = alphat_t(P.mn[k], Ep, m2), tm = alphat_t(P.mn[k], Em, m2);
+    unsigned m = 0;
+    if (kPart != 1 && P.majorana) {
+        if (dilog1over1mdiff_mid(tp, tm)) m |= kAe1o;
+        if (dilog1pdiff_mid(tm, tp)) m |= kAe1p;
+    }
+    if (kPart != 0 && !(-tp < 1e-5)) {
+        const cd den = C(gr, 2.0);
+        if (dilogdiff_c_mid(C(1 - tm), C(1 - tp))) m |= kAe78;
+        if (dilogdiff_c_mid(C(0.0, 1 - tp) / den, C(0.0, 1 - tm) / den)) m |= kAe51;
+    }
+    return m;
+}
 template <bool kRef, int kPart, class Sink>   // kRef: NUSI_OPT_REFERENCE_ORDER (GSL's dilogarithms, nusi_gsl.hpp)
-NUSI_FN void alphat_k(const Point& P, const SplineSet& spl, int k, double Em, double Ep, Sink& tot, int& warn)
+NUSI_FN void alphat_k(const Point& P, const SplineSet& spl, int k, double Em, double Ep, Sink& tot, int& warn,
+                      const AlphatEdgePair* ae = nullptr)
 {
     const double g = P.g, mphi = P.mphi, Ga = P.Ga;
     const double g4 = (g * g) * (g * g), m2 = mphi * mphi, m4 = (mphi * mphi) * (mphi * mphi);
@@ -370,8 +446,9 @@ NUSI_FN void alphat_k(const Point& P, const SplineSet& spl, int k, double Em, do
             atu = g4 / (32 * kPi * m4 * (1 + tm) * tp) *
                   (2 * (2 * (1 + tm) * (tm - tp) - 2 * (1 + tm) * tp * nm::atanh(1 / (1 - tp)) * nm::atanh((tm - tp) / (-2 + tm + tp))
                         + tm * tp * (-Lmt + Lmp) + (1 + tm) * (Lmt - Lmp - Ld) + tp * (-Lmt + Lmp + Ld) - tm * tp * nm::log(tm / tp))
-                   + (1 + tm) * tp * ((-(Lmt * Lmt) + Lmp * Lmp) / 2. + dilog1over1mdiff<kRef>(tp, tm))
-                   - (1 + tm) * tp * (dilog1pdiff<kRef>(tm, tp) + combi));
+                   + (1 + tm) * tp * ((-(Lmt * Lmt) + Lmp * Lmp) / 2.
+                                      + (ae ? dilog1over1mdiff_pre(tp, tm, ae->hi.e1o, ae->lo.e1o) : dilog1over1mdiff<kRef>(tp, tm)))
+                   - (1 + tm) * tp * ((ae ? dilog1pdiff_pre(tm, tp, ae->lo.e1p, ae->hi.e1p) : dilog1pdiff<kRef>(tm, tp)) + combi));
             if (atu < 0) atu = gl33_tri(2, tp, tm) * (g4 / (16 * kPi * m4));
         }
         atu *= uk;
@@ -399,8 +476,8 @@ NUSI_FN void alphat_k(const Point& P, const SplineSet& spl, int k, double Em, do
             const cd z4 = (1 + tm - tp) / dt_m;
             const cd z5 = C(0.0, 1 - tp) / den;
             const double z6 = 1 - tp / (1 + tm);
-            d78 = dilogdiff_c<kRef>(C(1 - tm), C(1 - tp));
-            d51 = dilogdiff_c<kRef>(z5, z1);
+            d78 = ae ? dilogdiff_c_pre(C(1 - tm), C(1 - tp), ae->lo.e78, ae->hi.e78) : dilogdiff_c<kRef>(C(1 - tm), C(1 - tp));
+            d51 = ae ? dilogdiff_c_pre(z5, z1, ae->hi.e51, ae->lo.e51) : dilogdiff_c<kRef>(z5, z1);
             d26 = dilogdiff_c<kRef>(C(z2), C(z6));
             d43 = dilogdiff_c<kRef>(z4, z3);
         }

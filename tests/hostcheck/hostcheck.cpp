@@ -53,6 +53,67 @@ int hc_tables_ref(const double* pt, const int* flags, int T, const double* lo, c
 
 }  // extern "C"
 
+// Host emulation of k_gamma_alphat's edge-shared path (round 6): every bin's edge dilogarithms by gamma_edge_vals /
+// alphat_edge_vals at the bin's own lower and upper edge (the kernel takes the upper edge's from the next lane, which
+// evaluates the same function at the same bits), the channels through gamma_k / alphat_k with the pair, summed as the
+// kernel's wave 0 sums them.  parts = 1: one pass per mass state (scans); 2: the two channel parts (few tables).
+struct SlotSink {
+    double* v;
+    NUSI_FN void put(int slot, double x, double) { v[slot] = x; }
+};
+template <bool kRef>
+static int ga_shared_t(const double* pt, const int* flags, int T, const double* lo, const double* hi, int parts,
+                       double* G, double* At)
+{
+    using namespace nusi;
+    const Point P = mk(pt, flags);
+    SplineSet spl{};
+    int warn = 0;
+    for (int n = 0; n < T; ++n) {
+        double g = 0.0, a = 0.0;
+        for (int k = 0; k < 3; ++k) {
+            double vg[kAlphatSlots] = {}, va[kAlphatSlots] = {};
+            SlotSink sg{vg}, sa{va};
+            for (int part = (parts == 1 ? -1 : 0); part < (parts == 1 ? 0 : 2); ++part) {
+                const unsigned ng = part < 0 ? gamma_edge_need<-1>(P, k, lo[n], hi[n])
+                                    : part == 0 ? gamma_edge_need<0>(P, k, lo[n], hi[n]) : gamma_edge_need<1>(P, k, lo[n], hi[n]);
+                const unsigned na = part < 0 ? alphat_edge_need<-1>(P, k, lo[n], hi[n])
+                                    : part == 0 ? alphat_edge_need<0>(P, k, lo[n], hi[n]) : alphat_edge_need<1>(P, k, lo[n], hi[n]);
+                GammaEdgePair ge{};
+                AlphatEdgePair ae{};
+                gamma_edge_vals<kRef>(P, k, lo[n], ng, ge.lo);
+                gamma_edge_vals<kRef>(P, k, hi[n], ng, ge.hi);
+                alphat_edge_vals<kRef>(P, k, lo[n], na, ae.lo);
+                alphat_edge_vals<kRef>(P, k, hi[n], na, ae.hi);
+                if (part < 0) {
+                    gamma_k<kRef, -1>(P, k, lo[n], hi[n], sg, warn, &ge);
+                    alphat_k<kRef, -1>(P, spl, k, lo[n], hi[n], sa, warn, &ae);
+                } else if (part == 0) {
+                    gamma_k<kRef, 0>(P, k, lo[n], hi[n], sg, warn, &ge);
+                    alphat_k<kRef, 0>(P, spl, k, lo[n], hi[n], sa, warn, &ae);
+                } else {
+                    gamma_k<kRef, 1>(P, k, lo[n], hi[n], sg, warn, &ge);
+                    alphat_k<kRef, 1>(P, spl, k, lo[n], hi[n], sa, warn, &ae);
+                }
+            }
+            const int ng = !P.non_resonant ? 1 : kGammaSlots, na = !P.non_resonant ? 1 : kAlphatSlots;
+            for (int i = 0; i < ng; ++i) g += vg[i];
+            for (int i = 0; i < na; ++i) a += va[i];
+        }
+        G[n] = g;
+        At[n] = a;
+    }
+    return warn;
+}
+
+extern "C" {
+int hc_ga_shared(const double* pt, const int* flags, int T, const double* lo, const double* hi, int parts, int ref,
+                 double* G, double* At)
+{
+    return ref ? ga_shared_t<true>(pt, flags, T, lo, hi, parts, G, At) : ga_shared_t<false>(pt, flags, T, lo, hi, parts, G, At);
+}
+}  // extern "C"
+
 // Host emulation of k_alpha_tile: the same edge lists, job helpers and TileLeaves combine, one
 // tile at a time (work-items run sequentially, phases in kernel order).  alpha dense T*T, m > n.
 template <bool kRef>

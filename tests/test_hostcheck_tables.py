@@ -122,3 +122,26 @@ def test_reference_order_tables_bit_identical(oracle_mod, name):
         if kw["majorana"]:
             _, _, al0 = o.tables()
             assert np.any(al0[iu] != al[iu])
+
+
+@pytest.mark.parametrize("parts", [1, 2])
+@pytest.mark.parametrize("ref", [0, 1])
+@pytest.mark.parametrize("name", sorted(cases.SMALL_CASES))
+def test_edge_shared_gamma_alphat_bit_identical(oracle_mod, name, ref, parts):
+    """k_gamma_alphat's edge-shared path (round 6: each bin edge's dilogarithms evaluated once and handed to the
+    neighbouring bin; gamma_edge_vals / alphat_edge_vals + the *_pre differences), emulated on the host in both
+    channel splits, against the oracle in both arithmetics: Gamma and alphaTilde bit for bit."""
+    from tests.hostcheck import build_hostcheck
+    H = build_hostcheck()
+    kw = dict(cases.SMALL_CASES[name], N_bins_E=40)
+    o = oracle_mod.Oracle(**cases.oracle_kwargs(kw))
+    with oracle_mod.reference_order(ref):
+        G, aT, _ = o.tables()
+    lo, hi = extended_axis(o)
+    pt, flags = point_array(o, kw)
+    T = o.T
+    Gh, aTh = np.zeros(T), np.zeros(T)
+    H.hc_ga_shared.restype = ctypes.c_int
+    H.hc_ga_shared(_dp(pt), flags, T, _dp(lo), _dp(hi), parts, ref, _dp(Gh), _dp(aTh))
+    assert np.array_equal(Gh, G), "Gamma differs at %s" % np.flatnonzero(Gh != G)[:5]
+    assert np.array_equal(aTh, aT), "alphaTilde differs at %s" % np.flatnonzero(aTh != aT)[:5]
