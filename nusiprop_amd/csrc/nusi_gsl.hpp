@@ -359,6 +359,13 @@ NUSI_FN void cseries_t(bool s2, double r, double lr, double x, double y, double&
     auto stop = [&]() { return quot_lt<kExact>(dr * dr + di * di, real_sum * real_sum + imag_sum * imag_sum, 0x1p-104); };
     int k = 2;
     bool done = false;
+#ifdef NUSI_GSL_STUB_SERIES   // timing A/B only (wrong values): the complex series without its terms
+    if (k < kmax) {
+        re = real_sum;
+        im = imag_sum;
+        return;
+    }
+#endif
     if (!kExact) {
         // the first loop leaves together (wave votes), so k stays wave-uniform and the table rows scalar loads: at the
         // first k where a lane reaches its kmax (no term k), or where a lane's term falls below its bound (term k

@@ -13,6 +13,7 @@
 #   vbench=<v>,<a>,..       bench.py <a> .. on the A/B library build/variants/libnusi_<v>.so (scripts/build_variant.sh)
 #   vpy=<v>,<script>,<a>,.. python <script> <a> .. on that library                   -> vpy_<i>.out / .err
 #   vprof=<v>,<a>,..        prof= of bench.py <a> .. on that library                  -> vkt_<i>_<v>/
+#   vpmc=<v>,<workload>     SQ instruction / busy counters of bench.py on library v (base = libnusi.so) -> vpmc_<i>_<v>/
 set -o pipefail
 TAG=${1:?tag}
 shift
@@ -53,6 +54,13 @@ for STEP in "$@"; do
       V=${ARGS%% *}; A=${ARGS#* }; [ "$A" = "$ARGS" ] && A=""
       NUSIPROP_LIB=$PWD/build/variants/libnusi_$V.so timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/vkt_${i}_$V \
         -o kt --output-format csv -- python3 bench.py $A > $OUT/vkt_${i}_$V.log 2>&1 || exit 1 ;;
+    vpmc)   # vpmc=<v>,<workload>: SQ instruction counters of the A/B library's kernels (v = base: libnusi.so)
+      V=${ARGS%% *}; W=${ARGS#* }
+      L=$PWD/build/variants/libnusi_$V.so; [ "$V" = base ] && L=$PWD/nusiprop_amd/libnusi.so
+      NUSIPROP_LIB=$L timeout -s KILL 300 rocprofv3 --kernel-trace --output-format csv -d $OUT/vpmc_${i}_$V \
+        --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES SQ_WAVES SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 \
+        -o pmc -- python3 bench.py --workload $W --steps 3 --warmup 1 --no-cpu-baseline --no-secondary --no-parity \
+        > $OUT/vpmc_${i}_$V.log 2>&1 || exit 1 ;;
     vpy)
       V=${ARGS%% *}; A=${ARGS#* }
       NUSIPROP_LIB=$PWD/build/variants/libnusi_$V.so timeout -k 10 600 python $A > $OUT/vpy_${i}_$V.out \
