@@ -457,7 +457,7 @@ NUSI_FN void cseries_3(double r, double lr, double x, double y, double& re, doub
 // dilogc_fundamental (r < 1, x <= 0.732): series_3 above r = 0.98, dilogc_series_2 above 0.25, else series_1.  Every
 // branch takes log(r) (series_3's expansion variable, the series' kmax): formed once, and returned in lr for
 // unitdisk's log(1 - z) of a reflected argument (the same call on the same value)
-NUSI_FN_OUT cd fundamental(double r, double x, double y, double& lr)
+NUSI_FN cd fundamental_body(double r, double x, double y, double& lr)
 {
     double re, im;
     lr = GSL_LOG(r);
@@ -480,7 +480,10 @@ NUSI_FN_OUT cd fundamental(double r, double x, double y, double& lr)
     const double r_y = (1.0 - x) * t_y - y * t_x;
     return cd{re + r_x + 1.0, im + r_y};
 }
-// dilogc_unitdisk: |z| < 1; x > 0.732 reflected, Li2(z) = -Li2(1 - z) + zeta2 - log(z) log(1 - z)
+NUSI_FN_OUT cd fundamental(double r, double x, double y, double& lr) { return fundamental_body(r, x, y, lr); }
+// dilogc_unitdisk: |z| < 1; x > 0.732 reflected, Li2(z) = -Li2(1 - z) + zeta2 - log(z) log(1 - z).  kInl: fundamental
+// inline (the member-corner kernel's single call site, gsl_cli2_inl), else the out-of-line instance
+template <bool kInl = false>
 NUSI_FN cd unitdisk(double x, double y)
 {
     const double zeta2 = kPiD * kPiD / 6.0;
@@ -491,7 +494,7 @@ NUSI_FN cd unitdisk(double x, double y)
     const double fx = refl ? x_tmp : x, fy = refl ? y_tmp : y;
     const double rf = gsl::hypot(fx, fy);
     double lr;
-    const cd f = fundamental(rf, fx, fy, lr);   // one call site
+    const cd f = kInl ? fundamental_body(rf, fx, fy, lr) : fundamental(rf, fx, fy, lr);   // one call site
     if (!refl) return f;
     const double r = gsl::hypot(x, y);
     const double lnz = GSL_LOG(r), lnomz = lr;   // log(r_tmp)
@@ -530,8 +533,12 @@ NUSI_FN_OUT double gsl_li2(double x)
 NUSI_FN cd gsl_cli2_real(double x) { return cd{gsl_li2(x), (x >= 1.0) ? -gsl::kPiD * GSL_LOG(x) : 0.0}; }
 
 // gsl_sf_complex_dilog_xy_e: the real axis; |z| within eps of 1 (Lewin A.2.4.1 / A.2.4.2); the unit disk; 1/z
-// into the unit disk, unwound with Li2(z) + Li2(1/z) = -zeta2 - log(-z)^2 / 2
-NUSI_FN_OUT cd gsl_cli2(double x, double y)
+// into the unit disk, unwound with Li2(z) + Li2(1/z) = -zeta2 - log(-z)^2 / 2.  gsl_cli2_t<true> (gsl_cli2_inl) is the
+// whole call inline -- the member-corner kernel's one call site, where the call boundaries' argument moves, SGPR
+// lane spills and callee-saved register traffic were VALU work of their own; gsl_cli2 the out-of-line instance the
+// table kernels call from many sites
+template <bool kInl>
+NUSI_FN cd gsl_cli2_t(double x, double y)
 {
     const double zeta2 = gsl::kPiD * gsl::kPiD / 6.0;
     const double r2 = x * x + y * y;
@@ -542,7 +549,7 @@ NUSI_FN_OUT cd gsl_cli2(double x, double y)
         return cd{zeta2 + term1 - term2, gsl::clausen(theta)};
     }
     const bool inv = !(r2 < 1.0);
-    const cd u = gsl::unitdisk(inv ? x / r2 : x, inv ? -y / r2 : y);   // one instance
+    const cd u = gsl::unitdisk<kInl>(inv ? x / r2 : x, inv ? -y / r2 : y);   // one instance
     if (!inv) return u;
     const double r = sqrt(r2);
     const double theta = GSL_ATAN2(y, x), theta_abs = fabs(theta), theta_sgn = (theta < 0.0 ? -1.0 : 1.0);
@@ -551,5 +558,12 @@ NUSI_FN_OUT cd gsl_cli2(double x, double y)
     const double lmz2_im = 2.0 * ln_minusz_re * ln_minusz_im;
     return cd{-u.r - 0.5 * lmz2_re - zeta2, -u.i - 0.5 * lmz2_im};
 }
+
+NUSI_FN_OUT cd gsl_cli2(double x, double y) { return gsl_cli2_t<false>(x, y); }
+#ifndef NUSI_MC_CALL   // (A/B: the member-corner kernel's GSL call out of line, as before round 6)
+NUSI_FN cd gsl_cli2_inl(double x, double y) { return gsl_cli2_t<true>(x, y); }
+#else
+NUSI_FN cd gsl_cli2_inl(double x, double y) { return gsl_cli2(x, y); }
+#endif
 
 }  // namespace nusi

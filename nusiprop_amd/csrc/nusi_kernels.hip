@@ -501,7 +501,7 @@ void k_alpha_mcorner(const Point* __restrict__ pts, const int* __restrict__ batc
         const int cl = j / nb, q = j - cl * nb;
         if (c0 + cl >= mc.NC) break;
         const double S = cst[0][cl], t = cst[1][cl], gr = pts[p0 + q].a_gr;
-        const cd Dc = NUSI_REFO_STUB == 2 ? C(0.0) : alpha_member_ref_dc(S, t, gr);
+        const cd Dc = NUSI_REFO_STUB == 2 ? C(0.0) : alpha_member_ref_dc_inl(S, t, gr);
         v[2 * (q * cb + cl)] = Dc.r;
         v[2 * (q * cb + cl) + 1] = Dc.i;
     }

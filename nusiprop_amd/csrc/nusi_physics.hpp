@@ -671,6 +671,12 @@ NUSI_FN cd alpha_member_ref_dc(double S, double t, double gr)
     const cd z = (1 + S + t) / C(2 + t, -gr);
     return NUSI_REFO_STUB == 1 ? z : gsl_cli2(z.r, z.i);
 }
+// the same, with GSL's call inline (k_alpha_mcorner's single call site)
+NUSI_FN cd alpha_member_ref_dc_inl(double S, double t, double gr)
+{
+    const cd z = (1 + S + t) / C(2 + t, -gr);
+    return NUSI_REFO_STUB == 1 ? z : gsl_cli2_inl(z.r, z.i);
+}
 NUSI_FN double alpha_member_ref_arg(double S, double t, double gr)
 {
     return carg_i(-(C(-1 + S, gr) / C(2 + t, -gr)));   // (atan2 inline)
