@@ -113,6 +113,17 @@ NUSI_FN double hypot(double x, double y)
 {
     double a = fabs(x), b = fabs(y);
     if (a < b) { const double t = a; a = b; b = t; }
+#ifdef __HIP_DEVICE_COMPILE__
+    // the common case (2^-500 <= b <= a <= 2^500) voted once per wave: the same operations without the scaling
+    // branches, whose exec masks stayed live in SGPRs
+    if (__all(b >= 0x1p-500 && a <= 0x1p+500)) {
+        const double a2 = a * a, ea = fma(a, a, -a2), b2 = b * b, eb = fma(b, b, -b2);
+        double h = sqrt(a2 + b2);
+        const double h2 = h * h, eh = fma(h, h, -h2);
+        const double r = ((a2 - h2) + b2) + ((ea + eb) - eh);
+        return h + r / (2.0 * h);
+    }
+#endif
     if (b == 0.0 || !(a <= 1.79769313486231570815e+308)) return a + b;
     double s = 1.0;
     if (a > 0x1p+500) { a *= 0x1p-600; b *= 0x1p-600; s = 0x1p+600; }

@@ -211,7 +211,7 @@ NUSI_FN double atan_i(double x)
 }
 
 // e_atan2.c
-NUSI_FN double atan2_i(double y, double x)
+NUSI_FN double atan2_full(double y, double x)
 {
     constexpr double pi_o_2 = 1.5707963267948965580E+00, pi = 3.1415926535897931160E+00,
                      pi_lo = 1.2246467991473531772E-16, pi_o_4 = 7.8539816339744827900E-01;
@@ -259,6 +259,64 @@ NUSI_FN double atan2_i(double y, double x)
     case 2: return pi - (z - pi_lo);
     default: return (z - pi_lo) - pi;
     }
+}
+
+// atan2 without fdlibm's special-case branches, for the common case: y and x finite and nonzero, x != 1.0 and
+// |k| <= 60 (k = (iy - ix) >> 20, the exponent difference).  There e_atan2.c computes z = atan(|y / x|) and fixes the
+// octant, and s_atan.c reduces |y / x| by range; here the range's numerator and denominator, the table constants and
+// the octant are selected instead of branched on (range -1 divides by 1.0, exactly), the same operations on the same
+// operands, so the same bits.  Every branch of the full version kept an exec mask live in SGPRs -- inside GSL's complex
+// dilogarithm that spilled SGPRs into VGPR lanes -- and the wave votes for this path once (a wave with any other
+// argument takes atan2_full; tests/test_specfun.py compares the two bit for bit).
+NUSI_FN bool atan2_plain(double y, double x)
+{
+    const int hx = hiw(x), hy = hiw(y);
+    const int ix = hx & 0x7fffffff, iy = hy & 0x7fffffff;
+    const int k = (iy - ix) >> 20;
+    return ix < 0x7ff00000 && iy < 0x7ff00000 && ((unsigned)ix | low(x)) != 0u && ((unsigned)iy | low(y)) != 0u &&
+           !(hx == 0x3ff00000 && low(x) == 0u) && k <= 60 && k >= -60;
+}
+NUSI_FN double atan2_sel(double y, double x)
+{
+    constexpr double pi = 3.1415926535897931160E+00, pi_lo = 1.2246467991473531772E-16;
+    constexpr double aT[11] = {3.33333333333329318027e-01,  -1.99999999998764832476e-01, 1.42857142725034663711e-01,
+                               -1.11111104054623557880e-01, 9.09088713343650656196e-02,  -7.69187620504482999495e-02,
+                               6.66107313738753120669e-02,  -5.83357013379057348645e-02, 4.97687799461593236017e-02,
+                               -3.65315727442169155270e-02, 1.62858201153657823623e-02};
+    const double t = fabs(y / x);   // s_atan.c's argument, >= 0 and finite here
+    const int it = hiw(t);
+    const bool r_1 = it < 0x3fdc0000, r0 = it < 0x3fe60000, r1 = it < 0x3ff30000, r2 = it < 0x40038000;
+    const double num = r_1 ? t : r0 ? 2.0 * t - 1.0 : r1 ? t - 1.0 : r2 ? t - 1.5 : -1.0;
+    const double den = r_1 ? 1.0 : r0 ? 2.0 + t : r1 ? t + 1.0 : r2 ? 1.0 + 1.5 * t : t;
+    const double xr = num / den;
+    const double z = xr * xr;
+    const double w = z * z;
+    const double s1 = z * (aT[0] + w * (aT[2] + w * (aT[4] + w * (aT[6] + w * (aT[8] + w * aT[10])))));
+    const double s2 = w * (aT[1] + w * (aT[3] + w * (aT[5] + w * (aT[7] + w * aT[9]))));
+    const double ahi = r0 ? 4.63647609000806093515e-01 : r1 ? 7.85398163397448278999e-01
+                     : r2 ? 9.82793723247329054082e-01 : 1.57079632679489655800e+00;
+    const double alo = r0 ? 2.26987774529616870924e-17 : r1 ? 3.06161699786838301793e-17
+                     : r2 ? 1.39033110312309984516e-17 : 6.12323399573676603587e-17;
+    double at = r_1 ? xr - xr * (s1 + s2) : ahi - ((xr * (s1 + s2) - alo) - xr);
+    if (it < 0x3e200000) at = t;   // |t| < 2^-29 (a select)
+    const int m = ((hiw(y) >> 31) & 1) | ((hiw(x) >> 30) & 2);   // 2 sign(x) + sign(y)
+    const double zz = at - pi_lo;
+    return m == 0 ? at : m == 1 ? -at : m == 2 ? pi - zz : zz - pi;
+}
+NUSI_FN bool wave_all_l(bool p)
+{
+#ifdef __HIP_DEVICE_COMPILE__
+    return __all(p);
+#else
+    return p;
+#endif
+}
+NUSI_FN double atan2_i(double y, double x)
+{
+#ifndef NUSI_ATAN2_FULL   // (A/B: fdlibm's branches only)
+    if (wave_all_l(atan2_plain(y, x))) return atan2_sel(y, x);
+#endif
+    return atan2_full(y, x);
 }
 
 // Out-of-line entry points (see NUSI_LM); the *_i bodies above are inlined where a caller wants

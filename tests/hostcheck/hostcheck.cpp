@@ -190,6 +190,9 @@ double hc_gsl_li2(double x) { return nusi::gsl_li2(x); }
 void hc_gsl_cli2(double x, double y, double* re, double* im) { const nusi::cd r = nusi::gsl_cli2(x, y); *re = r.r; *im = r.i; }
 double hc_gsl_clausen(double x) { return nusi::gsl::clausen(x); }
 double hc_hypot(double x, double y) { return nusi::gsl::hypot(x, y); }
+// the libm atan2 the device runs (nusi_libm.hpp: the select-based common path, else fdlibm's branches)
+double hc_atan2(double y, double x) { return nusi::nm::atan2_i(y, x); }
+double hc_atan2_full(double y, double x) { return nusi::nm::atan2_full(y, x); }
 // the series' per-k table row (d1, d2, y1, y2, l1, l2) and its division, for the two-part-reciprocal test
 void hc_gsl_krow(int k, double* o)
 {

@@ -250,3 +250,36 @@ def test_gsl_series_division_two_part_reciprocal(hlib):
             for _ in range(40):
                 a = rng.uniform(0.5, 1.0) * 2.0 ** rng.randint(-470, 0)
                 assert hlib.hc_gsl_div_k(a, d, y, l) == a / d, (k, d, a)
+
+
+def test_device_atan2_select_path_bit_identical(olib, hlib):
+    """nusi_libm.hpp's atan2 (round 6: the common case -- finite nonzero arguments, x != 1, exponent difference
+    within 60 -- by selects instead of fdlibm's branches; every other argument through fdlibm's full code) against the
+    oracle's fdlibm e_atan2.c (ora_libm.c), bit for bit: seeded arguments over 40 decades and both signs, every
+    s_atan.c range boundary, the octants, and the special values (zeros, infinities, NaN, x = 1, extreme ratios)."""
+    import numpy as np
+    H = hlib
+    for f in ("hc_atan2", "hc_atan2_full"):
+        getattr(H, f).restype = D
+        getattr(H, f).argtypes = [D, D]
+    rng = np.random.default_rng(20250213)
+    n = 200000
+    mag = 10.0 ** rng.uniform(-20, 20, size=(n, 2))
+    sgn = rng.choice([-1.0, 1.0], size=(n, 2))
+    args = list(map(tuple, mag * sgn))
+    # the reduction's range edges |y/x| = 7/16, 11/16, 19/16, 39/16, 2^-29, 2^66 (and neighbours), all octants
+    edges = [7 / 16, 11 / 16, 19 / 16, 39 / 16, 2.0 ** -29, 2.0 ** 60, 2.0 ** -60, 2.0 ** 61, 2.0 ** -61, 1.0]
+    for e in edges:
+        for d in (np.nextafter(e, 0), e, np.nextafter(e, np.inf)):
+            for sy in (1.0, -1.0):
+                for sx in (1.0, -1.0):
+                    args.append((sy * d * 3.0, sx * 3.0))
+                    args.append((sy * d, sx * 1.0))
+    sp = [0.0, -0.0, np.inf, -np.inf, np.nan, 1.0, -1.0, 5e-324, 1e308, 1e-308]
+    args += [(a, b) for a in sp for b in sp]
+    bad = 0
+    for y, x in args:
+        a, b, c = H.hc_atan2(y, x), H.hc_atan2_full(y, x), olib.ora_atan2(y, x)
+        same = (a == c or (a != a and c != c)) and np.signbit(a) == np.signbit(c) and (b == c or (b != b and c != c))
+        bad += not same
+    assert bad == 0, bad
