@@ -384,13 +384,6 @@ constexpr bool kBatchPipe = NUSI_BATCH_PIPE != 0;
 #define NUSI_REFO_PREFETCH 1
 #endif
 constexpr bool kRefPrefetch = NUSI_REFO_PREFETCH != 0;
-// NUSI_REFO_PIPE (A/B): the reference-order member corners in two LDS buffers by point parity (X's Dcr, Dci fields
-// and mem, which the reference order does not use otherwise): point q + 1's are stored while point q combines, so one
-// barrier per point instead of two, the block's values loaded two points ahead
-#ifndef NUSI_REFO_PIPE
-#define NUSI_REFO_PIPE 1
-#endif
-constexpr bool kRefPipe = NUSI_REFO_PIPE != 0;
 #ifndef NUSI_BATCH_KLAUNCH   // A/B: 1 = the non-phi-phi batch kernels as one launch per mass state (kOneK)
 #define NUSI_BATCH_KLAUNCH 0
 #endif
@@ -663,7 +656,7 @@ void k_alpha_batch(GridDev g, const Point* __restrict__ pts, const SplineSet* __
             const int us = mc.eu[ssrc[si]], ut = mc.eu[tsrc[ti]];
             if (ut <= us) {
                 moff = us * (us + 1) / 2 + ut;
-                if ((kRefPrefetch || kRefPipe) && !(NUSI_REFO_BSTUB & 2)) mcv = mcb[moff];
+                if (kRefPrefetch && !(NUSI_REFO_BSTUB & 2)) mcv = mcb[moff];
             }
         }
 #pragma unroll 1
@@ -688,11 +681,6 @@ void k_alpha_batch(GridDev g, const Point* __restrict__ pts, const SplineSet* __
                         kPP ? b_marg(S, t, pts[p0 + q0 + qq].a_gr) : alpha_member_ref_arg(S, t, pts[p0 + q0 + qq].a_gr);
             }
             constexpr bool pipe = kBatchPipe && !kRef;
-            constexpr bool rpipe = kRef && kRefPipe;
-            if (rpipe && q0 == 0 && moff >= 0) {   // point 0 of this mass state into buffer 0 (X)
-                X[tid] = mcv.x; X[kCC + tid] = mcv.y;
-                if (nb > 1 && !(NUSI_REFO_BSTUB & 2)) mcv = mcb[mc.NC + moff];
-            }
             if (pipe) {
                 __syncthreads();   // member edges written
                 if (cornered)
@@ -707,14 +695,7 @@ void k_alpha_batch(GridDev g, const Point* __restrict__ pts, const SplineSet* __
                 double tot = tnext;   // after states < k
                 if (reload && q + 1 < nb) tnext = A[(size_t)(p0 + q + 1) * g.PT + eidx];
                 double* memq = mem;
-                if (rpipe) {
-                    if (qq == 0) __syncthreads();   // the chunk's member edges and A, and point q's corners, written
-                    if (moff >= 0 && q + 1 < nb) {   // point q + 1's into the other buffer (point q - 1's: read before
-                        double* const nx = ((q + 1) & 1) ? mem : X;   // the barrier that ended q - 1)
-                        nx[tid] = mcv.x; nx[kCC + tid] = mcv.y;
-                        if (q + 2 < nb && !(NUSI_REFO_BSTUB & 2)) mcv = mcb[(size_t)(q + 2) * mc.NC + moff];
-                    }
-                } else if (pipe) {
+                if (pipe) {
                     memq = mem + (qq & 1) * 2 * ccmax;
                     __syncthreads();   // mem of q written / the previous point's combine is done with the other buffer
                     if (cornered && qq + 1 < nq)
@@ -743,7 +724,7 @@ void k_alpha_batch(GridDev g, const Point* __restrict__ pts, const SplineSet* __
                     SplitLeavesT<kRef> lv;
                     lv.cf[0] = P3; lv.cf[1] = P3; lv.cf[2] = P3; lv.cf[3] = P3; lv.cf[4] = P3;
                     lv.cf[5] = P3 + kCC; lv.cf[6] = P3 + 2 * kCC;   // (LL, TU1, TU2, G are not read with pre)
-                    lv.corm = kRef ? ((rpipe && (q & 1)) ? mem : X) : memq;
+                    lv.corm = kRef ? X : memq;
                     lv.cc = cc; lv.ct = ct; lv.cs = cs; lv.mb = lm; lv.nb = ln;
                     lv.sidx[0] = sl[lm]; lv.sidx[1] = sh[lm]; lv.tidx[0] = tl[ln]; lv.tidx[1] = th[ln];
                     lv.ted = edgk; lv.sed = edgk + kTEdgeFields * ct; lv.mbv = lv.sed + kSEdgeFields * cs;
@@ -766,8 +747,7 @@ void k_alpha_batch(GridDev g, const Point* __restrict__ pts, const SplineSet* __
                     }
                 } else if (valid) A[(size_t)(p0 + q) * g.PT + eidx] = needed ? tot : 0.0;
                 if (w) warn_entry(warn, wmin, T, p0 + q, w, n, m);
-                if (rpipe && qq + 1 < nq) __syncthreads();   // point q's combine is done with its buffer (the
-            }                                                // chunk's last: the next chunk's or mass state's barrier)
+            }
         }
     }
     if (wsh)   // (the batch-shared phi-phi term of this thread's entry)
