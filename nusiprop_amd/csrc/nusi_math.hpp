@@ -71,17 +71,15 @@ NUSI_FN cd operator*(cd a, cd b) { return cd{a.r * b.r - a.i * b.i, a.r * b.i + 
 NUSI_FN cd operator*(double s, cd a) { return cd{s * a.r, s * a.i}; }
 NUSI_FN cd operator*(cd a, double s) { return cd{a.r * s, a.i * s}; }
 NUSI_FN cd operator/(cd a, double s) { return cd{a.r / s, a.i / s}; }
-// Smith's two cases (|c| < |d|: ratio = c / d, re ((a.r ratio) + a.i) / den, im ((a.i ratio) - a.r) / den; else ratio =
-// d / c, re ((a.i ratio) + a.r) / den, im (a.i - (a.r ratio)) / den) by operand selects, the same operations on the same
-// operands in either case: lanes of a wave that take different cases no longer run both cases' three divisions
 NUSI_FN cd operator/(cd a, cd b)
 {
     const double c = b.r, d = b.i;
-    const bool sw = fabs(c) < fabs(d);
-    const double num = sw ? c : d, dvs = sw ? d : c, u = sw ? a.r : a.i, v = sw ? a.i : a.r;
-    const double ratio = num / dvs, den = (num * ratio) + dvs;
-    const double t = v * ratio;
-    return cd{((u * ratio) + v) / den, (sw ? t - a.r : a.i - t) / den};
+    if (fabs(c) < fabs(d)) {
+        const double ratio = c / d, den = (c * ratio) + d;
+        return cd{((a.r * ratio) + a.i) / den, ((a.i * ratio) - a.r) / den};
+    }
+    const double ratio = d / c, den = (d * ratio) + c;
+    return cd{((a.i * ratio) + a.r) / den, (a.i - (a.r * ratio)) / den};
 }
 NUSI_FN cd operator/(double s, cd b) { return C(s) / b; }
 NUSI_FN cd conj(cd a) { return cd{a.r, -a.i}; }
