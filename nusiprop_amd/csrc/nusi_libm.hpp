@@ -311,10 +311,16 @@ NUSI_FN bool wave_all_l(bool p)
     return p;
 #endif
 }
+// the rare waves' fdlibm atan2 as a call: inlined at every atan2 site it was most of k_alpha_mcorner's code (~1 700
+// of its 8 600 instructions per site, against an instruction cache shared by two CUs); NUSI_ATAN2_RARE_INLINE: inline
+NUSI_LM double atan2_rare(double y, double x) { return atan2_full(y, x); }
 NUSI_FN double atan2_i(double y, double x)
 {
 #ifndef NUSI_ATAN2_FULL   // (A/B: fdlibm's branches only)
     if (wave_all_l(atan2_plain(y, x))) return atan2_sel(y, x);
+#ifndef NUSI_ATAN2_RARE_INLINE
+    return atan2_rare(y, x);
+#endif
 #endif
     return atan2_full(y, x);
 }
