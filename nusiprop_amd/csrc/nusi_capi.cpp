@@ -460,6 +460,8 @@ struct nusi_plan {
     double* d_scratch = nullptr;   // flux outputs when the caller passes NULL
     double* d_kt = nullptr;        // the k-split alpha path's term buffer (TablesDev::Kt), kt_doubles doubles
     size_t kt_doubles = 0;
+    double* d_gpre = nullptr;      // the reference order's Gamma / alphaTilde dilogarithms (TablesDev::Gpre)
+    size_t gpre_doubles = 0;
     std::shared_ptr<SplineStore> spl;
     nusi::SplineSet* d_nospl = nullptr;   // an empty spline set in device memory (no phi-phi tables loaded)
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
@@ -609,6 +611,10 @@ AlphaBatches alpha_batches(nusi_plan* pl, int ntab, std::vector<int>& perm)
 // NUSI_OPT_REFO_CORNER_MB (automatic: kMCornerBudget bytes and half the free memory) of tables, at least the largest
 // batch; launch_alpha runs the batches in chunks that fit
 constexpr size_t kMCornerBudget = size_t(8) << 30;
+#ifndef NUSI_GA_PRE   // A/B: 0 = the reference order's Gamma / alphaTilde of few tables without k_ga_dilogs
+#define NUSI_GA_PRE 1
+#endif
+constexpr bool kGaPre = NUSI_GA_PRE != 0;
 constexpr int kOverlapTables = 16;   // calls of at most this many tables overlap Gamma / alphaTilde with alpha
 constexpr size_t kStageBytes = size_t(4) << 20;   // nusi_plan_evolve_host's pinned output staging, at most
 constexpr int kSplitTables = 2;   // calls of at most this many tables (no phi-phi) run the k-split alpha path
@@ -840,6 +846,7 @@ void nusi_plan_destroy(nusi_plan* pl)
     hipFree(pl->mc.ue);
     hipFree(pl->d_scratch);
     hipFree(pl->d_kt);
+    hipFree(pl->d_gpre);
     if (pl->stream) hipStreamDestroy(pl->stream);
     pl->spl.reset();
     nusi_plan* sh = pl->shift;
@@ -1153,6 +1160,20 @@ int nusi_plan_evolve(nusi_plan* pl, const nusi_params* pts, int n, double* d_flu
             pl->kt_doubles = need;
         }
         pl->tabs.Kt = pl->d_kt;
+    }
+    // a call of few tables in the reference order: Gamma / alphaTilde's GSL dilogarithms one per work-item first
+    // (k_ga_dilogs; 2.2 MB per table at N_E = 300)
+    pl->tabs.Gpre = nullptr;
+    if (kGaPre && refo && nbase == 0 && nd > 0 && nd <= kOverlapTables) {
+        const size_t need = nusi::gamma_alphat_pre_doubles(pl->gd.T, nd);
+        if (pl->gpre_doubles < need) {
+            hipFree(pl->d_gpre);
+            pl->d_gpre = nullptr;
+            pl->gpre_doubles = 0;
+            HIPCHECK(hipMalloc(&pl->d_gpre, sizeof(double) * need));
+            pl->gpre_doubles = need;
+        }
+        pl->tabs.Gpre = pl->d_gpre;
     }
     // one upload: the zeroed warnings, batches, gamma groups, points and tables (nusi_plan::d_in)
     HIPCHECK(hipMemcpyAsync(pl->d_in, pl->h_in, pl->in_tpts + sizeof(nusi::Point) * ntab, hipMemcpyHostToDevice, s));

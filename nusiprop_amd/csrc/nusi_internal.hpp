@@ -39,6 +39,8 @@ struct TablesDev {
                   // that k_table_shift passes on exactly the warnings of the rows a shifted slot reads
     double* Kt = nullptr;   // [npts][3][PT][8] or nullptr: the k-split alpha path of calls of few tables
                             // (launch_alpha): each mass state's terms of every entry, summed in order by k_alpha_ksum
+    double* Gpre = nullptr;   // [npts][3][kGaPreFields][T] or nullptr: the reference order's Gamma / alphaTilde
+                              // dilogarithms of calls of few tables (k_ga_dilogs, launch_gamma_alphat)
 };
 
 // Tiles of the alpha table for k_alpha_tile: kAlphaTile x kAlphaTile (n, m) bin blocks with
@@ -70,6 +72,7 @@ struct MCornerDev {
 };
 // ref: NUSI_OPT_REFERENCE_ORDER (the kernels' kRef instances: the reference's own operation order for the complex
 // dilogarithms and the s-t interference member leaves, bit-identical to the oracle's ora_set_reference_order(1))
+size_t gamma_alphat_pre_doubles(int T, int npts);   // TablesDev::Gpre's size
 hipError_t launch_gamma_alphat(const GridDev& g, const Point* pts, int npts, const SplineSet* spl, TablesDev t,
                                int* warn, hipStream_t s, bool ref);
 // batches: device [nbatches] of first table | count << 24 (count <= gmax), tables of a batch sharing

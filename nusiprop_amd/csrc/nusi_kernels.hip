@@ -56,10 +56,13 @@ struct LdsSink {
 NUSI_FN double shfl_dn(double x) { return __shfl_down(x, 1, 64); }
 NUSI_FN double shfl_upd(double x) { return __shfl_up(x, 1, 64); }
 NUSI_FN cd shfl_dn(cd z) { return cd{__shfl_down(z.r, 1, 64), __shfl_down(z.i, 1, 64)}; }
-template <bool kRef, int kParts>
+// kPre (reference order, calls of few tables): every dilogarithm value from k_ga_dilogs' block pre (ga_pre_load)
+// instead of the lanes' own GSL calls
+template <bool kRef, int kParts, bool kPre = false>
 __global__ __launch_bounds__(192 * kParts) __attribute__((amdgpu_waves_per_eu(NUSI_GA_WAVES, NUSI_GA_WAVES))) void k_gamma_alphat(GridDev g, const Point* __restrict__ pts, const SplineSet* __restrict__ splp,
                                                      double* __restrict__ G, double* __restrict__ At,
-                                                     int* __restrict__ warn, int* __restrict__ wmin)
+                                                     int* __restrict__ warn, int* __restrict__ wmin,
+                                                     const double* __restrict__ pre = nullptr)
 {
     __shared__ double v[3][kGaTerms][64], raw[kParts == 2 ? 3 : 1][kGaTerms][64];
     __shared__ int wk[3 * kParts][64];
@@ -77,7 +80,21 @@ __global__ __launch_bounds__(192 * kParts) __attribute__((amdgpu_waves_per_eu(NU
     const bool up_sh = act && (n + 1 == T || g.hi[n] == g.lo[n + 1]);   // bin n's upper edge is lane + 1's
     int w = 0;
     LdsSink sk{&v[k][0][lane], &raw[kParts == 2 ? k : 0][0][lane]};
-    if (gam) {
+    if (kPre) {
+        if (act) {
+            GammaEdgePair ge;
+            AlphatEdgePair ae;
+            AlphatBinVals bv;
+            ga_pre_load(pre + (size_t)(p * 3 + k) * kGaPreFields * T, T, n, ge, ae, bv);
+            if (gam) {
+                if (part == 0) gamma_k<kRef, 0>(P, k, lo, hi, sk, w, &ge);
+                else gamma_k<kRef, 1>(P, k, lo, hi, sk, w, &ge);
+            } else {
+                if (part == 0) alphat_k<kRef, 0>(P, spl, k, lo, hi, sk, w, &ae, &bv);
+                else alphat_k<kRef, 1>(P, spl, k, lo, hi, sk, w, &ae, &bv);
+            }
+        }
+    } else if (gam) {
         GammaEdgePair ge{};
         unsigned need = 0;
         if (act) need = kParts == 1 ? gamma_edge_need<-1>(P, k, lo, hi) : part == 0 ? gamma_edge_need<0>(P, k, lo, hi)
@@ -191,10 +208,36 @@ void k_alpha(GridDev g, const Point* __restrict__ pts, const SplineSet* __restri
     if (w) warn_entry(warn, wmin, g.T, p, w, n, m);
 }
 
+// Calls of few tables in the reference order: every GSL dilogarithm of Gamma / alphaTilde, one per work-item
+// (ga_pre_slot; grid (bins / 64, points, 3 mass states x kGaPreSlots)) into pre [point][k][kGaPreFields][T], before
+// k_gamma_alphat<true, 2, true> combines them: a lane no longer walks its bin's six GSL series one after the other
+__global__ __launch_bounds__(64) void k_ga_dilogs(GridDev g, const Point* __restrict__ pts, double* __restrict__ pre)
+{
+    const int n = blockIdx.x * 64 + threadIdx.x, p = blockIdx.y, T = g.T;
+    const int k = blockIdx.z / kGaPreSlots, slot = blockIdx.z - k * kGaPreSlots;   // (wave-uniform slot)
+    if (n >= T) return;
+    const Point& P = pts[p];
+    if (!P.non_resonant) return;   // (gamma_k / alphat_k return before any dilogarithm)
+    double v[2];
+    int f;
+    const int nv = ga_pre_slot(P, k, g.lo[n], g.hi[n], slot, v, &f);
+    double* o = pre + ((size_t)(p * 3 + k) * kGaPreFields + f) * T + n;
+    o[0] = v[0];
+    if (nv == 2) o[T] = v[1];
+}
+
+size_t gamma_alphat_pre_doubles(int T, int npts) { return (size_t)3 * kGaPreFields * T * npts; }
+
 hipError_t launch_gamma_alphat(const GridDev& g, const Point* pts, int npts, const SplineSet* spl, TablesDev t,
                                int* warn, hipStream_t s, bool ref)
 {
     dim3 grid((g.T + 62) / 63, npts, 2);   // (63 bins per workgroup: the edge-shared lanes)
+    if (ref && t.Gpre && npts <= 16) {   // (the dilogarithms one per work-item first)
+        hipLaunchKernelGGL(k_ga_dilogs, dim3((g.T + 63) / 64, npts, 3 * kGaPreSlots), dim3(64), 0, s, g, pts, t.Gpre);
+        hipLaunchKernelGGL((k_gamma_alphat<true, 2, true>), grid, dim3(384), 0, s, g, pts, spl, t.G, t.At, warn, t.Wmin,
+                           t.Gpre);
+        return hipGetLastError();
+    }
     if (npts <= 16) {   // (a few tables: the channels split too, kParts = 2)
         if (ref) hipLaunchKernelGGL((k_gamma_alphat<true, 2>), grid, dim3(384), 0, s, g, pts, spl, t.G, t.At, warn, t.Wmin);
         else hipLaunchKernelGGL((k_gamma_alphat<false, 2>), grid, dim3(384), 0, s, g, pts, spl, t.G, t.At, warn, t.Wmin);

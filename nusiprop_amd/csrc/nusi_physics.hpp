@@ -371,9 +371,13 @@ NUSI_FN unsigned alphat_edge_need(const Point& P, int k, double Em, double Ep)
     }
     return m;
 }
+// alphaTilde's dilogarithms of one bin that are not edge values: the s-t interference's d26 = Li2(z2) - Li2(z6) and
+// d43 = Li2(z4) - Li2(z3) (their four gsl_sf_complex_dilog_xy_e values) and the t-u combination's four gsl_sf_dilog
+// values (k_ga_dilogs evaluates them one per work-item for calls of few tables)
+struct AlphatBinVals { cd d26a, d26b, d43a, d43b; double c1, c2, c3, c4; };
 template <bool kRef, int kPart, class Sink>   // kRef: NUSI_OPT_REFERENCE_ORDER (GSL's dilogarithms, nusi_gsl.hpp)
 NUSI_FN void alphat_k(const Point& P, const SplineSet& spl, int k, double Em, double Ep, Sink& tot, int& warn,
-                      const AlphatEdgePair* ae = nullptr)
+                      const AlphatEdgePair* ae = nullptr, const AlphatBinVals* bv = nullptr)
 {
     const double g = P.g, mphi = P.mphi, Ga = P.Ga;
     const double g4 = (g * g) * (g * g), m2 = mphi * mphi, m4 = (mphi * mphi) * (mphi * mphi);
@@ -441,7 +445,9 @@ NUSI_FN void alphat_k(const Point& P, const SplineSet& spl, int k, double Em, do
                 combi = (-2 * (-1 + d) * lq) / tp - (2 * (-1 + nm::log(-(d / ((-1 + d) * tp))))) / (tp * tp)
                         + (-6 + 4 * d + d2 - 2 * d3 - 8 * lq + 8 * d * lq + 2 * d3 * lq - 2 * d4 * lq - 6 * lt + 6 * d * lt) / (3. * (-1 + d) * (tp * tp * tp))
                         + (8 - 12 * d + 3 * d2 + 12 * lq - 24 * d * lq + 12 * d2 * lq + 12 * lt - 24 * d * lt + 12 * d2 * lt) / (3. * ((-1 + d) * (-1 + d)) * ((tp * tp) * (tp * tp)));
-            } else
+            } else if (bv)
+                combi = bv->c1 - bv->c2 + bv->c3 - bv->c4;   // (the same four values, the same left-to-right sum)
+            else
                 combi = li2_t<kRef>(1 + 1 / (-2 + tp)) - li2_t<kRef>((-1 + tm) / (-2 + tp)) + li2_t<kRef>(1 + (1 + tm - tp) / tp) - li2_t<kRef>(1 + 1 / tp);
             atu = g4 / (32 * kPi * m4 * (1 + tm) * tp) *
                   (2 * (2 * (1 + tm) * (tm - tp) - 2 * (1 + tm) * tp * nm::atanh(1 / (1 - tp)) * nm::atanh((tm - tp) / (-2 + tm + tp))
@@ -478,8 +484,8 @@ NUSI_FN void alphat_k(const Point& P, const SplineSet& spl, int k, double Em, do
             const double z6 = 1 - tp / (1 + tm);
             d78 = ae ? dilogdiff_c_pre(C(1 - tm), C(1 - tp), ae->lo.e78, ae->hi.e78) : dilogdiff_c<kRef>(C(1 - tm), C(1 - tp));
             d51 = ae ? dilogdiff_c_pre(z5, z1, ae->hi.e51, ae->lo.e51) : dilogdiff_c<kRef>(z5, z1);
-            d26 = dilogdiff_c<kRef>(C(z2), C(z6));
-            d43 = dilogdiff_c<kRef>(z4, z3);
+            d26 = bv ? dilogdiff_c_pre(C(z2), C(z6), bv->d26a, bv->d26b) : dilogdiff_c<kRef>(C(z2), C(z6));
+            d43 = bv ? dilogdiff_c_pre(z4, z3, bv->d43a, bv->d43b) : dilogdiff_c<kRef>(z4, z3);
         }
         const double Lgp = nm::log1p(((1 + tp) * (1 + tp)) / gr2), Lgm = nm::log1p(((1 + tm) * (1 + tm)) / gr2);
         const double Am = carg(C(-1 - tm, gr)), Ap = carg(C(-1 - tp, gr));
@@ -537,6 +543,75 @@ NUSI_FN double alphat_entry(const Point& P, const SplineSet& spl, double Em, dou
     NUSI_MASS_LOOP
     for (int k = 0; k < 3; ++k) alphat_k<kRef, -1>(P, spl, k, Em, Ep, tot, warn);
     return tot.tot;
+}
+
+// Calls of few tables in the reference order (k_ga_dilogs): every GSL dilogarithm Gamma and alphaTilde read for
+// (point, mass state k, bin [Em, Ep]) -- the edge values at both edges (gamma_edge_vals, alphat_edge_vals) and
+// alphaTilde's bin values (AlphatBinVals) -- one slot per work-item, the same functions on the same arguments as
+// gamma_k / alphat_k would call them (so the same bits), into kGaPreFields fields per (point, k, bin):
+//   0 ls, 1 l1s, 2-3 cz at Em | 4 ls, 5 l1s, 6-7 cz at Ep | 8-9 e78, 10-11 e51, 12 e1o, 13 e1p at Em | 14-19 at Ep |
+//   20-21 d26a, 22-23 d26b, 24-25 d43a, 26-27 d43b, 28-31 c1 .. c4
+// Values no branch of the bin reads are evaluated too (and not read).  v[0], v[1] at field *f (v[1]: complex only);
+// returns the count.
+constexpr int kGaPreSlots = 22, kGaPreFields = 32;
+NUSI_FN int ga_pre_slot(const Point& P, int k, double Em, double Ep, int slot, double* v, int* f)
+{
+    if (slot < 6) {   // Gamma's edge values (reference order: no conj z value)
+        const int side = slot / 3, which = slot - 3 * side;
+        GammaEdgeVals e{};
+        gamma_edge_vals<true>(P, k, side ? Ep : Em, which == 0 ? kGeLs : which == 1 ? kGeL1s : kGeCz, e);
+        *f = 4 * side + which;
+        if (which == 0) { v[0] = e.ls; return 1; }
+        if (which == 1) { v[0] = e.l1s; return 1; }
+        v[0] = e.cz.r; v[1] = e.cz.i;
+        return 2;
+    }
+    if (slot < 14) {   // alphaTilde's edge values
+        const int side = (slot - 6) / 4, which = slot - 6 - 4 * side;
+        AlphatEdgeVals e{};
+        alphat_edge_vals<true>(P, k, side ? Ep : Em, which == 0 ? kAe78 : which == 1 ? kAe51 : which == 2 ? kAe1o : kAe1p, e);
+        const int f0 = 8 + 6 * side;
+        if (which == 0) { *f = f0; v[0] = e.e78.r; v[1] = e.e78.i; return 2; }
+        if (which == 1) { *f = f0 + 2; v[0] = e.e51.r; v[1] = e.e51.i; return 2; }
+        *f = f0 + 2 + which;
+        v[0] = which == 2 ? e.e1o : e.e1p;
+        return 1;
+    }
+    // alphaTilde's bin values: tm, tp, z2 .. z6 and the combination's arguments as alphat_k forms them
+    const double mphi = P.mphi, Ga = P.Ga, m2 = mphi * mphi, gr = Ga / mphi, mk = P.mn[k];
+    double tp = -2 * mk * Ep / m2, tm = -2 * mk * Em / m2;
+    if (fabs(tm + 1) < 1e-7) tm += tm * 1e-6;
+    if (fabs(tp + 1) < 1e-7) tp += tp * 1e-6;
+    const int b = slot - 14;
+    if (b < 4) {
+        const cd dt_m = C(2 + tm, -gr);
+        cd z;
+        if (b == 0) z = C(1 / (1 + tm));
+        else if (b == 1) z = C(1 - tp / (1 + tm));
+        else if (b == 2) z = (1 + tm - tp) / dt_m;
+        else z = 1 / dt_m;
+        const cd d = cli2_t<true>(z);
+        *f = 20 + 2 * b;
+        v[0] = d.r; v[1] = d.i;
+        return 2;
+    }
+    const double x = b == 4 ? 1 + 1 / (-2 + tp) : b == 5 ? (-1 + tm) / (-2 + tp) : b == 6 ? 1 + (1 + tm - tp) / tp : 1 + 1 / tp;
+    *f = 28 + (b - 4);
+    v[0] = li2_t<true>(x);
+    return 1;
+}
+// the fields of (point, k, bin n) -> the pairs and bin values gamma_k / alphat_k take (fb: field 0 of (point, k),
+// fields T doubles apart)
+NUSI_FN void ga_pre_load(const double* fb, int T, int n, GammaEdgePair& ge, AlphatEdgePair& ae, AlphatBinVals& bv)
+{
+    const double* x = fb + n;
+    auto F = [&](int i) { return x[(size_t)i * T]; };
+    ge.lo.ls = F(0); ge.lo.l1s = F(1); ge.lo.cz = C(F(2), F(3));
+    ge.hi.ls = F(4); ge.hi.l1s = F(5); ge.hi.cz = C(F(6), F(7));
+    ae.lo.e78 = C(F(8), F(9)); ae.lo.e51 = C(F(10), F(11)); ae.lo.e1o = F(12); ae.lo.e1p = F(13);
+    ae.hi.e78 = C(F(14), F(15)); ae.hi.e51 = C(F(16), F(17)); ae.hi.e1o = F(18); ae.hi.e1p = F(19);
+    bv.d26a = C(F(20), F(21)); bv.d26b = C(F(22), F(23)); bv.d43a = C(F(24), F(25)); bv.d43b = C(F(26), F(27));
+    bv.c1 = F(28); bv.c2 = F(29); bv.c3 = F(30); bv.c4 = F(31);
 }
 
 // ---------------------------------------------------------------------------

@@ -106,7 +106,52 @@ static int ga_shared_t(const double* pt, const int* flags, int T, const double* 
     return warn;
 }
 
+// Host emulation of the reference order's few-table path: k_ga_dilogs' slots (ga_pre_slot) into a bin's fields, read
+// back by ga_pre_load, the channels through gamma_k / alphat_k in the two parts, summed as the kernel's wave 0 sums them
+static int ga_pre_t(const double* pt, const int* flags, int T, const double* lo, const double* hi, double* G, double* At)
+{
+    using namespace nusi;
+    const Point P = mk(pt, flags);
+    SplineSet spl{};
+    int warn = 0;
+    for (int n = 0; n < T; ++n) {
+        double g = 0.0, a = 0.0;
+        for (int k = 0; k < 3; ++k) {
+            double fld[kGaPreFields];
+            for (int i = 0; i < kGaPreFields; ++i) fld[i] = __builtin_nan("");
+            if (P.non_resonant)
+                for (int slot = 0; slot < kGaPreSlots; ++slot) {
+                    double v[2];
+                    int f;
+                    const int nv = ga_pre_slot(P, k, lo[n], hi[n], slot, v, &f);
+                    fld[f] = v[0];
+                    if (nv == 2) fld[f + 1] = v[1];
+                }
+            GammaEdgePair ge;
+            AlphatEdgePair ae;
+            AlphatBinVals bv;
+            ga_pre_load(fld, 1, 0, ge, ae, bv);
+            double vg[kAlphatSlots] = {}, va[kAlphatSlots] = {};
+            SlotSink sg{vg}, sa{va};
+            gamma_k<true, 0>(P, k, lo[n], hi[n], sg, warn, &ge);
+            gamma_k<true, 1>(P, k, lo[n], hi[n], sg, warn, &ge);
+            alphat_k<true, 0>(P, spl, k, lo[n], hi[n], sa, warn, &ae, &bv);
+            alphat_k<true, 1>(P, spl, k, lo[n], hi[n], sa, warn, &ae, &bv);
+            const int ng = !P.non_resonant ? 1 : kGammaSlots, na = !P.non_resonant ? 1 : kAlphatSlots;
+            for (int i = 0; i < ng; ++i) g += vg[i];
+            for (int i = 0; i < na; ++i) a += va[i];
+        }
+        G[n] = g;
+        At[n] = a;
+    }
+    return warn;
+}
+
 extern "C" {
+int hc_ga_pre(const double* pt, const int* flags, int T, const double* lo, const double* hi, double* G, double* At)
+{
+    return ga_pre_t(pt, flags, T, lo, hi, G, At);
+}
 int hc_ga_shared(const double* pt, const int* flags, int T, const double* lo, const double* hi, int parts, int ref,
                  double* G, double* At)
 {

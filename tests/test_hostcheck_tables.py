@@ -145,3 +145,26 @@ def test_edge_shared_gamma_alphat_bit_identical(oracle_mod, name, ref, parts):
     H.hc_ga_shared(_dp(pt), flags, T, _dp(lo), _dp(hi), parts, ref, _dp(Gh), _dp(aTh))
     assert np.array_equal(Gh, G), "Gamma differs at %s" % np.flatnonzero(Gh != G)[:5]
     assert np.array_equal(aTh, aT), "alphaTilde differs at %s" % np.flatnonzero(aTh != aT)[:5]
+
+
+@pytest.mark.parametrize("name", sorted(cases.SMALL_CASES) + ["C2A", "C2B"])
+def test_ga_dilogs_prepass_bit_identical(oracle_mod, name):
+    """The reference order's few-table path (round 6): k_ga_dilogs evaluates every GSL dilogarithm of
+    Gamma / alphaTilde one per work-item (ga_pre_slot: both edges' values and alphaTilde's bin values d26, d43 and the
+    t-u combination's four), k_gamma_alphat<.., kPre> reads them (ga_pre_load) -- emulated on the host: Gamma and
+    alphaTilde bit for bit against the reference-order oracle (the fields start as NaN, so a field no slot writes would
+    show).  BASELINE configs 2a / 2b at their own N_E = 300, the small cases at 40 bins."""
+    from tests.hostcheck import build_hostcheck
+    H = build_hostcheck()
+    kw = getattr(cases, name) if name in ("C2A", "C2B") else dict(cases.SMALL_CASES[name], N_bins_E=40)
+    o = oracle_mod.Oracle(**cases.oracle_kwargs(kw))
+    with oracle_mod.reference_order(1):
+        G, aT, _ = o.tables()
+    lo, hi = extended_axis(o)
+    pt, flags = point_array(o, kw)
+    T = o.T
+    Gh, aTh = np.zeros(T), np.zeros(T)
+    H.hc_ga_pre.restype = ctypes.c_int
+    H.hc_ga_pre(_dp(pt), flags, T, _dp(lo), _dp(hi), _dp(Gh), _dp(aTh))
+    assert np.array_equal(Gh, G), "Gamma differs at %s" % np.flatnonzero(Gh != G)[:5]
+    assert np.array_equal(aTh, aT), "alphaTilde differs at %s" % np.flatnonzero(aTh != aT)[:5]
