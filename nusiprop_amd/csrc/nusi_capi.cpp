@@ -631,9 +631,6 @@ int mcorner_ensure(nusi_plan* p, int ntab, const AlphaBatches& ab, int budget_mb
         HIPCHECK(hipMemcpy(mc.ue, ue.data(), sizeof(double) * ue.size(), hipMemcpyHostToDevice));
         mc.U = (int)ue.size();
         mc.NC = (long long)mc.U * (mc.U + 1) / 2;
-        // the cost order of calls of few tables (launch_alpha: chunks of fewer than 2048 x 256 member-corner calls)
-        mc.sort_cap = 2048LL * 256;
-        HIPCHECK(hipMalloc(&mc.sortbuf, sizeof(int) * (2 * (size_t)mc.sort_cap + 128)));
     }
     const size_t per = sizeof(double) * 6 * (size_t)mc.NC;
     if (mc.buf && budget_mb == 0 && mc.cap_tables >= ntab && per * mc.cap_tables <= kMCornerBudget)
@@ -847,7 +844,6 @@ void nusi_plan_destroy(nusi_plan* pl)
     hipFree(pl->mc.buf);
     hipFree(pl->mc.eu);
     hipFree(pl->mc.ue);
-    hipFree(pl->mc.sortbuf);
     hipFree(pl->d_scratch);
     hipFree(pl->d_kt);
     hipFree(pl->d_gpre);

@@ -69,8 +69,6 @@ struct MCornerDev {
     double* ue = nullptr;    // [U]: the energy of each edge
     long long NC = 0;
     int U = 0, cap_tables = 0;
-    int* sortbuf = nullptr;   // calls of few tables: [sort_cap] keys | [sort_cap] order | [2 64] counts, cursors
-    long long sort_cap = 0;
 };
 // ref: NUSI_OPT_REFERENCE_ORDER (the kernels' kRef instances: the reference's own operation order for the complex
 // dilogarithms and the s-t interference member leaves, bit-identical to the oracle's ora_set_reference_order(1))

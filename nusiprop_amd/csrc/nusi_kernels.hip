@@ -518,10 +518,6 @@ __global__ __launch_bounds__(256) void k_alpha_medge(GridDev g, const Point* __r
 // ns per call against 0.06, scripts/dev/gsl_bench.hip).  The values pass through LDS to leave as runs of cb corners
 // per (field, table), the layout the batch kernel reads a tile's corner rows from.
 constexpr int kMcJobs = 1024;
-#ifndef NUSI_MC_SORT   // A/B: 0 = the member corners of few tables in corner order (k_alpha_mcorner)
-#define NUSI_MC_SORT 1
-#endif
-constexpr bool kMcSort = NUSI_MC_SORT != 0;
 #ifndef NUSI_MC_WAVES   // A/B: waves per SIMD the member-corner kernel is built for (0: the compiler's choice)
 #define NUSI_MC_WAVES 0
 #endif
@@ -558,92 +554,6 @@ void k_alpha_mcorner(const Point* __restrict__ pts, const int* __restrict__ batc
         const int q = e / (2 * cb), r = e - q * 2 * cb;
         if (c0 + r / 2 < mc.NC) o[((size_t)q * mc.NC + c0) * 2 + r] = v[e];
     }
-}
-
-// Calls of few tables (a single propagation): the chunk's member-corner calls are too few to fill the GPU several
-// times over, and a wave's 64 neighbouring corners take 64 different GSL series lengths (up to ~1 100 terms near
-// |w| = 0.98), so the kernel lasts as long as its waves' slowest lanes.  There the calls are ordered by GSL's
-// estimated iterations first (gsl_cli2_cost: a bucket per 16 iterations, the longest first) -- k_mc_key, a histogram;
-// k_mc_scatter, a counting sort's placement -- and k_alpha_mcorner_perm evaluates them in that order, each call's
-// value into its own place of the block: the same functions on the same arguments, so the same bits; the order only
-// decides which lanes share a wave.  Job j = (table t of the chunk, mass state k, corner c), j = (t 3 + k) NC + c.
-constexpr int kMcBuckets = 64;
-struct McJob {
-    int p, q, nb, p0;   // table, its place in its batch of nb tables starting at p0
-    int k;
-    long long c;
-};
-NUSI_FN McJob mc_job(const int* __restrict__ batches, int nbat, int pc0, long long NC, long long j)
-{
-    McJob J;
-    const long long t = j / (3 * NC), r = j - t * 3 * NC;
-    J.k = (int)(r / NC);
-    J.c = r - (long long)J.k * NC;
-    J.p = pc0 + (int)t;
-    J.p0 = J.p;
-    J.nb = 1;
-    for (int i = 0; i < nbat; ++i) {
-        const int bw = batches[i], p0 = bw & 0xffffff, nb = (int)((unsigned)bw >> 24);
-        if (J.p >= p0 && J.p < p0 + nb) { J.p0 = p0; J.nb = nb; break; }
-    }
-    J.q = J.p - J.p0;
-    return J;
-}
-__global__ __launch_bounds__(256) void k_mc_key(const Point* __restrict__ pts, const int* __restrict__ batches, int nbat,
-                                                MCornerDev mc, int pc0, long long tot, int* __restrict__ key,
-                                                int* __restrict__ hist)
-{
-    __shared__ int h[kMcBuckets];
-    if (threadIdx.x < kMcBuckets) h[threadIdx.x] = 0;
-    __syncthreads();
-    const long long j = (long long)blockIdx.x * 256 + threadIdx.x;
-    if (j < tot) {
-        const McJob J = mc_job(batches, nbat, pc0, mc.NC, j);
-        const Point& P = pts[J.p0];
-        int b = kMcBuckets - 1;   // (no member corners: a bucket of its own at the end, evaluated as nothing)
-        if (P.non_resonant && P.majorana) {
-            double S, t;
-            alpha_mcorner_st(P, J.k, J.c, mc.ue, S, t);
-            const cd z = (1 + S + t) / C(2 + t, -pts[J.p].a_gr);
-            const double it = gsl_cli2_cost(z.r, z.i);
-            b = (kMcBuckets - 2) - (int)fmin((double)(kMcBuckets - 2), it * (1.0 / 16.0));
-        }
-        key[j] = b;
-        atomicAdd(&h[b], 1);
-    }
-    __syncthreads();
-    if (threadIdx.x < kMcBuckets && h[threadIdx.x]) atomicAdd(&hist[threadIdx.x], h[threadIdx.x]);
-}
-// hist [kMcBuckets] counts, then [kMcBuckets] placement cursors (zeroed with the counts)
-__global__ __launch_bounds__(256) void k_mc_scatter(const int* __restrict__ key, long long tot, int* __restrict__ hist,
-                                                    int* __restrict__ perm)
-{
-    __shared__ int base[kMcBuckets];
-    if (threadIdx.x == 0) {
-        int a = 0;
-        for (int b = 0; b < kMcBuckets; ++b) { base[b] = a; a += hist[b]; }
-    }
-    __syncthreads();
-    const long long j = (long long)blockIdx.x * 256 + threadIdx.x;
-    if (j >= tot) return;
-    const int b = key[j];
-    perm[base[b] + atomicAdd(&hist[kMcBuckets + b], 1)] = (int)j;
-}
-__global__ __launch_bounds__(256) void k_alpha_mcorner_perm(const Point* __restrict__ pts, const int* __restrict__ batches,
-                                                            int nbat, MCornerDev mc, int pc0, long long tot,
-                                                            const int* __restrict__ perm)
-{
-    const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
-    if (i >= tot) return;
-    const McJob J = mc_job(batches, nbat, pc0, mc.NC, perm[i]);
-    const Point& P = pts[J.p0];
-    if (!(P.non_resonant && P.majorana)) return;   // (no member corners)
-    double S, t;
-    alpha_mcorner_st(P, J.k, J.c, mc.ue, S, t);
-    const cd Dc = alpha_member_ref_dc_inl(S, t, pts[J.p].a_gr);
-    double* const o = mc.buf + (size_t)(J.p0 - pc0) * 6 * mc.NC + (size_t)J.k * 2 * J.nb * mc.NC;
-    o[((size_t)J.q * mc.NC + J.c) * 2] = Dc.r;
-    o[((size_t)J.q * mc.NC + J.c) * 2 + 1] = Dc.i;
 }
 
 void mcorner_edges(int T, const double* lo, const double* hi, std::vector<int>& eu, std::vector<double>& ue)
@@ -1100,23 +1010,10 @@ static hipError_t launch_alpha_t(const GridDev& g, const Point* pts, int npts, c
                         // jobs per workgroup: 4 per work-item on scans, 1 when the chunk is too small to fill ~2048
                         // workgroups (a single propagation: one GSL call per work-item, not four in a row)
                         const long long tot = mc->NC * 3 * ntb;
-                        if (kMcSort && mc->sortbuf && tot <= mc->sort_cap) {   // (few tables: the calls by cost first)
-                            int* const key = mc->sortbuf;
-                            int* const perm = key + mc->sort_cap;
-                            int* const hist = perm + mc->sort_cap;
-                            if (hipError_t err = hipMemsetAsync(hist, 0, sizeof(int) * 2 * kMcBuckets, s)) return err;
-                            const unsigned nblk = (unsigned)((tot + 255) / 256);
-                            hipLaunchKernelGGL(k_mc_key, dim3(nblk), dim3(256), 0, s, pts, batches + b, e - b, *mc, pc0, tot,
-                                               key, hist);
-                            hipLaunchKernelGGL(k_mc_scatter, dim3(nblk), dim3(256), 0, s, key, tot, hist, perm);
-                            hipLaunchKernelGGL(k_alpha_mcorner_perm, dim3(nblk), dim3(256), 0, s, pts, batches + b, e - b,
-                                               *mc, pc0, tot, perm);
-                        } else {
-                            const int jobs = 256 * (int)std::max(1LL, std::min<long long>(kMcJobs / 256, tot / (2048 * 256)));
-                            const int cbmin = jobs / nbmax;
-                            hipLaunchKernelGGL(k_alpha_mcorner, dim3((unsigned)((mc->NC + cbmin - 1) / cbmin), e - b, 3),
-                                               dim3(256), 0, s, pts, batches + b, *mc, pc0, jobs);
-                        }
+                        const int jobs = 256 * (int)std::max(1LL, std::min<long long>(kMcJobs / 256, tot / (2048 * 256)));
+                        const int cbmin = jobs / nbmax;
+                        hipLaunchKernelGGL(k_alpha_mcorner, dim3((unsigned)((mc->NC + cbmin - 1) / cbmin), e - b, 3),
+                                           dim3(256), 0, s, pts, batches + b, *mc, pc0, jobs);
                         if (split) {
                             hipLaunchKernelGGL((k_alpha_batch<false, true, true>), dim3(at.ncls[0], e - b, 3),
                                                dim3(kTileThreads), lds, s, g, pts, spl, at.tiles, batches + b, t.A, t.Med,
