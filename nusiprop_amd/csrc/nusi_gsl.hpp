@@ -383,25 +383,16 @@ NUSI_FN void cseries_t(bool s2, double r, double lr, double x, double y, double&
         // added, then each lane's test at k -- false for the lanes still above it)
         const double big = r * 0x1p-50;
         bool small = false;
-        // two terms per vote while both are below every lane's kmax: the state after the first is kept, and if a
-        // lane's first term fell below its bound the wave returns to it -- the same terms and exit as one at a time,
-        // with one wave vote (a VALU -> SALU round trip that a lone wave waits out) per two terms
+        // two terms per kmax vote while both are below every lane's kmax (the same terms and exit as one at a time)
         while (wave_all(k + 1 < kmax)) {
             term(k);
-            const bool s1 = q < big;
-            const double ck1 = ck, sk1 = sk, rk1 = rk, re1 = real_sum, im1 = imag_sum, q1 = q, dr1 = dr, di1 = di;
-            const KRow nx1 = next;
-            term(k + 1);
-            if (wave_any(s1 || q < big)) {
-                if (wave_any(s1)) {
-                    ck = ck1; sk = sk1; rk = rk1; real_sum = re1; imag_sum = im1; q = q1; dr = dr1; di = di1; next = nx1;
-                } else {
-                    ++k;
-                }
-                small = true;
-                break;
-            }
-            k += 2;
+            small = wave_any(q < big);
+            if (small) break;
+            ++k;
+            term(k);
+            small = wave_any(q < big);
+            if (small) break;
+            ++k;
         }
         if (!small)
             while (wave_all(k < kmax)) {
