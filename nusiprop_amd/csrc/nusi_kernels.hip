@@ -431,7 +431,8 @@ constexpr bool kRefPrefetch = NUSI_REFO_PREFETCH != 0;
 #define NUSI_BATCH_KLAUNCH 0
 #endif
 constexpr bool kBatchKLaunch = NUSI_BATCH_KLAUNCH != 0;
-#ifndef NUSI_REFO_BSTUB   // timing A/B only (wrong tables): bit 1 the batch kernel without the block's loads
+#ifndef NUSI_REFO_BSTUB   // timing A/B only (wrong tables): bit 1 the batch kernel without the block's loads, bit 2
+                          // without the chunk's A (atan2 of the member quotient), bit 3 without the per-point combine
 #define NUSI_REFO_BSTUB 0
 #endif
 __host__ __device__ inline int alpha_batch_lds_doubles()
@@ -721,7 +722,8 @@ void k_alpha_batch(GridDev g, const Point* __restrict__ pts, const SplineSet* __
 #pragma unroll 1
                 for (int qq = 0; qq < nq; ++qq)   // (inline: C4 7.42 -> 7.28 ms, r6p; kPP, whose point loop holds
                     X[(3 + qq) * kCC + tid] =     // the phi-phi term too, as a call: C3 12.33 -> 11.24 ms, r6q)
-                        kPP ? b_marg(S, t, pts[p0 + q0 + qq].a_gr) : alpha_member_ref_arg(S, t, pts[p0 + q0 + qq].a_gr);
+                        (NUSI_REFO_BSTUB & 4) ? S + t : kPP ? b_marg(S, t, pts[p0 + q0 + qq].a_gr)
+                                                            : alpha_member_ref_arg(S, t, pts[p0 + q0 + qq].a_gr);
             }
             constexpr bool pipe = kBatchPipe && !kRef;
             if (pipe) {
@@ -763,7 +765,7 @@ void k_alpha_batch(GridDev g, const Point* __restrict__ pts, const SplineSet* __
                 }
                 int w = 0;
                 TermRec rec;
-                if (needed) {
+                if (needed && !(kRef && (NUSI_REFO_BSTUB & 8))) {
                     SplitLeavesT<kRef> lv;
                     lv.cf[0] = P3; lv.cf[1] = P3; lv.cf[2] = P3; lv.cf[3] = P3; lv.cf[4] = P3;
                     lv.cf[5] = P3 + kCC; lv.cf[6] = P3 + 2 * kCC;   // (LL, TU1, TU2, G are not read with pre)
