@@ -427,10 +427,6 @@ constexpr bool kBatchPipe = NUSI_BATCH_PIPE != 0;
 #define NUSI_REFO_PREFETCH 1
 #endif
 constexpr bool kRefPrefetch = NUSI_REFO_PREFETCH != 0;
-#ifndef NUSI_REFO_ARGN   // A/B: 0 = the chunk's A point by point (alpha_member_ref_arg in a loop)
-#define NUSI_REFO_ARGN 1
-#endif
-constexpr bool kRefArgN = NUSI_REFO_ARGN != 0;
 #ifndef NUSI_BATCH_KLAUNCH   // A/B: 1 = the non-phi-phi batch kernels as one launch per mass state (kOneK)
 #define NUSI_BATCH_KLAUNCH 0
 #endif
@@ -723,21 +719,11 @@ void k_alpha_batch(GridDev g, const Point* __restrict__ pts, const SplineSet* __
             if (kRef && moff >= 0) {
                 const int si = tid / ct, ti = tid - si * ct;
                 const double S = edgk[kTEdgeFields * ct + kSEdgeVal * cs + si], t = edgk[kTEdgeVal * ct + ti];
-if (kPP || !kRefArgN) {
 #pragma unroll 1
-                    for (int qq = 0; qq < nq; ++qq)   // (inline: C4 7.42 -> 7.28 ms, r6p; kPP, whose point loop holds
-                        X[(3 + qq) * kCC + tid] =     // the phi-phi term too, as a call: C3 12.33 -> 11.24 ms, r6q)
-                            (NUSI_REFO_BSTUB & 4) ? S + t : kPP ? b_marg(S, t, pts[p0 + q0 + qq].a_gr)
-                                                                : alpha_member_ref_arg(S, t, pts[p0 + q0 + qq].a_gr);
-                } else {   // the chunk's points at once, straight-line (alpha_member_ref_arg_n)
-                    double grq[kBatchQC], Aq[kBatchQC];
-#pragma unroll
-                    for (int qq = 0; qq < kBatchQC; ++qq) grq[qq] = pts[p0 + q0 + (qq < nq ? qq : nq - 1)].a_gr;
-                    alpha_member_ref_arg_n<kBatchQC>(S, t, grq, Aq);
-#pragma unroll
-                    for (int qq = 0; qq < kBatchQC; ++qq)
-                        if (qq < nq) X[(3 + qq) * kCC + tid] = Aq[qq];
-                }
+                for (int qq = 0; qq < nq; ++qq)   // (inline: C4 7.42 -> 7.28 ms, r6p; kPP, whose point loop holds
+                    X[(3 + qq) * kCC + tid] =     // the phi-phi term too, as a call: C3 12.33 -> 11.24 ms, r6q)
+                        (NUSI_REFO_BSTUB & 4) ? S + t : kPP ? b_marg(S, t, pts[p0 + q0 + qq].a_gr)
+                                                            : alpha_member_ref_arg(S, t, pts[p0 + q0 + qq].a_gr);
             }
             constexpr bool pipe = kBatchPipe && !kRef;
             if (pipe) {
