@@ -570,6 +570,23 @@ void mcorner_edges(int T, const double* lo, const double* hi, std::vector<int>& 
 }
 
 
+// Diagnostic build only (-DNUSI_BATCH_TRACE, scripts/build_variant.sh): s_memtime stamps of the reference-order batch
+// kernel's phases in workgroups (x < 4, y < 4), per wave, in program order (per mass state: its start, the edge
+// leaves' barrier, the shared corners' barrier, the brackets' barrier; per chunk: its start, its member edges and A
+// done; per point: its two barriers and its combine done).  nusi_debug_batch_trace() copies them out; compiled out of
+// the product.
+#ifdef NUSI_BATCH_TRACE
+constexpr int kBtWg = 16, kBtN = 512;
+__device__ unsigned long long g_bt[kBtWg * 4 * kBtN];
+#define NUSI_BT()                                                                                                   \
+    do {                                                                                                            \
+        if (kRef && !kPP && !kSplit && blockIdx.x < 4 && blockIdx.y < 4 && (threadIdx.x & 63) == 0 && bt_i < kBtN) \
+            g_bt[((blockIdx.y * 4 + blockIdx.x) * 4 + (threadIdx.x >> 6)) * kBtN + bt_i] = __builtin_amdgcn_s_memtime(); \
+        ++bt_i;                                                                                                     \
+    } while (0)
+#else
+#define NUSI_BT() do { } while (0)
+#endif
 // kPP: the batches' tables have the phi-phi channel (its shared term per k).  kRef: NUSI_OPT_REFERENCE_ORDER -- each
 // point's member corners in the reference's operation order, read from k_alpha_mcorner's block mc (Dcr, Dci, A into
 // the X block, which then holds no Taylor coefficients; pc0: the first table of the launch chunk), the rest of the
@@ -649,11 +666,16 @@ void k_alpha_batch(GridDev g, const Point* __restrict__ pts, const SplineSet* __
     const int mjobs = ct + cs + kAlphaTile;
     int wsh = 0;
     const int kb = kSplit ? (int)blockIdx.z : kOneK ? kone : 0, ke = (kSplit || kOneK) ? kb + 1 : 3;
+#ifdef NUSI_BATCH_TRACE
+    int bt_i = 0;
+#endif
 #pragma unroll 1
     for (int k = kb; k < ke; ++k) {
+        NUSI_BT();
         __syncthreads();   // the previous k's points are done with P3, X, mem, edgk, membq
         if (tid < mjobs) alpha_tile_edge_job_k(P, k, tid, tE, ct, sE, cs, g.lo, g.hi, m0, Tm, edgk);
         __syncthreads();
+        NUSI_BT();
         // ---- the batch's shared leaves and brackets of mass state k
         AlphaPre pre{};
         PPTerm ppt{0.0, 1.0, 1.0};
@@ -662,6 +684,7 @@ void k_alpha_batch(GridDev g, const Point* __restrict__ pts, const SplineSet* __
             for (int j = tid; j < kAlphaTile * (cs + ct); j += kTileThreads)
                 alpha_batch_mixed_job(j, edgk, ct, cs, tl, th, sl, sh, n0, m0, T, Tm, mix, mix + kAlphaTile * cs);
             __syncthreads();
+            NUSI_BT();
             if (needed) {
                 pre = b_pre(P, k, g.lo[n], g.hi[n], g.lo[m], g.hi[m], P3, tmp, mix, edgk, cs, ct, lm, ln, sl[lm], sh[lm],
                             tl[ln], th[ln]);
@@ -672,6 +695,7 @@ void k_alpha_batch(GridDev g, const Point* __restrict__ pts, const SplineSet* __
                 }
             }
             __syncthreads();   // X is rewritten with the member coefficients (kRef: with the member corners)
+            NUSI_BT();
             if (!kRef)
                 for (int j = tid; j < cc; j += kTileThreads) b_xshared(j, edgk, ct, cs, X);
         }
@@ -707,6 +731,7 @@ void k_alpha_batch(GridDev g, const Point* __restrict__ pts, const SplineSet* __
         for (int q0 = 0; q0 < nb; q0 += kBatchQC) {
             const int nq = (nb - q0 < kBatchQC) ? nb - q0 : kBatchQC;
             __syncthreads();   // the previous chunk is done with membq (and mem)
+            NUSI_BT();
             if (mq < nq) {
                 MedVals mv{};
                 alpha_batch_medge_load(nonres, mjob, tsrc, ct, ssrc, cs, m0, Tm, T,
@@ -726,6 +751,7 @@ void k_alpha_batch(GridDev g, const Point* __restrict__ pts, const SplineSet* __
                                                             : alpha_member_ref_arg(S, t, pts[p0 + q0 + qq].a_gr);
             }
             constexpr bool pipe = kBatchPipe && !kRef;
+            NUSI_BT();
             if (pipe) {
                 __syncthreads();   // member edges written
                 if (cornered)
@@ -749,6 +775,7 @@ void k_alpha_batch(GridDev g, const Point* __restrict__ pts, const SplineSet* __
                                                     mem + ((qq + 1) & 1) * 2 * ccmax);
                 } else {
                     __syncthreads();   // member edges written / the previous point's combine is done with mem
+                    NUSI_BT();
                     if (cornered) {
                         if (kRef) {
                             if (moff >= 0) {
@@ -762,6 +789,7 @@ void k_alpha_batch(GridDev g, const Point* __restrict__ pts, const SplineSet* __
                             for (int j = tid; j < cc; j += kTileThreads) alpha_batch_mcorner_job(Q, j, edgk, ct, cs, X, memb, mem);
                     }
                     __syncthreads();   // mem of q written
+                    NUSI_BT();
                 }
                 int w = 0;
                 TermRec rec;
@@ -792,6 +820,7 @@ void k_alpha_batch(GridDev g, const Point* __restrict__ pts, const SplineSet* __
                     }
                 } else if (valid) A[(size_t)(p0 + q) * g.PT + eidx] = needed ? tot : 0.0;
                 if (w) warn_entry(warn, wmin, T, p0 + q, w, n, m);
+                NUSI_BT();
             }
         }
     }
@@ -1100,3 +1129,12 @@ hipError_t launch_alpha(const GridDev& g, const Point* pts, int npts, const Spli
 }
 
 }  // namespace nusi
+
+#ifdef NUSI_BATCH_TRACE
+// diagnostic build: the batch kernel's phase stamps of the latest launch, [workgroup][wave][stamp]
+extern "C" int nusi_debug_batch_trace(unsigned long long* out, int n)
+{
+    const int m = n < nusi::kBtWg * 4 * nusi::kBtN ? n : nusi::kBtWg * 4 * nusi::kBtN;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(nusi::g_bt), sizeof(unsigned long long) * m) == hipSuccess ? 0 : -5;
+}
+#endif
