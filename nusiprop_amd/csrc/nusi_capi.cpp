@@ -618,43 +618,7 @@ constexpr bool kGaPre = NUSI_GA_PRE != 0;
 constexpr int kOverlapTables = 16;   // calls of at most this many tables overlap Gamma / alphaTilde with alpha
 constexpr size_t kStageBytes = size_t(4) << 20;   // nusi_plan_evolve_host's pinned output staging, at most
 constexpr int kSplitTables = 2;   // calls of at most this many tables (no phi-phi) run the k-split alpha path
-int mcorner_block_ensure(nusi_plan* p, int ntab, const AlphaBatches& ab, int budget_mb);
-// the shared corner leaves' block (MCornerDev::sc, k_alpha_scorner): room for the most batches a chunk of this call
-// holds (launch_alpha's grouping), 0.5 MB per batch and mass state at N_E = 300; past kScBudget none, and the batch
-// kernel forms the leaves itself (the same bits either way)
-constexpr size_t kScBudget = (size_t)4 << 30;
-int scorner_ensure(nusi_plan* p, const AlphaBatches& ab)
-{
-    nusi::MCornerDev& mc = p->mc;
-    int maxb = 0;
-    for (int b = 0; b < ab.nbatch;) {
-        const int lim = b < ab.nb_plain ? ab.nb_plain : ab.nbatch;
-        int e = b, ntb = 0;
-        while (e < lim) {
-            const int nbe = (int)((unsigned)p->h_batches[e] >> 24);
-            if (e > b && ntb + nbe > mc.cap_tables) break;
-            ntb += nbe;
-            ++e;
-        }
-        maxb = std::max(maxb, e - b);
-        b = e;
-    }
-    if (maxb <= mc.sc_batches) return NUSI_OK;
-    hipFree(mc.sc);
-    mc.sc = nullptr;
-    mc.sc_batches = 0;
-    const size_t bytes = sizeof(double) * nusi::scorner_doubles(mc.NC, maxb);
-    if (bytes > kScBudget) return NUSI_OK;
-    HIPCHECK(hipMalloc(&mc.sc, bytes));
-    mc.sc_batches = maxb;
-    return NUSI_OK;
-}
 int mcorner_ensure(nusi_plan* p, int ntab, const AlphaBatches& ab, int budget_mb)
-{
-    if (int r = mcorner_block_ensure(p, ntab, ab, budget_mb)) return r;
-    return scorner_ensure(p, ab);
-}
-int mcorner_block_ensure(nusi_plan* p, int ntab, const AlphaBatches& ab, int budget_mb)
 {
     nusi::MCornerDev& mc = p->mc;
     if (!mc.eu) {
@@ -880,7 +844,6 @@ void nusi_plan_destroy(nusi_plan* pl)
     hipFree(pl->mc.buf);
     hipFree(pl->mc.eu);
     hipFree(pl->mc.ue);
-    hipFree(pl->mc.sc);
     hipFree(pl->d_scratch);
     hipFree(pl->d_kt);
     hipFree(pl->d_gpre);

@@ -69,13 +69,10 @@ struct MCornerDev {
     double* ue = nullptr;    // [U]: the energy of each edge
     long long NC = 0;
     int U = 0, cap_tables = 0;
-    double* sc = nullptr;   // the batches' shared corner leaves [batch of the chunk][3][NC][kScFields] (k_alpha_scorner), or
-    int sc_batches = 0;     // nullptr (the batch kernel forms them itself); room for sc_batches batches
 };
 // ref: NUSI_OPT_REFERENCE_ORDER (the kernels' kRef instances: the reference's own operation order for the complex
 // dilogarithms and the s-t interference member leaves, bit-identical to the oracle's ora_set_reference_order(1))
 size_t gamma_alphat_pre_doubles(int T, int npts);   // TablesDev::Gpre's size
-size_t scorner_doubles(long long NC, int nbatch);      // MCornerDev::sc's size for nbatch batches
 hipError_t launch_gamma_alphat(const GridDev& g, const Point* pts, int npts, const SplineSet* spl, TablesDev t,
                                int* warn, hipStream_t s, bool ref);
 // batches: device [nbatches] of first table | count << 24 (count <= gmax), tables of a batch sharing
