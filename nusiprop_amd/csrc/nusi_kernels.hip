@@ -427,10 +427,6 @@ constexpr bool kBatchPipe = NUSI_BATCH_PIPE != 0;
 #define NUSI_REFO_PREFETCH 1
 #endif
 constexpr bool kRefPrefetch = NUSI_REFO_PREFETCH != 0;
-#ifndef NUSI_REFO_ARGN   // A/B: 0 = the chunk's A point by point (alpha_member_ref_arg in a loop)
-#define NUSI_REFO_ARGN 1
-#endif
-constexpr bool kRefArgN = NUSI_REFO_ARGN != 0;
 #ifndef NUSI_BATCH_KLAUNCH   // A/B: 1 = the non-phi-phi batch kernels as one launch per mass state (kOneK)
 #define NUSI_BATCH_KLAUNCH 0
 #endif
@@ -475,18 +471,6 @@ NUSI_BCOLD void b_corner(int j, const double* edgk, int ct, int cs, double* per,
 }
 // (kRef, kPP) A of a member corner, out of line (the phi-phi instance's point loop spills more with it inline)
 NUSI_BCOLD double b_marg(double S, double t, double gr) { return alpha_member_ref_arg(S, t, gr); }
-// (kRef, no phi-phi) A of this work-item's corner for the chunk's nq points at once (alpha_member_ref_arg_n), into
-// x[qq kCC]; out of line, so that the straight-line block's registers do not shape the point loop's allocation
-NUSI_BCOLD void b_marg_chunk(double S, double t, const Point* q, int nq, double* x)
-{
-    double grq[kBatchQC], Aq[kBatchQC];
-#pragma unroll
-    for (int qq = 0; qq < kBatchQC; ++qq) grq[qq] = q[qq < nq ? qq : nq - 1].a_gr;
-    alpha_member_ref_arg_n<kBatchQC>(S, t, grq, Aq);
-#pragma unroll
-    for (int qq = 0; qq < kBatchQC; ++qq)
-        if (qq < nq) x[qq * kCC] = Aq[qq];
-}
 NUSI_BCOLD void b_xshared(int j, const double* edgk, int ct, int cs, double* X) { alpha_batch_xshared_job(j, edgk, ct, cs, X); }
 // The leaves the batch's shared brackets read (alpha_k_pre, alpha_k_pp): the shared corner blocks P3 | tmp, the
 // edge block edgk and the mixed logs; no member leaf
@@ -760,14 +744,11 @@ void k_alpha_batch(GridDev g, const Point* __restrict__ pts, const SplineSet* __
             if (kRef && moff >= 0) {
                 const int si = tid / ct, ti = tid - si * ct;
                 const double S = edgk[kTEdgeFields * ct + kSEdgeVal * cs + si], t = edgk[kTEdgeVal * ct + ti];
-if (kPP || !kRefArgN) {
 #pragma unroll 1
-                    for (int qq = 0; qq < nq; ++qq)   // (inline: C4 7.42 -> 7.28 ms, r6p; kPP, whose point loop holds
-                        X[(3 + qq) * kCC + tid] =     // the phi-phi term too, as a call: C3 12.33 -> 11.24 ms, r6q)
-                            (NUSI_REFO_BSTUB & 4) ? S + t : kPP ? b_marg(S, t, pts[p0 + q0 + qq].a_gr)
-                                                                : alpha_member_ref_arg(S, t, pts[p0 + q0 + qq].a_gr);
-                } else   // the chunk's points at once, straight-line, out of line (its registers its own)
-                    b_marg_chunk(S, t, pts + p0 + q0, nq, X + 3 * kCC + tid);
+                for (int qq = 0; qq < nq; ++qq)   // (inline: C4 7.42 -> 7.28 ms, r6p; kPP, whose point loop holds
+                    X[(3 + qq) * kCC + tid] =     // the phi-phi term too, as a call: C3 12.33 -> 11.24 ms, r6q)
+                        (NUSI_REFO_BSTUB & 4) ? S + t : kPP ? b_marg(S, t, pts[p0 + q0 + qq].a_gr)
+                                                            : alpha_member_ref_arg(S, t, pts[p0 + q0 + qq].a_gr);
             }
             constexpr bool pipe = kBatchPipe && !kRef;
             NUSI_BT();

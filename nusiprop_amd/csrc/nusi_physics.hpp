@@ -756,34 +756,6 @@ NUSI_FN double alpha_member_ref_arg(double S, double t, double gr)
 {
     return carg_i(-(C(-1 + S, gr) / C(2 + t, -gr)));   // (atan2 inline)
 }
-// alpha_member_ref_arg of one corner (S, t) for N couplings gr[0..N-1] at once (the batch kernel's chunk of points):
-// the same operations on the same operands -- the quotient's two Smith cases (operator/(cd, cd)) by operand selects
-// and atan2's common path voted once for all N -- as straight-line code, so that the N evaluations interleave
-template <int N>
-NUSI_FN void alpha_member_ref_arg_n(double S, double t, const double* gr, double* A)
-{
-    double y[N], x[N];
-    bool plain = true;
-#pragma unroll
-    for (int i = 0; i < N; ++i) {
-        const double ar = -1 + S, ai = gr[i], c = 2 + t, d = -gr[i];
-        const bool sw = fabs(c) < fabs(d);   // Smith: ratio = c / d, else d / c
-        const double num = sw ? c : d, dvs = sw ? d : c, u = sw ? ar : ai, v = sw ? ai : ar;
-        const double ratio = num / dvs, den = (num * ratio) + dvs;
-        const double vr = v * ratio;
-        const double re = ((u * ratio) + v) / den, im = (sw ? vr - ar : ai - vr) / den;
-        y[i] = -im;   // carg(-(quotient))
-        x[i] = -re;
-        plain = plain && nm::atan2_plain(y[i], x[i]);
-    }
-    if (nm::wave_all_l(plain)) {
-#pragma unroll
-        for (int i = 0; i < N; ++i) A[i] = nm::atan2_sel(y[i], x[i]);
-    } else {
-#pragma unroll
-        for (int i = 0; i < N; ++i) A[i] = nm::atan2_i(y[i], x[i]);
-    }
-}
 NUSI_FN void alpha_member_ref(double S, double t, double gr, double& Dcr, double& Dci, double& A)
 {
     if (NUSI_REFO_STUB == 2) { Dcr = Dci = A = 0.0; return; }

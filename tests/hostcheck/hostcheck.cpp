@@ -148,15 +148,6 @@ static int ga_pre_t(const double* pt, const int* flags, int T, const double* lo,
 }
 
 extern "C" {
-// alpha_member_ref_arg_n (the batch kernel's chunk of points at once) against alpha_member_ref_arg point by point:
-// out[2 i] / out[2 i + 1], n corners of 5 couplings each (S[i], t[i], gr[5 i ..])
-void hc_member_arg_n(int n, const double* S, const double* t, const double* gr, double* out_n, double* out_1)
-{
-    for (int i = 0; i < n; ++i) {
-        nusi::alpha_member_ref_arg_n<5>(S[i], t[i], gr + 5 * i, out_n + 5 * i);
-        for (int j = 0; j < 5; ++j) out_1[5 * i + j] = nusi::alpha_member_ref_arg(S[i], t[i], gr[5 * i + j]);
-    }
-}
 int hc_ga_pre(const double* pt, const int* flags, int T, const double* lo, const double* hi, double* G, double* At)
 {
     return ga_pre_t(pt, flags, T, lo, hi, G, At);

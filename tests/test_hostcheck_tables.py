@@ -168,22 +168,3 @@ def test_ga_dilogs_prepass_bit_identical(oracle_mod, name):
     H.hc_ga_pre(_dp(pt), flags, T, _dp(lo), _dp(hi), _dp(Gh), _dp(aTh))
     assert np.array_equal(Gh, G), "Gamma differs at %s" % np.flatnonzero(Gh != G)[:5]
     assert np.array_equal(aTh, aT), "alphaTilde differs at %s" % np.flatnonzero(aTh != aT)[:5]
-
-
-def test_member_arg_chunk_form_bit_identical():
-    """The batch kernel's chunk of member-corner arguments at once (alpha_member_ref_arg_n: Smith's two cases by operand
-    selects, atan2's common path voted once for the chunk) against alpha_member_ref_arg point by point, bit for bit:
-    random (S', t, gr) over the scan's ranges, both Smith cases (|2 + t| below and above gr) and the atan2 edge
-    cases (x = 1 exactly is out of reach here; y, x of every sign)."""
-    from tests.hostcheck import build_hostcheck
-    H = build_hostcheck()
-    rng = np.random.default_rng(7)
-    n = 40000
-    S = np.concatenate([10 ** rng.uniform(-8, 8, n // 2), rng.uniform(0, 3, n // 2)])
-    t = np.concatenate([-(10 ** rng.uniform(-8, 8, n // 2)), -2 + rng.uniform(-0.05, 0.05, n // 2)])
-    gr = 10 ** rng.uniform(-12, -0.5, 5 * n)
-    on, o1 = np.zeros(5 * n), np.zeros(5 * n)
-    H.hc_member_arg_n(ctypes.c_int(n), _dp(S), _dp(t), _dp(gr), _dp(on), _dp(o1))
-    assert np.array_equal(on.view(np.uint64), o1.view(np.uint64))
-    sw = np.abs(2 + np.repeat(t, 5)) < gr
-    assert sw.sum() > 100 and (~sw).sum() > 100   # both Smith cases reached
