@@ -354,7 +354,11 @@ NUSI_FN void cseries_t(bool s2, double r, double lr, double x, double y, double&
     double q = 0.0, dr = 0.0, di = 0.0;
     auto term = [&](int k) {
         const KRow kr = next;
+#ifdef NUSI_GSL_ROW_STUB   // timing A/B only (wrong values): every term reads row 2 (no table load in the loop)
+        (void)k;
+#else
         next = kKT.row[k + 1];
+#endif
         const double ck_tmp = ck;
         ck = ck - (alpha * ck + beta * sk);
         sk = sk - (alpha * sk - beta * ck_tmp);
