@@ -87,15 +87,6 @@ constexpr KTab make_ktab()
     return t;
 }
 constexpr KTab kKT = make_ktab();
-// The series' reciprocals alone, for an LDS copy (kernels of few tables, where one lane's series is the critical path:
-// a term's table row from L2 is a scalar load whose latency a lone wave cannot hide, an LDS row one term ahead is):
-// d1, d2 are formed from k instead, by the table's own expressions (exact)
-struct KRowY { double y1, y2, l1, l2; };
-constexpr int kKRowY = 1000;
-NUSI_FN void krowy_fill(KRowY* t, int tid, int nthreads)
-{
-    for (int k = tid; k < kKRowY; k += nthreads) t[k] = KRowY{kKT.row[k].y1, kKT.row[k].y2, kKT.row[k].l1, kKT.row[k].l2};
-}
 
 // RN(a / d) for the series' terms.  kExact: the division; else fma(a, y, RN(a l)) from the two-part reciprocal
 // y + l (header comment), valid for a, d > 0 with a l normal (a >= 2^-900) -- the callers take kExact for arguments
@@ -348,8 +339,8 @@ NUSI_FN_OUT double clausen(double x)
 // sk^2)^(1/2) with q = RN(r^k / d_k) and the rotated (ck, sk) of modulus 1 to ~1e-13 (<= 1000 rotations); so while q
 // >= 2^-50 r (2.4 times the bound's 1.645 2^-52 r) the test is false, and the loop runs without it until the first
 // term below, whose test is GSL's test at that k (the values are unchanged: the same terms, the same break).
-template <bool kExact, int kS2, bool kL = false>   // kL: the reciprocals from an LDS copy ly (krowy_fill)
-NUSI_FN void cseries_t(bool s2, double r, double lr, double x, double y, double& re, double& im, const KRowY* ly = nullptr)
+template <bool kExact, int kS2>
+NUSI_FN void cseries_t(bool s2, double r, double lr, double x, double y, double& re, double& im)
 {
     const bool t2 = kS2 == 2 ? s2 : kS2 == 1;
     const double cos_theta = x / r, sin_theta = y / r;
@@ -360,32 +351,20 @@ NUSI_FN void cseries_t(bool s2, double r, double lr, double x, double y, double&
     const double nlr = -lr;   // -log(r)
     const int kmax = t2 ? 30 + (int)(18.0 / nlr) : 50 + (int)(22.0 / nlr);
     KRow next = kKT.row[2];   // (the table row of the next iteration is loaded one iteration ahead; kmax <= 921)
-    KRowY nexty = kL ? ly[2] : KRowY{};
     double q = 0.0, dr = 0.0, di = 0.0;
     auto term = [&](int k) {
-        double d, yk, lk;
-        if (kL) {
-            const KRowY kr = nexty;
-            nexty = ly[k + 1];
-            const double d1 = (double)k * k;
-            d = t2 ? d1 * (k + 1.0) : d1;   // the table's (double) k * k * (k + 1.0) or (double) k * k
-            yk = t2 ? kr.y2 : kr.y1;
-            lk = t2 ? kr.l2 : kr.l1;
-        } else {
-            const KRow kr = next;
+        const KRow kr = next;
 #ifdef NUSI_GSL_ROW_STUB   // timing A/B only (wrong values): every term reads row 2 (no table load in the loop)
-            (void)k;
+        (void)k;
 #else
-            next = kKT.row[k + 1];
+        next = kKT.row[k + 1];
 #endif
-            d = t2 ? kr.d2 : kr.d1;   // (double) k * k * (k + 1.0) or (double) k * k
-            yk = t2 ? kr.y2 : kr.y1;
-            lk = t2 ? kr.l2 : kr.l1;
-        }
         const double ck_tmp = ck;
         ck = ck - (alpha * ck + beta * sk);
         sk = sk - (alpha * sk - beta * ck_tmp);
         rk *= r;
+        const double d = t2 ? kr.d2 : kr.d1;   // (double) k * k * (k + 1.0) or (double) k * k
+        const double yk = t2 ? kr.y2 : kr.y1, lk = t2 ? kr.l2 : kr.l1;
         q = div_k<kExact>(rk, d, yk, lk);
         dr = q * ck;
         di = q * sk;
@@ -441,20 +420,19 @@ NUSI_FN void cseries_t(bool s2, double r, double lr, double x, double y, double&
 }
 // (the terms r^k stay above 2^-960 and |sum|^2 above 2^-900 unless r < 2^-400: the series breaks at a term
 // below 2^-52 of the sum, and kmax bounds r^k for larger r)
-template <bool kL = false>
-NUSI_FN void cseries(bool s2, double r, double lr, double x, double y, double& re, double& im, const KRowY* ly = nullptr)
+NUSI_FN void cseries(bool s2, double r, double lr, double x, double y, double& re, double& im)
 {
     if (r < 0x1p-400) {
-        cseries_t<true, 2, kL>(s2, r, lr, x, y, re, im, ly);
+        cseries_t<true, 2>(s2, r, lr, x, y, re, im);
         return;
     }
 #ifdef __HIP_DEVICE_COMPILE__
     const unsigned long long act = __ballot(1), two = __ballot(s2);
-    if (two == act) cseries_t<false, 1, kL>(s2, r, lr, x, y, re, im, ly);
-    else if (two == 0) cseries_t<false, 0, kL>(s2, r, lr, x, y, re, im, ly);
-    else cseries_t<false, 2, kL>(s2, r, lr, x, y, re, im, ly);
+    if (two == act) cseries_t<false, 1>(s2, r, lr, x, y, re, im);
+    else if (two == 0) cseries_t<false, 0>(s2, r, lr, x, y, re, im);
+    else cseries_t<false, 2>(s2, r, lr, x, y, re, im);
 #else
-    cseries_t<false, 2, kL>(s2, r, lr, x, y, re, im, ly);
+    cseries_t<false, 2>(s2, r, lr, x, y, re, im);
 #endif
 }
 // dilogc_series_3: |z| near 1, sum_{n <= 6} (log r)^n / n! H_n(theta)
@@ -494,8 +472,7 @@ NUSI_FN void cseries_3(double r, double lr, double x, double y, double& re, doub
 // dilogc_fundamental (r < 1, x <= 0.732): series_3 above r = 0.98, dilogc_series_2 above 0.25, else series_1.  Every
 // branch takes log(r) (series_3's expansion variable, the series' kmax): formed once, and returned in lr for
 // unitdisk's log(1 - z) of a reflected argument (the same call on the same value)
-template <bool kL = false>
-NUSI_FN cd fundamental_body(double r, double x, double y, double& lr, const KRowY* ly = nullptr)
+NUSI_FN cd fundamental_body(double r, double x, double y, double& lr)
 {
     double re, im;
     lr = GSL_LOG(r);
@@ -504,7 +481,7 @@ NUSI_FN cd fundamental_body(double r, double x, double y, double& lr, const KRow
         return cd{re, im};
     }
     const bool s2 = r > 0.25;
-    cseries<kL>(s2, r, lr, x, y, re, im, ly);
+    cseries(s2, r, lr, x, y, re, im);
     if (!s2) return cd{re, im};
     // dilogc_series_2: + (1 - z) log(1 - z) / z + 1, log(1 - z) by gsl_sf_complex_log_e
     const double zr = 1.0 - x, zi = -y;
@@ -518,11 +495,11 @@ NUSI_FN cd fundamental_body(double r, double x, double y, double& lr, const KRow
     const double r_y = (1.0 - x) * t_y - y * t_x;
     return cd{re + r_x + 1.0, im + r_y};
 }
-NUSI_FN_OUT cd fundamental(double r, double x, double y, double& lr) { return fundamental_body<false>(r, x, y, lr); }
+NUSI_FN_OUT cd fundamental(double r, double x, double y, double& lr) { return fundamental_body(r, x, y, lr); }
 // dilogc_unitdisk: |z| < 1; x > 0.732 reflected, Li2(z) = -Li2(1 - z) + zeta2 - log(z) log(1 - z).  kInl: fundamental
 // inline (the member-corner kernel's single call site, gsl_cli2_inl), else the out-of-line instance
-template <bool kInl = false, bool kL = false>   // kL (inline only): the series' reciprocals from ly
-NUSI_FN cd unitdisk(double x, double y, const KRowY* ly = nullptr)
+template <bool kInl = false>
+NUSI_FN cd unitdisk(double x, double y)
 {
     const double zeta2 = kPiD * kPiD / 6.0;
     const bool refl = x > 0.732;
@@ -532,7 +509,7 @@ NUSI_FN cd unitdisk(double x, double y, const KRowY* ly = nullptr)
     const double fx = refl ? x_tmp : x, fy = refl ? y_tmp : y;
     const double rf = gsl::hypot(fx, fy);
     double lr;
-    const cd f = kInl ? fundamental_body<kL>(rf, fx, fy, lr, ly) : fundamental(rf, fx, fy, lr);   // one call site
+    const cd f = kInl ? fundamental_body(rf, fx, fy, lr) : fundamental(rf, fx, fy, lr);   // one call site
     if (!refl) return f;
     const double r = gsl::hypot(x, y);
     const double lnz = GSL_LOG(r), lnomz = lr;   // log(r_tmp)
@@ -575,8 +552,8 @@ NUSI_FN cd gsl_cli2_real(double x) { return cd{gsl_li2(x), (x >= 1.0) ? -gsl::kP
 // whole call inline -- the member-corner kernel's one call site, where the call boundaries' argument moves, SGPR
 // lane spills and callee-saved register traffic were VALU work of their own; gsl_cli2 the out-of-line instance the
 // table kernels call from many sites
-template <bool kInl, bool kL = false>
-NUSI_FN cd gsl_cli2_t(double x, double y, const gsl::KRowY* ly = nullptr)
+template <bool kInl>
+NUSI_FN cd gsl_cli2_t(double x, double y)
 {
     const double zeta2 = gsl::kPiD * gsl::kPiD / 6.0;
     const double r2 = x * x + y * y;
@@ -587,7 +564,7 @@ NUSI_FN cd gsl_cli2_t(double x, double y, const gsl::KRowY* ly = nullptr)
         return cd{zeta2 + term1 - term2, gsl::clausen(theta)};
     }
     const bool inv = !(r2 < 1.0);
-    const cd u = gsl::unitdisk<kInl, kL>(inv ? x / r2 : x, inv ? -y / r2 : y, ly);   // one instance
+    const cd u = gsl::unitdisk<kInl>(inv ? x / r2 : x, inv ? -y / r2 : y);   // one instance
     if (!inv) return u;
     const double r = sqrt(r2);
     const double theta = GSL_ATAN2(y, x), theta_abs = fabs(theta), theta_sgn = (theta < 0.0 ? -1.0 : 1.0);
@@ -598,8 +575,6 @@ NUSI_FN cd gsl_cli2_t(double x, double y, const gsl::KRowY* ly = nullptr)
 }
 
 NUSI_FN_OUT cd gsl_cli2(double x, double y) { return gsl_cli2_t<false>(x, y); }
-// inline, the series' reciprocals from an LDS copy (gsl::krowy_fill): kernels of few tables
-NUSI_FN cd gsl_cli2_lds(double x, double y, const gsl::KRowY* ly) { return gsl_cli2_t<true, true>(x, y, ly); }
 #ifndef NUSI_MC_CALL   // (A/B: the member-corner kernel's GSL call out of line, as before round 6)
 NUSI_FN cd gsl_cli2_inl(double x, double y) { return gsl_cli2_t<true>(x, y); }
 #else

@@ -208,10 +208,6 @@ void k_alpha(GridDev g, const Point* __restrict__ pts, const SplineSet* __restri
     if (w) warn_entry(warn, wmin, g.T, p, w, n, m);
 }
 
-#ifndef NUSI_LDS_ROWS   // A/B: 0 = the few-table kernels' GSL series read their reciprocals from the global table
-#define NUSI_LDS_ROWS 1
-#endif
-constexpr bool kGaLdsRows = NUSI_LDS_ROWS != 0;
 // Calls of few tables in the reference order: every GSL dilogarithm of Gamma / alphaTilde, one per work-item
 // (ga_pre_slot; grid (bins / 64, points, 3 mass states x kGaPreSlots)) into pre [point][k][kGaPreFields][T], before
 // k_gamma_alphat<true, 2, true> combines them: a lane no longer walks its bin's six GSL series one after the other
@@ -219,17 +215,12 @@ __global__ __launch_bounds__(64) void k_ga_dilogs(GridDev g, const Point* __rest
 {
     const int n = blockIdx.x * 64 + threadIdx.x, p = blockIdx.y, T = g.T;
     const int k = blockIdx.z / kGaPreSlots, slot = blockIdx.z - k * kGaPreSlots;   // (wave-uniform slot)
+    if (n >= T) return;
     const Point& P = pts[p];
     if (!P.non_resonant) return;   // (gamma_k / alphat_k return before any dilogarithm)
-    __shared__ gsl::KRowY ly[kGaLdsRows ? gsl::kKRowY : 1];   // (the complex series' reciprocals, one term ahead)
-    if (kGaLdsRows) {
-        gsl::krowy_fill(ly, threadIdx.x, 64);
-        __syncthreads();
-    }
-    if (n >= T) return;
     double v[2];
     int f;
-    const int nv = ga_pre_slot<kGaLdsRows>(P, k, g.lo[n], g.hi[n], slot, v, &f, ly);
+    const int nv = ga_pre_slot(P, k, g.lo[n], g.hi[n], slot, v, &f);
     double* o = pre + ((size_t)(p * 3 + k) * kGaPreFields + f) * T + n;
     o[0] = v[0];
     if (nv == 2) o[T] = v[1];
@@ -531,9 +522,6 @@ constexpr int kMcJobs = 1024;
 #ifndef NUSI_MC_WAVES   // A/B: waves per SIMD the member-corner kernel is built for (0: the compiler's choice)
 #define NUSI_MC_WAVES 0
 #endif
-// kL (calls of few tables, one job per work-item): GSL's series read their reciprocals from an LDS copy (a lone
-// wave's series waits on each term's table row from L2 otherwise: the single-propagation critical path)
-template <bool kL = false>
 __global__ __launch_bounds__(256)
 #if NUSI_MC_WAVES
 __attribute__((amdgpu_waves_per_eu(NUSI_MC_WAVES, NUSI_MC_WAVES)))
@@ -541,11 +529,8 @@ __attribute__((amdgpu_waves_per_eu(NUSI_MC_WAVES, NUSI_MC_WAVES)))
 void k_alpha_mcorner(const Point* __restrict__ pts, const int* __restrict__ batches,
                                                        MCornerDev mc, int pc0, int jobs)
 {
-    constexpr int kJ = kL ? 256 : kMcJobs;
-    __shared__ double v[2 * kJ];   // [q][cl][Dcr, Dci]
-    __shared__ double cst[2][kJ];           // S', t of corner c0 + cl (shared by the batch's tables)
-    __shared__ gsl::KRowY ly[kL ? gsl::kKRowY : 1];
-    if (kL) gsl::krowy_fill(ly, threadIdx.x, 256);   // (before any return: the barrier below is the workgroup's)
+    __shared__ double v[2 * kMcJobs];   // [q][cl][Dcr, Dci]
+    __shared__ double cst[2][kMcJobs];           // S', t of corner c0 + cl (shared by the batch's tables)
     const int bw = batches[blockIdx.y], k = blockIdx.z, tid = threadIdx.x;
     const int p0 = bw & 0xffffff, nb = (int)((unsigned)bw >> 24);
     const Point& P = pts[p0];
@@ -560,7 +545,7 @@ void k_alpha_mcorner(const Point* __restrict__ pts, const int* __restrict__ batc
         const int cl = j / nb, q = j - cl * nb;
         if (c0 + cl >= mc.NC) break;
         const double S = cst[0][cl], t = cst[1][cl], gr = pts[p0 + q].a_gr;
-        const cd Dc = NUSI_REFO_STUB == 2 ? C(0.0) : kL ? alpha_member_ref_dc_lds(S, t, gr, ly) : alpha_member_ref_dc_inl(S, t, gr);
+        const cd Dc = NUSI_REFO_STUB == 2 ? C(0.0) : alpha_member_ref_dc_inl(S, t, gr);
         v[2 * (q * cb + cl)] = Dc.r;
         v[2 * (q * cb + cl) + 1] = Dc.i;
     }
@@ -1058,12 +1043,8 @@ static hipError_t launch_alpha_t(const GridDev& g, const Point* pts, int npts, c
                         const long long tot = mc->NC * 3 * ntb;
                         const int jobs = 256 * (int)std::max(1LL, std::min<long long>(kMcJobs / 256, tot / (2048 * 256)));
                         const int cbmin = jobs / nbmax;
-                        if (kGaLdsRows && jobs == 256)   // (one GSL call per work-item: the latency-bound calls)
-                            hipLaunchKernelGGL((k_alpha_mcorner<true>), dim3((unsigned)((mc->NC + cbmin - 1) / cbmin), e - b, 3),
-                                               dim3(256), 0, s, pts, batches + b, *mc, pc0, jobs);
-                        else
-                            hipLaunchKernelGGL((k_alpha_mcorner<false>), dim3((unsigned)((mc->NC + cbmin - 1) / cbmin), e - b, 3),
-                                               dim3(256), 0, s, pts, batches + b, *mc, pc0, jobs);
+                        hipLaunchKernelGGL(k_alpha_mcorner, dim3((unsigned)((mc->NC + cbmin - 1) / cbmin), e - b, 3),
+                                           dim3(256), 0, s, pts, batches + b, *mc, pc0, jobs);
                         if (split) {
                             hipLaunchKernelGGL((k_alpha_batch<false, true, true>), dim3(at.ncls[0], e - b, 3),
                                                dim3(kTileThreads), lds, s, g, pts, spl, at.tiles, batches + b, t.A, t.Med,

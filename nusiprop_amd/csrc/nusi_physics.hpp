@@ -210,8 +210,8 @@ NUSI_FN int alphat_warn(double as, double at, double au, double atu, double ast,
 struct GammaEdgeVals { double ls, l1s; cd cz, czc; };
 struct GammaEdgePair { GammaEdgeVals lo, hi; };
 constexpr unsigned kGeLs = 1, kGeL1s = 2, kGeCz = 4;
-template <bool kRef, bool kL = false>   // kL (reference order): GSL's complex series reading the LDS reciprocals ly
-NUSI_FN void gamma_edge_vals(const Point& P, int j, double E, unsigned need, GammaEdgeVals& v, const gsl::KRowY* ly = nullptr)
+template <bool kRef>
+NUSI_FN void gamma_edge_vals(const Point& P, int j, double E, unsigned need, GammaEdgeVals& v)
 {
     const double mphi = P.mphi, Ga = P.Ga, m2 = mphi * mphi, gr = Ga / mphi;
     const double s = 2 * P.mn[j] * E / m2;   // gamma_k's sp / sm
@@ -219,7 +219,7 @@ NUSI_FN void gamma_edge_vals(const Point& P, int j, double E, unsigned need, Gam
     if (need & kGeL1s) v.l1s = li2_t<kRef>(-1 - s);
     if (need & kGeCz) {
         const cd z = C(0.0, 1 + s) / C(gr, 2.0);
-        v.cz = kL ? gsl_cli2_lds(z.r, z.i, ly) : cli2_t<kRef>(z);
+        v.cz = cli2_t<kRef>(z);
         if (!kRef) v.czc = cli2_t<kRef>(conj(z));
     }
 }
@@ -343,16 +343,13 @@ NUSI_FN double alphat_t(double mk, double E, double m2)
     if (fabs(t + 1) < 1e-7) t += t * 1e-6;
     return t;
 }
-template <bool kRef, bool kL = false>
-NUSI_FN void alphat_edge_vals(const Point& P, int k, double E, unsigned need, AlphatEdgeVals& v, const gsl::KRowY* ly = nullptr)
+template <bool kRef>
+NUSI_FN void alphat_edge_vals(const Point& P, int k, double E, unsigned need, AlphatEdgeVals& v)
 {
     const double mphi = P.mphi, Ga = P.Ga, m2 = mphi * mphi, gr = Ga / mphi;
     const double t = alphat_t(P.mn[k], E, m2);
     if (need & kAe78) v.e78 = cli2_t<kRef>(C(1 - t));
-    if (need & kAe51) {
-        const cd z = C(0.0, 1 - t) / C(gr, 2.0);
-        v.e51 = kL ? gsl_cli2_lds(z.r, z.i, ly) : cli2_t<kRef>(z);
-    }
+    if (need & kAe51) v.e51 = cli2_t<kRef>(C(0.0, 1 - t) / C(gr, 2.0));
     if (need & kAe1o) v.e1o = li2_t<kRef>(1 / (1 - t));
     if (need & kAe1p) v.e1p = li2_t<kRef>(1 + t);
 }
@@ -557,13 +554,12 @@ NUSI_FN double alphat_entry(const Point& P, const SplineSet& spl, double Em, dou
 // Values no branch of the bin reads are evaluated too (and not read).  v[0], v[1] at field *f (v[1]: complex only);
 // returns the count.
 constexpr int kGaPreSlots = 22, kGaPreFields = 32;
-template <bool kL = false>   // kL: the complex series' reciprocals from the LDS copy ly
-NUSI_FN int ga_pre_slot(const Point& P, int k, double Em, double Ep, int slot, double* v, int* f, const gsl::KRowY* ly = nullptr)
+NUSI_FN int ga_pre_slot(const Point& P, int k, double Em, double Ep, int slot, double* v, int* f)
 {
     if (slot < 6) {   // Gamma's edge values (reference order: no conj z value)
         const int side = slot / 3, which = slot - 3 * side;
         GammaEdgeVals e{};
-        gamma_edge_vals<true, kL>(P, k, side ? Ep : Em, which == 0 ? kGeLs : which == 1 ? kGeL1s : kGeCz, e, ly);
+        gamma_edge_vals<true>(P, k, side ? Ep : Em, which == 0 ? kGeLs : which == 1 ? kGeL1s : kGeCz, e);
         *f = 4 * side + which;
         if (which == 0) { v[0] = e.ls; return 1; }
         if (which == 1) { v[0] = e.l1s; return 1; }
@@ -573,7 +569,7 @@ NUSI_FN int ga_pre_slot(const Point& P, int k, double Em, double Ep, int slot, d
     if (slot < 14) {   // alphaTilde's edge values
         const int side = (slot - 6) / 4, which = slot - 6 - 4 * side;
         AlphatEdgeVals e{};
-        alphat_edge_vals<true, kL>(P, k, side ? Ep : Em, which == 0 ? kAe78 : which == 1 ? kAe51 : which == 2 ? kAe1o : kAe1p, e, ly);
+        alphat_edge_vals<true>(P, k, side ? Ep : Em, which == 0 ? kAe78 : which == 1 ? kAe51 : which == 2 ? kAe1o : kAe1p, e);
         const int f0 = 8 + 6 * side;
         if (which == 0) { *f = f0; v[0] = e.e78.r; v[1] = e.e78.i; return 2; }
         if (which == 1) { *f = f0 + 2; v[0] = e.e51.r; v[1] = e.e51.i; return 2; }
@@ -594,7 +590,7 @@ NUSI_FN int ga_pre_slot(const Point& P, int k, double Em, double Ep, int slot, d
         else if (b == 1) z = C(1 - tp / (1 + tm));
         else if (b == 2) z = (1 + tm - tp) / dt_m;
         else z = 1 / dt_m;
-        const cd d = (kL && b >= 2) ? gsl_cli2_lds(z.r, z.i, ly) : cli2_t<true>(z);   // (d26's are real-axis calls)
+        const cd d = cli2_t<true>(z);
         *f = 20 + 2 * b;
         v[0] = d.r; v[1] = d.i;
         return 2;
@@ -755,12 +751,6 @@ NUSI_FN cd alpha_member_ref_dc_inl(double S, double t, double gr)
 {
     const cd z = (1 + S + t) / C(2 + t, -gr);
     return NUSI_REFO_STUB == 1 ? z : gsl_cli2_inl(z.r, z.i);
-}
-// the same, GSL's series reading the LDS reciprocals ly (k_alpha_mcorner's instance for calls of few tables)
-NUSI_FN cd alpha_member_ref_dc_lds(double S, double t, double gr, const gsl::KRowY* ly)
-{
-    const cd z = (1 + S + t) / C(2 + t, -gr);
-    return NUSI_REFO_STUB == 1 ? z : gsl_cli2_lds(z.r, z.i, ly);
 }
 NUSI_FN double alpha_member_ref_arg(double S, double t, double gr)
 {

@@ -148,18 +148,6 @@ static int ga_pre_t(const double* pt, const int* flags, int T, const double* lo,
 }
 
 extern "C" {
-// GSL's complex dilogarithm with the series' reciprocals from a copy of the table (gsl_cli2_lds, the few-table kernels'
-// LDS instance, d1 and d2 formed from k) against gsl_cli2, on n points
-void hc_cli2_lds(int n, const double* x, const double* y, double* out_l, double* out_g)
-{
-    static nusi::gsl::KRowY tab[nusi::gsl::kKRowY];
-    nusi::gsl::krowy_fill(tab, 0, 1);
-    for (int i = 0; i < n; ++i) {
-        const nusi::cd a = nusi::gsl_cli2_lds(x[i], y[i], tab), b = nusi::gsl_cli2(x[i], y[i]);
-        out_l[2 * i] = a.r; out_l[2 * i + 1] = a.i;
-        out_g[2 * i] = b.r; out_g[2 * i + 1] = b.i;
-    }
-}
 int hc_ga_pre(const double* pt, const int* flags, int T, const double* lo, const double* hi, double* G, double* At)
 {
     return ga_pre_t(pt, flags, T, lo, hi, G, At);

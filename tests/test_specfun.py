@@ -283,19 +283,3 @@ def test_device_atan2_select_path_bit_identical(olib, hlib):
         same = (a == c or (a != a and c != c)) and np.signbit(a) == np.signbit(c) and (b == c or (b != b and c != c))
         bad += not same
     assert bad == 0, bad
-
-
-def test_gsl_cli2_lds_rows_bit_identical(hlib):
-    """The few-table kernels' GSL complex dilogarithm (gsl_cli2_lds: the series' reciprocals from an LDS copy of the
-    table, k^2 and k^2 (k + 1) formed from k by the table's own expressions) against gsl_cli2, bit for bit, on points
-    across the unit disk and outside it -- |z| near 0.98 included, where series_2 runs ~900 terms."""
-    import numpy as np
-    rng = np.random.default_rng(11)
-    n = 20000
-    r = np.concatenate([rng.uniform(0.0, 3.0, n // 2), rng.uniform(0.95, 1.0 / 0.95, n // 2)])
-    th = rng.uniform(-np.pi, np.pi, n)
-    x, y = r * np.cos(th), r * np.sin(th)
-    ol, og = np.zeros(2 * n), np.zeros(2 * n)
-    dp = lambda a: a.ctypes.data_as(ctypes.POINTER(ctypes.c_double))
-    hlib.hc_cli2_lds(ctypes.c_int(n), dp(x), dp(y), dp(ol), dp(og))
-    assert np.array_equal(ol.view(np.uint64), og.view(np.uint64))
