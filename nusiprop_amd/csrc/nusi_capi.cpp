@@ -1164,7 +1164,10 @@ int nusi_plan_evolve(nusi_plan* pl, const nusi_params* pts, int n, double* d_flu
     // a call of few tables in the reference order: Gamma / alphaTilde's GSL dilogarithms one per work-item first
     // (k_ga_dilogs; 2.2 MB per table at N_E = 300)
     pl->tabs.Gpre = nullptr;
-    if (kGaPre && refo && nbase == 0 && nd > 0 && nd <= kOverlapTables) {
+#ifndef NUSI_GA_PRE_ALL
+#define NUSI_GA_PRE_ALL 0
+#endif
+    if (kGaPre && refo && nbase == 0 && nd > 0 && (nd <= kOverlapTables || NUSI_GA_PRE_ALL)) {
         const size_t need = nusi::gamma_alphat_pre_doubles(pl->gd.T, nd);
         if (pl->gpre_doubles < need) {
             hipFree(pl->d_gpre);

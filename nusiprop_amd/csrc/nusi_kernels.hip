@@ -226,13 +226,16 @@ __global__ __launch_bounds__(64) void k_ga_dilogs(GridDev g, const Point* __rest
     if (nv == 2) o[T] = v[1];
 }
 
+#ifndef NUSI_GA_PRE_ALL   // A/B: 1 = scans too take the dilogarithm pre-pass (k_ga_dilogs)
+#define NUSI_GA_PRE_ALL 0
+#endif
 size_t gamma_alphat_pre_doubles(int T, int npts) { return (size_t)3 * kGaPreFields * T * npts; }
 
 hipError_t launch_gamma_alphat(const GridDev& g, const Point* pts, int npts, const SplineSet* spl, TablesDev t,
                                int* warn, hipStream_t s, bool ref)
 {
     dim3 grid((g.T + 62) / 63, npts, 2);   // (63 bins per workgroup: the edge-shared lanes)
-    if (ref && t.Gpre && npts <= 16) {   // (the dilogarithms one per work-item first)
+    if (ref && t.Gpre && (npts <= 16 || NUSI_GA_PRE_ALL)) {   // (the dilogarithms one per work-item first)
         hipLaunchKernelGGL(k_ga_dilogs, dim3((g.T + 63) / 64, npts, 3 * kGaPreSlots), dim3(64), 0, s, g, pts, t.Gpre);
         hipLaunchKernelGGL((k_gamma_alphat<true, 2, true>), grid, dim3(384), 0, s, g, pts, spl, t.G, t.At, warn, t.Wmin,
                            t.Gpre);
