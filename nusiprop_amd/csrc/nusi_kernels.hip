@@ -564,43 +564,27 @@ void k_alpha_mcorner(const Point* __restrict__ pts, const int* __restrict__ batc
 // dilogarithms in a row) of every (batch, mass state, corner), one corner per work-item, into mc.sc: the batch kernel
 // had formed them itself, one corner per work-item of a workgroup between two barriers, ~13 % of its time (the
 // trace build, profiles/r6/r7z).  S' and t by alpha_mcorner_st, the tile's own values (as k_alpha_mcorner's), so the
-// same bits.  Grid (NC / 256, batches of the chunk, 3 mass states x 3 parts)
+// same bits.  Grid (NC / 256, batches of the chunk, 3)
 constexpr int kScFields = 8;   // (7 leaves, padded to 64 B)
 __global__ __launch_bounds__(256) void k_alpha_scorner(const Point* __restrict__ pts, const int* __restrict__ batches,
                                                        MCornerDev mc)
 {
     const long long c = (long long)blockIdx.x * 256 + threadIdx.x;
     if (c >= mc.NC) return;
-    const int k = blockIdx.z / 3, part = blockIdx.z - 3 * k;   // (one GSL call per work-item: the part wave-uniform)
+    const int k = blockIdx.z;
     const Point& P = pts[batches[blockIdx.y] & 0xffffff];
     if (!(P.non_resonant && P.majorana)) return;   // (not cornered: the batch kernel reads none)
     double S, t;
     alpha_mcorner_st(P, k, c, mc.ue, S, t);
+    AlphaCorner cr;
+    alpha_corner_shared<true>(S, t, cr);
     double* const o = mc.sc + (((size_t)blockIdx.y * 3 + k) * mc.NC + c) * kScFields;
-    // alpha_corner_shared<true>'s expressions, split over three work-items: (L, LL, TU1, TU2) | G | (Drr, Dri)
-    if (part == 0) {
-        o[0] = NUSI_CLOG1P(S + t);
-        o[3] = NUSI_CLOG(1 + S + t);
-        if (t < -1) {
-            o[4] = li2_t<true>((1 + S + t) / S);
-            o[5] = 0.0;
-        } else {
-            o[4] = li2_t<true>(S / (1 + S + t));
-            o[5] = NUSI_CLOG((1 + S + t) / S);
-        }
-    } else if (part == 1) {
-        o[6] = li2_t<true>((1 + S + t) / (2 + S));
-        o[7] = 0.0;
-    } else {
-        const cd Dr = cli2_real_t<true>((1 + S + t) / (1 + t));
-        o[1] = Dr.r;
-        o[2] = Dr.i;
-    }
+    o[0] = cr.L; o[1] = cr.Drr; o[2] = cr.Dri; o[3] = cr.LL; o[4] = cr.TU1; o[5] = cr.TU2; o[6] = cr.G; o[7] = 0.0;
 }
 size_t scorner_doubles(long long NC, int nbatch) { return (size_t)nbatch * 3 * (size_t)NC * kScFields; }
 hipError_t launch_scorner(const Point* pts, const int* batches, int nbatch, const MCornerDev& mc, hipStream_t s)
 {
-    hipLaunchKernelGGL(k_alpha_scorner, dim3((unsigned)((mc.NC + 255) / 256), nbatch, 9), dim3(256), 0, s, pts, batches, mc);
+    hipLaunchKernelGGL(k_alpha_scorner, dim3((unsigned)((mc.NC + 255) / 256), nbatch, 3), dim3(256), 0, s, pts, batches, mc);
     return hipGetLastError();
 }
 
