@@ -469,7 +469,6 @@ struct nusi_plan {
     hipEvent_t ev_done = nullptr;      // end of the latest call's kernels (the next call waits for it)
     hipStream_t side = nullptr;        // Gamma / alphaTilde beside alpha in calls of few tables (kOverlapTables)
     hipEvent_t ev_fork = nullptr;
-    hipEvent_t ev_sc = nullptr;        // k_alpha_scorner's end on the side stream (the k-split path)
     bool ran = false;
     int last_n = 0;
     std::vector<hipEvent_t> prof_ev;   // 4 per recorded call
@@ -612,10 +611,6 @@ AlphaBatches alpha_batches(nusi_plan* pl, int ntab, std::vector<int>& perm)
 // NUSI_OPT_REFO_CORNER_MB (automatic: kMCornerBudget bytes and half the free memory) of tables, at least the largest
 // batch; launch_alpha runs the batches in chunks that fit
 constexpr size_t kMCornerBudget = size_t(8) << 30;
-#ifndef NUSI_SCORNER   // A/B: 0 = the k-split batch kernel forms the shared corner leaves itself
-#define NUSI_SCORNER 1
-#endif
-constexpr bool kScSplit = NUSI_SCORNER != 0;
 #ifndef NUSI_GA_PRE   // A/B: 0 = the reference order's Gamma / alphaTilde of few tables without k_ga_dilogs
 #define NUSI_GA_PRE 1
 #endif
@@ -623,42 +618,7 @@ constexpr bool kGaPre = NUSI_GA_PRE != 0;
 constexpr int kOverlapTables = 16;   // calls of at most this many tables overlap Gamma / alphaTilde with alpha
 constexpr size_t kStageBytes = size_t(4) << 20;   // nusi_plan_evolve_host's pinned output staging, at most
 constexpr int kSplitTables = 2;   // calls of at most this many tables (no phi-phi) run the k-split alpha path
-int mcorner_block_ensure(nusi_plan* p, int ntab, const AlphaBatches& ab, int budget_mb);
-// the shared corner leaves' block (MCornerDev::sc, k_alpha_scorner; the k-split path of few tables only): room for the
-// most batches a chunk of this call holds (launch_alpha's grouping), 1.9 MB per batch and mass state at N_E = 300; past
-// kScBudget none, and the batch kernel forms the leaves itself (the same bits either way)
-constexpr size_t kScBudget = (size_t)4 << 30;
-int scorner_ensure(nusi_plan* p, const AlphaBatches& ab)
-{
-    nusi::MCornerDev& mc = p->mc;
-    int maxb = 0;
-    for (int b = 0; b < ab.nbatch;) {
-        const int lim = b < ab.nb_plain ? ab.nb_plain : ab.nbatch;
-        int e = b, ntb = 0;
-        while (e < lim) {
-            const int nbe = (int)((unsigned)p->h_batches[e] >> 24);
-            if (e > b && ntb + nbe > mc.cap_tables) break;
-            ntb += nbe;
-            ++e;
-        }
-        maxb = std::max(maxb, e - b);
-        b = e;
-    }
-    if (maxb <= mc.sc_batches) return NUSI_OK;
-    hipFree(mc.sc);
-    mc.sc = nullptr;
-    mc.sc_batches = 0;
-    const size_t bytes = sizeof(double) * nusi::scorner_doubles(mc.NC, maxb);
-    if (bytes > kScBudget) return NUSI_OK;
-    HIPCHECK(hipMalloc(&mc.sc, bytes));
-    mc.sc_batches = maxb;
-    return NUSI_OK;
-}
 int mcorner_ensure(nusi_plan* p, int ntab, const AlphaBatches& ab, int budget_mb)
-{
-    return mcorner_block_ensure(p, ntab, ab, budget_mb);
-}
-int mcorner_block_ensure(nusi_plan* p, int ntab, const AlphaBatches& ab, int budget_mb)
 {
     nusi::MCornerDev& mc = p->mc;
     if (!mc.eu) {
@@ -864,7 +824,6 @@ void nusi_plan_destroy(nusi_plan* pl)
     if (pl->ev_copy) hipEventDestroy(pl->ev_copy);
     if (pl->ev_done) hipEventDestroy(pl->ev_done);
     if (pl->ev_fork) hipEventDestroy(pl->ev_fork);
-    if (pl->ev_sc) hipEventDestroy(pl->ev_sc);
     if (pl->side) hipStreamDestroy(pl->side);
     for (auto& e : pl->prof_ev) hipEventDestroy(e);
     hipFree(pl->d_grid);
@@ -885,7 +844,6 @@ void nusi_plan_destroy(nusi_plan* pl)
     hipFree(pl->mc.buf);
     hipFree(pl->mc.eu);
     hipFree(pl->mc.ue);
-    hipFree(pl->mc.sc);
     hipFree(pl->d_scratch);
     hipFree(pl->d_kt);
     hipFree(pl->d_gpre);
@@ -920,7 +878,6 @@ int nusi_plan_create(int device, int N_bins_E, double lEmin, double lEmax, doubl
     HIPCHECK(hipEventCreateWithFlags(&pl->ev_done, hipEventDisableTiming));
     HIPCHECK(hipStreamCreateWithFlags(&pl->side, hipStreamNonBlocking));
     HIPCHECK(hipEventCreateWithFlags(&pl->ev_fork, hipEventDisableTiming));
-    HIPCHECK(hipEventCreateWithFlags(&pl->ev_sc, hipEventDisableTiming));
     // grid arrays in one allocation
     const size_t ng = 2 * (size_t)G.N + 2 * (size_t)G.T + 4 * (size_t)G.Nz;
     HIPCHECK(hipMalloc(&pl->d_grid, sizeof(double) * ng));
@@ -1204,16 +1161,6 @@ int nusi_plan_evolve(nusi_plan* pl, const nusi_params* pts, int n, double* d_flu
         }
         pl->tabs.Kt = pl->d_kt;
     }
-    // the k-split path's shared corner leaves (three GSL real dilogarithms each, one corner per work-item of the batch
-    // kernel between two barriers otherwise: ~60 % of its workgroups' time there) from k_alpha_scorner, run on the side
-    // stream beside k_alpha_mcorner; the batch kernel waits for it (launch_alpha's sc_ready)
-    bool sc_go = false;
-    if (kScSplit && mcorn && pl->tabs.Kt && nbase == 0 && nd <= kOverlapTables && nbatch > 0) {
-        AlphaBatches ab;
-        ab.nbatch = nbatch;
-        if (int r = scorner_ensure(pl, ab)) return r;
-        sc_go = pl->mc.sc && nbatch <= pl->mc.sc_batches;
-    }
     // a call of few tables in the reference order: Gamma / alphaTilde's GSL dilogarithms one per work-item first
     // (k_ga_dilogs; 2.2 MB per table at N_E = 300)
     pl->tabs.Gpre = nullptr;
@@ -1271,10 +1218,6 @@ int nusi_plan_evolve(nusi_plan* pl, const nusi_params* pts, int n, double* d_flu
         HIPCHECK(hipEventRecord(pl->ev_fork, s));
         HIPCHECK(hipStreamWaitEvent(pl->side, pl->ev_fork, 0));
         join.armed = true;
-        if (sc_go) {
-            HIPCHECK(nusi::launch_scorner(pl->d_tpts, pl->d_batches, nbatch, pl->mc, pl->side));
-            HIPCHECK(hipEventRecord(pl->ev_sc, pl->side));
-        }
         HIPCHECK(nusi::launch_gamma_alphat(pl->gd, pl->d_tpts, nd, spl, pl->tabs, pl->d_warn, pl->side, refo));
         HIPCHECK(hipEventRecord(ev[1], pl->side));
     } else {
@@ -1284,8 +1227,7 @@ int nusi_plan_evolve(nusi_plan* pl, const nusi_params* pts, int n, double* d_flu
     }
     if (nd) {
         HIPCHECK(nusi::launch_alpha(pl->gd, pl->d_tpts, nd, spl, pl->atiles, pl->tabs, pl->d_warn, s, pl->d_batches,
-                                    nbatch, cap, pl->alpha_kind, nb_plain, refo, pl->h_batches, &pl->mc,
-                                    sc_go ? pl->ev_sc : nullptr));
+                                    nbatch, cap, pl->alpha_kind, nb_plain, refo, pl->h_batches, &pl->mc));
     }
     if (sp) {
         const AlphaBatches& bb = pl->shift_batches;

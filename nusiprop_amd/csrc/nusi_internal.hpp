@@ -69,13 +69,10 @@ struct MCornerDev {
     double* ue = nullptr;    // [U]: the energy of each edge
     long long NC = 0;
     int U = 0, cap_tables = 0;
-    double* sc = nullptr;   // the batches' shared corner leaves [batch of the chunk][3][NC][kScFields] (k_alpha_scorner), or
-    int sc_batches = 0;     // nullptr (the batch kernel forms them itself); room for sc_batches batches
 };
 // ref: NUSI_OPT_REFERENCE_ORDER (the kernels' kRef instances: the reference's own operation order for the complex
 // dilogarithms and the s-t interference member leaves, bit-identical to the oracle's ora_set_reference_order(1))
 size_t gamma_alphat_pre_doubles(int T, int npts);   // TablesDev::Gpre's size
-size_t scorner_doubles(long long NC, int nbatch);      // MCornerDev::sc's size for nbatch batches
 hipError_t launch_gamma_alphat(const GridDev& g, const Point* pts, int npts, const SplineSet* spl, TablesDev t,
                                int* warn, hipStream_t s, bool ref);
 // batches: device [nbatches] of first table | count << 24 (count <= gmax), tables of a batch sharing
@@ -87,10 +84,7 @@ hipError_t launch_gamma_alphat(const GridDev& g, const Point* pts, int npts, con
 hipError_t launch_alpha(const GridDev& g, const Point* pts, int npts, const SplineSet* spl, const AlphaTilesDev& tiles,
                         TablesDev t, int* warn, hipStream_t s, const int* batches, int nbatches, int gmax,
                         int kernel, int nb_plain, bool ref, const int* h_batches = nullptr,
-                        const MCornerDev* mc = nullptr, hipEvent_t sc_ready = nullptr);
-// k_alpha_scorner: the reference order's shared corner leaves of the batches into mc.sc (the k-split path of few
-// tables runs it on a side stream; launch_alpha's sc_ready then orders the batch kernel after it)
-hipError_t launch_scorner(const Point* pts, const int* batches, int nbatch, const MCornerDev& mc, hipStream_t s);
+                        const MCornerDev* mc = nullptr);
 // the edge numbering of MCornerDev for a table axis (hi[n] == lo[n + 1] bitwise: one edge): eu [2 T], ue [U]
 void mcorner_edges(int T, const double* lo, const double* hi, std::vector<int>& eu, std::vector<double>& ue);
 // NUSI_OPT_SHIFT_REUSE: tables s0 .. s0 + nshift - 1 of t (grid g) <- base tables map[q].x of tb (grid gb, the

@@ -560,34 +560,6 @@ void k_alpha_mcorner(const Point* __restrict__ pts, const int* __restrict__ batc
     }
 }
 
-// The reference order's shared corner leaves (L, Drr, Dri, LL, TU1, TU2, G: alpha_corner_shared, three GSL real
-// dilogarithms in a row) of every (batch, mass state, corner), one corner per work-item, into mc.sc: the batch kernel
-// had formed them itself, one corner per work-item of a workgroup between two barriers, ~13 % of its time (the
-// trace build, profiles/r6/r7z).  S' and t by alpha_mcorner_st, the tile's own values (as k_alpha_mcorner's), so the
-// same bits.  Grid (NC / 256, batches of the chunk, 3)
-constexpr int kScFields = 8;   // (7 leaves, padded to 64 B)
-__global__ __launch_bounds__(256) void k_alpha_scorner(const Point* __restrict__ pts, const int* __restrict__ batches,
-                                                       MCornerDev mc)
-{
-    const long long c = (long long)blockIdx.x * 256 + threadIdx.x;
-    if (c >= mc.NC) return;
-    const int k = blockIdx.z;
-    const Point& P = pts[batches[blockIdx.y] & 0xffffff];
-    if (!(P.non_resonant && P.majorana)) return;   // (not cornered: the batch kernel reads none)
-    double S, t;
-    alpha_mcorner_st(P, k, c, mc.ue, S, t);
-    AlphaCorner cr;
-    alpha_corner_shared<true>(S, t, cr);
-    double* const o = mc.sc + (((size_t)blockIdx.y * 3 + k) * mc.NC + c) * kScFields;
-    o[0] = cr.L; o[1] = cr.Drr; o[2] = cr.Dri; o[3] = cr.LL; o[4] = cr.TU1; o[5] = cr.TU2; o[6] = cr.G; o[7] = 0.0;
-}
-size_t scorner_doubles(long long NC, int nbatch) { return (size_t)nbatch * 3 * (size_t)NC * kScFields; }
-hipError_t launch_scorner(const Point* pts, const int* batches, int nbatch, const MCornerDev& mc, hipStream_t s)
-{
-    hipLaunchKernelGGL(k_alpha_scorner, dim3((unsigned)((mc.NC + 255) / 256), nbatch, 3), dim3(256), 0, s, pts, batches, mc);
-    return hipGetLastError();
-}
-
 void mcorner_edges(int T, const double* lo, const double* hi, std::vector<int>& eu, std::vector<double>& ue)
 {
     eu.assign(2 * (size_t)T, 0);
@@ -711,20 +683,7 @@ void k_alpha_batch(GridDev g, const Point* __restrict__ pts, const SplineSet* __
         AlphaPre pre{};
         PPTerm ppt{0.0, 1.0, 1.0};
         if (cornered) {
-            if (kRef && mc.sc) {   // (from k_alpha_scorner's block: the corners the entries n < m read, ut <= us)
-                const double* const scb = mc.sc + ((size_t)by * 3 + k) * mc.NC * kScFields;
-                for (int j = tid; j < cc; j += kTileThreads) {
-                    const int si = j / ct, ti = j - si * ct;
-                    const int us = mc.eu[ssrc[si]], ut = mc.eu[tsrc[ti]];
-                    if (ut <= us) {
-                        const double2* f = reinterpret_cast<const double2*>(scb + ((size_t)us * (us + 1) / 2 + ut) * kScFields);
-                        const double2 a0 = f[0], a1 = f[1], a2 = f[2], a3 = f[3];
-                        P3[j] = a0.x; P3[kCC + j] = a0.y; P3[2 * kCC + j] = a1.x;
-                        tmp[j] = a1.y; tmp[kCC + j] = a2.x; tmp[2 * kCC + j] = a2.y; tmp[3 * kCC + j] = a3.x;
-                    }
-                }
-            } else
-                for (int j = tid; j < cc; j += kTileThreads) b_corner<kRef>(j, edgk, ct, cs, P3, tmp);
+            for (int j = tid; j < cc; j += kTileThreads) b_corner<kRef>(j, edgk, ct, cs, P3, tmp);
             for (int j = tid; j < kAlphaTile * (cs + ct); j += kTileThreads)
                 alpha_batch_mixed_job(j, edgk, ct, cs, tl, th, sl, sh, n0, m0, T, Tm, mix, mix + kAlphaTile * cs);
             __syncthreads();
@@ -1019,7 +978,7 @@ template <bool kRef>
 static hipError_t launch_alpha_t(const GridDev& g, const Point* pts, int npts, const SplineSet* spl,
                                  const AlphaTilesDev& at, TablesDev t, int* warn, hipStream_t s, const int* batches,
                                  int nbatches, int gmax, int kernel, int nb_plain, const int* h_batches,
-                                 const MCornerDev* mc, hipEvent_t sc_ready)
+                                 const MCornerDev* mc)
 {
     t_alpha_kernel = kRef ? "k_alpha_tile[refo]" : "k_alpha_tile";
     if (kernel == 0 && batches) {
@@ -1087,32 +1046,26 @@ static hipError_t launch_alpha_t(const GridDev& g, const Point* pts, int npts, c
                         const long long tot = mc->NC * 3 * ntb;
                         const int jobs = 256 * (int)std::max(1LL, std::min<long long>(kMcJobs / 256, tot / (2048 * 256)));
                         const int cbmin = jobs / nbmax;
-                        // (the k-split path of few tables: the shared corners from k_alpha_scorner, which the caller
-                        // ran on its side stream beside this one, when sc_ready is given)
-                        MCornerDev mcc = *mc;
-                        if (!(split && sc_ready && mc->sc && b == 0 && e == nbatches && e - b <= mc->sc_batches)) mcc.sc = nullptr;
                         hipLaunchKernelGGL(k_alpha_mcorner, dim3((unsigned)((mc->NC + cbmin - 1) / cbmin), e - b, 3),
-                                           dim3(256), 0, s, pts, batches + b, mcc, pc0, jobs);
+                                           dim3(256), 0, s, pts, batches + b, *mc, pc0, jobs);
                         if (split) {
-                            if (mcc.sc)
-                                if (hipError_t err = hipStreamWaitEvent(s, sc_ready, 0)) return err;
                             hipLaunchKernelGGL((k_alpha_batch<false, true, true>), dim3(at.ncls[0], e - b, 3),
                                                dim3(kTileThreads), lds, s, g, pts, spl, at.tiles, batches + b, t.A, t.Med,
-                                               warn, t.Wmin, mcc, pc0, t.Kt);
+                                               warn, t.Wmin, *mc, pc0, t.Kt);
                             hipLaunchKernelGGL(k_alpha_ksum, dim3(at.ncls[0], e - b), dim3(kTileThreads), 0, s, g,
                                                at.tiles, batches + b, t.Kt, t.A);
                         } else if (b < nb_plain && kBatchKLaunch) {
                             for (int kk = 0; kk < 3; ++kk)
                                 hipLaunchKernelGGL((k_alpha_batch<false, true, false, true>), dim3(at.ncls[0], e - b),
                                                    dim3(kTileThreads), lds, s, g, pts, spl, at.tiles, batches + b, t.A,
-                                                   t.Med, warn, t.Wmin, mcc, pc0, nullptr, kk);
+                                                   t.Med, warn, t.Wmin, *mc, pc0, nullptr, kk);
                         } else if (b < nb_plain)
                             hipLaunchKernelGGL((k_alpha_batch<false, true>), dim3(at.ncls[0], e - b), dim3(kTileThreads),
-                                               lds, s, g, pts, spl, at.tiles, batches + b, t.A, t.Med, warn, t.Wmin, mcc,
+                                               lds, s, g, pts, spl, at.tiles, batches + b, t.A, t.Med, warn, t.Wmin, *mc,
                                                pc0, nullptr);
                         else
                             hipLaunchKernelGGL((k_alpha_batch<true, true>), dim3(at.ncls[0], e - b), dim3(kTileThreads),
-                                               lds, s, g, pts, spl, at.tiles, batches + b, t.A, t.Med, warn, t.Wmin, mcc,
+                                               lds, s, g, pts, spl, at.tiles, batches + b, t.A, t.Med, warn, t.Wmin, *mc,
                                                pc0, nullptr);
                         b = e;
                     }
@@ -1169,14 +1122,13 @@ static hipError_t launch_alpha_t(const GridDev& g, const Point* pts, int npts, c
 
 hipError_t launch_alpha(const GridDev& g, const Point* pts, int npts, const SplineSet* spl, const AlphaTilesDev& at,
                         TablesDev t, int* warn, hipStream_t s, const int* batches, int nbatches, int gmax,
-                        int kernel, int nb_plain, bool ref, const int* h_batches, const MCornerDev* mc,
-                        hipEvent_t sc_ready)
+                        int kernel, int nb_plain, bool ref, const int* h_batches, const MCornerDev* mc)
 {
     if (ref)
         return launch_alpha_t<true>(g, pts, npts, spl, at, t, warn, s, batches, nbatches, gmax, kernel, nb_plain,
-                                    h_batches, mc, sc_ready);
+                                    h_batches, mc);
     return launch_alpha_t<false>(g, pts, npts, spl, at, t, warn, s, batches, nbatches, gmax, kernel, nb_plain, h_batches,
-                                 mc, nullptr);
+                                 mc);
 }
 
 }  // namespace nusi
