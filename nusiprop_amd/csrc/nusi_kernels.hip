@@ -521,7 +521,10 @@ __global__ __launch_bounds__(256) void k_alpha_medge(GridDev g, const Point* __r
 // only -- take similar GSL branches and series lengths (in the tile's corner order the lanes of a wave diverge: 0.21
 // ns per call against 0.06, scripts/dev/gsl_bench.hip).  The values pass through LDS to leave as runs of cb corners
 // per (field, table), the layout the batch kernel reads a tile's corner rows from.
-constexpr int kMcJobs = 1024;
+#ifndef NUSI_MC_JOBS   // A/B: jobs (corner x point) per k_alpha_mcorner workgroup on scans, a multiple of 256
+#define NUSI_MC_JOBS 1024
+#endif
+constexpr int kMcJobs = NUSI_MC_JOBS;
 #ifndef NUSI_MC_WAVES   // A/B: waves per SIMD the member-corner kernel is built for (0: the compiler's choice)
 #define NUSI_MC_WAVES 0
 #endif
