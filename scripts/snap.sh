@@ -14,7 +14,7 @@ rm -rf .snap
 mkdir .snap
 git archive HEAD | tar -x -C .snap
 rm -rf .snap/profiles/r1* .snap/profiles/r2* .snap/profiles/r3 .snap/profiles/r4 .snap/BENCH_r* .snap/GPUTEST_r* \
-       .snap/MULTICHIP_r* .snap/SCALE_r* .snap/SURVEY.md .snap/PAPERS.md .snap/SNIPPETS.md .snap/profiles/r6/r7*
+       .snap/MULTICHIP_r* .snap/SCALE_r* .snap/SURVEY.md .snap/PAPERS.md .snap/SNIPPETS.md .snap/profiles/r6/r7* .snap/profiles/r6/r8*
 for f in nusiprop_amd/libnusi.so nusiprop_amd/tools/phiphi_text_to_binary oracle/_build/libnusi_oracle.so \
          tests/_build/libhostcheck.so scripts/calib/pmc_calib scripts/dev/gsl_bench; do
   [ -e "$f" ] && { mkdir -p ".snap/$(dirname "$f")"; cp -p "$f" ".snap/$f"; }
