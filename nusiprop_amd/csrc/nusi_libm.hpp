@@ -56,7 +56,10 @@ constexpr double two54 = 1.80143985094819840000e+16;
 // ~20 integer / branch instructions each) with one table load and ~25 fp64 operations.
 constexpr double kLn2hi = 0x1.62e42fefa3800p-1, kLn2lo = 0x1.ef35793c76730p-45;   // k * kLn2hi exact
 // log(2^kadj * x) + c / x for a normal positive double x = from_bits(ix); c: log1p's rounding
-// correction of 1 + x (0 for log)
+// correction of 1 + x (0 for log).  kC = false (log): c = 0 and the correction term, fma(-sc, r, sc) with sc = +0, is
+// +0 -- which the sum it is added to never is -0 (its first addend is +0 or nonzero) -- so it is left out: the same bits
+// without the correction's six instructions (the compiler cannot drop a product with 0 itself)
+template <bool kC = true>
 NUSI_FN double log_kernel(unsigned long long ix, double c, int kadj)
 {
     const unsigned long long tmp = ix - 0x3fe6000000000000ULL;
@@ -77,6 +80,7 @@ NUSI_FN double log_kernel(unsigned long long ix, double c, int kadj)
     q = fma(r, q, 1.0 / 3);
     q = fma(r, q, -0.5);
     const double p = (r * r) * q;
+    if (!kC) return s2 + ((fma(kd, kLn2lo, lcl) + (e1 + e2)) + p);
     // c / x = c invc 2^-k / (1 + r) ~ sc (1 - r); 2^-k = 0 past the normal range (c / x negligible)
     const double sc = c * (invc * ((k < 1023) ? from_bits((unsigned long long)(1023 - k) << 52) : 0.0));
     return s2 + (((fma(kd, kLn2lo, lcl) + (e1 + e2)) + p) + fma(-sc, r, sc));
@@ -89,9 +93,9 @@ NUSI_FN double log_i(double x)
         if (x != x || x == 1.0 / 0.0) return x + x;
         if (x == 0.0) return -1.0 / 0.0;
         if (x < 0.0) return (x - x) / 0.0;
-        return log_kernel(bits(x * 0x1p52), 0.0, -52);           // subnormal
+        return log_kernel<false>(bits(x * 0x1p52), 0.0, -52);    // subnormal
     }
-    return log_kernel(ix, 0.0, 0);
+    return log_kernel<false>(ix, 0.0, 0);
 }
 
 // log1p(x) = log(u) + c / u, u = 1 + x rounded, c its exact rounding error (Fast2Sum)

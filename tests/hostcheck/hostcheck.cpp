@@ -237,6 +237,9 @@ double hc_gsl_clausen(double x) { return nusi::gsl::clausen(x); }
 double hc_hypot(double x, double y) { return nusi::gsl::hypot(x, y); }
 // the libm atan2 the device runs (nusi_libm.hpp: the select-based common path, else fdlibm's branches)
 double hc_atan2(double y, double x) { return nusi::nm::atan2_i(y, x); }
+// the GPU's inline log / log1p (nusi_libm.hpp: log_i without the c = 0 correction term) on n arguments
+void hc_log_n(int n, const double* x, double* out) { for (int i = 0; i < n; ++i) out[i] = nusi::nm::log_i(x[i]); }
+void hc_log1p_n(int n, const double* x, double* out) { for (int i = 0; i < n; ++i) out[i] = nusi::nm::log1p_i(x[i]); }
 double hc_atan2_full(double y, double x) { return nusi::nm::atan2_full(y, x); }
 // the series' per-k table row (d1, d2, y1, y2, l1, l2) and its division, for the two-part-reciprocal test
 void hc_gsl_krow(int k, double* o)
