@@ -349,7 +349,7 @@ NUSI_FN void cseries_t(bool s2, double r, double lr, double x, double y, double&
     double real_sum = t2 ? 0.5 * r * ck : r * ck;
     double imag_sum = t2 ? 0.5 * r * sk : r * sk;
     const double nlr = -lr;   // -log(r)
-    const int kmax = t2 ? 30 + (int)(18.0 / nlr) : 50 + (int)(22.0 / nlr);
+    const int kmax = (t2 ? 30 : 50) + (int)((t2 ? 18.0 : 22.0) / nlr);   // (one division for a wave of both series)
     KRow next = kKT.row[2];   // (the table row of the next iteration is loaded one iteration ahead; kmax <= 921)
     double q = 0.0, dr = 0.0, di = 0.0;
     auto term = [&](int k) {
