@@ -33,8 +33,10 @@ BUDGET = {
     r"k_cascade_bsILi48ELi1ELi1ELi4ELi1ELb1E": (4, 112),
     r"k_cascade_bsILi16ELi1ELi1ELi8ELi1E": (6, 128),
     r"k_cascade_bsILi(16|32)ELi2ELi1ELi2ELi2E": (0, 96),
-    r"k_cascade_bsILi48ELi2ELi1ELi2ELi2E": (4, 112),
-    r"k_cascade_bsILi6ELi16ELi1ELi2ELi2E": (4, 112),
+    # (round 6: 4 -> 6 with the cheaper log's different call frames in the prologue's pow(); C5's gamma-batch cascade
+    # measured unchanged, 21.5 -> 21.6 ms, profiles/r6/r7w -> r8o)
+    r"k_cascade_bsILi48ELi2ELi1ELi2ELi2E": (6, 112),
+    r"k_cascade_bsILi6ELi16ELi1ELi2ELi2E": (6, 112),
 }
 
 
