@@ -87,6 +87,10 @@ constexpr KTab make_ktab()
     return t;
 }
 constexpr KTab kKT = make_ktab();
+#ifndef NUSI_S2_VLOAD   // A/B: 0 = waves of both complex series select each lane's row columns (scalar row)
+#define NUSI_S2_VLOAD 1
+#endif
+constexpr bool kS2VecRows = NUSI_S2_VLOAD != 0;
 
 // RN(a / d) for the series' terms.  kExact: the division; else fma(a, y, RN(a l)) from the two-part reciprocal
 // y + l (header comment), valid for a, d > 0 with a l normal (a >= 2^-900) -- the callers take kExact for arguments
@@ -351,20 +355,37 @@ NUSI_FN void cseries_t(bool s2, double r, double lr, double x, double y, double&
     const double nlr = -lr;   // -log(r)
     const int kmax = (t2 ? 30 : 50) + (int)((t2 ? 18.0 : 22.0) / nlr);   // (one division for a wave of both series)
     KRow next = kKT.row[2];   // (the table row of the next iteration is loaded one iteration ahead; kmax <= 921)
+    // kS2 == 2 (a wave of both series): each lane loads its own columns of the row (vector loads at its t2 offset from
+    // the row's uniform address) instead of selecting between the scalar row's columns -- three 64-bit selects a term
+    constexpr bool vrow = kS2 == 2 && kS2VecRows;
+    const int toff = t2 ? 1 : 0;
+    double nd = 0.0, ny = 0.0, nl = 0.0;
+    if (vrow) {
+        const double* rp = &kKT.row[2].d1;
+        nd = rp[toff]; ny = rp[2 + toff]; nl = rp[4 + toff];
+    }
     double q = 0.0, dr = 0.0, di = 0.0;
     auto term = [&](int k) {
-        const KRow kr = next;
+        double d, yk, lk;
+        if (vrow) {
+            d = nd; yk = ny; lk = nl;
+            const double* rp = &kKT.row[k + 1].d1;
+            nd = rp[toff]; ny = rp[2 + toff]; nl = rp[4 + toff];
+        } else {
+            const KRow kr = next;
 #ifdef NUSI_GSL_ROW_STUB   // timing A/B only (wrong values): every term reads row 2 (no table load in the loop)
-        (void)k;
+            (void)k;
 #else
-        next = kKT.row[k + 1];
+            next = kKT.row[k + 1];
 #endif
+            d = t2 ? kr.d2 : kr.d1;   // (double) k * k * (k + 1.0) or (double) k * k
+            yk = t2 ? kr.y2 : kr.y1;
+            lk = t2 ? kr.l2 : kr.l1;
+        }
         const double ck_tmp = ck;
         ck = ck - (alpha * ck + beta * sk);
         sk = sk - (alpha * sk - beta * ck_tmp);
         rk *= r;
-        const double d = t2 ? kr.d2 : kr.d1;   // (double) k * k * (k + 1.0) or (double) k * k
-        const double yk = t2 ? kr.y2 : kr.y1, lk = t2 ? kr.l2 : kr.l1;
         q = div_k<kExact>(rk, d, yk, lk);
         dr = q * ck;
         di = q * sk;
