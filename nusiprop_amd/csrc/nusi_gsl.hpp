@@ -269,8 +269,7 @@ NUSI_FN_OUT double dilog_xge0(double x)
     const double ser = dilog_series_2(u);
     if (br == 3) return ser;
     const double log_x = GSL_LOG(x);
-    // log(1 - 1/x) resp. log(1 - x); (not formed by a wave whose lanes are all past x = 2: the select had evaluated it)
-    const double log_u = wave_any(br != 0) ? (br == 0 ? 0.0 : GSL_LOG(u)) : 0.0;
+    const double log_u = br == 0 ? 0.0 : GSL_LOG(u);   // log(1 - 1/x) resp. log(1 - x)
     if (br == 0) {
         const double t1 = kPiD * kPiD / 3.0, t2 = ser, t3 = 0.5 * log_x * log_x;
         return t1 - t2 - t3;
@@ -567,9 +566,7 @@ NUSI_FN_OUT double gsl_li2(double x)
 
 // gsl_sf_complex_dilog_xy_e on the real axis (gsl_cli2's y == 0 branch, alone: a caller with real arguments keeps
 // the complex series' registers out of its own budget)
-// (the imaginary part's log only where a lane of the wave has x >= 1: the select had evaluated it for every wave)
-NUSI_FN double gsl_cli2_real_im(double x) { return gsl::wave_any(x >= 1.0) ? ((x >= 1.0) ? -gsl::kPiD * GSL_LOG(x) : 0.0) : 0.0; }
-NUSI_FN cd gsl_cli2_real(double x) { return cd{gsl_li2(x), gsl_cli2_real_im(x)}; }
+NUSI_FN cd gsl_cli2_real(double x) { return cd{gsl_li2(x), (x >= 1.0) ? -gsl::kPiD * GSL_LOG(x) : 0.0}; }
 
 // gsl_sf_complex_dilog_xy_e: the real axis; |z| within eps of 1 (Lewin A.2.4.1 / A.2.4.2); the unit disk; 1/z
 // into the unit disk, unwound with Li2(z) + Li2(1/z) = -zeta2 - log(-z)^2 / 2.  gsl_cli2_t<true> (gsl_cli2_inl) is the
@@ -581,7 +578,7 @@ NUSI_FN cd gsl_cli2_t(double x, double y)
 {
     const double zeta2 = gsl::kPiD * gsl::kPiD / 6.0;
     const double r2 = x * x + y * y;
-    if (y == 0.0) return cd{gsl_li2(x), gsl_cli2_real_im(x)};
+    if (y == 0.0) return cd{gsl_li2(x), (x >= 1.0) ? -gsl::kPiD * GSL_LOG(x) : 0.0};
     if (fabs(r2 - 1.0) < gsl::kEps) {
         const double theta = GSL_ATAN2(y, x);
         const double term1 = theta * theta / 4.0, term2 = gsl::kPiD * fabs(theta) / 2.0;
