@@ -353,6 +353,10 @@ __global__ __launch_bounds__(64) void k_cascade(GridDev g, const Point* __restri
 typedef double nusi_f64x4 __attribute__((ext_vector_type(4)));
 
 // ---------------------------------------------------------------------------
+#ifndef NUSI_BS_SRC_AHEAD   // A/B: 0 = the DSNB sources loaded and stored within one phase B
+#define NUSI_BS_SRC_AHEAD 1
+#endif
+constexpr bool kSrcAhead = NUSI_BS_SRC_AHEAD != 0;
 // Helpers of the MFMA cascade k_cascade_bs (below): the power-law source, the DSNB source table, the chain's
 // hand-off between redshift steps and the resonant-only running sum.
 // ---------------------------------------------------------------------------
@@ -800,6 +804,44 @@ void k_cascade_bs(GridDev g, const Point* __restrict__ pts, const int* __restric
                 }
             }
         };
+        // The DSNB sources of block qb from k_source_dsnb's table a block ahead (src_load into registers in phase B of
+        // block qb - 2, src_store into srcb in phase B of block qb - 1): the table's latency off the record wave's path
+        // (sources() loaded and stored them within one phase B: C2a's cascade 0.295 against C2b's 0.176 ms).  The same
+        // values in the same places.
+        constexpr bool kAhead = kSrcAhead && P == 1 && RT == 4;   // (one point, one pass shape: the others' registers)
+        constexpr int SQL = (S4 * P + 63) / 64;
+        auto src_valid = [&](int qb, int e, int& p, int& b, int& i) {
+            p = e % P;
+            const int sj = e / P, sb = sj / NJ, jj = sj - NJ * sb, s2 = 4 * qb + sb;
+            b = N - 1 - s2 + jj;
+            i = Nz - 1 - jb - jj;
+            return e < S4 * P && p < R && jj < njp && s2 < Ts && b >= 0 && b < N;
+        };
+        auto src_load = [&](int qb, double (&v)[SQL]) {
+            if (!any_dsnb) return;
+#pragma unroll
+            for (int u = 0; u < SQL; ++u) {
+                int p, b, i;
+                const int e = lane + 64 * u;
+                v[u] = (src_valid(qb, e, p, b, i) && pinf[2 * P + p] == 0.0)
+                           ? t.Src[(size_t)pinf[3 * P + p] * T * nst + src_index(Nz, jb + (e / P) % NJ, b)] : 0.0;
+            }
+        };
+        auto src_store = [&](int qb, const double (&v)[SQL]) {
+            if (!kSrcRec && !any_dsnb) return;
+#pragma unroll
+            for (int u = 0; u < SQL; ++u) {
+                int p, b, i;
+                const int e = lane + 64 * u;
+                if (src_valid(qb, e, p, b, i)) {
+                    if (pinf[2 * P + p] == 0.0)
+                        srcb[(qb & 1) * 4 * NC + e] = v[u];
+                    else if (kSrcRec)
+                        srcb[(qb & 1) * 4 * NC + e] =
+                            powerlaw_src_h(gl, SrcFactors{pinf[p], pinf[P + p]}, pw + (size_t)p * (T + 2), i, b);
+                }
+            }
+        };
         auto finalise = [&](int qb) {   // the last pass' stages of block qb (nuSIprop.hpp:328-336)
             for (int e = lane; e < 4 * P; e += 64) {
                 const int d = e / P, p = e - P * (e / P), sg = 4 * qb + d, b = N - 1 - sg + njp - 1;
@@ -841,6 +883,8 @@ void k_cascade_bs(GridDev g, const Point* __restrict__ pts, const int* __restric
             for (int p = 0; p < R; ++p) any_dsnb = any_dsnb || pinf[2 * P + p] == 0.0;
             records(0, 0, S4);
             sources(0);
+            double sv[SQL];
+            if (kAhead) src_load(1, sv);
             double fv[FQL];
             fifo_load(pass, 0, fv);
             fifo_store(0, fv);
@@ -857,7 +901,11 @@ void k_cascade_bs(GridDev g, const Point* __restrict__ pts, const int* __restric
                 NUSI_BS_STAMP(pass * nblk + q, 2);
                 if (4 * (q + 1) < Ts) {                                // phase B
                     records(q + 1, kRecSplit, S4);
-                    sources(q + 1);
+                    if (kAhead) {
+                        src_store(q + 1, sv);           // block q + 1's sources (loaded a block ago)
+                        if (4 * (q + 2) < Ts) src_load(q + 2, sv);
+                    } else
+                        sources(q + 1);
                 }
                 if (pass == npass - 1 && q > 0) finalise(q - 1);
                 NUSI_BS_STAMP(pass * nblk + q, 3);
